@@ -1,0 +1,205 @@
+/*
+ * xdrg.h — C-ABI of the MI355X XDR batch engine (libxdrgpu.so).
+ *
+ * This is the drop-in boundary for the oncrpc4j XDR hot path.  Every entry
+ * point below names the reference interface it replaces (paths are relative
+ * to /root/reference/oncrpc4j-core/src/main/java/org/dcache/oncrpc4j/):
+ *
+ *   xdr/XdrEncodingStream.java:32-57   per-field encode surface  -> xdrg_encode_batch
+ *   xdr/XdrDecodingStream.java:33-58   per-field decode surface  -> xdrg_decode_batch
+ *   xdr/Xdr.java:39-1039               concrete codec semantics (bit-exact contract)
+ *   grizzly/GrizzlyRpcTransport.java:97-110   record-mark prepend on send -> XDRG_FRAME_RM
+ *   rpc/RpcMessageParserTCP.java:63-140       record-mark walk on receive -> xdrg_frame_scan
+ *
+ * The reference is per-field and per-record (an XdrAble encodes its fields in
+ * declaration order into one Xdr; xdr/XdrAble.java:40,49).  The engine works on
+ * a BATCH of N records of one schema.  A schema is the field tape rpcgen emits
+ * for a struct (oncrpc4j-rpcgen .../jrpcgen/jrpcgen.java:661-913): each field is
+ * a base type (jrpcgen.java:608-618, plus enum/unsigned/opaque) with a
+ * declaration kind (JrpcgenDeclaration.java:64-81: SCALAR, FIXEDVECTOR,
+ * DYNAMICVECTOR).  Records live natively as columns (one per field, native
+ * little-endian), the XDR side is one contiguous big-endian byte stream.
+ *
+ * Conventions
+ *   - plain C types only; no C++ or torch types cross this boundary;
+ *   - every call returns an int status (XDRG_OK or an XDRG_E_* code) and never
+ *     throws; the Java/JNI side rethrows;
+ *   - the caller owns every buffer; the engine keeps no pointer past return
+ *     except its context's own device workspace;
+ *   - a context is used by one thread at a time (mirrors Xdr's single-owner
+ *     model, xdr/Xdr.java:56,71); use one context per worker thread;
+ *   - all data pointers are DEVICE pointers (HBM) unless a call says otherwise.
+ */
+#ifndef XDRG_H
+#define XDRG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XDRG_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+/* Error parity with the reference (xdr/Xdr.java:1028-1037,
+ * xdr/BadXdrOncRpcException.java:24):                                       */
+#define XDRG_OK           0
+#define XDRG_E_SHORT      1  /* BadXdrOncRpcException("xdr stream too short")  Xdr.java:1030 */
+#define XDRG_E_CORRUPT    2  /* BadXdrOncRpcException("corrupted xdr")         Xdr.java:1036 */
+#define XDRG_E_FIXED_LEN  3  /* IllegalArgumentException("array size does not match
+                                protocol specification")                       Xdr.java:625-627 */
+#define XDRG_E_CAPACITY   4  /* output buffer too small (the reference grows: Xdr.java:1020-1026) */
+#define XDRG_E_FRAME      5  /* fixed-stride framed decode met a record mark that is not
+                                (LAST | record size) — a multi-fragment or foreign record */
+#define XDRG_E_INVAL      6  /* bad argument / unsupported schema */
+#define XDRG_E_HIP        7  /* HIP runtime error (see xdrg_last_error) */
+#define XDRG_E_NOMEM      8  /* allocation failed */
+#define XDRG_E_INCOMPLETE 9  /* frame scan: not all fragments arrived -> NextAction STOP
+                                (RpcMessageParserTCP.java:51-53) */
+
+/* ---- schema vocabulary (rpcgen) ------------------------------------------ */
+/* Base types.  Native element sizes: INT/UINT/ENUM/FLOAT 4, HYPER/UHYPER/
+ * DOUBLE 8, SHORT 2, BYTE/BOOL/OPAQUE/STRING 1.  XDR element sizes: 4 for
+ * every scalar type (BYTE and SHORT are sign-extended to an XDR int,
+ * Xdr.java:919-936; byte vectors use 4 bytes per element, Xdr.java:878-888),
+ * 8 for HYPER/UHYPER/DOUBLE, and 1 byte + trailing zero pad to a multiple of
+ * 4 for OPAQUE/STRING (Xdr.java:776-781).                                   */
+#define XDRG_T_INT     1   /* xdrEncodeInt            Xdr.java:545  / xdrDecodeInt     :171 */
+#define XDRG_T_UINT    2   /* rpcgen "unsigned int" -> int  (JrpcgenParser.cup:658)         */
+#define XDRG_T_ENUM    3   /* enums are ints           (jrpcgen.java:688-695)                */
+#define XDRG_T_BOOL    4   /* xdrEncodeBoolean         Xdr.java:803  / decode != 0     :404 */
+#define XDRG_T_HYPER   5   /* xdrEncodeLong            Xdr.java:812  / xdrDecodeLong   :417 */
+#define XDRG_T_UHYPER  6
+#define XDRG_T_FLOAT   7   /* floatToIntBits (NaN canonical) Xdr.java:674 / raw bits :255 */
+#define XDRG_T_DOUBLE  8   /* doubleToLongBits (NaN canonical) Xdr.java:685 / raw  :267 */
+#define XDRG_T_SHORT   9   /* sign-extend / truncate   Xdr.java:934 / :497               */
+#define XDRG_T_BYTE   10   /* sign-extend / truncate   Xdr.java:919 / :485               */
+#define XDRG_T_OPAQUE 11   /* opaque x[N] / x<>        Xdr.java:776, :797 / :341, :374     */
+#define XDRG_T_STRING 12   /* string s<> as UTF-8 bytes Xdr.java:760 / :392              */
+
+/* Declaration kinds (JrpcgenDeclaration.java:64-81).                         */
+#define XDRG_K_SCALAR  0   /* one element                                              */
+#define XDRG_K_FIXED   1   /* T x[count]: count elements, no length word               */
+#define XDRG_K_DYNAMIC 2   /* T x<count?>: 4-byte BE length word + elements (count = max,
+                              0 = unbounded; the reference never enforces a max)       */
+
+typedef struct xdrg_field {
+    uint32_t type;      /* XDRG_T_* */
+    uint32_t kind;      /* XDRG_K_* */
+    uint32_t count;     /* FIXED: element count; DYNAMIC: max (0 = none); SCALAR: ignored */
+    uint32_t reserved;  /* must be 0 */
+} xdrg_field;
+
+/* One native column.  Fixed-size fields (SCALAR / FIXED): record i's first
+ * element is at  data + i*stride  (stride 0 = packed = elem_size*count), so
+ * both struct-of-arrays (stride = element bytes) and array-of-structs
+ * (data = &recs[0].field, stride = sizeof(rec)) describe the same batch.
+ * DYNAMIC fields: record i owns elements [offsets[i], offsets[i+1]) of data
+ * (element units: bytes for OPAQUE/STRING).  On decode the engine writes
+ * offsets[0..n] (offsets[0] = 0) and needs cap >= total elements.           */
+typedef struct xdrg_column {
+    void     *data;
+    int64_t   stride;
+    uint64_t *offsets;
+    uint64_t  cap;
+} xdrg_column;
+
+/* ---- flags --------------------------------------------------------------- */
+/* Prepend one RFC 1831 record mark per record: BE(len | 0x80000000), one
+ * last fragment per message (GrizzlyRpcTransport.java:103-110,
+ * RpcMessageParserTCP.java:37-41, docs/rfc1831.txt:696-705).  On decode the
+ * engine expects and strips one mark per record.                             */
+#define XDRG_FRAME_RM      0x1u
+/* out_len / first_bad / err are DEVICE pointers; the call does not
+ * synchronise the stream (graph-capturable).                                  */
+#define XDRG_ASYNC         0x2u
+
+/* ---- opaque handles ------------------------------------------------------- */
+typedef struct xdrg_ctx    xdrg_ctx;
+typedef struct xdrg_schema xdrg_schema;
+
+/* ---- version / diagnostics ------------------------------------------------ */
+int         xdrg_abi_version(void);
+const char *xdrg_status_string(int status);   /* reference exception message */
+const char *xdrg_last_error(xdrg_ctx *ctx);   /* last HIP / argument detail   */
+
+/* ---- context -------------------------------------------------------------- */
+/* A context binds one device and one stream and owns scratch workspace.
+ * Replaces the per-call `new Xdr(...)` buffer ownership of the reference
+ * (Xdr.java:82-119, RpcCall.java:460).                                        */
+#define XDRG_CTX_TIMING 0x1u    /* record HIP events around every kernel launch */
+int  xdrg_ctx_create(int device, uint32_t flags, xdrg_ctx **out);
+int  xdrg_ctx_destroy(xdrg_ctx *ctx);
+/* stream is a hipStream_t (NULL = the default stream). */
+int  xdrg_ctx_set_stream(xdrg_ctx *ctx, void *stream);
+/* Per-kernel launch statistics (only with XDRG_CTX_TIMING): kernel ids below. */
+#define XDRG_KERNEL_FIXED_ENCODE 0
+#define XDRG_KERNEL_FIXED_DECODE 1
+#define XDRG_KERNEL_VAR_SIZE     2
+#define XDRG_KERNEL_VAR_SCAN     3
+#define XDRG_KERNEL_VAR_ENCODE   4
+#define XDRG_KERNEL_VAR_DECODE   5
+#define XDRG_KERNEL_FRAME_SCAN   6
+#define XDRG_KERNEL_COUNT        7
+int  xdrg_ctx_kernel_stats(xdrg_ctx *ctx, int kernel, uint64_t *launches, double *total_ms);
+int  xdrg_ctx_reset_stats(xdrg_ctx *ctx);
+
+/* ---- schema ----------------------------------------------------------------- */
+/* Compile a field tape (rpcgen struct body, jrpcgen.java:758-913) into an
+ * engine schema.  Host-side object; may be shared by contexts.                 */
+int  xdrg_schema_create(const xdrg_field *fields, size_t nfields, xdrg_schema **out);
+int  xdrg_schema_destroy(xdrg_schema *schema);
+/* XDR bytes of one record when every field is fixed-size (no DYNAMIC field),
+ * excluding any record mark; 0 for variable-size schemas.                      */
+uint64_t xdrg_schema_fixed_size(const xdrg_schema *schema);
+
+/* ---- encode ------------------------------------------------------------------ */
+/* Encode n records into one contiguous XDR stream `out` (capacity out_cap
+ * bytes).  The stream is the concatenation of every record's encoding in
+ * record order, each record the concatenation of its fields' encodings in
+ * declaration order (XdrAble.xdrEncode via rpcgen codingMethod), prefixed per
+ * record by a record mark when XDRG_FRAME_RM is set.  rec_offsets (n+1
+ * entries, nullable) receives the byte offset of each record (of its mark
+ * when framed) and the total.  *out_len receives the total byte count.
+ * Pad bytes are written as zeros (RFC 4506; Xdr.java:765-781).
+ * Returns XDRG_E_CAPACITY (and writes nothing) if out_cap is too small.     */
+int  xdrg_encode_batch(xdrg_ctx *ctx, const xdrg_schema *schema,
+                       const xdrg_column *cols, uint64_t n,
+                       uint8_t *out, uint64_t out_cap,
+                       uint64_t *rec_offsets, uint32_t flags,
+                       uint64_t *out_len);
+
+/* ---- decode ------------------------------------------------------------------ */
+/* Decode n records from `in` (in_len bytes) into native columns.
+ * rec_offsets (n+1 entries): record i occupies [rec_offsets[i],
+ * rec_offsets[i+1]) (its mark first when XDRG_FRAME_RM); NULL is allowed for
+ * fixed-size schemas (records back to back at the fixed stride).  Records
+ * are decoded independently with the reference's check order
+ * (Xdr.java:171-531, 1028-1037); trailing bytes inside a record's extent are
+ * ignored as RpcCall.retrieveCall does (RpcCall.java:351-354).  On error the
+ * status is returned, *first_bad = the smallest failing record index and
+ * *err = its code — what a sequential reference decode would throw first.
+ * Columns of records before first_bad hold their decoded values.           */
+int  xdrg_decode_batch(xdrg_ctx *ctx, const xdrg_schema *schema,
+                       const uint8_t *in, uint64_t in_len,
+                       const uint64_t *rec_offsets, uint64_t n,
+                       xdrg_column *cols, uint32_t flags,
+                       uint64_t *first_bad, int *err);
+
+/* ---- framing (receive side) ----------------------------------------------------- */
+/* Walk the record marks of a TCP byte stream (RpcMessageParserTCP.java:63-99):
+ * writes msg_offsets[k] = offset of message k's first mark for every complete
+ * message (all fragments present), msg_offsets[*n_msgs] = offset just past the
+ * last complete message (the "reminder" split point, :57-58).  Returns
+ * XDRG_OK, or XDRG_E_INCOMPLETE when no complete message is present (STOP).
+ * `in` is a device pointer; msg_offsets is a device array of cap+1 entries;
+ * *n_msgs is a host pointer.                                                     */
+int  xdrg_frame_scan(xdrg_ctx *ctx, const uint8_t *in, uint64_t len,
+                     uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XDRG_H */

@@ -1,0 +1,380 @@
+// kernels_fixed.hip — fixed-size record kernels of the MI355X XDR engine.
+//
+// A fixed-size XDR record (no dynamic field) is a sequence of 4-byte
+// big-endian words (RFC 4506 §3; oncrpc4j xdr/Xdr.java:545-548, 812-815).
+// Two kernels cover every fixed schema:
+//
+//  * k_stream_*  — the native record is word-for-word the XDR record
+//    (array-of-structs whose fields sit at their XDR word positions: int,
+//    float, hyper, double, 4-multiple opaque).  The batch is then one flat
+//    stream of 16-byte vectors; each lane byte-swaps (v_perm_b32) whole
+//    dwordx4 vectors, U vectors in flight per lane.  Pure HBM streaming: 1
+//    read + 1 write of every byte, the copy-kernel roofline.
+//
+//  * k_wordmap_* — any other fixed layout (struct-of-arrays columns,
+//    strided columns, bool/short/byte, odd opaque sizes, record marks).
+//    Each lane owns 4 consecutive XDR words (one dwordx4 of the stream) and
+//    maps each to its native column through a per-word op table held in
+//    LDS.  XDR side: coalesced 16-byte accesses; native side: per-element.
+#include <hip/hip_runtime.h>
+
+#include "xdrg_internal.h"
+
+namespace xdrg {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// Float.floatToIntBits: every NaN -> 0x7fc00000 (Xdr.java:674-676).
+__device__ __forceinline__ uint32_t canon_f32(uint32_t u) {
+    return ((u & 0x7fffffffu) > 0x7f800000u) ? 0x7fc00000u : u;
+}
+// Double.doubleToLongBits: every NaN -> 0x7ff8000000000000 (Xdr.java:685-687).
+__device__ __forceinline__ void canon_f64(uint32_t &hi, uint32_t &lo) {
+    const uint32_t h = hi & 0x7fffffffu;
+    if (h > 0x7ff00000u || (h == 0x7ff00000u && lo != 0)) { hi = 0x7ff80000u; lo = 0; }
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld4(const u32x4 *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st4(u32x4 *p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// ---------------------------------------------------------------------------
+// Streaming kernels (AoS-dense layouts).
+// ---------------------------------------------------------------------------
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_stream_bswap(const u32x4 *__restrict__ src,
+                                                      u32x4 *__restrict__ dst, uint64_t nvec) {
+    const uint64_t step = (uint64_t)gridDim.x * (256 * U);
+    for (uint64_t i = (uint64_t)blockIdx.x * (256 * U) + threadIdx.x; i < nvec; i += step) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + (uint64_t)u * 256;
+            if (k < nvec) v[u] = ld4<NT>(src + k);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + (uint64_t)u * 256;
+            if (k < nvec) {
+                u32x4 o;
+                o.x = bswap32(v[u].x); o.y = bswap32(v[u].y);
+                o.z = bswap32(v[u].z); o.w = bswap32(v[u].w);
+                st4<NT>(dst + k, o);
+            }
+        }
+    }
+}
+
+// One XDR/native word of a mixed AoS-dense record.  x[] holds the 4 words of
+// the vector; q is the record word position of x[j].  HYPER/DOUBLE pairs are
+// guaranteed (host check) to sit in one vector: HI at an even j, LO at j+1.
+__device__ __forceinline__ uint32_t stream_word(uint8_t op, const uint32_t *x, int j) {
+    switch (op) {
+    case OP_FLOAT: return bswap32(canon_f32(x[j]));
+    case OP_HYPER_HI: return bswap32(x[j + 1]);
+    case OP_HYPER_LO: return bswap32(x[j - 1]);
+    case OP_DOUBLE_HI: { uint32_t hi = x[j + 1], lo = x[j]; canon_f64(hi, lo); return bswap32(hi); }
+    case OP_DOUBLE_LO: { uint32_t hi = x[j], lo = x[j - 1]; canon_f64(hi, lo); return bswap32(lo); }
+    case OP_OPAQUE: return x[j];
+    default: return bswap32(x[j]);
+    }
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_stream_ops(const StreamArgs a) {
+    __shared__ uint8_t sops[kMaxWords];
+    for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
+    __syncthreads();
+    const u32x4 *__restrict__ src = (const u32x4 *)a.src;
+    u32x4 *__restrict__ dst = (u32x4 *)a.dst;
+    const uint64_t step = (uint64_t)gridDim.x * (256 * U);
+    for (uint64_t i = (uint64_t)blockIdx.x * (256 * U) + threadIdx.x; i < a.nvec; i += step) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + (uint64_t)u * 256;
+            if (k < a.nvec) v[u] = ld4<NT>(src + k);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t k = i + (uint64_t)u * 256;
+            if (k < a.nvec) {
+                uint32_t p = (uint32_t)((k * 4) % a.w);
+                const uint32_t x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                uint32_t o[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    o[j] = stream_word(sops[p], x, j);
+                    if (++p == a.w) p = 0;
+                }
+                u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+                st4<NT>(dst + k, ov);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Word-map kernels (any fixed layout).
+// ---------------------------------------------------------------------------
+struct WordMapShared {
+    WordOp ops[kMaxWords];
+    uint8_t *base[kMaxCols];
+    int64_t stride[kMaxCols];
+};
+
+__device__ __forceinline__ void wordmap_stage(const WordMapArgs &a, WordMapShared &s) {
+    for (int t = threadIdx.x; t < (int)a.nops; t += blockDim.x) s.ops[t] = a.ops[t];
+    if (threadIdx.x < kMaxCols) {
+        s.base[threadIdx.x] = a.base[threadIdx.x];
+        s.stride[threadIdx.x] = a.stride[threadIdx.x];
+    }
+    __syncthreads();
+}
+
+// Encode one XDR word of record r (Xdr.java encoders, see WordOpKind).
+__device__ __forceinline__ uint32_t enc_word(const WordMapShared &s, const WordOp o, uint64_t r,
+                                             uint32_t mark) {
+    if (o.op == OP_MARK) return mark;
+    const uint8_t *p = s.base[o.col] + (int64_t)r * s.stride[o.col] + o.off;
+    switch (o.op) {
+    case OP_BSWAP: return bswap32(*(const uint32_t *)p);
+    case OP_FLOAT: return bswap32(canon_f32(*(const uint32_t *)p));
+    case OP_HYPER_HI: return bswap32(*(const uint32_t *)(p + 4));
+    case OP_HYPER_LO: return bswap32(*(const uint32_t *)p);
+    case OP_DOUBLE_HI:
+    case OP_DOUBLE_LO: {
+        uint32_t lo = *(const uint32_t *)p, hi = *(const uint32_t *)(p + 4);
+        canon_f64(hi, lo);
+        return bswap32(o.op == OP_DOUBLE_HI ? hi : lo);
+    }
+    case OP_BOOL: return *p ? 0x01000000u : 0u;
+    case OP_SHORT: return bswap32((uint32_t)(int32_t)*(const int16_t *)p);
+    case OP_BYTE: return bswap32((uint32_t)(int32_t)*(const int8_t *)p);
+    case OP_OPAQUE: {
+        uint32_t v = 0;
+        for (uint32_t b = 0; b < o.aux; ++b) v |= (uint32_t)p[b] << (8 * b);
+        return v;
+    }
+    default: return 0;
+    }
+}
+
+// Decode one XDR word v of record r into its native column.
+__device__ __forceinline__ void dec_word(const WordMapShared &s, const WordOp o, uint64_t r,
+                                         uint32_t w, uint32_t v, const WordMapArgs &a) {
+    if (o.op == OP_MARK) {
+        if (v != a.mark_le) atomicMin(a.errkey, err_key(r, w, XDRG_E_FRAME));
+        return;
+    }
+    uint8_t *p = s.base[o.col] + (int64_t)r * s.stride[o.col] + o.off;
+    switch (o.op) {
+    case OP_BSWAP:
+    case OP_FLOAT:      // intBitsToFloat keeps the raw bits (Xdr.java:255-257)
+    case OP_HYPER_LO:
+    case OP_DOUBLE_LO: *(uint32_t *)p = bswap32(v); break;
+    case OP_HYPER_HI:
+    case OP_DOUBLE_HI: *(uint32_t *)(p + 4) = bswap32(v); break;
+    case OP_BOOL: *p = v != 0; break;
+    case OP_SHORT: *(uint16_t *)p = (uint16_t)bswap32(v); break;
+    case OP_BYTE: *p = (uint8_t)bswap32(v); break;
+    case OP_OPAQUE:
+        for (uint32_t b = 0; b < o.aux; ++b) p[b] = (uint8_t)(v >> (8 * b));
+        break;
+    default: break;
+    }
+}
+
+template <bool A16>
+__global__ __launch_bounds__(256) void k_wordmap_encode(const WordMapArgs a) {
+    __shared__ WordMapShared s;
+    wordmap_stage(a, s);
+    const uint64_t total = a.n * a.wt;
+    const uint64_t nchunks = (total + 3) >> 2;
+    const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    uint64_t r = (c * 4) / a.wt;
+    uint32_t w = (uint32_t)(c * 4 - r * a.wt);
+    for (; c < nchunks; c += S) {
+        uint32_t v[4];
+        uint64_t rr = r;
+        uint32_t ww = w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] = rr < a.n ? enc_word(s, s.ops[ww], rr, a.mark_le) : 0u;
+            if (++ww == a.wt) { ww = 0; ++rr; }
+        }
+        const uint64_t g = c * 4;
+        if (A16 && g + 4 <= total) {
+            u32x4 o; o.x = v[0]; o.y = v[1]; o.z = v[2]; o.w = v[3];
+            *(u32x4 *)(a.xdr + g * 4) = o;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (g + j < total) *(uint32_t *)(a.xdr + (g + j) * 4) = v[j];
+        }
+        r += a.dr; w += a.dw;
+        if (w >= a.wt) { w -= a.wt; ++r; }
+    }
+}
+
+template <bool A16>
+__global__ __launch_bounds__(256) void k_wordmap_decode(const WordMapArgs a) {
+    __shared__ WordMapShared s;
+    wordmap_stage(a, s);
+    const uint64_t total = a.n * a.wt;
+    const uint64_t avail = a.xdr_len >> 2;  // whole words present in the input
+    const uint64_t valid = total < avail ? total : avail;
+    const uint64_t nchunks = (valid + 3) >> 2;
+    const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    uint64_t r = (c * 4) / a.wt;
+    uint32_t w = (uint32_t)(c * 4 - r * a.wt);
+    for (; c < nchunks; c += S) {
+        const uint64_t g = c * 4;
+        uint32_t v[4];
+        if (A16 && g + 4 <= valid) {
+            const u32x4 x = *(const u32x4 *)(a.xdr + g * 4);
+            v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                v[j] = g + j < valid ? *(const uint32_t *)(a.xdr + (g + j) * 4) : 0u;
+        }
+        uint64_t rr = r;
+        uint32_t ww = w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (g + j < valid) dec_word(s, s.ops[ww], rr, ww, v[j], a);
+            if (++ww == a.wt) { ww = 0; ++rr; }
+        }
+        r += a.dr; w += a.dw;
+        if (w >= a.wt) { w -= a.wt; ++r; }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launchers.
+// ---------------------------------------------------------------------------
+static int g_num_cu = 0;
+static int num_cu() {
+    if (!g_num_cu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&g_num_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            g_num_cu <= 0)
+            g_num_cu = 256;
+    }
+    return g_num_cu;
+}
+
+static uint64_t grid_for(uint64_t work_items, uint64_t per_block, uint64_t max_blocks) {
+    uint64_t b = (work_items + per_block - 1) / per_block;
+    if (b > max_blocks) b = max_blocks;
+    return b ? b : 1;
+}
+
+// variant bits: 0x1 = nontemporal, 0x2 = op table (mixed types)
+int launch_stream_words(const StreamArgs &a, int variant, void *stream) {
+    if (!a.nvec) return hipSuccess;
+    hipStream_t st = (hipStream_t)stream;
+    constexpr int U = 4;
+    const uint64_t blocks = grid_for(a.nvec, 256 * U, (uint64_t)num_cu() * 16);
+    const bool nt = variant & 1;
+    if (a.all_bswap) {
+        const u32x4 *src = (const u32x4 *)a.src;
+        u32x4 *dst = (u32x4 *)a.dst;
+        if (nt) hipLaunchKernelGGL((k_stream_bswap<U, true>), dim3(blocks), dim3(256), 0, st, src, dst, a.nvec);
+        else hipLaunchKernelGGL((k_stream_bswap<U, false>), dim3(blocks), dim3(256), 0, st, src, dst, a.nvec);
+    } else {
+        if (nt) hipLaunchKernelGGL((k_stream_ops<U, true>), dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_stream_ops<U, false>), dim3(blocks), dim3(256), 0, st, a);
+    }
+    return (int)hipGetLastError();
+}
+
+static void wordmap_grid(WordMapArgs &a, uint64_t words, uint64_t *blocks) {
+    const uint64_t chunks = (words + 3) >> 2;
+    *blocks = grid_for(chunks, 256, (uint64_t)num_cu() * 16);
+    const uint64_t adv = *blocks * 256 * 4;  // words advanced per grid-stride step
+    a.dr = adv / a.wt;
+    a.dw = (uint32_t)(adv % a.wt);
+}
+
+int launch_wordmap_encode(const WordMapArgs &args, bool aligned16, void *stream) {
+    WordMapArgs a = args;
+    if (!a.n) return hipSuccess;
+    uint64_t blocks;
+    wordmap_grid(a, a.n * a.wt, &blocks);
+    hipStream_t st = (hipStream_t)stream;
+    if (aligned16) hipLaunchKernelGGL(k_wordmap_encode<true>, dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_wordmap_encode<false>, dim3(blocks), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+int launch_wordmap_decode(const WordMapArgs &args, bool aligned16, void *stream) {
+    WordMapArgs a = args;
+    const uint64_t total = a.n * a.wt, avail = a.xdr_len >> 2;
+    const uint64_t valid = total < avail ? total : avail;
+    if (!valid) return hipSuccess;
+    uint64_t blocks;
+    wordmap_grid(a, valid, &blocks);
+    hipStream_t st = (hipStream_t)stream;
+    if (aligned16) hipLaunchKernelGGL(k_wordmap_decode<true>, dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_wordmap_decode<false>, dim3(blocks), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+}  // namespace xdrg
+
+namespace xdrg {
+
+__global__ void k_iota(uint64_t *dst, uint64_t n, uint64_t stride) {
+    const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += S) dst[i] = i * stride;
+}
+
+int launch_iota(uint64_t *dst, uint64_t n, uint64_t stride, void *stream) {
+    const uint64_t blocks = grid_for(n + 1, 256, (uint64_t)num_cu() * 8);
+    hipLaunchKernelGGL(k_iota, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dst, n, stride);
+    return (int)hipGetLastError();
+}
+
+__global__ void k_finalize(const unsigned long long *errkey, unsigned long long extra, uint64_t n,
+                           uint64_t *first_bad, int *err) {
+    if (threadIdx.x || blockIdx.x) return;
+    unsigned long long k = errkey ? *errkey : kNoError;
+    if (extra < k) k = extra;
+    if (first_bad) *first_bad = k == kNoError ? n : (uint64_t)(k >> 16);
+    if (err) *err = k == kNoError ? 0 : (int)(k & 0xf);
+}
+
+int launch_finalize(const unsigned long long *errkey, unsigned long long extra_key, uint64_t n,
+                    uint64_t *first_bad, int *err, void *stream) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, (hipStream_t)stream, errkey, extra_key, n,
+                       first_bad, err);
+    return (int)hipGetLastError();
+}
+
+}  // namespace xdrg
+
+namespace xdrg {
+__global__ void k_store_u64(uint64_t *dst, uint64_t v) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *dst = v;
+}
+int launch_store_u64(uint64_t *dst, uint64_t value, void *stream) {
+    hipLaunchKernelGGL(k_store_u64, dim3(1), dim3(64), 0, (hipStream_t)stream, dst, value);
+    return (int)hipGetLastError();
+}
+}  // namespace xdrg

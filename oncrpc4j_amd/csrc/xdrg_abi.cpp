@@ -1,0 +1,662 @@
+// xdrg_abi.cpp — host side of libxdrgpu.so: the C-ABI of include/xdrg.h.
+//
+// Owns schema compilation (rpcgen field tape -> word program / record
+// descriptors), per-call validation with the reference's error contract,
+// path selection (streaming / word-map / record path), device workspace and
+// per-kernel HIP-event timing.  Every entry point cites the reference
+// interface it replaces in include/xdrg.h.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "xdrg_internal.h"
+
+using namespace xdrg;
+
+// ---------------------------------------------------------------------------
+// schema
+// ---------------------------------------------------------------------------
+struct xdrg_schema {
+    std::vector<xdrg_field> f;
+    std::vector<uint32_t> nsz;      // native element bytes per field
+    std::vector<uint32_t> xsz;      // XDR element bytes per field (1 = bytes)
+    std::vector<uint32_t> xbytes;   // fixed fields: XDR bytes of the field
+    std::vector<uint32_t> wpos;     // fixed fields: XDR word position in the record
+    std::vector<WordOp> ops;        // fixed schemas: one op per XDR word
+    uint64_t fixed_size = 0;        // XDR bytes per record (no dynamic field), else 0
+    uint64_t fixed_part = 0;        // XDR bytes of the fixed fields
+    bool has_dyn = false;
+    bool stream_types = true;       // every field is word-for-word (int/float/hyper/double/opaque%4)
+    uint32_t nwords = 0;
+};
+
+static uint32_t native_size(uint32_t t) {
+    switch (t) {
+    case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: case XDRG_T_FLOAT: return 4;
+    case XDRG_T_HYPER: case XDRG_T_UHYPER: case XDRG_T_DOUBLE: return 8;
+    case XDRG_T_SHORT: return 2;
+    case XDRG_T_BYTE: case XDRG_T_BOOL: case XDRG_T_OPAQUE: case XDRG_T_STRING: return 1;
+    default: return 0;
+    }
+}
+static uint32_t xdr_elem_size(uint32_t t) {
+    switch (t) {
+    case XDRG_T_HYPER: case XDRG_T_UHYPER: case XDRG_T_DOUBLE: return 8;
+    case XDRG_T_OPAQUE: case XDRG_T_STRING: return 1;
+    default: return native_size(t) ? 4 : 0;
+    }
+}
+// (type, kind) pairs rpcgen emits against the Xdr surface (jrpcgen.java:661-739).
+static bool field_valid(const xdrg_field &f) {
+    if (!native_size(f.type) || f.kind > XDRG_K_DYNAMIC || f.reserved) return false;
+    if (f.type == XDRG_T_BOOL && f.kind != XDRG_K_SCALAR) return false;
+    if (f.type == XDRG_T_STRING && f.kind != XDRG_K_DYNAMIC) return false;
+    if (f.type == XDRG_T_OPAQUE && f.kind == XDRG_K_SCALAR) return false;
+    if (f.kind == XDRG_K_FIXED && f.count > 0x7fffffffu) return false;
+    return true;
+}
+static uint8_t scalar_op(uint32_t t, bool second_half) {
+    switch (t) {
+    case XDRG_T_FLOAT: return OP_FLOAT;
+    case XDRG_T_HYPER: case XDRG_T_UHYPER: return second_half ? OP_HYPER_LO : OP_HYPER_HI;
+    case XDRG_T_DOUBLE: return second_half ? OP_DOUBLE_LO : OP_DOUBLE_HI;
+    case XDRG_T_BOOL: return OP_BOOL;
+    case XDRG_T_SHORT: return OP_SHORT;
+    case XDRG_T_BYTE: return OP_BYTE;
+    default: return OP_BSWAP;
+    }
+}
+
+extern "C" int xdrg_schema_create(const xdrg_field *fields, size_t nfields, xdrg_schema **out) {
+    if (!out) return XDRG_E_INVAL;
+    *out = nullptr;
+    if (!fields || !nfields || nfields > (size_t)kMaxFields) return XDRG_E_INVAL;
+    xdrg_schema *s = new (std::nothrow) xdrg_schema();
+    if (!s) return XDRG_E_NOMEM;
+    uint64_t words = 0;
+    for (size_t k = 0; k < nfields; ++k) {
+        const xdrg_field &f = fields[k];
+        if (!field_valid(f)) { delete s; return XDRG_E_INVAL; }
+        s->f.push_back(f);
+        s->nsz.push_back(native_size(f.type));
+        s->xsz.push_back(xdr_elem_size(f.type));
+        s->wpos.push_back((uint32_t)words);
+        if (f.kind == XDRG_K_DYNAMIC) {
+            s->has_dyn = true;
+            s->xbytes.push_back(0);
+            s->stream_types = false;
+            continue;
+        }
+        const uint64_t cnt = f.kind == XDRG_K_FIXED ? f.count : 1;
+        uint64_t xb;
+        if (f.type == XDRG_T_OPAQUE) {
+            xb = cnt + ((4 - (cnt & 3)) & 3);  // Xdr.java:776-781
+            if (cnt & 3) s->stream_types = false;
+            for (uint64_t i = 0; i < xb / 4 && words + i < kMaxWords; ++i) {
+                const uint64_t rem = cnt - 4 * i;
+                s->ops.push_back({OP_OPAQUE, (uint8_t)k, (uint8_t)(rem < 4 ? rem : 4), 0, (uint32_t)(4 * i)});
+            }
+        } else {
+            const uint32_t xs = xdr_elem_size(f.type), ns = native_size(f.type);
+            xb = cnt * xs;
+            if (ns != xs) s->stream_types = false;  // bool/short/byte widen on the wire
+            for (uint64_t e = 0; e < cnt && words + (e * xs) / 4 < kMaxWords; ++e) {
+                s->ops.push_back({scalar_op(f.type, false), (uint8_t)k, 0, 0, (uint32_t)(e * ns)});
+                if (xs == 8) s->ops.push_back({scalar_op(f.type, true), (uint8_t)k, 0, 0, (uint32_t)(e * ns)});
+            }
+        }
+        if (xb > 0xffffffffull) { delete s; return XDRG_E_INVAL; }
+        s->xbytes.push_back((uint32_t)xb);
+        s->fixed_part += xb;
+        words += xb / 4;
+    }
+    s->nwords = (uint32_t)(words < 0xffffffffull ? words : 0xffffffffull);
+    s->fixed_size = s->has_dyn ? 0 : s->fixed_part;
+    if (s->has_dyn || words > kMaxWords) s->ops.clear();
+    *out = s;
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_schema_destroy(xdrg_schema *s) {
+    delete s;
+    return XDRG_OK;
+}
+
+extern "C" uint64_t xdrg_schema_fixed_size(const xdrg_schema *s) { return s ? s->fixed_size : 0; }
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct Timed {
+    int kernel;
+    hipEvent_t a, b;
+};
+
+struct xdrg_ctx {
+    int device = 0;
+    uint32_t flags = 0;
+    hipStream_t stream = nullptr;
+    // device status block: [0] error key, [1] frame-scan result
+    unsigned long long *d_stat = nullptr;
+    unsigned long long *h_stat = nullptr;  // pinned mirror
+    uint64_t *d_ws = nullptr;
+    size_t ws_words = 0;
+    std::string err;
+    std::deque<Timed> pending;
+    std::vector<hipEvent_t> pool;
+    uint64_t launches[XDRG_KERNEL_COUNT] = {};
+    double ms[XDRG_KERNEL_COUNT] = {};
+};
+
+static int hip_fail(xdrg_ctx *c, hipError_t e, const char *what) {
+    if (c) {
+        char buf[256];
+        snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+        c->err = buf;
+    }
+    return XDRG_E_HIP;
+}
+static int inval(xdrg_ctx *c, const char *what) {
+    if (c) c->err = what;
+    return XDRG_E_INVAL;
+}
+#define HIPCHK(c, x)                                       \
+    do {                                                   \
+        hipError_t e_ = (x);                               \
+        if (e_ != hipSuccess) return hip_fail(c, e_, #x);  \
+    } while (0)
+
+static hipEvent_t ev_get(xdrg_ctx *c) {
+    if (!c->pool.empty()) {
+        hipEvent_t e = c->pool.back();
+        c->pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+static void resolve_one(xdrg_ctx *c) {
+    Timed t = c->pending.front();
+    c->pending.pop_front();
+    float ms = 0.f;
+    if (hipEventSynchronize(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+        c->launches[t.kernel] += 1;
+        c->ms[t.kernel] += ms;
+    }
+    c->pool.push_back(t.a);
+    c->pool.push_back(t.b);
+}
+
+// Bracket one launch with timing events when XDRG_CTX_TIMING is set.
+struct TimedLaunch {
+    xdrg_ctx *c;
+    int kernel;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimedLaunch(xdrg_ctx *c_, int k) : c(c_), kernel(k) {
+        if (!(c->flags & XDRG_CTX_TIMING)) return;
+        if (c->pending.size() > 4096) resolve_one(c);
+        a = ev_get(c);
+        b = ev_get(c);
+        if (a) (void)hipEventRecord(a, c->stream);
+    }
+    ~TimedLaunch() {
+        if (!a || !b) return;
+        (void)hipEventRecord(b, c->stream);
+        c->pending.push_back({kernel, a, b});
+    }
+};
+
+extern "C" int xdrg_abi_version(void) { return XDRG_ABI_VERSION; }
+
+extern "C" const char *xdrg_status_string(int status) {
+    switch (status) {
+    case XDRG_OK: return "ok";
+    case XDRG_E_SHORT: return "xdr stream too short";        // Xdr.java:1030
+    case XDRG_E_CORRUPT: return "corrupted xdr";              // Xdr.java:1036
+    case XDRG_E_FIXED_LEN: return "array size does not match protocol specification";  // :625-627
+    case XDRG_E_CAPACITY: return "output buffer too small";
+    case XDRG_E_FRAME: return "record mark does not frame the record";
+    case XDRG_E_INVAL: return "invalid argument";
+    case XDRG_E_HIP: return "HIP runtime error";
+    case XDRG_E_NOMEM: return "out of memory";
+    case XDRG_E_INCOMPLETE: return "not all fragments arrived";
+    default: return "unknown status";
+    }
+}
+
+extern "C" const char *xdrg_last_error(xdrg_ctx *c) { return c ? c->err.c_str() : ""; }
+
+extern "C" int xdrg_ctx_create(int device, uint32_t flags, xdrg_ctx **out) {
+    if (!out) return XDRG_E_INVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return XDRG_E_HIP;
+    if (hipSetDevice(device) != hipSuccess) return XDRG_E_HIP;
+    xdrg_ctx *c = new (std::nothrow) xdrg_ctx();
+    if (!c) return XDRG_E_NOMEM;
+    c->device = device;
+    c->flags = flags;
+    if (hipMalloc(&c->d_stat, 64) != hipSuccess ||
+        hipHostMalloc(&c->h_stat, 64, hipHostMallocDefault) != hipSuccess) {
+        if (c->d_stat) (void)hipFree(c->d_stat);
+        delete c;
+        return XDRG_E_HIP;
+    }
+    *out = c;
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_ctx_destroy(xdrg_ctx *c) {
+    if (!c) return XDRG_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    while (!c->pending.empty()) resolve_one(c);
+    for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
+    if (c->d_ws) (void)hipFree(c->d_ws);
+    if (c->d_stat) (void)hipFree(c->d_stat);
+    if (c->h_stat) (void)hipHostFree(c->h_stat);
+    delete c;
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_ctx_set_stream(xdrg_ctx *c, void *stream) {
+    if (!c) return XDRG_E_INVAL;
+    c->stream = (hipStream_t)stream;
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_ctx_kernel_stats(xdrg_ctx *c, int kernel, uint64_t *launches, double *total_ms) {
+    if (!c || kernel < 0 || kernel >= XDRG_KERNEL_COUNT) return XDRG_E_INVAL;
+    (void)hipSetDevice(c->device);
+    while (!c->pending.empty()) resolve_one(c);
+    if (launches) *launches = c->launches[kernel];
+    if (total_ms) *total_ms = c->ms[kernel];
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_ctx_reset_stats(xdrg_ctx *c) {
+    if (!c) return XDRG_E_INVAL;
+    (void)hipSetDevice(c->device);
+    while (!c->pending.empty()) resolve_one(c);
+    for (int k = 0; k < XDRG_KERNEL_COUNT; ++k) { c->launches[k] = 0; c->ms[k] = 0; }
+    return XDRG_OK;
+}
+
+static int ensure_ws(xdrg_ctx *c, size_t words) {
+    if (words <= c->ws_words) return XDRG_OK;
+    if (c->d_ws) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(c->d_ws));
+        c->d_ws = nullptr;
+        c->ws_words = 0;
+    }
+    HIPCHK(c, hipMalloc(&c->d_ws, words * sizeof(uint64_t)));
+    c->ws_words = words;
+    return XDRG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+static inline bool aligned(const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
+
+static int64_t eff_stride(const xdrg_schema *s, size_t k, const xdrg_column &col) {
+    if (col.stride) return col.stride;
+    const uint64_t cnt = s->f[k].kind == XDRG_K_FIXED ? s->f[k].count : 1;
+    return (int64_t)(s->nsz[k] * cnt);
+}
+
+// Native element alignment the kernels rely on (4-byte units for hyper/double).
+static int check_columns(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
+                         bool decode) {
+    if (!cols) return inval(c, "columns are NULL");
+    for (size_t k = 0; k < s->f.size(); ++k) {
+        const xdrg_field &f = s->f[k];
+        const uint32_t al = s->nsz[k] >= 4 ? 4 : s->nsz[k];
+        if (f.kind == XDRG_K_DYNAMIC) {
+            if (!cols[k].offsets) return inval(c, "dynamic column without offsets");
+            if (n && !cols[k].data && !decode) { /* all-empty columns may have no data */ }
+            if (!aligned(cols[k].data, al)) return inval(c, "dynamic column data misaligned");
+        } else {
+            const int64_t st = eff_stride(s, k, cols[k]);
+            if (s->xbytes[k] && n && !cols[k].data) return inval(c, "fixed column data is NULL");
+            if (!aligned(cols[k].data, al) || (st % (int64_t)al)) return inval(c, "fixed column misaligned");
+        }
+    }
+    return XDRG_OK;
+}
+
+// Streaming path eligibility: unframed, array-of-structs whose fields sit at
+// their XDR word positions, 16-byte aligned ends, 2-word types even-aligned.
+static bool stream_eligible(const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
+                            const void *xdr, const uint8_t **base_out) {
+    if (s->has_dyn || !s->stream_types || s->ops.empty() || !s->nwords) return false;
+    if (((n * s->nwords) & 3) != 0) return false;
+    const int64_t rec = (int64_t)s->nwords * 4;
+    const uint8_t *base = nullptr;
+    for (size_t k = 0; k < s->f.size(); ++k) {
+        if (!s->xbytes[k]) continue;
+        const uint8_t *b = (const uint8_t *)cols[k].data - 4 * (uint64_t)s->wpos[k];
+        if (!base) base = b;
+        if (b != base) return false;
+        if (eff_stride(s, k, cols[k]) != rec) return false;
+    }
+    if (!base || !aligned(base, 16) || !aligned(xdr, 16)) return false;
+    for (size_t w = 0; w < s->ops.size(); ++w) {
+        const uint8_t op = s->ops[w].op;
+        if ((op == OP_HYPER_HI || op == OP_DOUBLE_HI) && ((w & 1) || (s->nwords & 1))) return false;
+    }
+    *base_out = base;
+    return true;
+}
+
+static void fill_stream_ops(const xdrg_schema *s, bool decode, StreamArgs &a) {
+    a.all_bswap = 1;
+    for (size_t w = 0; w < s->ops.size(); ++w) {
+        uint8_t op = s->ops[w].op;
+        if (decode) {  // decode keeps raw float/double bits (Xdr.java:255-269)
+            if (op == OP_FLOAT) op = OP_BSWAP;
+            else if (op == OP_DOUBLE_HI) op = OP_HYPER_HI;
+            else if (op == OP_DOUBLE_LO) op = OP_HYPER_LO;
+        }
+        a.ops[w] = op;
+        if (op != OP_BSWAP) a.all_bswap = 0;
+    }
+}
+
+static void fill_wordmap(const xdrg_schema *s, const xdrg_column *cols, bool framed, WordMapArgs &a) {
+    memset(&a, 0, sizeof a);
+    uint32_t w = 0;
+    if (framed) a.ops[w++] = {OP_MARK, 0, 0, 0, 0};
+    for (const WordOp &o : s->ops) a.ops[w++] = o;
+    a.wt = w;
+    a.nops = w;
+    const uint32_t m = (uint32_t)(s->fixed_size | kLastFrag);
+    a.mark_le = __builtin_bswap32(m);
+    for (size_t k = 0; k < s->f.size(); ++k) {
+        a.base[k] = (uint8_t *)cols[k].data;
+        a.stride[k] = eff_stride(s, k, cols[k]);
+    }
+}
+
+static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64_t n, bool framed,
+                    RecArgs &a) {
+    memset(&a, 0, sizeof a);
+    a.n = n;
+    a.nf = (uint32_t)s->f.size();
+    a.framed = framed;
+    a.fixed_xdr = (uint32_t)(s->fixed_part + (framed ? 4 : 0));
+    for (size_t k = 0; k < s->f.size(); ++k) {
+        VField &v = a.f[k];
+        const xdrg_field &f = s->f[k];
+        v.type = (uint8_t)f.type;
+        v.kind = (uint8_t)f.kind;
+        v.nsz = (uint8_t)s->nsz[k];
+        v.xsz = (uint8_t)s->xsz[k];
+        v.count = f.count;
+        v.xbytes = s->xbytes[k];
+        v.data = (uint8_t *)cols[k].data;
+        v.stride = f.kind == XDRG_K_DYNAMIC ? 0 : eff_stride(s, k, cols[k]);
+        v.offsets = cols[k].offsets;
+        v.cap = cols[k].cap;
+        if (f.kind == XDRG_K_DYNAMIC) a.dyn_idx[a.ndyn++] = (uint8_t)k;
+    }
+    a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;
+    if (!a.nblocks) a.nblocks = 1;
+    const size_t rows = a.ndyn ? a.ndyn : 1;
+    int rc = ensure_ws(c, rows * a.nblocks + rows + 8);
+    if (rc) return rc;
+    a.block_sums = c->d_ws;
+    a.totals = c->d_ws + rows * a.nblocks;
+    a.errkey = c->d_stat;
+    return XDRG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// encode
+// ---------------------------------------------------------------------------
+extern "C" int xdrg_encode_batch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols,
+                                 uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_offsets,
+                                 uint32_t flags, uint64_t *out_len) {
+    if (!c || !s) return XDRG_E_INVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool framed = flags & XDRG_FRAME_RM;
+    const bool async = flags & XDRG_ASYNC;
+    if (!aligned(out, 4)) return inval(c, "XDR buffer not 4-byte aligned");
+    if (n && !out) return inval(c, "XDR buffer is NULL");
+    int rc = check_columns(c, s, cols, n, false);
+    if (rc) return rc;
+
+    if (!s->has_dyn) {
+        const uint64_t stride = s->fixed_size + (framed ? 4 : 0);
+        const uint64_t total = n * stride;
+        if (n && total / n != stride) return inval(c, "batch size overflows");
+        if (total > out_cap) {
+            if (out_len && !async) *out_len = total;
+            c->err = "output buffer too small";
+            return XDRG_E_CAPACITY;
+        }
+        if (rec_offsets) {
+            TimedLaunch t(c, XDRG_KERNEL_FIXED_ENCODE);
+            HIPCHK(c, (hipError_t)launch_iota(rec_offsets, n, stride, c->stream));
+        }
+        const uint8_t *base = nullptr;
+        if (n && !framed && stream_eligible(s, cols, n, out, &base)) {
+            StreamArgs a;
+            memset(&a, 0, sizeof a);
+            a.src = base;
+            a.dst = out;
+            a.nvec = total / 16;
+            a.w = s->nwords;
+            fill_stream_ops(s, false, a);
+            TimedLaunch t(c, XDRG_KERNEL_FIXED_ENCODE);
+            HIPCHK(c, (hipError_t)launch_stream_words(a, 0, c->stream));
+        } else if (n && s->nwords + (framed ? 1 : 0) <= (uint32_t)kMaxWords && !s->ops.empty() &&
+                   s->f.size() <= (size_t)kMaxCols) {
+            WordMapArgs a;
+            fill_wordmap(s, cols, framed, a);
+            a.n = n;
+            a.xdr = out;
+            TimedLaunch t(c, XDRG_KERNEL_FIXED_ENCODE);
+            HIPCHK(c, (hipError_t)launch_wordmap_encode(a, aligned(out, 16), c->stream));
+        } else if (n && total) {
+            RecArgs a;
+            rc = fill_rec(c, s, (xdrg_column *)cols, n, framed, a);
+            if (rc) return rc;
+            a.xdr = out;
+            a.xdr_cap = out_cap;
+            a.rec_out = nullptr;
+            for (int ph = REC_ENC_SIZES; ph <= REC_ENC_PLACE; ++ph) {
+                TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE + ph);
+                HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+            }
+        }
+        if (out_len) {
+            if (async) HIPCHK(c, (hipError_t)launch_store_u64(out_len, total, c->stream));
+            else *out_len = total;
+        }
+        if (!async) HIPCHK(c, hipStreamSynchronize(c->stream));
+        return XDRG_OK;
+    }
+
+    // variable-size records: size -> scan -> place
+    if (n == 0) {
+        if (rec_offsets) HIPCHK(c, hipMemsetAsync(rec_offsets, 0, 8, c->stream));
+        if (out_len && !async) *out_len = 0;
+        if (out_len && async) HIPCHK(c, (hipError_t)launch_store_u64(out_len, 0, c->stream));
+        if (!async) HIPCHK(c, hipStreamSynchronize(c->stream));
+        return XDRG_OK;
+    }
+    RecArgs a;
+    rc = fill_rec(c, s, (xdrg_column *)cols, n, framed, a);
+    if (rc) return rc;
+    a.xdr = out;
+    a.xdr_cap = out_cap;
+    a.rec_out = rec_offsets;
+    for (int ph = REC_ENC_SIZES; ph <= REC_ENC_PLACE; ++ph) {
+        TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE + ph);
+        HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+    }
+    if (async) {
+        if (out_len) HIPCHK(c, hipMemcpyAsync(out_len, a.totals, 8, hipMemcpyDeviceToDevice, c->stream));
+        return XDRG_OK;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->h_stat, a.totals, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t total = c->h_stat[0];
+    if (out_len) *out_len = total;
+    if (total > out_cap) {
+        c->err = "output buffer too small";
+        return XDRG_E_CAPACITY;
+    }
+    return XDRG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// decode
+// ---------------------------------------------------------------------------
+static int rec_dec_kernel_id(int ph) {
+    return ph == REC_DEC_SIZES ? XDRG_KERNEL_VAR_SIZE
+         : ph == REC_DEC_SCAN ? XDRG_KERNEL_VAR_SCAN : XDRG_KERNEL_VAR_DECODE;
+}
+
+static int finish_decode(xdrg_ctx *c, uint64_t n, unsigned long long host_key, bool used_dev_key,
+                         bool async, uint64_t *first_bad, int *err) {
+    if (async) {
+        if (first_bad || err)
+            HIPCHK(c, (hipError_t)launch_finalize(used_dev_key ? c->d_stat : nullptr, host_key, n,
+                                                  first_bad, err, c->stream));
+        return XDRG_OK;
+    }
+    unsigned long long key = host_key;
+    if (used_dev_key) {
+        HIPCHK(c, hipMemcpyAsync(c->h_stat, c->d_stat, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->h_stat[0] < key) key = c->h_stat[0];
+    } else {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (key == kNoError) {
+        if (first_bad) *first_bad = n;
+        if (err) *err = XDRG_OK;
+        return XDRG_OK;
+    }
+    const int code = (int)(key & 0xf);
+    if (first_bad) *first_bad = (uint64_t)(key >> 16);
+    if (err) *err = code;
+    c->err = xdrg_status_string(code);
+    return code;
+}
+
+extern "C" int xdrg_decode_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in,
+                                 uint64_t in_len, const uint64_t *rec_offsets, uint64_t n,
+                                 xdrg_column *cols, uint32_t flags, uint64_t *first_bad, int *err) {
+    if (!c || !s) return XDRG_E_INVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool framed = flags & XDRG_FRAME_RM;
+    const bool async = flags & XDRG_ASYNC;
+    if (!aligned(in, 4)) return inval(c, "XDR buffer not 4-byte aligned");
+    if (n && in_len && !in) return inval(c, "XDR buffer is NULL");
+    if (s->has_dyn && !rec_offsets) return inval(c, "variable-size schema needs record offsets");
+    int rc = check_columns(c, s, cols, n, true);
+    if (rc) return rc;
+
+    if (!s->has_dyn && !rec_offsets) {
+        const uint64_t stride = s->fixed_size + (framed ? 4 : 0);
+        const uint64_t total = n * stride;
+        if (n && total / n != stride) return inval(c, "batch size overflows");
+        // records wholly inside in_len decode; the first one that is not
+        // fails "xdr stream too short" at its first missing word (Xdr.java:1028-1031)
+        unsigned long long host_key = kNoError;
+        if (stride && in_len < total) {
+            const uint64_t rs = in_len / stride;
+            const uint64_t ws = (in_len - rs * stride) / 4;
+            host_key = err_key(rs, (uint32_t)ws, XDRG_E_SHORT);
+        }
+        bool dev_key = false;
+        const uint8_t *base = nullptr;
+        if (n && !framed && in_len >= total && stream_eligible(s, cols, n, in, &base)) {
+            StreamArgs a;
+            memset(&a, 0, sizeof a);
+            a.src = in;
+            a.dst = (uint8_t *)base;
+            a.nvec = total / 16;
+            a.w = s->nwords;
+            fill_stream_ops(s, true, a);
+            TimedLaunch t(c, XDRG_KERNEL_FIXED_DECODE);
+            HIPCHK(c, (hipError_t)launch_stream_words(a, 0, c->stream));
+        } else if (n && stride && s->nwords + (framed ? 1 : 0) <= (uint32_t)kMaxWords &&
+                   !s->ops.empty() && s->f.size() <= (size_t)kMaxCols) {
+            WordMapArgs a;
+            fill_wordmap(s, cols, framed, a);
+            a.n = n;
+            a.xdr = (uint8_t *)in;
+            a.xdr_len = in_len;
+            a.errkey = c->d_stat;
+            dev_key = framed;
+            if (dev_key) HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
+            TimedLaunch t(c, XDRG_KERNEL_FIXED_DECODE);
+            HIPCHK(c, (hipError_t)launch_wordmap_decode(a, aligned(in, 16), c->stream));
+        } else if (n && stride) {
+            RecArgs a;
+            rc = fill_rec(c, s, cols, n, framed, a);
+            if (rc) return rc;
+            a.xdr = (uint8_t *)in;
+            a.xdr_cap = in_len;
+            a.rec_in = nullptr;
+            a.rec_stride = stride;
+            HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
+            dev_key = true;
+            for (int ph = REC_DEC_SIZES; ph <= REC_DEC_PLACE; ++ph) {
+                TimedLaunch t(c, rec_dec_kernel_id(ph));
+                HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+            }
+        }
+        return finish_decode(c, n, host_key, dev_key, async, first_bad, err);
+    }
+
+    // record path: extents from rec_offsets
+    RecArgs a;
+    rc = fill_rec(c, s, cols, n, framed, a);
+    if (rc) return rc;
+    if (n == 0) {
+        for (uint32_t d = 0; d < a.ndyn; ++d)
+            HIPCHK(c, hipMemsetAsync(cols[a.dyn_idx[d]].offsets, 0, 8, c->stream));
+        return finish_decode(c, n, kNoError, false, async, first_bad, err);
+    }
+    a.xdr = (uint8_t *)in;
+    a.xdr_cap = in_len;
+    a.rec_in = rec_offsets;
+    HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
+    for (int ph = REC_DEC_SIZES; ph <= REC_DEC_PLACE; ++ph) {
+        TimedLaunch t(c, rec_dec_kernel_id(ph));
+        HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+    }
+    return finish_decode(c, n, kNoError, true, async, first_bad, err);
+}
+
+// ---------------------------------------------------------------------------
+// framing
+// ---------------------------------------------------------------------------
+extern "C" int xdrg_frame_scan(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint64_t *msg_offsets,
+                               uint64_t cap, uint64_t *n_msgs) {
+    if (!c || !msg_offsets || !n_msgs) return XDRG_E_INVAL;
+    if (len && !in) return XDRG_E_INVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    {
+        TimedLaunch t(c, XDRG_KERNEL_FRAME_SCAN);
+        HIPCHK(c, (hipError_t)launch_frame_scan(in, len, msg_offsets, cap, (uint64_t *)c->d_stat + 1,
+                                               c->stream));
+    }
+    HIPCHK(c, hipMemcpyAsync(c->h_stat + 1, c->d_stat + 1, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *n_msgs = c->h_stat[1];
+    return *n_msgs ? XDRG_OK : XDRG_E_INCOMPLETE;
+}

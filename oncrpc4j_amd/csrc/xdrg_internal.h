@@ -1,0 +1,152 @@
+// xdrg_internal.h — shared definitions of the MI355X XDR batch engine
+// (libxdrgpu.so).  Host and device code include this; nothing here crosses
+// the C-ABI (include/xdrg.h is the boundary).
+//
+// Reference semantics restated here (paths under /root/reference/
+// oncrpc4j-core/src/main/java/org/dcache/oncrpc4j/):
+//   xdr/Xdr.java:545-548 / :171-175   int  <-> 4 bytes big-endian
+//   xdr/Xdr.java:812-815 / :417-420   long <-> 8 bytes BE, high word first
+//   xdr/Xdr.java:674-687              float/double via floatToIntBits /
+//                                     doubleToLongBits (every NaN canonical)
+//   xdr/Xdr.java:803-805 / :404-407   boolean 1/0, decode any non-zero = true
+//   xdr/Xdr.java:919-936 / :485-499   byte/short sign-extended / truncated
+//   xdr/Xdr.java:776-781 / :341-349   opaque bytes + zero pad to 4
+//   grizzly/GrizzlyRpcTransport.java:103-110  record mark BE(len | LAST)
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/xdrg.h"
+
+namespace xdrg {
+
+// ---- limits of the kernel-argument descriptors --------------------------
+constexpr int kMaxWords  = 128;  // XDR words per record on the word-map path
+constexpr int kMaxCols   = 32;   // fields per schema on the word-map path
+constexpr int kMaxFields = 32;   // fields per schema on the record path
+
+constexpr uint32_t kLastFrag = 0x80000000u;  // RpcMessageParserTCP.java:37
+constexpr uint32_t kSizeMask = 0x7fffffffu;  // RpcMessageParserTCP.java:41
+
+// ---- one XDR word of a fixed-size record --------------------------------
+// Every fixed-size XDR record is a sequence of 4-byte words (RFC 4506 §3);
+// each word is produced (encode) or consumed (decode) by one WordOp that
+// names the native column, the byte offset inside that record's native
+// element run, and the conversion.
+enum WordOpKind : uint8_t {
+    OP_BSWAP = 0,     // int/uint/enum: u32 native <-> BE word
+    OP_FLOAT = 1,     // float: encode canonicalises NaN (Xdr.java:674-676)
+    OP_HYPER_HI = 2,  // long high word: native bytes [off+4, off+8)
+    OP_HYPER_LO = 3,  // long low word:  native bytes [off,   off+4)
+    OP_DOUBLE_HI = 4, // double: as HYPER, encode canonicalises NaN (:685-687)
+    OP_DOUBLE_LO = 5,
+    OP_BOOL = 6,      // native u8: encode 0/1, decode != 0 (:803, :404)
+    OP_SHORT = 7,     // native i16: sign-extend / truncate (:934, :497)
+    OP_BYTE = 8,      // native i8 : sign-extend / truncate (:919, :485)
+    OP_OPAQUE = 9,    // aux = 1..4 payload bytes copied raw, rest zero pad
+    OP_MARK = 10,     // record mark (encode: write, decode: check)
+};
+
+struct WordOp {
+    uint8_t op;
+    uint8_t col;   // field index
+    uint8_t aux;   // OP_OPAQUE: payload bytes in this word
+    uint8_t rsv;
+    uint32_t off;  // byte offset inside the record's native element run
+};
+
+// Word-map kernel arguments (passed by value; < 2 KiB of kernarg).
+struct WordMapArgs {
+    uint64_t n;                  // records
+    uint32_t wt;                 // XDR words per record (incl. mark when framed)
+    uint32_t mark_le;            // record mark as it sits in memory (BE bytes)
+    uint64_t dr;                 // grid-stride advance of the record index ...
+    uint32_t dw;                 // ... and of the word index (per 4*stride words)
+    uint32_t nops;               // == wt
+    uint8_t *xdr;                // XDR stream
+    uint64_t xdr_len;            // decode: valid input bytes
+    unsigned long long *errkey;  // decode: min error key
+    uint8_t *base[kMaxCols];     // native column bases
+    int64_t stride[kMaxCols];    // native column strides (bytes per record)
+    WordOp ops[kMaxWords];
+};
+
+// Streaming (register) kernel arguments: AoS-dense records whose native
+// layout is word-for-word the XDR layout.
+struct StreamArgs {
+    const uint8_t *src;
+    uint8_t *dst;
+    uint64_t nvec;        // 16-byte vectors
+    uint32_t w;           // words per record
+    uint32_t all_bswap;   // 1: every word is a plain byte swap
+    uint8_t ops[kMaxWords];  // per record word: OP_BSWAP/FLOAT/HYPER_*/DOUBLE_*/OPAQUE
+};
+
+// ---- record path (variable-size schemas) --------------------------------
+struct VField {
+    uint8_t type;     // XDRG_T_*
+    uint8_t kind;     // XDRG_K_*
+    uint8_t nsz;      // native element bytes
+    uint8_t xsz;      // XDR element bytes (1 for opaque/string)
+    uint32_t count;   // FIXED count
+    uint32_t xbytes;  // fixed fields: XDR bytes of the field (incl. pad)
+    uint32_t rsv;
+    uint8_t *data;
+    int64_t stride;
+    uint64_t *offsets;
+    uint64_t cap;
+};
+
+struct RecArgs {
+    uint64_t n;
+    uint32_t nf;
+    uint32_t framed;
+    uint32_t fixed_xdr;        // XDR bytes of all fixed fields (plus mark)
+    uint32_t ndyn;
+    uint8_t *xdr;
+    uint64_t xdr_cap;          // encode: out_cap; decode: in_len
+    const uint64_t *rec_in;    // decode: record extents (n+1), or NULL (fixed stride)
+    uint64_t rec_stride;       // decode with rec_in == NULL
+    uint64_t *rec_out;         // encode: record offsets (n+1), nullable
+    uint64_t *block_sums;      // workspace [ndyn+1][nblocks]
+    uint64_t nblocks;
+    uint64_t *totals;          // workspace [ndyn+1]: scanned totals
+    unsigned long long *errkey;
+    uint8_t dyn_idx[kMaxFields];  // dynamic field -> field index
+    VField f[kMaxFields];
+};
+
+// Error key: smaller = what a sequential reference decode throws first.
+//   key = record << 16 | sub << 4 | code
+// sub orders the checks inside a record (word index on the word-map path;
+// 2*field+1 / 2*field+2 on the record path, 0 for the record mark).
+__host__ __device__ inline unsigned long long err_key(uint64_t rec, uint32_t sub, uint32_t code) {
+    return ((unsigned long long)rec << 16) | ((unsigned long long)(sub & 0xfffu) << 4) |
+           (code & 0xfu);
+}
+constexpr unsigned long long kNoError = ~0ull;
+
+// ---- launchers (kernels.hip) -------------------------------------------
+// All launches go on `stream`; each returns hipSuccess or the launch error.
+int launch_stream_words(const StreamArgs &a, int variant, void *stream);
+int launch_wordmap_encode(const WordMapArgs &a, bool aligned16, void *stream);
+int launch_wordmap_decode(const WordMapArgs &a, bool aligned16, void *stream);
+enum RecPhase { REC_ENC_SIZES, REC_ENC_SCAN, REC_ENC_PLACE, REC_DEC_SIZES, REC_DEC_SCAN, REC_DEC_PLACE };
+int launch_rec_phase(const RecArgs &a, int phase, void *stream);
+// *dst = value (stream-ordered)
+int launch_store_u64(uint64_t *dst, uint64_t value, void *stream);
+// rec_offsets[i] = i * stride for i in [0, n]
+int launch_iota(uint64_t *dst, uint64_t n, uint64_t stride, void *stream);
+// Combine the device error key with a host-side key and write the public
+// results (async mode); any output pointer may be NULL.
+int launch_finalize(const unsigned long long *errkey, unsigned long long extra_key, uint64_t n,
+                    uint64_t *first_bad, int *err, void *stream);
+int launch_frame_scan(const uint8_t *in, uint64_t len, uint64_t *msg_offsets, uint64_t cap,
+                      uint64_t *result, void *stream);
+
+constexpr int kRecThreads = 256;   // record path: threads per block
+constexpr int kRecPerThread = 8;   // records per thread in the size/scan pass
+constexpr int kRecPerBlock = kRecThreads * kRecPerThread;
+
+}  // namespace xdrg

@@ -1,0 +1,210 @@
+"""engine.py — Python host binding of libxdrgpu.so (the C-ABI of include/xdrg.h).
+
+This is the drop-in boundary seen from Python: the same entry points a JNI or
+Panama shim in oncrpc4j-core binds.  The library is the only
+compute path; if it is missing or no GPU is present the calls raise — there is
+no CPU fallback.
+
+Error mapping mirrors the reference: XDRG_E_SHORT / XDRG_E_CORRUPT raise
+BadXdrOncRpcException with the reference's messages (xdr/Xdr.java:1028-1037,
+xdr/BadXdrOncRpcException.java:24), XDRG_E_FIXED_LEN raises ValueError
+(IllegalArgumentException, Xdr.java:625-627).
+"""
+import ctypes
+import os
+
+from . import abi
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.so")
+
+_LIB = None
+
+
+def lib():
+    """Load libxdrgpu.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                "libxdrgpu.so is not built (run `python -c 'import __graft_entry__ as g; g.build()'`)")
+        _LIB = abi.bind(ctypes.CDLL(LIB_PATH))
+        v = _LIB.xdrg_abi_version()
+        if v != abi.ABI_VERSION:
+            raise RuntimeError(f"libxdrgpu.so ABI {v} != {abi.ABI_VERSION}")
+    return _LIB
+
+
+class XdrgError(Exception):
+    """A non-OK engine status.  .code = XDRG_E_*, .first_bad = record index."""
+
+    def __init__(self, code, msg, first_bad=None):
+        super().__init__(msg)
+        self.code = code
+        self.first_bad = first_bad
+
+
+class BadXdrOncRpcException(XdrgError, IOError):
+    """org.dcache.oncrpc4j.xdr.BadXdrOncRpcException (an IOException)."""
+
+
+class CapacityError(XdrgError):
+    pass
+
+
+def _raise(code, ctx=None, first_bad=None):
+    L = lib()
+    msg = L.xdrg_status_string(code).decode()
+    if ctx is not None:
+        detail = L.xdrg_last_error(ctx).decode()
+        if detail and detail != msg:
+            msg = f"{msg} ({detail})"
+    if code in (abi.E_SHORT, abi.E_CORRUPT):
+        raise BadXdrOncRpcException(code, msg, first_bad)
+    if code == abi.E_FIXED_LEN:
+        raise ValueError(msg)
+    if code == abi.E_CAPACITY:
+        raise CapacityError(code, msg, first_bad)
+    raise XdrgError(code, msg, first_bad)
+
+
+class Schema:
+    """A compiled field tape (rpcgen struct body).  fields: [(type, kind, count)]."""
+
+    def __init__(self, fields):
+        self.fields = [tuple(int(x) for x in f) for f in fields]
+        arr = (abi.Field * len(self.fields))()
+        for i, (t, k, c) in enumerate(self.fields):
+            arr[i].type, arr[i].kind, arr[i].count, arr[i].reserved = t, k, c, 0
+        h = ctypes.c_void_p()
+        rc = lib().xdrg_schema_create(arr, len(self.fields), ctypes.byref(h))
+        if rc:
+            _raise(rc)
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def fixed_size(self):
+        """XDR bytes per record for fixed-size schemas, 0 otherwise."""
+        return int(lib().xdrg_schema_fixed_size(self._h))
+
+    @property
+    def is_fixed(self):
+        return all(k != abi.K_DYNAMIC for _, k, _ in self.fields)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _LIB is not None:
+            _LIB.xdrg_schema_destroy(h)
+            self._h = None
+
+
+def _ptr(x):
+    """Device/host address of a torch tensor, an int or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    return x.data_ptr()
+
+
+def columns_array(cols):
+    """[(data, stride, offsets, cap)] -> ctypes xdrg_column array."""
+    arr = (abi.Column * len(cols))()
+    for i, (data, stride, offsets, cap) in enumerate(cols):
+        arr[i].data = _ptr(data)
+        arr[i].stride = int(stride)
+        arr[i].offsets = _ptr(offsets)
+        arr[i].cap = int(cap)
+    return arr
+
+
+class Context:
+    """xdrg_ctx: one device, one stream, its own workspace (Xdr.java:56,71:
+    one owner at a time — use one Context per thread)."""
+
+    def __init__(self, device=0, timing=False):
+        L = lib()
+        h = ctypes.c_void_p()
+        rc = L.xdrg_ctx_create(int(device), abi.CTX_TIMING if timing else 0, ctypes.byref(h))
+        if rc:
+            _raise(rc)
+        self._h = h
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream):
+        """stream: a torch.cuda.Stream, a raw hipStream_t (int) or None."""
+        raw = getattr(stream, "cuda_stream", stream)
+        rc = lib().xdrg_ctx_set_stream(self._h, raw)
+        if rc:
+            _raise(rc, self._h)
+
+    def encode(self, schema, cols, n, out, out_cap, rec_offsets=None, framed=False, async_=False,
+               out_len=None):
+        """xdrg_encode_batch -> bytes written (sync mode)."""
+        flags = (abi.FRAME_RM if framed else 0) | (abi.ASYNC if async_ else 0)
+        carr = cols if isinstance(cols, ctypes.Array) else columns_array(cols)
+        ol = ctypes.c_uint64(0)
+        olp = _ptr(out_len) if async_ else ctypes.addressof(ol)
+        rc = lib().xdrg_encode_batch(self._h, schema.handle, carr, int(n), _ptr(out), int(out_cap),
+                                     _ptr(rec_offsets), flags, olp)
+        if rc:
+            _raise(rc, self._h)
+        return None if async_ else ol.value
+
+    def decode(self, schema, xdr, xdr_len, n, cols, rec_offsets=None, framed=False, async_=False,
+               first_bad=None, err=None, raise_on_error=True):
+        """xdrg_decode_batch -> (status, first_bad, err) in sync mode."""
+        flags = (abi.FRAME_RM if framed else 0) | (abi.ASYNC if async_ else 0)
+        carr = cols if isinstance(cols, ctypes.Array) else columns_array(cols)
+        fb = ctypes.c_uint64(0)
+        er = ctypes.c_int(0)
+        fbp = _ptr(first_bad) if async_ else ctypes.addressof(fb)
+        erp = _ptr(err) if async_ else ctypes.addressof(er)
+        rc = lib().xdrg_decode_batch(self._h, schema.handle, _ptr(xdr), int(xdr_len),
+                                     _ptr(rec_offsets), int(n), carr, flags, fbp, erp)
+        if rc and raise_on_error:
+            _raise(rc, self._h, None if async_ else fb.value)
+        return rc, (None if async_ else fb.value), (None if async_ else er.value)
+
+    def frame_scan(self, data, length, msg_offsets, cap):
+        """xdrg_frame_scan -> number of complete messages (0 = STOP)."""
+        nm = ctypes.c_uint64(0)
+        rc = lib().xdrg_frame_scan(self._h, _ptr(data), int(length), _ptr(msg_offsets), int(cap),
+                                   ctypes.byref(nm))
+        if rc not in (abi.OK, abi.E_INCOMPLETE):
+            _raise(rc, self._h)
+        return nm.value
+
+    def kernel_stats(self, kernel):
+        """-> (launches, total_ms) for one XDRG_KERNEL_* id (needs timing=True)."""
+        n = ctypes.c_uint64(0)
+        ms = ctypes.c_double(0)
+        lib().xdrg_ctx_kernel_stats(self._h, int(kernel), ctypes.byref(n), ctypes.byref(ms))
+        return n.value, ms.value
+
+    def reset_stats(self):
+        lib().xdrg_ctx_reset_stats(self._h)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            lib().xdrg_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -1,0 +1,683 @@
+/*
+ * xdr_oracle.c — TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ *
+ * Plain-C restatement of org.dcache.oncrpc4j.xdr.Xdr and of the RFC 1831
+ * record-mark framing of oncrpc4j.  Each function cites the reference lines
+ * it follows; paths are relative to
+ * /root/reference/oncrpc4j-core/src/main/java/org/dcache/oncrpc4j/.
+ * Never linked into the product library.
+ */
+#include "xdr_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---- big-endian helpers (util/Bytes.java:39-107) ------------------------ */
+static inline void put_be32(uint8_t *p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16);
+    p[2] = (uint8_t)(v >> 8);  p[3] = (uint8_t)v;
+}
+static inline uint32_t get_be32(const uint8_t *p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+static inline void put_be64(uint8_t *p, uint64_t v) {   /* Bytes.putLong :39-54 */
+    put_be32(p, (uint32_t)(v >> 32)); put_be32(p + 4, (uint32_t)v);
+}
+static inline uint64_t get_be64(const uint8_t *p) {     /* Bytes.getLong :84-93 */
+    return ((uint64_t)get_be32(p) << 32) | get_be32(p + 4);
+}
+
+/* ---- stream state (Xdr.java:82-154) ------------------------------------ */
+int xo_stream_alloc(xo_stream *s, size_t size) {
+    s->buf = (uint8_t *)calloc(size ? size : 1, 1);   /* fresh heap buffer: zeroed */
+    if (!s->buf) return XDRG_E_NOMEM;
+    s->cap = size; s->pos = 0; s->limit = size; s->in_use = 0; s->growable = 1;
+    return XDRG_OK;
+}
+void xo_stream_wrap(xo_stream *s, uint8_t *buf, size_t len) {
+    s->buf = buf; s->cap = len; s->pos = 0; s->limit = len; s->in_use = 0; s->growable = 0;
+}
+void xo_stream_free(xo_stream *s) {
+    if (s->growable) free(s->buf);
+    s->buf = NULL; s->cap = s->pos = s->limit = 0;
+}
+void xo_begin_encoding(xo_stream *s) { s->pos = 0; s->limit = s->cap; s->in_use = 1; } /* clear() :138 */
+void xo_end_encoding(xo_stream *s)   { s->limit = s->pos; s->pos = 0; s->in_use = 0; } /* flip()  :144 */
+void xo_begin_decoding(xo_stream *s) { s->pos = 0; s->in_use = 1; }                    /* rewind():126 */
+void xo_end_decoding(xo_stream *s)   { s->pos = 0; s->in_use = 0; }                    /* rewind():132 */
+size_t xo_remaining(const xo_stream *s) { return s->limit - s->pos; }
+int xo_has_more_data(const xo_stream *s) { return s->pos < s->limit; }                /* :152-154 */
+
+/* ensureCapacity (Xdr.java:1020-1026): grow to max(cap*3/2+1, cap+size). */
+static int ensure_capacity(xo_stream *s, size_t size) {
+    if (xo_remaining(s) >= size) return XDRG_OK;
+    if (!s->growable) return XDRG_E_CAPACITY;
+    size_t old = s->cap;
+    size_t ncap = old * 3 / 2 + 1;
+    if (ncap < old + size) ncap = old + size;
+    uint8_t *nb = (uint8_t *)realloc(s->buf, ncap);
+    if (!nb) return XDRG_E_NOMEM;
+    memset(nb + old, 0, ncap - old);
+    s->buf = nb; s->cap = ncap; s->limit = ncap;
+    return XDRG_OK;
+}
+/* ensureBytes (Xdr.java:1028-1032) */
+static inline int ensure_bytes(const xo_stream *s, size_t size) {
+    return xo_remaining(s) < size ? XDRG_E_SHORT : XDRG_OK;
+}
+/* checkArraySize (Xdr.java:1034-1038) */
+static inline int check_array_size(int32_t len) { return len < 0 ? XDRG_E_CORRUPT : XDRG_OK; }
+
+static inline uint32_t pad4(size_t len) { return (uint32_t)((4 - (len & 3)) & 3); } /* :777 */
+
+/* ---- encoders ------------------------------------------------------------ */
+int xo_encode_int(xo_stream *s, int32_t v) {                 /* Xdr.java:545-548 */
+    int rc = ensure_capacity(s, 4); if (rc) return rc;
+    put_be32(s->buf + s->pos, (uint32_t)v); s->pos += 4;
+    return XDRG_OK;
+}
+int xo_encode_long(xo_stream *s, int64_t v) {                /* Xdr.java:812-815 */
+    int rc = ensure_capacity(s, 8); if (rc) return rc;
+    put_be64(s->buf + s->pos, (uint64_t)v); s->pos += 8;
+    return XDRG_OK;
+}
+/* Float.floatToIntBits: every NaN collapses to 0x7fc00000 (Xdr.java:674-676). */
+static inline uint32_t float_to_int_bits(float f) {
+    uint32_t u; memcpy(&u, &f, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return 0x7fc00000u;
+    return u;
+}
+/* Double.doubleToLongBits: every NaN collapses to 0x7ff8000000000000 (:685-687). */
+static inline uint64_t double_to_long_bits(double d) {
+    uint64_t u; memcpy(&u, &d, 8);
+    if ((u & 0x7ff0000000000000ull) == 0x7ff0000000000000ull && (u & 0x000fffffffffffffull))
+        return 0x7ff8000000000000ull;
+    return u;
+}
+int xo_encode_float(xo_stream *s, float v)   { return xo_encode_int(s, (int32_t)float_to_int_bits(v)); }
+int xo_encode_double(xo_stream *s, double v) { return xo_encode_long(s, (int64_t)double_to_long_bits(v)); }
+int xo_encode_boolean(xo_stream *s, int v)   { return xo_encode_int(s, v ? 1 : 0); }       /* :803-805 */
+int xo_encode_byte(xo_stream *s, int8_t v)   { return xo_encode_int(s, (int32_t)v); }      /* :919-925 */
+int xo_encode_short(xo_stream *s, int16_t v) { return xo_encode_int(s, (int32_t)v); }      /* :934-936 */
+
+/* xdrEncodeOpaque(bytes, offset, len) (Xdr.java:776-781): bytes then zero pad. */
+int xo_encode_opaque(xo_stream *s, const uint8_t *b, size_t off, size_t len) {
+    uint32_t pad = pad4(len);
+    int rc = ensure_capacity(s, len + pad); if (rc) return rc;
+    if (len) memcpy(s->buf + s->pos, b + off, len);
+    s->pos += len;
+    memset(s->buf + s->pos, 0, pad);                 /* paddingZeros :765 */
+    s->pos += pad;
+    return XDRG_OK;
+}
+int xo_encode_dynamic_opaque(xo_stream *s, const uint8_t *b, size_t len) { /* :797-800 */
+    int rc = xo_encode_int(s, (int32_t)len); if (rc) return rc;
+    return xo_encode_opaque(s, b, 0, len);
+}
+int xo_encode_string(xo_stream *s, const uint8_t *utf8, size_t len) {    /* :760-763 */
+    if (!utf8) len = 0;                              /* null -> "" */
+    return xo_encode_dynamic_opaque(s, utf8, len);
+}
+/* xdrEncodeByteBuffer (Xdr.java:824-831): the pad is a position skip, not a
+ * write; a fresh (zeroed) buffer therefore carries zero pad bytes.            */
+int xo_encode_byte_buffer(xo_stream *s, const uint8_t *b, size_t len) {
+    uint32_t pad = pad4(len);
+    int rc = xo_encode_int(s, (int32_t)len); if (rc) return rc;
+    rc = ensure_capacity(s, len + pad); if (rc) return rc;
+    if (len) memcpy(s->buf + s->pos, b, len);
+    s->pos += len + pad;
+    return XDRG_OK;
+}
+/* xdrEncodeIntVector (Xdr.java:607-613): one capacity check, count + ints. */
+int xo_encode_int_vector(xo_stream *s, const int32_t *v, size_t n) {
+    int rc = ensure_capacity(s, 4 + 4 * n); if (rc) return rc;
+    put_be32(s->buf + s->pos, (uint32_t)n); s->pos += 4;
+    for (size_t i = 0; i < n; i++) { put_be32(s->buf + s->pos, (uint32_t)v[i]); s->pos += 4; }
+    return XDRG_OK;
+}
+/* Fixed-vector encoders reject value.length != length (Xdr.java:624-631 etc.). */
+#define FIXED_CHECK(n, length) if ((size_t)(length) != (n) || (length) < 0) return XDRG_E_FIXED_LEN
+int xo_encode_int_fixed_vector(xo_stream *s, const int32_t *v, size_t n, int32_t length) {
+    FIXED_CHECK(n, length);
+    for (size_t i = 0; i < n; i++) { int rc = xo_encode_int(s, v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+int xo_encode_long_vector(xo_stream *s, const int64_t *v, size_t n) {    /* :641-647 */
+    int rc = ensure_capacity(s, 4 + 8 * n); if (rc) return rc;
+    put_be32(s->buf + s->pos, (uint32_t)n); s->pos += 4;
+    for (size_t i = 0; i < n; i++) { put_be64(s->buf + s->pos, (uint64_t)v[i]); s->pos += 8; }
+    return XDRG_OK;
+}
+int xo_encode_long_fixed_vector(xo_stream *s, const int64_t *v, size_t n, int32_t length) {
+    FIXED_CHECK(n, length);                                             /* :658-665 */
+    for (size_t i = 0; i < n; i++) { int rc = xo_encode_long(s, v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+int xo_encode_float_vector(xo_stream *s, const float *v, size_t n) {     /* :696-702 */
+    int rc = xo_encode_int(s, (int32_t)n); if (rc) return rc;
+    for (size_t i = 0; i < n; i++) { rc = xo_encode_float(s, v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+int xo_encode_float_fixed_vector(xo_stream *s, const float *v, size_t n, int32_t length) {
+    FIXED_CHECK(n, length);                                             /* :713-720 */
+    for (size_t i = 0; i < n; i++) { int rc = xo_encode_float(s, v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+int xo_encode_double_vector(xo_stream *s, const double *v, size_t n) {   /* :729-735 */
+    int rc = xo_encode_int(s, (int32_t)n); if (rc) return rc;
+    for (size_t i = 0; i < n; i++) { rc = xo_encode_double(s, v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+int xo_encode_double_fixed_vector(xo_stream *s, const double *v, size_t n, int32_t length) {
+    FIXED_CHECK(n, length);                                             /* :746-753 */
+    for (size_t i = 0; i < n; i++) { int rc = xo_encode_double(s, v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+int xo_encode_short_vector(xo_stream *s, const int16_t *v, size_t n) {   /* :945-951 */
+    int rc = xo_encode_int(s, (int32_t)n); if (rc) return rc;
+    for (size_t i = 0; i < n; i++) { rc = xo_encode_short(s, v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+int xo_encode_short_fixed_vector(xo_stream *s, const int16_t *v, size_t n, int32_t length) {
+    FIXED_CHECK(n, length);                                             /* :962-969 */
+    for (size_t i = 0; i < n; i++) { int rc = xo_encode_short(s, v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+int xo_encode_byte_vector(xo_stream *s, const int8_t *v, size_t n) {     /* :878-888 */
+    int rc = xo_encode_int(s, (int32_t)n); if (rc) return rc;
+    for (size_t i = 0; i < n; i++) { rc = xo_encode_byte(s, v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+int xo_encode_byte_fixed_vector(xo_stream *s, const int8_t *v, size_t n, int32_t length) {
+    FIXED_CHECK(n, length);                                             /* :900-911 */
+    for (size_t i = 0; i < n; i++) { int rc = xo_encode_int(s, (int32_t)v[i]); if (rc) return rc; }
+    return XDRG_OK;
+}
+
+/* ---- decoders ------------------------------------------------------------ */
+int xo_decode_int(xo_stream *s, int32_t *v) {                 /* Xdr.java:171-175 */
+    int rc = ensure_bytes(s, 4); if (rc) return rc;
+    *v = (int32_t)get_be32(s->buf + s->pos); s->pos += 4;
+    return XDRG_OK;
+}
+int xo_decode_long(xo_stream *s, int64_t *v) {                /* Xdr.java:417-420 */
+    int rc = ensure_bytes(s, 8); if (rc) return rc;
+    *v = (int64_t)get_be64(s->buf + s->pos); s->pos += 8;
+    return XDRG_OK;
+}
+int xo_decode_float(xo_stream *s, float *v) {                 /* :255-257 intBitsToFloat */
+    int32_t i; int rc = xo_decode_int(s, &i); if (rc) return rc;
+    memcpy(v, &i, 4); return XDRG_OK;
+}
+int xo_decode_double(xo_stream *s, double *v) {               /* :267-269 longBitsToDouble */
+    int64_t l; int rc = xo_decode_long(s, &l); if (rc) return rc;
+    memcpy(v, &l, 8); return XDRG_OK;
+}
+int xo_decode_boolean(xo_stream *s, int *v) {                 /* :404-407 any non-zero */
+    int32_t i; int rc = xo_decode_int(s, &i); if (rc) return rc;
+    *v = i != 0; return XDRG_OK;
+}
+int xo_decode_byte(xo_stream *s, int8_t *v) {                 /* :485-487 (byte) */
+    int32_t i; int rc = xo_decode_int(s, &i); if (rc) return rc;
+    *v = (int8_t)i; return XDRG_OK;
+}
+int xo_decode_short(xo_stream *s, int16_t *v) {               /* :497-499 (short) */
+    int32_t i; int rc = xo_decode_int(s, &i); if (rc) return rc;
+    *v = (int16_t)i; return XDRG_OK;
+}
+/* xdrDecodeOpaque(buf, off, len) (Xdr.java:341-349): len 0 returns at once;
+ * the pad is skipped without being checked.                                  */
+int xo_decode_opaque(xo_stream *s, uint8_t *dst, size_t len) {
+    if (len == 0) return XDRG_OK;
+    uint32_t pad = pad4(len);
+    int rc = ensure_bytes(s, len + pad); if (rc) return rc;
+    if (dst) memcpy(dst, s->buf + s->pos, len);
+    s->pos += len + pad;
+    return XDRG_OK;
+}
+/* xdrDecodeDynamicOpaque (Xdr.java:374-383) and xdrDecodeString (:392-401):
+ * length; 0 -> empty before any sign check; negative -> corrupted; bytes.    */
+static int decode_counted_bytes(xo_stream *s, const uint8_t **p, size_t *len) {
+    int32_t l; int rc = xo_decode_int(s, &l); if (rc) return rc;
+    *p = s->buf + s->pos; *len = 0;
+    if (l == 0) return XDRG_OK;
+    rc = check_array_size(l); if (rc) return rc;
+    *p = s->buf + s->pos;
+    rc = xo_decode_opaque(s, NULL, (size_t)l); if (rc) return rc;
+    *len = (size_t)l;
+    return XDRG_OK;
+}
+int xo_decode_dynamic_opaque(xo_stream *s, const uint8_t **p, size_t *len) { return decode_counted_bytes(s, p, len); }
+int xo_decode_string(xo_stream *s, const uint8_t **p, size_t *len)         { return decode_counted_bytes(s, p, len); }
+/* xdrDecodeByteBuffer (Xdr.java:423-439): sign check first (0 passes), then
+ * ensureBytes(len + pad); returns a view.                                     */
+int xo_decode_byte_buffer(xo_stream *s, const uint8_t **p, size_t *len) {
+    int32_t l; int rc = xo_decode_int(s, &l); if (rc) return rc;
+    rc = check_array_size(l); if (rc) return rc;
+    uint32_t pad = pad4((size_t)l);
+    rc = ensure_bytes(s, (size_t)l + pad); if (rc) return rc;
+    *p = s->buf + s->pos; *len = (size_t)l;
+    s->pos += (size_t)l + pad;
+    return XDRG_OK;
+}
+/* Dynamic vectors (Xdr.java:184-193, 219-228, 278-282, 308-312, 452-456,
+ * 509-513): count; negative -> corrupted; then element by element, each
+ * running ensureBytes.  The reference allocates `new T[count]` before the
+ * first element check; for an absurd count that is an OutOfMemoryError in
+ * the JVM where this restatement (and the engine) report "too short".      */
+#define DECODE_VECTOR(NAME, T, XSZ, GET)                                        \
+int NAME(xo_stream *s, T *out, size_t cap, size_t *n) {                          \
+    int32_t l; int rc = xo_decode_int(s, &l); if (rc) return rc;                 \
+    rc = check_array_size(l); if (rc) return rc;                                 \
+    *n = 0;                                                                       \
+    if (xo_remaining(s) < (size_t)l * (XSZ)) return XDRG_E_SHORT;                \
+    if ((size_t)l > cap) return XDRG_E_CAPACITY;                                 \
+    for (int32_t i = 0; i < l; i++) { GET; s->pos += (XSZ); }                    \
+    *n = (size_t)l;                                                               \
+    return XDRG_OK;                                                              \
+}
+DECODE_VECTOR(xo_decode_int_vector, int32_t, 4, out[i] = (int32_t)get_be32(s->buf + s->pos))
+DECODE_VECTOR(xo_decode_long_vector, int64_t, 8, out[i] = (int64_t)get_be64(s->buf + s->pos))
+DECODE_VECTOR(xo_decode_float_vector, float, 4,
+              { uint32_t u = get_be32(s->buf + s->pos); memcpy(&out[i], &u, 4); })
+DECODE_VECTOR(xo_decode_double_vector, double, 8,
+              { uint64_t u = get_be64(s->buf + s->pos); memcpy(&out[i], &u, 8); })
+DECODE_VECTOR(xo_decode_short_vector, int16_t, 4, out[i] = (int16_t)get_be32(s->buf + s->pos))
+DECODE_VECTOR(xo_decode_byte_vector, int8_t, 4, out[i] = (int8_t)get_be32(s->buf + s->pos))
+
+/* ---- record marking (RFC 1831 §10, docs/rfc1831.txt:688-707) ------------- */
+#define RPC_LAST_FRAG 0x80000000u   /* RpcMessageParserTCP.java:37 */
+#define RPC_SIZE_MASK 0x7fffffffu   /* RpcMessageParserTCP.java:41 */
+
+uint32_t xo_record_mark(uint32_t payload_len) {             /* GrizzlyRpcTransport:104 */
+    return payload_len | RPC_LAST_FRAG;
+}
+/* isAllFragmentsArrived (RpcMessageParserTCP.java:63-99). */
+int xo_all_fragments_arrived(const uint8_t *buf, size_t len) {
+    size_t pos = 0;
+    if (len < 4) return 0;
+    do {
+        uint32_t m = get_be32(buf + pos); pos += 4;
+        size_t size = m & RPC_SIZE_MASK;
+        if (size > len - pos) return 0;          /* fragment bigger than received */
+        if (m & RPC_LAST_FRAG) return 1;         /* complete message */
+        pos += size;
+    } while (len - pos >= 4);
+    return 0;
+}
+/* assembleXdr (RpcMessageParserTCP.java:109-140): the payload is the
+ * concatenation of the fragment bodies.                                      */
+int xo_assemble(const uint8_t *buf, size_t len, uint8_t *payload, size_t payload_cap,
+                size_t *payload_len, size_t *consumed) {
+    size_t pos = 0, out = 0; int complete;
+    do {
+        if (len - pos < 4) return XDRG_E_INCOMPLETE;
+        uint32_t m = get_be32(buf + pos); pos += 4;
+        size_t size = m & RPC_SIZE_MASK;
+        complete = (m & RPC_LAST_FRAG) != 0;
+        if (size > len - pos) return XDRG_E_INCOMPLETE;
+        if (out + size > payload_cap) return XDRG_E_CAPACITY;
+        memcpy(payload + out, buf + pos, size);
+        out += size; pos += size;
+    } while (!complete);
+    *payload_len = out; *consumed = pos;
+    return XDRG_OK;
+}
+/* Repeated handleRead over one socket buffer (:44-61): every complete message
+ * is one INVOKE; the remainder is split off (:57-60).                        */
+int xo_frame_scan(const uint8_t *buf, size_t len, uint64_t *msg_offsets, uint64_t cap,
+                  uint64_t *n_msgs) {
+    size_t pos = 0; uint64_t k = 0;
+    while (k < cap && xo_all_fragments_arrived(buf + pos, len - pos)) {
+        if (msg_offsets) msg_offsets[k] = pos;
+        int last = 0;
+        while (!last) {
+            uint32_t m = get_be32(buf + pos); pos += 4;
+            last = (m & RPC_LAST_FRAG) != 0;
+            pos += m & RPC_SIZE_MASK;
+        }
+        k++;
+    }
+    if (msg_offsets) msg_offsets[k] = pos;
+    *n_msgs = k;
+    return k ? XDRG_OK : XDRG_E_INCOMPLETE;
+}
+/* toFragmentedBuffer (ctest/rpc/RpcMessageParserTCPTest.java:161-181). */
+size_t xo_fragment(const uint8_t *payload, size_t len, size_t frag, uint8_t *out, size_t cap) {
+    size_t nfrag = len / frag + 1, pos = 0, o = 0;
+    if (cap < len + 4 * nfrag) return 0;
+    do {
+        --nfrag;
+        size_t fs = len - pos < frag ? len - pos : frag;
+        uint32_t m = nfrag > 0 ? (uint32_t)fs : ((uint32_t)fs | RPC_LAST_FRAG);
+        put_be32(out + o, m); o += 4;
+        memcpy(out + o, payload + pos, fs); o += fs; pos += fs;
+    } while (nfrag > 0);
+    return o;
+}
+
+/* ---- batch driver -------------------------------------------------------- */
+static size_t native_size(uint32_t t) {
+    switch (t) {
+    case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: case XDRG_T_FLOAT: return 4;
+    case XDRG_T_HYPER: case XDRG_T_UHYPER: case XDRG_T_DOUBLE: return 8;
+    case XDRG_T_SHORT: return 2;
+    case XDRG_T_BYTE: case XDRG_T_BOOL: case XDRG_T_OPAQUE: case XDRG_T_STRING: return 1;
+    default: return 0;
+    }
+}
+/* Which (type, kind) pairs rpcgen can emit against the Xdr surface
+ * (jrpcgen.java:661-739): no boolean vectors, strings only as string<>,
+ * opaque only as opaque[N] / opaque<>.                                       */
+static int field_valid(const xdrg_field *f) {
+    if (!native_size(f->type) || f->kind > XDRG_K_DYNAMIC || f->reserved) return 0;
+    if (f->type == XDRG_T_BOOL && f->kind != XDRG_K_SCALAR) return 0;
+    if (f->type == XDRG_T_STRING && f->kind != XDRG_K_DYNAMIC) return 0;
+    if (f->type == XDRG_T_OPAQUE && f->kind == XDRG_K_SCALAR) return 0;
+    if (f->kind == XDRG_K_FIXED && f->count > 0x7fffffffu) return 0;
+    return 1;
+}
+static inline const uint8_t *fixed_ptr(const xdrg_field *f, const xdrg_column *c, uint64_t i) {
+    size_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
+    int64_t stride = c->stride ? c->stride : (int64_t)(native_size(f->type) * cnt);
+    return (const uint8_t *)c->data + (int64_t)i * stride;
+}
+
+/* One record's fields, in declaration order, through the stream encoders —
+ * what an rpcgen XdrAble.xdrEncode does (jrpcgen.java:788-808).              */
+static int encode_record(xo_stream *s, const xdrg_field *fs, size_t nf, const xdrg_column *cols,
+                         uint64_t i) {
+    for (size_t k = 0; k < nf; k++) {
+        const xdrg_field *f = &fs[k];
+        const xdrg_column *c = &cols[k];
+        int rc = XDRG_OK;
+        if (f->kind == XDRG_K_DYNAMIC) {
+            uint64_t a = c->offsets[i], b = c->offsets[i + 1];
+            const uint8_t *base = (const uint8_t *)c->data + a * native_size(f->type);
+            size_t n = (size_t)(b - a);
+            switch (f->type) {
+            case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM:
+                rc = xo_encode_int_vector(s, (const int32_t *)base, n); break;
+            case XDRG_T_HYPER: case XDRG_T_UHYPER:
+                rc = xo_encode_long_vector(s, (const int64_t *)base, n); break;
+            case XDRG_T_FLOAT:  rc = xo_encode_float_vector(s, (const float *)base, n); break;
+            case XDRG_T_DOUBLE: rc = xo_encode_double_vector(s, (const double *)base, n); break;
+            case XDRG_T_SHORT:  rc = xo_encode_short_vector(s, (const int16_t *)base, n); break;
+            case XDRG_T_BYTE:   rc = xo_encode_byte_vector(s, (const int8_t *)base, n); break;
+            case XDRG_T_OPAQUE: rc = xo_encode_dynamic_opaque(s, base, n); break;
+            case XDRG_T_STRING: rc = xo_encode_string(s, base, n); break;
+            default: rc = XDRG_E_INVAL;
+            }
+        } else if (f->kind == XDRG_K_FIXED) {
+            const uint8_t *p = fixed_ptr(f, c, i);
+            size_t n = f->count; int32_t len = (int32_t)f->count;
+            switch (f->type) {
+            case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM:
+                rc = xo_encode_int_fixed_vector(s, (const int32_t *)p, n, len); break;
+            case XDRG_T_HYPER: case XDRG_T_UHYPER:
+                rc = xo_encode_long_fixed_vector(s, (const int64_t *)p, n, len); break;
+            case XDRG_T_FLOAT:  rc = xo_encode_float_fixed_vector(s, (const float *)p, n, len); break;
+            case XDRG_T_DOUBLE: rc = xo_encode_double_fixed_vector(s, (const double *)p, n, len); break;
+            case XDRG_T_SHORT:  rc = xo_encode_short_fixed_vector(s, (const int16_t *)p, n, len); break;
+            case XDRG_T_BYTE:   rc = xo_encode_byte_fixed_vector(s, (const int8_t *)p, n, len); break;
+            case XDRG_T_OPAQUE: rc = xo_encode_opaque(s, p, 0, n); break;
+            default: rc = XDRG_E_INVAL;
+            }
+        } else {
+            const uint8_t *p = fixed_ptr(f, c, i);
+            switch (f->type) {
+            case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: {
+                int32_t v; memcpy(&v, p, 4); rc = xo_encode_int(s, v); break; }
+            case XDRG_T_HYPER: case XDRG_T_UHYPER: {
+                int64_t v; memcpy(&v, p, 8); rc = xo_encode_long(s, v); break; }
+            case XDRG_T_FLOAT:  { float v; memcpy(&v, p, 4); rc = xo_encode_float(s, v); break; }
+            case XDRG_T_DOUBLE: { double v; memcpy(&v, p, 8); rc = xo_encode_double(s, v); break; }
+            case XDRG_T_BOOL:   rc = xo_encode_boolean(s, *p != 0); break;
+            case XDRG_T_SHORT:  { int16_t v; memcpy(&v, p, 2); rc = xo_encode_short(s, v); break; }
+            case XDRG_T_BYTE:   rc = xo_encode_byte(s, (int8_t)*p); break;
+            default: rc = XDRG_E_INVAL;
+            }
+        }
+        if (rc) return rc;
+    }
+    return XDRG_OK;
+}
+
+static int check_schema(const xdrg_field *fs, size_t nf) {
+    if (!fs || !nf) return XDRG_E_INVAL;
+    for (size_t k = 0; k < nf; k++) if (!field_valid(&fs[k])) return XDRG_E_INVAL;
+    return XDRG_OK;
+}
+
+int xo_encode_batch(const xdrg_field *fs, size_t nf, const xdrg_column *cols, uint64_t n,
+                    uint8_t *out, uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags,
+                    uint64_t *out_len) {
+    int rc = check_schema(fs, nf); if (rc) return rc;
+    const int framed = (flags & XDRG_FRAME_RM) != 0;
+    uint64_t pos = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (rec_offsets) rec_offsets[i] = pos;
+        uint64_t body = pos + (framed ? 4 : 0);
+        if (body > out_cap) return XDRG_E_CAPACITY;
+        /* the record is encoded as its own Xdr message (RpcCall.acceptedReply
+         * encodes one message per Xdr, RpcCall.java:323-343) ...            */
+        xo_stream s;
+        xo_stream_wrap(&s, out + body, (size_t)(out_cap - body));
+        xo_begin_encoding(&s);
+        rc = encode_record(&s, fs, nf, cols, i);
+        if (rc) return rc;
+        xo_end_encoding(&s);
+        /* ... and framed as GrizzlyRpcTransport.sendDefault does (:103-110). */
+        if (framed) put_be32(out + pos, xo_record_mark((uint32_t)s.limit));
+        pos = body + s.limit;
+    }
+    if (rec_offsets) rec_offsets[n] = pos;
+    if (out_len) *out_len = pos;
+    return XDRG_OK;
+}
+
+/* One record's fields through the stream decoders (XdrAble.xdrDecode). */
+static int decode_record(xo_stream *s, const xdrg_field *fs, size_t nf, xdrg_column *cols,
+                         uint64_t i) {
+    for (size_t k = 0; k < nf; k++) {
+        const xdrg_field *f = &fs[k];
+        xdrg_column *c = &cols[k];
+        int rc = XDRG_OK;
+        if (f->kind == XDRG_K_DYNAMIC) {
+            size_t es = native_size(f->type);
+            uint64_t a = c->offsets[i];
+            uint8_t *base = (uint8_t *)c->data + a * es;
+            size_t cap = c->cap > a ? (size_t)(c->cap - a) : 0, got = 0;
+            switch (f->type) {
+            case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM:
+                rc = xo_decode_int_vector(s, (int32_t *)base, cap, &got); break;
+            case XDRG_T_HYPER: case XDRG_T_UHYPER:
+                rc = xo_decode_long_vector(s, (int64_t *)base, cap, &got); break;
+            case XDRG_T_FLOAT:  rc = xo_decode_float_vector(s, (float *)base, cap, &got); break;
+            case XDRG_T_DOUBLE: rc = xo_decode_double_vector(s, (double *)base, cap, &got); break;
+            case XDRG_T_SHORT:  rc = xo_decode_short_vector(s, (int16_t *)base, cap, &got); break;
+            case XDRG_T_BYTE:   rc = xo_decode_byte_vector(s, (int8_t *)base, cap, &got); break;
+            case XDRG_T_OPAQUE: case XDRG_T_STRING: {
+                const uint8_t *p; size_t len;
+                rc = f->type == XDRG_T_OPAQUE ? xo_decode_dynamic_opaque(s, &p, &len)
+                                              : xo_decode_string(s, &p, &len);
+                if (!rc && len > cap) rc = XDRG_E_CAPACITY;
+                if (!rc) { memcpy(base, p, len); got = len; }
+                break; }
+            default: rc = XDRG_E_INVAL;
+            }
+            if (rc) return rc;
+            c->offsets[i + 1] = a + got;
+        } else {
+            size_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
+            uint8_t *p = (uint8_t *)fixed_ptr(f, c, i);
+            if (f->type == XDRG_T_OPAQUE) { rc = xo_decode_opaque(s, p, cnt); if (rc) return rc; continue; }
+            for (size_t e = 0; e < cnt && !rc; e++) {
+                switch (f->type) {
+                case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: {
+                    int32_t v; rc = xo_decode_int(s, &v); if (!rc) memcpy(p + 4 * e, &v, 4); break; }
+                case XDRG_T_FLOAT: {
+                    float v; rc = xo_decode_float(s, &v); if (!rc) memcpy(p + 4 * e, &v, 4); break; }
+                case XDRG_T_HYPER: case XDRG_T_UHYPER: {
+                    int64_t v; rc = xo_decode_long(s, &v); if (!rc) memcpy(p + 8 * e, &v, 8); break; }
+                case XDRG_T_DOUBLE: {
+                    double v; rc = xo_decode_double(s, &v); if (!rc) memcpy(p + 8 * e, &v, 8); break; }
+                case XDRG_T_BOOL: { int v; rc = xo_decode_boolean(s, &v); if (!rc) p[e] = (uint8_t)v; break; }
+                case XDRG_T_SHORT: {
+                    int16_t v; rc = xo_decode_short(s, &v); if (!rc) memcpy(p + 2 * e, &v, 2); break; }
+                case XDRG_T_BYTE: { int8_t v; rc = xo_decode_byte(s, &v); if (!rc) p[e] = (uint8_t)v; break; }
+                default: rc = XDRG_E_INVAL;
+                }
+            }
+            if (rc) return rc;
+        }
+    }
+    return XDRG_OK;
+}
+
+static uint64_t schema_fixed_size(const xdrg_field *fs, size_t nf) {
+    uint64_t sz = 0;
+    for (size_t k = 0; k < nf; k++) {
+        const xdrg_field *f = &fs[k];
+        if (f->kind == XDRG_K_DYNAMIC) return 0;
+        uint64_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
+        if (f->type == XDRG_T_OPAQUE) sz += cnt + pad4((size_t)cnt);
+        else if (f->type == XDRG_T_HYPER || f->type == XDRG_T_UHYPER || f->type == XDRG_T_DOUBLE) sz += 8 * cnt;
+        else sz += 4 * cnt;
+    }
+    return sz;
+}
+
+int xo_decode_batch(const xdrg_field *fs, size_t nf, const uint8_t *in, uint64_t in_len,
+                    const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
+                    uint64_t *first_bad, int *err) {
+    int rc = check_schema(fs, nf); if (rc) return rc;
+    const int framed = (flags & XDRG_FRAME_RM) != 0;
+    const uint64_t fixed = schema_fixed_size(fs, nf);
+    if (!rec_offsets && !fixed) return XDRG_E_INVAL;
+    for (size_t k = 0; k < nf; k++)
+        if (fs[k].kind == XDRG_K_DYNAMIC && n) cols[k].offsets[0] = 0;
+    const uint64_t stride = fixed + (framed ? 4 : 0);
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t a, b;
+        if (rec_offsets) { a = rec_offsets[i]; b = rec_offsets[i + 1]; }
+        else { a = i * stride; b = a + stride; }
+        if (b > in_len) b = in_len;
+        if (a > b) a = b;
+        rc = XDRG_OK;
+        if (framed) {
+            /* one record = one single-fragment message (GrizzlyRpcTransport:104) */
+            if (b - a < 4) rc = XDRG_E_SHORT;
+            else {
+                uint32_t m = get_be32(in + a);
+                uint64_t want = rec_offsets ? (b - a - 4) : fixed;
+                if (!(m & RPC_LAST_FRAG) || (m & RPC_SIZE_MASK) != want) rc = XDRG_E_FRAME;
+                a += 4;
+            }
+        }
+        if (!rc) {
+            xo_stream s;
+            xo_stream_wrap(&s, (uint8_t *)in + a, (size_t)(b - a));
+            xo_begin_decoding(&s);
+            rc = decode_record(&s, fs, nf, cols, i);
+        }
+        if (rc) {
+            if (first_bad) *first_bad = i;
+            if (err) *err = rc;
+            return rc;
+        }
+    }
+    if (first_bad) *first_bad = n;
+    if (err) *err = XDRG_OK;
+    return XDRG_OK;
+}
+
+/* ---- multithreaded driver (all-cores CPU baseline) ------------------------- */
+typedef struct {
+    const xdrg_field *fs; size_t nf; const xdrg_column *cols; xdrg_column *ocols;
+    uint64_t lo, hi; uint8_t *buf; uint64_t stride; uint64_t in_len;
+    uint32_t flags; int rc; uint64_t first_bad; int err;
+} mt_job;
+
+static void *enc_worker(void *arg) {
+    mt_job *j = (mt_job *)arg;
+    xdrg_column sub[64];
+    for (size_t k = 0; k < j->nf; k++) {
+        sub[k] = j->cols[k];
+        size_t cnt = j->fs[k].kind == XDRG_K_FIXED ? j->fs[k].count : 1;
+        int64_t st = sub[k].stride ? sub[k].stride : (int64_t)(native_size(j->fs[k].type) * cnt);
+        sub[k].data = (uint8_t *)sub[k].data + (int64_t)j->lo * st;
+    }
+    uint64_t len;
+    j->rc = xo_encode_batch(j->fs, j->nf, sub, j->hi - j->lo, j->buf + j->lo * j->stride,
+                            (j->hi - j->lo) * j->stride, NULL, j->flags, &len);
+    return NULL;
+}
+static void *dec_worker(void *arg) {
+    mt_job *j = (mt_job *)arg;
+    xdrg_column sub[64];
+    for (size_t k = 0; k < j->nf; k++) {
+        sub[k] = j->ocols[k];
+        size_t cnt = j->fs[k].kind == XDRG_K_FIXED ? j->fs[k].count : 1;
+        int64_t st = sub[k].stride ? sub[k].stride : (int64_t)(native_size(j->fs[k].type) * cnt);
+        sub[k].data = (uint8_t *)sub[k].data + (int64_t)j->lo * st;
+    }
+    uint64_t start = j->lo * j->stride;
+    uint64_t avail = j->in_len > start ? j->in_len - start : 0;
+    j->rc = xo_decode_batch(j->fs, j->nf, j->buf + start, avail, NULL, j->hi - j->lo, sub,
+                            j->flags, &j->first_bad, &j->err);
+    j->first_bad += j->lo;
+    return NULL;
+}
+static int run_mt(void *(*fn)(void *), mt_job *proto, uint64_t n, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256]; mt_job jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = *proto;
+        jobs[t].lo = n * (uint64_t)t / (uint64_t)threads;
+        jobs[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
+        if (pthread_create(&th[t], NULL, fn, &jobs[t])) { threads = t; break; }
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    int rc = XDRG_OK; uint64_t fb = n; int err = XDRG_OK;
+    for (int t = 0; t < threads; t++) {
+        if (jobs[t].rc && jobs[t].first_bad < fb) { fb = jobs[t].first_bad; err = jobs[t].err; rc = jobs[t].rc; }
+        else if (jobs[t].rc && !rc) rc = jobs[t].rc;
+    }
+    proto->first_bad = fb; proto->err = err;
+    return rc;
+}
+int xo_encode_batch_mt(const xdrg_field *fs, size_t nf, const xdrg_column *cols, uint64_t n,
+                       uint8_t *out, uint64_t out_cap, uint32_t flags, uint64_t *out_len,
+                       int threads) {
+    int rc = check_schema(fs, nf); if (rc) return rc;
+    if (nf > 64) return XDRG_E_INVAL;
+    uint64_t fixed = schema_fixed_size(fs, nf);
+    if (!fixed) return XDRG_E_INVAL;
+    uint64_t stride = fixed + ((flags & XDRG_FRAME_RM) ? 4 : 0);
+    if (out_cap < n * stride) return XDRG_E_CAPACITY;
+    mt_job p; memset(&p, 0, sizeof p);
+    p.fs = fs; p.nf = nf; p.cols = cols; p.buf = out; p.stride = stride; p.flags = flags;
+    p.first_bad = n;
+    rc = run_mt(enc_worker, &p, n, threads);
+    if (!rc && out_len) *out_len = n * stride;
+    return rc;
+}
+int xo_decode_batch_mt(const xdrg_field *fs, size_t nf, const uint8_t *in, uint64_t in_len,
+                       uint64_t n, xdrg_column *cols, uint32_t flags, uint64_t *first_bad,
+                       int *err, int threads) {
+    int rc = check_schema(fs, nf); if (rc) return rc;
+    if (nf > 64) return XDRG_E_INVAL;
+    uint64_t fixed = schema_fixed_size(fs, nf);
+    if (!fixed) return XDRG_E_INVAL;
+    mt_job p; memset(&p, 0, sizeof p);
+    p.fs = fs; p.nf = nf; p.ocols = cols; p.buf = (uint8_t *)in; p.in_len = in_len;
+    p.stride = fixed + ((flags & XDRG_FRAME_RM) ? 4 : 0); p.flags = flags; p.first_bad = n;
+    rc = run_mt(dec_worker, &p, n, threads);
+    if (first_bad) *first_bad = p.first_bad;
+    if (err) *err = p.err;
+    return rc;
+}

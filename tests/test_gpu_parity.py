@@ -1,0 +1,296 @@
+"""GPU parity: libxdrgpu.so (HIP, gfx950) against the pinned CPU oracle and the
+golden fixtures.  Bit-exact for every byte and every decoded value; error
+parity = same first failing record and same code as a sequential reference
+decode (Xdr.java:1028-1037)."""
+import zlib
+
+import numpy as np
+import pytest
+
+import gold
+import oracle
+from oncrpc4j_amd import abi, engine
+from oncrpc4j_amd.columns import DeviceBatch, HostBatch, aos_columns, random_batch, xdr_word_offsets
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+I, U, E, B = abi.T_INT, abi.T_UINT, abi.T_ENUM, abi.T_BOOL
+H, UH, F, D = abi.T_HYPER, abi.T_UHYPER, abi.T_FLOAT, abi.T_DOUBLE
+S, BY, O, STR = abi.T_SHORT, abi.T_BYTE, abi.T_OPAQUE, abi.T_STRING
+SC, FX, DY = abi.K_SCALAR, abi.K_FIXED, abi.K_DYNAMIC
+
+SCHEMAS = {
+    "cfg2_8xint": [(I, SC, 0)] * 8,
+    "cfg1_int_int_string": [(I, SC, 0), (I, SC, 0), (STR, DY, 0)],
+    "cfg3_6xint_opaque": [(I, SC, 0)] * 6 + [(O, DY, 0)],
+    "cfg4_int_string_intvec": [(I, SC, 0), (STR, DY, 0), (I, DY, 0)],
+    "all_scalars": [(I, SC, 0), (U, SC, 0), (E, SC, 0), (B, SC, 0), (H, SC, 0), (UH, SC, 0),
+                    (F, SC, 0), (D, SC, 0), (S, SC, 0), (BY, SC, 0)],
+    "fixed_arrays": [(I, FX, 3), (H, FX, 2), (F, FX, 2), (D, FX, 1), (S, FX, 3), (BY, FX, 5),
+                     (O, FX, 5), (O, FX, 8), (U, FX, 1), (O, FX, 0)],
+    "dyn_vectors": [(H, DY, 0), (UH, DY, 0), (F, DY, 0), (D, DY, 0), (S, DY, 0), (BY, DY, 0),
+                    (U, DY, 0), (O, DY, 0), (E, DY, 0), (STR, DY, 0)],
+    "words_mixed": [(I, SC, 0), (F, SC, 0), (H, SC, 0), (D, SC, 0), (O, FX, 8), (I, FX, 2)],
+    "odd_words": [(I, SC, 0)] * 3,
+    "big_fixed": [(I, FX, 200), (O, FX, 37)],   # beyond the word-map limit -> record path
+}
+
+
+# ---- helpers ----------------------------------------------------------------
+def gpu_encode(ctx, fields, hb, framed=False, cap_slack=0):
+    sch = engine.Schema(fields)
+    db = DeviceBatch.from_host(hb)
+    total = hb.xdr_total(framed)
+    out = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+    offs = torch.zeros(hb.n + 1, dtype=torch.int64, device="cuda")
+    ln = ctx.encode(sch, db.columns(), hb.n, out, total + cap_slack, rec_offsets=offs, framed=framed)
+    assert ln == total
+    assert not out[total:].any(), "engine wrote past the stream end"
+    return out[:ln].cpu().numpy().tobytes(), offs.cpu().numpy().view(np.uint64)
+
+
+def gpu_decode(ctx, fields, xdr, n, rec_offsets, caps, framed=False, use_offsets=True):
+    sch = engine.Schema(fields)
+    db = DeviceBatch.empty(fields, n, caps)
+    buf = torch.from_numpy(np.frombuffer(xdr, dtype=np.uint8).copy()).cuda() if xdr else \
+        torch.zeros(4, dtype=torch.uint8, device="cuda")
+    ro = None
+    if use_offsets and rec_offsets is not None:
+        ro = torch.from_numpy(np.asarray(rec_offsets, dtype=np.uint64).view(np.int64)).cuda()
+    rc, fb, err = ctx.decode(sch, buf, len(xdr), n, db.columns(), rec_offsets=ro, framed=framed,
+                             raise_on_error=False)
+    return rc, fb, err, db.to_host()
+
+
+def oracle_decode(fields, xdr, n, rec_offsets, caps, framed=False):
+    out = HostBatch.empty(fields, n, caps)
+    ro = None if rec_offsets is None else np.asarray(rec_offsets, dtype=np.uint64)
+    rc, fb, err = oracle.decode_batch(fields, xdr, ro, n, out.columns(), framed=framed)
+    return rc, fb, err, out
+
+
+# ---- golden fixtures ------------------------------------------------------------
+@pytest.mark.parametrize("b", gold.load("xdrlib_vectors.json")["batches"],
+                         ids=lambda b: f'{b["name"]}-{"rm" if b["framed"] else "raw"}')
+def test_golden_xdrlib(gpu_ctx, b):
+    fields = [tuple(f) for f in b["fields"]]
+    hb = gold.batch_from_records(fields, b["records"])
+    xdr, offs = gpu_encode(gpu_ctx, fields, hb, b["framed"])
+    assert xdr.hex() == b["xdr"]
+    assert offs.tolist() == b["rec_offsets"]
+    rc, fb, err, out = gpu_decode(gpu_ctx, fields, xdr, hb.n, offs, hb.dyn_caps(), b["framed"])
+    assert (rc, fb, err) == (0, hb.n, 0)
+    assert out.equal(hb)
+
+
+@pytest.mark.parametrize("case", gold.load("kat_reference.json")["scalars"], ids=lambda c: c["name"])
+def test_golden_kat(gpu_ctx, case):
+    fields = [tuple(f) for f in case["fields"]]
+    hb = gold.batch_from_records(fields, [case["values"]])
+    xdr, offs = gpu_encode(gpu_ctx, fields, hb)
+    assert xdr.hex() == case["xdr"]
+    rc, fb, err, out = gpu_decode(gpu_ctx, fields, xdr, 1, offs, hb.dyn_caps())
+    assert rc == 0 and out.equal(hb)
+
+
+@pytest.mark.parametrize("case", gold.load("kat_reference.json")["errors"], ids=lambda c: c["name"])
+def test_golden_kat_errors(gpu_ctx, case):
+    fields = [tuple(f) for f in case["fields"]]
+    xdr = bytes.fromhex(case["xdr"])
+    rc, fb, err, _ = gpu_decode(gpu_ctx, fields, xdr, 1, [0, len(xdr)], {0: 64})
+    assert (rc, fb, err) == (case["code"], 0, case["code"])
+
+
+def test_jdk_nan(gpu_ctx):
+    d = gold.load("kat_jdk_nan.json")
+    for t, key in ((F, "float"), (D, "double")):
+        fields = [(t, SC, 0)]
+        hb = gold.batch_from_records(fields, [[int(c["bits"], 16)] for c in d[key]])
+        xdr, _ = gpu_encode(gpu_ctx, fields, hb)
+        assert xdr.hex() == "".join(c["xdr"] for c in d[key])
+
+
+# ---- random batches vs the oracle ---------------------------------------------------
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+@pytest.mark.parametrize("n", [1, 7, 2049, 20000])
+@pytest.mark.parametrize("name", sorted(SCHEMAS))
+def test_random_parity(gpu_ctx, name, n, framed):
+    fields = SCHEMAS[name]
+    hb = random_batch(fields, n, seed=zlib.crc32(f"{name}/{n}/{framed}".encode()), dyn_len=(0, 40))
+    rc, want, want_offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total(framed) + 8,
+                                              framed=framed)
+    assert rc == 0
+    xdr, offs = gpu_encode(gpu_ctx, fields, hb, framed)
+    assert xdr == want
+    assert np.array_equal(offs, want_offs)
+    caps = hb.dyn_caps()
+    g = gpu_decode(gpu_ctx, fields, xdr, n, offs, caps, framed)
+    o = oracle_decode(fields, xdr, n, offs, caps, framed)
+    assert g[:3] == o[:3] == (0, n, 0)
+    assert g[3].equal(o[3])
+    if all(k != DY for _, k, _ in fields):   # fixed-stride decode without offsets
+        g2 = gpu_decode(gpu_ctx, fields, xdr, n, None, caps, framed, use_offsets=False)
+        assert g2[:3] == (0, n, 0) and g2[3].equal(o[3])
+
+
+@pytest.mark.parametrize("n", [4099, 4100])
+@pytest.mark.parametrize("name", ["cfg2_8xint", "words_mixed", "odd_words"])
+def test_aos_layout(gpu_ctx, name, n):
+    """Array-of-structs native records (one struct per record, fields at their
+    XDR word positions): the streaming path when n*words is a multiple of 4,
+    the word-map path over strided columns otherwise."""
+    fields = SCHEMAS[name]
+    hb = random_batch(fields, n, seed=7)
+    rc, want, _ = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total() + 8)
+    assert rc == 0
+    offs = xdr_word_offsets(fields)
+    rec = hb.xdr_total() // n
+    # pack the SoA host batch into one AoS buffer (native little-endian values)
+    aos = np.zeros((n, rec), dtype=np.uint8)
+    for k, a in enumerate(hb.arrays):
+        raw = np.ascontiguousarray(a).view(np.uint8).reshape(n, -1)
+        aos[:, offs[k]:offs[k] + raw.shape[1]] = raw
+    dev = torch.from_numpy(aos).cuda()
+    sch = engine.Schema(fields)
+    cols = aos_columns(fields, dev.data_ptr(), rec, offs)
+    out = torch.zeros(n * rec, dtype=torch.uint8, device="cuda")
+    assert gpu_ctx.encode(sch, cols, n, out, n * rec) == n * rec
+    assert out.cpu().numpy().tobytes() == want
+    back = torch.zeros_like(dev)
+    cols2 = aos_columns(fields, back.data_ptr(), rec, offs)
+    gpu_ctx.decode(sch, out, n * rec, n, cols2)
+    o = oracle_decode(fields, want, n, None, {})[3]
+    ob = np.zeros((n, rec), dtype=np.uint8)
+    for k, a in enumerate(o.arrays):
+        raw = np.ascontiguousarray(a).view(np.uint8).reshape(n, -1)
+        ob[:, offs[k]:offs[k] + raw.shape[1]] = raw
+    assert np.array_equal(back.cpu().numpy(), ob)
+
+
+# ---- error parity ------------------------------------------------------------------
+def _corrupt_cases(fields, hb, xdr, offs, framed):
+    """(description, bytes, rec_offsets) with one defect each."""
+    rng = np.random.default_rng(1)
+    cases = []
+    n = hb.n
+    b = bytearray(xdr)
+    cases.append(("truncated", bytes(b[:len(b) - 3]), offs))
+    cases.append(("truncated-half", bytes(b[:len(b) // 2]), offs))
+    dyn = [k for k, f in enumerate(fields) if f[1] == DY]
+    if dyn:
+        for val, desc in ((0xfffffffe, "negative"), (0x7ffffff0, "huge")):
+            bb = bytearray(xdr)
+            r = int(rng.integers(0, n))
+            pos = int(offs[r]) + (4 if framed else 0)
+            for k, f in enumerate(fields):
+                if f[1] == DY:
+                    break
+                pos += 4 * (f[2] if f[1] == FX else 1)   # only int fields precede it here
+            bb[pos:pos + 4] = val.to_bytes(4, "big")
+            cases.append((desc, bytes(bb), offs))
+    if framed:
+        bb = bytearray(xdr)
+        r = int(rng.integers(0, n))
+        bb[int(offs[r])] ^= 0x80   # clear LAST_FRAG
+        cases.append(("bad-mark", bytes(bb), offs))
+    return cases
+
+
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+@pytest.mark.parametrize("name", ["cfg2_8xint", "cfg4_int_string_intvec", "cfg3_6xint_opaque",
+                                  "cfg1_int_int_string"])
+def test_error_parity(gpu_ctx, name, framed):
+    fields = SCHEMAS[name]
+    n = 3000
+    hb = random_batch(fields, n, seed=11, dyn_len=(0, 20))
+    rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total(framed), framed=framed)
+    caps = hb.dyn_caps()
+    for desc, bad, ro in _corrupt_cases(fields, hb, xdr, offs, framed):
+        o = oracle_decode(fields, bad, n, ro, caps, framed)
+        g = gpu_decode(gpu_ctx, fields, bad, n, ro, caps, framed)
+        assert o[0] != 0, desc
+        assert g[:3] == o[:3], desc
+        assert g[3].equal(o[3], upto=o[1]), desc   # records before first_bad decoded
+        if all(k != DY for _, k, _ in fields):
+            g2 = gpu_decode(gpu_ctx, fields, bad, n, None, caps, framed, use_offsets=False)
+            o2 = oracle_decode(fields, bad, n, None, caps, framed)
+            assert g2[:3] == o2[:3], desc
+
+
+def test_decode_capacity(gpu_ctx):
+    fields = SCHEMAS["cfg4_int_string_intvec"]
+    hb = random_batch(fields, 500, seed=3, dyn_len=(1, 20))
+    rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), 500, hb.xdr_total())
+    caps = hb.dyn_caps()
+    small = dict(caps)
+    small[1] = caps[1] // 2
+    o = oracle_decode(fields, xdr, 500, offs, small)
+    g = gpu_decode(gpu_ctx, fields, xdr, 500, offs, small)
+    assert o[0] == abi.E_CAPACITY
+    assert g[:3] == o[:3]
+
+
+def test_encode_capacity(gpu_ctx):
+    for name in ("cfg2_8xint", "cfg4_int_string_intvec"):
+        fields = SCHEMAS[name]
+        hb = random_batch(fields, 100, seed=5, dyn_len=(1, 9))
+        total = hb.xdr_total()
+        sch = engine.Schema(fields)
+        db = DeviceBatch.from_host(hb)
+        out = torch.zeros(total, dtype=torch.uint8, device="cuda")
+        with pytest.raises(engine.CapacityError):
+            gpu_ctx.encode(sch, db.columns(), 100, out, total - 4)
+        assert not out.any(), "nothing may be written on XDRG_E_CAPACITY"
+
+
+def test_empty_batch(gpu_ctx):
+    for name in ("cfg2_8xint", "cfg4_int_string_intvec"):
+        fields = SCHEMAS[name]
+        hb = random_batch(fields, 0, seed=1)
+        xdr, offs = gpu_encode(gpu_ctx, fields, hb)
+        assert xdr == b"" and offs.tolist() == [0]
+        g = gpu_decode(gpu_ctx, fields, b"", 0, [0], {})
+        assert g[:3] == (0, 0, 0)
+
+
+# ---- framing ------------------------------------------------------------------------
+@pytest.mark.parametrize("case", gold.load("framing.json")["cases"], ids=lambda c: c["name"])
+def test_frame_scan(gpu_ctx, case):
+    stream = bytes.fromhex(case["stream"])
+    dev = torch.from_numpy(np.frombuffer(stream, dtype=np.uint8).copy()).cuda() if stream else \
+        torch.zeros(4, dtype=torch.uint8, device="cuda")
+    offs = torch.zeros(17, dtype=torch.int64, device="cuda")
+    k = gpu_ctx.frame_scan(dev, len(stream), offs, 16)
+    assert k == case["complete"]
+    assert offs[:k + 1].cpu().tolist() == case["offsets"]
+    rc, want = oracle.frame_scan(stream, 16)
+    assert want == case["offsets"]
+
+
+# ---- BASELINE-size properties (size-independent checks) -------------------------------
+@pytest.mark.slow
+def test_cfg2_full_size_roundtrip(gpu_ctx):
+    """configs[1]: 64 Mi records of 8 x int32: XDR == per-word byte reversal of
+    the native records, and decode(encode(x)) == x bit for bit."""
+    n = 64 << 20
+    fields = SCHEMAS["cfg2_8xint"]
+    g = torch.Generator(device="cuda").manual_seed(0x0DCAC4E5 + 2)
+    nat = torch.randint(-2**31, 2**31 - 1, (n, 8), dtype=torch.int32, device="cuda", generator=g)
+    sch = engine.Schema(fields)
+    cols = aos_columns(fields, nat.data_ptr(), 32, xdr_word_offsets(fields))
+    out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    assert gpu_ctx.encode(sch, cols, n, out, n * 32) == n * 32
+    assert torch.equal(out.view(-1, 4), nat.view(torch.uint8).view(-1, 4).flip(1))
+    back = torch.empty_like(nat)
+    gpu_ctx.decode(sch, out, n * 32, n, aos_columns(fields, back.data_ptr(), 32,
+                                                    xdr_word_offsets(fields)))
+    assert torch.equal(back, nat)
+    # framed variant: every 36-byte record = mark + the same 32 bytes
+    outf = torch.empty(n * 36, dtype=torch.uint8, device="cuda")
+    assert gpu_ctx.encode(sch, cols, n, outf, n * 36, framed=True) == n * 36
+    v = outf.view(n, 36)
+    assert torch.equal(v[:, 4:], out.view(n, 32))
+    mark = torch.tensor([0x80, 0, 0, 32], dtype=torch.uint8, device="cuda")
+    assert torch.equal(v[:, :4], mark.expand(n, 4))
