@@ -24,6 +24,9 @@
 // inter-workgroup hand-off), so nothing depends on XCD placement.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "xdrg_internal.h"
 
 namespace xdrg {
@@ -46,7 +49,7 @@ __device__ __forceinline__ uint64_t dyn_xdr_bytes(const VField &f, uint64_t cnt)
 
 // ---- element words ---------------------------------------------------------
 // XDR word `half` (0 = first) of one native element at p.
-__device__ __forceinline__ uint32_t enc_elem(uint8_t type, const uint8_t *p, uint32_t half) {
+__device__ __forceinline__ uint32_t enc_elem(uint32_t type, const uint8_t *p, uint32_t half) {
     switch (type) {
     case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: return bswap32r(*(const uint32_t *)p);
     case XDRG_T_FLOAT: return bswap32r(canon_f32r(*(const uint32_t *)p));
@@ -62,7 +65,7 @@ __device__ __forceinline__ uint32_t enc_elem(uint8_t type, const uint8_t *p, uin
     default: return 0;
     }
 }
-__device__ __forceinline__ void dec_elem(uint8_t type, uint8_t *p, uint32_t half, uint32_t v) {
+__device__ __forceinline__ void dec_elem(uint32_t type, uint8_t *p, uint32_t half, uint32_t v) {
     switch (type) {
     case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: case XDRG_T_FLOAT:
         *(uint32_t *)p = bswap32r(v); break;
@@ -496,7 +499,38 @@ __global__ void k_frame_scan(const uint8_t *in, uint64_t len, uint64_t *msg_offs
 // ===========================================================================
 // Launchers
 // ===========================================================================
+__global__ void k_debug_recargs(const RecArgs a) {
+    if (threadIdx.x || blockIdx.x) return;
+    printf("RecArgs n=%llu nf=%u framed=%u fixed_xdr=%u ndyn=%u xdr=%p cap=%llu rec_in=%p stride=%llu "
+           "nblocks=%llu\n", (unsigned long long)a.n, a.nf, a.framed, a.fixed_xdr, a.ndyn, a.xdr,
+           (unsigned long long)a.xdr_cap, a.rec_in, (unsigned long long)a.rec_stride,
+           (unsigned long long)a.nblocks);
+    if (a.rec_in) printf("  rec_in[0..2]=%llu %llu %llu\n", (unsigned long long)a.rec_in[0],
+                         (unsigned long long)a.rec_in[1], (unsigned long long)a.rec_in[2]);
+    for (uint32_t k = 0; k < a.nf; ++k)
+        printf("  f%u type=%u kind=%u nsz=%u xsz=%u count=%u xbytes=%u data=%p off=%p cap=%llu\n", k,
+               a.f[k].type, a.f[k].kind, a.f[k].nsz, a.f[k].xsz, a.f[k].count, a.f[k].xbytes,
+               a.f[k].data, a.f[k].offsets, (unsigned long long)a.f[k].cap);
+    uint64_t c;
+    uint32_t sub;
+    const uint32_t e = walk_record(a, 0, a.ndyn ? a.dyn_idx[0] : 0, &c, &sub);
+    printf("  walk(0) -> err=%u sub=%u cnt=%llu\n", e, sub, (unsigned long long)c);
+    const uint32_t *w = (const uint32_t *)a.xdr;
+    printf("  xdr words: %08x %08x %08x %08x  be: %u %u %u\n", w[0], w[1], w[2], w[3], ld_be32(a.xdr),
+           ld_be32(a.xdr + 4), ld_be32(a.xdr + 8));
+    const Extent ex = rec_extent(a, 0);
+    uint64_t pos = ex.a + 8;
+    const int32_t len = (int32_t)ld_be32(a.xdr + pos);
+    pos += 4;
+    const uint64_t need = (uint64_t)len + pad4((uint64_t)len);
+    printf("  ext=[%llu,%llu) len=%d need=%llu room=%llu pad=%u\n", (unsigned long long)ex.a,
+           (unsigned long long)ex.b, len, (unsigned long long)need, (unsigned long long)(ex.b - pos),
+           pad4((uint64_t)len));
+}
+
 int launch_rec_phase(const RecArgs &a, int phase, void *stream) {
+    if (phase == REC_DEC_SIZES && getenv("XDRG_DEBUG"))
+        hipLaunchKernelGGL(k_debug_recargs, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
     switch (phase) {

@@ -396,17 +396,17 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
     for (size_t k = 0; k < s->f.size(); ++k) {
         VField &v = a.f[k];
         const xdrg_field &f = s->f[k];
-        v.type = (uint8_t)f.type;
-        v.kind = (uint8_t)f.kind;
-        v.nsz = (uint8_t)s->nsz[k];
-        v.xsz = (uint8_t)s->xsz[k];
+        v.type = f.type;
+        v.kind = f.kind;
+        v.nsz = s->nsz[k];
+        v.xsz = s->xsz[k];
         v.count = f.count;
         v.xbytes = s->xbytes[k];
         v.data = (uint8_t *)cols[k].data;
         v.stride = f.kind == XDRG_K_DYNAMIC ? 0 : eff_stride(s, k, cols[k]);
         v.offsets = cols[k].offsets;
         v.cap = cols[k].cap;
-        if (f.kind == XDRG_K_DYNAMIC) a.dyn_idx[a.ndyn++] = (uint8_t)k;
+        if (f.kind == XDRG_K_DYNAMIC) a.dyn_idx[a.ndyn++] = (uint32_t)k;
     }
     a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;
     if (!a.nblocks) a.nblocks = 1;

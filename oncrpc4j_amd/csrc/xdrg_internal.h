@@ -84,14 +84,18 @@ struct StreamArgs {
 };
 
 // ---- record path (variable-size schemas) --------------------------------
+// Every member is 32 or 64 bits wide: the record kernels read these
+// descriptors with scalar (SMEM) loads at uniform field indices, and a
+// byte-wide member lets the compiler form a misaligned SMEM base whose low
+// address bits the scalar unit drops (observed on gfx950: a dword load at
+// base 0x81 + 7 returned the dword at 0x84).
 struct VField {
-    uint8_t type;     // XDRG_T_*
-    uint8_t kind;     // XDRG_K_*
-    uint8_t nsz;      // native element bytes
-    uint8_t xsz;      // XDR element bytes (1 for opaque/string)
+    uint32_t type;    // XDRG_T_*
+    uint32_t kind;    // XDRG_K_*
+    uint32_t nsz;     // native element bytes
+    uint32_t xsz;     // XDR element bytes (1 for opaque/string)
     uint32_t count;   // FIXED count
     uint32_t xbytes;  // fixed fields: XDR bytes of the field (incl. pad)
-    uint32_t rsv;
     uint8_t *data;
     int64_t stride;
     uint64_t *offsets;
@@ -113,7 +117,7 @@ struct RecArgs {
     uint64_t nblocks;
     uint64_t *totals;          // workspace [ndyn+1]: scanned totals
     unsigned long long *errkey;
-    uint8_t dyn_idx[kMaxFields];  // dynamic field -> field index
+    uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
 };
 
