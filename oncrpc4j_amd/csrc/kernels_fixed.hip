@@ -50,7 +50,7 @@ __device__ __forceinline__ void st4(u32x4 *p, u32x4 v) {
 // ---------------------------------------------------------------------------
 // Streaming kernels (AoS-dense layouts).
 // ---------------------------------------------------------------------------
-template <int U, bool NT>
+template <int U, bool NTL, bool NTS>
 __global__ __launch_bounds__(256) void k_stream_bswap(const u32x4 *__restrict__ src,
                                                       u32x4 *__restrict__ dst, uint64_t nvec) {
     const uint64_t step = (uint64_t)gridDim.x * (256 * U);
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void k_stream_bswap(const u32x4 *__restrict__ 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t k = i + (uint64_t)u * 256;
-            if (k < nvec) v[u] = ld4<NT>(src + k);
+            if (k < nvec) v[u] = ld4<NTL>(src + k);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void k_stream_bswap(const u32x4 *__restrict__ 
                 u32x4 o;
                 o.x = bswap32(v[u].x); o.y = bswap32(v[u].y);
                 o.z = bswap32(v[u].z); o.w = bswap32(v[u].w);
-                st4<NT>(dst + k, o);
+                st4<NTS>(dst + k, o);
             }
         }
     }
@@ -285,23 +285,58 @@ static uint64_t grid_for(uint64_t work_items, uint64_t per_block, uint64_t max_b
     return b ? b : 1;
 }
 
-// variant bits: 0x1 = nontemporal, 0x2 = op table (mixed types)
+// Streaming-kernel tuning (defaults chosen by tools/tune_stream.py on MI355X;
+// see DESIGN.md).  Set through xdrg_internal_tune(), outside the C-ABI.
+static int g_stream_unroll = 1;         // 16-byte vectors in flight per lane
+static int g_stream_nt = 3;             // bit 0: nontemporal loads, bit 1: stores
+static int g_stream_blocks_per_cu = 0;  // grid = min(needed, CUs * this); 0 = one pass
+
+template <int U>
+static void launch_bswap_u(const u32x4 *src, u32x4 *dst, uint64_t nvec, uint64_t blocks, int nt,
+                           hipStream_t st) {
+    switch (nt & 3) {
+    case 0: hipLaunchKernelGGL((k_stream_bswap<U, false, false>), dim3(blocks), dim3(256), 0, st, src, dst, nvec); break;
+    case 1: hipLaunchKernelGGL((k_stream_bswap<U, true, false>), dim3(blocks), dim3(256), 0, st, src, dst, nvec); break;
+    case 2: hipLaunchKernelGGL((k_stream_bswap<U, false, true>), dim3(blocks), dim3(256), 0, st, src, dst, nvec); break;
+    default: hipLaunchKernelGGL((k_stream_bswap<U, true, true>), dim3(blocks), dim3(256), 0, st, src, dst, nvec); break;
+    }
+}
+
 int launch_stream_words(const StreamArgs &a, int variant, void *stream) {
+    (void)variant;
     if (!a.nvec) return hipSuccess;
     hipStream_t st = (hipStream_t)stream;
-    constexpr int U = 4;
-    const uint64_t blocks = grid_for(a.nvec, 256 * U, (uint64_t)num_cu() * 16);
-    const bool nt = variant & 1;
+    const int U = g_stream_unroll;
+    const uint64_t cap = g_stream_blocks_per_cu > 0 ? (uint64_t)num_cu() * g_stream_blocks_per_cu : ~0ull;
+    const uint64_t blocks = grid_for(a.nvec, 256 * (uint64_t)U, cap);
     if (a.all_bswap) {
         const u32x4 *src = (const u32x4 *)a.src;
         u32x4 *dst = (u32x4 *)a.dst;
-        if (nt) hipLaunchKernelGGL((k_stream_bswap<U, true>), dim3(blocks), dim3(256), 0, st, src, dst, a.nvec);
-        else hipLaunchKernelGGL((k_stream_bswap<U, false>), dim3(blocks), dim3(256), 0, st, src, dst, a.nvec);
+        switch (U) {
+        case 1: launch_bswap_u<1>(src, dst, a.nvec, blocks, g_stream_nt, st); break;
+        case 2: launch_bswap_u<2>(src, dst, a.nvec, blocks, g_stream_nt, st); break;
+        case 8: launch_bswap_u<8>(src, dst, a.nvec, blocks, g_stream_nt, st); break;
+        default: launch_bswap_u<4>(src, dst, a.nvec, blocks, g_stream_nt, st); break;
+        }
     } else {
-        if (nt) hipLaunchKernelGGL((k_stream_ops<U, true>), dim3(blocks), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((k_stream_ops<U, false>), dim3(blocks), dim3(256), 0, st, a);
+        const uint64_t b4 = grid_for(a.nvec, 256 * 4, cap);
+        if (g_stream_nt) hipLaunchKernelGGL((k_stream_ops<4, true>), dim3(b4), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((k_stream_ops<4, false>), dim3(b4), dim3(256), 0, st, a);
     }
     return (int)hipGetLastError();
+}
+
+// key 1: unroll (1/2/4/8), key 2: nontemporal bits, key 3: blocks per CU (0 = one pass)
+int set_tuning(int key, long long value) {
+    switch (key) {
+    case 1:
+        if (value != 1 && value != 2 && value != 4 && value != 8) return -1;
+        g_stream_unroll = (int)value;
+        return 0;
+    case 2: g_stream_nt = (int)(value & 3); return 0;
+    case 3: if (value < 0) return -1; g_stream_blocks_per_cu = (int)value; return 0;
+    default: return -1;
+    }
 }
 
 static void wordmap_grid(WordMapArgs &a, uint64_t words, uint64_t *blocks) {

@@ -215,6 +215,9 @@ struct TimedLaunch {
 
 extern "C" int xdrg_abi_version(void) { return XDRG_ABI_VERSION; }
 
+// Not part of include/xdrg.h: kernel tuning knobs for tools/tune_stream.py.
+extern "C" int xdrg_internal_tune(int key, long long value) { return set_tuning(key, value); }
+
 extern "C" const char *xdrg_status_string(int status) {
     switch (status) {
     case XDRG_OK: return "ok";

@@ -134,6 +134,7 @@ constexpr unsigned long long kNoError = ~0ull;
 // ---- launchers (kernels.hip) -------------------------------------------
 // All launches go on `stream`; each returns hipSuccess or the launch error.
 int launch_stream_words(const StreamArgs &a, int variant, void *stream);
+int set_tuning(int key, long long value);  // streaming-kernel knobs (tools/tune_stream.py)
 int launch_wordmap_encode(const WordMapArgs &a, bool aligned16, void *stream);
 int launch_wordmap_decode(const WordMapArgs &a, bool aligned16, void *stream);
 enum RecPhase { REC_ENC_SIZES, REC_ENC_SCAN, REC_ENC_PLACE, REC_DEC_SIZES, REC_DEC_SCAN, REC_DEC_PLACE };
