@@ -37,7 +37,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--records", type=int, default=64 << 20, help="records per GPU")
+    p.add_argument("--config", type=int, default=2, choices=[2, 3, 4],
+                   help="BASELINE config: 2 = 8 x int32 (the metric's workload), 3 = 6 x int32 + "
+                        "opaque<4096>, 4 = int32 + string(8..256) + int32<0..16>")
+    p.add_argument("--records", type=int, default=0, help="records per GPU (0 = the config's size)")
     p.add_argument("--framed", action="store_true", help="record-marked variant (36 B records)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline budget (0 = skip)")
     p.add_argument("--no-host-inclusive", action="store_true")
@@ -185,79 +188,173 @@ def host_inclusive(ctx, sch, cols_fn, n, rec_bytes):
             "method": "pinned host, 4 Mi-record chunks, 2 streams, H2D/encode/D2H then H2D/decode/D2H"}
 
 
+class Workload:
+    """One BASELINE config made concrete: device-resident native columns, the
+    XDR stream, decode targets, and one step = encode batch + decode batch."""
+
+    def __init__(self, cfg, n, framed, rank):
+        import torch
+        from oncrpc4j_amd import abi, engine
+        from oncrpc4j_amd.columns import aos_columns
+        self.cfg, self.n, self.framed = cfg, n, framed
+        I, SC, DY = abi.T_INT, abi.K_SCALAR, abi.K_DYNAMIC
+        g = torch.Generator(device="cuda").manual_seed(0x0DCAC4E5 + cfg + 1000 * rank)
+        dev = "cuda"
+        if cfg == 2:
+            self.fields = [(I, SC, 0)] * 8
+            rec = 36 if framed else 32
+            self.nat = torch.randint(-2**31, 2**31 - 1, (n, 8), dtype=torch.int32, device=dev, generator=g)
+            self.back = torch.empty_like(self.nat)
+            offs = [4 * k for k in range(8)]
+            self.cin = aos_columns(self.fields, self.nat.data_ptr(), 32, offs)
+            self.cout = aos_columns(self.fields, self.back.data_ptr(), 32, offs)
+            self.xlen = n * rec
+            self.native_bytes = n * 32
+            self.rec_offsets = None
+            self.kernels = ("k_wordmap_encode" if framed else "k_stream_bswap",
+                            abi.KERNEL_FIXED_ENCODE, abi.KERNEL_FIXED_DECODE)
+            self.desc = ("configs[1]: 64 Mi fixed-schema records of 8 x int32 (32 B), encode+decode "
+                         "round trip, array-of-structs native records" if not framed else
+                         "configs[1] record-marked variant (36 B XDR records)")
+        else:
+            if cfg == 3:   # 6 x int32 header (AoS) + opaque<> of 4096 B
+                self.fields = [(I, SC, 0)] * 6 + [(abi.T_OPAQUE, DY, 0)]
+                nh = 6
+                lens = torch.full((n,), 4096, dtype=torch.int64, device=dev)
+            else:          # int32 + string(8..256) + int32<0..16>
+                self.fields = [(I, SC, 0), (abi.T_STRING, DY, 0), (I, DY, 0)]
+                nh = 1
+                lens = torch.randint(8, 257, (n,), dtype=torch.int64, device=dev, generator=g)
+            self.hdr = torch.randint(-2**31, 2**31 - 1, (n, nh), dtype=torch.int32, device=dev, generator=g)
+            self.hdr_back = torch.empty_like(self.hdr)
+            self.dyn = []       # (values, offsets, values_back, offsets_back) per dynamic field
+            offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(lens, 0, out=offs[1:])
+            total = int(offs[-1])
+            if cfg == 3:
+                vals = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+            else:
+                vals = torch.randint(97, 123, (total,), dtype=torch.uint8, device=dev, generator=g)
+            self.dyn.append((vals, offs, torch.empty_like(vals), torch.empty_like(offs)))
+            if cfg == 4:
+                k = torch.randint(0, 17, (n,), dtype=torch.int64, device=dev, generator=g)
+                o2 = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+                torch.cumsum(k, 0, out=o2[1:])
+                v2 = torch.randint(-2**31, 2**31 - 1, (int(o2[-1]),), dtype=torch.int32, device=dev,
+                                   generator=g)
+                self.dyn.append((v2, o2, torch.empty_like(v2), torch.empty_like(o2)))
+            self.cin = self._cols(self.hdr, [(d[0], d[1]) for d in self.dyn], nh)
+            self.cout = self._cols(self.hdr_back, [(d[2], d[3]) for d in self.dyn], nh)
+            # XDR sizes: fixed part + per dynamic field 4 + payload (+pad)
+            size = torch.full((n,), 4 * nh + (4 if framed else 0), dtype=torch.int64, device=dev)
+            for (t, kd, _), d in zip([f for f in self.fields if f[1] == DY], self.dyn):
+                cnt = d[1][1:] - d[1][:-1]
+                size += 4 + (cnt + ((4 - (cnt & 3)) & 3) if t in (abi.T_OPAQUE, abi.T_STRING) else 4 * cnt)
+            self.xlen = int(size.sum())
+            self.rec_offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            self.native_bytes = n * 4 * nh + sum(d[0].numel() * d[0].element_size() for d in self.dyn)
+            self.kernels = ("k_enc_place/k_dec_place", abi.KERNEL_VAR_ENCODE, abi.KERNEL_VAR_DECODE)
+            self.desc = ("configs[2]: 16 Mi NFS-WRITE-shaped records, 6 x int32 + opaque<4096>"
+                         if cfg == 3 else
+                         "configs[3]: 32 Mi records int32 + string(8..256) + int32<0..16>")
+        self.xdr = torch.empty(self.xlen, dtype=torch.uint8, device=dev)
+        self.sch = engine.Schema(self.fields)
+        # per-record algorithmic bytes: encode reads native + writes XDR, decode the reverse
+        self.bytes_per_step = 2 * (self.native_bytes + self.xlen)
+
+    def _cols(self, hdr, dyn, nh):
+        from oncrpc4j_amd import abi
+        arr = (abi.Column * len(self.fields))()
+        for k in range(nh):
+            arr[k].data = hdr.data_ptr() + 4 * k
+            arr[k].stride = 4 * nh
+        for j, (v, o) in enumerate(dyn):
+            arr[nh + j].data = v.data_ptr()
+            arr[nh + j].offsets = o.data_ptr()
+            arr[nh + j].cap = v.numel()
+        arr._keep = (hdr, dyn)
+        return arr
+
+    def step(self, ctx):
+        ctx.encode(self.sch, self.cin, self.n, self.xdr, self.xlen, rec_offsets=self.rec_offsets,
+                   framed=self.framed, async_=True)
+        ctx.decode(self.sch, self.xdr, self.xlen, self.n, self.cout, rec_offsets=self.rec_offsets,
+                   framed=self.framed, async_=True)
+
+    def check(self):
+        import torch
+        if self.cfg == 2:
+            assert torch.equal(self.back, self.nat), "decode(encode(x)) != x"
+            if not self.framed:
+                m = min(self.n, 1 << 20) * 8
+                assert torch.equal(self.xdr.view(-1, 4)[:m], self.nat.view(torch.uint8).view(-1, 4)[:m].flip(1))
+            return
+        assert torch.equal(self.hdr_back, self.hdr), "header columns differ"
+        for v, o, vb, ob in self.dyn:
+            assert torch.equal(ob, o), "offsets differ"
+            assert torch.equal(vb, v), "values differ"
+
+
 def main():
     args = parse()
     import torch
-    from oncrpc4j_amd import abi, engine
-    from oncrpc4j_amd.columns import aos_columns
+    from oncrpc4j_amd import engine
 
     world, rank, local = dist_setup(args)
-    n = args.records
-    rec_bytes = 36 if args.framed else 32
-    fields = [(abi.T_INT, abi.K_SCALAR, 0)] * 8
-    offs = [4 * k for k in range(8)]
-    sch = engine.Schema(fields)
+    n = args.records if args.records else {2: 64 << 20, 3: 16 << 20, 4: 32 << 20}[args.config]
+    wl = Workload(args.config, n, args.framed, rank)
     ctx = engine.Context(local, timing=True)
-    stream = torch.cuda.current_stream()
-    ctx.set_stream(stream)
-
-    g = torch.Generator(device="cuda").manual_seed(0x0DCAC4E5 + 2 + rank)
-    nat = torch.randint(-2**31, 2**31 - 1, (n, 8), dtype=torch.int32, device="cuda", generator=g)
-    back = torch.empty_like(nat)
-    xdr = torch.empty(n * rec_bytes, dtype=torch.uint8, device="cuda")
-    cin = aos_columns(fields, nat.data_ptr(), 32, offs)
-    cout = aos_columns(fields, back.data_ptr(), 32, offs)
-    xlen = n * rec_bytes
-
-    def step():
-        ctx.encode(sch, cin, n, xdr, xlen, framed=args.framed, async_=True)
-        ctx.decode(sch, xdr, xlen, n, cout, framed=args.framed, async_=True)
+    ctx.set_stream(torch.cuda.current_stream())
 
     for _ in range(args.warmup):
-        step()
+        wl.step(ctx)
     torch.cuda.synchronize()
-    # correctness of the measured path (outside the timed region)
-    assert torch.equal(back, nat), "decode(encode(x)) != x"
-    if not args.framed:
-        assert torch.equal(xdr.view(-1, 4)[:1 << 20], nat.view(torch.uint8).view(-1, 4)[:1 << 20].flip(1))
+    wl.check()   # correctness of the measured path, outside the timed region
     ctx.reset_stats()
 
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        wl.step(ctx)
     torch.cuda.synchronize()
     barrier(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
 
-    # per-kernel HIP-event durations (same stream, same timed region)
-    ne, ms_e = ctx.kernel_stats(abi.KERNEL_FIXED_ENCODE)
-    nd, ms_d = ctx.kernel_stats(abi.KERNEL_FIXED_DECODE)
-    kernel = "k_wordmap_encode" if args.framed else "k_stream_bswap"
+    # dominant kernel(s): per-launch HIP-event durations, same stream, same region
+    kname, kid_e, kid_d = wl.kernels
+    ne, ms_e = ctx.kernel_stats(kid_e)
+    nd, ms_d = ctx.kernel_stats(kid_d)
     launches = ne + nd
     avg_ms = (ms_e + ms_d) / max(launches, 1)
-    per_launch_bytes = n * (rec_bytes + 32)       # read one side + write the other
+    per_launch_bytes = wl.native_bytes + wl.xlen   # one side read, the other written
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    step_kernel_ms = {}
+    for kid, name in ((0, "fixed_encode"), (1, "fixed_decode"), (2, "var_size"), (3, "var_scan"),
+                      (4, "var_encode"), (5, "var_decode")):
+        c, ms = ctx.kernel_stats(kid)
+        if c:
+            step_kernel_ms[name] = round(ms / args.steps, 4)
 
     total_records = n * world * args.steps
-    value = total_records * (BYTES_PER_RECORD + (2 * 4 if args.framed else 0)) / dt / GIB
+    value = wl.bytes_per_step * world * args.steps / dt / GIB
 
     gather = None
     if world > 1:
         import torch.distributed as dist
+        xlen = wl.xlen
         full = torch.empty(world * xlen, dtype=torch.uint8, device="cuda")
-        dist.all_gather_into_tensor(full, xdr)
+        dist.all_gather_into_tensor(full, wl.xdr)
         torch.cuda.synchronize()
         barrier(world)
         t1 = time.perf_counter()
         reps = 3
         for _ in range(reps):
-            dist.all_gather_into_tensor(full, xdr)
+            dist.all_gather_into_tensor(full, wl.xdr)
         torch.cuda.synchronize()
         barrier(world)
         gdt = max_over_ranks((time.perf_counter() - t1) / reps, world)
-        ok = torch.equal(full[rank * xlen:(rank + 1) * xlen], xdr)
+        ok = torch.equal(full[rank * xlen:(rank + 1) * xlen], wl.xdr)
         gather = {"ms": round(gdt * 1e3, 3), "bytes_in_per_gpu": (world - 1) * xlen,
                   "GBps_in_per_gpu": round((world - 1) * xlen / gdt / 1e9, 2),
                   "stream_bytes": world * xlen, "own_shard_ok": bool(ok),
@@ -266,9 +363,9 @@ def main():
 
     cpu = None
     hinc = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and args.config == 2 and not args.framed:
         if not args.no_host_inclusive:
-            hinc = host_inclusive(ctx, sch, None, min(n, 64 << 20), rec_bytes)
+            hinc = host_inclusive(ctx, wl.sch, None, min(n, 64 << 20), 32)
         if args.cpu_seconds > 0:
             cpu = cpu_baseline(args.cpu_seconds)
 
@@ -278,21 +375,19 @@ def main():
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
-            "data": "synthetic (seeded uniform int32)",
-            "config": {"workload": "configs[1]: 64 Mi fixed-schema records of 8 x int32 (32 B), "
-                                   "encode+decode round trip, array-of-structs native records"
-                       if not args.framed else
-                       "configs[1] record-marked variant (36 B XDR records)",
-                       "records_per_gpu": n, "record_bytes_native": 32, "record_bytes_xdr": rec_bytes,
-                       "bytes_per_record": BYTES_PER_RECORD + (8 if args.framed else 0),
+            "data": "synthetic (seeded uniform int32 / random bytes / [a-z] strings)",
+            "config": {"workload": wl.desc, "records_per_gpu": n, "xdr_bytes_per_gpu": wl.xlen,
+                       "native_bytes_per_gpu": wl.native_bytes, "bytes_per_step_per_gpu": wl.bytes_per_step,
+                       "framed": bool(args.framed),
                        "parallelism": f"records sharded {world} ways" if world > 1 else "single GPU"},
             "mrecords_per_s": round(total_records / dt / 1e6, 2),
-            "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
-                         "traffic": load_traffic(kernel, n),
+                         "traffic": load_traffic(kname, n),
                          "launches": launches, "avg_launch_ms": round(avg_ms, 4),
                          "bytes_per_launch": per_launch_bytes},
+            "kernel_ms_per_step": step_kernel_ms,
             "cpu_baseline": cpu,
             "host_inclusive": hinc,
             "gather": gather,
