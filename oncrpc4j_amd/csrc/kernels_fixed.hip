@@ -326,7 +326,8 @@ int launch_stream_words(const StreamArgs &a, int variant, void *stream) {
     return (int)hipGetLastError();
 }
 
-// key 1: unroll (1/2/4/8), key 2: nontemporal bits, key 3: blocks per CU (0 = one pass)
+// key 1: unroll (1/2/4/8), key 2: nontemporal bits, key 3: blocks per CU (0 = one pass),
+// keys 4/5: record-path encode/decode copy unroll (1/2/4)
 int set_tuning(int key, long long value) {
     switch (key) {
     case 1:
@@ -335,6 +336,7 @@ int set_tuning(int key, long long value) {
         return 0;
     case 2: g_stream_nt = (int)(value & 3); return 0;
     case 3: if (value < 0) return -1; g_stream_blocks_per_cu = (int)value; return 0;
+    case 4: case 5: case 6: case 7: case 8: return set_rec_tuning(key, value);
     default: return -1;
     }
 }

@@ -414,10 +414,14 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
     a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;
     if (!a.nblocks) a.nblocks = 1;
     const size_t rows = a.ndyn ? a.ndyn : 1;
-    int rc = ensure_ws(c, rows * a.nblocks + rows + 8);
+    // block sums [rows][nblocks] | totals [rows] (+ pad) | per-record counts u32 [ndyn][n]
+    const size_t sums_words = rows * a.nblocks + rows + 8;
+    const size_t cnt_words = (a.ndyn * n + 1) / 2;
+    int rc = ensure_ws(c, sums_words + cnt_words);
     if (rc) return rc;
     a.block_sums = c->d_ws;
     a.totals = c->d_ws + rows * a.nblocks;
+    a.rec_cnt = (uint32_t *)(c->d_ws + sums_words);
     a.errkey = c->d_stat;
     return XDRG_OK;
 }

@@ -117,6 +117,11 @@ struct RecArgs {
     uint64_t nblocks;
     uint64_t *totals;          // workspace [ndyn+1]: scanned totals
     unsigned long long *errkey;
+    uint32_t *rec_cnt;         // decode workspace [ndyn][n]: element count per record
+    uint32_t force_g;          // 0 = group size from the average field size, else lanes per record
+    uint32_t lane_bytes_enc;   // group sizing: target XDR bytes per lane (encode / decode)
+    uint32_t lane_bytes_dec;
+    uint32_t rsv0;
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
 };
@@ -134,7 +139,8 @@ constexpr unsigned long long kNoError = ~0ull;
 // ---- launchers (kernels.hip) -------------------------------------------
 // All launches go on `stream`; each returns hipSuccess or the launch error.
 int launch_stream_words(const StreamArgs &a, int variant, void *stream);
-int set_tuning(int key, long long value);  // streaming-kernel knobs (tools/tune_stream.py)
+int set_tuning(int key, long long value);      // kernel knobs (tools/tune_*.py)
+int set_rec_tuning(int key, long long value);
 int launch_wordmap_encode(const WordMapArgs &a, bool aligned16, void *stream);
 int launch_wordmap_decode(const WordMapArgs &a, bool aligned16, void *stream);
 enum RecPhase { REC_ENC_SIZES, REC_ENC_SCAN, REC_ENC_PLACE, REC_DEC_SIZES, REC_DEC_SCAN, REC_DEC_PLACE };
@@ -151,7 +157,8 @@ int launch_frame_scan(const uint8_t *in, uint64_t len, uint64_t *msg_offsets, ui
                       uint64_t *result, void *stream);
 
 constexpr int kRecThreads = 256;   // record path: threads per block
-constexpr int kRecPerThread = 8;   // records per thread in the size/scan pass
+constexpr int kRecPerThread = 4;   // records per thread in the size/scan pass
 constexpr int kRecPerBlock = kRecThreads * kRecPerThread;
+constexpr int kMaxDynLds = 4;      // dynamic fields whose per-record metadata is staged in LDS
 
 }  // namespace xdrg

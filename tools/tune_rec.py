@@ -1,0 +1,66 @@
+"""Interleaved sweep of the record-path copy unroll (encode / decode place
+kernels) on BASELINE configs 3 and 4 (bench.py workloads), one process."""
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from oncrpc4j_amd import abi, engine  # noqa: E402
+
+
+def main():
+    cfgs = [int(c) for c in os.environ.get("CONFIGS", "4,3").split(",")]
+    rounds = int(os.environ.get("ROUNDS", 5))
+    L = engine.lib()
+    L.xdrg_internal_tune.argtypes = [ctypes.c_int, ctypes.c_longlong]
+    for cfg in cfgs:
+        n = {3: 16 << 20, 4: 32 << 20}[cfg]
+        wl = bench.Workload(cfg, n, False, 0)
+        ctx = engine.Context(0, timing=True)
+        ctx.set_stream(torch.cuda.current_stream())
+        wl.step(ctx)
+        torch.cuda.synchronize()
+        wl.check()
+        res = {}
+        variants = [(u, lb) for u in (1, 2) for lb in (16, 32, 64, 128, 256, 512)]
+        for r in range(rounds):
+            for u, g in variants:
+                L.xdrg_internal_tune(4, u)
+                L.xdrg_internal_tune(5, u)
+                L.xdrg_internal_tune(7, g)
+                L.xdrg_internal_tune(8, g)
+                ctx.reset_stats()
+                wl.step(ctx)
+                torch.cuda.synchronize()
+                for kid, name in ((abi.KERNEL_VAR_SIZE, "sizes"), (abi.KERNEL_VAR_SCAN, "scan"),
+                                  (abi.KERNEL_VAR_ENCODE, "enc_place"), (abi.KERNEL_VAR_DECODE, "dec_place")):
+                    c, ms = ctx.kernel_stats(kid)
+                    res.setdefault((u, g, name), []).append(ms)
+        L.xdrg_internal_tune(4, 2)   # defaults (kernels_rec.hip)
+        L.xdrg_internal_tune(5, 2)
+        L.xdrg_internal_tune(7, 32)
+        L.xdrg_internal_tune(8, 32)
+        wl.step(ctx)
+        torch.cuda.synchronize()
+        wl.check()
+        per_launch = wl.native_bytes + wl.xlen
+        for (u, g, name), t in sorted(res.items()):
+            med = statistics.median(t)
+            d = {"config": cfg, "unroll": u, "lane_bytes": g, "kernel": name, "median_ms": round(med, 4)}
+            if name.endswith("place"):
+                d["GBps"] = round(per_launch / med / 1e6, 1)
+            print(json.dumps(d), flush=True)
+        ctx.close()
+        del wl
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
