@@ -979,6 +979,785 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_flat(const RecArgs a) {
 }
 
 // ===========================================================================
+// Column-major place kernels (the default for <= kMaxDynLds dynamic fields)
+//
+// Pass R, one thread per record: the small parts of every record — record
+// mark, fixed fields, length words, zero pad (and the rare 2-byte/1-byte/
+// 8-byte dynamic vectors).  Pass C, once per opaque/string/4-byte-vector
+// column: the column's contiguous native range of the block is swept in
+// 16-byte chunks (coalesced on the native side, kFlatU chunks per lane in
+// flight); a chunk finds its record through a coarse LDS table and moves with
+// one unaligned 16-byte access on the XDR side.  Chunks straddling a record
+// boundary (one per record per column) go byte by byte.
+// ===========================================================================
+__device__ __forceinline__ uint32_t chunk_byte(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t i) {
+    const uint32_t w = i < 4 ? w0 : i < 8 ? w1 : i < 12 ? w2 : w3;
+    return (w >> (8 * (i & 3))) & 0xffu;
+}
+__device__ __forceinline__ uint32_t chunk_word(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t i) {
+    return i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+}
+
+// Table entry e: record holding element max(first element of chunk
+// cbase + (e << sh), lo).
+__device__ __forceinline__ void build_tab(const uint64_t *key, uint32_t n, uint64_t cbase, uint32_t sh,
+                                          uint32_t per_chunk_shift, uint64_t lo, uint32_t *tab) {
+    for (uint32_t e = threadIdx.x; e <= kLookup; e += blockDim.x) {
+        uint64_t q = (cbase + ((uint64_t)e << sh)) << per_chunk_shift;
+        if (q < lo) q = lo;
+        tab[e] = find_rec(key, n, q);
+    }
+}
+__device__ __forceinline__ uint32_t tab_find(const uint64_t *key, uint32_t n, const uint32_t *tab, uint64_t cbase,
+                                             uint32_t sh, uint64_t c, uint64_t q) {
+    const uint64_t e = (c - cbase) >> sh;
+    uint32_t lo = tab[e];
+    uint32_t hi = tab[e + 1] + 1;
+    if (hi > n) hi = n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (key[mid] <= q) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// LDS: soff[RPB + 2] u64 | ssrc[ND][RPB] u64 | scnt[ND][RPB] u32 | spst[ND][RPB] u32
+__host__ __device__ constexpr size_t enc_col_lds_bytes(uint32_t nd) {
+    return (size_t)(kRecPerBlock + 2) * 8 + (size_t)nd * kRecPerBlock * 16;
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_enc_col(const RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t ND = a.ndyn;
+    uint64_t *soff = (uint64_t *)smem;
+    uint64_t *ssrc = soff + kRecPerBlock + 2;
+    uint32_t *scnt = (uint32_t *)(ssrc + (size_t)ND * kRecPerBlock);
+    uint32_t *spst = scnt + (size_t)ND * kRecPerBlock;
+    __shared__ uint32_t tab[kLookup + 1];
+    __shared__ VField sf[kMaxFields];
+    const uint64_t total = a.totals[0];
+    if (total > a.xdr_cap) return;  // XDRG_E_CAPACITY: write nothing
+    stage_fields(a, sf);
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t t0 = threadIdx.x * kRecPerThread;
+    uint64_t sz[kRecPerThread];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        const uint64_t r = rb + t0 + j;
+        uint64_t pos = 0;
+        if (r < a.n) {
+            pos = a.framed ? 4 : 0;
+            uint32_t d = 0;
+            for (uint32_t k = 0; k < a.nf; ++k) {
+                const VField &f = a.f[k];
+                if (f.kind != XDRG_K_DYNAMIC) { pos += f.xbytes; continue; }
+                const uint64_t o0 = f.offsets[r], cnt = f.offsets[r + 1] - o0;
+                ssrc[(size_t)d * kRecPerBlock + t0 + j] = o0;
+                scnt[(size_t)d * kRecPerBlock + t0 + j] = (uint32_t)cnt;
+                spst[(size_t)d * kRecPerBlock + t0 + j] = (uint32_t)(pos + 4);
+                pos += dyn_xdr_bytes(f, cnt);
+                ++d;
+            }
+        }
+        sz[j] = pos;
+        s += pos;
+    }
+    uint64_t btot;
+    uint64_t off = a.block_sums[blockIdx.x] + block_excl_scan(s, &btot);
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        soff[t0 + j] = off;
+        if (a.rec_out && rb + t0 + j < a.n) a.rec_out[rb + t0 + j] = off;
+        off += sz[j];
+    }
+    if (threadIdx.x == kRecThreads - 1) soff[kRecPerBlock] = off;
+    if (a.rec_out && blockIdx.x == 0 && threadIdx.x == 0) a.rec_out[a.n] = total;
+    __syncthreads();
+    const uint32_t nrec = (uint32_t)(a.n - rb < kRecPerBlock ? a.n - rb : kRecPerBlock);
+    uint8_t *out = a.xdr;
+
+    // ---- pass R: marks, fixed fields, length words, pads, rare vectors
+    for (uint32_t j = threadIdx.x; j < nrec; j += kRecThreads) {
+        const uint64_t r = rb + j;
+        uint8_t *base = out + soff[j];
+        uint64_t pos = 0;
+        if (a.framed) {
+            *(uint32_t *)base = bswap32r((uint32_t)(soff[j + 1] - soff[j] - 4) | kLastFrag);
+            pos = 4;
+        }
+        uint32_t d = 0;
+        for (uint32_t k = 0; k < a.nf; ++k) {
+            const VField &f = sf[k];
+            if (f.kind != XDRG_K_DYNAMIC) {
+                const uint32_t nw = f.xbytes >> 2;
+                for (uint32_t i = 0; i < nw; ++i) *(uint32_t *)(base + pos + 4 * i) = fixed_word(f, r, 4 * i);
+                pos += f.xbytes;
+                continue;
+            }
+            const uint64_t cnt = scnt[(size_t)d * kRecPerBlock + j];
+            *(uint32_t *)(base + pos) = bswap32r((uint32_t)cnt);
+            if (f.xsz == 1) {
+                const uint32_t pad = pad4(cnt);
+                for (uint32_t b = 0; b < pad; ++b) base[pos + 4 + cnt + b] = 0;
+            } else if (!is_word4(f)) {
+                const uint64_t e0 = ssrc[(size_t)d * kRecPerBlock + j];
+                const uint64_t nw = cnt * (f.xsz >> 2);
+                for (uint64_t i = 0; i < nw; ++i)
+                    *(uint32_t *)(base + pos + 4 + 4 * i) = dyn_word(f, e0, cnt, 4 + 4 * i);
+            }
+            pos += dyn_xdr_bytes(f, cnt);
+            ++d;
+        }
+    }
+
+    // ---- pass C: one flat sweep per byte / 4-byte-element column
+    uint32_t d = 0;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = sf[k];
+        if (f.kind != XDRG_K_DYNAMIC) continue;
+        const uint32_t dd = d++;
+        const bool bytes = f.xsz == 1;
+        if (!bytes && !is_word4(f)) continue;
+        const bool fl = f.type == XDRG_T_FLOAT;
+        const uint32_t esh = bytes ? 0 : 2;              // log2 native element size
+        const uint32_t cps = 4 - esh;                    // log2 elements per 16-B chunk
+        const uint64_t *key = ssrc + (size_t)dd * kRecPerBlock;
+        const uint32_t *cn = scnt + (size_t)dd * kRecPerBlock;
+        const uint32_t *ps = spst + (size_t)dd * kRecPerBlock;
+        const uint64_t S0 = key[0], S1 = key[nrec - 1] + cn[nrec - 1];   // elements
+        if (S1 <= S0) continue;
+        const uint64_t cbase = S0 >> cps, cend = (S1 + (1u << cps) - 1) >> cps;
+        const uint32_t lsh = lookup_shift(cend - cbase);
+        __syncthreads();   // previous column's table readers are done
+        build_tab(key, nrec, cbase, lsh, cps, S0, tab);
+        __syncthreads();
+        const uint8_t *col = f.data;
+        for (uint64_t c0 = cbase + threadIdx.x; c0 < cend; c0 += (uint64_t)kRecThreads * kFlatU) {
+            uint32_t w[kFlatU][4];
+            uint32_t jj[kFlatU];
+            bool full[kFlatU];
+#pragma unroll
+            for (int u = 0; u < kFlatU; ++u) {   // A: native loads + record lookup
+                const uint64_t c = c0 + (uint64_t)u * kRecThreads;
+                full[u] = false;
+                jj[u] = 0;
+                if (c >= cend) continue;
+                const uint64_t e = c << cps;
+                full[u] = e >= S0 && e + (1u << cps) <= S1;
+                const uint8_t *src = col + (c << 4);
+                if (full[u]) {
+                    const u32x4u v = *(const u32x4u *)src;
+                    w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
+                } else {   // edge chunk: only bytes of [S0, S1) are read
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) w[u][i] = 0;
+                    for (uint32_t b = 0; b < 16; ++b) {
+                        const uint64_t x = ((c << 4) + b) >> esh;
+                        if (x >= S0 && x < S1) w[u][b >> 2] |= (uint32_t)src[b] << (8 * (b & 3));
+                    }
+                }
+                jj[u] = tab_find(key, nrec, tab, cbase, lsh, c, e > S0 ? e : S0);
+            }
+#pragma unroll
+            for (int u = 0; u < kFlatU; ++u) {   // B: XDR stores
+                const uint64_t c = c0 + (uint64_t)u * kRecThreads;
+                if (c >= cend) break;
+                const uint64_t e = c << cps;
+                uint32_t j = jj[u];
+                if (full[u] && key[j] <= e && e + (1u << cps) <= key[j] + cn[j]) {
+                    uint8_t *dst = out + soff[j] + ps[j] + ((e - key[j]) << esh);
+                    if (bytes) {
+                        u32x4u o; o.x = w[u][0]; o.y = w[u][1]; o.z = w[u][2]; o.w = w[u][3];
+                        *(u32x4u *)dst = o;
+                    } else {
+                        u32x4a o;
+                        o.x = bswap32r(fl ? canon_f32r(w[u][0]) : w[u][0]);
+                        o.y = bswap32r(fl ? canon_f32r(w[u][1]) : w[u][1]);
+                        o.z = bswap32r(fl ? canon_f32r(w[u][2]) : w[u][2]);
+                        o.w = bswap32r(fl ? canon_f32r(w[u][3]) : w[u][3]);
+                        *(u32x4a *)dst = o;
+                    }
+                    continue;
+                }
+                // boundary chunk: element by element into each record's run
+                const uint64_t lo_c = e > S0 ? e : S0;
+                const uint64_t hi_c = e + (1u << cps) < S1 ? e + (1u << cps) : S1;
+                for (uint64_t x = lo_c; x < hi_c; ++x) {
+                    while (j + 1 < nrec && key[j] + cn[j] <= x) ++j;
+                    if (x < key[j] || x >= key[j] + cn[j]) continue;
+                    uint8_t *dst = out + soff[j] + ps[j] + ((x - key[j]) << esh);
+                    const uint32_t i = (uint32_t)(x - e);
+                    if (bytes) {
+                        *dst = (uint8_t)chunk_byte(w[u][0], w[u][1], w[u][2], w[u][3], i);
+                    } else {
+                        const uint32_t v = chunk_word(w[u][0], w[u][1], w[u][2], w[u][3], i);
+                        *(uint32_t *)dst = bswap32r(fl ? canon_f32r(v) : v);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// LDS: sstart[RPB + 2] u64 | snoff[ND][RPB] u64 | scnt[ND][RPB] u32 | spst[ND][RPB] u32 | supto[RPB] u32
+__host__ __device__ constexpr size_t dec_col_lds_bytes(uint32_t nd) {
+    return (size_t)(kRecPerBlock + 2) * 8 + (size_t)kRecPerBlock * 4 + (size_t)nd * kRecPerBlock * 16;
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_dec_col(const RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t ND = a.ndyn;
+    uint64_t *sstart = (uint64_t *)smem;
+    uint64_t *snoff = sstart + kRecPerBlock + 2;
+    uint32_t *scnt = (uint32_t *)(snoff + (size_t)ND * kRecPerBlock);
+    uint32_t *spst = scnt + (size_t)ND * kRecPerBlock;
+    uint32_t *supto = spst + (size_t)ND * kRecPerBlock;
+    __shared__ uint32_t tab[kLookup + 1];
+    __shared__ VField sf[kMaxFields];
+    stage_fields(a, sf);
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t t0 = threadIdx.x * kRecPerThread;
+    const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
+    const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
+    const uint64_t lim = bad < a.n ? bad : a.n;
+    const uint32_t nlive = (uint32_t)(lim > rb ? (lim - rb < kRecPerBlock ? lim - rb : kRecPerBlock) : 0);
+    for (uint32_t i = threadIdx.x; i < kRecPerBlock; i += kRecThreads) {
+        const bool live = i < nlive;
+        const uint64_t r = rb + i;
+        uint64_t pos = a.framed ? 4 : 0;
+        uint32_t d = 0;
+        for (uint32_t k = 0; k < a.nf; ++k) {
+            const VField &f = a.f[k];
+            if (f.kind != XDRG_K_DYNAMIC) { pos += f.xbytes; continue; }
+            const uint64_t c = live ? a.rec_cnt[(uint64_t)d * a.n + r] : 0u;
+            scnt[(size_t)d * kRecPerBlock + i] = (uint32_t)c;
+            spst[(size_t)d * kRecPerBlock + i] = (uint32_t)(pos + 4);
+            pos += dyn_xdr_bytes(f, c);
+            ++d;
+        }
+        supto[i] = live ? a.nf : 0u;
+        if (live) sstart[i] = rec_extent(a, r).a;
+    }
+    __syncthreads();
+    for (uint32_t d = 0; d < ND; ++d) {
+        const uint32_t k = a.dyn_idx[d];
+        const VField &f = a.f[k];
+        uint64_t pss = 0;
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) pss += scnt[(size_t)d * kRecPerBlock + t0 + j];
+        uint64_t btot;
+        uint64_t off = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x] + block_excl_scan(pss, &btot);
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            const uint64_t r = rb + t0 + j;
+            const uint64_t c = scnt[(size_t)d * kRecPerBlock + t0 + j];
+            snoff[(size_t)d * kRecPerBlock + t0 + j] = off;
+            if (r < a.n) {
+                f.offsets[r] = off;
+                if (r < bad && off + c > f.cap) {   // native column too small
+                    atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
+                    atomicMin(&supto[t0 + j], k);
+                }
+            }
+            off += c;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) f.offsets[a.n] = a.totals[d];
+    }
+    __syncthreads();
+    if (!nlive) return;
+    const uint8_t *in = a.xdr;
+
+    // ---- pass R: fixed fields and the rare 2/1/8-byte dynamic vectors
+    for (uint32_t j = threadIdx.x; j < nlive; j += kRecThreads) {
+        const uint64_t r = rb + j;
+        const uint8_t *base = in + sstart[j];
+        uint64_t pos = a.framed ? 4 : 0;
+        uint32_t d = 0;
+        const uint32_t upto = supto[j];
+        for (uint32_t k = 0; k < upto; ++k) {
+            const VField &f = sf[k];
+            if (f.kind != XDRG_K_DYNAMIC) {
+                const uint32_t nw = f.xbytes >> 2;
+                for (uint32_t i = 0; i < nw; ++i) fixed_store(f, r, 4 * i, *(const uint32_t *)(base + pos + 4 * i));
+                pos += f.xbytes;
+                continue;
+            }
+            const uint64_t cnt = scnt[(size_t)d * kRecPerBlock + j];
+            if (f.xsz != 1 && !is_word4(f)) {
+                const uint64_t no = snoff[(size_t)d * kRecPerBlock + j];
+                const uint64_t nw = cnt * (f.xsz >> 2);
+                for (uint64_t i = 0; i < nw; ++i)
+                    dyn_store(f, no, cnt, 4 + 4 * i, *(const uint32_t *)(base + pos + 4 + 4 * i));
+            }
+            pos += dyn_xdr_bytes(f, cnt);
+            ++d;
+        }
+    }
+
+    // ---- pass C: one flat sweep per byte / 4-byte-element native column
+    uint32_t d = 0;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = sf[k];
+        if (f.kind != XDRG_K_DYNAMIC) continue;
+        const uint32_t dd = d++;
+        const bool bytes = f.xsz == 1;
+        if (!bytes && !is_word4(f)) continue;
+        const uint32_t esh = bytes ? 0 : 2;
+        const uint32_t cps = 4 - esh;
+        const uint64_t *key = snoff + (size_t)dd * kRecPerBlock;
+        const uint32_t *cn = scnt + (size_t)dd * kRecPerBlock;
+        const uint32_t *ps = spst + (size_t)dd * kRecPerBlock;
+        const uint64_t N0 = key[0];
+        uint64_t N1 = key[nlive - 1] + cn[nlive - 1];
+        if (N1 > f.cap) N1 = f.cap;            // records past capacity are excluded below
+        if (N1 <= N0) continue;
+        const uint64_t cbase = N0 >> cps, cend = (N1 + (1u << cps) - 1) >> cps;
+        const uint32_t lsh = lookup_shift(cend - cbase);
+        __syncthreads();
+        build_tab(key, nlive, cbase, lsh, cps, N0, tab);
+        __syncthreads();
+        uint8_t *col = f.data;
+        for (uint64_t c0 = cbase + threadIdx.x; c0 < cend; c0 += (uint64_t)kRecThreads * kFlatU) {
+            uint32_t w[kFlatU][4];
+            uint32_t jj[kFlatU];
+            bool fast[kFlatU];
+#pragma unroll
+            for (int u = 0; u < kFlatU; ++u) {   // A: lookup + XDR loads
+                const uint64_t c = c0 + (uint64_t)u * kRecThreads;
+                fast[u] = false;
+                jj[u] = 0;
+                if (c >= cend) continue;
+                const uint64_t e = c << cps;
+                const uint32_t j = tab_find(key, nlive, tab, cbase, lsh, c, e > N0 ? e : N0);
+                jj[u] = j;
+                if (e >= N0 && e + (1u << cps) <= N1 && key[j] <= e && e + (1u << cps) <= key[j] + cn[j] &&
+                    k < supto[j]) {
+                    const uint8_t *src = in + sstart[j] + ps[j] + ((e - key[j]) << esh);
+                    if (bytes) {
+                        const u32x4u v = *(const u32x4u *)src;
+                        w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
+                    } else {
+                        const u32x4a v = *(const u32x4a *)src;
+                        w[u][0] = bswap32r(v.x); w[u][1] = bswap32r(v.y);
+                        w[u][2] = bswap32r(v.z); w[u][3] = bswap32r(v.w);
+                    }
+                    fast[u] = true;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kFlatU; ++u) {   // B: native stores
+                const uint64_t c = c0 + (uint64_t)u * kRecThreads;
+                if (c >= cend) break;
+                uint8_t *dst = col + (c << 4);
+                if (fast[u]) {
+                    u32x4u o; o.x = w[u][0]; o.y = w[u][1]; o.z = w[u][2]; o.w = w[u][3];
+                    *(u32x4u *)dst = o;
+                    continue;
+                }
+                const uint64_t e = c << cps;
+                uint32_t j = jj[u];
+                const uint64_t lo_c = e > N0 ? e : N0;
+                const uint64_t hi_c = e + (1u << cps) < N1 ? e + (1u << cps) : N1;
+                for (uint64_t x = lo_c; x < hi_c; ++x) {
+                    while (j + 1 < nlive && key[j] + cn[j] <= x) ++j;
+                    if (x < key[j] || x >= key[j] + cn[j] || k >= supto[j]) continue;
+                    const uint8_t *src = in + sstart[j] + ps[j] + ((x - key[j]) << esh);
+                    if (bytes) dst[x - e] = *src;
+                    else *(uint32_t *)(dst + ((x - e) << 2)) = bswap32r(*(const uint32_t *)src);
+                }
+            }
+        }
+    }
+}
+
+// ===========================================================================
+// Group-per-record place kernels (the default; field-major)
+//
+// Phase 1 as in the flat kernels (metadata in LDS).  Phase 2 walks the fields
+// in schema order; for each field every record of the block is handled by a
+// group of G lanes, G (1..64) chosen per field from that field's average size
+// in the block.  Opaque/string fields move as one blob [length][payload][zero
+// pad] in 16-byte chunks, kCopyU chunks per lane in flight, realigned with
+// v_alignbyte_b32 so every global access is dword-aligned.  Measured on
+// MI355X this beat the flat and column-major kernels on configs 3 and 4
+// (DESIGN.md §5.3).
+// ===========================================================================
+__device__ __forceinline__ uint32_t mask_bytes(uint32_t v, int64_t valid) {
+    if (valid >= 4) return v;
+    if (valid <= 0) return 0;
+    return v & ((1u << (8 * valid)) - 1u);
+}
+
+struct Chunk5 { uint32_t q0, q1, q2, q3, q4; };
+
+__device__ __forceinline__ uint32_t pow2_lanes(uint64_t bytes_per_rec, uint32_t bytes_per_lane) {
+    uint32_t g = 1;
+    while (g < 64 && (uint64_t)g * bytes_per_lane < bytes_per_rec) g <<= 1;
+    return g;
+}
+
+// One opaque/string field as one blob: [BE length][payload][zero pad] (Xdr.java:776-800).
+template <int kCopyU>
+__device__ __forceinline__ void enc_blob_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                               uint64_t cnt, uint32_t G, uint32_t gl) {
+    const uint64_t nwb = 1 + ((cnt + 3) >> 2), nch = (nwb + 3) >> 2;
+    const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
+    const uint8_t *sa = src - sh;
+    const uint8_t *end = src + cnt;
+    const uint32_t lenw = bswap32r((uint32_t)cnt);
+    for (uint64_t c0 = gl; c0 < nch; c0 += (uint64_t)G * kCopyU) {
+        Chunk5 ch[kCopyU];
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const uint64_t c = c0 + (uint64_t)u * G;
+            if (c >= nch) continue;
+            const uint8_t *p = sa + 16 * c;   // words at p - 4 + 4m, m = 0..4
+            if (c > 0 && p + 16 <= end) {
+                const u32x4a v = *(const u32x4a *)(p - 4);
+                ch[u].q0 = v.x; ch[u].q1 = v.y; ch[u].q2 = v.z; ch[u].q3 = v.w;
+                ch[u].q4 = sh ? *(const uint32_t *)(p + 12) : 0u;
+            } else {
+                ch[u].q0 = (c > 0 && p - 4 < end) ? *(const uint32_t *)(p - 4) : 0u;
+                ch[u].q1 = p < end ? *(const uint32_t *)p : 0u;
+                ch[u].q2 = p + 4 < end ? *(const uint32_t *)(p + 4) : 0u;
+                ch[u].q3 = p + 8 < end ? *(const uint32_t *)(p + 8) : 0u;
+                ch[u].q4 = (sh && p + 12 < end) ? *(const uint32_t *)(p + 12) : 0u;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const uint64_t c = c0 + (uint64_t)u * G;
+            if (c >= nch) break;
+            const Chunk5 &q = ch[u];
+            uint32_t o0 = sh ? __builtin_amdgcn_alignbyte(q.q1, q.q0, sh) : q.q0;
+            uint32_t o1 = sh ? __builtin_amdgcn_alignbyte(q.q2, q.q1, sh) : q.q1;
+            uint32_t o2 = sh ? __builtin_amdgcn_alignbyte(q.q3, q.q2, sh) : q.q2;
+            uint32_t o3 = sh ? __builtin_amdgcn_alignbyte(q.q4, q.q3, sh) : q.q3;
+            const int64_t rem = 4 + (int64_t)cnt - 16 * (int64_t)c;   // blob bytes from chunk start
+            if (rem < 16) {
+                o0 = mask_bytes(o0, rem); o1 = mask_bytes(o1, rem - 4);
+                o2 = mask_bytes(o2, rem - 8); o3 = mask_bytes(o3, rem - 12);
+            }
+            if (c == 0) o0 = lenw;
+            uint8_t *d = dst + 16 * c;
+            if (4 * c + 4 <= nwb) {
+                u32x4a o; o.x = o0; o.y = o1; o.z = o2; o.w = o3;
+                *(u32x4a *)d = o;
+            } else {
+                const uint64_t left = nwb - 4 * c;
+                *(uint32_t *)d = o0;
+                if (left > 1) *(uint32_t *)(d + 4) = o1;
+                if (left > 2) *(uint32_t *)(d + 8) = o2;
+            }
+        }
+    }
+}
+
+// int/uint/enum/float vector as one blob: [BE count][BE elements...].
+__device__ __forceinline__ void enc_blob_words4(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                                uint64_t cnt, bool fl, uint32_t G, uint32_t gl) {
+    const uint64_t nwb = 1 + cnt, nch = (nwb + 3) >> 2;
+    const uint32_t *p0 = (const uint32_t *)src;   // element e = blob word e + 1
+    for (uint64_t c = gl; c < nch; c += G) {
+        uint32_t w[4];
+        if (c > 0 && 4 * c + 4 <= nwb) {
+            const u32x4a v = *(const u32x4a *)(p0 + 4 * c - 1);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t b = 4 * c + j;   // blob word
+                w[j] = (b >= 1 && b < nwb) ? p0[b - 1] : 0u;
+            }
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = bswap32r(fl ? canon_f32r(w[j]) : w[j]);
+        if (c == 0) o[0] = bswap32r((uint32_t)cnt);
+        uint32_t *d = (uint32_t *)(dst + 16 * c);
+        if (4 * c + 4 <= nwb) {
+            u32x4a ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+            *(u32x4a *)d = ov;
+        } else {
+            for (uint64_t j = 0; 4 * c + j < nwb; ++j) d[j] = o[j];
+        }
+    }
+}
+
+// XDR payload (4-aligned src, cnt bytes) -> native bytes at any alignment.
+// Partial head/tail dwords are written byte by byte: their other bytes
+// belong to neighbouring records.
+template <int kCopyU>
+__device__ __forceinline__ void dec_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                          uint64_t cnt, uint32_t G, uint32_t gl) {
+    if (!cnt) return;
+    const uint32_t sh = (uint32_t)((uintptr_t)dst & 3);
+    uint8_t *da = dst - sh;
+    const uint64_t nd = (sh + cnt + 3) >> 2, nch = (nd + 3) >> 2, nsw = (cnt + 3) >> 2;
+    const uint32_t *q = (const uint32_t *)src;
+    for (uint64_t c0 = gl; c0 < nch; c0 += (uint64_t)G * kCopyU) {
+        Chunk5 ch[kCopyU];   // q0 = word before the chunk, q1..q4 = the chunk's source words
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const uint64_t i0 = 4 * (c0 + (uint64_t)u * G);
+            if (i0 >= 4 * nch) continue;
+            if (i0 + 4 <= nsw) {
+                const u32x4a v = *(const u32x4a *)(q + i0);
+                ch[u].q1 = v.x; ch[u].q2 = v.y; ch[u].q3 = v.z; ch[u].q4 = v.w;
+            } else {
+                ch[u].q1 = i0 < nsw ? q[i0] : 0u;
+                ch[u].q2 = i0 + 1 < nsw ? q[i0 + 1] : 0u;
+                ch[u].q3 = i0 + 2 < nsw ? q[i0 + 2] : 0u;
+                ch[u].q4 = i0 + 3 < nsw ? q[i0 + 3] : 0u;
+            }
+            ch[u].q0 = (sh && i0) ? q[i0 - 1] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kCopyU; ++u) {
+            const uint64_t c = c0 + (uint64_t)u * G;
+            if (c >= nch) break;
+            const uint64_t i0 = 4 * c;
+            const Chunk5 &w = ch[u];
+            uint32_t v[4];
+            if (sh) {
+                const uint32_t s = 4 - sh;
+                v[0] = __builtin_amdgcn_alignbyte(w.q1, w.q0, s); v[1] = __builtin_amdgcn_alignbyte(w.q2, w.q1, s);
+                v[2] = __builtin_amdgcn_alignbyte(w.q3, w.q2, s); v[3] = __builtin_amdgcn_alignbyte(w.q4, w.q3, s);
+            } else {
+                v[0] = w.q1; v[1] = w.q2; v[2] = w.q3; v[3] = w.q4;
+            }
+            uint8_t *d = da + 16 * c;
+            if ((i0 > 0 || sh == 0) && 4 * (i0 + 4) <= sh + cnt) {
+                u32x4a o; o.x = v[0]; o.y = v[1]; o.z = v[2]; o.w = v[3];
+                *(u32x4a *)d = o;
+                continue;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t i = i0 + j;
+                if (i >= nd) break;
+                const uint32_t lo = i == 0 ? sh : 0;
+                const uint64_t he = sh + cnt - 4 * i;
+                const uint32_t hi = he < 4 ? (uint32_t)he : 4u;
+                if (lo == 0 && hi == 4) *(uint32_t *)(d + 4 * j) = v[j];
+                else for (uint32_t b = lo; b < hi; ++b) d[4 * j + b] = (uint8_t)(v[j] >> (8 * b));
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void dec_words4(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                           uint64_t cnt, uint32_t G, uint32_t gl) {
+    const uint64_t nch = (cnt + 3) >> 2;
+    for (uint64_t c = gl; c < nch; c += G) {
+        const uint32_t *p = (const uint32_t *)(src + 16 * c);
+        uint32_t *d = (uint32_t *)(dst + 16 * c);
+        if (4 * c + 4 <= cnt) {
+            const u32x4a v = *(const u32x4a *)p;
+            u32x4a o; o.x = bswap32r(v.x); o.y = bswap32r(v.y); o.z = bswap32r(v.z); o.w = bswap32r(v.w);
+            *(u32x4a *)d = o;
+        } else {
+            for (uint64_t j = 0; 4 * c + j < cnt; ++j) d[j] = bswap32r(p[j]);
+        }
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(kRecThreads) void k_enc_place_g(const RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint64_t *soff = (uint64_t *)smem;
+    uint64_t *ssrc = soff + kRecPerBlock + 2;
+    uint32_t *scnt = (uint32_t *)(ssrc + (size_t)a.ndyn * kRecPerBlock);
+    const uint64_t total = a.totals[0];
+    if (total > a.xdr_cap) return;  // XDRG_E_CAPACITY: write nothing
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t t0 = threadIdx.x * kRecPerThread;
+    uint64_t sz[kRecPerThread];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        const uint64_t r = rb + t0 + j;
+        uint64_t size = 0;
+        if (r < a.n) {
+            size = a.fixed_xdr;
+            for (uint32_t d = 0; d < a.ndyn; ++d) {
+                const VField &f = a.f[a.dyn_idx[d]];
+                const uint64_t o0 = f.offsets[r], cnt = f.offsets[r + 1] - o0;
+                ssrc[(size_t)d * kRecPerBlock + t0 + j] = o0;
+                scnt[(size_t)d * kRecPerBlock + t0 + j] = (uint32_t)cnt;
+                size += dyn_xdr_bytes(f, cnt);
+            }
+        } else {
+            for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
+        }
+        sz[j] = size;
+        s += size;
+    }
+    uint64_t btot;
+    uint64_t off = a.block_sums[blockIdx.x] + block_excl_scan(s, &btot);
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        soff[t0 + j] = off;
+        if (a.rec_out && rb + t0 + j < a.n) a.rec_out[rb + t0 + j] = off;
+        off += sz[j];
+    }
+    if (threadIdx.x == kRecThreads - 1) soff[kRecPerBlock] = off;
+    if (a.rec_out && blockIdx.x == 0 && threadIdx.x == 0) a.rec_out[a.n] = total;
+    __syncthreads();
+    uint64_t nrec = a.n - rb;
+    if (nrec > kRecPerBlock) nrec = kRecPerBlock;
+    uint8_t *out = a.xdr;
+    const uint32_t tid = threadIdx.x;
+    if (a.framed) {   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
+        for (uint32_t j = tid; j < nrec; j += kRecThreads)
+            *(uint32_t *)(out + soff[j]) = bswap32r((uint32_t)(soff[j + 1] - soff[j] - 4) | kLastFrag);
+    }
+    uint64_t fixed_delta = a.framed ? 4 : 0;
+    uint32_t d = 0;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind != XDRG_K_DYNAMIC) {
+            const uint32_t nw = f.xbytes >> 2;
+            if (nw) {
+                const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
+                const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+                for (uint32_t j = tid / G; j < nrec; j += ng) {
+                    uint8_t *dst = out + soff[j] + fixed_delta;
+                    for (uint32_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
+                }
+            }
+            fixed_delta += f.xbytes;
+            continue;
+        }
+        const uint32_t *cn = scnt + (size_t)d * kRecPerBlock;
+        const uint64_t *sr = ssrc + (size_t)d * kRecPerBlock;
+        uint64_t ps = 0;
+        for (uint32_t j = tid; j < nrec; j += kRecThreads) ps += cn[j];
+        const uint64_t fbytes = block_sum(ps) * (f.xsz == 1 ? 1 : f.xsz) + 4 * nrec;
+        const uint32_t G = a.force_g ? a.force_g : pow2_lanes(nrec ? fbytes / nrec : 0, a.lane_bytes_enc);
+        const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+        for (uint32_t j = tid / G; j < nrec; j += ng) {
+            const uint64_t cnt = cn[j], e0 = sr[j];
+            uint8_t *dst = out + soff[j] + fixed_delta;
+            if (f.xsz == 1) {
+                enc_blob_bytes<U>(dst, f.data + e0, cnt, G, gl);
+            } else if (is_word4(f)) {
+                enc_blob_words4(dst, f.data + e0 * 4, cnt, f.type == XDRG_T_FLOAT, G, gl);
+            } else {
+                if (gl == 0) *(uint32_t *)dst = bswap32r((uint32_t)cnt);
+                const uint64_t nw = cnt * (f.xsz >> 2);
+                for (uint64_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 + 4 * i) = dyn_word(f, e0, cnt, 4 + 4 * i);
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = tid; j < nrec; j += kRecThreads) soff[j] += dyn_xdr_bytes(f, cn[j]);
+        __syncthreads();
+        ++d;
+    }
+}
+
+// LDS: sstart[RPB] u64 | snoff[ND][RPB] u64 | scnt[ND][RPB] u32 | supto[RPB] u32
+__host__ __device__ constexpr size_t dec_g_lds_bytes(uint32_t nd) {
+    return (size_t)kRecPerBlock * 12 + (size_t)nd * kRecPerBlock * 12;
+}
+
+template <int U>
+__global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint64_t *sstart = (uint64_t *)smem;
+    uint64_t *snoff = sstart + kRecPerBlock;
+    uint32_t *scnt = (uint32_t *)(snoff + (size_t)a.ndyn * kRecPerBlock);
+    uint32_t *supto = scnt + (size_t)a.ndyn * kRecPerBlock;
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t t0 = threadIdx.x * kRecPerThread;
+    const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
+    const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
+    for (uint32_t i = threadIdx.x; i < kRecPerBlock; i += kRecThreads) {
+        const uint64_t r = rb + i;
+        const bool live = r < a.n && r < bad;
+        for (uint32_t d = 0; d < a.ndyn; ++d)
+            scnt[(size_t)d * kRecPerBlock + i] = live ? a.rec_cnt[(uint64_t)d * a.n + r] : 0u;
+        supto[i] = live ? a.nf : 0u;
+        if (live) sstart[i] = rec_extent(a, r).a + (a.framed ? 4 : 0);
+    }
+    __syncthreads();
+    for (uint32_t d = 0; d < a.ndyn; ++d) {
+        const uint32_t k = a.dyn_idx[d];
+        const VField &f = a.f[k];
+        uint64_t s = 0;
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) s += scnt[(size_t)d * kRecPerBlock + t0 + j];
+        uint64_t btot;
+        uint64_t off = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x] + block_excl_scan(s, &btot);
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            const uint64_t r = rb + t0 + j;
+            const uint64_t c = scnt[(size_t)d * kRecPerBlock + t0 + j];
+            snoff[(size_t)d * kRecPerBlock + t0 + j] = off;
+            if (r < a.n) {
+                f.offsets[r] = off;
+                if (r < bad && off + c > f.cap) {   // native column too small
+                    atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
+                    atomicMin(&supto[t0 + j], k);
+                }
+            }
+            off += c;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) f.offsets[a.n] = a.totals[d];
+    }
+    __syncthreads();
+    uint64_t nrec = a.n > rb ? a.n - rb : 0;
+    if (nrec > kRecPerBlock) nrec = kRecPerBlock;
+    const uint8_t *in = a.xdr;
+    const uint32_t tid = threadIdx.x;
+    uint64_t fixed_delta = 0;
+    uint32_t d = 0;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind != XDRG_K_DYNAMIC) {
+            const uint32_t nw = f.xbytes >> 2;
+            if (nw) {
+                const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
+                const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+                for (uint32_t j = tid / G; j < nrec; j += ng) {
+                    if (k >= supto[j]) continue;
+                    const uint8_t *src = in + sstart[j] + fixed_delta;
+                    for (uint32_t i = gl; i < nw; i += G) fixed_store(f, rb + j, 4 * i, *(const uint32_t *)(src + 4 * i));
+                }
+            }
+            fixed_delta += f.xbytes;
+            continue;
+        }
+        const uint32_t *cn = scnt + (size_t)d * kRecPerBlock;
+        const uint64_t *no = snoff + (size_t)d * kRecPerBlock;
+        uint64_t ps = 0;
+        for (uint32_t j = tid; j < nrec; j += kRecThreads) ps += cn[j];
+        const uint64_t fbytes = block_sum(ps) * (f.xsz == 1 ? 1 : f.xsz) + 4 * nrec;
+        const uint32_t G = a.force_g ? a.force_g : pow2_lanes(nrec ? fbytes / nrec : 0, a.lane_bytes_dec);
+        const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+        for (uint32_t j = tid / G; j < nrec; j += ng) {
+            if (k >= supto[j]) continue;
+            const uint64_t cnt = cn[j];
+            const uint8_t *src = in + sstart[j] + fixed_delta + 4;
+            if (f.xsz == 1) {
+                dec_bytes<U>(f.data + no[j], src, cnt, G, gl);
+            } else if (is_word4(f)) {
+                dec_words4(f.data + no[j] * 4, src, cnt, G, gl);
+            } else {
+                const uint64_t nw = cnt * (f.xsz >> 2);
+                for (uint64_t i = gl; i < nw; i += G) dyn_store(f, no[j], cnt, 4 + 4 * i, *(const uint32_t *)(src + 4 * i));
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = tid; j < nrec; j += kRecThreads) sstart[j] += dyn_xdr_bytes(f, cn[j]);
+        __syncthreads();
+        ++d;
+    }
+}
+
+// ===========================================================================
 // Frame walk (RpcMessageParserTCP.isAllFragmentsArrived/assembleXdr :63-140)
 // ===========================================================================
 __device__ __forceinline__ uint32_t ld_be32_u(const uint8_t *p) {
@@ -1046,8 +1825,14 @@ __global__ void k_debug_recargs(const RecArgs a) {
 // copy unroll of the group kernels (tools/tune_rec.py; set_tuning keys 4 and 5)
 static int g_enc_u = 2, g_dec_u = 2;
 static uint32_t g_force_g = 0;
+static int g_rec_kernel = 0;   // 0 = group per record (default), 1 = flat, 2 = column-major
 static uint32_t g_lane_bytes_enc = 32, g_lane_bytes_dec = 32;
 int set_rec_tuning(int key, long long value) {
+    if (key == 9) {
+        if (value < 0 || value > 2) return -1;
+        g_rec_kernel = (int)value;
+        return 0;
+    }
     if (key == 7 || key == 8) {   // target payload bytes per lane when sizing groups
         if (value < 4 || value > 65536) return -1;
         (key == 7 ? g_lane_bytes_enc : g_lane_bytes_dec) = (uint32_t)value;
@@ -1081,7 +1866,12 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
         hipLaunchKernelGGL(k_scan_rows, dim3(1), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_ENC_PLACE:
-        if (grp) hipLaunchKernelGGL(k_enc_flat, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
+        if (grp) {
+            if (g_rec_kernel == 1) hipLaunchKernelGGL(k_enc_flat, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
+            else if (g_rec_kernel == 2) hipLaunchKernelGGL(k_enc_col, dim3(nb), dim3(kRecThreads), enc_col_lds_bytes(a.ndyn), st, a);
+            else if (g_enc_u == 1) hipLaunchKernelGGL(k_enc_place_g<1>, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
+            else hipLaunchKernelGGL(k_enc_place_g<2>, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
+        }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SIZES:
@@ -1094,7 +1884,12 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
             hipLaunchKernelGGL(k_scan_rows, dim3(a.ndyn), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_DEC_PLACE:
-        if (grp) hipLaunchKernelGGL(k_dec_flat, dim3(nb), dim3(kRecThreads), dec_lds_bytes(a.ndyn), st, a);
+        if (grp) {
+            if (g_rec_kernel == 1) hipLaunchKernelGGL(k_dec_flat, dim3(nb), dim3(kRecThreads), dec_lds_bytes(a.ndyn), st, a);
+            else if (g_rec_kernel == 2) hipLaunchKernelGGL(k_dec_col, dim3(nb), dim3(kRecThreads), dec_col_lds_bytes(a.ndyn), st, a);
+            else if (g_dec_u == 1) hipLaunchKernelGGL(k_dec_place_g<1>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+            else hipLaunchKernelGGL(k_dec_place_g<2>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+        }
         else hipLaunchKernelGGL(k_dec_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     default: return (int)hipErrorInvalidValue;

@@ -29,9 +29,11 @@ def main():
         torch.cuda.synchronize()
         wl.check()
         res = {}
-        variants = [(u, lb) for u in (1, 2) for lb in (16, 32, 64, 128, 256, 512)]
+        # (kernel, unroll, lane bytes): kernel 0 = group, 1 = flat, 2 = column-major
+        variants = [(0, u, lb) for u in (1, 2) for lb in (16, 32, 64)] + [(1, 1, 32), (2, 1, 32)]
         for r in range(rounds):
-            for u, g in variants:
+            for kern, u, g in variants:
+                L.xdrg_internal_tune(9, kern)
                 L.xdrg_internal_tune(4, u)
                 L.xdrg_internal_tune(5, u)
                 L.xdrg_internal_tune(7, g)
@@ -42,8 +44,9 @@ def main():
                 for kid, name in ((abi.KERNEL_VAR_SIZE, "sizes"), (abi.KERNEL_VAR_SCAN, "scan"),
                                   (abi.KERNEL_VAR_ENCODE, "enc_place"), (abi.KERNEL_VAR_DECODE, "dec_place")):
                     c, ms = ctx.kernel_stats(kid)
-                    res.setdefault((u, g, name), []).append(ms)
-        L.xdrg_internal_tune(4, 2)   # defaults (kernels_rec.hip)
+                    res.setdefault((kern, u, g, name), []).append(ms)
+        L.xdrg_internal_tune(9, 0)   # defaults (kernels_rec.hip)
+        L.xdrg_internal_tune(4, 2)
         L.xdrg_internal_tune(5, 2)
         L.xdrg_internal_tune(7, 32)
         L.xdrg_internal_tune(8, 32)
@@ -51,9 +54,10 @@ def main():
         torch.cuda.synchronize()
         wl.check()
         per_launch = wl.native_bytes + wl.xlen
-        for (u, g, name), t in sorted(res.items()):
+        for (kern, u, g, name), t in sorted(res.items()):
             med = statistics.median(t)
-            d = {"config": cfg, "unroll": u, "lane_bytes": g, "kernel": name, "median_ms": round(med, 4)}
+            d = {"config": cfg, "impl": ["group", "flat", "column"][kern], "unroll": u, "lane_bytes": g,
+                 "kernel": name, "median_ms": round(med, 4)}
             if name.endswith("place"):
                 d["GBps"] = round(per_launch / med / 1e6, 1)
             print(json.dumps(d), flush=True)
