@@ -211,7 +211,7 @@ class Workload:
             self.xlen = n * rec
             self.native_bytes = n * 32
             self.rec_offsets = None
-            self.kernels = ("k_wordmap_encode" if framed else "k_stream_bswap",
+            self.kernels = ("k_stream_framed_enc/dec" if framed else "k_stream_bswap",
                             abi.KERNEL_FIXED_ENCODE, abi.KERNEL_FIXED_DECODE)
             self.desc = ("configs[1]: 64 Mi fixed-schema records of 8 x int32 (32 B), encode+decode "
                          "round trip, array-of-structs native records" if not framed else

@@ -124,6 +124,140 @@ __global__ __launch_bounds__(256) void k_stream_ops(const StreamArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Record-marked streaming kernels (AoS-dense records of 4-byte words: int,
+// uint, enum, float, 4-multiple opaque).  XDR record = mark + W words, native
+// record = W words.  One lane per 16-byte chunk of the destination: it reads
+// the (at most 5) source words its chunk needs with one 4-byte-aligned
+// 16-byte load plus one dword, inserts or skips the record mark, and writes
+// one aligned 16-byte vector.  Decode checks every mark (the lane whose
+// chunk holds a record's first native word checks that record's mark).
+// ---------------------------------------------------------------------------
+typedef uint32_t u32x4w __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ uint32_t pick5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t i) {
+    return i == 0 ? a : i == 1 ? b : i == 2 ? c : i == 3 ? d : e;
+}
+__device__ __forceinline__ uint32_t word_op(uint8_t op, uint32_t x) {
+    return op == OP_FLOAT ? bswap32(canon_f32(x)) : op == OP_OPAQUE ? x : bswap32(x);
+}
+// q = x / d, r = x % d for x < 2^52 (double reciprocal + one correction)
+__device__ __forceinline__ void divmod(uint64_t x, uint32_t d, double inv, uint64_t &q, uint32_t &r) {
+    q = (uint64_t)((double)x * inv);
+    int64_t rr = (int64_t)(x - q * d);
+    if (rr < 0) { --q; rr += d; }
+    else if (rr >= (int64_t)d) { ++q; rr -= d; }
+    r = (uint32_t)rr;
+}
+
+__global__ __launch_bounds__(256) void k_stream_framed_enc(const StreamArgs a, uint64_t n, uint32_t mark_le,
+                                                           double inv_wt) {
+    __shared__ uint8_t sops[kMaxWords];
+    for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
+    __syncthreads();
+    const uint32_t W = a.w, Wt = a.w + 1;
+    const uint64_t total = n * Wt;                 // output words
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t g0 = c * 4;
+    if (g0 >= total) return;
+    uint64_t r0; uint32_t w0;
+    divmod(g0, Wt, inv_wt, r0, w0);
+    const uint64_t nin = n * W;                    // input words
+    const uint64_t i0 = r0 * W + (w0 ? w0 - 1 : 0);
+    const uint32_t *src = (const uint32_t *)a.src;
+    uint32_t x0, x1, x2, x3, x4 = 0;
+    if (i0 + 5 <= nin) {
+        const u32x4w v = __builtin_nontemporal_load((const u32x4w *)(src + i0));
+        x0 = v.x; x1 = v.y; x2 = v.z; x3 = v.w;
+    } else {
+        x0 = i0 < nin ? src[i0] : 0u; x1 = i0 + 1 < nin ? src[i0 + 1] : 0u;
+        x2 = i0 + 2 < nin ? src[i0 + 2] : 0u; x3 = i0 + 3 < nin ? src[i0 + 3] : 0u;
+    }
+    (void)x4;
+    uint32_t o[4];
+    uint32_t k = 0, w = w0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (w == 0) {
+            o[j] = mark_le;
+        } else {
+            o[j] = word_op(sops[w - 1], pick5(x0, x1, x2, x3, x4, k));
+            ++k;
+        }
+        if (++w == Wt) w = 0;
+    }
+    u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+    uint8_t *dst = a.dst + g0 * 4;
+    if (g0 + 4 <= total) {
+        __builtin_nontemporal_store(ov, (u32x4 *)dst);
+    } else {
+        for (uint64_t j = 0; g0 + j < total; ++j) ((uint32_t *)dst)[j] = o[j];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_stream_framed_dec(const StreamArgs a, uint64_t n, uint32_t mark_le,
+                                                           double inv_w, unsigned long long *errkey) {
+    __shared__ uint8_t sops[kMaxWords];
+    for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
+    __syncthreads();
+    const uint32_t W = a.w, Wt = a.w + 1;
+    const uint64_t total = n * W;                  // native words
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t n0 = c * 4;
+    if (n0 >= total) return;
+    uint64_t r0; uint32_t w0;
+    divmod(n0, W, inv_w, r0, w0);
+    const uint64_t x0i = r0 * Wt + 1 + w0;          // XDR word of native word n0
+    const uint64_t nx = n * Wt;
+    const uint32_t *src = (const uint32_t *)a.src;
+    uint32_t y0, y1, y2, y3, y4;
+    if (x0i + 5 <= nx) {
+        const u32x4w v = __builtin_nontemporal_load((const u32x4w *)(src + x0i));
+        y0 = v.x; y1 = v.y; y2 = v.z; y3 = v.w;
+        y4 = src[x0i + 4];
+    } else {
+        y0 = x0i < nx ? src[x0i] : 0u; y1 = x0i + 1 < nx ? src[x0i + 1] : 0u;
+        y2 = x0i + 2 < nx ? src[x0i + 2] : 0u; y3 = x0i + 3 < nx ? src[x0i + 3] : 0u;
+        y4 = x0i + 4 < nx ? src[x0i + 4] : 0u;
+    }
+    uint32_t o[4];
+    uint32_t k = 0, w = w0;
+    uint64_t r = r0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (n0 + j >= total) { o[j] = 0; continue; }
+        if (w == 0) {   // first word of record r: check its mark (the word before)
+            const uint32_t m = k == 0 ? src[x0i - 1] : pick5(y0, y1, y2, y3, y4, k - 1);
+            if (m != mark_le) atomicMin(errkey, err_key(r, 0, XDRG_E_FRAME));
+        }
+        o[j] = word_op(sops[w], pick5(y0, y1, y2, y3, y4, k));
+        ++k;
+        if (++w == W) { w = 0; ++r; ++k; }   // skip the next record's mark
+    }
+    u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+    uint8_t *dst = a.dst + n0 * 4;
+    if (n0 + 4 <= total) {
+        __builtin_nontemporal_store(ov, (u32x4 *)dst);
+    } else {
+        for (uint64_t j = 0; n0 + j < total; ++j) ((uint32_t *)dst)[j] = o[j];
+    }
+}
+
+int launch_stream_framed(const StreamArgs &a, uint64_t n, uint32_t mark_le, bool decode,
+                         unsigned long long *errkey, void *stream) {
+    if (!n || !a.w) return hipSuccess;
+    hipStream_t st = (hipStream_t)stream;
+    const uint64_t words = decode ? n * a.w : n * (a.w + 1);
+    const uint64_t blocks = (((words + 3) >> 2) + 255) / 256;
+    if (decode)
+        hipLaunchKernelGGL(k_stream_framed_dec, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
+                           1.0 / (double)a.w, errkey);
+    else
+        hipLaunchKernelGGL(k_stream_framed_enc, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
+                           1.0 / (double)(a.w + 1));
+    return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Word-map kernels (any fixed layout).
 // ---------------------------------------------------------------------------
 struct WordMapShared {

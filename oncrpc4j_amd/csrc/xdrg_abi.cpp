@@ -360,6 +360,29 @@ static bool stream_eligible(const xdrg_schema *s, const xdrg_column *cols, uint6
     return true;
 }
 
+// Framed streaming path: as stream_eligible (layout) but only single-word
+// ops (no hyper/double pairs) and any word count; the XDR side may be only
+// 4-byte aligned.
+static bool framed_stream_eligible(const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
+                                   const void *xdr, const uint8_t **base_out) {
+    if (s->has_dyn || !s->stream_types || s->ops.empty() || !s->nwords) return false;
+    const int64_t rec = (int64_t)s->nwords * 4;
+    const uint8_t *base = nullptr;
+    for (size_t k = 0; k < s->f.size(); ++k) {
+        if (!s->xbytes[k]) continue;
+        const uint8_t *b = (const uint8_t *)cols[k].data - 4 * (uint64_t)s->wpos[k];
+        if (!base) base = b;
+        if (b != base) return false;
+        if (eff_stride(s, k, cols[k]) != rec) return false;
+    }
+    if (!base || !aligned(base, 16) || !aligned(xdr, 16)) return false;
+    for (const WordOp &o : s->ops)
+        if (o.op != OP_BSWAP && o.op != OP_FLOAT && o.op != OP_OPAQUE) return false;
+    (void)n;
+    *base_out = base;
+    return true;
+}
+
 static void fill_stream_ops(const xdrg_schema *s, bool decode, StreamArgs &a) {
     a.all_bswap = 1;
     for (size_t w = 0; w < s->ops.size(); ++w) {
@@ -465,6 +488,16 @@ extern "C" int xdrg_encode_batch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_c
             fill_stream_ops(s, false, a);
             TimedLaunch t(c, XDRG_KERNEL_FIXED_ENCODE);
             HIPCHK(c, (hipError_t)launch_stream_words(a, 0, c->stream));
+        } else if (n && framed && framed_stream_eligible(s, cols, n, out, &base)) {
+            StreamArgs a;
+            memset(&a, 0, sizeof a);
+            a.src = base;
+            a.dst = out;
+            a.w = s->nwords;
+            fill_stream_ops(s, false, a);
+            TimedLaunch t(c, XDRG_KERNEL_FIXED_ENCODE);
+            HIPCHK(c, (hipError_t)launch_stream_framed(a, n, __builtin_bswap32((uint32_t)(s->fixed_size | kLastFrag)),
+                                                       false, nullptr, c->stream));
         } else if (n && s->nwords + (framed ? 1 : 0) <= (uint32_t)kMaxWords && !s->ops.empty() &&
                    s->f.size() <= (size_t)kMaxCols) {
             WordMapArgs a;
@@ -599,6 +632,18 @@ extern "C" int xdrg_decode_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8_
             fill_stream_ops(s, true, a);
             TimedLaunch t(c, XDRG_KERNEL_FIXED_DECODE);
             HIPCHK(c, (hipError_t)launch_stream_words(a, 0, c->stream));
+        } else if (n && framed && in_len >= total && framed_stream_eligible(s, cols, n, in, &base)) {
+            StreamArgs a;
+            memset(&a, 0, sizeof a);
+            a.src = in;
+            a.dst = (uint8_t *)base;
+            a.w = s->nwords;
+            fill_stream_ops(s, true, a);
+            dev_key = true;
+            HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
+            TimedLaunch t(c, XDRG_KERNEL_FIXED_DECODE);
+            HIPCHK(c, (hipError_t)launch_stream_framed(a, n, __builtin_bswap32((uint32_t)(s->fixed_size | kLastFrag)),
+                                                       true, c->d_stat, c->stream));
         } else if (n && stride && s->nwords + (framed ? 1 : 0) <= (uint32_t)kMaxWords &&
                    !s->ops.empty() && s->f.size() <= (size_t)kMaxCols) {
             WordMapArgs a;

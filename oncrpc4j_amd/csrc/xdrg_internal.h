@@ -141,6 +141,9 @@ constexpr unsigned long long kNoError = ~0ull;
 int launch_stream_words(const StreamArgs &a, int variant, void *stream);
 int set_tuning(int key, long long value);      // kernel knobs (tools/tune_*.py)
 int set_rec_tuning(int key, long long value);
+// record-marked AoS-dense stream (words: BSWAP / FLOAT / OPAQUE only)
+int launch_stream_framed(const StreamArgs &a, uint64_t n, uint32_t mark_le, bool decode,
+                         unsigned long long *errkey, void *stream);
 int launch_wordmap_encode(const WordMapArgs &a, bool aligned16, void *stream);
 int launch_wordmap_decode(const WordMapArgs &a, bool aligned16, void *stream);
 enum RecPhase { REC_ENC_SIZES, REC_ENC_SCAN, REC_ENC_PLACE, REC_DEC_SIZES, REC_DEC_SCAN, REC_DEC_PLACE };

@@ -135,15 +135,17 @@ def test_random_parity(gpu_ctx, name, n, framed):
         assert g2[:3] == (0, n, 0) and g2[3].equal(o[3])
 
 
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("n", [4099, 4100])
-@pytest.mark.parametrize("name", ["cfg2_8xint", "words_mixed", "odd_words"])
-def test_aos_layout(gpu_ctx, name, n):
+@pytest.mark.parametrize("name", ["cfg2_8xint", "words_mixed", "odd_words", "float_words"])
+def test_aos_layout(gpu_ctx, name, n, framed):
     """Array-of-structs native records (one struct per record, fields at their
-    XDR word positions): the streaming path when n*words is a multiple of 4,
-    the word-map path over strided columns otherwise."""
-    fields = SCHEMAS[name]
+    XDR word positions): the streaming paths (raw: n*words a multiple of 4;
+    record-marked: single-word types) and the word-map path otherwise."""
+    fields = SCHEMAS.get(name, [(F, SC, 0), (I, SC, 0), (O, FX, 4)] * 2)
     hb = random_batch(fields, n, seed=7)
-    rc, want, _ = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total() + 8)
+    total = hb.xdr_total(framed)
+    rc, want, _ = oracle.encode_batch(fields, hb.columns(), n, total + 8, framed=framed)
     assert rc == 0
     offs = xdr_word_offsets(fields)
     rec = hb.xdr_total() // n
@@ -155,18 +157,27 @@ def test_aos_layout(gpu_ctx, name, n):
     dev = torch.from_numpy(aos).cuda()
     sch = engine.Schema(fields)
     cols = aos_columns(fields, dev.data_ptr(), rec, offs)
-    out = torch.zeros(n * rec, dtype=torch.uint8, device="cuda")
-    assert gpu_ctx.encode(sch, cols, n, out, n * rec) == n * rec
-    assert out.cpu().numpy().tobytes() == want
+    out = torch.zeros(total + 16, dtype=torch.uint8, device="cuda")
+    assert gpu_ctx.encode(sch, cols, n, out, total, framed=framed) == total
+    assert out[:total].cpu().numpy().tobytes() == want
+    assert not out[total:].any()
     back = torch.zeros_like(dev)
     cols2 = aos_columns(fields, back.data_ptr(), rec, offs)
-    gpu_ctx.decode(sch, out, n * rec, n, cols2)
-    o = oracle_decode(fields, want, n, None, {})[3]
+    gpu_ctx.decode(sch, out, total, n, cols2, framed=framed)
+    o = oracle_decode(fields, want, n, None, {}, framed)[3]
     ob = np.zeros((n, rec), dtype=np.uint8)
     for k, a in enumerate(o.arrays):
         raw = np.ascontiguousarray(a).view(np.uint8).reshape(n, -1)
         ob[:, offs[k]:offs[k] + raw.shape[1]] = raw
     assert np.array_equal(back.cpu().numpy(), ob)
+    if framed:   # a corrupted mark: same first bad record and code as the oracle
+        bad = bytearray(want)
+        r = n // 3
+        bad[r * (rec + 4) + 3] ^= 0x10
+        tb = torch.from_numpy(np.frombuffer(bytes(bad), dtype=np.uint8).copy()).cuda()
+        rc, fb, err = gpu_ctx.decode(sch, tb, total, n, cols2, framed=True, raise_on_error=False)
+        oo = oracle_decode(fields, bytes(bad), n, None, {}, True)
+        assert (rc, fb, err) == oo[:3] == (abi.E_FRAME, r, abi.E_FRAME)
 
 
 # ---- error parity ------------------------------------------------------------------
