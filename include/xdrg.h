@@ -106,6 +106,13 @@ typedef struct xdrg_column {
     uint64_t  cap;
 } xdrg_column;
 
+/* Encode only: a SCALAR / FIXED column whose records all read the element
+ * run at `data` — a constant field such as the msg_type, reply_stat,
+ * verifier and accept_stat words every accepted reply carries
+ * (rpc/RpcCall.java:328-332) or a call's rpcvers/prog/vers
+ * (RpcCall.java:462-467).  Decode rejects it with XDRG_E_INVAL.            */
+#define XDRG_STRIDE_CONST INT64_MIN
+
 /* ---- flags --------------------------------------------------------------- */
 /* Prepend one RFC 1831 record mark per record: BE(len | 0x80000000), one
  * last fragment per message (GrizzlyRpcTransport.java:103-110,

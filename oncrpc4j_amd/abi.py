@@ -35,6 +35,7 @@ K_SCALAR, K_FIXED, K_DYNAMIC = 0, 1, 2
 # flags
 FRAME_RM = 0x1
 ASYNC = 0x2
+STRIDE_CONST = -(1 << 63)   # XDRG_STRIDE_CONST: every record reads element run 0 (encode only)
 CTX_TIMING = 0x1
 
 # kernel ids for xdrg_ctx_kernel_stats

@@ -1758,6 +1758,254 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
 }
 
 // ===========================================================================
+// Lane-per-record kernels (small records).  The group kernels above give a
+// record a group of lanes per field and so keep only one or two 16-byte
+// loads per lane in flight; here every lane owns whole records and issues up
+// to kLaneU unaligned 16-byte loads of a payload before its stores, the
+// pattern that measured 4.4-5.5 TB/s for 128-192 B records on MI355X
+// (tools/probes/pattern_bw.hip, B vs D).  Records are taken strided
+// (thread t: block records t, t + 256, ...), so neighbouring lanes write
+// neighbouring records.  The prologue (block scan, LDS layout) is the group
+// kernels'.
+// ===========================================================================
+constexpr int kLaneU = 4;   // 16-byte chunks per lane in flight
+
+// [BE count][payload][zero pad] from bytes at any alignment to a 4-aligned dst.
+__device__ __forceinline__ void lane_enc_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                               uint32_t cnt) {
+    *(uint32_t *)dst = bswap32r(cnt);
+    dst += 4;
+    const uint32_t nfull = cnt >> 4;
+    for (uint32_t c = 0; c < nfull; c += kLaneU) {
+        u32x4u v[kLaneU];
+#pragma unroll
+        for (int u = 0; u < kLaneU; ++u)
+            if (c + u < nfull) v[u] = *(const u32x4u *)(src + 16 * (c + u));
+#pragma unroll
+        for (int u = 0; u < kLaneU; ++u)
+            if (c + u < nfull) *(u32x4u *)(dst + 16 * (c + u)) = v[u];
+    }
+    const uint32_t rem = cnt & 15, o = 16 * nfull;
+    for (uint32_t i = 0; 4 * i < rem; ++i) {
+        const uint32_t k = rem - 4 * i;
+        *(uint32_t *)(dst + o + 4 * i) = load_bytes(src + o + 4 * i, k < 4 ? k : 4u);   // zero pad (Xdr.java:765-781)
+    }
+}
+
+// [BE count][BE elements] from a 4-aligned native int/uint/enum/float run.
+__device__ __forceinline__ void lane_enc_words(uint8_t *__restrict__ dst, const uint32_t *__restrict__ src,
+                                               uint32_t cnt, bool fl) {
+    *(uint32_t *)dst = bswap32r(cnt);
+    dst += 4;
+    const uint32_t nfull = cnt >> 2;
+    for (uint32_t c = 0; c < nfull; c += kLaneU) {
+        u32x4a v[kLaneU];
+#pragma unroll
+        for (int u = 0; u < kLaneU; ++u)
+            if (c + u < nfull) v[u] = *(const u32x4a *)(src + 4 * (c + u));
+#pragma unroll
+        for (int u = 0; u < kLaneU; ++u) {
+            if (c + u >= nfull) continue;
+            u32x4a o;
+            o.x = bswap32r(fl ? canon_f32r(v[u].x) : v[u].x); o.y = bswap32r(fl ? canon_f32r(v[u].y) : v[u].y);
+            o.z = bswap32r(fl ? canon_f32r(v[u].z) : v[u].z); o.w = bswap32r(fl ? canon_f32r(v[u].w) : v[u].w);
+            *(u32x4u *)(dst + 16 * (c + u)) = o;
+        }
+    }
+    for (uint32_t i = 4 * nfull; i < cnt; ++i) {
+        const uint32_t w = src[i];
+        *(uint32_t *)(dst + 4 * i) = bswap32r(fl ? canon_f32r(w) : w);
+    }
+}
+
+// XDR payload (4-aligned) -> native bytes at any alignment; exactly cnt
+// bytes are written (the next record's bytes follow in the column).
+__device__ __forceinline__ void lane_dec_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                               uint32_t cnt) {
+    const uint32_t nfull = cnt >> 4;
+    for (uint32_t c = 0; c < nfull; c += kLaneU) {
+        u32x4a v[kLaneU];
+#pragma unroll
+        for (int u = 0; u < kLaneU; ++u)
+            if (c + u < nfull) v[u] = *(const u32x4a *)(src + 16 * (c + u));
+#pragma unroll
+        for (int u = 0; u < kLaneU; ++u)
+            if (c + u < nfull) *(u32x4u *)(dst + 16 * (c + u)) = v[u];
+    }
+    const uint32_t rem = cnt & 15, o = 16 * nfull;
+    for (uint32_t i = 0; 4 * i < rem; ++i) {
+        const uint32_t w = *(const uint32_t *)(src + o + 4 * i), k = rem - 4 * i;
+        if (k >= 4) *(u32u *)(dst + o + 4 * i) = w;
+        else for (uint32_t b = 0; b < k; ++b) dst[o + 4 * i + b] = (uint8_t)(w >> (8 * b));
+    }
+}
+
+__device__ __forceinline__ void lane_dec_words(uint32_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                               uint32_t cnt) {
+    const uint32_t nfull = cnt >> 2;
+    for (uint32_t c = 0; c < nfull; c += kLaneU) {
+        u32x4a v[kLaneU];
+#pragma unroll
+        for (int u = 0; u < kLaneU; ++u)
+            if (c + u < nfull) v[u] = *(const u32x4a *)(src + 16 * (c + u));
+#pragma unroll
+        for (int u = 0; u < kLaneU; ++u) {
+            if (c + u >= nfull) continue;
+            u32x4a o;
+            o.x = bswap32r(v[u].x); o.y = bswap32r(v[u].y); o.z = bswap32r(v[u].z); o.w = bswap32r(v[u].w);
+            *(u32x4a *)(dst + 4 * (c + u)) = o;
+        }
+    }
+    for (uint32_t i = 4 * nfull; i < cnt; ++i) dst[i] = bswap32r(*(const uint32_t *)(src + 4 * i));
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_enc_lane(const RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint64_t *soff = (uint64_t *)smem;
+    uint64_t *ssrc = soff + kRecPerBlock + 2;
+    uint32_t *scnt = (uint32_t *)(ssrc + (size_t)a.ndyn * kRecPerBlock);
+    const uint64_t total = a.totals[0];
+    if (total > a.xdr_cap) return;  // XDRG_E_CAPACITY: write nothing
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t t0 = threadIdx.x * kRecPerThread;
+    uint64_t sz[kRecPerThread];
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        const uint64_t r = rb + t0 + j;
+        uint64_t size = 0;
+        if (r < a.n) {
+            size = a.fixed_xdr;
+            for (uint32_t d = 0; d < a.ndyn; ++d) {
+                const VField &f = a.f[a.dyn_idx[d]];
+                const uint64_t o0 = f.offsets[r], cnt = f.offsets[r + 1] - o0;
+                ssrc[(size_t)d * kRecPerBlock + t0 + j] = o0;
+                scnt[(size_t)d * kRecPerBlock + t0 + j] = (uint32_t)cnt;
+                size += dyn_xdr_bytes(f, cnt);
+            }
+        }
+        sz[j] = size;
+        s += size;
+    }
+    uint64_t btot;
+    uint64_t off = a.block_sums[blockIdx.x] + block_excl_scan(s, &btot);
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        soff[t0 + j] = off;
+        if (a.rec_out && rb + t0 + j < a.n) a.rec_out[rb + t0 + j] = off;
+        off += sz[j];
+    }
+    if (threadIdx.x == kRecThreads - 1) soff[kRecPerBlock] = off;
+    if (a.rec_out && blockIdx.x == 0 && threadIdx.x == 0) a.rec_out[a.n] = total;
+    __syncthreads();
+    const uint64_t nrec = a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock;
+    for (uint32_t j = threadIdx.x; j < nrec; j += kRecThreads) {
+        const uint64_t r = rb + j;
+        uint8_t *dst = a.xdr + soff[j];
+        if (a.framed) {   // GrizzlyRpcTransport.java:103-110
+            *(uint32_t *)dst = bswap32r((uint32_t)(soff[j + 1] - soff[j] - 4) | kLastFrag);
+            dst += 4;
+        }
+        uint32_t d = 0;
+        for (uint32_t k = 0; k < a.nf; ++k) {
+            const VField &f = a.f[k];
+            if (f.kind != XDRG_K_DYNAMIC) {
+                const uint32_t nw = f.xbytes >> 2;
+                for (uint32_t i = 0; i < nw; ++i) *(uint32_t *)(dst + 4 * i) = fixed_word(f, r, 4 * i);
+                dst += f.xbytes;
+                continue;
+            }
+            const uint32_t cnt = scnt[(size_t)d * kRecPerBlock + j];
+            const uint64_t e0 = ssrc[(size_t)d * kRecPerBlock + j];
+            if (f.xsz == 1) {
+                lane_enc_bytes(dst, f.data + e0, cnt);
+            } else if (is_word4(f)) {
+                lane_enc_words(dst, (const uint32_t *)(f.data + e0 * 4), cnt, f.type == XDRG_T_FLOAT);
+            } else {
+                *(uint32_t *)dst = bswap32r(cnt);
+                const uint64_t nw = (uint64_t)cnt * (f.xsz >> 2);
+                for (uint64_t i = 0; i < nw; ++i) *(uint32_t *)(dst + 4 + 4 * i) = dyn_word(f, e0, cnt, 4 + 4 * i);
+            }
+            dst += dyn_xdr_bytes(f, cnt);
+            ++d;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint64_t *sstart = (uint64_t *)smem;
+    uint64_t *snoff = sstart + kRecPerBlock;
+    uint32_t *scnt = (uint32_t *)(snoff + (size_t)a.ndyn * kRecPerBlock);
+    uint32_t *supto = scnt + (size_t)a.ndyn * kRecPerBlock;
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t t0 = threadIdx.x * kRecPerThread;
+    const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
+    const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
+    for (uint32_t i = threadIdx.x; i < kRecPerBlock; i += kRecThreads) {
+        const uint64_t r = rb + i;
+        const bool live = r < a.n && r < bad;
+        for (uint32_t d = 0; d < a.ndyn; ++d)
+            scnt[(size_t)d * kRecPerBlock + i] = live ? a.rec_cnt[(uint64_t)d * a.n + r] : 0u;
+        supto[i] = live ? a.nf : 0u;
+        if (live) sstart[i] = rec_extent(a, r).a + (a.framed ? 4 : 0);
+    }
+    __syncthreads();
+    for (uint32_t d = 0; d < a.ndyn; ++d) {
+        const uint32_t k = a.dyn_idx[d];
+        const VField &f = a.f[k];
+        uint64_t s = 0;
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) s += scnt[(size_t)d * kRecPerBlock + t0 + j];
+        uint64_t btot;
+        uint64_t off = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x] + block_excl_scan(s, &btot);
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            const uint64_t r = rb + t0 + j;
+            const uint64_t c = scnt[(size_t)d * kRecPerBlock + t0 + j];
+            snoff[(size_t)d * kRecPerBlock + t0 + j] = off;
+            if (r < a.n) {
+                f.offsets[r] = off;
+                if (r < bad && off + c > f.cap) {   // native column too small
+                    atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
+                    atomicMin(&supto[t0 + j], k);
+                }
+            }
+            off += c;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) f.offsets[a.n] = a.totals[d];
+    }
+    __syncthreads();
+    const uint64_t nrec = a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0;
+    for (uint32_t j = threadIdx.x; j < nrec; j += kRecThreads) {
+        const uint32_t upto = supto[j];
+        if (!upto) continue;
+        const uint64_t r = rb + j;
+        const uint8_t *src = a.xdr + sstart[j];
+        uint32_t d = 0;
+        for (uint32_t k = 0; k < upto; ++k) {
+            const VField &f = a.f[k];
+            if (f.kind != XDRG_K_DYNAMIC) {
+                const uint32_t nw = f.xbytes >> 2;
+                for (uint32_t i = 0; i < nw; ++i) fixed_store(f, r, 4 * i, *(const uint32_t *)(src + 4 * i));
+                src += f.xbytes;
+                continue;
+            }
+            const uint32_t cnt = scnt[(size_t)d * kRecPerBlock + j];
+            const uint64_t no = snoff[(size_t)d * kRecPerBlock + j];
+            if (f.xsz == 1) lane_dec_bytes(f.data + no, src + 4, cnt);
+            else if (is_word4(f)) lane_dec_words((uint32_t *)(f.data + no * 4), src + 4, cnt);
+            else {
+                const uint64_t nw = (uint64_t)cnt * (f.xsz >> 2);
+                for (uint64_t i = 0; i < nw; ++i) dyn_store(f, no, cnt, 4 + 4 * i, *(const uint32_t *)(src + 4 + 4 * i));
+            }
+            src += dyn_xdr_bytes(f, cnt);
+            ++d;
+        }
+    }
+}
+
+// ===========================================================================
 // Frame walk (RpcMessageParserTCP.isAllFragmentsArrived/assembleXdr :63-140)
 // ===========================================================================
 __device__ __forceinline__ uint32_t ld_be32_u(const uint8_t *p) {
@@ -1825,11 +2073,11 @@ __global__ void k_debug_recargs(const RecArgs a) {
 // copy unroll of the group kernels (tools/tune_rec.py; set_tuning keys 4 and 5)
 static int g_enc_u = 2, g_dec_u = 2;
 static uint32_t g_force_g = 0;
-static int g_rec_kernel = 0;   // 0 = group per record (default), 1 = flat, 2 = column-major
+static int g_rec_kernel = 0;   // 0 = group per record (default), 1 = flat, 2 = column-major, 3 = lane per record
 static uint32_t g_lane_bytes_enc = 32, g_lane_bytes_dec = 32;
 int set_rec_tuning(int key, long long value) {
     if (key == 9) {
-        if (value < 0 || value > 2) return -1;
+        if (value < 0 || value > 3) return -1;
         g_rec_kernel = (int)value;
         return 0;
     }
@@ -1866,7 +2114,9 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
         hipLaunchKernelGGL(k_scan_rows, dim3(1), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_ENC_PLACE:
-        if (grp) {
+        if (grp && g_rec_kernel == 3) {
+            hipLaunchKernelGGL(k_enc_lane, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
+        } else if (grp) {
             if (g_rec_kernel == 1) hipLaunchKernelGGL(k_enc_flat, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
             else if (g_rec_kernel == 2) hipLaunchKernelGGL(k_enc_col, dim3(nb), dim3(kRecThreads), enc_col_lds_bytes(a.ndyn), st, a);
             else if (g_enc_u == 1) hipLaunchKernelGGL(k_enc_place_g<1>, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
@@ -1884,7 +2134,9 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
             hipLaunchKernelGGL(k_scan_rows, dim3(a.ndyn), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_DEC_PLACE:
-        if (grp) {
+        if (grp && g_rec_kernel == 3) {
+            hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+        } else if (grp) {
             if (g_rec_kernel == 1) hipLaunchKernelGGL(k_dec_flat, dim3(nb), dim3(kRecThreads), dec_lds_bytes(a.ndyn), st, a);
             else if (g_rec_kernel == 2) hipLaunchKernelGGL(k_dec_col, dim3(nb), dim3(kRecThreads), dec_col_lds_bytes(a.ndyn), st, a);
             else if (g_dec_u == 1) hipLaunchKernelGGL(k_dec_place_g<1>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);

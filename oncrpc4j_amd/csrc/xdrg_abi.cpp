@@ -311,6 +311,7 @@ static int ensure_ws(xdrg_ctx *c, size_t words) {
 static inline bool aligned(const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; }
 
 static int64_t eff_stride(const xdrg_schema *s, size_t k, const xdrg_column &col) {
+    if (col.stride == XDRG_STRIDE_CONST) return 0;   // every record reads element run 0
     if (col.stride) return col.stride;
     const uint64_t cnt = s->f[k].kind == XDRG_K_FIXED ? s->f[k].count : 1;
     return (int64_t)(s->nsz[k] * cnt);
@@ -328,6 +329,7 @@ static int check_columns(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *c
             if (n && !cols[k].data && !decode) { /* all-empty columns may have no data */ }
             if (!aligned(cols[k].data, al)) return inval(c, "dynamic column data misaligned");
         } else {
+            if (decode && cols[k].stride == XDRG_STRIDE_CONST) return inval(c, "constant column on decode");
             const int64_t st = eff_stride(s, k, cols[k]);
             if (s->xbytes[k] && n && !cols[k].data) return inval(c, "fixed column data is NULL");
             if (!aligned(cols[k].data, al) || (st % (int64_t)al)) return inval(c, "fixed column misaligned");

@@ -19,6 +19,10 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 _LIB = None
 
+# record-path implementation the library starts with (kernels_rec.hip
+# g_rec_kernel: 0 = group per record, 3 = lane per record)
+DEFAULT_REC_KERNEL = 0
+
 
 def lib():
     """Load libxdrgpu.so (raises if it has not been built)."""

@@ -379,10 +379,13 @@ static int field_valid(const xdrg_field *f) {
     if (f->kind == XDRG_K_FIXED && f->count > 0x7fffffffu) return 0;
     return 1;
 }
-static inline const uint8_t *fixed_ptr(const xdrg_field *f, const xdrg_column *c, uint64_t i) {
+static inline int64_t col_stride(const xdrg_field *f, const xdrg_column *c) {
     size_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
-    int64_t stride = c->stride ? c->stride : (int64_t)(native_size(f->type) * cnt);
-    return (const uint8_t *)c->data + (int64_t)i * stride;
+    if (c->stride == XDRG_STRIDE_CONST) return 0;   /* constant field (encode only) */
+    return c->stride ? c->stride : (int64_t)(native_size(f->type) * cnt);
+}
+static inline const uint8_t *fixed_ptr(const xdrg_field *f, const xdrg_column *c, uint64_t i) {
+    return (const uint8_t *)c->data + (int64_t)i * col_stride(f, c);
 }
 
 /* One record's fields, in declaration order, through the stream encoders —
@@ -558,6 +561,8 @@ int xo_decode_batch(const xdrg_field *fs, size_t nf, const uint8_t *in, uint64_t
     const uint64_t fixed = schema_fixed_size(fs, nf);
     if (!rec_offsets && !fixed) return XDRG_E_INVAL;
     for (size_t k = 0; k < nf; k++)
+        if (fs[k].kind != XDRG_K_DYNAMIC && cols[k].stride == XDRG_STRIDE_CONST) return XDRG_E_INVAL;
+    for (size_t k = 0; k < nf; k++)
         if (fs[k].kind == XDRG_K_DYNAMIC && n) cols[k].offsets[0] = 0;
     const uint64_t stride = fixed + (framed ? 4 : 0);
     for (uint64_t i = 0; i < n; i++) {
@@ -606,9 +611,7 @@ static void *enc_worker(void *arg) {
     xdrg_column sub[64];
     for (size_t k = 0; k < j->nf; k++) {
         sub[k] = j->cols[k];
-        size_t cnt = j->fs[k].kind == XDRG_K_FIXED ? j->fs[k].count : 1;
-        int64_t st = sub[k].stride ? sub[k].stride : (int64_t)(native_size(j->fs[k].type) * cnt);
-        sub[k].data = (uint8_t *)sub[k].data + (int64_t)j->lo * st;
+        sub[k].data = (uint8_t *)sub[k].data + (int64_t)j->lo * col_stride(&j->fs[k], &sub[k]);
     }
     uint64_t len;
     j->rc = xo_encode_batch(j->fs, j->nf, sub, j->hi - j->lo, j->buf + j->lo * j->stride,
@@ -620,9 +623,7 @@ static void *dec_worker(void *arg) {
     xdrg_column sub[64];
     for (size_t k = 0; k < j->nf; k++) {
         sub[k] = j->ocols[k];
-        size_t cnt = j->fs[k].kind == XDRG_K_FIXED ? j->fs[k].count : 1;
-        int64_t st = sub[k].stride ? sub[k].stride : (int64_t)(native_size(j->fs[k].type) * cnt);
-        sub[k].data = (uint8_t *)sub[k].data + (int64_t)j->lo * st;
+        sub[k].data = (uint8_t *)sub[k].data + (int64_t)j->lo * col_stride(&j->fs[k], &sub[k]);
     }
     uint64_t start = j->lo * j->stride;
     uint64_t avail = j->in_len > start ? j->in_len - start : 0;

@@ -16,6 +16,9 @@ fixtures are plain JSON data and travel, this script's inputs do not need to.
 3. framing.json — RFC 1831 record-marked streams built like
    ctest/rpc/RpcMessageParserTCPTest.java:94-181 (CALL header + AUTH_NONE +
    string args, re-fragmented into 1 KiB fragments).
+4. rpc_vectors.json — record-marked accepted replies (RpcCall.acceptedReply)
+   and AUTH_UNIX calls (RpcCall.callInternal + RpcAuthTypeUnix) packed by
+   xdrlib in the reference's field order (oncrpc4j_amd/rpc.py batches them).
 """
 import json
 import os
@@ -257,9 +260,96 @@ def framing():
             "cases": cases}
 
 
+# ---- RPC messages ---------------------------------------------------------------
+def mark(payload):
+    return struct.pack(">I", len(payload) | 0x80000000) + payload
+
+
+def accepted_reply(xid, stat, body):
+    """RpcCall.acceptedReply (rpc/RpcCall.java:328-333) with the AUTH_NONE
+    verifier (RpcAuthTypeNone.java:35, RpcAuthVerifier.java:58-61)."""
+    p = xdrlib.Packer()
+    p.pack_int(xid)
+    p.pack_int(1)            # RpcMessageType.REPLY
+    p.pack_int(0)            # RpcReplyStatus.MSG_ACCEPTED
+    p.pack_int(0)            # verifier flavour AUTH_NONE
+    p.pack_opaque(b"")       # verifier body
+    p.pack_int(stat)         # RpcAccepsStatus
+    return p.get_buffer() + body
+
+
+def unix_call(xid, rpcvers, prog, vers, proc, stamp, machine, uid, gid, gids, args):
+    """RpcCall.callInternal (RpcCall.java:462-470) with an AUTH_UNIX credential
+    (RpcAuthTypeUnix.java:123-131) and the AUTH_NONE verifier."""
+    body = xdrlib.Packer()
+    body.pack_int(stamp)
+    body.pack_string(machine)
+    body.pack_int(uid)
+    body.pack_int(gid)
+    body.pack_array(gids, body.pack_int)
+    p = xdrlib.Packer()
+    for v in (xid, 0, rpcvers, prog, vers, proc):
+        p.pack_int(v)
+    p.pack_int(1)                    # AUTH_UNIX
+    p.pack_opaque(body.get_buffer())  # == _len + the fields: the body is 4-aligned
+    p.pack_int(0)
+    p.pack_opaque(b"")
+    return p.get_buffer() + args
+
+
+def rpc_vectors(seed=0x5EED):
+    rng = random.Random(seed)
+    T = (T_INT, K_SCALAR, 0)
+    S = (T_STRING, K_DYNAMIC, 0)
+    replies = []
+    for name, body_fields, mk in (
+            ("NULL procedure replies (no body)", [], lambda: []),
+            ("PMAPPROC_GETPORT replies (int port)", [T], lambda: [rng.randrange(-2**31, 2**31)]),
+            ("RPCBPROC_GETADDR replies (universal address string)", [S],
+             lambda: [bytes(rng.choice(b"0123456789.") for _ in range(rng.randrange(0, 24))).hex()])):
+        xids = [0x12345678, 1, 0x7fffffff, -1, 0] + [rng.randrange(-2**31, 2**31) for _ in range(11)]
+        bodies = [mk() for _ in xids]
+        stream, offs = b"", [0]
+        for x, b in zip(xids, bodies):
+            p = xdrlib.Packer()
+            for (t, k, c), v in zip(body_fields, b):
+                if t == T_STRING:
+                    p.pack_string(bytes.fromhex(v))
+                else:
+                    p.pack_int(v)
+            stream += mark(accepted_reply(x, 0, p.get_buffer()))
+            offs.append(len(stream))
+        replies.append({"name": name, "cite": "rpc/RpcCall.java:323-343, grizzly/GrizzlyRpcTransport.java:103-110",
+                        "body_fields": [list(f) for f in body_fields], "xids": xids, "bodies": bodies,
+                        "stream": stream.hex(), "rec_offsets": offs})
+    calls, stream, offs = [], b"", [0]
+    for i in range(24):
+        rec = {"xid": rng.randrange(-2**31, 2**31), "rpcvers": 3 if i in (5, 17) else 2,
+               "prog": 100003, "vers": 4, "proc": 1, "stamp": rng.randrange(0, 2**31),
+               "machine": bytes(rng.choice(b"abcdefghij-.") for _ in range(rng.randrange(0, 20))).hex(),
+               "uid": rng.randrange(0, 70000), "gid": rng.randrange(0, 70000),
+               "gids": [rng.randrange(0, 70000) for _ in range(rng.randrange(0, 17))],
+               "arg_int": rng.randrange(-2**31, 2**31),
+               "arg_str": bytes(rng.choice(b"xyz/") for _ in range(rng.randrange(0, 40))).hex()}
+        a = xdrlib.Packer()
+        a.pack_int(rec["arg_int"])
+        a.pack_string(bytes.fromhex(rec["arg_str"]))
+        m = unix_call(rec["xid"], rec["rpcvers"], rec["prog"], rec["vers"], rec["proc"], rec["stamp"],
+                      bytes.fromhex(rec["machine"]), rec["uid"], rec["gid"], rec["gids"], a.get_buffer())
+        stream += mark(m)
+        offs.append(len(stream))
+        calls.append(rec)
+    return {"source": "xdrlib-built RPC messages following the reference's encode order",
+            "replies": replies,
+            "calls": {"name": "AUTH_UNIX calls, args (int, string); rpcvers 3 at records 5 and 17",
+                      "cite": "rpc/RpcCall.java:206-216,462-470, rpc/RpcAuthTypeUnix.java:71-79,123-131",
+                      "records": calls, "stream": stream.hex(), "rec_offsets": offs}}
+
+
 def main():
     for name, obj in (("kat_reference.json", kat_reference()), ("kat_jdk_nan.json", kat_jdk_nan()),
-                      ("xdrlib_vectors.json", xdrlib_vectors()), ("framing.json", framing())):
+                      ("xdrlib_vectors.json", xdrlib_vectors()), ("framing.json", framing()),
+                      ("rpc_vectors.json", rpc_vectors())):
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1)
             f.write("\n")

@@ -38,6 +38,22 @@ SCHEMAS = {
 }
 
 
+# Record-path implementations (kernels_rec.hip launch_rec_phase): 0 = group
+# per record, 3 = lane per record.  Tests taking `rec_kernel` run under each.
+REC_KERNELS = {"group": 0, "lane": 3}
+
+
+@pytest.fixture(params=sorted(REC_KERNELS), ids=str)
+def rec_kernel(request):
+    import ctypes
+    L = engine.lib()
+    L.xdrg_internal_tune.argtypes = [ctypes.c_int, ctypes.c_longlong]
+    L.xdrg_internal_tune.restype = ctypes.c_int
+    assert L.xdrg_internal_tune(9, REC_KERNELS[request.param]) == 0
+    yield request.param
+    L.xdrg_internal_tune(9, engine.DEFAULT_REC_KERNEL)
+
+
 # ---- helpers ----------------------------------------------------------------
 def gpu_encode(ctx, fields, hb, framed=False, cap_slack=0):
     sch = engine.Schema(fields)
@@ -74,7 +90,7 @@ def oracle_decode(fields, xdr, n, rec_offsets, caps, framed=False):
 # ---- golden fixtures ------------------------------------------------------------
 @pytest.mark.parametrize("b", gold.load("xdrlib_vectors.json")["batches"],
                          ids=lambda b: f'{b["name"]}-{"rm" if b["framed"] else "raw"}')
-def test_golden_xdrlib(gpu_ctx, b):
+def test_golden_xdrlib(gpu_ctx, rec_kernel, b):
     fields = [tuple(f) for f in b["fields"]]
     hb = gold.batch_from_records(fields, b["records"])
     xdr, offs = gpu_encode(gpu_ctx, fields, hb, b["framed"])
@@ -116,7 +132,7 @@ def test_jdk_nan(gpu_ctx):
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("n", [1, 7, 2049, 20000])
 @pytest.mark.parametrize("name", sorted(SCHEMAS))
-def test_random_parity(gpu_ctx, name, n, framed):
+def test_random_parity(gpu_ctx, rec_kernel, name, n, framed):
     fields = SCHEMAS[name]
     hb = random_batch(fields, n, seed=zlib.crc32(f"{name}/{n}/{framed}".encode()), dyn_len=(0, 40))
     rc, want, want_offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total(framed) + 8,
@@ -212,7 +228,7 @@ def _corrupt_cases(fields, hb, xdr, offs, framed):
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("name", ["cfg2_8xint", "cfg4_int_string_intvec", "cfg3_6xint_opaque",
                                   "cfg1_int_int_string"])
-def test_error_parity(gpu_ctx, name, framed):
+def test_error_parity(gpu_ctx, rec_kernel, name, framed):
     fields = SCHEMAS[name]
     n = 3000
     hb = random_batch(fields, n, seed=11, dyn_len=(0, 20))
@@ -230,7 +246,7 @@ def test_error_parity(gpu_ctx, name, framed):
             assert g2[:3] == o2[:3], desc
 
 
-def test_decode_capacity(gpu_ctx):
+def test_decode_capacity(gpu_ctx, rec_kernel):
     fields = SCHEMAS["cfg4_int_string_intvec"]
     hb = random_batch(fields, 500, seed=3, dyn_len=(1, 20))
     rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), 500, hb.xdr_total())
@@ -243,7 +259,7 @@ def test_decode_capacity(gpu_ctx):
     assert g[:3] == o[:3]
 
 
-def test_encode_capacity(gpu_ctx):
+def test_encode_capacity(gpu_ctx, rec_kernel):
     for name in ("cfg2_8xint", "cfg4_int_string_intvec"):
         fields = SCHEMAS[name]
         hb = random_batch(fields, 100, seed=5, dyn_len=(1, 9))
@@ -254,6 +270,34 @@ def test_encode_capacity(gpu_ctx):
         with pytest.raises(engine.CapacityError):
             gpu_ctx.encode(sch, db.columns(), 100, out, total - 4)
         assert not out.any(), "nothing may be written on XDRG_E_CAPACITY"
+
+
+@pytest.mark.parametrize("junk", [1, 3, 4, 8], ids=lambda j: f"junk{j}")
+@pytest.mark.parametrize("name", ["cfg4_int_string_intvec", "dyn_vectors", "fixed_arrays"])
+def test_decode_extents_with_unread_bytes(gpu_ctx, rec_kernel, name, junk):
+    """Record extents longer than the record: the reference decodes each
+    message from its own Xdr and leaves the rest unread
+    (RpcMessageParserTCP.java:109-140).  junk % 4 != 0 puts the records off
+    one dword grid (segment kernel: per-record path)."""
+    fields = SCHEMAS[name]
+    n = 1500
+    hb = random_batch(fields, n, seed=junk, dyn_len=(0, 33))
+    rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total())
+    rng = np.random.default_rng(junk)
+    parts, ro, pos = [], [0], 0
+    for r in range(n):
+        rec = xdr[int(offs[r]):int(offs[r + 1])]
+        extra = int(rng.integers(0, junk + 1)) if junk % 4 else junk
+        parts.append(rec + bytes(rng.integers(0, 256, extra, dtype=np.uint8)))
+        pos += len(rec) + extra
+        ro.append(pos)
+    stream = b"".join(parts)
+    caps = hb.dyn_caps()
+    o = oracle_decode(fields, stream, n, ro, caps)
+    g = gpu_decode(gpu_ctx, fields, stream, n, ro, caps)
+    assert o[:3] == (0, n, 0)
+    assert g[:3] == o[:3]
+    assert g[3].equal(o[3])
 
 
 def test_empty_batch(gpu_ctx):
