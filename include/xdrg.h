@@ -206,6 +206,36 @@ int  xdrg_decode_batch(xdrg_ctx *ctx, const xdrg_schema *schema,
 int  xdrg_frame_scan(xdrg_ctx *ctx, const uint8_t *in, uint64_t len,
                      uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs);
 
+/* ---- multi-GPU, one process ---------------------------
+ * For a caller that drives several devices from one process (a JVM with one
+ * context per GPU).  Records are independent (xdr/XdrAble.java:40,49), so a
+ * batch shards into consecutive record ranges, context i owning counts[i]
+ * records in context order (first_i = counts[0] + ... + counts[i-1]).  At
+ * most 8 contexts; contexts may share a device.  Both calls synchronise.
+ *
+ * Encode: context i encodes its shard from its own device columns cols[i]
+ * straight into out[i] (device of context i, out_cap bytes) at the shard's
+ * stream offset, then every context pulls its peers' shards out of their
+ * HBM over xGMI (peer access is enabled on first use).  On return every
+ * out[i] holds the whole stream — byte-identical to one context encoding
+ * all records — and rec_offsets[i] (nullable; n_total + 1 entries) its
+ * record offsets.  *out_len (host) = stream bytes.
+ *
+ * Decode: context i decodes records [first_i, first_i + counts[i]) of the
+ * stream in[i] resident on its device (in_len bytes; rec_offsets[i] = the
+ * stream's n_total + 1 record offsets, or NULL for fixed-size schemas) into
+ * its shard's columns cols[i].  *first_bad / *err (host) = the reference's
+ * first error over the whole batch: the smallest failing record.          */
+int  xdrg_encode_batch_multi(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *schema,
+                             const xdrg_column *const *cols, const uint64_t *counts,
+                             uint8_t *const *out, uint64_t out_cap, uint64_t *const *rec_offsets,
+                             uint32_t flags, uint64_t *out_len);
+int  xdrg_decode_batch_multi(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *schema,
+                             const uint8_t *const *in, uint64_t in_len,
+                             const uint64_t *const *rec_offsets, const uint64_t *counts,
+                             xdrg_column *const *cols, uint32_t flags,
+                             uint64_t *first_bad, int *err);
+
 #ifdef __cplusplus
 }
 #endif

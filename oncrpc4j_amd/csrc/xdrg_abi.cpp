@@ -714,3 +714,185 @@ extern "C" int xdrg_frame_scan(xdrg_ctx *c, const uint8_t *in, uint64_t len, uin
     *n_msgs = c->h_stat[1];
     return *n_msgs ? XDRG_OK : XDRG_E_INCOMPLETE;
 }
+
+// ---------------------------------------------------------------------------
+// multi-GPU, one process
+// ---------------------------------------------------------------------------
+// Peer access from `dev` to `peer`, enabled once per pair.
+static int enable_peer(xdrg_ctx *c, int dev, int peer) {
+    if (dev == peer) return XDRG_OK;
+    int can = 0;
+    HIPCHK(c, hipDeviceCanAccessPeer(&can, dev, peer));
+    if (!can) {
+        c->err = "device pair has no peer access";
+        return XDRG_E_HIP;
+    }
+    HIPCHK(c, hipSetDevice(dev));
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return hip_fail(c, e, "hipDeviceEnablePeerAccess");
+    (void)hipGetLastError();   // clear a sticky "already enabled"
+    return XDRG_OK;
+}
+
+static int multi_args(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *s, const uint64_t *counts,
+                      uint32_t flags) {
+    if (!ctxs || !s || !counts || nctx == 0 || nctx > (uint32_t)kMaxGatherSeg / 2) return XDRG_E_INVAL;
+    for (uint32_t i = 0; i < nctx; ++i)
+        if (!ctxs[i]) return XDRG_E_INVAL;
+    if (flags & ~XDRG_FRAME_RM) return inval(ctxs[0], "multi-GPU calls are synchronous (no XDRG_ASYNC)");
+    return XDRG_OK;
+}
+
+// XDR bytes of one shard: closed form for fixed-size schemas, else the size
+// and scan passes on the context's stream (result in c->h_stat[2] after a sync).
+static int shard_size_launch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
+                             bool framed, uint64_t *size, bool *on_device) {
+    *on_device = false;
+    if (!s->has_dyn || n == 0) {
+        *size = s->has_dyn ? 0 : n * (s->fixed_size + (framed ? 4 : 0));
+        return XDRG_OK;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    RecArgs a;
+    int rc = fill_rec(c, s, (xdrg_column *)cols, n, framed, a);
+    if (rc) return rc;
+    for (int ph = REC_ENC_SIZES; ph <= REC_ENC_SCAN; ++ph) HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, a.totals, 8, hipMemcpyDeviceToHost, c->stream));
+    *on_device = true;
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_encode_batch_multi(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *s,
+                                       const xdrg_column *const *cols, const uint64_t *counts,
+                                       uint8_t *const *out, uint64_t out_cap, uint64_t *const *rec_offsets,
+                                       uint32_t flags, uint64_t *out_len) {
+    int rc = multi_args(ctxs, nctx, s, counts, flags);
+    if (rc) return rc;
+    if (!cols || !out) return inval(ctxs[0], "columns / outputs are NULL");
+    const bool framed = flags & XDRG_FRAME_RM;
+    // 1. shard sizes (all devices in flight, then one sync each)
+    std::vector<uint64_t> size(nctx), base(nctx + 1, 0), first(nctx + 1, 0);
+    std::vector<char> dev(nctx);
+    for (uint32_t i = 0; i < nctx; ++i) {
+        rc = check_columns(ctxs[i], s, cols[i], counts[i], false);
+        if (rc) return rc;
+        bool d = false;
+        rc = shard_size_launch(ctxs[i], s, cols[i], counts[i], framed, &size[i], &d);
+        if (rc) return rc;
+        dev[i] = d;
+    }
+    for (uint32_t i = 0; i < nctx; ++i) {
+        if (dev[i]) {
+            HIPCHK(ctxs[i], hipSetDevice(ctxs[i]->device));
+            HIPCHK(ctxs[i], hipStreamSynchronize(ctxs[i]->stream));
+            size[i] = ctxs[i]->h_stat[2];
+        }
+        base[i + 1] = base[i] + size[i];
+        first[i + 1] = first[i] + counts[i];
+    }
+    const uint64_t total = base[nctx];
+    if (out_len) *out_len = total;
+    if (total > out_cap) {
+        ctxs[0]->err = "output buffer too small";
+        return XDRG_E_CAPACITY;
+    }
+    // 2. every context encodes its shard in place, at the shard's stream offset
+    for (uint32_t i = 0; i < nctx; ++i) {
+        xdrg_ctx *c = ctxs[i];
+        uint64_t *ro = rec_offsets && rec_offsets[i] ? rec_offsets[i] + first[i] : nullptr;
+        rc = xdrg_encode_batch(c, s, cols[i], counts[i], out[i] + base[i], out_cap - base[i], ro,
+                               (framed ? XDRG_FRAME_RM : 0) | XDRG_ASYNC, nullptr);
+        if (rc) return rc;
+        if (ro) {
+            if (counts[i] == 0) HIPCHK(c, (hipError_t)launch_store_u64(ro, 0, c->stream));
+            HIPCHK(c, (hipError_t)launch_add_u64(ro, counts[i] + 1, base[i], c->stream));
+        }
+    }
+    for (uint32_t i = 0; i < nctx; ++i) {
+        HIPCHK(ctxs[i], hipSetDevice(ctxs[i]->device));
+        HIPCHK(ctxs[i], hipStreamSynchronize(ctxs[i]->stream));
+    }
+    if (nctx == 1) return XDRG_OK;
+    // 3. full-mesh all-gather: context i pulls every peer's shard (and offsets)
+    for (uint32_t i = 0; i < nctx; ++i) {
+        xdrg_ctx *c = ctxs[i];
+        GatherArgs g;
+        memset(&g, 0, sizeof g);
+        for (uint32_t j = 0; j < nctx; ++j) {
+            if (j == i) continue;
+            if (out[j] != out[i] && size[j]) {
+                rc = enable_peer(c, c->device, ctxs[j]->device);
+                if (rc) return rc;
+                g.src[g.nseg] = out[j] + base[j];
+                g.dst[g.nseg] = out[i] + base[j];
+                g.bytes[g.nseg++] = size[j];
+            }
+            if (rec_offsets && rec_offsets[i] && rec_offsets[j] && rec_offsets[j] != rec_offsets[i]) {
+                rc = enable_peer(c, c->device, ctxs[j]->device);
+                if (rc) return rc;
+                g.src[g.nseg] = (const uint8_t *)(rec_offsets[j] + first[j]);
+                g.dst[g.nseg] = (uint8_t *)(rec_offsets[i] + first[j]);
+                g.bytes[g.nseg++] = (counts[j] + 1) * 8;
+            }
+        }
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, (hipError_t)launch_gather(g, c->stream));
+    }
+    for (uint32_t i = 0; i < nctx; ++i) {
+        HIPCHK(ctxs[i], hipSetDevice(ctxs[i]->device));
+        HIPCHK(ctxs[i], hipStreamSynchronize(ctxs[i]->stream));
+    }
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_decode_batch_multi(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *s,
+                                       const uint8_t *const *in, uint64_t in_len,
+                                       const uint64_t *const *rec_offsets, const uint64_t *counts,
+                                       xdrg_column *const *cols, uint32_t flags, uint64_t *first_bad, int *err) {
+    int rc = multi_args(ctxs, nctx, s, counts, flags);
+    if (rc) return rc;
+    if (!cols || !in) return inval(ctxs[0], "columns / inputs are NULL");
+    const bool framed = flags & XDRG_FRAME_RM;
+    const uint64_t stride = s->fixed_size + (framed ? 4 : 0);
+    uint64_t first = 0, n_total = 0;
+    for (uint32_t i = 0; i < nctx; ++i) n_total += counts[i];
+    // every shard in flight; results land in each context's pinned status block
+    for (uint32_t i = 0; i < nctx; ++i) {
+        xdrg_ctx *c = ctxs[i];
+        const uint64_t *ro = rec_offsets ? rec_offsets[i] : nullptr;
+        const uint8_t *src = in[i];
+        uint64_t len = in_len;
+        if (ro) {
+            ro += first;
+        } else {   // fixed stride: the shard starts at record `first`
+            const uint64_t skip = first * stride;
+            src += skip < in_len ? skip : in_len;
+            len = in_len > skip ? in_len - skip : 0;
+        }
+        rc = xdrg_decode_batch(c, s, src, len, ro, counts[i], cols[i],
+                               (framed ? XDRG_FRAME_RM : 0) | XDRG_ASYNC,
+                               (uint64_t *)(c->d_stat + 4), (int *)(c->d_stat + 5));
+        if (rc) return rc;
+        HIPCHK(c, hipMemcpyAsync(c->h_stat + 4, c->d_stat + 4, 16, hipMemcpyDeviceToHost, c->stream));
+        first += counts[i];
+    }
+    uint64_t fb = n_total;
+    int code = XDRG_OK;
+    first = 0;
+    for (uint32_t i = 0; i < nctx; ++i) {
+        xdrg_ctx *c = ctxs[i];
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const uint64_t f = c->h_stat[4];
+        const int e = (int)(uint32_t)c->h_stat[5];
+        if (e != XDRG_OK && first + f < fb) {   // the sequential reference stops at the smallest
+            fb = first + f;
+            code = e;
+        }
+        first += counts[i];
+    }
+    if (first_bad) *first_bad = fb;
+    if (err) *err = code;
+    if (code) ctxs[0]->err = xdrg_status_string(code);
+    return code;
+}

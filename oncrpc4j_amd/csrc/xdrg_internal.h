@@ -159,6 +159,18 @@ int launch_finalize(const unsigned long long *errkey, unsigned long long extra_k
 int launch_frame_scan(const uint8_t *in, uint64_t len, uint64_t *msg_offsets, uint64_t cap,
                       uint64_t *result, void *stream);
 
+// ---- multi-GPU exchange (kernels_multi.hip) -------------------------------
+constexpr int kMaxGatherSeg = 16;
+struct GatherArgs {             // copy bytes[s] from src[s] (a peer's HBM) to dst[s]
+    uint32_t nseg;
+    uint32_t rsv;
+    const uint8_t *src[kMaxGatherSeg];
+    uint8_t *dst[kMaxGatherSeg];
+    uint64_t bytes[kMaxGatherSeg];
+};
+int launch_gather(const GatherArgs &a, void *stream);
+int launch_add_u64(uint64_t *p, uint64_t n, uint64_t delta, void *stream);   // p[0..n) += delta
+
 constexpr int kRecThreads = 256;   // record path: threads per block
 constexpr int kRecPerThread = 4;   // records per thread in the size/scan pass
 constexpr int kRecPerBlock = kRecThreads * kRecPerThread;

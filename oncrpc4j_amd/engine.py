@@ -212,3 +212,44 @@ class Context:
 
     def __exit__(self, *exc):
         self.close()
+
+
+# ---- multi-GPU, one process (xdrg_encode_batch_multi / xdrg_decode_batch_multi) ----
+def _ptr_array(ctype, items):
+    arr = (ctype * len(items))()
+    for i, x in enumerate(items):
+        arr[i] = _ptr(x) if not isinstance(x, ctypes.Array) else ctypes.addressof(x)
+    return arr
+
+
+def encode_multi(ctxs, schema, cols, counts, outs, out_cap, rec_offsets=None, framed=False):
+    """Shard-parallel encode + xGMI all-gather over len(ctxs) contexts ->
+    stream bytes; every outs[i] then holds the whole stream."""
+    k = len(ctxs)
+    carrs = [c if isinstance(c, ctypes.Array) else columns_array(c) for c in cols]
+    ol = ctypes.c_uint64(0)
+    ro = _ptr_array(ctypes.c_void_p, rec_offsets) if rec_offsets is not None else None
+    rc = lib().xdrg_encode_batch_multi(_ptr_array(ctypes.c_void_p, [c.handle.value for c in ctxs]), k,
+                                       schema.handle, _ptr_array(ctypes.c_void_p, carrs),
+                                       (ctypes.c_uint64 * k)(*counts), _ptr_array(ctypes.c_void_p, outs),
+                                       int(out_cap), ro, abi.FRAME_RM if framed else 0, ctypes.byref(ol))
+    if rc:
+        _raise(rc, ctxs[0].handle)
+    return ol.value
+
+
+def decode_multi(ctxs, schema, ins, in_len, counts, cols, rec_offsets=None, framed=False,
+                 raise_on_error=True):
+    """Shard-parallel decode -> (status, first_bad, err) over the whole batch."""
+    k = len(ctxs)
+    carrs = [c if isinstance(c, ctypes.Array) else columns_array(c) for c in cols]
+    fb = ctypes.c_uint64(0)
+    er = ctypes.c_int(0)
+    ro = _ptr_array(ctypes.c_void_p, rec_offsets) if rec_offsets is not None else None
+    rc = lib().xdrg_decode_batch_multi(_ptr_array(ctypes.c_void_p, [c.handle.value for c in ctxs]), k,
+                                       schema.handle, _ptr_array(ctypes.c_void_p, ins), int(in_len), ro,
+                                       (ctypes.c_uint64 * k)(*counts), _ptr_array(ctypes.c_void_p, carrs),
+                                       abi.FRAME_RM if framed else 0, ctypes.byref(fb), ctypes.byref(er))
+    if rc and raise_on_error:
+        _raise(rc, ctxs[0].handle, fb.value)
+    return rc, fb.value, er.value
