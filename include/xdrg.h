@@ -206,6 +206,26 @@ int  xdrg_decode_batch(xdrg_ctx *ctx, const xdrg_schema *schema,
 int  xdrg_frame_scan(xdrg_ctx *ctx, const uint8_t *in, uint64_t len,
                      uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs);
 
+/* Deframe a received TCP byte stream: RpcMessageParserTCP.handleRead for a
+ * whole socket-buffer batch (isAllFragmentsArrived :63-99 and assembleXdr
+ * :109-140, repeated while complete messages remain).  The fragment bodies
+ * of each complete message (at most cap) are concatenated, marks stripped,
+ * into `payload` (device, payload_cap bytes) back to back; message i is
+ * payload[msg_offsets[i], msg_offsets[i+1]) (device, cap + 1 entries).
+ * *n_msgs (host) = messages delivered; *consumed (host) = stream bytes they
+ * occupied — the remainder starts there (handleRead's split, :57-60).
+ * Returns XDRG_OK, XDRG_E_INCOMPLETE (no complete message: STOP), or
+ * XDRG_E_CAPACITY (payload_cap too small; *consumed = bytes needed).  The
+ * messages then decode from payload + msg_offsets without XDRG_FRAME_RM.
+ * xdrg_frame_scan is the zero-copy form: stream offsets of each message's
+ * first mark (single-fragment messages decode in place with XDRG_FRAME_RM).
+ * Both walk the marks in parallel (list ranking over 4-byte positions); a
+ * stream whose chain meets a fragment size that is not a multiple of 4 is
+ * walked serially, with the same result.                                    */
+int  xdrg_deframe(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *payload,
+                  uint64_t payload_cap, uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs,
+                  uint64_t *consumed);
+
 /* ---- multi-GPU, one process ---------------------------
  * For a caller that drives several devices from one process (a JVM with one
  * context per GPU).  Records are independent (xdr/XdrAble.java:40,49), so a

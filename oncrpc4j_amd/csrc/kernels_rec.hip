@@ -2006,39 +2006,6 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
 }
 
 // ===========================================================================
-// Frame walk (RpcMessageParserTCP.isAllFragmentsArrived/assembleXdr :63-140)
-// ===========================================================================
-__device__ __forceinline__ uint32_t ld_be32_u(const uint8_t *p) {
-    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
-}
-
-// Serial mark walk by one lane (marks form a dependent chain).  result[0] =
-// complete messages found.
-__global__ void k_frame_scan(const uint8_t *in, uint64_t len, uint64_t *msg_offsets, uint64_t cap,
-                             uint64_t *result) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    uint64_t pos = 0, k = 0;
-    while (k < cap) {
-        uint64_t p = pos;
-        bool complete = false;
-        if (len - p < 4) break;
-        do {
-            const uint32_t m = ld_be32_u(in + p);
-            p += 4;
-            const uint64_t size = m & kSizeMask;
-            if (size > len - p) break;           // fragment not fully received
-            p += size;
-            if (m & kLastFrag) { complete = true; break; }
-        } while (len - p >= 4);
-        if (!complete) break;
-        msg_offsets[k++] = pos;
-        pos = p;
-    }
-    msg_offsets[k] = pos;
-    result[0] = k;
-}
-
-// ===========================================================================
 // Launchers
 // ===========================================================================
 __global__ void k_debug_recargs(const RecArgs a) {
@@ -2149,11 +2116,6 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
     return (int)hipGetLastError();
 }
 
-int launch_frame_scan(const uint8_t *in, uint64_t len, uint64_t *msg_offsets, uint64_t cap,
-                      uint64_t *result, void *stream) {
-    hipLaunchKernelGGL(k_frame_scan, dim3(1), dim3(64), 0, (hipStream_t)stream, in, len,
-                       msg_offsets, cap, result);
-    return (int)hipGetLastError();
-}
+
 
 }  // namespace xdrg

@@ -156,8 +156,36 @@ int launch_iota(uint64_t *dst, uint64_t n, uint64_t stride, void *stream);
 // results (async mode); any output pointer may be NULL.
 int launch_finalize(const unsigned long long *errkey, unsigned long long extra_key, uint64_t n,
                     uint64_t *first_bad, int *err, void *stream);
-int launch_frame_scan(const uint8_t *in, uint64_t len, uint64_t *msg_offsets, uint64_t cap,
-                      uint64_t *result, void *stream);
+
+// ---- parallel record-mark walk (kernels_frame.hip) ------------------------
+constexpr uint32_t kFChunk = 1024;            // words per level-1 chunk (4 KiB of stream)
+constexpr uint32_t kFSuper = kFChunk * 256;   // words per super-chunk (1 MiB)
+constexpr uint32_t kFStop = 0xffffffffu;      // chain ends: fragment not fully received
+constexpr uint32_t kFUnal = 0xfffffffeu;      // chain meets a size % 4 != 0 (serial fallback)
+constexpr uint32_t kFNone = 0xffffffffu;      // no entry
+struct FrameWs {                              // device workspace of one walk
+    uint32_t *exit1, *exit2;                  // [Q] word-position exits (L1 chunk, L2 super-chunk)
+    uint32_t *sentry, *centry;                // [nsuper], [nchunks] chain entries
+    uint32_t *counts, *base;                  // [nchunks] fragments per chunk, exclusive scan
+    uint64_t *frag_pos;                       // [nfrag] stream offset of each fragment's mark
+    uint32_t *frag_mark;                      // [nfrag] the raw mark (size | LAST)
+    uint64_t *size, *pay_off;                 // [nfrag] body sizes, body offsets in the payload
+    uint32_t *last, *msg_id;                  // [nfrag] LAST flags, message index
+    uint64_t *res;                            // [0] chain terminal [1] complete fragments
+                                              // [2] fragments (serial) [3] consumed stream bytes
+    void *tmp;                                // rocPRIM scan storage
+    size_t tmp_bytes;
+};
+size_t frame_scan_tmp_bytes(uint64_t n);
+int frame_levels(const uint8_t *in, uint64_t len, FrameWs &ws, void *stream);
+int frame_serial(const uint8_t *in, uint64_t len, FrameWs &ws, void *stream);
+int frame_last(FrameWs &ws, uint64_t nfrag, void *stream);
+// msg_offsets[0..min(n, cap)] of the messages formed by the first nf
+// (complete) fragments: stream offsets of their marks, or offsets in the
+// payload (bodies back to back); res[3] = stream bytes of messages < cap.
+int frame_messages(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, bool stream_offsets,
+                   uint64_t *msg_offsets, void *stream);
+int frame_copy(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, uint8_t *payload, void *stream);
 
 // ---- multi-GPU exchange (kernels_multi.hip) -------------------------------
 constexpr int kMaxGatherSeg = 16;

@@ -186,6 +186,16 @@ class Context:
             _raise(rc, self._h)
         return nm.value
 
+    def deframe(self, data, length, payload, payload_cap, msg_offsets, cap):
+        """xdrg_deframe -> (messages, consumed stream bytes); (0, 0) = STOP."""
+        nm = ctypes.c_uint64(0)
+        used = ctypes.c_uint64(0)
+        rc = lib().xdrg_deframe(self._h, _ptr(data), int(length), _ptr(payload), int(payload_cap),
+                                _ptr(msg_offsets), int(cap), ctypes.byref(nm), ctypes.byref(used))
+        if rc not in (abi.OK, abi.E_INCOMPLETE):
+            _raise(rc, self._h)
+        return nm.value, used.value
+
     def kernel_stats(self, kernel):
         """-> (launches, total_ms) for one XDRG_KERNEL_* id (needs timing=True)."""
         n = ctypes.c_uint64(0)

@@ -1,0 +1,132 @@
+"""Parallel record-mark walk (kernels_frame.hip):
+xdrg_frame_scan and xdrg_deframe against the serial oracle (oracle/xdr_oracle.c
+xo_frame_scan, a restatement of RpcMessageParserTCP.isAllFragmentsArrived /
+assembleXdr, rpc/RpcMessageParserTCP.java:63-140) and the golden framing
+fixtures.  Streams span several 1 MiB super-chunks, carry fragments of many
+sizes (the re-fragmenter of ctest/rpc/RpcMessageParserTCPTest.java:161-181,
+oracle.fragment), bodies full of small integers that look like marks, cut
+tails, and fragment sizes that are not multiples of 4 (serial path)."""
+import numpy as np
+import pytest
+
+import gold
+import oracle
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _dev(b):
+    if not b:
+        return torch.zeros(4, dtype=torch.uint8, device="cuda")
+    return torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy()).cuda()
+
+
+def build(rng, nmsg, aligned=True, big=0, marks_in_body=False):
+    """-> (stream, bodies): nmsg messages, each re-fragmented."""
+    bodies, parts = [], []
+    for i in range(nmsg):
+        n = int(rng.integers(0, 400))
+        if aligned:
+            n &= ~3
+        if big and i % max(nmsg // big, 1) == 7:
+            n = int(rng.integers(1 << 20, 3 << 20)) & ~3
+        if marks_in_body:   # small BE ints everywhere: false chains through every body
+            body = (rng.integers(0, 12, (n + 3) // 4, dtype=np.uint32) * 4).astype(">u4").tobytes()[:n]
+        else:
+            body = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        frag = int(rng.choice([4, 16, 64, 1024, 1 << 16, 1 << 22]))
+        if not aligned:
+            frag += int(rng.integers(0, 4))
+        bodies.append(body)
+        parts.append(oracle.fragment(body, frag))
+    return b"".join(parts), bodies
+
+
+def check(ctx, stream, bodies_all=None, cap=1 << 22):
+    rc, want = oracle.frame_scan(stream, cap)
+    k_want = len(want) - 1
+    dev = _dev(stream)
+    offs = torch.zeros(cap + 1, dtype=torch.int64, device="cuda")
+    k = ctx.frame_scan(dev, len(stream), offs, cap)
+    assert k == k_want
+    assert offs[:k + 1].cpu().tolist() == want
+    # assembled bodies
+    payload = torch.zeros(len(stream) + 16, dtype=torch.uint8, device="cuda")
+    moffs = torch.zeros(cap + 1, dtype=torch.int64, device="cuda")
+    k2, used = ctx.deframe(dev, len(stream), payload, payload.numel(), moffs, cap)
+    assert k2 == k_want and used == want[-1]
+    mo = moffs[:k2 + 1].cpu().numpy()
+    pl = payload[:int(mo[-1]) if k2 else 0].cpu().numpy().tobytes()
+    got = [pl[mo[i]:mo[i + 1]] for i in range(k2)]
+    if bodies_all is not None:
+        assert got == bodies_all[:k2]
+    return k, got
+
+
+def test_golden_framing_deframe(gpu_ctx):
+    for case in gold.load("framing.json")["cases"]:
+        stream = bytes.fromhex(case["stream"])
+        k, got = check(gpu_ctx, stream, cap=16)
+        assert k == case["complete"]
+        assert [g.hex() for g in got] == case["messages"]
+
+
+@pytest.mark.parametrize("marks_in_body", [False, True], ids=["random-bodies", "mark-like-bodies"])
+def test_parallel_walk_many_messages(gpu_ctx, marks_in_body):
+    rng = np.random.default_rng(11 + marks_in_body)
+    stream, bodies = build(rng, 30000, big=3, marks_in_body=marks_in_body)
+    assert len(stream) > (8 << 20)   # several 1 MiB super-chunks
+    k, _ = check(gpu_ctx, stream, bodies)
+    assert k == len(bodies)
+
+
+def test_parallel_walk_cut_tails(gpu_ctx):
+    rng = np.random.default_rng(5)
+    stream, bodies = build(rng, 6000, big=1)
+    for cut in [3, 4, 5, len(stream) // 3, len(stream) // 2 + 1, len(stream) - 1, len(stream) - 4]:
+        check(gpu_ctx, stream[:cut], bodies)
+
+
+def test_unaligned_fragment_sizes_use_the_serial_walk(gpu_ctx):
+    rng = np.random.default_rng(8)
+    stream, bodies = build(rng, 3000, aligned=False)
+    k, _ = check(gpu_ctx, stream, bodies)
+    assert k == len(bodies)
+
+
+def test_cap_limits_messages(gpu_ctx):
+    rng = np.random.default_rng(2)
+    stream, bodies = build(rng, 500)
+    rc, want = oracle.frame_scan(stream, 10)
+    dev = _dev(stream)
+    payload = torch.zeros(len(stream), dtype=torch.uint8, device="cuda")
+    moffs = torch.zeros(11, dtype=torch.int64, device="cuda")
+    k, used = gpu_ctx.deframe(dev, len(stream), payload, payload.numel(), moffs, 10)
+    assert k == 10 and used == want[-1]
+    mo = moffs.cpu().numpy()
+    pl = payload[:int(mo[-1])].cpu().numpy().tobytes()
+    assert [pl[mo[i]:mo[i + 1]] for i in range(10)] == bodies[:10]
+
+
+def test_payload_capacity(gpu_ctx):
+    from oncrpc4j_amd import engine
+    stream, bodies = build(np.random.default_rng(4), 50)
+    need = sum(len(b) for b in bodies)
+    payload = torch.zeros(need, dtype=torch.uint8, device="cuda")
+    moffs = torch.zeros(51, dtype=torch.int64, device="cuda")
+    with pytest.raises(engine.CapacityError):
+        gpu_ctx.deframe(_dev(stream), len(stream), payload, need - 1, moffs, 50)
+    assert not payload.any()
+
+
+def test_framed_cfg2_stream_offsets(gpu_ctx):
+    """A record-marked configs[1] stream (36-byte messages): offsets 36 i."""
+    n = 1 << 20
+    words = np.random.default_rng(1).integers(0, 2**32, (n, 9), dtype=np.uint64).astype(np.uint32)
+    words[:, 0] = np.uint32(0x80000020).byteswap()
+    dev = torch.from_numpy(words.view(np.uint8).reshape(-1)).cuda()
+    offs = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    k = gpu_ctx.frame_scan(dev, 36 * n, offs, n)
+    assert k == n
+    assert torch.equal(offs, torch.arange(0, 36 * (n + 1), 36, dtype=torch.int64, device="cuda"))
