@@ -1,0 +1,467 @@
+"""rpcgen.py — XDR language (.x) files -> engine field tapes.
+
+oncrpc4j's jrpcgen turns a .x file into XdrAble classes whose xdrEncode /
+xdrDecode call the stream once per declaration, in declaration order
+(oncrpc4j-rpcgen .../jrpcgen/jrpcgen.java:758-913 `codingMethod`), so the
+record's bytes are the concatenation of its declarations' encodings, nested
+structs included.  This module reads the same .x language (grammar:
+jrpcgen/JrpcgenParser.cup) and emits that concatenation as an engine field
+tape (include/xdrg.h xdrg_field: type x kind x count), so unchanged .x files
+drive the batch engine:
+
+  const, typedef, enum, struct (flattened), program / version / procedure
+  (argument and result tapes, multi-argument procedures as jrpcgen encodes
+  them: one after another), base types as JrpcgenParser.cup:716-802 maps
+  them (char -> byte, short, int/long, hyper, unsigned X -> X's bytes, bool,
+  float, double, quadruple -> double), opaque[n] / opaque<n>, string<n>,
+  T[n] / T<n> of base types.
+
+Not expressible as ONE tape (records of the same type would differ in
+shape): unions (jrpcgen.java:1240-1340 encodes the discriminant, then one
+arm), optional data `T *x` (JrpcgenDeclaration.INDIRECTION: a bool, then T
+or nothing) and arrays of structs.  Asking for their tape raises
+NotBatchable naming the declaration; the parsed Union keeps its arms so a
+caller can split a batch by discriminant value.
+"""
+import re
+
+from . import abi
+
+INT = (abi.T_INT, abi.K_SCALAR, 0)
+
+
+class XdrSyntaxError(ValueError):
+    pass
+
+
+class NotBatchable(ValueError):
+    """The type's records do not share one field tape (union / optional / array of structs)."""
+
+
+# ---- lexer ----------------------------------------------------------------------
+_TOKEN = re.compile(r"""
+    (?P<ws>\s+) | (?P<comment>/\*.*?\*/|//[^\n]*) | (?P<pass>^%[^\n]*) |
+    (?P<num>-?(?:0[xX][0-9a-fA-F]+|\d+)) | (?P<id>[A-Za-z_][A-Za-z0-9_]*) | (?P<sym>[;,:=*(){}\[\]<>])
+    """, re.X | re.S | re.M)
+
+
+def _tokens(text):
+    pos = 0
+    out = []
+    while pos < len(text):
+        m = _TOKEN.match(text, pos)
+        if not m:
+            raise XdrSyntaxError(f"unexpected {text[pos:pos + 20]!r} at offset {pos}")
+        pos = m.end()
+        kind = m.lastgroup
+        if kind in ("ws", "comment", "pass"):
+            continue
+        out.append((kind, m.group()))
+    return out
+
+
+def _int_literal(s):
+    """C integer literal: decimal, 0x hex, leading-0 octal (Calculator.x consts)."""
+    neg = s.startswith("-")
+    t = s[1:] if neg else s
+    if t[:2] in ("0x", "0X"):
+        v = int(t, 16)
+    elif len(t) > 1 and t[0] == "0":
+        v = int(t, 8)
+    else:
+        v = int(t)
+    return -v if neg else v
+
+
+# ---- declarations ----------------------------------------------------------------
+BASE = {  # JrpcgenParser.cup:716-802 (+ string / opaque declarations)
+    "int": abi.T_INT, "long": abi.T_INT, "short": abi.T_SHORT, "char": abi.T_BYTE,
+    "hyper": abi.T_HYPER, "bool": abi.T_BOOL, "float": abi.T_FLOAT, "double": abi.T_DOUBLE,
+    "quadruple": abi.T_DOUBLE,
+}
+UNSIGNED = {abi.T_INT: abi.T_UINT, abi.T_HYPER: abi.T_UHYPER, abi.T_SHORT: abi.T_SHORT,
+            abi.T_BYTE: abi.T_BYTE}
+
+
+class Decl:
+    """One declaration: name, type (base id or type name), kind, size expr."""
+
+    def __init__(self, name, type_, kind, size=None):
+        self.name, self.type, self.kind, self.size = name, type_, kind, size
+
+    def __repr__(self):
+        return f"Decl({self.name!r}, {self.type!r}, {self.kind}, {self.size!r})"
+
+
+SCALAR, FIXED, DYNAMIC, OPTIONAL, VOID = "scalar", "fixed", "dynamic", "optional", "void"
+
+
+class Struct:
+    def __init__(self, name, decls):
+        self.name, self.decls = name, decls
+
+
+class Union:
+    def __init__(self, name, disc, arms, default):
+        self.name, self.disc, self.arms, self.default = name, disc, arms, default   # arms: [(values, Decl)]
+
+
+class Enum:
+    def __init__(self, name, values):
+        self.name, self.values = name, values
+
+
+class Procedure:
+    def __init__(self, name, number, result, args):
+        self.name, self.number, self.result, self.args = name, number, result, args
+
+
+class Spec:
+    """A parsed .x file."""
+
+    def __init__(self):
+        self.consts = {}
+        self.types = {}      # name -> Struct | Union | Enum | Decl (typedef)
+        self.programs = {}   # name -> (number, {version name: (number, [Procedure])})
+
+    # ---- constants --------------------------------------------------------------
+    def value(self, v):
+        if v is None:
+            return 0
+        if isinstance(v, int):
+            return v
+        if re.fullmatch(r"-?(0[xX][0-9a-fA-F]+|\d+)", v):
+            return _int_literal(v)
+        if v in self.consts:
+            return self.value(self.consts[v])
+        for t in self.types.values():
+            if isinstance(t, Enum) and v in t.values:
+                return self.value(t.values[v])
+        raise XdrSyntaxError(f"unknown constant {v!r}")
+
+    # ---- tapes --------------------------------------------------------------------
+    def fields(self, type_name):
+        """Field tape of one record of `type_name` (structs flattened)."""
+        return self._type_fields(type_name, type_name)
+
+    def _type_fields(self, t, where):
+        if t in BASE or t in ("unsigned",):
+            return [(BASE.get(t, abi.T_INT), abi.K_SCALAR, 0)]
+        if t == "string":
+            return [(abi.T_STRING, abi.K_DYNAMIC, 0)]
+        d = self.types.get(t)
+        if d is None:
+            raise XdrSyntaxError(f"unknown type {t!r} (in {where})")
+        if isinstance(d, Enum):
+            return [(abi.T_ENUM, abi.K_SCALAR, 0)]
+        if isinstance(d, Struct):
+            out = []
+            for decl in d.decls:
+                out += self._decl_fields(decl, f"{where}.{decl.name}")
+            return out
+        if isinstance(d, Union):
+            raise NotBatchable(f"{where}: union {t} switches its arms per record "
+                               f"(jrpcgen.java:1240-1340); split the batch by discriminant")
+        return self._decl_fields(d, where)   # typedef
+
+    def _elem(self, t, where):
+        """Base element type id of an array declaration's element type."""
+        d = self.types.get(t)
+        while isinstance(d, Decl) and d.kind == SCALAR:   # typedef chain to a scalar
+            t, d = d.type, self.types.get(d.type)
+        if isinstance(d, Enum):
+            return abi.T_ENUM
+        if t in BASE or t == "unsigned":
+            return BASE.get(t, abi.T_INT)
+        if isinstance(t, tuple):   # ("unsigned", base)
+            return t[1]
+        raise NotBatchable(f"{where}: array of {t!r} (arrays of structs / unions have no flat tape)")
+
+    def _decl_fields(self, decl, where):
+        if decl.kind == VOID:
+            return []
+        if decl.kind == OPTIONAL:
+            raise NotBatchable(f"{where}: optional data '{decl.type} *{decl.name}' encodes a bool and "
+                               f"then the value or nothing, per record")
+        t = decl.type
+        if t == "opaque":
+            n = self.value(decl.size)
+            return [(abi.T_OPAQUE, abi.K_FIXED if decl.kind == FIXED else abi.K_DYNAMIC,
+                     n if decl.kind == FIXED else 0)]
+        if t == "string":
+            return [(abi.T_STRING, abi.K_DYNAMIC, 0)]
+        if decl.kind == SCALAR:
+            if isinstance(t, tuple):
+                return [(t[1], abi.K_SCALAR, 0)]
+            return self._type_fields(t, where)
+        base = t[1] if isinstance(t, tuple) else self._elem(t, where)
+        if decl.kind == FIXED:
+            return [(base, abi.K_FIXED, self.value(decl.size))]
+        return [(base, abi.K_DYNAMIC, 0)]
+
+    # ---- procedures ---------------------------------------------------------------
+    def procedures(self):
+        """(prog, vers, proc) -> Procedure, for every program in the file."""
+        out = {}
+        for pname, (pnum, versions) in self.programs.items():
+            for vname, (vnum, procs) in versions.items():
+                for p in procs:
+                    out[(pnum, vnum, p.number)] = p
+        return out
+
+    def args_fields(self, prog, vers, proc):
+        """Argument tape of a call (arguments one after another, jrpcgen
+        multi-argument procedures)."""
+        p = self.procedures()[(prog, vers, proc)]
+        out = []
+        for i, a in enumerate(p.args):
+            out += self._arg_fields(a, f"{p.name} argument {i}")
+        return out
+
+    def result_fields(self, prog, vers, proc):
+        p = self.procedures()[(prog, vers, proc)]
+        return self._arg_fields(p.result, f"{p.name} result")
+
+    def _arg_fields(self, t, where):
+        if t == "void":
+            return []
+        if isinstance(t, tuple):
+            return [(t[1], abi.K_SCALAR, 0)]
+        return self._type_fields(t, where)
+
+
+# ---- parser ---------------------------------------------------------------------
+class _Parser:
+    def __init__(self, text):
+        self.t = _tokens(text)
+        self.i = 0
+        self.spec = Spec()
+
+    def peek(self, k=0):
+        return self.t[self.i + k][1] if self.i + k < len(self.t) else None
+
+    def next(self):
+        if self.i >= len(self.t):
+            raise XdrSyntaxError("unexpected end of file")
+        self.i += 1
+        return self.t[self.i - 1][1]
+
+    def expect(self, s):
+        got = self.next()
+        if got != s:
+            raise XdrSyntaxError(f"expected {s!r}, got {got!r} (token {self.i})")
+
+    def ident(self):
+        k, v = self.t[self.i]
+        if k != "id":
+            raise XdrSyntaxError(f"expected an identifier, got {v!r}")
+        self.i += 1
+        return v
+
+    def value(self):
+        k, v = self.t[self.i]
+        self.i += 1
+        return _int_literal(v) if k == "num" else v
+
+    def parse(self):
+        while self.i < len(self.t):
+            kw = self.next()
+            if kw == "const":
+                name = self.ident()
+                self.expect("=")
+                self.spec.consts[name] = self.value()
+                self.expect(";")
+            elif kw == "typedef":
+                d = self.declaration()
+                self.spec.types[d.name] = d
+                self.expect(";")
+            elif kw == "enum":
+                name = self.ident()
+                self.spec.types[name] = self.enum_body(name)
+                self.expect(";")
+            elif kw == "struct":
+                name = self.ident()
+                self.spec.types[name] = Struct(name, self.struct_body())
+                self.expect(";")
+            elif kw == "union":
+                name = self.ident()
+                self.spec.types[name] = self.union_body(name)
+                self.expect(";")
+            elif kw in ("program", "PROGRAM"):
+                self.program()
+            else:
+                raise XdrSyntaxError(f"unexpected {kw!r} at top level")
+        return self.spec
+
+    def type_spec(self):
+        """-> base name, ("unsigned", type id), or a type name."""
+        w = self.next()
+        if w == "unsigned":
+            nxt = self.peek()
+            if nxt in ("int", "long", "hyper", "short", "char"):
+                self.next()
+                if nxt in ("long", "hyper", "short") and self.peek() == "int":
+                    self.next()
+                return ("unsigned", UNSIGNED[BASE[nxt]])
+            return ("unsigned", abi.T_UINT)
+        if w in ("long", "hyper", "short") and self.peek() == "int":
+            self.next()
+        if w in ("struct", "enum", "union"):
+            if self.peek() == "{":   # anonymous inline definition
+                name = f"_anon{self.i}"
+                if w == "struct":
+                    self.spec.types[name] = Struct(name, self.struct_body())
+                elif w == "enum":
+                    self.spec.types[name] = self.enum_body(name)
+                else:
+                    self.spec.types[name] = self.union_body(name)
+                return name
+            return self.ident()
+        return w
+
+    def declaration(self):
+        if self.peek() == "void":
+            self.next()
+            return Decl(None, "void", VOID)
+        if self.peek() in ("opaque", "string"):
+            t = self.next()
+            name = self.ident()
+            if self.peek() == "[":
+                self.next()
+                size = self.value()
+                self.expect("]")
+                return Decl(name, t, FIXED, size)
+            self.expect("<")
+            size = None if self.peek() == ">" else self.value()
+            self.expect(">")
+            return Decl(name, t, DYNAMIC, size)
+        t = self.type_spec()
+        if self.peek() == "*":
+            self.next()
+            return Decl(self.ident(), t, OPTIONAL)
+        name = self.ident()
+        if self.peek() == "[":
+            self.next()
+            size = self.value()
+            self.expect("]")
+            return Decl(name, t, FIXED, size)
+        if self.peek() == "<":
+            self.next()
+            size = None if self.peek() == ">" else self.value()
+            self.expect(">")
+            return Decl(name, t, DYNAMIC, size)
+        return Decl(name, t, SCALAR)
+
+    def enum_body(self, name):
+        self.expect("{")
+        values = {}
+        while True:
+            n = self.ident()
+            self.expect("=")
+            values[n] = self.value()
+            if self.next() == "}":
+                break
+        return Enum(name, values)
+
+    def struct_body(self):
+        self.expect("{")
+        decls = []
+        while self.peek() != "}":
+            decls.append(self.declaration())
+            self.expect(";")
+        self.next()
+        return decls
+
+    def union_body(self, name):
+        self.expect("switch")
+        self.expect("(")
+        disc = self.declaration()
+        self.expect(")")
+        self.expect("{")
+        arms, default, values = [], None, []
+        while self.peek() != "}":
+            w = self.next()
+            if w == "case":
+                values.append(self.value())
+                self.expect(":")
+                if self.peek() == "case":
+                    continue
+                d = self.declaration()
+                self.expect(";")
+                arms.append((values, d))
+                values = []
+            elif w == "default":
+                self.expect(":")
+                default = self.declaration()
+                self.expect(";")
+            else:
+                raise XdrSyntaxError(f"unexpected {w!r} in union {name}")
+        self.next()
+        return Union(name, disc, arms, default)
+
+    def program(self):
+        pname = self.ident()
+        self.expect("{")
+        versions = {}
+        while self.peek() != "}":
+            kw = self.next()
+            if kw not in ("version", "VERSION"):
+                raise XdrSyntaxError(f"expected version, got {kw!r}")
+            vname = self.ident()
+            self.expect("{")
+            procs = []
+            while self.peek() != "}":
+                rtype = "void" if self.peek() == "void" else None
+                if rtype:
+                    self.next()
+                else:
+                    rtype = "string" if self.peek() == "string" else None
+                    if rtype:
+                        self.next()
+                    else:
+                        rtype = self.type_spec()
+                name = self.ident()
+                self.expect("(")
+                args = []
+                while self.peek() != ")":
+                    if self.peek() == "void":
+                        self.next()
+                    elif self.peek() == "string":
+                        self.next()
+                        args.append("string")
+                    else:
+                        args.append(self.type_spec())
+                    if self.t[self.i][0] == "id" and self.peek() not in (",", ")"):
+                        self.next()   # parameter name
+                    if self.peek() == ",":
+                        self.next()
+                self.expect(")")
+                self.expect("=")
+                procs.append(Procedure(name, None, rtype, args))
+                procs[-1].number = self.value()
+                self.expect(";")
+            self.next()
+            self.expect("=")
+            vnum = self.value()
+            self.expect(";")
+            versions[vname] = (vnum, procs)
+        self.next()
+        self.expect("=")
+        pnum = self.value()
+        self.expect(";")
+        self.spec.programs[pname] = (pnum, versions)
+
+
+def parse(text):
+    """Parse .x source -> Spec (numbers resolved lazily through Spec.value)."""
+    spec = _Parser(text).parse()
+    for pname, (pnum, versions) in list(spec.programs.items()):
+        vv = {vn: (spec.value(n), [Procedure(p.name, spec.value(p.number), p.result, p.args) for p in ps])
+              for vn, (n, ps) in versions.items()}
+        spec.programs[pname] = (spec.value(pnum), vv)
+    return spec
+
+
+def parse_file(path):
+    with open(path) as f:
+        return parse(f.read())
