@@ -191,18 +191,20 @@ __global__ __launch_bounds__(256) void k_frame_copy(const uint8_t *in, const uin
                                                      const uint32_t *frag_mark, const uint64_t *pay_off,
                                                      const uint32_t *msg_id, uint64_t nf, uint64_t cap,
                                                      uint8_t *payload) {
-    const uint64_t f = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63;
-    if (f >= nf || msg_id[f] >= cap) return;
-    const uint8_t *src = in + frag_pos[f] + 4;
-    uint8_t *dst = payload + pay_off[f];
-    const uint64_t n = frag_mark[f] & kSizeMask;
-    if ((((uintptr_t)src | (uintptr_t)dst | n) & 3) == 0) {
-        const uint32_t *s = (const uint32_t *)src;
-        uint32_t *d = (uint32_t *)dst;
-        for (uint64_t i = lane; i < n / 4; i += 64) d[i] = s[i];
-    } else {
-        for (uint64_t i = lane; i < n; i += 64) dst[i] = src[i];
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t f = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; f < nf; f += nwaves) {
+        if (msg_id[f] >= cap) return;   // fragments are in message order
+        const uint8_t *src = in + frag_pos[f] + 4;
+        uint8_t *dst = payload + pay_off[f];
+        const uint64_t n = frag_mark[f] & kSizeMask;
+        if ((((uintptr_t)src | (uintptr_t)dst | n) & 3) == 0) {
+            const uint32_t *s = (const uint32_t *)src;
+            uint32_t *d = (uint32_t *)dst;
+            for (uint64_t i = lane; i < n / 4; i += 64) d[i] = s[i];
+        } else {
+            for (uint64_t i = lane; i < n; i += 64) dst[i] = src[i];
+        }
     }
 }
 
@@ -271,7 +273,8 @@ int frame_messages(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, bo
 }
 
 int frame_copy(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, uint8_t *payload, void *stream) {
-    hipLaunchKernelGGL(k_frame_copy, grid1(nf * 64, 256), dim3(256), 0, (hipStream_t)stream, in, ws.frag_pos,
+    const uint64_t blocks = (nf + 3) / 4 < 65536 ? (nf + 3) / 4 : 65536;   // 4 waves per block, grid-stride
+    hipLaunchKernelGGL(k_frame_copy, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, in, ws.frag_pos,
                        ws.frag_mark, ws.pay_off, ws.msg_id, nf, cap, payload);
     return (int)hipGetLastError();
 }

@@ -464,20 +464,11 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_wave(const RecArgs a)
 }
 
 // ===========================================================================
-// Flat place kernels (schemas with <= kMaxDynLds dynamic fields)
-//
-// Phase 1, one thread per record: sizes / counts, block scan, and every
-// record's metadata (stream offset, dynamic counts, native offsets) staged in
-// LDS.  Phase 2 sweeps the block's contiguous XDR byte range in 16-byte
-// chunks, one chunk per lane per step, so the stream side is perfectly
-// coalesced (aligned dwordx4).  A lane finds its chunk's record by binary
-// search over the LDS offsets and the field by walking the schema; a chunk
-// that lies inside one dynamic payload moves with one 16-byte access on the
-// native side (byte-unaligned global accesses are supported on gfx950 under
-// the HSA unaligned-access mode, tools/probes/unaligned.hip); other chunks are
-// assembled dword by dword.  Measured pattern ceilings that chose this shape
-// (tools/probes/pattern_bw.hip, MI355X): coalesced stream + misaligned other
-// side 6.1-6.3 TB/s; record-at-a-time groups 2.4-5.4 TB/s.
+// Shared helpers of the place kernels (schemas with <= kMaxDynLds dynamic
+// fields).  Byte-unaligned global dword / dwordx4 accesses are used where
+// a payload moves between the 4-aligned stream and byte-packed native
+// columns: gfx950 supports them under the HSA unaligned-access mode
+// (tools/probes/unaligned.hip).
 // ===========================================================================
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -486,89 +477,6 @@ typedef uint32_t u32u __attribute__((aligned(1)));
 __device__ __forceinline__ bool is_word4(const VField &f) {
     return f.type == XDRG_T_INT || f.type == XDRG_T_UINT || f.type == XDRG_T_ENUM ||
            f.type == XDRG_T_FLOAT;
-}
-
-// Last j in [0, n) with key[j] <= q (key non-decreasing, key[0] <= q).
-__device__ __forceinline__ uint32_t find_rec(const uint64_t *key, uint32_t n, uint64_t q) {
-    uint32_t lo = 0, hi = n;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (key[mid] <= q) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
-// Coarse chunk -> record table: entry e holds the record containing chunk
-// cbase + (e << shift), so a chunk's record is found by a short binary search
-// between two neighbouring entries instead of over the whole block.
-constexpr int kLookup = 256;
-constexpr int kFlatU = 4;     // chunks per lane in flight in the flat kernels
-
-__device__ __forceinline__ void build_lookup(const uint64_t *key, uint32_t n, uint64_t cbase, uint32_t shift,
-                                             uint64_t lo_byte, uint32_t *tab) {
-    for (uint32_t e = threadIdx.x; e <= kLookup; e += blockDim.x) {
-        uint64_t q = (cbase + ((uint64_t)e << shift)) << 4;
-        if (q < lo_byte) q = lo_byte;
-        tab[e] = find_rec(key, n, q);
-    }
-}
-__device__ __forceinline__ uint32_t lookup_rec(const uint64_t *key, uint32_t n, const uint32_t *tab,
-                                               uint64_t cbase, uint32_t shift, uint64_t q) {
-    const uint64_t e = ((q >> 4) - cbase) >> shift;
-    uint32_t lo = tab[e], hi = e + 1 <= (uint64_t)kLookup ? tab[e + 1] + 1 : n;
-    if (hi > n) hi = n;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (key[mid] <= q) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-__device__ __forceinline__ uint32_t lookup_shift(uint64_t nchunks) {
-    uint32_t sh = 0;
-    while ((nchunks >> sh) > (uint64_t)kLookup - 1) ++sh;
-    return sh;
-}
-
-// Where byte o of a record falls: segment kind, field, dynamic index, offset
-// inside the field's XDR bytes.  cnt(d) gives dynamic field d's count.
-enum SegKind : uint32_t { SEG_NONE = 0, SEG_MARK = 1, SEG_FIXED = 2, SEG_DYN = 3 };
-struct Seg {
-    uint32_t kind, k, d;
-    uint64_t rel;   // byte offset inside the field's XDR bytes
-    uint64_t cnt;   // SEG_DYN: element count
-    uint64_t len;   // XDR bytes of the field
-};
-
-template <class CntFn>
-__device__ __forceinline__ Seg locate(const RecArgs &a, const VField *F, uint64_t o, CntFn cnt_of) {
-    Seg s;
-    s.kind = SEG_NONE; s.k = 0; s.d = 0; s.rel = 0; s.cnt = 0; s.len = 0;
-    uint64_t pos = 0;
-    if (a.framed) {
-        if (o < 4) { s.kind = SEG_MARK; s.rel = o; return s; }
-        pos = 4;
-    }
-    uint32_t d = 0;
-    for (uint32_t k = 0; k < a.nf; ++k) {
-        const VField &f = F[k];
-        uint64_t len, c = 0;
-        if (f.kind != XDRG_K_DYNAMIC) {
-            len = f.xbytes;
-        } else {
-            c = cnt_of(d);
-            len = dyn_xdr_bytes(f, c);
-        }
-        if (o < pos + len) {
-            s.kind = f.kind != XDRG_K_DYNAMIC ? SEG_FIXED : SEG_DYN;
-            s.k = k; s.d = d; s.rel = o - pos; s.cnt = c; s.len = len;
-            return s;
-        }
-        pos += len;
-        if (f.kind == XDRG_K_DYNAMIC) ++d;
-    }
-    return s;
 }
 
 // XDR word at byte offset rel (multiple of 4) of fixed field f, record r.
@@ -624,143 +532,10 @@ __device__ __forceinline__ void dyn_store(const VField &f, uint64_t e0, uint64_t
     else dec_elem(f.type, f.data + (e0 + (b >> 2)) * f.nsz, 0, v);
 }
 
-// Field descriptors staged in LDS: phase 2 indexes them with per-lane field
-// numbers, which on the kernel-argument struct would become per-lane global
-// loads of the kernarg segment.
-__device__ __forceinline__ void stage_fields(const RecArgs &a, VField *sf) {
-    for (uint32_t k = threadIdx.x; k < a.nf; k += blockDim.x) sf[k] = a.f[k];
-}
-
 // ---- encode -------------------------------------------------------------------
 // LDS: soff[RPB + 2] u64 | ssrc[ND][RPB] u64 | scnt[ND][RPB] u32
 __host__ __device__ constexpr size_t enc_lds_bytes(uint32_t nd) {
     return (size_t)(kRecPerBlock + 2) * 8 + (size_t)nd * kRecPerBlock * 12;
-}
-
-__global__ __launch_bounds__(kRecThreads) void k_enc_flat(const RecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint64_t *soff = (uint64_t *)smem;
-    uint64_t *ssrc = soff + kRecPerBlock + 2;
-    uint32_t *scnt = (uint32_t *)(ssrc + (size_t)a.ndyn * kRecPerBlock);
-    const uint64_t total = a.totals[0];
-    if (total > a.xdr_cap) return;  // XDRG_E_CAPACITY: write nothing
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
-    const uint32_t t0 = threadIdx.x * kRecPerThread;
-    uint64_t sz[kRecPerThread];
-    uint64_t s = 0;
-#pragma unroll
-    for (int j = 0; j < kRecPerThread; ++j) {
-        const uint64_t r = rb + t0 + j;
-        uint64_t size = 0;
-        if (r < a.n) {
-            size = a.fixed_xdr;
-            for (uint32_t d = 0; d < a.ndyn; ++d) {
-                const VField &f = a.f[a.dyn_idx[d]];
-                const uint64_t o0 = f.offsets[r], cnt = f.offsets[r + 1] - o0;
-                ssrc[(size_t)d * kRecPerBlock + t0 + j] = o0;
-                scnt[(size_t)d * kRecPerBlock + t0 + j] = (uint32_t)cnt;
-                size += dyn_xdr_bytes(f, cnt);
-            }
-        }
-        sz[j] = size;
-        s += size;
-    }
-    uint64_t btot;
-    uint64_t off = a.block_sums[blockIdx.x] + block_excl_scan(s, &btot);
-#pragma unroll
-    for (int j = 0; j < kRecPerThread; ++j) {
-        soff[t0 + j] = off;
-        if (a.rec_out && rb + t0 + j < a.n) a.rec_out[rb + t0 + j] = off;
-        off += sz[j];
-    }
-    if (threadIdx.x == kRecThreads - 1) soff[kRecPerBlock] = off;
-    if (a.rec_out && blockIdx.x == 0 && threadIdx.x == 0) a.rec_out[a.n] = total;
-    __syncthreads();
-    uint32_t nrec = (uint32_t)(a.n - rb < kRecPerBlock ? a.n - rb : kRecPerBlock);
-    const uint64_t O0 = soff[0], O1 = soff[nrec];   // entries past nrec hold the end
-    const uint64_t cbase = O0 >> 4, cend = (O1 + 15) >> 4;
-    const uint32_t lsh = lookup_shift(cend - cbase);
-    __shared__ uint32_t tab[kLookup + 1];
-    __shared__ VField sf[kMaxFields];
-    build_lookup(soff, nrec, cbase, lsh, O0, tab);
-    stage_fields(a, sf);
-    __syncthreads();
-    uint8_t *out = a.xdr;
-    for (uint64_t c0 = cbase + threadIdx.x; c0 < cend; c0 += (uint64_t)kRecThreads * kFlatU) {
-        // A: classify kFlatU chunks and issue their fast-path loads
-        u32x4a fv[kFlatU];
-        uint32_t jj[kFlatU];
-        bool fast[kFlatU];
-#pragma unroll
-        for (int u = 0; u < kFlatU; ++u) {
-            const uint64_t c = c0 + (uint64_t)u * kRecThreads;
-            fast[u] = false;
-            jj[u] = 0;
-            if (c >= cend) continue;
-            const uint64_t p = c << 4;
-            const uint64_t q0 = p > O0 ? p : O0;
-            const uint32_t j = lookup_rec(soff, nrec, tab, cbase, lsh, q0);
-            jj[u] = j;
-            if (p < O0 || p + 16 > soff[j + 1]) continue;
-            auto cnt_of = [&](uint32_t d) -> uint64_t { return scnt[(size_t)d * kRecPerBlock + j]; };
-            const Seg g = locate(a, sf, p - soff[j], cnt_of);
-            if (g.kind != SEG_DYN || g.rel < 4 || g.rel + 16 > g.len) continue;
-            const VField &f = sf[g.k];
-            const uint64_t e0 = ssrc[(size_t)g.d * kRecPerBlock + j];
-            const uint64_t b = g.rel - 4;
-            if (f.xsz == 1 && b + 16 <= g.cnt) {
-                const u32x4u v = *(const u32x4u *)(f.data + e0 + b);
-                fv[u].x = v.x; fv[u].y = v.y; fv[u].z = v.z; fv[u].w = v.w;
-                fast[u] = true;
-            } else if (is_word4(f)) {
-                const u32x4a v = *(const u32x4a *)(f.data + (e0 + (b >> 2)) * 4);
-                const bool fl = f.type == XDRG_T_FLOAT;
-                fv[u].x = bswap32r(fl ? canon_f32r(v.x) : v.x); fv[u].y = bswap32r(fl ? canon_f32r(v.y) : v.y);
-                fv[u].z = bswap32r(fl ? canon_f32r(v.z) : v.z); fv[u].w = bswap32r(fl ? canon_f32r(v.w) : v.w);
-                fast[u] = true;
-            }
-        }
-        // B: store; general chunks are assembled dword by dword
-#pragma unroll
-        for (int u = 0; u < kFlatU; ++u) {
-            const uint64_t c = c0 + (uint64_t)u * kRecThreads;
-            if (c >= cend) break;
-            const uint64_t p = c << 4;
-            if (fast[u]) {
-                *(u32x4a *)(out + p) = fv[u];
-                continue;
-            }
-            uint32_t j = jj[u];
-            uint32_t w[4];
-            uint32_t valid = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint64_t q = p + 4 * i;
-                w[i] = 0;
-                if (q < O0 || q >= O1) continue;
-                while (j + 1 < nrec && q >= soff[j + 1]) ++j;
-                auto cnt_j = [&](uint32_t d) -> uint64_t { return scnt[(size_t)d * kRecPerBlock + j]; };
-                const Seg gg = locate(a, sf, q - soff[j], cnt_j);
-                valid |= 1u << i;
-                const uint64_t r = rb + j;
-                if (gg.kind == SEG_MARK) {
-                    w[i] = bswap32r((uint32_t)(soff[j + 1] - soff[j] - 4) | kLastFrag);
-                } else if (gg.kind == SEG_FIXED) {
-                    w[i] = fixed_word(sf[gg.k], r, gg.rel);
-                } else if (gg.kind == SEG_DYN) {
-                    w[i] = dyn_word(sf[gg.k], ssrc[(size_t)gg.d * kRecPerBlock + j], gg.cnt, gg.rel);
-                }
-            }
-            if (valid == 0xf) {
-                u32x4a o; o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
-                *(u32x4a *)(out + p) = o;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (valid & (1u << i)) *(uint32_t *)(out + p + 4 * i) = w[i];
-            }
-        }
-    }
 }
 
 // ---- decode ------------------------------------------------------------------------
@@ -847,542 +622,20 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_sizes_g(const RecArgs a) {
     }
 }
 
-// LDS: sstart[RPB + 2] u64 | snoff[ND][RPB] u64 | scnt[ND][RPB] u32 | supto[RPB] u32
-__host__ __device__ constexpr size_t dec_lds_bytes(uint32_t nd) {
-    return (size_t)(kRecPerBlock + 2) * 8 + (size_t)kRecPerBlock * 4 + (size_t)nd * kRecPerBlock * 12;
-}
-
-__global__ __launch_bounds__(kRecThreads) void k_dec_flat(const RecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint64_t *sstart = (uint64_t *)smem;                         // record start in the stream
-    uint64_t *snoff = sstart + kRecPerBlock + 2;
-    uint32_t *scnt = (uint32_t *)(snoff + (size_t)a.ndyn * kRecPerBlock);
-    uint32_t *supto = scnt + (size_t)a.ndyn * kRecPerBlock;
-    __shared__ uint64_t s_end;
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
-    const uint32_t t0 = threadIdx.x * kRecPerThread;
-    const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
-    const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
-    // live records of the block: validated by k_dec_sizes_g (before `bad`)
-    const uint64_t lim = bad < a.n ? bad : a.n;
-    const uint32_t nlive = (uint32_t)(lim > rb ? (lim - rb < kRecPerBlock ? lim - rb : kRecPerBlock) : 0);
-    for (uint32_t i = threadIdx.x; i < kRecPerBlock; i += kRecThreads) {
-        const bool live = i < nlive;
-        const uint64_t r = rb + i;
-        for (uint32_t d = 0; d < a.ndyn; ++d)
-            scnt[(size_t)d * kRecPerBlock + i] = live ? a.rec_cnt[(uint64_t)d * a.n + r] : 0u;
-        supto[i] = live ? a.nf : 0u;
-        if (live) {
-            const Extent e = rec_extent(a, r);
-            sstart[i] = e.a;
-            if (i + 1 == nlive) s_end = e.b;
-        }
-    }
-    __syncthreads();
-    for (uint32_t d = 0; d < a.ndyn; ++d) {
-        const uint32_t k = a.dyn_idx[d];
-        const VField &f = a.f[k];
-        uint64_t ps = 0;
-#pragma unroll
-        for (int j = 0; j < kRecPerThread; ++j) ps += scnt[(size_t)d * kRecPerBlock + t0 + j];
-        uint64_t btot;
-        uint64_t off = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x] + block_excl_scan(ps, &btot);
-#pragma unroll
-        for (int j = 0; j < kRecPerThread; ++j) {
-            const uint64_t r = rb + t0 + j;
-            const uint64_t c = scnt[(size_t)d * kRecPerBlock + t0 + j];
-            snoff[(size_t)d * kRecPerBlock + t0 + j] = off;
-            if (r < a.n) {
-                f.offsets[r] = off;
-                if (r < bad && off + c > f.cap) {   // native column too small
-                    atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
-                    atomicMin(&supto[t0 + j], k);
-                }
-            }
-            off += c;
-        }
-        if (blockIdx.x == 0 && threadIdx.x == 0) f.offsets[a.n] = a.totals[d];
-    }
-    __syncthreads();
-    if (!nlive) return;
-    const uint64_t I0 = sstart[0], I1 = s_end;
-    const uint64_t cbase = I0 >> 4, cend = (I1 + 15) >> 4;
-    const uint32_t lsh = lookup_shift(cend - cbase);
-    __shared__ uint32_t tab[kLookup + 1];
-    __shared__ VField sf[kMaxFields];
-    build_lookup(sstart, nlive, cbase, lsh, I0, tab);
-    stage_fields(a, sf);
-    __syncthreads();
-    const uint8_t *in = a.xdr;
-    const uint64_t in_words = a.xdr_cap >> 2;
-    for (uint64_t c0 = cbase + threadIdx.x; c0 < cend; c0 += (uint64_t)kRecThreads * kFlatU) {
-        uint32_t w[kFlatU][4];
-        uint32_t jj[kFlatU];
-#pragma unroll
-        for (int u = 0; u < kFlatU; ++u) {   // A: loads and record lookups
-            const uint64_t c = c0 + (uint64_t)u * kRecThreads;
-            jj[u] = 0;
-            if (c >= cend) continue;
-            const uint64_t p = c << 4;
-            if (4 * c + 4 <= in_words) {
-                const u32x4a v = *(const u32x4a *)(in + p);
-                w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    w[u][i] = 4 * c + i < in_words ? *(const uint32_t *)(in + p + 4 * i) : 0u;
-            }
-            jj[u] = lookup_rec(sstart, nlive, tab, cbase, lsh, p > I0 ? p : I0);
-        }
-#pragma unroll
-        for (int u = 0; u < kFlatU; ++u) {   // B: scatter to the native columns
-            const uint64_t c = c0 + (uint64_t)u * kRecThreads;
-            if (c >= cend) break;
-            const uint64_t p = c << 4;
-            uint32_t j = jj[u];
-            const uint64_t rend0 = j + 1 < nlive ? sstart[j + 1] : I1;
-            if (p >= I0 && p + 16 <= rend0) {
-                auto cnt_of = [&](uint32_t d) -> uint64_t { return scnt[(size_t)d * kRecPerBlock + j]; };
-                const Seg g = locate(a, sf, p - sstart[j], cnt_of);
-                if (g.kind == SEG_DYN && g.rel >= 4 && g.rel + 16 <= g.len && g.k < supto[j]) {
-                    const VField &f = sf[g.k];
-                    const uint64_t no = snoff[(size_t)g.d * kRecPerBlock + j];
-                    const uint64_t b = g.rel - 4;
-                    if (f.xsz == 1 && b + 16 <= g.cnt) {
-                        u32x4u o; o.x = w[u][0]; o.y = w[u][1]; o.z = w[u][2]; o.w = w[u][3];
-                        *(u32x4u *)(f.data + no + b) = o;
-                        continue;
-                    }
-                    if (is_word4(f)) {
-                        u32x4a o;
-                        o.x = bswap32r(w[u][0]); o.y = bswap32r(w[u][1]);
-                        o.z = bswap32r(w[u][2]); o.w = bswap32r(w[u][3]);
-                        *(u32x4a *)(f.data + (no + (b >> 2)) * 4) = o;
-                        continue;
-                    }
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint64_t q = p + 4 * i;
-                if (q < I0 || q >= I1) continue;
-                while (j + 1 < nlive && q >= sstart[j + 1]) ++j;
-                auto cnt_j = [&](uint32_t d) -> uint64_t { return scnt[(size_t)d * kRecPerBlock + j]; };
-                const Seg gg = locate(a, sf, q - sstart[j], cnt_j);
-                if (gg.kind == SEG_NONE || gg.kind == SEG_MARK || gg.k >= supto[j]) continue;
-                const uint64_t r = rb + j;
-                if (gg.kind == SEG_FIXED) fixed_store(sf[gg.k], r, gg.rel, w[u][i]);
-                else dyn_store(sf[gg.k], snoff[(size_t)gg.d * kRecPerBlock + j], gg.cnt, gg.rel, w[u][i]);
-            }
-        }
-    }
-}
-
-// ===========================================================================
-// Column-major place kernels (the default for <= kMaxDynLds dynamic fields)
-//
-// Pass R, one thread per record: the small parts of every record — record
-// mark, fixed fields, length words, zero pad (and the rare 2-byte/1-byte/
-// 8-byte dynamic vectors).  Pass C, once per opaque/string/4-byte-vector
-// column: the column's contiguous native range of the block is swept in
-// 16-byte chunks (coalesced on the native side, kFlatU chunks per lane in
-// flight); a chunk finds its record through a coarse LDS table and moves with
-// one unaligned 16-byte access on the XDR side.  Chunks straddling a record
-// boundary (one per record per column) go byte by byte.
-// ===========================================================================
-__device__ __forceinline__ uint32_t chunk_byte(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t i) {
-    const uint32_t w = i < 4 ? w0 : i < 8 ? w1 : i < 12 ? w2 : w3;
-    return (w >> (8 * (i & 3))) & 0xffu;
-}
-__device__ __forceinline__ uint32_t chunk_word(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t i) {
-    return i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
-}
-
-// Table entry e: record holding element max(first element of chunk
-// cbase + (e << sh), lo).
-__device__ __forceinline__ void build_tab(const uint64_t *key, uint32_t n, uint64_t cbase, uint32_t sh,
-                                          uint32_t per_chunk_shift, uint64_t lo, uint32_t *tab) {
-    for (uint32_t e = threadIdx.x; e <= kLookup; e += blockDim.x) {
-        uint64_t q = (cbase + ((uint64_t)e << sh)) << per_chunk_shift;
-        if (q < lo) q = lo;
-        tab[e] = find_rec(key, n, q);
-    }
-}
-__device__ __forceinline__ uint32_t tab_find(const uint64_t *key, uint32_t n, const uint32_t *tab, uint64_t cbase,
-                                             uint32_t sh, uint64_t c, uint64_t q) {
-    const uint64_t e = (c - cbase) >> sh;
-    uint32_t lo = tab[e];
-    uint32_t hi = tab[e + 1] + 1;
-    if (hi > n) hi = n;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (key[mid] <= q) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
-// LDS: soff[RPB + 2] u64 | ssrc[ND][RPB] u64 | scnt[ND][RPB] u32 | spst[ND][RPB] u32
-__host__ __device__ constexpr size_t enc_col_lds_bytes(uint32_t nd) {
-    return (size_t)(kRecPerBlock + 2) * 8 + (size_t)nd * kRecPerBlock * 16;
-}
-
-__global__ __launch_bounds__(kRecThreads) void k_enc_col(const RecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t ND = a.ndyn;
-    uint64_t *soff = (uint64_t *)smem;
-    uint64_t *ssrc = soff + kRecPerBlock + 2;
-    uint32_t *scnt = (uint32_t *)(ssrc + (size_t)ND * kRecPerBlock);
-    uint32_t *spst = scnt + (size_t)ND * kRecPerBlock;
-    __shared__ uint32_t tab[kLookup + 1];
-    __shared__ VField sf[kMaxFields];
-    const uint64_t total = a.totals[0];
-    if (total > a.xdr_cap) return;  // XDRG_E_CAPACITY: write nothing
-    stage_fields(a, sf);
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
-    const uint32_t t0 = threadIdx.x * kRecPerThread;
-    uint64_t sz[kRecPerThread];
-    uint64_t s = 0;
-#pragma unroll
-    for (int j = 0; j < kRecPerThread; ++j) {
-        const uint64_t r = rb + t0 + j;
-        uint64_t pos = 0;
-        if (r < a.n) {
-            pos = a.framed ? 4 : 0;
-            uint32_t d = 0;
-            for (uint32_t k = 0; k < a.nf; ++k) {
-                const VField &f = a.f[k];
-                if (f.kind != XDRG_K_DYNAMIC) { pos += f.xbytes; continue; }
-                const uint64_t o0 = f.offsets[r], cnt = f.offsets[r + 1] - o0;
-                ssrc[(size_t)d * kRecPerBlock + t0 + j] = o0;
-                scnt[(size_t)d * kRecPerBlock + t0 + j] = (uint32_t)cnt;
-                spst[(size_t)d * kRecPerBlock + t0 + j] = (uint32_t)(pos + 4);
-                pos += dyn_xdr_bytes(f, cnt);
-                ++d;
-            }
-        }
-        sz[j] = pos;
-        s += pos;
-    }
-    uint64_t btot;
-    uint64_t off = a.block_sums[blockIdx.x] + block_excl_scan(s, &btot);
-#pragma unroll
-    for (int j = 0; j < kRecPerThread; ++j) {
-        soff[t0 + j] = off;
-        if (a.rec_out && rb + t0 + j < a.n) a.rec_out[rb + t0 + j] = off;
-        off += sz[j];
-    }
-    if (threadIdx.x == kRecThreads - 1) soff[kRecPerBlock] = off;
-    if (a.rec_out && blockIdx.x == 0 && threadIdx.x == 0) a.rec_out[a.n] = total;
-    __syncthreads();
-    const uint32_t nrec = (uint32_t)(a.n - rb < kRecPerBlock ? a.n - rb : kRecPerBlock);
-    uint8_t *out = a.xdr;
-
-    // ---- pass R: marks, fixed fields, length words, pads, rare vectors
-    for (uint32_t j = threadIdx.x; j < nrec; j += kRecThreads) {
-        const uint64_t r = rb + j;
-        uint8_t *base = out + soff[j];
-        uint64_t pos = 0;
-        if (a.framed) {
-            *(uint32_t *)base = bswap32r((uint32_t)(soff[j + 1] - soff[j] - 4) | kLastFrag);
-            pos = 4;
-        }
-        uint32_t d = 0;
-        for (uint32_t k = 0; k < a.nf; ++k) {
-            const VField &f = sf[k];
-            if (f.kind != XDRG_K_DYNAMIC) {
-                const uint32_t nw = f.xbytes >> 2;
-                for (uint32_t i = 0; i < nw; ++i) *(uint32_t *)(base + pos + 4 * i) = fixed_word(f, r, 4 * i);
-                pos += f.xbytes;
-                continue;
-            }
-            const uint64_t cnt = scnt[(size_t)d * kRecPerBlock + j];
-            *(uint32_t *)(base + pos) = bswap32r((uint32_t)cnt);
-            if (f.xsz == 1) {
-                const uint32_t pad = pad4(cnt);
-                for (uint32_t b = 0; b < pad; ++b) base[pos + 4 + cnt + b] = 0;
-            } else if (!is_word4(f)) {
-                const uint64_t e0 = ssrc[(size_t)d * kRecPerBlock + j];
-                const uint64_t nw = cnt * (f.xsz >> 2);
-                for (uint64_t i = 0; i < nw; ++i)
-                    *(uint32_t *)(base + pos + 4 + 4 * i) = dyn_word(f, e0, cnt, 4 + 4 * i);
-            }
-            pos += dyn_xdr_bytes(f, cnt);
-            ++d;
-        }
-    }
-
-    // ---- pass C: one flat sweep per byte / 4-byte-element column
-    uint32_t d = 0;
-    for (uint32_t k = 0; k < a.nf; ++k) {
-        const VField &f = sf[k];
-        if (f.kind != XDRG_K_DYNAMIC) continue;
-        const uint32_t dd = d++;
-        const bool bytes = f.xsz == 1;
-        if (!bytes && !is_word4(f)) continue;
-        const bool fl = f.type == XDRG_T_FLOAT;
-        const uint32_t esh = bytes ? 0 : 2;              // log2 native element size
-        const uint32_t cps = 4 - esh;                    // log2 elements per 16-B chunk
-        const uint64_t *key = ssrc + (size_t)dd * kRecPerBlock;
-        const uint32_t *cn = scnt + (size_t)dd * kRecPerBlock;
-        const uint32_t *ps = spst + (size_t)dd * kRecPerBlock;
-        const uint64_t S0 = key[0], S1 = key[nrec - 1] + cn[nrec - 1];   // elements
-        if (S1 <= S0) continue;
-        const uint64_t cbase = S0 >> cps, cend = (S1 + (1u << cps) - 1) >> cps;
-        const uint32_t lsh = lookup_shift(cend - cbase);
-        __syncthreads();   // previous column's table readers are done
-        build_tab(key, nrec, cbase, lsh, cps, S0, tab);
-        __syncthreads();
-        const uint8_t *col = f.data;
-        for (uint64_t c0 = cbase + threadIdx.x; c0 < cend; c0 += (uint64_t)kRecThreads * kFlatU) {
-            uint32_t w[kFlatU][4];
-            uint32_t jj[kFlatU];
-            bool full[kFlatU];
-#pragma unroll
-            for (int u = 0; u < kFlatU; ++u) {   // A: native loads + record lookup
-                const uint64_t c = c0 + (uint64_t)u * kRecThreads;
-                full[u] = false;
-                jj[u] = 0;
-                if (c >= cend) continue;
-                const uint64_t e = c << cps;
-                full[u] = e >= S0 && e + (1u << cps) <= S1;
-                const uint8_t *src = col + (c << 4);
-                if (full[u]) {
-                    const u32x4u v = *(const u32x4u *)src;
-                    w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
-                } else {   // edge chunk: only bytes of [S0, S1) are read
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) w[u][i] = 0;
-                    for (uint32_t b = 0; b < 16; ++b) {
-                        const uint64_t x = ((c << 4) + b) >> esh;
-                        if (x >= S0 && x < S1) w[u][b >> 2] |= (uint32_t)src[b] << (8 * (b & 3));
-                    }
-                }
-                jj[u] = tab_find(key, nrec, tab, cbase, lsh, c, e > S0 ? e : S0);
-            }
-#pragma unroll
-            for (int u = 0; u < kFlatU; ++u) {   // B: XDR stores
-                const uint64_t c = c0 + (uint64_t)u * kRecThreads;
-                if (c >= cend) break;
-                const uint64_t e = c << cps;
-                uint32_t j = jj[u];
-                if (full[u] && key[j] <= e && e + (1u << cps) <= key[j] + cn[j]) {
-                    uint8_t *dst = out + soff[j] + ps[j] + ((e - key[j]) << esh);
-                    if (bytes) {
-                        u32x4u o; o.x = w[u][0]; o.y = w[u][1]; o.z = w[u][2]; o.w = w[u][3];
-                        *(u32x4u *)dst = o;
-                    } else {
-                        u32x4a o;
-                        o.x = bswap32r(fl ? canon_f32r(w[u][0]) : w[u][0]);
-                        o.y = bswap32r(fl ? canon_f32r(w[u][1]) : w[u][1]);
-                        o.z = bswap32r(fl ? canon_f32r(w[u][2]) : w[u][2]);
-                        o.w = bswap32r(fl ? canon_f32r(w[u][3]) : w[u][3]);
-                        *(u32x4a *)dst = o;
-                    }
-                    continue;
-                }
-                // boundary chunk: element by element into each record's run
-                const uint64_t lo_c = e > S0 ? e : S0;
-                const uint64_t hi_c = e + (1u << cps) < S1 ? e + (1u << cps) : S1;
-                for (uint64_t x = lo_c; x < hi_c; ++x) {
-                    while (j + 1 < nrec && key[j] + cn[j] <= x) ++j;
-                    if (x < key[j] || x >= key[j] + cn[j]) continue;
-                    uint8_t *dst = out + soff[j] + ps[j] + ((x - key[j]) << esh);
-                    const uint32_t i = (uint32_t)(x - e);
-                    if (bytes) {
-                        *dst = (uint8_t)chunk_byte(w[u][0], w[u][1], w[u][2], w[u][3], i);
-                    } else {
-                        const uint32_t v = chunk_word(w[u][0], w[u][1], w[u][2], w[u][3], i);
-                        *(uint32_t *)dst = bswap32r(fl ? canon_f32r(v) : v);
-                    }
-                }
-            }
-        }
-    }
-}
-
-// LDS: sstart[RPB + 2] u64 | snoff[ND][RPB] u64 | scnt[ND][RPB] u32 | spst[ND][RPB] u32 | supto[RPB] u32
-__host__ __device__ constexpr size_t dec_col_lds_bytes(uint32_t nd) {
-    return (size_t)(kRecPerBlock + 2) * 8 + (size_t)kRecPerBlock * 4 + (size_t)nd * kRecPerBlock * 16;
-}
-
-__global__ __launch_bounds__(kRecThreads) void k_dec_col(const RecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t ND = a.ndyn;
-    uint64_t *sstart = (uint64_t *)smem;
-    uint64_t *snoff = sstart + kRecPerBlock + 2;
-    uint32_t *scnt = (uint32_t *)(snoff + (size_t)ND * kRecPerBlock);
-    uint32_t *spst = scnt + (size_t)ND * kRecPerBlock;
-    uint32_t *supto = spst + (size_t)ND * kRecPerBlock;
-    __shared__ uint32_t tab[kLookup + 1];
-    __shared__ VField sf[kMaxFields];
-    stage_fields(a, sf);
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
-    const uint32_t t0 = threadIdx.x * kRecPerThread;
-    const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
-    const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
-    const uint64_t lim = bad < a.n ? bad : a.n;
-    const uint32_t nlive = (uint32_t)(lim > rb ? (lim - rb < kRecPerBlock ? lim - rb : kRecPerBlock) : 0);
-    for (uint32_t i = threadIdx.x; i < kRecPerBlock; i += kRecThreads) {
-        const bool live = i < nlive;
-        const uint64_t r = rb + i;
-        uint64_t pos = a.framed ? 4 : 0;
-        uint32_t d = 0;
-        for (uint32_t k = 0; k < a.nf; ++k) {
-            const VField &f = a.f[k];
-            if (f.kind != XDRG_K_DYNAMIC) { pos += f.xbytes; continue; }
-            const uint64_t c = live ? a.rec_cnt[(uint64_t)d * a.n + r] : 0u;
-            scnt[(size_t)d * kRecPerBlock + i] = (uint32_t)c;
-            spst[(size_t)d * kRecPerBlock + i] = (uint32_t)(pos + 4);
-            pos += dyn_xdr_bytes(f, c);
-            ++d;
-        }
-        supto[i] = live ? a.nf : 0u;
-        if (live) sstart[i] = rec_extent(a, r).a;
-    }
-    __syncthreads();
-    for (uint32_t d = 0; d < ND; ++d) {
-        const uint32_t k = a.dyn_idx[d];
-        const VField &f = a.f[k];
-        uint64_t pss = 0;
-#pragma unroll
-        for (int j = 0; j < kRecPerThread; ++j) pss += scnt[(size_t)d * kRecPerBlock + t0 + j];
-        uint64_t btot;
-        uint64_t off = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x] + block_excl_scan(pss, &btot);
-#pragma unroll
-        for (int j = 0; j < kRecPerThread; ++j) {
-            const uint64_t r = rb + t0 + j;
-            const uint64_t c = scnt[(size_t)d * kRecPerBlock + t0 + j];
-            snoff[(size_t)d * kRecPerBlock + t0 + j] = off;
-            if (r < a.n) {
-                f.offsets[r] = off;
-                if (r < bad && off + c > f.cap) {   // native column too small
-                    atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
-                    atomicMin(&supto[t0 + j], k);
-                }
-            }
-            off += c;
-        }
-        if (blockIdx.x == 0 && threadIdx.x == 0) f.offsets[a.n] = a.totals[d];
-    }
-    __syncthreads();
-    if (!nlive) return;
-    const uint8_t *in = a.xdr;
-
-    // ---- pass R: fixed fields and the rare 2/1/8-byte dynamic vectors
-    for (uint32_t j = threadIdx.x; j < nlive; j += kRecThreads) {
-        const uint64_t r = rb + j;
-        const uint8_t *base = in + sstart[j];
-        uint64_t pos = a.framed ? 4 : 0;
-        uint32_t d = 0;
-        const uint32_t upto = supto[j];
-        for (uint32_t k = 0; k < upto; ++k) {
-            const VField &f = sf[k];
-            if (f.kind != XDRG_K_DYNAMIC) {
-                const uint32_t nw = f.xbytes >> 2;
-                for (uint32_t i = 0; i < nw; ++i) fixed_store(f, r, 4 * i, *(const uint32_t *)(base + pos + 4 * i));
-                pos += f.xbytes;
-                continue;
-            }
-            const uint64_t cnt = scnt[(size_t)d * kRecPerBlock + j];
-            if (f.xsz != 1 && !is_word4(f)) {
-                const uint64_t no = snoff[(size_t)d * kRecPerBlock + j];
-                const uint64_t nw = cnt * (f.xsz >> 2);
-                for (uint64_t i = 0; i < nw; ++i)
-                    dyn_store(f, no, cnt, 4 + 4 * i, *(const uint32_t *)(base + pos + 4 + 4 * i));
-            }
-            pos += dyn_xdr_bytes(f, cnt);
-            ++d;
-        }
-    }
-
-    // ---- pass C: one flat sweep per byte / 4-byte-element native column
-    uint32_t d = 0;
-    for (uint32_t k = 0; k < a.nf; ++k) {
-        const VField &f = sf[k];
-        if (f.kind != XDRG_K_DYNAMIC) continue;
-        const uint32_t dd = d++;
-        const bool bytes = f.xsz == 1;
-        if (!bytes && !is_word4(f)) continue;
-        const uint32_t esh = bytes ? 0 : 2;
-        const uint32_t cps = 4 - esh;
-        const uint64_t *key = snoff + (size_t)dd * kRecPerBlock;
-        const uint32_t *cn = scnt + (size_t)dd * kRecPerBlock;
-        const uint32_t *ps = spst + (size_t)dd * kRecPerBlock;
-        const uint64_t N0 = key[0];
-        uint64_t N1 = key[nlive - 1] + cn[nlive - 1];
-        if (N1 > f.cap) N1 = f.cap;            // records past capacity are excluded below
-        if (N1 <= N0) continue;
-        const uint64_t cbase = N0 >> cps, cend = (N1 + (1u << cps) - 1) >> cps;
-        const uint32_t lsh = lookup_shift(cend - cbase);
-        __syncthreads();
-        build_tab(key, nlive, cbase, lsh, cps, N0, tab);
-        __syncthreads();
-        uint8_t *col = f.data;
-        for (uint64_t c0 = cbase + threadIdx.x; c0 < cend; c0 += (uint64_t)kRecThreads * kFlatU) {
-            uint32_t w[kFlatU][4];
-            uint32_t jj[kFlatU];
-            bool fast[kFlatU];
-#pragma unroll
-            for (int u = 0; u < kFlatU; ++u) {   // A: lookup + XDR loads
-                const uint64_t c = c0 + (uint64_t)u * kRecThreads;
-                fast[u] = false;
-                jj[u] = 0;
-                if (c >= cend) continue;
-                const uint64_t e = c << cps;
-                const uint32_t j = tab_find(key, nlive, tab, cbase, lsh, c, e > N0 ? e : N0);
-                jj[u] = j;
-                if (e >= N0 && e + (1u << cps) <= N1 && key[j] <= e && e + (1u << cps) <= key[j] + cn[j] &&
-                    k < supto[j]) {
-                    const uint8_t *src = in + sstart[j] + ps[j] + ((e - key[j]) << esh);
-                    if (bytes) {
-                        const u32x4u v = *(const u32x4u *)src;
-                        w[u][0] = v.x; w[u][1] = v.y; w[u][2] = v.z; w[u][3] = v.w;
-                    } else {
-                        const u32x4a v = *(const u32x4a *)src;
-                        w[u][0] = bswap32r(v.x); w[u][1] = bswap32r(v.y);
-                        w[u][2] = bswap32r(v.z); w[u][3] = bswap32r(v.w);
-                    }
-                    fast[u] = true;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kFlatU; ++u) {   // B: native stores
-                const uint64_t c = c0 + (uint64_t)u * kRecThreads;
-                if (c >= cend) break;
-                uint8_t *dst = col + (c << 4);
-                if (fast[u]) {
-                    u32x4u o; o.x = w[u][0]; o.y = w[u][1]; o.z = w[u][2]; o.w = w[u][3];
-                    *(u32x4u *)dst = o;
-                    continue;
-                }
-                const uint64_t e = c << cps;
-                uint32_t j = jj[u];
-                const uint64_t lo_c = e > N0 ? e : N0;
-                const uint64_t hi_c = e + (1u << cps) < N1 ? e + (1u << cps) : N1;
-                for (uint64_t x = lo_c; x < hi_c; ++x) {
-                    while (j + 1 < nlive && key[j] + cn[j] <= x) ++j;
-                    if (x < key[j] || x >= key[j] + cn[j] || k >= supto[j]) continue;
-                    const uint8_t *src = in + sstart[j] + ps[j] + ((x - key[j]) << esh);
-                    if (bytes) dst[x - e] = *src;
-                    else *(uint32_t *)(dst + ((x - e) << 2)) = bswap32r(*(const uint32_t *)src);
-                }
-            }
-        }
-    }
-}
-
 // ===========================================================================
 // Group-per-record place kernels (the default; field-major)
 //
-// Phase 1 as in the flat kernels (metadata in LDS).  Phase 2 walks the fields
+// Phase 1, one thread per kRecPerThread records: sizes / counts, block scan,
+// and every record's metadata (stream offset, dynamic counts, native offsets)
+// staged in LDS.  Phase 2 walks the fields
 // in schema order; for each field every record of the block is handled by a
 // group of G lanes, G (1..64) chosen per field from that field's average size
 // in the block.  Opaque/string fields move as one blob [length][payload][zero
 // pad] in 16-byte chunks, kCopyU chunks per lane in flight, realigned with
 // v_alignbyte_b32 so every global access is dword-aligned.  Measured on
-// MI355X this beat the flat and column-major kernels on configs 3 and 4
-// (DESIGN.md §5.3).
+// MI355X this beat a flat (output-stationary chunk sweep), a column-major, a
+// segment-table and a lane-per-record design on configs 3 and 4 (DESIGN.md
+// §5.3).
 // ===========================================================================
 __device__ __forceinline__ uint32_t mask_bytes(uint32_t v, int64_t valid) {
     if (valid >= 4) return v;
@@ -2040,11 +1293,11 @@ __global__ void k_debug_recargs(const RecArgs a) {
 // copy unroll of the group kernels (tools/tune_rec.py; set_tuning keys 4 and 5)
 static int g_enc_u = 2, g_dec_u = 2;
 static uint32_t g_force_g = 0;
-static int g_rec_kernel = 0;   // 0 = group per record (default), 1 = flat, 2 = column-major, 3 = lane per record
+static int g_rec_kernel = 0;   // 0 = group per record (default), 3 = lane per record
 static uint32_t g_lane_bytes_enc = 32, g_lane_bytes_dec = 32;
 int set_rec_tuning(int key, long long value) {
     if (key == 9) {
-        if (value < 0 || value > 3) return -1;
+        if (value != 0 && value != 3) return -1;
         g_rec_kernel = (int)value;
         return 0;
     }
@@ -2084,9 +1337,7 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
         if (grp && g_rec_kernel == 3) {
             hipLaunchKernelGGL(k_enc_lane, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
-            if (g_rec_kernel == 1) hipLaunchKernelGGL(k_enc_flat, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
-            else if (g_rec_kernel == 2) hipLaunchKernelGGL(k_enc_col, dim3(nb), dim3(kRecThreads), enc_col_lds_bytes(a.ndyn), st, a);
-            else if (g_enc_u == 1) hipLaunchKernelGGL(k_enc_place_g<1>, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
+            if (g_enc_u == 1) hipLaunchKernelGGL(k_enc_place_g<1>, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
             else hipLaunchKernelGGL(k_enc_place_g<2>, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
         }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
@@ -2104,9 +1355,7 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
         if (grp && g_rec_kernel == 3) {
             hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
-            if (g_rec_kernel == 1) hipLaunchKernelGGL(k_dec_flat, dim3(nb), dim3(kRecThreads), dec_lds_bytes(a.ndyn), st, a);
-            else if (g_rec_kernel == 2) hipLaunchKernelGGL(k_dec_col, dim3(nb), dim3(kRecThreads), dec_col_lds_bytes(a.ndyn), st, a);
-            else if (g_dec_u == 1) hipLaunchKernelGGL(k_dec_place_g<1>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+            if (g_dec_u == 1) hipLaunchKernelGGL(k_dec_place_g<1>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
             else hipLaunchKernelGGL(k_dec_place_g<2>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
         }
         else hipLaunchKernelGGL(k_dec_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
