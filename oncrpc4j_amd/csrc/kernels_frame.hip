@@ -11,14 +11,14 @@
 // every 4-byte position of the stream (fragment sizes are multiples of 4 in
 // XDR traffic; a stream whose real chain meets another size falls back to
 // the exact serial walk):
-//   L1  k_frame_l1     per 4 KiB chunk, in LDS: every word position's exit =
-//                      first chain position at or past the chunk end (10
+//   L1  k_frame_l1     per 16 KiB chunk, in LDS: every word position's exit =
+//                      first chain position at or past the chunk end (12
 //                      rounds of pointer jumping).
-//   L2  k_frame_l2 x8  per 1 MiB super-chunk, in HBM: pointer doubling of the
-//                      L1 exits (a hop crosses >= 1 chunk, so 8 rounds).
+//   L2  k_frame_l2 x6  per 1 MiB super-chunk, in HBM: pointer doubling of the
+//                      L1 exits (a hop crosses >= 1 chunk, so 6 rounds).
 //   L3  k_frame_fix    one lane hops super-chunk to super-chunk from offset 0
 //                      (<= len / 1 MiB dependent loads), k_frame_entries one
-//                      lane per super-chunk hops its chunks (<= 256), giving
+//                      lane per super-chunk hops its chunks (<= 64), giving
 //                      every chunk's true entry; k_frame_count/emit walk each
 //                      chunk's own marks in parallel.
 // Fragments are then grouped into messages with two scans (rocPRIM) and the
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void k_frame_l1(const uint32_t *w, uint64_t le
         J[i] = q < Q ? frag_next(w, len, q) : kFStop;
     }
     __syncthreads();
-    for (int round = 0; round < 10; ++round) {   // chains inside a chunk have <= 1024 hops
+    for (int round = 0; round < kFChunkLog2; ++round) {   // chains inside a chunk have <= kFChunk hops
         uint32_t v[kFChunk / 256];
 #pragma unroll
         for (int k = 0; k < kFChunk / 256; ++k) {
@@ -151,10 +151,24 @@ __global__ void k_frame_serial(const uint8_t *in, uint64_t len, uint64_t *frag_p
     res[0] = n;
 }
 
-// Complete fragments end with the last LAST mark: res[1] = its index + 1.
-__global__ void k_frame_lastmsg(const uint32_t *frag_mark, uint64_t nfrag, unsigned long long *res) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nfrag && (frag_mark[i] & kLastFrag)) atomicMax(res, (unsigned long long)(i + 1));
+// Complete fragments end with the last LAST mark: res[1] = its index + 1
+// (grid-stride max, one atomic per block).
+__global__ __launch_bounds__(256) void k_frame_lastmsg(const uint32_t *frag_mark, uint64_t nfrag,
+                                                        unsigned long long *res) {
+    __shared__ unsigned long long wmax[4];
+    unsigned long long m = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nfrag; i += (uint64_t)gridDim.x * blockDim.x)
+        if (frag_mark[i] & kLastFrag) m = i + 1;
+    for (int d = 32; d > 0; d >>= 1) {
+        const unsigned long long o = __shfl_down(m, d, 64);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) m = wmax[w] > m ? wmax[w] : m;
+        if (m) atomicMax(res, m);
+    }
 }
 
 // Per-fragment scan inputs: body size and last flag.
@@ -185,25 +199,27 @@ __global__ void k_frame_msgs(const uint64_t *frag_pos, const uint32_t *frag_mark
     }
 }
 
-// One wave per fragment copies its body (4-byte aligned on both sides on the
-// fast path; bytes on the fallback path).
+// A group of G lanes per fragment copies its body (G sized by the host from
+// the average fragment): 16-byte accesses (dword-aligned, so unaligned
+// vectors on gfx950) with a dword tail; byte copies on the fallback path.
+typedef uint32_t u32x4f __attribute__((ext_vector_type(4), aligned(4)));
 __global__ __launch_bounds__(256) void k_frame_copy(const uint8_t *in, const uint64_t *frag_pos,
                                                      const uint32_t *frag_mark, const uint64_t *pay_off,
                                                      const uint32_t *msg_id, uint64_t nf, uint64_t cap,
-                                                     uint8_t *payload) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t f = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; f < nf; f += nwaves) {
+                                                     uint32_t G, uint8_t *payload) {
+    const uint32_t gl = threadIdx.x & (G - 1);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x / G);
+    for (uint64_t f = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; f < nf; f += ngroups) {
         if (msg_id[f] >= cap) return;   // fragments are in message order
         const uint8_t *src = in + frag_pos[f] + 4;
         uint8_t *dst = payload + pay_off[f];
         const uint64_t n = frag_mark[f] & kSizeMask;
         if ((((uintptr_t)src | (uintptr_t)dst | n) & 3) == 0) {
-            const uint32_t *s = (const uint32_t *)src;
-            uint32_t *d = (uint32_t *)dst;
-            for (uint64_t i = lane; i < n / 4; i += 64) d[i] = s[i];
+            const uint64_t nv = n >> 4;
+            for (uint64_t i = gl; i < nv; i += G) *(u32x4f *)(dst + 16 * i) = *(const u32x4f *)(src + 16 * i);
+            for (uint64_t i = 4 * nv + gl; i < n / 4; i += G) ((uint32_t *)dst)[i] = ((const uint32_t *)src)[i];
         } else {
-            for (uint64_t i = lane; i < n; i += 64) dst[i] = src[i];
+            for (uint64_t i = gl; i < n; i += G) dst[i] = src[i];
         }
     }
 }
@@ -216,7 +232,7 @@ int frame_levels(const uint8_t *in, uint64_t len, FrameWs &ws, void *stream) {
     const uint32_t *w = (const uint32_t *)in;
     const uint64_t Q = len / 4, nch = (Q + kFChunk - 1) / kFChunk, nsup = (Q + kFSuper - 1) / kFSuper;
     hipLaunchKernelGGL(k_frame_l1, dim3((uint32_t)nch), dim3(256), 0, st, w, len, Q, ws.exit1, ws.exit2);
-    for (int r = 0; r < 8; ++r) hipLaunchKernelGGL(k_frame_l2, grid1(Q, 256), dim3(256), 0, st, ws.exit2, Q);
+    for (uint32_t r = 0; r < kFSuperLog2; ++r) hipLaunchKernelGGL(k_frame_l2, grid1(Q, 256), dim3(256), 0, st, ws.exit2, Q);
     if (hipMemsetAsync(ws.sentry, 0xff, nsup * 4, st) != hipSuccess) return (int)hipErrorUnknown;
     if (hipMemsetAsync(ws.centry, 0xff, nch * 4, st) != hipSuccess) return (int)hipErrorUnknown;
     hipLaunchKernelGGL(k_frame_fix, dim3(1), dim3(64), 0, st, ws.exit2, Q, ws.sentry, ws.res);
@@ -250,7 +266,9 @@ int frame_serial(const uint8_t *in, uint64_t len, FrameWs &ws, void *stream) {
 int frame_last(FrameWs &ws, uint64_t nfrag, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(ws.res + 1, 0, 8, st) != hipSuccess) return (int)hipErrorUnknown;
-    if (nfrag) hipLaunchKernelGGL(k_frame_lastmsg, grid1(nfrag, 256), dim3(256), 0, st, ws.frag_mark, nfrag,
+    uint64_t blocks = (nfrag + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (nfrag) hipLaunchKernelGGL(k_frame_lastmsg, dim3((uint32_t)blocks), dim3(256), 0, st, ws.frag_mark, nfrag,
                                   (unsigned long long *)ws.res + 1);
     return (int)hipGetLastError();
 }
@@ -272,10 +290,15 @@ int frame_messages(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, bo
     return (int)hipGetLastError();
 }
 
-int frame_copy(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, uint8_t *payload, void *stream) {
-    const uint64_t blocks = (nf + 3) / 4 < 65536 ? (nf + 3) / 4 : 65536;   // 4 waves per block, grid-stride
+int frame_copy(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, uint64_t payload_bytes, uint8_t *payload,
+               void *stream) {
+    uint32_t G = 1;   // lanes per fragment: ~16 bytes per lane for the average fragment
+    while (G < 64 && 16ull * G * nf < payload_bytes) G <<= 1;
+    uint64_t blocks = (nf + 256 / G - 1) / (256 / G);
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_frame_copy, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, in, ws.frag_pos,
-                       ws.frag_mark, ws.pay_off, ws.msg_id, nf, cap, payload);
+                       ws.frag_mark, ws.pay_off, ws.msg_id, nf, cap, G, payload);
     return (int)hipGetLastError();
 }
 

@@ -795,7 +795,7 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
             if (consumed) *consumed = c->h_stat[2];
             return XDRG_E_CAPACITY;
         }
-        HIPCHK(c, (hipError_t)frame_copy(in, ws, nf, cap, payload, c->stream));
+        HIPCHK(c, (hipError_t)frame_copy(in, ws, nf, cap, c->h_stat[2], payload, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     return nout ? XDRG_OK : XDRG_E_INCOMPLETE;

@@ -158,8 +158,10 @@ int launch_finalize(const unsigned long long *errkey, unsigned long long extra_k
                     uint64_t *first_bad, int *err, void *stream);
 
 // ---- parallel record-mark walk (kernels_frame.hip) ------------------------
-constexpr uint32_t kFChunk = 1024;            // words per level-1 chunk (4 KiB of stream)
-constexpr uint32_t kFSuper = kFChunk * 256;   // words per super-chunk (1 MiB)
+constexpr uint32_t kFChunkLog2 = 12;
+constexpr uint32_t kFChunk = 1u << kFChunkLog2;      // words per level-1 chunk (16 KiB of stream)
+constexpr uint32_t kFSuperLog2 = 6;                  // level-1 chunks per super-chunk, log2
+constexpr uint32_t kFSuper = kFChunk << kFSuperLog2; // words per super-chunk (1 MiB)
 constexpr uint32_t kFStop = 0xffffffffu;      // chain ends: fragment not fully received
 constexpr uint32_t kFUnal = 0xfffffffeu;      // chain meets a size % 4 != 0 (serial fallback)
 constexpr uint32_t kFNone = 0xffffffffu;      // no entry
@@ -185,7 +187,8 @@ int frame_last(FrameWs &ws, uint64_t nfrag, void *stream);
 // payload (bodies back to back); res[3] = stream bytes of messages < cap.
 int frame_messages(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, bool stream_offsets,
                    uint64_t *msg_offsets, void *stream);
-int frame_copy(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, uint8_t *payload, void *stream);
+int frame_copy(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, uint64_t payload_bytes, uint8_t *payload,
+               void *stream);
 
 // ---- multi-GPU exchange (kernels_multi.hip) -------------------------------
 constexpr int kMaxGatherSeg = 16;
