@@ -281,6 +281,18 @@ class Workload:
         ctx.decode(self.sch, self.xdr, self.xlen, self.n, self.cout, rec_offsets=self.rec_offsets,
                    framed=self.framed, async_=True)
 
+    def clear_outputs(self):
+        """Zero the XDR stream and every decode target (tools/tune_*.py: each
+        kernel variant must round-trip on its own writes)."""
+        self.xdr.zero_()
+        if self.cfg == 2:
+            self.back.zero_()
+            return
+        self.hdr_back.zero_()
+        for _, _, vb, ob in self.dyn:
+            vb.zero_()
+            ob.zero_()
+
     def check(self):
         import torch
         if self.cfg == 2:

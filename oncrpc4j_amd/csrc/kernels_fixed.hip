@@ -461,7 +461,9 @@ int launch_stream_words(const StreamArgs &a, int variant, void *stream) {
 }
 
 // key 1: unroll (1/2/4/8), key 2: nontemporal bits, key 3: blocks per CU (0 = one pass),
-// keys 4/5: record-path encode/decode copy unroll (1/2/4)
+// keys 4/5: record-path encode/decode copy unroll (1/2/4), 6-9: record-path
+// group sizing / kernel choice, 10/11: record-path records per lane in flight,
+// 12: staged record kernels LDS tile bytes, 13: staged/group split (bytes per record)
 int set_tuning(int key, long long value) {
     switch (key) {
     case 1:
@@ -470,7 +472,7 @@ int set_tuning(int key, long long value) {
         return 0;
     case 2: g_stream_nt = (int)(value & 3); return 0;
     case 3: if (value < 0) return -1; g_stream_blocks_per_cu = (int)value; return 0;
-    case 4: case 5: case 6: case 7: case 8: case 9: return set_rec_tuning(key, value);
+    case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12: case 13: return set_rec_tuning(key, value);
     default: return -1;
     }
 }

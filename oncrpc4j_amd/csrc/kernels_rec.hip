@@ -651,173 +651,276 @@ __device__ __forceinline__ uint32_t pow2_lanes(uint64_t bytes_per_rec, uint32_t 
     return g;
 }
 
-// One opaque/string field as one blob: [BE length][payload][zero pad] (Xdr.java:776-800).
-template <int kCopyU>
-__device__ __forceinline__ void enc_blob_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
-                                               uint64_t cnt, uint32_t G, uint32_t gl) {
-    const uint64_t nwb = 1 + ((cnt + 3) >> 2), nch = (nwb + 3) >> 2;
-    const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
-    const uint8_t *sa = src - sh;
-    const uint8_t *end = src + cnt;
-    const uint32_t lenw = bswap32r((uint32_t)cnt);
-    for (uint64_t c0 = gl; c0 < nch; c0 += (uint64_t)G * kCopyU) {
-        Chunk5 ch[kCopyU];
+// ---- 16-byte chunk helpers ---------------------------------------------------
+// A lane moves one 16-byte chunk of a record's field at a time.  The copy
+// loops keep U chunks of each of R records (R iterations of the group's
+// record loop) in flight per lane: every load of an iteration is issued
+// unconditionally, before any value is used, so the wave waits once per
+// iteration instead of once per load.  (Loads guarded by per-lane
+// conditions were each followed by their own s_waitcnt vmcnt(0), one
+// outstanding load per wave)
+//
+// A Span is the 4-aligned extent [loA, endA) holding a source's valid bytes
+// (a native column or the XDR stream).  A chunk reads a 20-byte window at a
+// 4-aligned address w; the load is clamped into [loA, hi = endA - 20] so it
+// never touches a page without valid bytes.  Windows that had to be clamped
+// (the first/last chunks of a span, or a span shorter than 20 bytes: then
+// every load reads `dummy`, any 20 readable bytes) are re-read word by word
+// after all loads of the iteration are in flight.  Bytes a window holds
+// beyond its record belong to neighbouring records and are masked on store.
+struct Span {
+    const uint8_t *loA, *endA, *hi, *dummy;
+};
+__device__ __forceinline__ Span make_span(const uint8_t *first, const uint8_t *end, const uint8_t *dummy) {
+    Span s;
+    s.loA = (const uint8_t *)((uintptr_t)first & ~(uintptr_t)3);
+    s.endA = (const uint8_t *)(((uintptr_t)end + 3) & ~(uintptr_t)3);
+    s.hi = (uintptr_t)s.endA >= (uintptr_t)s.loA + 20 ? s.endA - 20 : nullptr;
+    s.dummy = dummy;
+    return s;
+}
+__device__ __forceinline__ const uint8_t *span_clamp(const Span &s, const uint8_t *w) {
+    if (!s.hi) return s.dummy;
+    return w < s.loA ? s.loA : (w > s.hi ? s.hi : w);
+}
+__device__ __forceinline__ uint32_t span_word(const Span &s, const uint8_t *a) {
+    return (a >= s.loA && a < s.endA) ? *(const uint32_t *)a : 0u;
+}
+// Unconditional window load (+ the fifth word when five are needed).
+__device__ __forceinline__ void win_load(Chunk5 &q, const Span &s, const uint8_t *w, bool five) {
+    const uint8_t *pa = span_clamp(s, w);
+    const u32x4a v = *(const u32x4a *)pa;
+    q.q0 = v.x; q.q1 = v.y; q.q2 = v.z; q.q3 = v.w;
+    q.q4 = five ? *(const uint32_t *)(pa + 16) : 0u;
+}
+// After the wait: redo a clamped window word by word.
+__device__ __forceinline__ void win_fix(Chunk5 &q, const Span &s, const uint8_t *w, bool five) {
+    if (span_clamp(s, w) == w) return;
+    q.q0 = span_word(s, w); q.q1 = span_word(s, w + 4);
+    q.q2 = span_word(s, w + 8); q.q3 = span_word(s, w + 12);
+    q.q4 = five ? span_word(s, w + 16) : 0u;
+}
+
+// Blob [BE length][payload][zero pad] of an opaque/string field
+// (Xdr.java:776-800): chunk c covers blob bytes [16c, 16c + 16).  The
+// payload starts at src (any alignment, sh = src & 3); q0..q4 are the words
+// at src - sh + 16c - 4 + 4m.
+__device__ __forceinline__ const uint8_t *blob_win(const uint8_t *src, uint64_t c) {
+    return src - ((uintptr_t)src & 3) + 16 * c - 4;
+}
+__device__ __forceinline__ void blob_store(uint8_t *dst, const Chunk5 &q, uint32_t sh, uint64_t c, uint64_t cnt) {
+    const uint64_t nwb = 1 + ((cnt + 3) >> 2);
+    uint32_t o0 = sh ? __builtin_amdgcn_alignbyte(q.q1, q.q0, sh) : q.q0;
+    uint32_t o1 = sh ? __builtin_amdgcn_alignbyte(q.q2, q.q1, sh) : q.q1;
+    uint32_t o2 = sh ? __builtin_amdgcn_alignbyte(q.q3, q.q2, sh) : q.q2;
+    uint32_t o3 = sh ? __builtin_amdgcn_alignbyte(q.q4, q.q3, sh) : q.q3;
+    const int64_t rem = 4 + (int64_t)cnt - 16 * (int64_t)c;   // blob bytes from chunk start
+    if (rem < 16) {   // zero pad (Xdr.java:765)
+        o0 = mask_bytes(o0, rem); o1 = mask_bytes(o1, rem - 4);
+        o2 = mask_bytes(o2, rem - 8); o3 = mask_bytes(o3, rem - 12);
+    }
+    if (c == 0) o0 = bswap32r((uint32_t)cnt);
+    uint8_t *d = dst + 16 * c;
+    if (4 * c + 4 <= nwb) {
+        u32x4a o; o.x = o0; o.y = o1; o.z = o2; o.w = o3;
+        *(u32x4a *)d = o;
+    } else {
+        const uint64_t left = nwb - 4 * c;
+        *(uint32_t *)d = o0;
+        if (left > 1) *(uint32_t *)(d + 4) = o1;
+        if (left > 2) *(uint32_t *)(d + 8) = o2;
+    }
+}
+
+// Chunk index a slot loads: inactive slots (c >= nch) re-read their
+// record's last chunk (a line the active slots fetch anyway).
+__device__ __forceinline__ uint64_t ld_chunk(uint64_t c, uint64_t nch) {
+    return c < nch ? c : (nch ? nch - 1 : 0);
+}
+
+// Chunks of R opaque/string blobs; nch[r] = 0 marks an unused slot.
+template <int U, int R>
+__device__ __forceinline__ void enc_blob_bytes(uint8_t *const (&dst)[R], const uint8_t *const (&src)[R],
+                                               const uint64_t (&cnt)[R], const uint64_t (&nch)[R],
+                                               const Span &sp, uint32_t G, uint32_t gl) {
+    uint64_t mx = 0;
 #pragma unroll
-        for (int u = 0; u < kCopyU; ++u) {
-            const uint64_t c = c0 + (uint64_t)u * G;
-            if (c >= nch) continue;
-            const uint8_t *p = sa + 16 * c;   // words at p - 4 + 4m, m = 0..4
-            if (c > 0 && p + 16 <= end) {
-                const u32x4a v = *(const u32x4a *)(p - 4);
-                ch[u].q0 = v.x; ch[u].q1 = v.y; ch[u].q2 = v.z; ch[u].q3 = v.w;
-                ch[u].q4 = sh ? *(const uint32_t *)(p + 12) : 0u;
-            } else {
-                ch[u].q0 = (c > 0 && p - 4 < end) ? *(const uint32_t *)(p - 4) : 0u;
-                ch[u].q1 = p < end ? *(const uint32_t *)p : 0u;
-                ch[u].q2 = p + 4 < end ? *(const uint32_t *)(p + 4) : 0u;
-                ch[u].q3 = p + 8 < end ? *(const uint32_t *)(p + 8) : 0u;
-                ch[u].q4 = (sh && p + 12 < end) ? *(const uint32_t *)(p + 12) : 0u;
-            }
-        }
+    for (int r = 0; r < R; ++r) mx = nch[r] > mx ? nch[r] : mx;
+    for (uint64_t c0 = gl; c0 < mx; c0 += (uint64_t)G * U) {
+        Chunk5 ch[R][U];
 #pragma unroll
-        for (int u = 0; u < kCopyU; ++u) {
-            const uint64_t c = c0 + (uint64_t)u * G;
-            if (c >= nch) break;
-            const Chunk5 &q = ch[u];
-            uint32_t o0 = sh ? __builtin_amdgcn_alignbyte(q.q1, q.q0, sh) : q.q0;
-            uint32_t o1 = sh ? __builtin_amdgcn_alignbyte(q.q2, q.q1, sh) : q.q1;
-            uint32_t o2 = sh ? __builtin_amdgcn_alignbyte(q.q3, q.q2, sh) : q.q2;
-            uint32_t o3 = sh ? __builtin_amdgcn_alignbyte(q.q4, q.q3, sh) : q.q3;
-            const int64_t rem = 4 + (int64_t)cnt - 16 * (int64_t)c;   // blob bytes from chunk start
-            if (rem < 16) {
-                o0 = mask_bytes(o0, rem); o1 = mask_bytes(o1, rem - 4);
-                o2 = mask_bytes(o2, rem - 8); o3 = mask_bytes(o3, rem - 12);
-            }
-            if (c == 0) o0 = lenw;
-            uint8_t *d = dst + 16 * c;
-            if (4 * c + 4 <= nwb) {
-                u32x4a o; o.x = o0; o.y = o1; o.z = o2; o.w = o3;
-                *(u32x4a *)d = o;
-            } else {
-                const uint64_t left = nwb - 4 * c;
-                *(uint32_t *)d = o0;
-                if (left > 1) *(uint32_t *)(d + 4) = o1;
-                if (left > 2) *(uint32_t *)(d + 8) = o2;
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                win_load(ch[r][u], sp, blob_win(src[r], ld_chunk(c0 + (uint64_t)u * G, nch[r])), true);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t sh = (uint32_t)((uintptr_t)src[r] & 3);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t c = c0 + (uint64_t)u * G;
+                if (c >= nch[r]) continue;
+                win_fix(ch[r][u], sp, blob_win(src[r], c), true);
+                blob_store(dst[r], ch[r][u], sh, c, cnt[r]);
             }
         }
     }
 }
 
-// int/uint/enum/float vector as one blob: [BE count][BE elements...].
-__device__ __forceinline__ void enc_blob_words4(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
-                                                uint64_t cnt, bool fl, uint32_t G, uint32_t gl) {
-    const uint64_t nwb = 1 + cnt, nch = (nwb + 3) >> 2;
-    const uint32_t *p0 = (const uint32_t *)src;   // element e = blob word e + 1
-    for (uint64_t c = gl; c < nch; c += G) {
-        uint32_t w[4];
-        if (c > 0 && 4 * c + 4 <= nwb) {
-            const u32x4a v = *(const u32x4a *)(p0 + 4 * c - 1);
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-        } else {
+// int/uint/enum/float vector as one blob: [BE count][BE elements...]; blob
+// word b is element b - 1 of the 4-aligned native run src, so chunk c
+// reads the words at src + 16c - 4.
+__device__ __forceinline__ void w4_store(uint8_t *dst, const Chunk5 &q, uint64_t c, uint64_t cnt, bool fl) {
+    const uint64_t nwb = 1 + cnt;
+    uint32_t o[4] = {q.q0, q.q1, q.q2, q.q3};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint64_t b = 4 * c + j;   // blob word
-                w[j] = (b >= 1 && b < nwb) ? p0[b - 1] : 0u;
+    for (int j = 0; j < 4; ++j) o[j] = bswap32r(fl ? canon_f32r(o[j]) : o[j]);
+    if (c == 0) o[0] = bswap32r((uint32_t)cnt);
+    uint32_t *d = (uint32_t *)(dst + 16 * c);
+    if (4 * c + 4 <= nwb) {
+        u32x4a ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+        *(u32x4a *)d = ov;
+    } else {
+        for (uint64_t j = 0; 4 * c + j < nwb; ++j) d[j] = o[j];
+    }
+}
+template <int U, int R>
+__device__ __forceinline__ void enc_blob_words4(uint8_t *const (&dst)[R], const uint8_t *const (&src)[R],
+                                                const uint64_t (&cnt)[R], const uint64_t (&nch)[R], bool fl,
+                                                const Span &sp, uint32_t G, uint32_t gl) {
+    uint64_t mx = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) mx = nch[r] > mx ? nch[r] : mx;
+    for (uint64_t c0 = gl; c0 < mx; c0 += (uint64_t)G * U) {
+        Chunk5 ch[R][U];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                win_load(ch[r][u], sp, src[r] + 16 * ld_chunk(c0 + (uint64_t)u * G, nch[r]) - 4, false);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t c = c0 + (uint64_t)u * G;
+                if (c >= nch[r]) continue;
+                win_fix(ch[r][u], sp, src[r] + 16 * c - 4, false);
+                w4_store(dst[r], ch[r][u], c, cnt[r], fl);
             }
-        }
-        uint32_t o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = bswap32r(fl ? canon_f32r(w[j]) : w[j]);
-        if (c == 0) o[0] = bswap32r((uint32_t)cnt);
-        uint32_t *d = (uint32_t *)(dst + 16 * c);
-        if (4 * c + 4 <= nwb) {
-            u32x4a ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
-            *(u32x4a *)d = ov;
-        } else {
-            for (uint64_t j = 0; 4 * c + j < nwb; ++j) d[j] = o[j];
-        }
     }
 }
 
 // XDR payload (4-aligned src, cnt bytes) -> native bytes at any alignment.
-// Partial head/tail dwords are written byte by byte: their other bytes
-// belong to neighbouring records.
-template <int kCopyU>
-__device__ __forceinline__ void dec_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
-                                          uint64_t cnt, uint32_t G, uint32_t gl) {
-    if (!cnt) return;
-    const uint32_t sh = (uint32_t)((uintptr_t)dst & 3);
-    uint8_t *da = dst - sh;
-    const uint64_t nd = (sh + cnt + 3) >> 2, nch = (nd + 3) >> 2, nsw = (cnt + 3) >> 2;
-    const uint32_t *q = (const uint32_t *)src;
-    for (uint64_t c0 = gl; c0 < nch; c0 += (uint64_t)G * kCopyU) {
-        Chunk5 ch[kCopyU];   // q0 = word before the chunk, q1..q4 = the chunk's source words
+// Destination dwords are aligned: da = dst - sh; chunk c covers native
+// dwords 4c..4c+3 and reads the stream words at src + 16c - 4 (q0 = the
+// word before the chunk, q1..q4 its words).  Partial head/tail dwords are
+// written byte by byte: their other bytes belong to neighbouring records.
+__device__ __forceinline__ void dec_store(uint8_t *da, const Chunk5 &w, uint64_t c, uint64_t cnt, uint32_t sh) {
+    const uint64_t i0 = 4 * c, nd = (sh + cnt + 3) >> 2;
+    uint32_t v[4];
+    if (sh) {
+        const uint32_t s = 4 - sh;
+        v[0] = __builtin_amdgcn_alignbyte(w.q1, w.q0, s); v[1] = __builtin_amdgcn_alignbyte(w.q2, w.q1, s);
+        v[2] = __builtin_amdgcn_alignbyte(w.q3, w.q2, s); v[3] = __builtin_amdgcn_alignbyte(w.q4, w.q3, s);
+    } else {
+        v[0] = w.q1; v[1] = w.q2; v[2] = w.q3; v[3] = w.q4;
+    }
+    uint8_t *d = da + 16 * c;
+    if ((i0 > 0 || sh == 0) && 4 * (i0 + 4) <= sh + cnt) {
+        u32x4a o; o.x = v[0]; o.y = v[1]; o.z = v[2]; o.w = v[3];
+        *(u32x4a *)d = o;
+        return;
+    }
 #pragma unroll
-        for (int u = 0; u < kCopyU; ++u) {
-            const uint64_t i0 = 4 * (c0 + (uint64_t)u * G);
-            if (i0 >= 4 * nch) continue;
-            if (i0 + 4 <= nsw) {
-                const u32x4a v = *(const u32x4a *)(q + i0);
-                ch[u].q1 = v.x; ch[u].q2 = v.y; ch[u].q3 = v.z; ch[u].q4 = v.w;
-            } else {
-                ch[u].q1 = i0 < nsw ? q[i0] : 0u;
-                ch[u].q2 = i0 + 1 < nsw ? q[i0 + 1] : 0u;
-                ch[u].q3 = i0 + 2 < nsw ? q[i0 + 2] : 0u;
-                ch[u].q4 = i0 + 3 < nsw ? q[i0 + 3] : 0u;
-            }
-            ch[u].q0 = (sh && i0) ? q[i0 - 1] : 0u;
-        }
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t i = i0 + j;
+        if (i >= nd) break;
+        const uint32_t lo = i == 0 ? sh : 0;
+        const uint64_t he = sh + cnt - 4 * i;
+        const uint32_t hi = he < 4 ? (uint32_t)he : 4u;
+        if (lo == 0 && hi == 4) *(uint32_t *)(d + 4 * j) = v[j];
+        else for (uint32_t b = lo; b < hi; ++b) d[4 * j + b] = (uint8_t)(v[j] >> (8 * b));
+    }
+}
+template <int U, int R>
+__device__ __forceinline__ void dec_bytes(uint8_t *const (&dst)[R], const uint8_t *const (&src)[R],
+                                          const uint64_t (&cnt)[R], const uint64_t (&nch)[R],
+                                          const Span &sp, uint32_t G, uint32_t gl) {
+    uint64_t mx = 0;
 #pragma unroll
-        for (int u = 0; u < kCopyU; ++u) {
-            const uint64_t c = c0 + (uint64_t)u * G;
-            if (c >= nch) break;
-            const uint64_t i0 = 4 * c;
-            const Chunk5 &w = ch[u];
-            uint32_t v[4];
-            if (sh) {
-                const uint32_t s = 4 - sh;
-                v[0] = __builtin_amdgcn_alignbyte(w.q1, w.q0, s); v[1] = __builtin_amdgcn_alignbyte(w.q2, w.q1, s);
-                v[2] = __builtin_amdgcn_alignbyte(w.q3, w.q2, s); v[3] = __builtin_amdgcn_alignbyte(w.q4, w.q3, s);
-            } else {
-                v[0] = w.q1; v[1] = w.q2; v[2] = w.q3; v[3] = w.q4;
-            }
-            uint8_t *d = da + 16 * c;
-            if ((i0 > 0 || sh == 0) && 4 * (i0 + 4) <= sh + cnt) {
-                u32x4a o; o.x = v[0]; o.y = v[1]; o.z = v[2]; o.w = v[3];
-                *(u32x4a *)d = o;
-                continue;
-            }
+    for (int r = 0; r < R; ++r) mx = nch[r] > mx ? nch[r] : mx;
+    for (uint64_t c0 = gl; c0 < mx; c0 += (uint64_t)G * U) {
+        Chunk5 ch[R][U];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint64_t i = i0 + j;
-                if (i >= nd) break;
-                const uint32_t lo = i == 0 ? sh : 0;
-                const uint64_t he = sh + cnt - 4 * i;
-                const uint32_t hi = he < 4 ? (uint32_t)he : 4u;
-                if (lo == 0 && hi == 4) *(uint32_t *)(d + 4 * j) = v[j];
-                else for (uint32_t b = lo; b < hi; ++b) d[4 * j + b] = (uint8_t)(v[j] >> (8 * b));
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                win_load(ch[r][u], sp, src[r] + 16 * ld_chunk(c0 + (uint64_t)u * G, nch[r]) - 4, true);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t sh = (uint32_t)((uintptr_t)dst[r] & 3);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t c = c0 + (uint64_t)u * G;
+                if (c >= nch[r]) continue;
+                win_fix(ch[r][u], sp, src[r] + 16 * c - 4, true);
+                dec_store(dst[r] - sh, ch[r][u], c, cnt[r], sh);
             }
         }
     }
 }
 
-__device__ __forceinline__ void dec_words4(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
-                                           uint64_t cnt, uint32_t G, uint32_t gl) {
-    const uint64_t nch = (cnt + 3) >> 2;
-    for (uint64_t c = gl; c < nch; c += G) {
-        const uint32_t *p = (const uint32_t *)(src + 16 * c);
-        uint32_t *d = (uint32_t *)(dst + 16 * c);
-        if (4 * c + 4 <= cnt) {
-            const u32x4a v = *(const u32x4a *)p;
-            u32x4a o; o.x = bswap32r(v.x); o.y = bswap32r(v.y); o.z = bswap32r(v.z); o.w = bswap32r(v.w);
-            *(u32x4a *)d = o;
-        } else {
-            for (uint64_t j = 0; 4 * c + j < cnt; ++j) d[j] = bswap32r(p[j]);
-        }
+// [BE elements] (4-aligned stream) -> native int/uint/enum/float run.
+template <int U, int R>
+__device__ __forceinline__ void dec_words4(uint8_t *const (&dst)[R], const uint8_t *const (&src)[R],
+                                           const uint64_t (&cnt)[R], const uint64_t (&nch)[R],
+                                           const Span &sp, uint32_t G, uint32_t gl) {
+    uint64_t mx = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) mx = nch[r] > mx ? nch[r] : mx;
+    for (uint64_t c0 = gl; c0 < mx; c0 += (uint64_t)G * U) {
+        Chunk5 ch[R][U];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                win_load(ch[r][u], sp, src[r] + 16 * ld_chunk(c0 + (uint64_t)u * G, nch[r]), false);
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t c = c0 + (uint64_t)u * G;
+                if (c >= nch[r]) continue;
+                win_fix(ch[r][u], sp, src[r] + 16 * c, false);
+                const uint32_t w[4] = {ch[r][u].q0, ch[r][u].q1, ch[r][u].q2, ch[r][u].q3};
+                uint32_t *d = (uint32_t *)(dst[r] + 16 * c);
+                if (4 * c + 4 <= cnt[r]) {
+                    u32x4a o;
+                    o.x = bswap32r(w[0]); o.y = bswap32r(w[1]); o.z = bswap32r(w[2]); o.w = bswap32r(w[3]);
+                    *(u32x4a *)d = o;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (4 * c + j < cnt[r]) d[j] = bswap32r(w[j]);
+                }
+            }
     }
 }
 
-template <int U>
+// Average XDR bytes per record of this block >= a.big_rec (the split between
+// the group and the staged kernels, both launched over the whole grid).
+// Encode reads the scanned block sums, decode the record extents.
+__device__ __forceinline__ bool block_is_big(const RecArgs &a, bool decode) {
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint64_t nrec = a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock;
+    uint64_t bytes;
+    if (!decode) bytes = (blockIdx.x + 1 < a.nblocks ? a.block_sums[blockIdx.x + 1] : a.totals[0]) - a.block_sums[blockIdx.x];
+    else if (a.rec_in) bytes = a.rec_in[rb + nrec] - a.rec_in[rb];
+    else bytes = a.rec_stride * nrec;
+    return bytes >= (uint64_t)a.big_rec * nrec;
+}
+
+template <int U, int R>
 __global__ __launch_bounds__(kRecThreads) void k_enc_place_g(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *soff = (uint64_t *)smem;
@@ -825,6 +928,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_place_g(const RecArgs a) {
     uint32_t *scnt = (uint32_t *)(ssrc + (size_t)a.ndyn * kRecPerBlock);
     const uint64_t total = a.totals[0];
     if (total > a.xdr_cap) return;  // XDRG_E_CAPACITY: write nothing
+    if (a.big_rec && !block_is_big(a, false)) return;   // the staged kernel's block
     const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
     const uint32_t t0 = threadIdx.x * kRecPerThread;
     uint64_t sz[kRecPerThread];
@@ -876,9 +980,20 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_place_g(const RecArgs a) {
             if (nw) {
                 const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
                 const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-                for (uint32_t j = tid / G; j < nrec; j += ng) {
-                    uint8_t *dst = out + soff[j] + fixed_delta;
-                    for (uint32_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
+                for (uint32_t j0 = tid / G; j0 < nrec; j0 += ng * R) {
+                    for (uint32_t i = gl; i < nw; i += G) {
+                        uint32_t v[R];
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {   // unconditional: a past-the-end slot re-reads the last record
+                            const uint32_t j = j0 + r * ng < nrec ? j0 + r * ng : (uint32_t)nrec - 1;
+                            v[r] = fixed_word(f, rb + j, 4 * i);
+                        }
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const uint32_t j = j0 + r * ng;
+                            if (j < nrec) *(uint32_t *)(out + soff[j] + fixed_delta + 4 * i) = v[r];
+                        }
+                    }
                 }
             }
             fixed_delta += f.xbytes;
@@ -891,17 +1006,39 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_place_g(const RecArgs a) {
         const uint64_t fbytes = block_sum(ps) * (f.xsz == 1 ? 1 : f.xsz) + 4 * nrec;
         const uint32_t G = a.force_g ? a.force_g : pow2_lanes(nrec ? fbytes / nrec : 0, a.lane_bytes_enc);
         const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-        for (uint32_t j = tid / G; j < nrec; j += ng) {
-            const uint64_t cnt = cn[j], e0 = sr[j];
-            uint8_t *dst = out + soff[j] + fixed_delta;
-            if (f.xsz == 1) {
-                enc_blob_bytes<U>(dst, f.data + e0, cnt, G, gl);
-            } else if (is_word4(f)) {
-                enc_blob_words4(dst, f.data + e0 * 4, cnt, f.type == XDRG_T_FLOAT, G, gl);
+        const bool bytes = f.xsz == 1, w4 = is_word4(f);
+        const uint64_t esz = bytes ? 1 : f.nsz;
+        const Span sp = make_span(f.data + f.offsets[0] * esz, f.data + f.offsets[a.n] * esz,
+                                  (const uint8_t *)a.block_sums);
+        for (uint32_t j0 = tid / G; j0 < nrec; j0 += ng * R) {
+            uint8_t *dst[R];
+            const uint8_t *src[R];
+            uint64_t cnt[R], nch[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t j = j0 + r * ng;
+                const bool live = j < nrec;
+                cnt[r] = live ? cn[j] : 0;
+                const uint64_t e0 = live ? sr[j] : 0;
+                dst[r] = out + (live ? soff[j] : 0) + fixed_delta;
+                src[r] = f.data + (bytes ? e0 : e0 * f.nsz);
+                const uint64_t nwb = 1 + (bytes ? (cnt[r] + 3) >> 2 : cnt[r] * (f.xsz >> 2));
+                nch[r] = live ? (nwb + 3) >> 2 : 0;
+            }
+            if (bytes) {
+                enc_blob_bytes<U, R>(dst, src, cnt, nch, sp, G, gl);
+            } else if (w4) {
+                enc_blob_words4<U, R>(dst, src, cnt, nch, f.type == XDRG_T_FLOAT, sp, G, gl);
             } else {
-                if (gl == 0) *(uint32_t *)dst = bswap32r((uint32_t)cnt);
-                const uint64_t nw = cnt * (f.xsz >> 2);
-                for (uint64_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 + 4 * i) = dyn_word(f, e0, cnt, 4 + 4 * i);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (!nch[r]) continue;
+                    const uint64_t e0 = sr[j0 + r * ng];
+                    if (gl == 0) *(uint32_t *)dst[r] = bswap32r((uint32_t)cnt[r]);
+                    const uint64_t nw = cnt[r] * (f.xsz >> 2);
+                    for (uint64_t i = gl; i < nw; i += G)
+                        *(uint32_t *)(dst[r] + 4 + 4 * i) = dyn_word(f, e0, cnt[r], 4 + 4 * i);
+                }
             }
         }
         __syncthreads();
@@ -916,13 +1053,14 @@ __host__ __device__ constexpr size_t dec_g_lds_bytes(uint32_t nd) {
     return (size_t)kRecPerBlock * 12 + (size_t)nd * kRecPerBlock * 12;
 }
 
-template <int U>
+template <int U, int R>
 __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *sstart = (uint64_t *)smem;
     uint64_t *snoff = sstart + kRecPerBlock;
     uint32_t *scnt = (uint32_t *)(snoff + (size_t)a.ndyn * kRecPerBlock);
     uint32_t *supto = scnt + (size_t)a.ndyn * kRecPerBlock;
+    if (a.big_rec && !block_is_big(a, true)) return;   // the staged kernel's block
     const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
     const uint32_t t0 = threadIdx.x * kRecPerThread;
     const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
@@ -974,10 +1112,22 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
             if (nw) {
                 const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
                 const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-                for (uint32_t j = tid / G; j < nrec; j += ng) {
-                    if (k >= supto[j]) continue;
-                    const uint8_t *src = in + sstart[j] + fixed_delta;
-                    for (uint32_t i = gl; i < nw; i += G) fixed_store(f, rb + j, 4 * i, *(const uint32_t *)(src + 4 * i));
+                for (uint32_t j0 = tid / G; j0 < nrec; j0 += ng * R) {
+                    for (uint32_t i = gl; i < nw; i += G) {
+                        uint32_t v[R];
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {   // unconditional: dead slots read the workspace
+                            const uint32_t j = j0 + r * ng;
+                            const bool live = j < nrec && k < supto[j];
+                            v[r] = *(const uint32_t *)(live ? in + sstart[j] + fixed_delta + 4 * i
+                                                            : (const uint8_t *)a.block_sums);
+                        }
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const uint32_t j = j0 + r * ng;
+                            if (j < nrec && k < supto[j]) fixed_store(f, rb + j, 4 * i, v[r]);
+                        }
+                    }
                 }
             }
             fixed_delta += f.xbytes;
@@ -990,17 +1140,37 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
         const uint64_t fbytes = block_sum(ps) * (f.xsz == 1 ? 1 : f.xsz) + 4 * nrec;
         const uint32_t G = a.force_g ? a.force_g : pow2_lanes(nrec ? fbytes / nrec : 0, a.lane_bytes_dec);
         const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-        for (uint32_t j = tid / G; j < nrec; j += ng) {
-            if (k >= supto[j]) continue;
-            const uint64_t cnt = cn[j];
-            const uint8_t *src = in + sstart[j] + fixed_delta + 4;
-            if (f.xsz == 1) {
-                dec_bytes<U>(f.data + no[j], src, cnt, G, gl);
-            } else if (is_word4(f)) {
-                dec_words4(f.data + no[j] * 4, src, cnt, G, gl);
+        const bool bytes = f.xsz == 1, w4 = is_word4(f);
+        const Span sp = make_span(in, in + a.xdr_cap, (const uint8_t *)a.block_sums);
+        for (uint32_t j0 = tid / G; j0 < nrec; j0 += ng * R) {
+            uint8_t *dst[R];
+            const uint8_t *src[R];
+            uint64_t cnt[R], nch[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t j = j0 + r * ng;
+                const bool live = j < nrec && k < supto[j];
+                cnt[r] = live ? cn[j] : 0;
+                const uint64_t e0 = live ? no[j] : 0;
+                src[r] = in + (live ? sstart[j] : 0) + fixed_delta + 4;
+                dst[r] = f.data + (bytes ? e0 : e0 * f.nsz);
+                const uint32_t sh = (uint32_t)((uintptr_t)dst[r] & 3);
+                const uint64_t nd = bytes ? (sh + cnt[r] + 3) >> 2 : cnt[r] * (f.xsz >> 2);
+                nch[r] = (live && cnt[r]) ? (nd + 3) >> 2 : 0;
+            }
+            if (bytes) {
+                dec_bytes<U, R>(dst, src, cnt, nch, sp, G, gl);
+            } else if (w4) {
+                dec_words4<U, R>(dst, src, cnt, nch, sp, G, gl);
             } else {
-                const uint64_t nw = cnt * (f.xsz >> 2);
-                for (uint64_t i = gl; i < nw; i += G) dyn_store(f, no[j], cnt, 4 + 4 * i, *(const uint32_t *)(src + 4 * i));
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (!nch[r]) continue;
+                    const uint64_t e0 = no[j0 + r * ng];
+                    const uint64_t nw = cnt[r] * (f.xsz >> 2);
+                    for (uint64_t i = gl; i < nw; i += G)
+                        dyn_store(f, e0, cnt[r], 4 + 4 * i, *(const uint32_t *)(src[r] + 4 * i));
+                }
             }
         }
         __syncthreads();
@@ -1259,6 +1429,520 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
 }
 
 // ===========================================================================
+// Staged place kernels (the default for schemas whose dynamic fields are all
+// opaque/string or int/uint/enum/float vectors, at most kMaxDynLds of them).
+//
+// Counters on config 4 (rocprofv3 FETCH_SIZE / WRITE_SIZE)
+// showed that the group kernels' field-major passes over a 1024-record block
+// (~180 KB of XDR) fall out of L2 between passes: encode wrote 1.5x its XDR
+// bytes to HBM (partial lines written back more than once) and decode
+// fetched the stream once per field.  Here a block works through its records
+// in sub-batches (at most kRecThreads records) whose dynamic source bytes fit
+// one LDS tile:
+//   1. stage: the sub-batch's source bytes are one contiguous range per
+//      column (encode: each dynamic native column; decode: the XDR stream)
+//      and are copied into LDS with coalesced 16-byte loads, all in flight;
+//   2. scatter: field-major over the sub-batch, a group of G lanes per record
+//      reads its field from LDS and writes it with 16-byte global stores; a
+//      sub-batch's output is written within one short window, so its lines
+//      merge in L2 before they are written back, and no global load waits
+//      behind these stores.
+// Fixed fields read (encode) or write (decode) their native columns
+// directly.  A record whose staged bytes exceed the tile, and every record of
+// a block whose column ranges do not fit 31-bit offsets, is moved by the
+// whole block straight between global buffers (enc/dec_record_block).
+// ===========================================================================
+constexpr uint32_t kStageSlack = 64;           // LDS bytes a chunk window may read past the tile
+typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));   // 16-byte aligned
+
+__host__ __device__ inline bool stage_type(uint32_t type, uint32_t xsz) {
+    return xsz == 1 || type == XDRG_T_INT || type == XDRG_T_UINT || type == XDRG_T_ENUM || type == XDRG_T_FLOAT;
+}
+
+// 16-aligned global extent [*a0, *a0 + 16 * chunks) covering [p0, p1).
+__device__ __forceinline__ uint32_t stage_chunks(const uint8_t *p0, const uint8_t *p1, const uint8_t **a0) {
+    const uintptr_t x0 = (uintptr_t)p0 & ~(uintptr_t)15, x1 = ((uintptr_t)p1 + 15) & ~(uintptr_t)15;
+    *a0 = (const uint8_t *)x0;
+    return p1 > p0 ? (uint32_t)((x1 - x0) >> 4) : 0u;
+}
+
+// Copy the staged ranges into the tile: range d is cb[d+1] - cb[d] chunks
+// from the 16-aligned a0[d] to tile offset 16 * cb[d].  Four loads per lane
+// are issued before their LDS writes.  A 16-byte aligned chunk that holds a
+// valid byte never leaves that byte's page.
+__device__ __forceinline__ void stage_copy(uint8_t *tile, const uint8_t *const (&a0)[kMaxDynLds],
+                                           const uint32_t (&cb)[kMaxDynLds + 1], uint32_t nd) {
+    const uint32_t total = cb[nd];
+    if (!total) return;
+    for (uint32_t i0 = threadIdx.x; i0 < total; i0 += 4 * kRecThreads) {
+        u32x4n v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + u * kRecThreads < total ? i0 + u * kRecThreads : total - 1;
+            const uint8_t *src = a0[0] + 16 * (uint64_t)i;
+#pragma unroll
+            for (int d = 1; d < kMaxDynLds; ++d)
+                if ((uint32_t)d < nd && i >= cb[d]) src = a0[d] + 16 * (uint64_t)(i - cb[d]);
+            v[u] = __builtin_nontemporal_load((const u32x4n *)src);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + u * kRecThreads;
+            if (i < total) *(u32x4n *)(tile + 16 * (size_t)i) = v[u];
+        }
+    }
+}
+
+// XDR bytes of record j's dynamic fields d < nd (counts from a rel table:
+// row d holds element offsets relative to the block's first record).
+__device__ __forceinline__ uint64_t dyn_before(const RecArgs &a, const uint32_t *rel, uint32_t j, uint32_t nd) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int d = 0; d < kMaxDynLds; ++d) {
+        if ((uint32_t)d >= nd) continue;
+        const uint32_t *r = rel + d * (kRecPerBlock + 1);
+        s += dyn_xdr_bytes(a.f[a.dyn_idx[d]], r[j + 1] - r[j]);
+    }
+    return s;
+}
+
+// ---- encode -------------------------------------------------------------------
+// LDS: soff[RPB + 1] u32 (record offset - block offset) | srel[ND][RPB + 1] u32 | tile
+__host__ __device__ constexpr size_t enc_stage_meta(uint32_t nd) {
+    return ((size_t)(nd + 1) * (kRecPerBlock + 1) * 4 + 15) & ~(size_t)15;
+}
+
+// The whole block writes record r at stream offset pos from the native
+// columns (records too large for the tile).
+__device__ void enc_record_block(const RecArgs &a, uint64_t r, uint64_t pos) {
+    const uint32_t tid = threadIdx.x;
+    uint8_t *out = a.xdr;
+    if (a.framed) pos += 4;   // the mark is written by the caller
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind != XDRG_K_DYNAMIC) {
+            const uint32_t nw = f.xbytes >> 2;
+            for (uint32_t i = tid; i < nw; i += kRecThreads) *(uint32_t *)(out + pos + 4 * i) = fixed_word(f, r, 4 * i);
+            pos += f.xbytes;
+            continue;
+        }
+        const bool bytes = f.xsz == 1;
+        const uint64_t esz = bytes ? 1 : f.nsz;
+        const uint64_t e0 = f.offsets[r], cnt1 = f.offsets[r + 1] - e0;
+        const Span sp = make_span(f.data + f.offsets[0] * esz, f.data + f.offsets[a.n] * esz,
+                                  (const uint8_t *)a.block_sums);
+        uint8_t *dst[1] = {out + pos};
+        const uint8_t *src[1] = {f.data + e0 * esz};
+        const uint64_t cnt[1] = {cnt1};
+        const uint64_t nwb = 1 + (bytes ? (cnt1 + 3) >> 2 : cnt1);
+        const uint64_t nch[1] = {(nwb + 3) >> 2};
+        if (bytes) enc_blob_bytes<2, 1>(dst, src, cnt, nch, sp, kRecThreads, tid);
+        else enc_blob_words4<2, 1>(dst, src, cnt, nch, f.type == XDRG_T_FLOAT, sp, kRecThreads, tid);
+        pos += dyn_xdr_bytes(f, cnt1);
+    }
+}
+
+// Records the sub-batch starting at js can take: [js, js + k) fit the tile
+// iff staging [js, js + 1 + t) fits for every t < k (monotone), counted with
+// one barrier (which also ends every use of the tile before it).  0 = record
+// js alone exceeds the tile.
+__device__ __forceinline__ uint32_t enc_fit(const RecArgs &a, const uint64_t (&base)[kMaxDynLds],
+                                            const uint32_t *srel, uint32_t js, uint32_t nrec) {
+    const uint32_t je = js + 1 + threadIdx.x;
+    bool fits = false;
+    if (je <= nrec) {
+        uint32_t need = 0;
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d) {
+            if ((uint32_t)d >= a.ndyn) continue;
+            const VField &f = a.f[a.dyn_idx[d]];
+            const uint64_t esz = f.xsz == 1 ? 1 : f.nsz;
+            const uint32_t *rel = srel + d * (kRecPerBlock + 1);
+            const uint8_t *a0;
+            need += 16 * stage_chunks(f.data + (base[d] + rel[js]) * esz, f.data + (base[d] + rel[je]) * esz, &a0);
+        }
+        fits = need <= a.tile_bytes;
+    }
+    return (uint32_t)__syncthreads_count(fits);
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr uint32_t RS = kRecPerBlock + 1;   // row stride of soff / srel
+    uint32_t *soff = (uint32_t *)smem;
+    uint32_t *srel = soff + RS;
+    uint8_t *tile = smem + enc_stage_meta(a.ndyn);
+    const uint64_t total = a.totals[0];
+    if (total > a.xdr_cap) return;  // XDRG_E_CAPACITY: write nothing
+    if (a.big_rec && block_is_big(a, false)) return;   // the group kernel's block
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t tid = threadIdx.x, t0 = tid * kRecPerThread;
+    const uint32_t nrec = (uint32_t)(a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock);
+    // ---- prologue: record sizes, column offsets relative to record rb, block scan
+    uint64_t sz[kRecPerThread];
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) sz[j] = t0 + j < nrec ? a.fixed_xdr : 0;
+    uint64_t base[kMaxDynLds];
+    bool wide = false;
+#pragma unroll
+    for (int d = 0; d < kMaxDynLds; ++d) {
+        base[d] = 0;
+        if ((uint32_t)d >= a.ndyn) continue;
+        const VField &f = a.f[a.dyn_idx[d]];
+        const uint64_t esz = f.xsz == 1 ? 1 : f.nsz;
+        base[d] = f.offsets[rb];
+        wide |= (f.offsets[rb + nrec] - base[d]) * esz >= (1ull << 31);
+        uint64_t o[kRecPerThread + 1];
+#pragma unroll
+        for (int j = 0; j <= kRecPerThread; ++j) {   // unconditional loads, index clamped
+            const uint64_t r = rb + t0 + j;
+            o[j] = f.offsets[r < a.n ? r : a.n];
+        }
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            if (t0 + j < nrec) sz[j] += dyn_xdr_bytes(f, o[j + 1] - o[j]);
+            srel[d * RS + t0 + j] = (uint32_t)(o[j] - base[d]);
+        }
+        if (tid == kRecThreads - 1) srel[d * RS + kRecPerBlock] = (uint32_t)(o[kRecPerThread] - base[d]);
+    }
+    uint64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) s += sz[j];
+    uint64_t btot;
+    const uint64_t bbase = a.block_sums[blockIdx.x];   // stream offset of record rb
+    uint64_t off = block_excl_scan(s, &btot);
+    wide |= btot >= (1ull << 32);
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        soff[t0 + j] = (uint32_t)off;
+        if (a.rec_out && t0 + j < nrec) a.rec_out[rb + t0 + j] = bbase + off;
+        off += sz[j];
+    }
+    if (tid == kRecThreads - 1) soff[kRecPerBlock] = (uint32_t)off;
+    if (a.rec_out && blockIdx.x == 0 && tid == 0) a.rec_out[a.n] = total;
+    __syncthreads();
+    if (wide) {   // block offsets beyond 32 bits: record by record, straight from global
+        uint64_t pos = bbase;
+        for (uint32_t j = 0; j < nrec; ++j) {
+            const uint64_t r = rb + j;
+            uint64_t size = a.fixed_xdr;
+            for (uint32_t d = 0; d < a.ndyn; ++d) {
+                const VField &f = a.f[a.dyn_idx[d]];
+                size += dyn_xdr_bytes(f, f.offsets[r + 1] - f.offsets[r]);
+            }
+            if (a.framed && tid == 0)   // GrizzlyRpcTransport:103-110
+                *(uint32_t *)(a.xdr + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
+            enc_record_block(a, r, pos);
+            pos += size;
+        }
+        return;
+    }
+    uint8_t *out = a.xdr + bbase;   // block-relative stream
+    if (a.framed)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
+        for (uint32_t j = tid; j < nrec; j += kRecThreads)
+            *(uint32_t *)(out + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
+    // ---- sub-batches
+    uint32_t js = 0;
+    uint32_t k1 = enc_fit(a, base, srel, js, nrec);
+    while (js < nrec) {
+        if (k1 == 0) {   // too large for the tile: the whole block writes record js
+            enc_record_block(a, rb + js, bbase + soff[js]);
+            ++js;
+            k1 = js < nrec ? enc_fit(a, base, srel, js, nrec) : 0;
+            continue;
+        }
+        const uint32_t je = js + k1;
+        // stage every dynamic column's range of the sub-batch
+        const uint8_t *a0[kMaxDynLds];
+        uint32_t cb[kMaxDynLds + 1];
+        cb[0] = 0;
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d) {
+            a0[d] = nullptr;
+            cb[d + 1] = cb[d];
+            if ((uint32_t)d >= a.ndyn) continue;
+            const VField &f = a.f[a.dyn_idx[d]];
+            const uint64_t esz = f.xsz == 1 ? 1 : f.nsz;
+            cb[d + 1] += stage_chunks(f.data + (base[d] + srel[d * RS + js]) * esz,
+                                      f.data + (base[d] + srel[d * RS + je]) * esz, &a0[d]);
+        }
+        stage_copy(tile, a0, cb, a.ndyn);
+        __syncthreads();
+        // scatter, field-major; field k of record j sits at
+        // soff[j] + (fixed bytes before k) + (dynamic bytes before k)
+        uint32_t fpre = a.framed ? 4 : 0;
+        uint32_t d = 0;
+        const uint32_t m = je - js;
+        for (uint32_t k = 0; k < a.nf; ++k) {
+            const VField &f = a.f[k];
+            if (f.kind != XDRG_K_DYNAMIC) {
+                const uint32_t nw = f.xbytes >> 2;
+                if (nw) {
+                    const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
+                    const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+                    for (uint32_t j = js + tid / G; j < je; j += ng) {
+                        uint8_t *dst = out + soff[j] + fpre + dyn_before(a, srel, j, d);
+                        for (uint32_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
+                    }
+                }
+                fpre += f.xbytes;
+                continue;
+            }
+            const bool bytes = f.xsz == 1;
+            const uint64_t esz = bytes ? 1 : f.nsz;
+            const uint32_t *rel = srel + d * RS;
+            const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
+            const uint32_t G = a.force_g ? a.force_g : pow2_lanes(fbytes / m, a.lane_bytes_enc);
+            const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+            const bool fl = f.type == XDRG_T_FLOAT;
+            // tile offset of the column byte at address x: lds0 + x
+            const int64_t lds0 = 16 * (int64_t)cb[d] - (int64_t)(uintptr_t)a0[d];
+            for (uint32_t j = js + tid / G; j < je; j += ng) {
+                const uint64_t cnt = rel[j + 1] - rel[j];
+                const uint8_t *p = f.data + (base[d] + rel[j]) * esz;
+                uint8_t *dst = out + soff[j] + fpre + dyn_before(a, srel, j, d);
+                const int64_t L = lds0 + (int64_t)(uintptr_t)p;   // tile offset of p
+                if (bytes) {
+                    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+                    const uint64_t nch = (1 + ((cnt + 3) >> 2) + 3) >> 2;
+                    for (uint64_t c = gl; c < nch; c += G) {
+                        const uint32_t *w = (const uint32_t *)(tile + (L - sh + 16 * (int64_t)c - 4));
+                        Chunk5 q;
+                        q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = w[4];
+                        blob_store(dst, q, sh, c, cnt);
+                    }
+                } else {
+                    const uint64_t nch = (1 + cnt + 3) >> 2;
+                    for (uint64_t c = gl; c < nch; c += G) {
+                        const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c - 4));
+                        Chunk5 q;
+                        q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = 0;
+                        w4_store(dst, q, c, cnt, fl);
+                    }
+                }
+            }
+            ++d;
+        }
+        js = je;
+        k1 = js < nrec ? enc_fit(a, base, srel, js, nrec) : 0;   // its barrier ends the tile's use
+    }
+}
+
+// ---- decode -------------------------------------------------------------------
+// LDS: sstart[RPB + 1] u64 | snrel[ND][RPB + 1] u32 | supto[RPB] u32 | tile[tile_bytes + slack]
+__host__ __device__ constexpr size_t dec_stage_meta(uint32_t nd) {
+    return ((size_t)(kRecPerBlock + 1) * 8 + (size_t)nd * (kRecPerBlock + 1) * 4 + (size_t)kRecPerBlock * 4 +
+            15) & ~(size_t)15;
+}
+
+// The whole block decodes fields [0, upto) of record r whose first field
+// starts at stream offset pos (records too large for the tile).  Native
+// offsets come from the columns' offsets arrays this block just wrote.
+__device__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uint32_t upto) {
+    const uint32_t tid = threadIdx.x;
+    const uint8_t *in = a.xdr;
+    const Span sp = make_span(in, in + a.xdr_cap, (const uint8_t *)a.block_sums);
+    uint32_t d = 0;
+    for (uint32_t k = 0; k < upto; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind != XDRG_K_DYNAMIC) {
+            const uint32_t nw = f.xbytes >> 2;
+            for (uint32_t i = tid; i < nw; i += kRecThreads) fixed_store(f, r, 4 * i, *(const uint32_t *)(in + pos + 4 * i));
+            pos += f.xbytes;
+            continue;
+        }
+        const bool bytes = f.xsz == 1;
+        const uint64_t cnt1 = a.rec_cnt[(uint64_t)d * a.n + r];
+        uint8_t *dst[1] = {f.data + f.offsets[r] * (bytes ? 1 : f.nsz)};
+        const uint8_t *src[1] = {in + pos + 4};
+        const uint64_t cnt[1] = {cnt1};
+        const uint32_t sh = (uint32_t)((uintptr_t)dst[0] & 3);
+        const uint64_t nd = bytes ? (sh + cnt1 + 3) >> 2 : cnt1;
+        const uint64_t nch[1] = {cnt1 ? (nd + 3) >> 2 : 0};
+        if (bytes) dec_bytes<2, 1>(dst, src, cnt, nch, sp, kRecThreads, tid);
+        else dec_words4<2, 1>(dst, src, cnt, nch, sp, kRecThreads, tid);
+        pos += dyn_xdr_bytes(f, cnt1);
+        ++d;
+    }
+}
+
+// As enc_fit, over the XDR stream range of records [js, js + 1 + t).
+__device__ __forceinline__ uint32_t dec_fit(const RecArgs &a, const uint64_t *sstart, const uint32_t *snrel,
+                                            uint32_t js, uint32_t nlive) {
+    const uint32_t je = js + 1 + threadIdx.x;
+    bool fits = false;
+    if (je <= nlive) {
+        const uint8_t *a0;
+        const uint64_t e = sstart[je - 1] + (a.fixed_xdr - (a.framed ? 4 : 0)) + dyn_before(a, snrel, je - 1, a.ndyn);
+        fits = 16 * stage_chunks(a.xdr + sstart[js], a.xdr + e, &a0) <= a.tile_bytes;
+    }
+    return (uint32_t)__syncthreads_count(fits);
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr uint32_t RS = kRecPerBlock + 1;
+    uint64_t *sstart = (uint64_t *)smem;
+    uint32_t *snrel = (uint32_t *)(sstart + RS);
+    uint32_t *supto = snrel + (size_t)a.ndyn * RS;
+    uint8_t *tile = smem + dec_stage_meta(a.ndyn);
+    __shared__ uint32_t s_wide;
+    if (a.big_rec && block_is_big(a, true)) return;   // the group kernel's block
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t tid = threadIdx.x, t0 = tid * kRecPerThread;
+    const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
+    const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
+    const uint32_t nrec = (uint32_t)(a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0);
+    const uint32_t nlive = bad > rb ? (uint32_t)(bad - rb < (uint64_t)nrec ? bad - rb : (uint64_t)nrec) : 0;
+    if (tid == 0) s_wide = 0;
+    // ---- prologue: counts, native offsets (written to the columns), capacity, extents
+    uint32_t upto[kRecPerThread];
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        const bool live = t0 + j < nlive;
+        upto[j] = live ? a.nf : 0u;
+        if (live) sstart[t0 + j] = rec_extent(a, rb + t0 + j).a + (a.framed ? 4 : 0);
+    }
+    bool wide = false;
+#pragma unroll
+    for (int d = 0; d < kMaxDynLds; ++d) {
+        if ((uint32_t)d >= a.ndyn) continue;
+        const uint32_t k = a.dyn_idx[d];
+        const VField &f = a.f[k];
+        uint32_t c[kRecPerThread];
+        uint64_t s = 0;
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            const uint64_t r = rb + t0 + j;
+            c[j] = t0 + j < nlive ? a.rec_cnt[(uint64_t)d * a.n + r] : 0u;
+            s += c[j];
+        }
+        uint64_t btot;
+        const uint64_t base = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x];
+        uint64_t off = base + block_excl_scan(s, &btot);
+        wide |= btot * (f.xsz == 1 ? 1 : f.nsz) >= (1ull << 31);
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            const uint64_t r = rb + t0 + j;
+            snrel[d * RS + t0 + j] = (uint32_t)(off - base);
+            if (t0 + j < nrec) {
+                f.offsets[r] = off;
+                if (t0 + j < nlive && off + c[j] > f.cap) {   // native column too small
+                    atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
+                    if (upto[j] > k) upto[j] = k;
+                }
+            }
+            off += c[j];
+        }
+        if (tid == kRecThreads - 1) snrel[d * RS + kRecPerBlock] = (uint32_t)(off - base);
+        if (blockIdx.x == 0 && tid == 0) f.offsets[a.n] = a.totals[d];
+    }
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) supto[t0 + j] = upto[j];
+    __syncthreads();
+    // staging needs every record's fields to end where the next begins or
+    // before (records in stream order); otherwise the block goes direct
+    const uint32_t fx = a.fixed_xdr - (a.framed ? 4 : 0);   // fixed XDR bytes of the fields
+    if (!wide) {
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            const uint32_t i = t0 + j;
+            if (i + 1 < nlive && (sstart[i + 1] < sstart[i] || sstart[i] + fx + dyn_before(a, snrel, i, a.ndyn) > sstart[i + 1]))
+                wide = true;
+        }
+    }
+    if (wide) s_wide = 1;
+    __syncthreads();
+    wide = s_wide != 0;
+    const uint8_t *in = a.xdr;
+
+    if (wide) {
+        for (uint32_t j = 0; j < nlive; ++j) dec_record_block(a, rb + j, sstart[j], supto[j]);
+        return;
+    }
+    // ---- sub-batches
+    uint32_t js = 0;
+    uint32_t k1 = nlive ? dec_fit(a, sstart, snrel, js, nlive) : 0;
+    while (js < nlive) {
+        if (k1 == 0) {   // too large for the tile: the whole block decodes record js
+            dec_record_block(a, rb + js, sstart[js], supto[js]);
+            ++js;
+            k1 = js < nlive ? dec_fit(a, sstart, snrel, js, nlive) : 0;
+            continue;
+        }
+        const uint32_t je = js + k1;
+        const uint8_t *a0[kMaxDynLds] = {nullptr, nullptr, nullptr, nullptr};
+        uint32_t cb[kMaxDynLds + 1] = {0, 0, 0, 0, 0};
+        cb[1] = stage_chunks(in + sstart[js], in + sstart[je - 1] + fx + dyn_before(a, snrel, je - 1, a.ndyn), &a0[0]);
+        stage_copy(tile, a0, cb, 1);
+        __syncthreads();
+        const int64_t lds0 = -(int64_t)(a0[0] - in);   // tile offset of stream offset x: lds0 + x
+        uint32_t fpre = 0;
+        uint32_t d = 0;
+        const uint32_t m = je - js;
+        for (uint32_t k = 0; k < a.nf; ++k) {
+            const VField &f = a.f[k];
+            if (f.kind != XDRG_K_DYNAMIC) {
+                const uint32_t nw = f.xbytes >> 2;
+                if (nw) {
+                    const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
+                    const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+                    for (uint32_t j = js + tid / G; j < je; j += ng) {
+                        if (k >= supto[j]) continue;
+                        const uint32_t *w = (const uint32_t *)(tile + (lds0 + (int64_t)(sstart[j] + fpre +
+                                                                                   dyn_before(a, snrel, j, d))));
+                        for (uint32_t i = gl; i < nw; i += G) fixed_store(f, rb + j, 4 * i, w[i]);
+                    }
+                }
+                fpre += f.xbytes;
+                continue;
+            }
+            const bool bytes = f.xsz == 1;
+            const uint64_t esz = bytes ? 1 : f.nsz;
+            const uint32_t *rel = snrel + d * RS;
+            const uint64_t base = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x];
+            const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
+            const uint32_t G = a.force_g ? a.force_g : pow2_lanes(fbytes / m, a.lane_bytes_dec);
+            const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+            for (uint32_t j = js + tid / G; j < je; j += ng) {
+                if (k >= supto[j]) continue;
+                const uint64_t cnt = rel[j + 1] - rel[j];
+                if (!cnt) continue;
+                // tile offset of the payload (after the length word)
+                const int64_t L = lds0 + (int64_t)(sstart[j] + fpre + dyn_before(a, snrel, j, d) + 4);
+                uint8_t *dst = f.data + (base + rel[j]) * esz;
+                if (bytes) {
+                    const uint32_t sh = (uint32_t)((uintptr_t)dst & 3);
+                    const uint64_t nch = (((sh + cnt + 3) >> 2) + 3) >> 2;
+                    for (uint64_t c = gl; c < nch; c += G) {
+                        const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c - 4));
+                        Chunk5 q;
+                        q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = w[4];
+                        dec_store(dst - sh, q, c, cnt, sh);
+                    }
+                } else {
+                    const uint64_t nch = (cnt + 3) >> 2;
+                    for (uint64_t c = gl; c < nch; c += G) {
+                        const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c));
+                        uint32_t *o = (uint32_t *)(dst + 16 * c);
+                        if (4 * c + 4 <= cnt) {
+                            u32x4a v;
+                            v.x = bswap32r(w[0]); v.y = bswap32r(w[1]); v.z = bswap32r(w[2]); v.w = bswap32r(w[3]);
+                            *(u32x4a *)o = v;
+                        } else {
+                            for (uint64_t e = 0; 4 * c + e < cnt; ++e) o[e] = bswap32r(w[e]);
+                        }
+                    }
+                }
+            }
+            ++d;
+        }
+        js = je;
+        k1 = js < nlive ? dec_fit(a, sstart, snrel, js, nlive) : 0;   // its barrier ends the tile's use
+    }
+}
+
+// ===========================================================================
 // Launchers
 // ===========================================================================
 __global__ void k_debug_recargs(const RecArgs a) {
@@ -1290,14 +1974,40 @@ __global__ void k_debug_recargs(const RecArgs a) {
            pad4((uint64_t)len));
 }
 
-// copy unroll of the group kernels (tools/tune_rec.py; set_tuning keys 4 and 5)
+// copy unroll of the group kernels (tools/tune_rec.py; set_tuning keys 4 and
+// 5: chunks per record, 10 and 11: records per lane in flight)
 static int g_enc_u = 2, g_dec_u = 2;
+static int g_enc_r = 1, g_dec_r = 1;
+
+template <template <int, int> class K>
+static void launch_ur(int u, int r, dim3 grid, size_t lds, hipStream_t st, const RecArgs &a) {
+#define XDRG_UR(U_, R_) \
+    if (u == U_ && r == R_) { hipLaunchKernelGGL((K<U_, R_>::fn), grid, dim3(kRecThreads), lds, st, a); return; }
+    XDRG_UR(1, 1) XDRG_UR(1, 2) XDRG_UR(1, 4)
+    XDRG_UR(2, 1) XDRG_UR(2, 2) XDRG_UR(2, 4)
+    XDRG_UR(4, 1) XDRG_UR(4, 2) XDRG_UR(4, 4)
+#undef XDRG_UR
+}
+template <int U, int R> struct EncG { static constexpr auto fn = k_enc_place_g<U, R>; };
+template <int U, int R> struct DecG { static constexpr auto fn = k_dec_place_g<U, R>; };
 static uint32_t g_force_g = 0;
-static int g_rec_kernel = 0;   // 0 = group per record (default), 3 = lane per record
+static int g_rec_kernel = 4;   // 4 = staged (default), 0 = group per record, 3 = lane per record
+static uint32_t g_tile_bytes = 16384;
+static uint32_t g_big_rec = 1024;   // XDR bytes per record from which blocks take the group kernel
 static uint32_t g_lane_bytes_enc = 32, g_lane_bytes_dec = 32;
 int set_rec_tuning(int key, long long value) {
+    if (key == 13) {   // staged kernels: group-kernel split (average XDR bytes per record; 0 = never)
+        if (value < 0 || value > (1ll << 31)) return -1;
+        g_big_rec = (uint32_t)value;
+        return 0;
+    }
+    if (key == 12) {   // staged kernels: LDS tile bytes per sub-batch
+        if (value < 1024 || value > 98304 || (value & 15)) return -1;
+        g_tile_bytes = (uint32_t)value;
+        return 0;
+    }
     if (key == 9) {
-        if (value != 0 && value != 3) return -1;
+        if (value != 0 && value != 3 && value != 4) return -1;
         g_rec_kernel = (int)value;
         return 0;
     }
@@ -1314,6 +2024,8 @@ int set_rec_tuning(int key, long long value) {
     if (value != 1 && value != 2 && value != 4) return -1;
     if (key == 4) g_enc_u = (int)value;
     else if (key == 5) g_dec_u = (int)value;
+    else if (key == 10) g_enc_r = (int)value;
+    else if (key == 11) g_dec_r = (int)value;
     else return -1;
     return 0;
 }
@@ -1323,22 +2035,31 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
     a.force_g = g_force_g;
     a.lane_bytes_enc = g_lane_bytes_enc;
     a.lane_bytes_dec = g_lane_bytes_dec;
+    a.tile_bytes = g_tile_bytes;
+    a.big_rec = 0;
     if (phase == REC_DEC_SIZES && getenv("XDRG_DEBUG"))
         hipLaunchKernelGGL(k_debug_recargs, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
     const bool grp = a.ndyn <= (uint32_t)kMaxDynLds;
+    bool stage = grp && g_rec_kernel == 4;
+    for (uint32_t d = 0; d < a.ndyn && stage; ++d)
+        stage = stage_type(a.f[a.dyn_idx[d]].type, a.f[a.dyn_idx[d]].xsz);
     switch (phase) {
     case REC_ENC_SIZES: hipLaunchKernelGGL(k_enc_sizes, dim3(nb), dim3(kRecThreads), 0, st, a); break;
     case REC_ENC_SCAN:
         hipLaunchKernelGGL(k_scan_rows, dim3(1), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_ENC_PLACE:
-        if (grp && g_rec_kernel == 3) {
+        if (stage) {   // small-record blocks staged, large-record blocks by the group kernel
+            a.big_rec = g_big_rec;
+            hipLaunchKernelGGL(k_enc_stage, dim3(nb), dim3(kRecThreads),
+                               enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            if (a.big_rec) launch_ur<EncG>(g_enc_u, g_enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
+        } else if (grp && g_rec_kernel == 3) {
             hipLaunchKernelGGL(k_enc_lane, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
-            if (g_enc_u == 1) hipLaunchKernelGGL(k_enc_place_g<1>, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
-            else hipLaunchKernelGGL(k_enc_place_g<2>, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
+            launch_ur<EncG>(g_enc_u, g_enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
         }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
@@ -1352,11 +2073,15 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
             hipLaunchKernelGGL(k_scan_rows, dim3(a.ndyn), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_DEC_PLACE:
-        if (grp && g_rec_kernel == 3) {
+        if (stage) {
+            a.big_rec = g_big_rec;
+            hipLaunchKernelGGL(k_dec_stage, dim3(nb), dim3(kRecThreads),
+                               dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            if (a.big_rec) launch_ur<DecG>(g_dec_u, g_dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
+        } else if (grp && g_rec_kernel == 3) {
             hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
-            if (g_dec_u == 1) hipLaunchKernelGGL(k_dec_place_g<1>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
-            else hipLaunchKernelGGL(k_dec_place_g<2>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+            launch_ur<DecG>(g_dec_u, g_dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
         }
         else hipLaunchKernelGGL(k_dec_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;

@@ -121,7 +121,10 @@ struct RecArgs {
     uint32_t force_g;          // 0 = group size from the average field size, else lanes per record
     uint32_t lane_bytes_enc;   // group sizing: target XDR bytes per lane (encode / decode)
     uint32_t lane_bytes_dec;
-    uint32_t rsv0;
+    uint32_t tile_bytes;       // staged place kernels: LDS tile per sub-batch
+    uint32_t big_rec;          // blocks averaging >= big_rec XDR bytes per record take the group
+                               // kernels, the others the staged ones (0: one kernel for all)
+    uint32_t rsv1;
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
 };

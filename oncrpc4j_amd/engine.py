@@ -20,8 +20,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 _LIB = None
 
 # record-path implementation the library starts with (kernels_rec.hip
-# g_rec_kernel: 0 = group per record, 3 = lane per record)
-DEFAULT_REC_KERNEL = 0
+# g_rec_kernel: 4 = staged sub-batches, 0 = group per record, 3 = lane per record)
+DEFAULT_REC_KERNEL = 4
 
 
 def lib():

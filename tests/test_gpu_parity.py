@@ -38,9 +38,18 @@ SCHEMAS = {
 }
 
 
-# Record-path implementations (kernels_rec.hip launch_rec_phase): 0 = group
-# per record, 3 = lane per record.  Tests taking `rec_kernel` run under each.
-REC_KERNELS = {"group": 0, "lane": 3}
+# Record-path implementations (kernels_rec.hip launch_rec_phase): 4 = staged
+# (sub-batches through an LDS tile, the default), 0 = group per record,
+# 3 = lane per record.  Tests taking `rec_kernel` run under each.
+REC_KERNELS = {"group": 0, "lane": 3, "staged": 4}
+
+
+def _tune(key, value):
+    import ctypes
+    L = engine.lib()
+    L.xdrg_internal_tune.argtypes = [ctypes.c_int, ctypes.c_longlong]
+    L.xdrg_internal_tune.restype = ctypes.c_int
+    assert L.xdrg_internal_tune(key, value) == 0
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
@@ -244,6 +253,38 @@ def test_error_parity(gpu_ctx, rec_kernel, name, framed):
             g2 = gpu_decode(gpu_ctx, fields, bad, n, None, caps, framed, use_offsets=False)
             o2 = oracle_decode(fields, bad, n, None, caps, framed)
             assert g2[:3] == o2[:3], desc
+
+
+@pytest.mark.parametrize("tile", [1024, 4096])
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+@pytest.mark.parametrize("name", ["cfg1_int_int_string", "cfg3_6xint_opaque", "cfg4_int_string_intvec",
+                                  "dyn_vectors"])
+def test_staged_tile_sizes(gpu_ctx, name, framed, tile):
+    """Staged place kernels with small LDS tiles: records whose staged bytes
+    exceed the tile take the whole-block direct path, the others form
+    sub-batches of every size (dyn_vectors has non-stageable vector types and
+    runs the group kernels)."""
+    fields = SCHEMAS[name]
+    n = 2500
+    hb = random_batch(fields, n, seed=zlib.crc32(f"tile/{name}/{framed}/{tile}".encode()), dyn_len=(0, 3000))
+    rc, want, want_offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total(framed) + 8, framed=framed)
+    assert rc == 0
+    _tune(9, 4)
+    _tune(12, tile)
+    _tune(13, 0)   # every block staged (no split of large-record blocks to the group kernel)
+    try:
+        xdr, offs = gpu_encode(gpu_ctx, fields, hb, framed)
+        assert xdr == want
+        assert np.array_equal(offs, want_offs)
+        caps = hb.dyn_caps()
+        g = gpu_decode(gpu_ctx, fields, xdr, n, offs, caps, framed)
+        o = oracle_decode(fields, xdr, n, offs, caps, framed)
+        assert g[:3] == o[:3] == (0, n, 0)
+        assert g[3].equal(o[3])
+    finally:
+        _tune(12, 16384)
+        _tune(13, 1024)
+        _tune(9, engine.DEFAULT_REC_KERNEL)
 
 
 def test_decode_capacity(gpu_ctx, rec_kernel):

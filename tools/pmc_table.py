@@ -1,0 +1,38 @@
+"""Per-kernel counter table from tools/prof_rec.sh output directories.
+
+  python tools/pmc_table.py gpurun_out/p_c4      (prefix of the *_fetch, *_sq ... dirs)
+
+Median over dispatches of every counter, per xdrg kernel; FETCH_SIZE is
+doubled (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md)."""
+import csv
+import glob
+import json
+import statistics
+import sys
+
+
+def main():
+    pre = sys.argv[1]
+    vals = {}
+    for path in glob.glob(pre + "_*/run_counter_collection.csv"):
+        for r in csv.DictReader(open(path)):
+            if "xdrg::" not in r["Kernel_Name"]:
+                continue
+            k = r["Kernel_Name"].replace("void ", "").replace("xdrg::", "").split("(")[0]
+            d = vals.setdefault(k, {})
+            d.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            d.setdefault("_vgpr", []).append(float(r["VGPR_Count"]))
+            d.setdefault("_ns", []).append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+    out = {}
+    for k, d in sorted(vals.items()):
+        m = {c: statistics.median(v) for c, v in d.items()}
+        if "FETCH_SIZE" in m:
+            m["FETCH_SIZE_x2_bytes"] = 2 * m["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in m:
+            m["WRITE_SIZE_bytes"] = m["WRITE_SIZE"] * 1024
+        out[k] = m
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -29,16 +29,23 @@ def main():
         torch.cuda.synchronize()
         wl.check()
         res = {}
-        # (kernel, unroll, lane bytes): kernel 0 = group per record, 3 = lane per record
-        variants = [(0, 2, 32), (3, 2, 32)] if os.environ.get("QUICK") else \
-            [(0, u, lb) for u in (1, 2) for lb in (16, 32, 64)] + [(3, 2, 32)]
+        # (kernel, chunks per record, records per lane, lane bytes, tile bytes):
+        # kernel 4 = staged sub-batches, 0 = group per record, 3 = lane per record
+        if os.environ.get("QUICK"):
+            variants = [(4, 2, 1, 32, 16384), (0, 2, 1, 32, 16384)]
+        else:
+            variants = [(4, 2, 1, lb, tb) for lb in (32, 64) for tb in (16384, 32768)] + \
+                       [(0, 2, 1, 32, 16384)]
         for r in range(rounds):
-            for kern, u, g in variants:
-                L.xdrg_internal_tune(9, kern)
-                L.xdrg_internal_tune(4, u)
-                L.xdrg_internal_tune(5, u)
-                L.xdrg_internal_tune(7, g)
-                L.xdrg_internal_tune(8, g)
+            for kern, u, rr, g, tb in variants:
+                assert L.xdrg_internal_tune(12, tb) == 0
+                assert L.xdrg_internal_tune(9, kern) == 0
+                assert L.xdrg_internal_tune(4, u) == 0
+                assert L.xdrg_internal_tune(5, u) == 0
+                assert L.xdrg_internal_tune(10, rr) == 0
+                assert L.xdrg_internal_tune(11, rr) == 0
+                assert L.xdrg_internal_tune(7, g) == 0
+                assert L.xdrg_internal_tune(8, g) == 0
                 if r == 0:   # every variant must round-trip on its own writes
                     wl.clear_outputs()
                 ctx.reset_stats()
@@ -49,19 +56,23 @@ def main():
                 for kid, name in ((abi.KERNEL_VAR_SIZE, "sizes"), (abi.KERNEL_VAR_SCAN, "scan"),
                                   (abi.KERNEL_VAR_ENCODE, "enc_place"), (abi.KERNEL_VAR_DECODE, "dec_place")):
                     c, ms = ctx.kernel_stats(kid)
-                    res.setdefault((kern, u, g, name), []).append(ms)
+                    res.setdefault((kern, u, rr, g, tb, name), []).append(ms)
         L.xdrg_internal_tune(9, engine.DEFAULT_REC_KERNEL)   # defaults (kernels_rec.hip)
         L.xdrg_internal_tune(4, 2)
         L.xdrg_internal_tune(5, 2)
+        L.xdrg_internal_tune(10, 1)
+        L.xdrg_internal_tune(11, 1)
         L.xdrg_internal_tune(7, 32)
         L.xdrg_internal_tune(8, 32)
+        L.xdrg_internal_tune(12, 16384)
         wl.step(ctx)
         torch.cuda.synchronize()
         wl.check()
         per_launch = wl.native_bytes + wl.xlen
-        for (kern, u, g, name), t in sorted(res.items()):
+        for (kern, u, rr, g, tb, name), t in sorted(res.items()):
             med = statistics.median(t)
-            d = {"config": cfg, "impl": {0: "group", 3: "lane"}[kern], "unroll": u, "lane_bytes": g,
+            d = {"config": cfg, "impl": {0: "group", 3: "lane", 4: "staged"}[kern], "unroll": u, "recs": rr,
+                 "lane_bytes": g, "tile": tb,
                  "kernel": name, "median_ms": round(med, 4)}
             if name.endswith("place"):
                 d["GBps"] = round(per_launch / med / 1e6, 1)
