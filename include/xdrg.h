@@ -158,6 +158,37 @@ int  xdrg_ctx_reset_stats(xdrg_ctx *ctx);
  * engine schema.  Host-side object; may be shared by contexts.                 */
 int  xdrg_schema_create(const xdrg_field *fields, size_t nfields, xdrg_schema **out);
 int  xdrg_schema_destroy(xdrg_schema *schema);
+
+/* Conditional fields: rpcgen unions and optional data, whose records of one
+ * type differ in shape.  A union (jrpcgen.java:1240-1340) encodes its
+ * discriminant and then the one arm whose case list holds the value (or the
+ * default arm, or nothing); optional data `T *x` (JrpcgenDeclaration
+ * INDIRECTION) encodes a bool and then T only when it is true.  Both flatten
+ * to one tape in which some fields carry a condition on an earlier
+ * discriminant field:
+ *   field k is present  iff  field `disc` is present  and
+ *                            (value(disc) in values[0..nvalues))  !=  negate
+ * value(disc) is the int / unsigned / enum as an int32, a bool as 0 or 1
+ * (decode: any non-zero word is true, Xdr.java:404-407).  Nested unions /
+ * optionals chain: an absent discriminant makes its dependants absent.
+ * Encode writes nothing for an absent field (its native slot is ignored);
+ * decode writes zero into an absent fixed field's native slot and an empty
+ * run (offsets[i+1] == offsets[i]) for an absent dynamic field — the
+ * defaults of a freshly constructed rpcgen object.  A schema with any
+ * condition is variable-size (xdrg_schema_fixed_size() == 0).  At most
+ * XDRG_MAX_DISC distinct discriminant fields and XDRG_MAX_CASES case values
+ * per schema.                                                                 */
+#define XDRG_MAX_DISC  8
+#define XDRG_MAX_CASES 64
+typedef struct xdrg_cond {
+    uint32_t field;          /* the conditional field (index into fields)                 */
+    uint32_t disc;           /* its discriminant: an earlier SCALAR INT/UINT/ENUM/BOOL field */
+    uint32_t negate;         /* 0: case arm (value in list); 1: default arm / optional (not in) */
+    uint32_t nvalues;
+    const int32_t *values;   /* host pointer, copied at schema creation                   */
+} xdrg_cond;
+int  xdrg_schema_create_cond(const xdrg_field *fields, size_t nfields, const xdrg_cond *conds,
+                             size_t nconds, xdrg_schema **out);
 /* XDR bytes of one record when every field is fixed-size (no DYNAMIC field),
  * excluding any record mark; 0 for variable-size schemas.                      */
 uint64_t xdrg_schema_fixed_size(const xdrg_schema *schema);

@@ -66,6 +66,16 @@ class Field(ctypes.Structure):
                 ("count", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
+class Cond(ctypes.Structure):
+    """xdrg_cond: field `field` present iff (value(disc) in values) != negate."""
+    _fields_ = [("field", ctypes.c_uint32), ("disc", ctypes.c_uint32), ("negate", ctypes.c_uint32),
+                ("nvalues", ctypes.c_uint32), ("values", ctypes.c_void_p)]
+
+
+MAX_DISC = 8
+MAX_CASES = 64
+
+
 class Column(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("stride", ctypes.c_int64),
                 ("offsets", ctypes.c_void_p), ("cap", ctypes.c_uint64)]
@@ -87,6 +97,9 @@ FUNCTIONS = {
     "xdrg_ctx_reset_stats": (ctypes.c_int, [_P]),
     "xdrg_schema_create": (ctypes.c_int, [ctypes.POINTER(Field), ctypes.c_size_t,
                                           ctypes.POINTER(_P)]),
+    "xdrg_schema_create_cond": (ctypes.c_int, [ctypes.POINTER(Field), ctypes.c_size_t,
+                                               ctypes.POINTER(Cond), ctypes.c_size_t,
+                                               ctypes.POINTER(_P)]),
     "xdrg_schema_destroy": (ctypes.c_int, [_P]),
     "xdrg_schema_fixed_size": (ctypes.c_uint64, [_P]),
     "xdrg_encode_batch": (ctypes.c_int, [_P, _P, ctypes.POINTER(Column), _U64, _P, _U64, _P,

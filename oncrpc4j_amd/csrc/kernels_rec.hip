@@ -47,6 +47,49 @@ __device__ __forceinline__ uint64_t dyn_xdr_bytes(const VField &f, uint64_t cnt)
     return 4 + (f.xsz == 1 ? cnt + pad4(cnt) : cnt * f.xsz);
 }
 
+// ---- conditional fields (rpcgen unions / optional data, xdrg_cond) ----------
+// Field k with f.cond = d + 1 is present iff field d is present and d's value
+// is / is not in its case list: the switch jrpcgen emits for a union
+// (jrpcgen.java:1240-1340; no matching arm and no default = nothing) and the
+// bool-then-value of optional data.  Discriminant values live in up to
+// XDRG_MAX_DISC slots; slot indices are uniform, so the selects below are
+// unrolled over constant register indices (no scratch).
+struct Disc {
+    uint32_t pres;              // bit k: field k present in this record
+    int32_t v[XDRG_MAX_DISC];
+    __device__ __forceinline__ int32_t get(uint32_t slot) const {
+        int32_t r = 0;
+#pragma unroll
+        for (int i = 0; i < XDRG_MAX_DISC; ++i) if ((uint32_t)i == slot) r = v[i];
+        return r;
+    }
+    __device__ __forceinline__ void set(uint32_t slot, int32_t x) {
+#pragma unroll
+        for (int i = 0; i < XDRG_MAX_DISC; ++i) if ((uint32_t)i == slot) v[i] = x;
+    }
+};
+// Is field k present, given the discriminants seen so far?
+__device__ __forceinline__ bool cond_present(const RecArgs &a, const VField &f, const Disc &dv) {
+    if (!f.cond) return true;
+    const uint32_t d = f.cond - 1;
+    if (!((dv.pres >> d) & 1u)) return false;
+    const int32_t x = dv.get(a.f[d].slot - 1);
+    bool in = false;
+    for (uint32_t i = 0; i < f.cnum; ++i) in |= a.cvals[f.cfirst + i] == x;
+    return in != (f.cneg != 0);
+}
+// Record field k as present with (discriminant) value x; bools count as 0/1
+// (Xdr.java:803-805 encode, :404-407 decode any non-zero = true).
+__device__ __forceinline__ void cond_mark(const VField &f, uint32_t k, int32_t x, Disc &dv) {
+    dv.pres |= 1u << k;
+    if (f.slot) dv.set(f.slot - 1, f.type == XDRG_T_BOOL ? (x != 0) : x);
+}
+// Native value of discriminant field f of record r (encode side).
+__device__ __forceinline__ int32_t disc_native(const VField &f, uint64_t r) {
+    const uint8_t *p = f.data + (int64_t)r * f.stride;
+    return f.type == XDRG_T_BOOL ? (int32_t)(*p != 0) : *(const int32_t *)p;
+}
+
 // ---- element words ---------------------------------------------------------
 // XDR word `half` (0 = first) of one native element at p.
 __device__ __forceinline__ uint32_t enc_elem(uint32_t type, const uint8_t *p, uint32_t half) {
@@ -156,7 +199,23 @@ __global__ __launch_bounds__(1024) void k_scan_rows(uint64_t *sums, uint64_t nbl
 // ===========================================================================
 // Encode
 // ===========================================================================
+// XDR size of record r of a schema with conditional fields (mark included).
+__device__ uint64_t enc_rec_size_cond(const RecArgs &a, uint64_t r) {
+    uint64_t s = a.framed ? 4 : 0;
+    Disc dv;
+    dv.pres = 0;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (!cond_present(a, f, dv)) continue;
+        cond_mark(f, k, f.slot ? disc_native(f, r) : 0, dv);
+        s += f.kind != XDRG_K_DYNAMIC ? (uint64_t)f.xbytes
+                                      : dyn_xdr_bytes(f, f.offsets[r + 1] - f.offsets[r]);
+    }
+    return s;
+}
+
 __device__ __forceinline__ uint64_t enc_rec_size(const RecArgs &a, uint64_t r) {
+    if (a.ncond) return enc_rec_size_cond(a, r);
     uint64_t s = a.fixed_xdr;
     for (uint32_t d = 0; d < a.ndyn; ++d) {
         const VField &f = a.f[a.dyn_idx[d]];
@@ -183,8 +242,14 @@ __device__ void enc_record_wave(const RecArgs &a, uint64_t r, uint64_t pos, uint
             *(uint32_t *)(out + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
         pos += 4;
     }
+    Disc dv;
+    dv.pres = 0;
     for (uint32_t k = 0; k < a.nf; ++k) {
         const VField &f = a.f[k];
+        if (a.ncond) {   // absent union arm / optional value: nothing on the wire
+            if (!cond_present(a, f, dv)) continue;
+            cond_mark(f, k, f.slot ? disc_native(f, r) : 0, dv);
+        }
         if (f.kind != XDRG_K_DYNAMIC) {
             const uint8_t *base = f.data + (int64_t)r * f.stride;
             const uint32_t nw = f.xbytes >> 2;
@@ -290,15 +355,20 @@ __device__ uint32_t walk_record(const RecArgs &a, uint64_t r, uint32_t want, uin
         if (!(m & kLastFrag) || (uint64_t)(m & kSizeMask) != want_len) return XDRG_E_FRAME;
         pos += 4;
     }
+    Disc dv;
+    dv.pres = 0;
     for (uint32_t k = 0; k < a.nf; ++k) {
         const VField &f = a.f[k];
         *sub = 2 * k + 1;
+        if (a.ncond && !cond_present(a, f, dv)) continue;
         if (f.kind != XDRG_K_DYNAMIC) {
             // ensureBytes per element / per opaque (Xdr.java:1028-1032)
             if (e.b - pos < f.xbytes) return XDRG_E_SHORT;
+            if (a.ncond) cond_mark(f, k, f.slot ? (int32_t)ld_be32(a.xdr + pos) : 0, dv);
             pos += f.xbytes;
             continue;
         }
+        if (a.ncond) cond_mark(f, k, 0, dv);
         if (e.b - pos < 4) return XDRG_E_SHORT;  // length word (Xdr.java:171-175)
         const int32_t len = (int32_t)ld_be32(a.xdr + pos);
         pos += 4;
@@ -347,8 +417,24 @@ __device__ void dec_record_wave(const RecArgs &a, uint64_t r, uint32_t upto) {
     const Extent e = rec_extent(a, r);
     uint64_t pos = e.a + (a.framed ? 4 : 0);
     const uint8_t *__restrict__ in = a.xdr;
+    Disc dv;
+    dv.pres = 0;
     for (uint32_t k = 0; k < upto; ++k) {
         const VField &f = a.f[k];
+        if (a.ncond) {
+            if (!cond_present(a, f, dv)) {
+                // absent: a fixed field reads as zero (a fresh rpcgen object's
+                // default); a dynamic one has an empty run (count 0 from the walk)
+                if (f.kind != XDRG_K_DYNAMIC) {
+                    uint8_t *base = f.data + (int64_t)r * f.stride;
+                    const uint32_t nb = f.type == XDRG_T_OPAQUE ? f.count
+                                      : (f.kind == XDRG_K_FIXED ? f.count : 1u) * f.nsz;
+                    for (uint32_t i = lane; i < nb; i += 64) base[i] = 0;
+                }
+                continue;
+            }
+            cond_mark(f, k, f.slot ? (int32_t)ld_be32(in + pos) : 0, dv);
+        }
         if (f.kind != XDRG_K_DYNAMIC) {
             uint8_t *base = f.data + (int64_t)r * f.stride;
             const uint32_t nw = f.xbytes >> 2;
@@ -2041,7 +2127,8 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
         hipLaunchKernelGGL(k_debug_recargs, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
-    const bool grp = a.ndyn <= (uint32_t)kMaxDynLds;
+    // conditional schemas (unions / optional data) take the wave-per-record kernels
+    const bool grp = a.ndyn <= (uint32_t)kMaxDynLds && !a.ncond;
     bool stage = grp && g_rec_kernel == 4;
     for (uint32_t d = 0; d < a.ndyn && stage; ++d)
         stage = stage_type(a.f[a.dyn_idx[d]].type, a.f[a.dyn_idx[d]].xsz);

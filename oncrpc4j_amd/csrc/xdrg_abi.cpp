@@ -31,7 +31,11 @@ struct xdrg_schema {
     std::vector<WordOp> ops;        // fixed schemas: one op per XDR word
     uint64_t fixed_size = 0;        // XDR bytes per record (no dynamic field), else 0
     uint64_t fixed_part = 0;        // XDR bytes of the fixed fields
-    bool has_dyn = false;
+    bool var_size = false;          // records differ in size (dynamic or conditional fields)
+    // conditional fields (xdrg_cond), per field; cvals = all case values
+    std::vector<uint32_t> cond, cneg, cfirst, cnum, slot;
+    std::vector<int32_t> cvals;
+    uint32_t ncond = 0;
     bool stream_types = true;       // every field is word-for-word (int/float/hyper/double/opaque%4)
     uint32_t nwords = 0;
 };
@@ -73,8 +77,10 @@ static uint8_t scalar_op(uint32_t t, bool second_half) {
     }
 }
 
-extern "C" int xdrg_schema_create(const xdrg_field *fields, size_t nfields, xdrg_schema **out) {
+extern "C" int xdrg_schema_create_cond(const xdrg_field *fields, size_t nfields,
+                                       const xdrg_cond *conds, size_t nconds, xdrg_schema **out) {
     if (!out) return XDRG_E_INVAL;
+    if (nconds && !conds) return XDRG_E_INVAL;
     *out = nullptr;
     if (!fields || !nfields || nfields > (size_t)kMaxFields) return XDRG_E_INVAL;
     xdrg_schema *s = new (std::nothrow) xdrg_schema();
@@ -88,7 +94,7 @@ extern "C" int xdrg_schema_create(const xdrg_field *fields, size_t nfields, xdrg
         s->xsz.push_back(xdr_elem_size(f.type));
         s->wpos.push_back((uint32_t)words);
         if (f.kind == XDRG_K_DYNAMIC) {
-            s->has_dyn = true;
+            s->var_size = true;
             s->xbytes.push_back(0);
             s->stream_types = false;
             continue;
@@ -117,10 +123,48 @@ extern "C" int xdrg_schema_create(const xdrg_field *fields, size_t nfields, xdrg
         words += xb / 4;
     }
     s->nwords = (uint32_t)(words < 0xffffffffull ? words : 0xffffffffull);
-    s->fixed_size = s->has_dyn ? 0 : s->fixed_part;
-    if (s->has_dyn || words > kMaxWords) s->ops.clear();
+    s->cond.assign(nfields, 0);
+    s->cneg.assign(nfields, 0);
+    s->cfirst.assign(nfields, 0);
+    s->cnum.assign(nfields, 0);
+    s->slot.assign(nfields, 0);
+    uint32_t nslots = 0;
+    for (size_t i = 0; i < nconds; ++i) {
+        const xdrg_cond &cd = conds[i];
+        const size_t k = cd.field, d = cd.disc;
+        // the discriminant: an earlier scalar int / unsigned / enum / bool
+        // (RFC 4506 §4.15; jrpcgen.java:1240-1340, JrpcgenDeclaration INDIRECTION)
+        if (k >= nfields || d >= k || s->cond[k] || cd.negate > 1 || (cd.nvalues && !cd.values) ||
+            s->cvals.size() + cd.nvalues > (size_t)XDRG_MAX_CASES) {
+            delete s;
+            return XDRG_E_INVAL;
+        }
+        const xdrg_field &df = fields[d];
+        if (df.kind != XDRG_K_SCALAR || (df.type != XDRG_T_INT && df.type != XDRG_T_UINT &&
+                                         df.type != XDRG_T_ENUM && df.type != XDRG_T_BOOL)) {
+            delete s;
+            return XDRG_E_INVAL;
+        }
+        if (!s->slot[d]) {
+            if (nslots == (uint32_t)XDRG_MAX_DISC) { delete s; return XDRG_E_INVAL; }
+            s->slot[d] = ++nslots;
+        }
+        s->cond[k] = (uint32_t)d + 1;
+        s->cneg[k] = cd.negate;
+        s->cfirst[k] = (uint32_t)s->cvals.size();
+        s->cnum[k] = cd.nvalues;
+        for (uint32_t j = 0; j < cd.nvalues; ++j) s->cvals.push_back(cd.values[j]);
+        ++s->ncond;
+    }
+    if (s->ncond) s->var_size = true;   // records of one schema now differ in shape
+    s->fixed_size = s->var_size ? 0 : s->fixed_part;
+    if (s->var_size || words > kMaxWords) s->ops.clear();
     *out = s;
     return XDRG_OK;
+}
+
+extern "C" int xdrg_schema_create(const xdrg_field *fields, size_t nfields, xdrg_schema **out) {
+    return xdrg_schema_create_cond(fields, nfields, nullptr, 0, out);
 }
 
 extern "C" int xdrg_schema_destroy(xdrg_schema *s) {
@@ -345,7 +389,7 @@ static int check_columns(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *c
 // their XDR word positions, 16-byte aligned ends, 2-word types even-aligned.
 static bool stream_eligible(const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
                             const void *xdr, const uint8_t **base_out) {
-    if (s->has_dyn || !s->stream_types || s->ops.empty() || !s->nwords) return false;
+    if (s->var_size || !s->stream_types || s->ops.empty() || !s->nwords) return false;
     if (((n * s->nwords) & 3) != 0) return false;
     const int64_t rec = (int64_t)s->nwords * 4;
     const uint8_t *base = nullptr;
@@ -370,7 +414,7 @@ static bool stream_eligible(const xdrg_schema *s, const xdrg_column *cols, uint6
 // 4-byte aligned.
 static bool framed_stream_eligible(const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
                                    const void *xdr, const uint8_t **base_out) {
-    if (s->has_dyn || !s->stream_types || s->ops.empty() || !s->nwords) return false;
+    if (s->var_size || !s->stream_types || s->ops.empty() || !s->nwords) return false;
     const int64_t rec = (int64_t)s->nwords * 4;
     const uint8_t *base = nullptr;
     for (size_t k = 0; k < s->f.size(); ++k) {
@@ -437,8 +481,15 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
         v.stride = f.kind == XDRG_K_DYNAMIC ? 0 : eff_stride(s, k, cols[k]);
         v.offsets = cols[k].offsets;
         v.cap = cols[k].cap;
+        v.cond = s->cond[k];
+        v.cneg = s->cneg[k];
+        v.cfirst = s->cfirst[k];
+        v.cnum = s->cnum[k];
+        v.slot = s->slot[k];
         if (f.kind == XDRG_K_DYNAMIC) a.dyn_idx[a.ndyn++] = (uint32_t)k;
     }
+    a.ncond = s->ncond;
+    for (size_t i = 0; i < s->cvals.size(); ++i) a.cvals[i] = s->cvals[i];
     a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;
     if (!a.nblocks) a.nblocks = 1;
     const size_t rows = a.ndyn ? a.ndyn : 1;
@@ -469,7 +520,7 @@ extern "C" int xdrg_encode_batch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_c
     int rc = check_columns(c, s, cols, n, false);
     if (rc) return rc;
 
-    if (!s->has_dyn) {
+    if (!s->var_size) {
         const uint64_t stride = s->fixed_size + (framed ? 4 : 0);
         const uint64_t total = n * stride;
         if (n && total / n != stride) return inval(c, "batch size overflows");
@@ -609,11 +660,11 @@ extern "C" int xdrg_decode_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8_
     const bool async = flags & XDRG_ASYNC;
     if (!aligned(in, 4)) return inval(c, "XDR buffer not 4-byte aligned");
     if (n && in_len && !in) return inval(c, "XDR buffer is NULL");
-    if (s->has_dyn && !rec_offsets) return inval(c, "variable-size schema needs record offsets");
+    if (s->var_size && !rec_offsets) return inval(c, "variable-size schema needs record offsets");
     int rc = check_columns(c, s, cols, n, true);
     if (rc) return rc;
 
-    if (!s->has_dyn && !rec_offsets) {
+    if (!s->var_size && !rec_offsets) {
         const uint64_t stride = s->fixed_size + (framed ? 4 : 0);
         const uint64_t total = n * stride;
         if (n && total / n != stride) return inval(c, "batch size overflows");
@@ -847,8 +898,8 @@ static int multi_args(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *s
 static int shard_size_launch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
                              bool framed, uint64_t *size, bool *on_device) {
     *on_device = false;
-    if (!s->has_dyn || n == 0) {
-        *size = s->has_dyn ? 0 : n * (s->fixed_size + (framed ? 4 : 0));
+    if (!s->var_size || n == 0) {
+        *size = s->var_size ? 0 : n * (s->fixed_size + (framed ? 4 : 0));
         return XDRG_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));

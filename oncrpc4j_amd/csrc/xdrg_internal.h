@@ -100,6 +100,14 @@ struct VField {
     int64_t stride;
     uint64_t *offsets;
     uint64_t cap;
+    // conditional fields (xdrg_cond): present iff field cond-1 is present and
+    // its value is (cneg = 0) / is not (cneg = 1) in cvals[cfirst, cfirst + cnum)
+    uint32_t cond;    // 0 = unconditional, else discriminant field index + 1
+    uint32_t cneg;
+    uint32_t cfirst;
+    uint32_t cnum;
+    uint32_t slot;    // 0, or 1 + this field's discriminant value slot
+    uint32_t rsv;
 };
 
 struct RecArgs {
@@ -124,10 +132,12 @@ struct RecArgs {
     uint32_t tile_bytes;       // staged place kernels: LDS tile per sub-batch
     uint32_t big_rec;          // blocks averaging >= big_rec XDR bytes per record take the group
                                // kernels, the others the staged ones (0: one kernel for all)
-    uint32_t rsv1;
+    uint32_t ncond;            // conditional fields in the schema (0: every record has all fields)
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
+    int32_t cvals[XDRG_MAX_CASES];  // case values of the conditional fields
 };
+static_assert(sizeof(RecArgs) <= 4096, "RecArgs must fit the kernel-argument segment");
 
 // Error key: smaller = what a sequential reference decode throws first.
 //   key = record << 16 | sub << 4 | code

@@ -72,15 +72,32 @@ def _raise(code, ctx=None, first_bad=None):
 
 
 class Schema:
-    """A compiled field tape (rpcgen struct body).  fields: [(type, kind, count)]."""
+    """A compiled field tape (rpcgen struct body).  fields: [(type, kind, count)].
 
-    def __init__(self, fields):
+    conds: optional [(field, disc, negate, [case values])] — rpcgen unions and
+    optional data (include/xdrg.h xdrg_cond): field `field` is present iff
+    field `disc` is and (value(disc) in values) != negate."""
+
+    def __init__(self, fields, conds=None):
         self.fields = [tuple(int(x) for x in f) for f in fields]
+        self.conds = [(int(f), int(d), int(n), [int(v) for v in vals])
+                      for f, d, n, vals in (conds or ())]
         arr = (abi.Field * len(self.fields))()
         for i, (t, k, c) in enumerate(self.fields):
             arr[i].type, arr[i].kind, arr[i].count, arr[i].reserved = t, k, c, 0
         h = ctypes.c_void_p()
-        rc = lib().xdrg_schema_create(arr, len(self.fields), ctypes.byref(h))
+        if self.conds:
+            ca = (abi.Cond * len(self.conds))()
+            keep = []
+            for i, (f, d, n, vals) in enumerate(self.conds):
+                v = (ctypes.c_int32 * max(len(vals), 1))(*vals)
+                keep.append(v)
+                ca[i].field, ca[i].disc, ca[i].negate, ca[i].nvalues = f, d, int(n), len(vals)
+                ca[i].values = ctypes.addressof(v)
+            rc = lib().xdrg_schema_create_cond(arr, len(self.fields), ca, len(self.conds),
+                                               ctypes.byref(h))
+        else:
+            rc = lib().xdrg_schema_create(arr, len(self.fields), ctypes.byref(h))
         if rc:
             _raise(rc)
         self._h = h
@@ -96,7 +113,7 @@ class Schema:
 
     @property
     def is_fixed(self):
-        return all(k != abi.K_DYNAMIC for _, k, _ in self.fields)
+        return not self.conds and all(k != abi.K_DYNAMIC for _, k, _ in self.fields)
 
     def __del__(self):
         h = getattr(self, "_h", None)

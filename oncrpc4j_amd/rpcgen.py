@@ -16,12 +16,16 @@ drive the batch engine:
   float, double, quadruple -> double), opaque[n] / opaque<n>, string<n>,
   T[n] / T<n> of base types.
 
-Not expressible as ONE tape (records of the same type would differ in
-shape): unions (jrpcgen.java:1240-1340 encodes the discriminant, then one
-arm), optional data `T *x` (JrpcgenDeclaration.INDIRECTION: a bool, then T
-or nothing) and arrays of structs.  Asking for their tape raises
-NotBatchable naming the declaration; the parsed Union keeps its arms so a
-caller can split a batch by discriminant value.
+Unions (jrpcgen.java:1240-1340 encodes the discriminant, then the arm whose
+case list holds it, the default arm, or nothing) and optional data `T *x`
+(JrpcgenDeclaration.INDIRECTION: a bool, then T or nothing) give records of
+one type different shapes.  Spec.tape() flattens them into one tape plus
+conditions (include/xdrg.h xdrg_cond: field k present iff its discriminant
+field is present and the discriminant's value is / is not in a case list),
+which the engine batches directly (engine.Schema(fields, conds)).
+Spec.fields() keeps the plain-tape contract and raises NotBatchable for
+them.  Still not one tape: arrays of structs / unions (a repeated group)
+and recursive types (linked lists through `T *next`).
 """
 import re
 
@@ -35,7 +39,8 @@ class XdrSyntaxError(ValueError):
 
 
 class NotBatchable(ValueError):
-    """The type's records do not share one field tape (union / optional / array of structs)."""
+    """The type's records do not share one field tape (union / optional / array of
+    structs / recursion); see Spec.tape() for the conditional form."""
 
 
 # ---- lexer ----------------------------------------------------------------------
@@ -130,6 +135,8 @@ class Spec:
             return 0
         if isinstance(v, int):
             return v
+        if v in ("TRUE", "FALSE"):    # bool union case labels (BlobStore.x)
+            return int(v == "TRUE")
         if re.fullmatch(r"-?(0[xX][0-9a-fA-F]+|\d+)", v):
             return _int_literal(v)
         if v in self.consts:
@@ -141,28 +148,23 @@ class Spec:
 
     # ---- tapes --------------------------------------------------------------------
     def fields(self, type_name):
-        """Field tape of one record of `type_name` (structs flattened)."""
-        return self._type_fields(type_name, type_name)
+        """Plain field tape of one record of `type_name` (structs flattened);
+        NotBatchable if the type needs conditions (use tape())."""
+        return self._plain(self.tape(type_name), type_name)
 
-    def _type_fields(self, t, where):
-        if t in BASE or t in ("unsigned",):
-            return [(BASE.get(t, abi.T_INT), abi.K_SCALAR, 0)]
-        if t == "string":
-            return [(abi.T_STRING, abi.K_DYNAMIC, 0)]
-        d = self.types.get(t)
-        if d is None:
-            raise XdrSyntaxError(f"unknown type {t!r} (in {where})")
-        if isinstance(d, Enum):
-            return [(abi.T_ENUM, abi.K_SCALAR, 0)]
-        if isinstance(d, Struct):
-            out = []
-            for decl in d.decls:
-                out += self._decl_fields(decl, f"{where}.{decl.name}")
-            return out
-        if isinstance(d, Union):
-            raise NotBatchable(f"{where}: union {t} switches its arms per record "
-                               f"(jrpcgen.java:1240-1340); split the batch by discriminant")
-        return self._decl_fields(d, where)   # typedef
+    def tape(self, type_name):
+        """(fields, conds) of one record of `type_name`: conds =
+        [(field, disc, negate, values)] for union arms and optional data."""
+        b = _Tape(self)
+        b.type_(type_name, type_name, None, ())
+        return b.result()
+
+    @staticmethod
+    def _plain(tape, where):
+        fields, conds = tape
+        if conds:
+            raise NotBatchable(f"{where}: {fields.reasons[0]}; Spec.tape() gives the conditional tape")
+        return list(fields)
 
     def _elem(self, t, where):
         """Base element type id of an array declaration's element type."""
@@ -176,28 +178,6 @@ class Spec:
         if isinstance(t, tuple):   # ("unsigned", base)
             return t[1]
         raise NotBatchable(f"{where}: array of {t!r} (arrays of structs / unions have no flat tape)")
-
-    def _decl_fields(self, decl, where):
-        if decl.kind == VOID:
-            return []
-        if decl.kind == OPTIONAL:
-            raise NotBatchable(f"{where}: optional data '{decl.type} *{decl.name}' encodes a bool and "
-                               f"then the value or nothing, per record")
-        t = decl.type
-        if t == "opaque":
-            n = self.value(decl.size)
-            return [(abi.T_OPAQUE, abi.K_FIXED if decl.kind == FIXED else abi.K_DYNAMIC,
-                     n if decl.kind == FIXED else 0)]
-        if t == "string":
-            return [(abi.T_STRING, abi.K_DYNAMIC, 0)]
-        if decl.kind == SCALAR:
-            if isinstance(t, tuple):
-                return [(t[1], abi.K_SCALAR, 0)]
-            return self._type_fields(t, where)
-        base = t[1] if isinstance(t, tuple) else self._elem(t, where)
-        if decl.kind == FIXED:
-            return [(base, abi.K_FIXED, self.value(decl.size))]
-        return [(base, abi.K_DYNAMIC, 0)]
 
     # ---- procedures ---------------------------------------------------------------
     def procedures(self):
@@ -213,21 +193,144 @@ class Spec:
         """Argument tape of a call (arguments one after another, jrpcgen
         multi-argument procedures)."""
         p = self.procedures()[(prog, vers, proc)]
-        out = []
-        for i, a in enumerate(p.args):
-            out += self._arg_fields(a, f"{p.name} argument {i}")
-        return out
+        return self._plain(self.args_tape(prog, vers, proc), f"{p.name} arguments")
 
     def result_fields(self, prog, vers, proc):
         p = self.procedures()[(prog, vers, proc)]
-        return self._arg_fields(p.result, f"{p.name} result")
+        return self._plain(self.result_tape(prog, vers, proc), f"{p.name} result")
 
-    def _arg_fields(self, t, where):
+    def args_tape(self, prog, vers, proc):
+        p = self.procedures()[(prog, vers, proc)]
+        b = _Tape(self)
+        for i, a in enumerate(p.args):
+            b.arg(a, f"{p.name} argument {i}")
+        return b.result()
+
+    def result_tape(self, prog, vers, proc):
+        p = self.procedures()[(prog, vers, proc)]
+        b = _Tape(self)
+        b.arg(p.result, f"{p.name} result")
+        return b.result()
+
+
+class _TapeFields(list):
+    """A field list that also remembers why it needed conditions."""
+    reasons = ()
+
+
+class _Tape:
+    """Flattens declarations into (fields, conds) in jrpcgen's encode order
+    (codingMethod, jrpcgen.java:758-913).  `guard` = (disc field index,
+    negate, values) is the condition every field emitted under it carries;
+    nesting chains through the discriminant's own condition."""
+
+    DISC_TYPES = (abi.T_INT, abi.T_UINT, abi.T_ENUM, abi.T_BOOL)
+
+    def __init__(self, spec):
+        self.s = spec
+        self.fields = _TapeFields()
+        self.fields.reasons = []
+        self.conds = []
+
+    def result(self):
+        return self.fields, self.conds
+
+    def add(self, f, guard):
+        k = len(self.fields)
+        self.fields.append(f)
+        if guard is not None:
+            d, neg, vals = guard
+            self.conds.append((k, d, neg, list(vals)))
+        return k
+
+    def arg(self, t, where):
         if t == "void":
-            return []
+            return
         if isinstance(t, tuple):
-            return [(t[1], abi.K_SCALAR, 0)]
-        return self._type_fields(t, where)
+            self.add((t[1], abi.K_SCALAR, 0), None)
+            return
+        self.type_(t, where, None, ())
+
+    def type_(self, t, where, guard, stack):
+        if t in BASE or t in ("unsigned",):
+            self.add((BASE.get(t, abi.T_INT), abi.K_SCALAR, 0), guard)
+            return
+        if t == "string":
+            self.add((abi.T_STRING, abi.K_DYNAMIC, 0), guard)
+            return
+        d = self.s.types.get(t)
+        if d is None:
+            raise XdrSyntaxError(f"unknown type {t!r} (in {where})")
+        if isinstance(d, Enum):
+            self.add((abi.T_ENUM, abi.K_SCALAR, 0), guard)
+            return
+        if isinstance(d, (Struct, Union)):
+            if t in stack:
+                raise NotBatchable(f"{where}: {t} contains itself (a recursive type has no "
+                                   f"bounded tape)")
+            stack = stack + (t,)
+        if isinstance(d, Struct):
+            for decl in d.decls:
+                self.decl(decl, f"{where}.{decl.name}", guard, stack)
+            return
+        if isinstance(d, Union):
+            self.union(d, where, guard, stack)
+            return
+        self.decl(d, where, guard, stack)   # typedef
+
+    def union(self, u, where, guard, stack):
+        # jrpcgen.java:1240-1340: the discriminant, then the matching arm
+        # (several case labels may share one arm), else the default arm, else nothing
+        self.fields.reasons.append(f"union {u.name} switches its arms per record "
+                                   f"(jrpcgen.java:1240-1340)")
+        k = len(self.fields)
+        self.decl(u.disc, f"{where}.{u.disc.name}", guard, stack)
+        if len(self.fields) != k + 1 or self.fields[k][1] != abi.K_SCALAR or \
+                self.fields[k][0] not in self.DISC_TYPES:
+            raise NotBatchable(f"{where}: union {u.name} discriminant is not an int / unsigned / "
+                               f"enum / bool")
+        every = []
+        for labels, d in u.arms:
+            vals = [self.s.value(v) for v in labels]
+            every += vals
+            self.decl(d, where, (k, False, vals), stack)
+        if u.default is not None:
+            self.decl(u.default, where, (k, True, every), stack)
+
+    def decl(self, decl, where, guard, stack):
+        if decl.kind == VOID:
+            return
+        if decl.kind == OPTIONAL:
+            # T *x: xdrEncodeBoolean(x != null), then x (JrpcgenDeclaration.INDIRECTION)
+            self.fields.reasons.append(f"optional data '{decl.type} *{decl.name}' encodes a bool "
+                                       f"and then the value or nothing, per record")
+            k = self.add((abi.T_BOOL, abi.K_SCALAR, 0), guard)
+            t = decl.type
+            if isinstance(t, tuple):
+                self.add((t[1], abi.K_SCALAR, 0), (k, True, [0]))
+            else:
+                self.type_(t, where, (k, True, [0]), stack)
+            return
+        t = decl.type
+        if t == "opaque":
+            n = self.s.value(decl.size)
+            self.add((abi.T_OPAQUE, abi.K_FIXED if decl.kind == FIXED else abi.K_DYNAMIC,
+                      n if decl.kind == FIXED else 0), guard)
+            return
+        if t == "string":
+            self.add((abi.T_STRING, abi.K_DYNAMIC, 0), guard)
+            return
+        if decl.kind == SCALAR:
+            if isinstance(t, tuple):
+                self.add((t[1], abi.K_SCALAR, 0), guard)
+            else:
+                self.type_(t, where, guard, stack)
+            return
+        base = t[1] if isinstance(t, tuple) else self.s._elem(t, where)
+        if decl.kind == FIXED:
+            self.add((base, abi.K_FIXED, self.s.value(decl.size)), guard)
+        else:
+            self.add((base, abi.K_DYNAMIC, 0), guard)
 
 
 # ---- parser ---------------------------------------------------------------------

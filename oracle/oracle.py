@@ -24,6 +24,11 @@ class Field(ctypes.Structure):
                 ("count", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
+class Cond(ctypes.Structure):
+    _fields_ = [("field", ctypes.c_uint32), ("disc", ctypes.c_uint32), ("negate", ctypes.c_uint32),
+                ("nvalues", ctypes.c_uint32), ("values", ctypes.c_void_p)]
+
+
 class Column(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("stride", ctypes.c_int64),
                 ("offsets", ctypes.c_void_p), ("cap", ctypes.c_uint64)]
@@ -74,6 +79,10 @@ _SIGS = {
     "xo_fragment": (_SZ, [_P, _SZ, _SZ, _P, _SZ]),
     "xo_encode_batch": (ctypes.c_int, [_PF, _SZ, _PC, _U64, _P, _U64, _P, ctypes.c_uint32, _P]),
     "xo_decode_batch": (ctypes.c_int, [_PF, _SZ, _P, _U64, _P, _U64, _PC, ctypes.c_uint32, _P, _P]),
+    "xo_encode_batch_cond": (ctypes.c_int, [_PF, _SZ, _P, _SZ, _PC, _U64, _P, _U64, _P,
+                                            ctypes.c_uint32, _P]),
+    "xo_decode_batch_cond": (ctypes.c_int, [_PF, _SZ, _P, _SZ, _P, _U64, _P, _U64, _PC,
+                                            ctypes.c_uint32, _P, _P]),
     "xo_encode_batch_mt": (ctypes.c_int, [_PF, _SZ, _PC, _U64, _P, _U64, ctypes.c_uint32, _P,
                                           ctypes.c_int]),
     "xo_decode_batch_mt": (ctypes.c_int, [_PF, _SZ, _P, _U64, _U64, _PC, ctypes.c_uint32, _P, _P,
@@ -109,30 +118,50 @@ def fields_array(fields):
     return arr
 
 
-def encode_batch(fields, cols, n, out_cap, framed=False):
+def conds_array(conds):
+    """[(field, disc, negate, [values])] -> (ctypes xdrg_cond array or None, keep-alive)."""
+    if not conds:
+        return None, None
+    arr = (Cond * len(conds))()
+    keep = []
+    for i, (f, d, neg, vals) in enumerate(conds):
+        v = (ctypes.c_int32 * max(len(vals), 1))(*vals)
+        keep.append(v)
+        arr[i].field, arr[i].disc, arr[i].negate, arr[i].nvalues = f, d, int(neg), len(vals)
+        arr[i].values = ctypes.addressof(v)
+    return arr, keep
+
+
+def encode_batch(fields, cols, n, out_cap, framed=False, conds=None):
     """-> (status, xdr bytes, record offsets[n+1])"""
     import numpy as np
     L = lib()
     fa = fields_array(fields)
+    ca, keep = conds_array(conds)
     out = np.zeros(max(out_cap, 1), dtype=np.uint8)
     offs = np.zeros(n + 1, dtype=np.uint64)
     out_len = _U64(0)
-    rc = L.xo_encode_batch(fa, len(fields), ctypes.addressof(cols), n, out.ctypes.data, out_cap,
-                           offs.ctypes.data, FRAME_RM if framed else 0, ctypes.byref(out_len))
+    rc = L.xo_encode_batch_cond(fa, len(fields), ca, len(conds or ()), ctypes.addressof(cols), n,
+                                out.ctypes.data, out_cap, offs.ctypes.data,
+                                FRAME_RM if framed else 0, ctypes.byref(out_len))
+    del keep
     return rc, out[:out_len.value].tobytes() if rc == OK else b"", offs
 
 
-def decode_batch(fields, xdr, rec_offsets, n, cols, framed=False):
+def decode_batch(fields, xdr, rec_offsets, n, cols, framed=False, conds=None):
     """-> (status, first_bad, err); cols (host Column array) receives the values."""
     import numpy as np
     L = lib()
     fa = fields_array(fields)
+    ca, keep = conds_array(conds)
     buf = np.frombuffer(xdr, dtype=np.uint8) if len(xdr) else np.zeros(1, np.uint8)
     fb = _U64(0)
     err = ctypes.c_int(0)
     ro = rec_offsets.ctypes.data if rec_offsets is not None else None
-    rc = L.xo_decode_batch(fa, len(fields), buf.ctypes.data, len(xdr), ro, n, ctypes.addressof(cols),
-                           FRAME_RM if framed else 0, ctypes.byref(fb), ctypes.byref(err))
+    rc = L.xo_decode_batch_cond(fa, len(fields), ca, len(conds or ()), buf.ctypes.data, len(xdr), ro,
+                                n, ctypes.addressof(cols), FRAME_RM if framed else 0,
+                                ctypes.byref(fb), ctypes.byref(err))
+    del keep
     return rc, fb.value, err.value
 
 

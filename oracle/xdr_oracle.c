@@ -390,12 +390,55 @@ static inline const uint8_t *fixed_ptr(const xdrg_field *f, const xdrg_column *c
 
 /* One record's fields, in declaration order, through the stream encoders —
  * what an rpcgen XdrAble.xdrEncode does (jrpcgen.java:788-808).              */
+/* Conditional fields (include/xdrg.h xdrg_cond): what rpcgen emits for a
+ * union — `switch (disc) { case v: arm; ... default: arm }` with no code for
+ * an unmatched value (jrpcgen.java:1240-1340) — and for optional data, a
+ * bool and then the value (JrpcgenDeclaration INDIRECTION).  cond_of[k]
+ * points at field k's condition or is NULL.                                 */
+typedef struct { const xdrg_cond *cond_of[64]; } xo_conds;
+
+static int cond_table(const xdrg_field *fs, size_t nf, const xdrg_cond *conds, size_t nc,
+                      xo_conds *t) {
+    memset(t, 0, sizeof *t);
+    if (nf > 64) return nc ? XDRG_E_INVAL : XDRG_OK;
+    for (size_t i = 0; i < nc; i++) {
+        const xdrg_cond *c = &conds[i];
+        if (c->field >= nf || c->disc >= c->field || t->cond_of[c->field]) return XDRG_E_INVAL;
+        const xdrg_field *d = &fs[c->disc];
+        if (d->kind != XDRG_K_SCALAR || !(d->type == XDRG_T_INT || d->type == XDRG_T_UINT ||
+                                          d->type == XDRG_T_ENUM || d->type == XDRG_T_BOOL))
+            return XDRG_E_INVAL;
+        t->cond_of[c->field] = c;
+    }
+    return XDRG_OK;
+}
+/* Is field k present, given the presence and values of the fields before it? */
+static int present(const xo_conds *t, size_t k, const int *pres, const int32_t *val) {
+    const xdrg_cond *c = t ? t->cond_of[k] : NULL;
+    if (!c) return 1;
+    if (!pres[c->disc]) return 0;
+    int in = 0;
+    for (uint32_t j = 0; j < c->nvalues; j++) in |= c->values[j] == val[c->disc];
+    return in != (c->negate != 0);
+}
+
 static int encode_record(xo_stream *s, const xdrg_field *fs, size_t nf, const xdrg_column *cols,
-                         uint64_t i) {
+                         uint64_t i, const xo_conds *cc) {
+    int pres[64]; int32_t val[64];
     for (size_t k = 0; k < nf; k++) {
         const xdrg_field *f = &fs[k];
         const xdrg_column *c = &cols[k];
         int rc = XDRG_OK;
+        if (k < 64) {
+            pres[k] = present(cc, k, pres, val);
+            if (!pres[k]) continue;
+            val[k] = 0;
+            if (f->kind == XDRG_K_SCALAR) {
+                const uint8_t *p = fixed_ptr(f, c, i);
+                if (f->type == XDRG_T_BOOL) val[k] = *p != 0;
+                else if (native_size(f->type) == 4) memcpy(&val[k], p, 4);
+            }
+        }
         if (f->kind == XDRG_K_DYNAMIC) {
             uint64_t a = c->offsets[i], b = c->offsets[i + 1];
             const uint8_t *base = (const uint8_t *)c->data + a * native_size(f->type);
@@ -457,7 +500,14 @@ static int check_schema(const xdrg_field *fs, size_t nf) {
 int xo_encode_batch(const xdrg_field *fs, size_t nf, const xdrg_column *cols, uint64_t n,
                     uint8_t *out, uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags,
                     uint64_t *out_len) {
+    return xo_encode_batch_cond(fs, nf, NULL, 0, cols, n, out, out_cap, rec_offsets, flags, out_len);
+}
+int xo_encode_batch_cond(const xdrg_field *fs, size_t nf, const xdrg_cond *conds, size_t nconds,
+                         const xdrg_column *cols, uint64_t n, uint8_t *out, uint64_t out_cap,
+                         uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len) {
     int rc = check_schema(fs, nf); if (rc) return rc;
+    xo_conds cc;
+    rc = cond_table(fs, nf, conds, nconds, &cc); if (rc) return rc;
     const int framed = (flags & XDRG_FRAME_RM) != 0;
     uint64_t pos = 0;
     for (uint64_t i = 0; i < n; i++) {
@@ -469,7 +519,7 @@ int xo_encode_batch(const xdrg_field *fs, size_t nf, const xdrg_column *cols, ui
         xo_stream s;
         xo_stream_wrap(&s, out + body, (size_t)(out_cap - body));
         xo_begin_encoding(&s);
-        rc = encode_record(&s, fs, nf, cols, i);
+        rc = encode_record(&s, fs, nf, cols, i, nconds ? &cc : NULL);
         if (rc) return rc;
         xo_end_encoding(&s);
         /* ... and framed as GrizzlyRpcTransport.sendDefault does (:103-110). */
@@ -483,11 +533,28 @@ int xo_encode_batch(const xdrg_field *fs, size_t nf, const xdrg_column *cols, ui
 
 /* One record's fields through the stream decoders (XdrAble.xdrDecode). */
 static int decode_record(xo_stream *s, const xdrg_field *fs, size_t nf, xdrg_column *cols,
-                         uint64_t i) {
+                         uint64_t i, const xo_conds *cc) {
+    int pres[64]; int32_t val[64];
     for (size_t k = 0; k < nf; k++) {
         const xdrg_field *f = &fs[k];
         xdrg_column *c = &cols[k];
         int rc = XDRG_OK;
+        if (k < 64) {
+            pres[k] = present(cc, k, pres, val);
+            val[k] = 0;
+            if (pres[k] && f->kind == XDRG_K_SCALAR && xo_remaining(s) >= 4) {
+                int32_t w = (int32_t)get_be32(s->buf + s->pos);   /* the value about to decode */
+                val[k] = f->type == XDRG_T_BOOL ? (w != 0) : w;
+            }
+            if (!pres[k]) {   /* absent: the defaults of a new rpcgen object */
+                if (f->kind == XDRG_K_DYNAMIC) c->offsets[i + 1] = c->offsets[i];
+                else {
+                    size_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
+                    memset((uint8_t *)fixed_ptr(f, c, i), 0, cnt * native_size(f->type));
+                }
+                continue;
+            }
+        }
         if (f->kind == XDRG_K_DYNAMIC) {
             size_t es = native_size(f->type);
             uint64_t a = c->offsets[i];
@@ -556,9 +623,18 @@ static uint64_t schema_fixed_size(const xdrg_field *fs, size_t nf) {
 int xo_decode_batch(const xdrg_field *fs, size_t nf, const uint8_t *in, uint64_t in_len,
                     const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
                     uint64_t *first_bad, int *err) {
+    return xo_decode_batch_cond(fs, nf, NULL, 0, in, in_len, rec_offsets, n, cols, flags,
+                                first_bad, err);
+}
+int xo_decode_batch_cond(const xdrg_field *fs, size_t nf, const xdrg_cond *conds, size_t nconds,
+                         const uint8_t *in, uint64_t in_len, const uint64_t *rec_offsets,
+                         uint64_t n, xdrg_column *cols, uint32_t flags, uint64_t *first_bad,
+                         int *err) {
     int rc = check_schema(fs, nf); if (rc) return rc;
+    xo_conds cc;
+    rc = cond_table(fs, nf, conds, nconds, &cc); if (rc) return rc;
     const int framed = (flags & XDRG_FRAME_RM) != 0;
-    const uint64_t fixed = schema_fixed_size(fs, nf);
+    const uint64_t fixed = nconds ? 0 : schema_fixed_size(fs, nf);
     if (!rec_offsets && !fixed) return XDRG_E_INVAL;
     for (size_t k = 0; k < nf; k++)
         if (fs[k].kind != XDRG_K_DYNAMIC && cols[k].stride == XDRG_STRIDE_CONST) return XDRG_E_INVAL;
@@ -586,7 +662,7 @@ int xo_decode_batch(const xdrg_field *fs, size_t nf, const uint8_t *in, uint64_t
             xo_stream s;
             xo_stream_wrap(&s, (uint8_t *)in + a, (size_t)(b - a));
             xo_begin_decoding(&s);
-            rc = decode_record(&s, fs, nf, cols, i);
+            rc = decode_record(&s, fs, nf, cols, i, nconds ? &cc : NULL);
         }
         if (rc) {
             if (first_bad) *first_bad = i;

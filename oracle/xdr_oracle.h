@@ -126,6 +126,16 @@ int xo_encode_batch(const xdrg_field *fields, size_t nfields, const xdrg_column 
 int xo_decode_batch(const xdrg_field *fields, size_t nfields, const uint8_t *in,
                     uint64_t in_len, const uint64_t *rec_offsets, uint64_t n,
                     xdrg_column *cols, uint32_t flags, uint64_t *first_bad, int *err);
+/* Same, with conditional fields (include/xdrg.h xdrg_cond: rpcgen unions
+ * and optional data, jrpcgen.java:1240-1340).                               */
+int xo_encode_batch_cond(const xdrg_field *fields, size_t nfields, const xdrg_cond *conds,
+                         size_t nconds, const xdrg_column *cols, uint64_t n, uint8_t *out,
+                         uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags,
+                         uint64_t *out_len);
+int xo_decode_batch_cond(const xdrg_field *fields, size_t nfields, const xdrg_cond *conds,
+                         size_t nconds, const uint8_t *in, uint64_t in_len,
+                         const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols,
+                         uint32_t flags, uint64_t *first_bad, int *err);
 /* Same, split over `threads` POSIX threads by contiguous record ranges (each
  * range encodes into its own slice; fixed-size schemas only for encode).  The
  * all-cores CPU baseline of SURVEY.md §8(d).                                  */

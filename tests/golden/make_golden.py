@@ -207,6 +207,89 @@ def xdrlib_vectors(seed=0x0DCAC4E5):
     return out
 
 
+# ---- unions and optional data (xdrg_cond) ------------------------------------
+# Tapes with conditional fields, as rpcgen flattens them (jrpcgen.java:1240-1340:
+# encode the discriminant, then the matching arm, the default arm or nothing;
+# optional data `T *x`: a bool, then T if true).  cond = (field, disc, negate, values).
+COND_SCHEMAS = {
+    # union switch (int status) { case 0: struct {int a; hyper b; string s<>;} ok; default: void; }
+    "result_union": ([[T_INT, K_SCALAR, 0], [T_INT, K_SCALAR, 0], [T_HYPER, K_SCALAR, 0],
+                      [T_STRING, K_DYNAMIC, 0]],
+                     [(1, 0, 0, [0]), (2, 0, 0, [0]), (3, 0, 0, [0])]),
+    # union switch (enum kind) { case 1: case 2: int x; case 3: opaque o<>; case 4: void;
+    #                            default: double d; }
+    "multi_arm": ([[T_ENUM, K_SCALAR, 0], [T_INT, K_SCALAR, 0], [T_OPAQUE, K_DYNAMIC, 0],
+                   [T_DOUBLE, K_SCALAR, 0]],
+                  [(1, 0, 0, [1, 2]), (2, 0, 0, [3]), (3, 0, 1, [1, 2, 3, 4])]),
+    # struct { int id; entry *next; }  entry = struct { unsigned v; string name<>; }
+    "optional": ([[T_INT, K_SCALAR, 0], [T_BOOL, K_SCALAR, 0], [T_UINT, K_SCALAR, 0],
+                  [T_STRING, K_DYNAMIC, 0]],
+                 [(2, 1, 1, [0]), (3, 1, 1, [0])]),
+    # struct { int a; u *opt; int tail; }  u = union switch (enum k) { case 7: int x;
+    #                                                  default: string s<>; }
+    "nested": ([[T_INT, K_SCALAR, 0], [T_BOOL, K_SCALAR, 0], [T_ENUM, K_SCALAR, 0],
+                [T_INT, K_SCALAR, 0], [T_STRING, K_DYNAMIC, 0], [T_INT, K_SCALAR, 0]],
+               [(2, 1, 1, [0]), (3, 2, 0, [7]), (4, 2, 1, [7])]),
+    # union switch (bool b) { case TRUE: int x<>; case FALSE: hyper h; }
+    "bool_union": ([[T_BOOL, K_SCALAR, 0], [T_INT, K_DYNAMIC, 0], [T_HYPER, K_SCALAR, 0]],
+                   [(1, 0, 0, [1]), (2, 0, 0, [0])]),
+    # fixed-size arms only: union switch (int d) { case 5: int v[3]; default: short s; }
+    # then opaque tag[6]
+    "fixed_arms": ([[T_INT, K_SCALAR, 0], [T_INT, K_FIXED, 3], [T_SHORT, K_SCALAR, 0],
+                    [T_OPAQUE, K_FIXED, 6]],
+                   [(1, 0, 0, [5]), (2, 0, 1, [5])]),
+}
+
+
+def cond_present(conds, disc_vals, k, pres):
+    for f, d, neg, vals in conds:
+        if f == k:
+            return pres[d] and ((disc_vals[d] in vals) != bool(neg))
+    return True
+
+
+def cond_vectors(seed=0xC0ED):
+    rng = random.Random(seed)
+    out = {"source": "CPython 3.10 stdlib xdrlib (RFC 1014), union / optional encodings in the "
+                     "order jrpcgen emits them (jrpcgen.java:1240-1340)", "seed": seed, "batches": []}
+    for name, (fields, conds) in COND_SCHEMAS.items():
+        case_vals = sorted({v for _, _, _, vals in conds for v in vals})
+        for framed in (False, True):
+            n = 24
+            records, present = [], []
+            chunks = []
+            for i in range(n):
+                rec = [rand_value(rng, t, k, c) for t, k, c in fields]
+                for _, d, _, _ in conds:   # discriminants: mostly case values, some others
+                    if fields[d][0] == T_BOOL:
+                        rec[d] = rng.randint(0, 1)
+                    else:
+                        rec[d] = rng.choice(case_vals + [case_vals[-1] + 1 + rng.randrange(9), -3])
+                p = xdrlib.Packer()
+                pres, dv = [], {}
+                for k, ((t, kd, c), v) in enumerate(zip(fields, rec)):
+                    ok = cond_present(conds, dv, k, pres)
+                    pres.append(ok)
+                    if ok:
+                        pack_value(p, t, kd, c, v)
+                        if kd == K_SCALAR and t in (T_INT, T_UINT, T_ENUM, T_BOOL):
+                            dv[k] = int(v != 0) if t == T_BOOL else v
+                body = p.get_buffer()
+                if framed:
+                    body = struct.pack(">I", len(body) | 0x80000000) + body
+                chunks.append(body)
+                records.append(rec)
+                present.append(pres)
+            offs = [0]
+            for ch in chunks:
+                offs.append(offs[-1] + len(ch))
+            out["batches"].append({"name": name, "framed": framed, "fields": fields,
+                                   "conds": [list(c) for c in conds], "n": n, "records": records,
+                                   "present": present, "xdr": b"".join(chunks).hex(),
+                                   "rec_offsets": offs})
+    return out
+
+
 # ---- framing -----------------------------------------------------------------
 def call_message(xid, args_string):
     """RpcMessageParserTCPTest.XdrStreamBuilder.build (:127-142): CALL header,
@@ -349,7 +432,8 @@ def rpc_vectors(seed=0x5EED):
 def main():
     for name, obj in (("kat_reference.json", kat_reference()), ("kat_jdk_nan.json", kat_jdk_nan()),
                       ("xdrlib_vectors.json", xdrlib_vectors()), ("framing.json", framing()),
-                      ("rpc_vectors.json", rpc_vectors())):
+                      ("rpc_vectors.json", rpc_vectors()),
+                      ("cond_vectors.json", cond_vectors())):
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1)
             f.write("\n")

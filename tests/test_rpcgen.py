@@ -195,3 +195,145 @@ def test_calculator_calls_decode_with_generated_tape(gpu_ctx):
     assert st == (0, n, 0)
     hb = batch.to_host()
     assert np.array_equal(hb.arrays[10], a) and np.array_equal(hb.arrays[11], b)
+
+
+# ---- conditional tapes: unions and optional data (Spec.tape) -------------------------
+def _walk(s, t, vals, emit, p):
+    """Consume one value per tape field of type t (in tape order) and pack the
+    ones the generated xdrEncode would write: a union packs its discriminant
+    and the matching arm / default arm (jrpcgen.java:1240-1340), optional
+    data packs a bool and the value if true (INDIRECTION)."""
+    d = s.types.get(t)
+    if isinstance(d, rpcgen.Union):
+        disc = vals[0]
+        _walk_decl(s, d.disc, vals, emit, p)
+        hit = False
+        for labels, arm in d.arms:
+            m = disc in [s.value(v) for v in labels]
+            hit |= m
+            _walk_decl(s, arm, vals, emit and m, p)
+        if d.default is not None:
+            _walk_decl(s, d.default, vals, emit and not hit, p)
+        return
+    if isinstance(d, rpcgen.Struct):
+        for sub in d.decls:
+            _walk_decl(s, sub, vals, emit, p)
+        return
+    _walk_decl(s, rpcgen.Decl("x", t, rpcgen.SCALAR), vals, emit, p)
+
+
+class _Null:
+    def __getattr__(self, name):
+        return lambda *a, **k: None
+
+
+def _walk_decl(s, decl, vals, emit, p):
+    if decl.kind == rpcgen.VOID:
+        return
+    if decl.kind == rpcgen.OPTIONAL:
+        present = vals[0] != 0
+        v = vals.pop(0)
+        (p if emit else _Null()).pack_bool(bool(v))
+        _walk(s, decl.type, vals, emit and present, p)
+        return
+    t = decl.type
+    if isinstance(t, str) and isinstance(s.types.get(t), (rpcgen.Union, rpcgen.Struct)) \
+            and decl.kind == rpcgen.SCALAR:
+        _walk(s, t, vals, emit, p)
+        return
+    if isinstance(t, str) and isinstance(s.types.get(t), rpcgen.Decl) and decl.kind == rpcgen.SCALAR:
+        td = s.types[t]
+        _walk_decl(s, rpcgen.Decl(decl.name, td.type, td.kind, td.size), vals, emit, p)
+        return
+    _pack_decl(s, p if emit else _Null(), decl, vals)
+
+
+def _cond_batch(fields, conds, n, seed):
+    hb = random_batch(fields, n, seed=seed, dyn_len=(0, 9), special_floats=False)
+    rng = np.random.default_rng(seed)
+    for k, (t, kind, c) in enumerate(fields):
+        if t == B:
+            hb.arrays[k][:] = rng.integers(0, 2, n, dtype=np.uint8)
+        elif t == E and kind == SC:   # enums / int discriminants take their case values mostly
+            hb.arrays[k][:] = rng.choice(np.array([0, 1, 2, 5, 9], np.int32), n)
+    for _, d, _, _ in conds:
+        if fields[d][0] == I:
+            hb.arrays[d][:] = rng.choice(np.array([0, 0, 1, 70], np.int32), n)
+    return hb
+
+
+@pytest.mark.parametrize("type_name", ["lookup_res", "entry", "kind_res", "listing"])
+def test_conditional_tape_matches_generated_encode(type_name):
+    s = spec("batch_types.x")
+    with pytest.raises(rpcgen.NotBatchable):
+        s.fields(type_name)
+    fields, conds = s.tape(type_name)
+    n = 200
+    hb = _cond_batch(fields, conds, n, seed=5)
+    rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total() + 8, conds=conds)
+    assert rc == 0
+    for i in range(n):
+        p = xdrlib.Packer()
+        vals = _record_values(fields, hb, i)
+        _walk(s, type_name, vals, True, p)
+        assert not vals
+        assert xdr[offs[i]:offs[i + 1]] == p.get_buffer(), f"record {i}"
+
+
+def test_conditional_tape_shapes():
+    s = spec("batch_types.x")
+    f, c = s.tape("lookup_res")
+    assert f == [(I, SC, 0)] + FATTR and c == [(k, 0, False, [0]) for k in range(1, 11)]
+    f, c = s.tape("kind_res")
+    # kind, size (REG|LNK), entry{id, name, bool, seconds, useconds} (DIR), why (default)
+    assert f == [(E, SC, 0), (H, SC, 0), (U, SC, 0), (STR, DY, 0), (B, SC, 0), (U, SC, 0), (U, SC, 0),
+                 (STR, DY, 0)]
+    assert c == [(1, 0, False, [1, 5]), (2, 0, False, [2]), (3, 0, False, [2]), (4, 0, False, [2]),
+                 (5, 4, True, [0]), (6, 4, True, [0]), (7, 0, True, [1, 5, 2])]
+    f, c = s.args_tape(400123, 1, 7)           # LIST(fhandle, kind_res): arguments back to back
+    assert f[0] == (O, FX, 32) and c[0] == (2, 1, False, [1, 5])
+    with pytest.raises(rpcgen.NotBatchable, match="contains itself"):
+        s.tape("optional_next")
+
+
+def test_blobstore_put_tape():
+    """The reference's own rpcgen input: put(Key, Value) with a bool union."""
+    s = spec("BlobStore.x")
+    f, c = s.args_tape(118, 1, 1)             # put
+    assert f == [(O, DY, 0), (B, SC, 0), (O, DY, 0)] and c == [(2, 1, False, [1])]
+
+
+@pytest.mark.gpu
+def test_gpu_blobstore_put_args(gpu_ctx):
+    """BlobStore put(Key, Value) argument batches through the engine with the
+    conditional tape, checked against xdrlib packing of the generated order."""
+    import torch
+    from oncrpc4j_amd import engine
+    from oncrpc4j_amd.columns import DeviceBatch, HostBatch
+    s = spec("BlobStore.x")
+    fields, conds = s.args_tape(118, 1, 1)
+    n = 5000
+    hb = _cond_batch(fields, conds, n, seed=118)
+    want = b""
+    offs = [0]
+    for i in range(n):
+        p = xdrlib.Packer()
+        vals = _record_values(fields, hb, i)
+        _walk(s, "Key", vals, True, p)
+        _walk(s, "Value", vals, True, p)
+        want += p.get_buffer()
+        offs.append(len(want))
+    sch = engine.Schema(fields, conds)
+    db = DeviceBatch.from_host(hb)
+    out = torch.zeros(hb.xdr_total(), dtype=torch.uint8, device="cuda")
+    ro = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    ln = gpu_ctx.encode(sch, db.columns(), n, out, hb.xdr_total(), rec_offsets=ro)
+    assert out[:ln].cpu().numpy().tobytes() == want
+    assert ro.cpu().tolist() == offs
+    back = DeviceBatch.empty(fields, n, hb.dyn_caps())
+    rc, fb, err = gpu_ctx.decode(sch, out, ln, n, back.columns(), rec_offsets=ro)
+    assert (rc, fb, err) == (0, n, 0)
+    ref = HostBatch.empty(fields, n, hb.dyn_caps())
+    assert oracle.decode_batch(fields, want, np.array(offs, np.uint64), n, ref.columns(),
+                               conds=conds) == (0, n, 0)
+    assert back.to_host().equal(ref)
