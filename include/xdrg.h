@@ -226,6 +226,42 @@ int  xdrg_decode_batch(xdrg_ctx *ctx, const xdrg_schema *schema,
                        xdrg_column *cols, uint32_t flags,
                        uint64_t *first_bad, int *err);
 
+/* ---- zero-copy payloads -------------------------------------
+ * Send side — xdrEncodeFileChunk (xdr/Xdr.java:978-988) and
+ * xdrEncodeShallowByteBuffer (:839-866): the payload of one dynamic
+ * OPAQUE/STRING field per record is encoded BY REFERENCE.  The device writes
+ * every other byte of each message (the length word included) into `out`;
+ * the payload and its zero padding stay where they are and go out as their
+ * own writable messages, as asBufferWritableMessages (:579-597) and
+ * GrizzlyRpcTransport.sendRawTCP (grizzly/GrizzlyRpcTransport.java:130-168)
+ * do.  Message i on the wire is
+ *     out[rec_offsets[i], splice[i])  payload(i)  zero pad(len_i)  out[splice[i], rec_offsets[i+1])
+ * with len_i = offsets[i+1] - offsets[i] of the field's column, pad =
+ * (4 - (len & 3)) & 3.  splice[i] = UINT64_MAX when the field is absent
+ * (conditional schemas): the message is out[rec_offsets[i], rec_offsets[i+1]).
+ * The field column's `data` is never dereferenced (it may be a host
+ * buffer, a file mapping or NULL); its `offsets` must be device memory.
+ * With XDRG_FRAME_RM each mark counts every part (sendRawTCP :135-139,
+ * getMessagesSize :224-231).  splice: device array of n entries.            */
+int  xdrg_encode_batch_shallow(xdrg_ctx *ctx, const xdrg_schema *schema,
+                               const xdrg_column *cols, uint64_t n,
+                               uint8_t *out, uint64_t out_cap,
+                               uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len,
+                               uint32_t field, uint64_t *splice);
+
+/* Receive side — xdrDecodeByteBuffer (xdr/Xdr.java:423-439): the payload of
+ * one dynamic OPAQUE/STRING field per record is returned as a slice of the
+ * stream instead of a copy.  payload_pos[i] (device, n entries) = offset in
+ * `in` of record i's payload (UINT64_MAX if absent); the column's offsets
+ * are written as for a copy (len_i = offsets[i+1] - offsets[i]); its data
+ * and cap are ignored.  Checks and error parity as xdrg_decode_batch.       */
+int  xdrg_decode_batch_view(xdrg_ctx *ctx, const xdrg_schema *schema,
+                            const uint8_t *in, uint64_t in_len,
+                            const uint64_t *rec_offsets, uint64_t n,
+                            xdrg_column *cols, uint32_t flags,
+                            uint64_t *first_bad, int *err,
+                            uint32_t field, uint64_t *payload_pos);
+
 /* ---- framing (receive side) ----------------------------------------------------- */
 /* Walk the record marks of a TCP byte stream (RpcMessageParserTCP.java:63-99):
  * writes msg_offsets[k] = offset of message k's first mark for every complete

@@ -106,6 +106,10 @@ FUNCTIONS = {
                                          ctypes.c_uint32, _P]),
     "xdrg_decode_batch": (ctypes.c_int, [_P, _P, _P, _U64, _P, _U64, ctypes.POINTER(Column),
                                          ctypes.c_uint32, _P, _P]),
+    "xdrg_encode_batch_shallow": (ctypes.c_int, [_P, _P, ctypes.POINTER(Column), _U64, _P, _U64, _P,
+                                                 ctypes.c_uint32, _P, ctypes.c_uint32, _P]),
+    "xdrg_decode_batch_view": (ctypes.c_int, [_P, _P, _P, _U64, _P, _U64, ctypes.POINTER(Column),
+                                              ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]),
     "xdrg_frame_scan": (ctypes.c_int, [_P, _P, _U64, _P, _U64, _PU64]),
     "xdrg_deframe": (ctypes.c_int, [_P, _P, _U64, _P, _U64, _P, _U64, _PU64, _PU64]),
     "xdrg_encode_batch_multi": (ctypes.c_int, [_P, ctypes.c_uint32, _P, _P, _P, _P, _U64, _P,

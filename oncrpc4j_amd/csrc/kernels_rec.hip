@@ -208,6 +208,7 @@ __device__ uint64_t enc_rec_size_cond(const RecArgs &a, uint64_t r) {
         const VField &f = a.f[k];
         if (!cond_present(a, f, dv)) continue;
         cond_mark(f, k, f.slot ? disc_native(f, r) : 0, dv);
+        if (k + 1 == a.byref) { s += 4; continue; }   // by reference: the length word only
         s += f.kind != XDRG_K_DYNAMIC ? (uint64_t)f.xbytes
                                       : dyn_xdr_bytes(f, f.offsets[r + 1] - f.offsets[r]);
     }
@@ -215,7 +216,7 @@ __device__ uint64_t enc_rec_size_cond(const RecArgs &a, uint64_t r) {
 }
 
 __device__ __forceinline__ uint64_t enc_rec_size(const RecArgs &a, uint64_t r) {
-    if (a.ncond) return enc_rec_size_cond(a, r);
+    if (a.ncond || a.byref) return enc_rec_size_cond(a, r);
     uint64_t s = a.fixed_xdr;
     for (uint32_t d = 0; d < a.ndyn; ++d) {
         const VField &f = a.f[a.dyn_idx[d]];
@@ -237,18 +238,31 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_sizes(const RecArgs a) {
 __device__ void enc_record_wave(const RecArgs &a, uint64_t r, uint64_t pos, uint64_t size) {
     const uint32_t lane = threadIdx.x & 63;
     uint8_t *out = a.xdr;
-    if (a.framed) {
-        if (lane == 0)
-            *(uint32_t *)(out + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
-        pos += 4;
-    }
+    const uint64_t mark_at = pos;
+    uint64_t ref_bytes = 0;   // payload + pad of a by-reference field (not in `out`)
+    if (a.framed) pos += 4;
     Disc dv;
     dv.pres = 0;
     for (uint32_t k = 0; k < a.nf; ++k) {
         const VField &f = a.f[k];
         if (a.ncond) {   // absent union arm / optional value: nothing on the wire
-            if (!cond_present(a, f, dv)) continue;
+            if (!cond_present(a, f, dv)) {
+                if (k + 1 == a.byref && lane == 0) a.ref_pos[r] = ~0ull;
+                continue;
+            }
             cond_mark(f, k, f.slot ? disc_native(f, r) : 0, dv);
+        }
+        if (k + 1 == a.byref) {
+            // xdrEncodeFileChunk (Xdr.java:978-988): the length word here, the
+            // payload and its padding spliced in by the sender at pos + 4
+            const uint64_t cnt = f.offsets[r + 1] - f.offsets[r];
+            if (lane == 0) {
+                *(uint32_t *)(out + pos) = bswap32r((uint32_t)cnt);
+                a.ref_pos[r] = pos + 4;
+            }
+            ref_bytes = cnt + pad4(cnt);
+            pos += 4;
+            continue;
         }
         if (f.kind != XDRG_K_DYNAMIC) {
             const uint8_t *base = f.data + (int64_t)r * f.stride;
@@ -290,6 +304,10 @@ __device__ void enc_record_wave(const RecArgs &a, uint64_t r, uint64_t pos, uint
             }
         }
     }
+    // one mark over every part of the message (GrizzlyRpcTransport.java:103-110,
+    // sendRawTCP :135-139 with a file chunk)
+    if (a.framed && lane == 0)
+        *(uint32_t *)(out + mark_at) = bswap32r((uint32_t)(size - 4 + ref_bytes) | kLastFrag);
 }
 
 __global__ __launch_bounds__(kRecThreads) void k_enc_place_wave(const RecArgs a) {
@@ -423,6 +441,7 @@ __device__ void dec_record_wave(const RecArgs &a, uint64_t r, uint32_t upto) {
         const VField &f = a.f[k];
         if (a.ncond) {
             if (!cond_present(a, f, dv)) {
+                if (k + 1 == a.byref && lane == 0) a.ref_pos[r] = ~0ull;
                 // absent: a fixed field reads as zero (a fresh rpcgen object's
                 // default); a dynamic one has an empty run (count 0 from the walk)
                 if (f.kind != XDRG_K_DYNAMIC) {
@@ -455,6 +474,11 @@ __device__ void dec_record_wave(const RecArgs &a, uint64_t r, uint32_t upto) {
         const int32_t len = (int32_t)ld_be32(in + pos);
         pos += 4;
         const uint64_t cnt = len > 0 ? (uint64_t)len : 0;
+        if (k + 1 == a.byref) {   // xdrDecodeByteBuffer (Xdr.java:423-439): a slice, no copy
+            if (lane == 0) a.ref_pos[r] = pos;
+            pos += cnt + pad4(cnt);
+            continue;
+        }
         const uint64_t e0 = f.offsets[r];
         if (f.xsz == 1) {
             // bytes to an arbitrarily aligned native destination: each lane
@@ -532,7 +556,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_wave(const RecArgs a)
             const uint64_t r = rb + t0 + j;
             if (r < a.n) {
                 f.offsets[r] = off;
-                if (r < bad && off + c[j] > f.cap) {   // native column too small
+                if (r < bad && k + 1 != a.byref && off + c[j] > f.cap) {   // native column too small
                     atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
                     if (s_upto[t0 + j] > k) s_upto[t0 + j] = k;
                 }
@@ -2128,7 +2152,7 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
     // conditional schemas (unions / optional data) take the wave-per-record kernels
-    const bool grp = a.ndyn <= (uint32_t)kMaxDynLds && !a.ncond;
+    const bool grp = a.ndyn <= (uint32_t)kMaxDynLds && !a.ncond && !a.byref;
     bool stage = grp && g_rec_kernel == 4;
     for (uint32_t d = 0; d < a.ndyn && stage; ++d)
         stage = stage_type(a.f[a.dyn_idx[d]].type, a.f[a.dyn_idx[d]].xsz);

@@ -508,9 +508,10 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
 // ---------------------------------------------------------------------------
 // encode
 // ---------------------------------------------------------------------------
-extern "C" int xdrg_encode_batch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols,
-                                 uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_offsets,
-                                 uint32_t flags, uint64_t *out_len) {
+// byref = 0, or 1 + the field encoded by reference (xdrg_encode_batch_shallow).
+static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
+                       uint8_t *out, uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags,
+                       uint64_t *out_len, uint32_t byref, uint64_t *ref_pos) {
     if (!c || !s) return XDRG_E_INVAL;
     HIPCHK(c, hipSetDevice(c->device));
     const bool framed = flags & XDRG_FRAME_RM;
@@ -596,6 +597,8 @@ extern "C" int xdrg_encode_batch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_c
     a.xdr = out;
     a.xdr_cap = out_cap;
     a.rec_out = rec_offsets;
+    a.byref = byref;
+    a.ref_pos = ref_pos;
     for (int ph = REC_ENC_SIZES; ph <= REC_ENC_PLACE; ++ph) {
         TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE + ph);
         HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
@@ -613,6 +616,32 @@ extern "C" int xdrg_encode_batch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_c
         return XDRG_E_CAPACITY;
     }
     return XDRG_OK;
+}
+
+extern "C" int xdrg_encode_batch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols,
+                                 uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_offsets,
+                                 uint32_t flags, uint64_t *out_len) {
+    return encode_impl(c, s, cols, n, out, out_cap, rec_offsets, flags, out_len, 0, nullptr);
+}
+
+// A dynamic opaque / string field may travel by reference (Xdr.java:839-866, 978-988).
+static int check_byref(xdrg_ctx *c, const xdrg_schema *s, uint32_t field, const void *pos) {
+    if (!c || !s) return XDRG_E_INVAL;
+    if (field >= s->f.size()) return inval(c, "by-reference field index out of range");
+    const xdrg_field &f = s->f[field];
+    if (f.kind != XDRG_K_DYNAMIC || (f.type != XDRG_T_OPAQUE && f.type != XDRG_T_STRING))
+        return inval(c, "by-reference field must be a dynamic opaque or string");
+    if (!pos) return inval(c, "splice / payload position array is NULL");
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_encode_batch_shallow(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols,
+                                         uint64_t n, uint8_t *out, uint64_t out_cap,
+                                         uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len,
+                                         uint32_t field, uint64_t *splice) {
+    const int rc = check_byref(c, s, field, n ? splice : (void *)1);
+    if (rc) return rc;
+    return encode_impl(c, s, cols, n, out, out_cap, rec_offsets, flags, out_len, field + 1, splice);
 }
 
 // ---------------------------------------------------------------------------
@@ -651,9 +680,9 @@ static int finish_decode(xdrg_ctx *c, uint64_t n, unsigned long long host_key, b
     return code;
 }
 
-extern "C" int xdrg_decode_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in,
-                                 uint64_t in_len, const uint64_t *rec_offsets, uint64_t n,
-                                 xdrg_column *cols, uint32_t flags, uint64_t *first_bad, int *err) {
+static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t in_len,
+                       const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
+                       uint64_t *first_bad, int *err, uint32_t byref, uint64_t *ref_pos) {
     if (!c || !s) return XDRG_E_INVAL;
     HIPCHK(c, hipSetDevice(c->device));
     const bool framed = flags & XDRG_FRAME_RM;
@@ -742,12 +771,30 @@ extern "C" int xdrg_decode_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8_
     a.xdr = (uint8_t *)in;
     a.xdr_cap = in_len;
     a.rec_in = rec_offsets;
+    a.byref = byref;
+    a.ref_pos = ref_pos;
     HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
     for (int ph = REC_DEC_SIZES; ph <= REC_DEC_PLACE; ++ph) {
         TimedLaunch t(c, rec_dec_kernel_id(ph));
         HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
     }
     return finish_decode(c, n, kNoError, true, async, first_bad, err);
+}
+
+extern "C" int xdrg_decode_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in,
+                                 uint64_t in_len, const uint64_t *rec_offsets, uint64_t n,
+                                 xdrg_column *cols, uint32_t flags, uint64_t *first_bad, int *err) {
+    return decode_impl(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err, 0, nullptr);
+}
+
+extern "C" int xdrg_decode_batch_view(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in,
+                                      uint64_t in_len, const uint64_t *rec_offsets, uint64_t n,
+                                      xdrg_column *cols, uint32_t flags, uint64_t *first_bad,
+                                      int *err, uint32_t field, uint64_t *payload_pos) {
+    const int rc = check_byref(c, s, field, n ? payload_pos : (void *)1);
+    if (rc) return rc;
+    return decode_impl(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err, field + 1,
+                       payload_pos);
 }
 
 // ---------------------------------------------------------------------------

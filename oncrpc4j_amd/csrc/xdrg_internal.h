@@ -133,6 +133,9 @@ struct RecArgs {
     uint32_t big_rec;          // blocks averaging >= big_rec XDR bytes per record take the group
                                // kernels, the others the staged ones (0: one kernel for all)
     uint32_t ncond;            // conditional fields in the schema (0: every record has all fields)
+    uint32_t byref;            // 0, or 1 + the field encoded by reference / decoded as a view
+    uint32_t rsv2;
+    uint64_t *ref_pos;         // byref: encode splice[n] / decode payload_pos[n]
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
     int32_t cvals[XDRG_MAX_CASES];  // case values of the conditional fields

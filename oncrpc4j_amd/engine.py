@@ -194,6 +194,37 @@ class Context:
             _raise(rc, self._h, None if async_ else fb.value)
         return rc, (None if async_ else fb.value), (None if async_ else er.value)
 
+    def encode_shallow(self, schema, cols, n, out, out_cap, field, splice, rec_offsets=None,
+                       framed=False):
+        """xdrg_encode_batch_shallow: field `field` travels by reference
+        (xdrEncodeFileChunk, Xdr.java:978-988); splice[i] = where record i's
+        payload + zero pad go in its message.  -> bytes written to out."""
+        flags = abi.FRAME_RM if framed else 0
+        carr = cols if isinstance(cols, ctypes.Array) else columns_array(cols)
+        ol = ctypes.c_uint64(0)
+        rc = lib().xdrg_encode_batch_shallow(self._h, schema.handle, carr, int(n), _ptr(out),
+                                             int(out_cap), _ptr(rec_offsets), flags,
+                                             ctypes.addressof(ol), int(field), _ptr(splice))
+        if rc:
+            _raise(rc, self._h)
+        return ol.value
+
+    def decode_view(self, schema, xdr, xdr_len, n, cols, field, payload_pos, rec_offsets=None,
+                    framed=False, raise_on_error=True):
+        """xdrg_decode_batch_view: field `field` decodes as a stream slice
+        (xdrDecodeByteBuffer, Xdr.java:423-439) -> (status, first_bad, err)."""
+        flags = abi.FRAME_RM if framed else 0
+        carr = cols if isinstance(cols, ctypes.Array) else columns_array(cols)
+        fb = ctypes.c_uint64(0)
+        er = ctypes.c_int(0)
+        rc = lib().xdrg_decode_batch_view(self._h, schema.handle, _ptr(xdr), int(xdr_len),
+                                          _ptr(rec_offsets), int(n), carr, flags,
+                                          ctypes.addressof(fb), ctypes.addressof(er), int(field),
+                                          _ptr(payload_pos))
+        if rc and raise_on_error:
+            _raise(rc, self._h, fb.value)
+        return rc, fb.value, er.value
+
     def frame_scan(self, data, length, msg_offsets, cap):
         """xdrg_frame_scan -> number of complete messages (0 = STOP)."""
         nm = ctypes.c_uint64(0)

@@ -83,6 +83,10 @@ _SIGS = {
                                             ctypes.c_uint32, _P]),
     "xo_decode_batch_cond": (ctypes.c_int, [_PF, _SZ, _P, _SZ, _P, _U64, _P, _U64, _PC,
                                             ctypes.c_uint32, _P, _P]),
+    "xo_encode_batch_shallow": (ctypes.c_int, [_PF, _SZ, _P, _SZ, _PC, _U64, _P, _U64, _P,
+                                               ctypes.c_uint32, _P, ctypes.c_uint32, _P]),
+    "xo_decode_batch_view": (ctypes.c_int, [_PF, _SZ, _P, _SZ, _P, _U64, _P, _U64, _PC,
+                                            ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]),
     "xo_encode_batch_mt": (ctypes.c_int, [_PF, _SZ, _PC, _U64, _P, _U64, ctypes.c_uint32, _P,
                                           ctypes.c_int]),
     "xo_decode_batch_mt": (ctypes.c_int, [_PF, _SZ, _P, _U64, _U64, _PC, ctypes.c_uint32, _P, _P,
@@ -184,3 +188,39 @@ def fragment(payload, frag):
     out = np.zeros(cap, dtype=np.uint8)
     w = L.xo_fragment(src.ctypes.data, len(payload), frag, out.ctypes.data, cap)
     return out[:w].tobytes()
+
+
+def encode_batch_shallow(fields, cols, n, out_cap, field, framed=False, conds=None):
+    """-> (status, buffer bytes, record offsets[n+1], splice[n]) — xdrEncodeFileChunk form."""
+    import numpy as np
+    L = lib()
+    fa = fields_array(fields)
+    ca, keep = conds_array(conds)
+    out = np.zeros(max(out_cap, 1), dtype=np.uint8)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    splice = np.zeros(max(n, 1), dtype=np.uint64)
+    out_len = _U64(0)
+    rc = L.xo_encode_batch_shallow(fa, len(fields), ca, len(conds or ()), ctypes.addressof(cols), n,
+                                   out.ctypes.data, out_cap, offs.ctypes.data,
+                                   FRAME_RM if framed else 0, ctypes.byref(out_len), field,
+                                   splice.ctypes.data)
+    del keep
+    return rc, out[:out_len.value].tobytes() if rc == OK else b"", offs, splice[:n]
+
+
+def decode_batch_view(fields, xdr, rec_offsets, n, cols, field, framed=False, conds=None):
+    """-> (status, first_bad, err, payload_pos[n]) — xdrDecodeByteBuffer form."""
+    import numpy as np
+    L = lib()
+    fa = fields_array(fields)
+    ca, keep = conds_array(conds)
+    buf = np.frombuffer(xdr, dtype=np.uint8) if len(xdr) else np.zeros(1, np.uint8)
+    pos = np.zeros(max(n, 1), dtype=np.uint64)
+    fb = _U64(0)
+    err = ctypes.c_int(0)
+    rc = L.xo_decode_batch_view(fa, len(fields), ca, len(conds or ()), buf.ctypes.data, len(xdr),
+                                rec_offsets.ctypes.data, n, ctypes.addressof(cols),
+                                FRAME_RM if framed else 0, ctypes.byref(fb), ctypes.byref(err),
+                                field, pos.ctypes.data)
+    del keep
+    return rc, fb.value, err.value, pos[:n]

@@ -130,6 +130,14 @@ int xo_encode_byte_buffer(xo_stream *s, const uint8_t *b, size_t len) {
     s->pos += len + pad;
     return XDRG_OK;
 }
+/* xdrEncodeFileChunk (Xdr.java:978-988): the length word only; the chunk and
+ * its zero padding stay outside the buffer and travel as their own writable
+ * messages (asBufferWritableMessages :579-597).                              */
+int xo_encode_file_chunk(xo_stream *s, size_t len, uint32_t *padding) {
+    int rc = xo_encode_int(s, (int32_t)len); if (rc) return rc;
+    *padding = pad4(len);
+    return XDRG_OK;
+}
 /* xdrEncodeIntVector (Xdr.java:607-613): one capacity check, count + ints. */
 int xo_encode_int_vector(xo_stream *s, const int32_t *v, size_t n) {
     int rc = ensure_capacity(s, 4 + 4 * n); if (rc) return rc;
@@ -422,8 +430,13 @@ static int present(const xo_conds *t, size_t k, const int *pres, const int32_t *
     return in != (c->negate != 0);
 }
 
-static int encode_record(xo_stream *s, const xdrg_field *fs, size_t nf, const xdrg_column *cols,
-                         uint64_t i, const xo_conds *cc) {
+/* shallow >= 0: that dynamic opaque/string field is encoded by reference
+ * (xdrEncodeFileChunk); *chunk_at = its splice position in the record's
+ * buffer, *chunk_len = its bytes (padding implied), or *chunk_at = ~0 when
+ * the field is absent.                                                       */
+static int encode_record_ex(xo_stream *s, const xdrg_field *fs, size_t nf, const xdrg_column *cols,
+                            uint64_t i, const xo_conds *cc, int shallow, uint64_t *chunk_at,
+                            uint64_t *chunk_len) {
     int pres[64]; int32_t val[64];
     for (size_t k = 0; k < nf; k++) {
         const xdrg_field *f = &fs[k];
@@ -438,6 +451,15 @@ static int encode_record(xo_stream *s, const xdrg_field *fs, size_t nf, const xd
                 if (f->type == XDRG_T_BOOL) val[k] = *p != 0;
                 else if (native_size(f->type) == 4) memcpy(&val[k], p, 4);
             }
+        }
+        if (f->kind == XDRG_K_DYNAMIC && (int)k == shallow) {
+            uint64_t a = c->offsets[i], b = c->offsets[i + 1];
+            uint32_t padding;
+            rc = xo_encode_file_chunk(s, (size_t)(b - a), &padding);
+            if (rc) return rc;
+            *chunk_at = s->pos;
+            *chunk_len = b - a;
+            continue;
         }
         if (f->kind == XDRG_K_DYNAMIC) {
             uint64_t a = c->offsets[i], b = c->offsets[i + 1];
@@ -491,6 +513,12 @@ static int encode_record(xo_stream *s, const xdrg_field *fs, size_t nf, const xd
     return XDRG_OK;
 }
 
+static int encode_record(xo_stream *s, const xdrg_field *fs, size_t nf, const xdrg_column *cols,
+                         uint64_t i, const xo_conds *cc) {
+    uint64_t at, len;
+    return encode_record_ex(s, fs, nf, cols, i, cc, -1, &at, &len);
+}
+
 static int check_schema(const xdrg_field *fs, size_t nf) {
     if (!fs || !nf) return XDRG_E_INVAL;
     for (size_t k = 0; k < nf; k++) if (!field_valid(&fs[k])) return XDRG_E_INVAL;
@@ -531,9 +559,48 @@ int xo_encode_batch_cond(const xdrg_field *fs, size_t nf, const xdrg_cond *conds
     return XDRG_OK;
 }
 
+/* Batch of messages each carrying one payload by reference: the buffer part
+ * of every record back to back in `out` (record offsets in rec_offsets),
+ * splice[i] = where record i's payload (then its zero padding) goes, or
+ * UINT64_MAX when the field is absent.  With XDRG_FRAME_RM the mark counts
+ * every part, as sendRawTCP does (GrizzlyRpcTransport.java:130-139,
+ * 224-231).                                                                  */
+int xo_encode_batch_shallow(const xdrg_field *fs, size_t nf, const xdrg_cond *conds, size_t nconds,
+                            const xdrg_column *cols, uint64_t n, uint8_t *out, uint64_t out_cap,
+                            uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len,
+                            uint32_t field, uint64_t *splice) {
+    int rc = check_schema(fs, nf); if (rc) return rc;
+    if (field >= nf || fs[field].kind != XDRG_K_DYNAMIC ||
+        (fs[field].type != XDRG_T_OPAQUE && fs[field].type != XDRG_T_STRING)) return XDRG_E_INVAL;
+    xo_conds cc;
+    rc = cond_table(fs, nf, conds, nconds, &cc); if (rc) return rc;
+    const int framed = (flags & XDRG_FRAME_RM) != 0;
+    uint64_t pos = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (rec_offsets) rec_offsets[i] = pos;
+        uint64_t body = pos + (framed ? 4 : 0);
+        if (body > out_cap) return XDRG_E_CAPACITY;
+        xo_stream s;
+        xo_stream_wrap(&s, out + body, (size_t)(out_cap - body));
+        xo_begin_encoding(&s);
+        uint64_t at = UINT64_MAX, len = 0;
+        rc = encode_record_ex(&s, fs, nf, cols, i, nconds ? &cc : NULL, (int)field, &at, &len);
+        if (rc) return rc;
+        xo_end_encoding(&s);
+        uint64_t chunk = at == UINT64_MAX ? 0 : len + pad4((size_t)len);
+        if (framed) put_be32(out + pos, xo_record_mark((uint32_t)(s.limit + chunk)));
+        splice[i] = at == UINT64_MAX ? UINT64_MAX : body + at;
+        pos = body + s.limit;
+    }
+    if (rec_offsets) rec_offsets[n] = pos;
+    if (out_len) *out_len = pos;
+    return XDRG_OK;
+}
+
 /* One record's fields through the stream decoders (XdrAble.xdrDecode). */
 static int decode_record(xo_stream *s, const xdrg_field *fs, size_t nf, xdrg_column *cols,
-                         uint64_t i, const xo_conds *cc) {
+                         uint64_t i, const xo_conds *cc, int view, const uint8_t *base_in,
+                         uint64_t *view_pos) {
     int pres[64]; int32_t val[64];
     for (size_t k = 0; k < nf; k++) {
         const xdrg_field *f = &fs[k];
@@ -547,6 +614,7 @@ static int decode_record(xo_stream *s, const xdrg_field *fs, size_t nf, xdrg_col
                 val[k] = f->type == XDRG_T_BOOL ? (w != 0) : w;
             }
             if (!pres[k]) {   /* absent: the defaults of a new rpcgen object */
+                if ((int)k == view) view_pos[i] = UINT64_MAX;
                 if (f->kind == XDRG_K_DYNAMIC) c->offsets[i + 1] = c->offsets[i];
                 else {
                     size_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
@@ -554,6 +622,15 @@ static int decode_record(xo_stream *s, const xdrg_field *fs, size_t nf, xdrg_col
                 }
                 continue;
             }
+        }
+        if (f->kind == XDRG_K_DYNAMIC && (int)k == view) {
+            /* xdrDecodeByteBuffer (Xdr.java:423-439): a slice of the stream */
+            const uint8_t *p; size_t len;
+            rc = xo_decode_byte_buffer(s, &p, &len);
+            if (rc) return rc;
+            view_pos[i] = (uint64_t)(p - base_in);
+            c->offsets[i + 1] = c->offsets[i] + len;
+            continue;
         }
         if (f->kind == XDRG_K_DYNAMIC) {
             size_t es = native_size(f->type);
@@ -630,7 +707,20 @@ int xo_decode_batch_cond(const xdrg_field *fs, size_t nf, const xdrg_cond *conds
                          const uint8_t *in, uint64_t in_len, const uint64_t *rec_offsets,
                          uint64_t n, xdrg_column *cols, uint32_t flags, uint64_t *first_bad,
                          int *err) {
+    return xo_decode_batch_view(fs, nf, conds, nconds, in, in_len, rec_offsets, n, cols, flags,
+                                first_bad, err, UINT32_MAX, NULL);
+}
+/* view < nfields: that dynamic opaque/string field decodes as a slice of the
+ * stream (xdrDecodeByteBuffer): view_pos[i] = its payload's offset in `in`,
+ * offsets[] as if copied; nothing is copied.                                 */
+int xo_decode_batch_view(const xdrg_field *fs, size_t nf, const xdrg_cond *conds, size_t nconds,
+                         const uint8_t *in, uint64_t in_len, const uint64_t *rec_offsets,
+                         uint64_t n, xdrg_column *cols, uint32_t flags, uint64_t *first_bad,
+                         int *err, uint32_t field, uint64_t *view_pos) {
     int rc = check_schema(fs, nf); if (rc) return rc;
+    const int view = field < nf ? (int)field : -1;
+    if (field != UINT32_MAX && (view < 0 || fs[field].kind != XDRG_K_DYNAMIC || !view_pos ||
+        (fs[field].type != XDRG_T_OPAQUE && fs[field].type != XDRG_T_STRING))) return XDRG_E_INVAL;
     xo_conds cc;
     rc = cond_table(fs, nf, conds, nconds, &cc); if (rc) return rc;
     const int framed = (flags & XDRG_FRAME_RM) != 0;
@@ -662,7 +752,7 @@ int xo_decode_batch_cond(const xdrg_field *fs, size_t nf, const xdrg_cond *conds
             xo_stream s;
             xo_stream_wrap(&s, (uint8_t *)in + a, (size_t)(b - a));
             xo_begin_decoding(&s);
-            rc = decode_record(&s, fs, nf, cols, i, nconds ? &cc : NULL);
+            rc = decode_record(&s, fs, nf, cols, i, nconds ? &cc : NULL, view, in, view_pos);
         }
         if (rc) {
             if (first_bad) *first_bad = i;

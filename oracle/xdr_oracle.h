@@ -136,6 +136,21 @@ int xo_decode_batch_cond(const xdrg_field *fields, size_t nfields, const xdrg_co
                          size_t nconds, const uint8_t *in, uint64_t in_len,
                          const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols,
                          uint32_t flags, uint64_t *first_bad, int *err);
+/* Zero-copy forms (include/xdrg.h
+ * xdrg_encode_batch_shallow / xdrg_decode_batch_view): a payload field
+ * encoded by reference (xdrEncodeFileChunk, Xdr.java:978-988, with
+ * asBufferWritableMessages :579-597) and decoded as a stream slice
+ * (xdrDecodeByteBuffer, :423-439).                                          */
+int xo_encode_file_chunk(xo_stream *s, size_t len, uint32_t *padding);
+int xo_encode_batch_shallow(const xdrg_field *fields, size_t nfields, const xdrg_cond *conds,
+                            size_t nconds, const xdrg_column *cols, uint64_t n, uint8_t *out,
+                            uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags,
+                            uint64_t *out_len, uint32_t field, uint64_t *splice);
+int xo_decode_batch_view(const xdrg_field *fields, size_t nfields, const xdrg_cond *conds,
+                         size_t nconds, const uint8_t *in, uint64_t in_len,
+                         const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols,
+                         uint32_t flags, uint64_t *first_bad, int *err, uint32_t field,
+                         uint64_t *view_pos);
 /* Same, split over `threads` POSIX threads by contiguous record ranges (each
  * range encodes into its own slice; fixed-size schemas only for encode).  The
  * all-cores CPU baseline of SURVEY.md §8(d).                                  */
