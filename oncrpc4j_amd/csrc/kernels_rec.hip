@@ -666,14 +666,22 @@ __device__ __forceinline__ uint32_t walk_counts(const RecArgs &a, uint64_t r, ui
         pos += 4;
     }
     uint32_t d = 0;
+    Disc dv;
+    dv.pres = 0;
     for (uint32_t k = 0; k < a.nf; ++k) {
         const VField &f = a.f[k];
         *sub = 2 * k + 1;
+        if (a.ncond && !cond_present(a, f, dv)) {   // absent arm: count 0
+            if (f.kind == XDRG_K_DYNAMIC) ++d;
+            continue;
+        }
         if (f.kind != XDRG_K_DYNAMIC) {
             if (e.b - pos < f.xbytes) return XDRG_E_SHORT;
+            if (a.ncond) cond_mark(f, k, f.slot ? (int32_t)ld_be32(a.xdr + pos) : 0, dv);
             pos += f.xbytes;
             continue;
         }
+        if (a.ncond) cond_mark(f, k, 0, dv);
         if (e.b - pos < 4) return XDRG_E_SHORT;
         const int32_t len = (int32_t)ld_be32(a.xdr + pos);
         pos += 4;
@@ -1416,6 +1424,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_lane(const RecArgs a) {
                 scnt[(size_t)d * kRecPerBlock + t0 + j] = (uint32_t)cnt;
                 size += dyn_xdr_bytes(f, cnt);
             }
+            if (a.ncond || a.byref) size = enc_rec_size_cond(a, r);   // arms / by-reference payload
         }
         sz[j] = size;
         s += size;
@@ -1435,13 +1444,31 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_lane(const RecArgs a) {
     for (uint32_t j = threadIdx.x; j < nrec; j += kRecThreads) {
         const uint64_t r = rb + j;
         uint8_t *dst = a.xdr + soff[j];
-        if (a.framed) {   // GrizzlyRpcTransport.java:103-110
-            *(uint32_t *)dst = bswap32r((uint32_t)(soff[j + 1] - soff[j] - 4) | kLastFrag);
-            dst += 4;
-        }
+        uint8_t *const mark = dst;
+        uint64_t ref_bytes = 0;   // by-reference payload + pad (sent beside `out`)
+        if (a.framed) dst += 4;
         uint32_t d = 0;
+        Disc dv;
+        dv.pres = 0;
         for (uint32_t k = 0; k < a.nf; ++k) {
             const VField &f = a.f[k];
+            if (a.ncond) {   // union arm / optional value not taken: nothing on the wire
+                if (!cond_present(a, f, dv)) {
+                    if (k + 1 == a.byref) a.ref_pos[r] = ~0ull;
+                    if (f.kind == XDRG_K_DYNAMIC) ++d;
+                    continue;
+                }
+                cond_mark(f, k, f.slot ? disc_native(f, r) : 0, dv);
+            }
+            if (k + 1 == a.byref) {   // xdrEncodeFileChunk (Xdr.java:978-988)
+                const uint32_t cnt = scnt[(size_t)d * kRecPerBlock + j];
+                *(uint32_t *)dst = bswap32r(cnt);
+                dst += 4;
+                a.ref_pos[r] = (uint64_t)(dst - a.xdr);
+                ref_bytes = cnt + pad4(cnt);
+                ++d;
+                continue;
+            }
             if (f.kind != XDRG_K_DYNAMIC) {
                 const uint32_t nw = f.xbytes >> 2;
                 for (uint32_t i = 0; i < nw; ++i) *(uint32_t *)(dst + 4 * i) = fixed_word(f, r, 4 * i);
@@ -1462,6 +1489,8 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_lane(const RecArgs a) {
             dst += dyn_xdr_bytes(f, cnt);
             ++d;
         }
+        if (a.framed)   // GrizzlyRpcTransport.java:103-110 (sendRawTCP :135-139: every part)
+            *(uint32_t *)mark = bswap32r((uint32_t)(soff[j + 1] - soff[j] - 4 + ref_bytes) | kLastFrag);
     }
 }
 
@@ -1499,7 +1528,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
             snoff[(size_t)d * kRecPerBlock + t0 + j] = off;
             if (r < a.n) {
                 f.offsets[r] = off;
-                if (r < bad && off + c > f.cap) {   // native column too small
+                if (r < bad && k + 1 != a.byref && off + c > f.cap) {   // native column too small
                     atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
                     atomicMin(&supto[t0 + j], k);
                 }
@@ -1516,8 +1545,24 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
         const uint64_t r = rb + j;
         const uint8_t *src = a.xdr + sstart[j];
         uint32_t d = 0;
+        Disc dv;
+        dv.pres = 0;
         for (uint32_t k = 0; k < upto; ++k) {
             const VField &f = a.f[k];
+            if (a.ncond) {
+                if (!cond_present(a, f, dv)) {
+                    // absent: fixed fields read as zero (a fresh rpcgen object), dynamic
+                    // ones have an empty run (count 0 from the walk)
+                    if (k + 1 == a.byref) a.ref_pos[r] = ~0ull;
+                    if (f.kind == XDRG_K_DYNAMIC) { ++d; continue; }
+                    uint8_t *base = f.data + (int64_t)r * f.stride;
+                    const uint32_t nb = f.type == XDRG_T_OPAQUE ? f.count
+                                      : (f.kind == XDRG_K_FIXED ? f.count : 1u) * f.nsz;
+                    for (uint32_t i = 0; i < nb; ++i) base[i] = 0;
+                    continue;
+                }
+                cond_mark(f, k, f.slot ? (int32_t)ld_be32(src) : 0, dv);
+            }
             if (f.kind != XDRG_K_DYNAMIC) {
                 const uint32_t nw = f.xbytes >> 2;
                 for (uint32_t i = 0; i < nw; ++i) fixed_store(f, r, 4 * i, *(const uint32_t *)(src + 4 * i));
@@ -1525,6 +1570,12 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
                 continue;
             }
             const uint32_t cnt = scnt[(size_t)d * kRecPerBlock + j];
+            if (k + 1 == a.byref) {   // xdrDecodeByteBuffer (Xdr.java:423-439): a slice
+                a.ref_pos[r] = (uint64_t)(src + 4 - a.xdr);
+                src += 4 + cnt + pad4(cnt);
+                ++d;
+                continue;
+            }
             const uint64_t no = snoff[(size_t)d * kRecPerBlock + j];
             if (f.xsz == 1) lane_dec_bytes(f.data + no, src + 4, cnt);
             else if (is_word4(f)) lane_dec_words((uint32_t *)(f.data + no * 4), src + 4, cnt);
@@ -2151,8 +2202,11 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
         hipLaunchKernelGGL(k_debug_recargs, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
-    // conditional schemas (unions / optional data) take the wave-per-record kernels
-    const bool grp = a.ndyn <= (uint32_t)kMaxDynLds && !a.ncond && !a.byref;
+    // conditional schemas (unions / optional data) and by-reference payloads take
+    // the lane-per-record kernels (wave per record beyond kMaxDynLds dynamic fields)
+    const bool special = a.ncond || a.byref;
+    const bool grp = a.ndyn <= (uint32_t)kMaxDynLds && !special;
+    const bool lane = a.ndyn <= (uint32_t)kMaxDynLds && special;
     bool stage = grp && g_rec_kernel == 4;
     for (uint32_t d = 0; d < a.ndyn && stage; ++d)
         stage = stage_type(a.f[a.dyn_idx[d]].type, a.f[a.dyn_idx[d]].xsz);
@@ -2167,7 +2221,7 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
             hipLaunchKernelGGL(k_enc_stage, dim3(nb), dim3(kRecThreads),
                                enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             if (a.big_rec) launch_ur<EncG>(g_enc_u, g_enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
-        } else if (grp && g_rec_kernel == 3) {
+        } else if (lane || (grp && g_rec_kernel == 3)) {
             hipLaunchKernelGGL(k_enc_lane, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
             launch_ur<EncG>(g_enc_u, g_enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
@@ -2175,7 +2229,7 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SIZES:
-        if (grp) hipLaunchKernelGGL(k_dec_sizes_g, dim3(nb), dim3(kRecThreads),
+        if (grp || lane) hipLaunchKernelGGL(k_dec_sizes_g, dim3(nb), dim3(kRecThreads),
                                     (size_t)a.ndyn * kRecPerBlock * 4, st, a);
         else hipLaunchKernelGGL(k_dec_sizes_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
@@ -2189,7 +2243,7 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
             hipLaunchKernelGGL(k_dec_stage, dim3(nb), dim3(kRecThreads),
                                dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             if (a.big_rec) launch_ur<DecG>(g_dec_u, g_dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
-        } else if (grp && g_rec_kernel == 3) {
+        } else if (lane || (grp && g_rec_kernel == 3)) {
             hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
             launch_ur<DecG>(g_dec_u, g_dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);

@@ -265,3 +265,28 @@ def test_engine_schema_disc_slots():
     bad = [(m + 1 + i, i, False, [i]) for i in range(m + 1)]
     with pytest.raises(engine.XdrgError):
         engine.Schema(fields, bad)
+
+
+WIDE = ([(I, SC, 0), (STR, DY, 0), (I, DY, 0), (O, DY, 0), (B, SC, 0), (STR, DY, 0), (H, DY, 0),
+         (O, DY, 0), (I, SC, 0)],
+        [(2, 0, False, [1, 2]), (3, 0, True, [1, 2]), (5, 4, True, [0]), (6, 4, True, [0]),
+         (8, 0, False, [2])])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+def test_gpu_cond_wide_schema_vs_oracle(gpu_ctx, framed):
+    """More dynamic fields than the lane kernels stage (wave-per-record path)."""
+    fields, conds = WIDE
+    n = 5003
+    hb = _random_cond_batch(fields, conds, n, seed=99)
+    rc, want, want_offs = oracle_roundtrip(fields, conds, hb, framed)
+    assert rc == 0
+    xdr, offs = gpu_encode(gpu_ctx, fields, conds, hb, framed)
+    assert xdr == want and np.array_equal(offs, want_offs)
+    ref = HostBatch.empty(fields, n, hb.dyn_caps())
+    assert oracle.decode_batch(fields, want, want_offs, n, ref.columns(), framed=framed,
+                               conds=conds) == (0, n, 0)
+    rc, fb, err, out = gpu_decode(gpu_ctx, fields, conds, xdr, n, offs, hb.dyn_caps(), framed)
+    assert (rc, fb, err) == (0, n, 0)
+    assert out.equal(ref)

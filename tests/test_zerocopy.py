@@ -226,3 +226,54 @@ def test_gpu_byref_rejects_non_bytes(gpu_ctx):
     with pytest.raises(engine.XdrgError) as ei:
         gpu_ctx.encode_shallow(sch, db.columns(), 8, out, 1024, 1, sp)
     assert ei.value.code == abi.E_INVAL
+
+
+WIDE_RES = [(I, SC, 0), (STR, DY, 0), (I, DY, 0), (O, DY, 0), (STR, DY, 0), (O, DY, 0), (I, SC, 0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+def test_gpu_byref_wide_schema(gpu_ctx, framed):
+    """By-reference payload in a schema with more dynamic fields than the lane
+    kernels stage (wave-per-record path): encode and view decode vs oracle."""
+    torch, engine, DeviceBatch = _dev()
+    fields, field, n = WIDE_RES, 3, 4001
+    hb = random_batch(fields, n, seed=21, dyn_len=(0, 90))
+    cap = hb.xdr_total(framed)
+    rc, want, want_offs, want_splice = oracle.encode_batch_shallow(fields, hb.columns(), n, cap, field,
+                                                                   framed=framed)
+    assert rc == 0
+    sch = engine.Schema(fields)
+    db = DeviceBatch.from_host(hb)
+    cols = db.columns()
+    cols[field].data = None
+    out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    offs = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    splice = torch.zeros(n, dtype=torch.int64, device="cuda")
+    ln = gpu_ctx.encode_shallow(sch, cols, n, out, cap, field, splice, rec_offsets=offs, framed=framed)
+    assert out[:ln].cpu().numpy().tobytes() == want
+    assert np.array_equal(splice.cpu().numpy().view(np.uint64), want_splice)
+    rc, deep, deep_offs = oracle.encode_batch(fields, hb.columns(), n, cap, framed=framed)
+    ref = HostBatch.empty(fields, n, hb.dyn_caps())
+    rc, fb, err, want_pos = oracle.decode_batch_view(fields, deep, deep_offs, n, ref.columns(), field,
+                                                     framed=framed)
+    caps = hb.dyn_caps()
+    caps[field] = 1
+    back = DeviceBatch.empty(fields, n, caps)
+    pos = torch.zeros(n, dtype=torch.int64, device="cuda")
+    buf = torch.from_numpy(np.frombuffer(deep, np.uint8).copy()).cuda()
+    got = gpu_ctx.decode_view(sch, buf, len(deep), n, back.columns(), field, pos,
+                              rec_offsets=torch.from_numpy(deep_offs.view(np.int64)).cuda(),
+                              framed=framed)
+    assert got == (0, n, 0)
+    assert np.array_equal(pos.cpu().numpy().view(np.uint64), want_pos)
+    h = back.to_host()
+    for k, f in enumerate(fields):
+        if k == field:
+            assert np.array_equal(h.arrays[k][1], ref.arrays[k][1])
+        elif f[1] == DY:
+            m = int(ref.arrays[k][1][-1])
+            assert np.array_equal(h.arrays[k][1], ref.arrays[k][1])
+            assert np.array_equal(h.arrays[k][0][:m], ref.arrays[k][0][:m])
+        else:
+            assert np.array_equal(h.arrays[k], ref.arrays[k])
