@@ -242,12 +242,279 @@ __global__ __launch_bounds__(256) void k_stream_framed_dec(const StreamArgs a, u
     }
 }
 
+// ---- wave-local LDS transpose variant ----------------------------------------
+// The direct kernels above read 4-aligned (not 16-aligned) 16-byte windows:
+// every lane's load straddles two 16-byte sectors.  Here each wavefront owns
+// 256 consecutive destination words: it loads the source words they need as
+// 16-byte ALIGNED vectors (coalesced, one per lane, nontemporal) into its own
+// LDS slice, then every lane gathers its 4 destination words from LDS and
+// writes one aligned 16-byte vector.  Only the wave synchronises (no block
+// barrier after the op-table staging).
+constexpr int kFrEncWords = 4 * 66;      // encode: <= 256 + 3 source words per wave
+constexpr int kFrDecWords = 4 * 130;     // decode: <= 256 * (W+1)/W + 4 <= 516 source words
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Stage source words [B, B + 4*nv) (B a multiple of 4) into t; words past
+// `limit` read as 0.
+__device__ __forceinline__ void wave_stage(uint32_t *t, const uint32_t *src, uint64_t B, uint32_t nv,
+                                           uint64_t limit, uint32_t lane) {
+    for (uint32_t v = lane; v < nv; v += 64) {
+        const uint64_t wi = B + 4 * (uint64_t)v;
+        u32x4 x;
+        if (wi + 4 <= limit) {
+            x = __builtin_nontemporal_load((const u32x4 *)(src + wi));
+        } else {
+            x.x = wi < limit ? src[wi] : 0u; x.y = wi + 1 < limit ? src[wi + 1] : 0u;
+            x.z = wi + 2 < limit ? src[wi + 2] : 0u; x.w = 0u;
+        }
+        *(u32x4 *)(t + 4 * v) = x;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_stream_framed_enc_lds(const StreamArgs a, uint64_t n,
+                                                               uint32_t mark_le, double inv_wt) {
+    __shared__ uint8_t sops[kMaxWords];
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[4][kFrEncWords];
+    for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
+    __syncthreads();
+    const uint32_t W = a.w, Wt = a.w + 1, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t total = n * Wt;                          // XDR words
+    const uint64_t g_first = ((uint64_t)blockIdx.x * 4 + wid) * 256;
+    if (g_first >= total) return;
+    uint64_t r0; uint32_t j0;
+    divmod(g_first, Wt, inv_wt, r0, j0);
+    const uint64_t B = (r0 * W + (j0 ? j0 - 1 : 0)) & ~3ull;   // first native word needed, aligned
+    uint32_t *t = sbuf[wid];
+    wave_stage(t, (const uint32_t *)a.src, B, 65, n * W, lane);
+    wave_lds_sync();
+    const uint64_t g0 = g_first + 4 * (uint64_t)lane;
+    if (g0 >= total) return;
+    uint64_t r; uint32_t j;
+    divmod(g0, Wt, inv_wt, r, j);
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        // word j of message r: its mark (GrizzlyRpcTransport.java:103-110) or native word j-1
+        o[k] = j == 0 ? mark_le : word_op(sops[j - 1], t[r * W + j - 1 - B]);
+        if (++j == Wt) { j = 0; ++r; }
+    }
+    uint8_t *dst = a.dst + g0 * 4;
+    if (g0 + 4 <= total) {
+        u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+        __builtin_nontemporal_store(ov, (u32x4 *)dst);
+    } else {
+        for (uint64_t k = 0; g0 + k < total; ++k) ((uint32_t *)dst)[k] = o[k];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_stream_framed_dec_lds(const StreamArgs a, uint64_t n,
+                                                               uint32_t mark_le, double inv_w,
+                                                               unsigned long long *errkey) {
+    __shared__ uint8_t sops[kMaxWords];
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[4][kFrDecWords];
+    for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
+    __syncthreads();
+    const uint32_t W = a.w, Wt = a.w + 1, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t total = n * W;                           // native words
+    const uint64_t g_first = ((uint64_t)blockIdx.x * 4 + wid) * 256;
+    if (g_first >= total) return;
+    uint64_t r0; uint32_t w0;
+    divmod(g_first, W, inv_w, r0, w0);
+    uint64_t g_last = g_first + 255;
+    if (g_last >= total) g_last = total - 1;
+    uint64_t rl; uint32_t wl;
+    divmod(g_last, W, inv_w, rl, wl);
+    const uint64_t B = (r0 * Wt + w0) & ~3ull;             // covers the first record's mark
+    const uint64_t x_last = rl * Wt + 1 + wl;
+    uint32_t *t = sbuf[wid];
+    wave_stage(t, (const uint32_t *)a.src, B, (uint32_t)((x_last - B) / 4 + 1), n * Wt, lane);
+    wave_lds_sync();
+    const uint64_t g0 = g_first + 4 * (uint64_t)lane;
+    if (g0 >= total) return;
+    uint64_t r; uint32_t w;
+    divmod(g0, W, inv_w, r, w);
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (g0 + k >= total) { o[k] = 0; continue; }
+        const uint64_t x = r * Wt + 1 + w - B;
+        // first native word of record r: check its mark (RpcMessageParserTCP.java:63-99)
+        if (w == 0 && t[x - 1] != mark_le) atomicMin(errkey, err_key(r, 0, XDRG_E_FRAME));
+        o[k] = word_op(sops[w], t[x]);
+        if (++w == W) { w = 0; ++r; }
+    }
+    uint8_t *dst = a.dst + g0 * 4;
+    if (g0 + 4 <= total) {
+        u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+        __builtin_nontemporal_store(ov, (u32x4 *)dst);
+    } else {
+        for (uint64_t k = 0; g0 + k < total; ++k) ((uint32_t *)dst)[k] = o[k];
+    }
+}
+
+// ---- lean variant ----------------------------------------------------------------
+// The direct kernels spend more VALU than memory time: a 64-bit double-
+// reciprocal divmod per lane, an LDS op-table read per word.  Here the
+// division happens once per wave on uniform values (scalar unit); a lane
+// only adds its 32-bit offset (4 * lane < 256 words) and splits it with a
+// float reciprocal; schemas of plain int/uint/enum words (ALLB) skip the op
+// table entirely.
+__device__ __forceinline__ void split_small(uint32_t x, uint32_t d, float inv, uint32_t &q, uint32_t &r) {
+    // x < 2^24: q = x / d, r = x % d
+    q = (uint32_t)((float)x * inv);
+    int32_t rr = (int32_t)(x - q * d);
+    if (rr < 0) { --q; rr += (int32_t)d; }
+    else if (rr >= (int32_t)d) { ++q; rr -= (int32_t)d; }
+    r = (uint32_t)rr;
+}
+
+template <bool ALLB>
+__global__ __launch_bounds__(256) void k_stream_framed_enc_lean(const StreamArgs a, uint64_t n, uint32_t mark_le) {
+    __shared__ uint8_t sops[kMaxWords];
+    if constexpr (!ALLB) {
+        for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
+        __syncthreads();
+    }
+    const uint32_t W = a.w, Wt = a.w + 1, lane = threadIdx.x & 63;
+    const uint64_t total = n * Wt;                                   // XDR words
+    const uint64_t gw = ((uint64_t)blockIdx.x * 256 + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u)) * 4;
+    if (gw >= total) return;
+    const uint64_t r0 = gw / Wt;                                     // wave-uniform
+    const uint32_t j0 = (uint32_t)(gw - r0 * Wt);
+    uint32_t q, j;
+    split_small(j0 + 4 * lane, Wt, 1.0f / (float)Wt, q, j);
+    const uint64_t g0 = gw + 4 * lane;
+    if (g0 >= total) return;
+    const uint64_t r = r0 + q;
+    const uint64_t i0 = r * W + (j ? j - 1 : 0);                     // first native word used
+    const uint64_t nin = n * W;
+    const uint32_t *src = (const uint32_t *)a.src;
+    uint32_t x0, x1, x2, x3;
+    if (i0 + 4 <= nin) {
+        const u32x4w v = __builtin_nontemporal_load((const u32x4w *)(src + i0));
+        x0 = v.x; x1 = v.y; x2 = v.z; x3 = v.w;
+    } else {
+        x0 = i0 < nin ? src[i0] : 0u; x1 = i0 + 1 < nin ? src[i0 + 1] : 0u;
+        x2 = i0 + 2 < nin ? src[i0 + 2] : 0u; x3 = 0u;
+    }
+    uint32_t o[4];
+    uint32_t k = 0, w = j;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        if (w == 0) {
+            o[t] = mark_le;                       // GrizzlyRpcTransport.java:103-110
+        } else {
+            const uint32_t x = k == 0 ? x0 : k == 1 ? x1 : k == 2 ? x2 : x3;
+            o[t] = ALLB ? bswap32(x) : word_op(sops[w - 1], x);
+            ++k;
+        }
+        if (++w == Wt) w = 0;
+    }
+    uint8_t *dst = a.dst + g0 * 4;
+    if (g0 + 4 <= total) {
+        u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+        __builtin_nontemporal_store(ov, (u32x4 *)dst);
+    } else {
+        for (uint64_t t = 0; g0 + t < total; ++t) ((uint32_t *)dst)[t] = o[t];
+    }
+}
+
+template <bool ALLB>
+__global__ __launch_bounds__(256) void k_stream_framed_dec_lean(const StreamArgs a, uint64_t n, uint32_t mark_le,
+                                                                unsigned long long *errkey) {
+    __shared__ uint8_t sops[kMaxWords];
+    if constexpr (!ALLB) {
+        for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
+        __syncthreads();
+    }
+    const uint32_t W = a.w, Wt = a.w + 1, lane = threadIdx.x & 63;
+    const uint64_t total = n * W;                                    // native words
+    const uint64_t gw = ((uint64_t)blockIdx.x * 256 + __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u)) * 4;
+    if (gw >= total) return;
+    const uint64_t r0 = gw / W;
+    const uint32_t w0 = (uint32_t)(gw - r0 * W);
+    uint32_t q, w;
+    split_small(w0 + 4 * lane, W, 1.0f / (float)W, q, w);
+    const uint64_t n0 = gw + 4 * lane;
+    if (n0 >= total) return;
+    uint64_t r = r0 + q;
+    const uint64_t x0i = r * Wt + 1 + w;                             // XDR word of native word n0
+    const uint64_t nx = n * Wt;
+    const uint32_t *src = (const uint32_t *)a.src;
+    // the 4 native words span at most 5 XDR words (W >= 3: one mark at most)
+    uint32_t y0, y1, y2, y3, y4;   // selects, not an indexed array (no scratch)
+    if (x0i + 5 <= nx) {
+        const u32x4w v = __builtin_nontemporal_load((const u32x4w *)(src + x0i));
+        y0 = v.x; y1 = v.y; y2 = v.z; y3 = v.w;
+        y4 = src[x0i + 4];
+    } else {
+        y0 = x0i < nx ? src[x0i] : 0u; y1 = x0i + 1 < nx ? src[x0i + 1] : 0u;
+        y2 = x0i + 2 < nx ? src[x0i + 2] : 0u; y3 = x0i + 3 < nx ? src[x0i + 3] : 0u;
+        y4 = x0i + 4 < nx ? src[x0i + 4] : 0u;
+    }
+    uint32_t o[4];
+    uint32_t k = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        if (n0 + t >= total) { o[t] = 0; continue; }
+        if (w == 0) {   // first word of record r: check its mark (RpcMessageParserTCP.java:63-99)
+            const uint32_t m = k == 0 ? src[x0i - 1] : pick5(y0, y1, y2, y3, y4, k - 1);
+            if (m != mark_le) atomicMin(errkey, err_key(r, 0, XDRG_E_FRAME));
+        }
+        const uint32_t x = pick5(y0, y1, y2, y3, y4, k);
+        o[t] = ALLB ? bswap32(x) : word_op(sops[w], x);
+        ++k;
+        if (++w == W) { w = 0; ++r; ++k; }   // skip the next record's mark
+    }
+    uint8_t *dst = a.dst + n0 * 4;
+    if (n0 + 4 <= total) {
+        u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
+        __builtin_nontemporal_store(ov, (u32x4 *)dst);
+    } else {
+        for (uint64_t t = 0; n0 + t < total; ++t) ((uint32_t *)dst)[t] = o[t];
+    }
+}
+
+static int g_framed_kernel = 2;   // 0 = direct 4-aligned windows, 1 = wave-local LDS transpose, 2 = lean (default)
+
 int launch_stream_framed(const StreamArgs &a, uint64_t n, uint32_t mark_le, bool decode,
                          unsigned long long *errkey, void *stream) {
     if (!n || !a.w) return hipSuccess;
     hipStream_t st = (hipStream_t)stream;
     const uint64_t words = decode ? n * a.w : n * (a.w + 1);
+    // the direct decode kernel holds 5 source words per lane: 4 native words
+    // of records of W < 3 words can span more (two marks), so those take the
+    // LDS variant whatever the knob says
+    if (g_framed_kernel == 1 || (decode && a.w < 3)) {
+        const uint64_t blocks = (words + 1023) / 1024;     // 4 waves x 256 words
+        if (decode)
+            hipLaunchKernelGGL(k_stream_framed_dec_lds, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
+                               1.0 / (double)a.w, errkey);
+        else
+            hipLaunchKernelGGL(k_stream_framed_enc_lds, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
+                               1.0 / (double)(a.w + 1));
+        return (int)hipGetLastError();
+    }
     const uint64_t blocks = (((words + 3) >> 2) + 255) / 256;
+    if (g_framed_kernel == 2) {
+        if (decode) {
+            if (a.all_bswap)
+                hipLaunchKernelGGL(k_stream_framed_dec_lean<true>, dim3(blocks), dim3(256), 0, st, a, n, mark_le, errkey);
+            else
+                hipLaunchKernelGGL(k_stream_framed_dec_lean<false>, dim3(blocks), dim3(256), 0, st, a, n, mark_le, errkey);
+        } else {
+            if (a.all_bswap)
+                hipLaunchKernelGGL(k_stream_framed_enc_lean<true>, dim3(blocks), dim3(256), 0, st, a, n, mark_le);
+            else
+                hipLaunchKernelGGL(k_stream_framed_enc_lean<false>, dim3(blocks), dim3(256), 0, st, a, n, mark_le);
+        }
+        return (int)hipGetLastError();
+    }
     if (decode)
         hipLaunchKernelGGL(k_stream_framed_dec, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
                            1.0 / (double)a.w, errkey);
@@ -473,6 +740,7 @@ int set_tuning(int key, long long value) {
     case 2: g_stream_nt = (int)(value & 3); return 0;
     case 3: if (value < 0) return -1; g_stream_blocks_per_cu = (int)value; return 0;
     case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12: case 13: return set_rec_tuning(key, value);
+    case 14: if (value < 0 || value > 2) return -1; g_framed_kernel = (int)value; return 0;
     default: return -1;
     }
 }

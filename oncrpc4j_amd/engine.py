@@ -22,6 +22,9 @@ _LIB = None
 # record-path implementation the library starts with (kernels_rec.hip
 # g_rec_kernel: 4 = staged sub-batches, 0 = group per record, 3 = lane per record)
 DEFAULT_REC_KERNEL = 4
+# record-marked streaming kernel the library starts with (kernels_fixed.hip
+# g_framed_kernel: 0 = direct 4-aligned windows, 1 = wave-local LDS transpose, 2 = lean)
+DEFAULT_FRAMED_KERNEL = 2
 
 
 def lib():

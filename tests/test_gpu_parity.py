@@ -160,14 +160,32 @@ def test_random_parity(gpu_ctx, rec_kernel, name, n, framed):
         assert g2[:3] == (0, n, 0) and g2[3].equal(o[3])
 
 
+AOS_EXTRA = {"float_words": [(F, SC, 0), (I, SC, 0), (O, FX, 4)] * 2,
+             "one_word": [(I, SC, 0)], "wide_words": [(I, FX, 37)]}
+
+
+FRAMED_KERNELS = {"direct": 0, "lds": 1, "lean": 2}
+
+
+@pytest.fixture(params=sorted(FRAMED_KERNELS))
+def framed_kernel(request):
+    """Record-marked streaming kernels (kernels_fixed.hip, tuning key 14):
+    direct 4-aligned windows, the wave-local LDS transpose, or the lean
+    variant (wave-uniform divmod, no op table for plain int words)."""
+    _tune(14, FRAMED_KERNELS[request.param])
+    yield request.param
+    _tune(14, engine.DEFAULT_FRAMED_KERNEL)
+
+
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
-@pytest.mark.parametrize("n", [4099, 4100])
-@pytest.mark.parametrize("name", ["cfg2_8xint", "words_mixed", "odd_words", "float_words"])
-def test_aos_layout(gpu_ctx, name, n, framed):
+@pytest.mark.parametrize("n", [4099, 4100, 70001])
+@pytest.mark.parametrize("name", ["cfg2_8xint", "words_mixed", "odd_words", "float_words", "one_word",
+                                  "wide_words"])
+def test_aos_layout(gpu_ctx, framed_kernel, name, n, framed):
     """Array-of-structs native records (one struct per record, fields at their
     XDR word positions): the streaming paths (raw: n*words a multiple of 4;
     record-marked: single-word types) and the word-map path otherwise."""
-    fields = SCHEMAS.get(name, [(F, SC, 0), (I, SC, 0), (O, FX, 4)] * 2)
+    fields = SCHEMAS.get(name) or AOS_EXTRA[name]
     hb = random_batch(fields, n, seed=7)
     total = hb.xdr_total(framed)
     rc, want, _ = oracle.encode_batch(fields, hb.columns(), n, total + 8, framed=framed)
