@@ -702,6 +702,93 @@ __device__ __forceinline__ uint32_t walk_counts(const RecArgs &a, uint64_t r, ui
     return 0;
 }
 
+// The kRecPerThread records of a thread walked in lockstep, field by field
+// (schemas without conditional fields): their length words are independent
+// loads, issued together (clamped addresses, no per-load guard) before any
+// is used, so a thread waits once per dynamic field instead of once per
+// record and field as the serial walk_counts does.  Per record the checks
+// and their order are walk_counts' (Xdr.java:171-531, 1028-1037): err[j] =
+// 0 or the code of its first failing check, sub[j] that check's position;
+// counts are stored for the dynamic fields the walk passed.
+__device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t r0, uint32_t nj,
+                                                     uint32_t *cnt_row, uint32_t (&err)[kRecPerThread],
+                                                     uint32_t (&sub)[kRecPerThread]) {
+    constexpr uint32_t kNone = 0xffu;                         // slot past the batch end
+    const uint8_t *dummy = (const uint8_t *)a.block_sums;     // any 4 readable bytes
+    uint64_t pos[kRecPerThread], end[kRecPerThread];
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        sub[j] = 0;
+        if ((uint32_t)j < nj) {
+            const Extent e = rec_extent(a, r0 + j);
+            pos[j] = e.a; end[j] = e.b; err[j] = 0;
+        } else {
+            pos[j] = end[j] = 0; err[j] = kNone;
+        }
+    }
+    if (a.framed) {   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
+        uint32_t m[kRecPerThread];
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            const bool ok = !err[j] && end[j] - pos[j] >= 4;
+            m[j] = *(const uint32_t *)(ok ? a.xdr + pos[j] : dummy);
+        }
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            if (err[j]) continue;
+            if (end[j] - pos[j] < 4) { err[j] = XDRG_E_SHORT; continue; }
+            const uint32_t mk = bswap32r(m[j]);
+            const uint64_t want_len = a.rec_in ? end[j] - pos[j] - 4 : a.rec_stride - 4;
+            if (!(mk & kLastFrag) || (uint64_t)(mk & kSizeMask) != want_len) { err[j] = XDRG_E_FRAME; continue; }
+            pos[j] += 4;
+        }
+    }
+    uint32_t d = 0;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind != XDRG_K_DYNAMIC) {
+#pragma unroll
+            for (int j = 0; j < kRecPerThread; ++j) {
+                if (err[j]) continue;
+                sub[j] = 2 * k + 1;
+                if (end[j] - pos[j] < f.xbytes) err[j] = XDRG_E_SHORT;   // ensureBytes
+                else pos[j] += f.xbytes;
+            }
+            continue;
+        }
+        uint32_t w[kRecPerThread];
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {   // all length words in flight
+            const bool ok = !err[j] && end[j] - pos[j] >= 4;
+            w[j] = *(const uint32_t *)(ok ? a.xdr + pos[j] : dummy);
+        }
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            if (err[j]) continue;
+            sub[j] = 2 * k + 1;
+            if (end[j] - pos[j] < 4) { err[j] = XDRG_E_SHORT; continue; }   // length word (Xdr.java:171-175)
+            const int32_t len = (int32_t)bswap32r(w[j]);
+            pos[j] += 4;
+            uint64_t need;
+            if (f.xsz == 1) {
+                if (len == 0) need = 0;                                      // Xdr.java:376-378
+                else if (len < 0) { err[j] = XDRG_E_CORRUPT; continue; }     // checkArraySize :1034-1037
+                else need = (uint64_t)len + pad4((uint64_t)len);
+            } else {
+                if (len < 0) { err[j] = XDRG_E_CORRUPT; continue; }
+                need = (uint64_t)len * f.xsz;
+            }
+            if (end[j] - pos[j] < need) { err[j] = XDRG_E_SHORT; continue; }
+            pos[j] += need;
+            cnt_row[(size_t)d * kRecPerBlock + j] = (uint32_t)len;
+        }
+        ++d;
+    }
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j)
+        if (err[j] == kNone) err[j] = 0;
+}
+
 // LDS: scnt[ND][RPB] u32.  Also stores every record's counts in
 // a.rec_cnt[d * n + r] so the place kernel never walks the stream again.
 __global__ __launch_bounds__(kRecThreads) void k_dec_sizes_g(const RecArgs a) {
@@ -710,8 +797,26 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_sizes_g(const RecArgs a) {
     const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
     const uint32_t t0 = threadIdx.x * kRecPerThread;
     bool dead = false;
+    if (!a.ncond) {
 #pragma unroll
-    for (int j = 0; j < kRecPerThread; ++j) {
+        for (int j = 0; j < kRecPerThread; ++j)
+            for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
+        const uint64_t r0 = rb + t0;
+        const uint32_t nj = r0 < a.n ? (uint32_t)(a.n - r0 < (uint64_t)kRecPerThread ? a.n - r0 : (uint64_t)kRecPerThread)
+                                     : 0u;
+        uint32_t err[kRecPerThread], sub[kRecPerThread];
+        walk_counts_lockstep(a, r0, nj, scnt + t0, err, sub);
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            if (!dead && err[j]) {
+                atomicMin(a.errkey, err_key(r0 + j, sub[j], err[j]));
+                dead = true;   // later records of this thread are past the error
+            }
+            if (dead)
+                for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
+        }
+    }
+    for (int j = 0; a.ncond && j < kRecPerThread; ++j) {   // conditional schemas: serial walk
         const uint64_t r = rb + t0 + j;
         for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
         if (r >= a.n || dead) continue;
@@ -1028,14 +1133,17 @@ __device__ __forceinline__ void dec_words4(uint8_t *const (&dst)[R], const uint8
 // Average XDR bytes per record of this block >= a.big_rec (the split between
 // the group and the staged kernels, both launched over the whole grid).
 // Encode reads the scanned block sums, decode the record extents.
-__device__ __forceinline__ bool block_is_big(const RecArgs &a, bool decode) {
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+__device__ __forceinline__ bool block_is_big_at(const RecArgs &a, uint64_t b, bool decode) {
+    const uint64_t rb = b * kRecPerBlock;
     const uint64_t nrec = a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock;
     uint64_t bytes;
-    if (!decode) bytes = (blockIdx.x + 1 < a.nblocks ? a.block_sums[blockIdx.x + 1] : a.totals[0]) - a.block_sums[blockIdx.x];
+    if (!decode) bytes = (b + 1 < a.nblocks ? a.block_sums[b + 1] : a.totals[0]) - a.block_sums[b];
     else if (a.rec_in) bytes = a.rec_in[rb + nrec] - a.rec_in[rb];
     else bytes = a.rec_stride * nrec;
     return bytes >= (uint64_t)a.big_rec * nrec;
+}
+__device__ __forceinline__ bool block_is_big(const RecArgs &a, bool decode) {
+    return block_is_big_at(a, blockIdx.x, decode);
 }
 
 template <int U, int R>

@@ -408,3 +408,36 @@ def test_cfg2_full_size_roundtrip(gpu_ctx):
     assert torch.equal(v[:, 4:], out.view(n, 32))
     mark = torch.tensor([0x80, 0, 0, 32], dtype=torch.uint8, device="cuda")
     assert torch.equal(v[:, :4], mark.expand(n, 4))
+
+
+# ---- big records (blocks averaging >= 1 KiB: the group kernels) and mixed blocks
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+@pytest.mark.parametrize("name", ["cfg3_6xint_opaque", "cfg4_int_string_intvec", "cfg1_int_int_string"])
+def test_big_records(gpu_ctx, name, framed):
+    """Records of 1-6 KiB (every block big) and a mix of small and big blocks:
+    bytes, offsets and values against the oracle; then error parity (cut
+    stream, negative / huge length) and a too-small native column."""
+    fields = SCHEMAS[name]
+    for n, dyn in ((3000, (1000, 6000)), (5000, (0, 2600))):
+        hb = random_batch(fields, n, seed=zlib.crc32(f"big/{name}/{framed}/{n}".encode()), dyn_len=dyn)
+        rc, want, want_offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total(framed) + 8,
+                                                  framed=framed)
+        assert rc == 0
+        xdr, offs = gpu_encode(gpu_ctx, fields, hb, framed)
+        assert xdr == want
+        assert np.array_equal(offs, want_offs)
+        caps = hb.dyn_caps()
+        g = gpu_decode(gpu_ctx, fields, xdr, n, offs, caps, framed)
+        o = oracle_decode(fields, xdr, n, offs, caps, framed)
+        assert g[:3] == o[:3] == (0, n, 0)
+        assert g[3].equal(o[3])
+        for desc, bad, ro in _corrupt_cases(fields, hb, xdr, offs, framed):
+            o = oracle_decode(fields, bad, n, ro, caps, framed)
+            g = gpu_decode(gpu_ctx, fields, bad, n, ro, caps, framed)
+            assert g[:3] == o[:3], desc
+            assert g[3].equal(o[3], upto=o[1]), desc
+        small = {k: v // 2 for k, v in caps.items()}
+        o = oracle_decode(fields, xdr, n, offs, small, framed)
+        g = gpu_decode(gpu_ctx, fields, xdr, n, offs, small, framed)
+        assert o[0] == abi.E_CAPACITY and g[:3] == o[:3]
+        assert g[3].equal(o[3], upto=o[1])
