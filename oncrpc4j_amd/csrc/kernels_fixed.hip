@@ -24,6 +24,8 @@ namespace xdrg {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+static int g_words_lane = 1;   // tuning key 16: 1 = lane-per-record word kernels where eligible
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // Float.floatToIntBits: every NaN -> 0x7fc00000 (Xdr.java:674-676).
@@ -741,6 +743,7 @@ int set_tuning(int key, long long value) {
     case 3: if (value < 0) return -1; g_stream_blocks_per_cu = (int)value; return 0;
     case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12: case 13: return set_rec_tuning(key, value);
     case 14: if (value < 0 || value > 2) return -1; g_framed_kernel = (int)value; return 0;
+    case 16: if (value < 0 || value > 1) return -1; g_words_lane = (int)value; return 0;
     default: return -1;
     }
 }
@@ -761,6 +764,123 @@ int launch_wordmap_encode(const WordMapArgs &args, bool aligned16, void *stream)
     hipStream_t st = (hipStream_t)stream;
     if (aligned16) hipLaunchKernelGGL(k_wordmap_encode<true>, dim3(blocks), dim3(256), 0, st, a);
     else hipLaunchKernelGGL(k_wordmap_encode<false>, dim3(blocks), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Lane-per-record word kernels: fixed schemas whose every XDR word is one
+// 4-byte native word (int/uint/enum/float, hyper halves, 4-byte opaque runs)
+// in any column layout — struct-of-arrays above all, the layout a Java
+// BatchXdrEncoder fills (one direct buffer per field).  A lane owns a record:
+// its native words are loads at uniform column bases (consecutive lanes,
+// consecutive elements: coalesced per column), its XDR record one contiguous
+// run written with 16-byte stores when records are 16-byte multiples.  The
+// word table is read at compile-time positions (the loop over the record's
+// words is unrolled), so no LDS and no per-word table lookup: the word-map
+// kernels' per-word LDS reads, 64-bit address math and op switch made them
+// VALU-bound (config 2 SoA: 1.11 / 0.96 ms vs 0.66 for the AoS stream).
+// ---------------------------------------------------------------------------
+constexpr int kLaneWords = 16;   // XDR words per record (incl. the mark) on these kernels
+
+__device__ __forceinline__ void lane_op(const WordMapArgs &a, int w, uint32_t &op, uint32_t &col, uint32_t &off) {
+    // the 8-byte WordOp as one aligned 64-bit kernel-argument load (no byte-wide
+    // member read at its own address: the SMEM base hazard of DESIGN.md §8)
+    const uint64_t raw = *(const uint64_t *)&a.ops[w];
+    op = (uint32_t)(raw & 0xff);
+    col = (uint32_t)((raw >> 8) & 0xff);
+    off = (uint32_t)(raw >> 32) + (op == OP_HYPER_HI ? 4u : 0u);   // HI: native bytes [off+4, off+8)
+}
+
+__device__ __forceinline__ uint32_t lane_enc_word(const WordMapArgs &a, int w, uint64_t r) {
+    uint32_t op, col, off;
+    lane_op(a, w, op, col, off);
+    if (op == OP_MARK) return a.mark_le;   // GrizzlyRpcTransport.java:103-110
+    const uint32_t x = *(const uint32_t *)(a.base[col] + (int64_t)r * a.stride[col] + off);
+    return op == OP_OPAQUE ? x : bswap32(op == OP_FLOAT ? canon_f32(x) : x);   // Xdr.java:545, :674
+}
+
+template <bool V16>
+__global__ __launch_bounds__(256) void k_words_lane_enc(const WordMapArgs a) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= a.n) return;
+    const uint32_t wt = a.wt;
+    uint32_t v[kLaneWords];
+#pragma unroll
+    for (int w = 0; w < kLaneWords; ++w)   // every load of the record in flight before the stores
+        v[w] = (uint32_t)w < wt ? lane_enc_word(a, w, r) : 0u;
+    uint8_t *dst = a.xdr + r * wt * 4;
+    if (V16) {
+#pragma unroll
+        for (int q = 0; q < kLaneWords / 4; ++q)
+            if ((uint32_t)(4 * q) < wt) {
+                u32x4 o; o.x = v[4 * q]; o.y = v[4 * q + 1]; o.z = v[4 * q + 2]; o.w = v[4 * q + 3];
+                __builtin_nontemporal_store(o, (u32x4 *)(dst + 16 * q));
+            }
+    } else {
+#pragma unroll
+        for (int w = 0; w < kLaneWords; ++w)
+            if ((uint32_t)w < wt) *(uint32_t *)(dst + 4 * w) = v[w];
+    }
+}
+
+template <bool V16>
+__global__ __launch_bounds__(256) void k_words_lane_dec(const WordMapArgs a) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t wt = a.wt;
+    // records wholly inside xdr_len; the first one that is not is the host's SHORT key
+    if (r >= a.n || (r + 1) * wt * 4 > a.xdr_len) return;
+    const uint8_t *src = a.xdr + r * wt * 4;
+    uint32_t v[kLaneWords];
+    if (V16) {
+#pragma unroll
+        for (int q = 0; q < kLaneWords / 4; ++q)
+            if ((uint32_t)(4 * q) < wt) {
+                const u32x4 x = __builtin_nontemporal_load((const u32x4 *)(src + 16 * q));
+                v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+            }
+    } else {
+#pragma unroll
+        for (int w = 0; w < kLaneWords; ++w)
+            v[w] = (uint32_t)w < wt ? *(const uint32_t *)(src + 4 * w) : 0u;
+    }
+#pragma unroll
+    for (int w = 0; w < kLaneWords; ++w) {
+        if ((uint32_t)w >= wt) continue;
+        uint32_t op, col, off;
+        lane_op(a, w, op, col, off);
+        if (op == OP_MARK) {   // RpcMessageParserTCP.java:63-99
+            if (v[w] != a.mark_le) atomicMin(a.errkey, err_key(r, (uint32_t)w, XDRG_E_FRAME));
+            continue;
+        }
+        // decode keeps raw float bits (Xdr.java:255-257); opaque bytes as they are
+        *(uint32_t *)(a.base[col] + (int64_t)r * a.stride[col] + off) = op == OP_OPAQUE ? v[w] : bswap32(v[w]);
+    }
+}
+
+bool words_lane_ok(const WordOp *ops, uint32_t nops) {
+    if (!nops || nops > (uint32_t)kLaneWords) return false;
+    for (uint32_t w = 0; w < nops; ++w) {
+        const uint8_t op = ops[w].op;
+        if (op == OP_OPAQUE ? ops[w].aux != 4
+                            : !(op == OP_BSWAP || op == OP_FLOAT || op == OP_HYPER_HI || op == OP_HYPER_LO ||
+                                op == OP_MARK))
+            return false;
+    }
+    return true;
+}
+
+int launch_words_lane(const WordMapArgs &a, bool decode, bool v16, void *stream) {
+    if (!g_words_lane) return -1;   // the caller falls back to the word-map kernels
+    if (!a.n) return hipSuccess;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)((a.n + 255) / 256));
+    if (decode) {
+        if (v16) hipLaunchKernelGGL(k_words_lane_dec<true>, grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_words_lane_dec<false>, grid, dim3(256), 0, st, a);
+    } else {
+        if (v16) hipLaunchKernelGGL(k_words_lane_enc<true>, grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_words_lane_enc<false>, grid, dim3(256), 0, st, a);
+    }
     return (int)hipGetLastError();
 }
 

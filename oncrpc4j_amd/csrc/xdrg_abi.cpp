@@ -562,7 +562,11 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
             a.n = n;
             a.xdr = out;
             TimedLaunch t(c, XDRG_KERNEL_FIXED_ENCODE);
-            HIPCHK(c, (hipError_t)launch_wordmap_encode(a, aligned(out, 16), c->stream));
+            int lr = -1;
+            if (words_lane_ok(a.ops, a.nops))
+                lr = launch_words_lane(a, false, aligned(out, 16) && (a.wt % 4) == 0, c->stream);
+            if (lr > 0) HIPCHK(c, (hipError_t)lr);
+            if (lr < 0) HIPCHK(c, (hipError_t)launch_wordmap_encode(a, aligned(out, 16), c->stream));
         } else if (n && total) {
             RecArgs a;
             rc = fill_rec(c, s, (xdrg_column *)cols, n, framed, a);
@@ -740,7 +744,11 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
             dev_key = framed;
             if (dev_key) HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
             TimedLaunch t(c, XDRG_KERNEL_FIXED_DECODE);
-            HIPCHK(c, (hipError_t)launch_wordmap_decode(a, aligned(in, 16), c->stream));
+            int lr = -1;
+            if (words_lane_ok(a.ops, a.nops))
+                lr = launch_words_lane(a, true, aligned(in, 16) && (a.wt % 4) == 0, c->stream);
+            if (lr > 0) HIPCHK(c, (hipError_t)lr);
+            if (lr < 0) HIPCHK(c, (hipError_t)launch_wordmap_decode(a, aligned(in, 16), c->stream));
         } else if (n && stride) {
             RecArgs a;
             rc = fill_rec(c, s, cols, n, framed, a);

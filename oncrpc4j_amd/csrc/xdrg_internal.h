@@ -161,6 +161,10 @@ int set_rec_tuning(int key, long long value);
 int launch_stream_framed(const StreamArgs &a, uint64_t n, uint32_t mark_le, bool decode,
                          unsigned long long *errkey, void *stream);
 int launch_wordmap_encode(const WordMapArgs &a, bool aligned16, void *stream);
+// lane-per-record word kernels (every XDR word one 4-byte native word, <= 32
+// words per record incl. the mark); returns -1 when switched off (tuning)
+bool words_lane_ok(const WordOp *ops, uint32_t nops);
+int launch_words_lane(const WordMapArgs &a, bool decode, bool v16, void *stream);
 int launch_wordmap_decode(const WordMapArgs &a, bool aligned16, void *stream);
 enum RecPhase { REC_ENC_SIZES, REC_ENC_SCAN, REC_ENC_PLACE, REC_DEC_SIZES, REC_DEC_SCAN, REC_DEC_PLACE };
 int launch_rec_phase(const RecArgs &a, int phase, void *stream);

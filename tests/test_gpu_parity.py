@@ -441,3 +441,65 @@ def test_big_records(gpu_ctx, name, framed):
         g = gpu_decode(gpu_ctx, fields, xdr, n, offs, small, framed)
         assert o[0] == abi.E_CAPACITY and g[:3] == o[:3]
         assert g[3].equal(o[3], upto=o[1])
+
+
+# ---- lane-per-record word kernels (kernels_fixed.hip k_words_lane_*, tuning key 16)
+@pytest.mark.parametrize("lane_kernel", [1, 0], ids=["lane", "wordmap"])
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+@pytest.mark.parametrize("name,fields", [
+    ("ints8", [(I, SC, 0)] * 8),
+    ("mixed_words", [(I, SC, 0), (F, SC, 0), (H, SC, 0), (U, FX, 3), (O, FX, 8), (E, SC, 0)]),
+    ("one_word", [(U, SC, 0)]),
+    ("wide", [(I, FX, 15)]),
+    ("past_lane_limit", [(I, FX, 31)]),   # > 16 words: the word-map kernels
+])
+def test_words_lane(gpu_ctx, lane_kernel, framed, name, fields):
+    """Struct-of-arrays and padded-stride columns of 4-byte words, raw and
+    record-marked: bytes and values against the oracle, a cut stream and a
+    corrupted mark against the oracle's first error."""
+    _tune(16, lane_kernel)
+    try:
+        n = 70001
+        hb = random_batch(fields, n, seed=zlib.crc32(f"lane/{name}/{framed}".encode()), special_floats=False)
+        total = hb.xdr_total(framed)
+        rc, want, want_offs = oracle.encode_batch(fields, hb.columns(), n, total + 8, framed=framed)
+        assert rc == 0
+        xdr, _ = gpu_encode(gpu_ctx, fields, hb, framed)
+        assert xdr == want
+        g = gpu_decode(gpu_ctx, fields, xdr, n, None, {}, framed, use_offsets=False)
+        o = oracle_decode(fields, xdr, n, None, {}, framed)
+        assert g[:3] == o[:3] == (0, n, 0) and g[3].equal(o[3])
+        # strided columns: every field of record i at base + 48*i (a padded struct)
+        sch = engine.Schema(fields)
+        rec_native = sum(abi.NATIVE_SIZE[t] * (c if k == FX else 1) for t, k, c in fields)
+        stride = ((rec_native + 47) // 48) * 48
+        offs = [int(x) for x in np.cumsum([0] + [abi.NATIVE_SIZE[t] * (c if k == FX else 1) for t, k, c in fields])[:-1]]
+        buf = np.zeros((n, stride), dtype=np.uint8)
+        expect = np.zeros((n, stride), dtype=np.uint8)
+        for k, a in enumerate(hb.arrays):
+            raw = np.ascontiguousarray(a).view(np.uint8).reshape(n, -1)
+            buf[:, offs[k]:offs[k] + raw.shape[1]] = raw
+            if fields[k][0] == F:   # encode canonicalises NaNs (Xdr.java:674-676); decode keeps those bits
+                bits = np.ascontiguousarray(a).view(np.uint32).copy()
+                bits[np.isnan(np.ascontiguousarray(a))] = 0x7fc00000
+                raw = bits.view(np.uint8).reshape(n, -1)
+            expect[:, offs[k]:offs[k] + raw.shape[1]] = raw
+        dev = torch.from_numpy(buf).cuda()
+        out = torch.zeros(total, dtype=torch.uint8, device="cuda")
+        assert gpu_ctx.encode(sch, aos_columns(fields, dev.data_ptr(), stride, list(offs)), n, out, total,
+                              framed=framed) == total
+        assert out.cpu().numpy().tobytes() == want
+        back = torch.zeros_like(dev)
+        gpu_ctx.decode(sch, out, total, n, aos_columns(fields, back.data_ptr(), stride, list(offs)), framed=framed)
+        assert torch.equal(back.cpu(), torch.from_numpy(expect))
+        # first error: a cut stream (SHORT) and, framed, a corrupted mark (FRAME)
+        cut = want[:len(want) - 5]
+        g = gpu_decode(gpu_ctx, fields, cut, n, None, {}, framed, use_offsets=False)
+        assert g[:3] == oracle_decode(fields, cut, n, None, {}, framed)[:3]
+        if framed:
+            bad = bytearray(want)
+            bad[int(want_offs[n // 2])] ^= 0x80
+            g = gpu_decode(gpu_ctx, fields, bytes(bad), n, None, {}, True, use_offsets=False)
+            assert g[:3] == oracle_decode(fields, bytes(bad), n, None, {}, True)[:3] == (abi.E_FRAME, n // 2, abi.E_FRAME)
+    finally:
+        _tune(16, 1)
