@@ -24,7 +24,7 @@ namespace xdrg {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-static int g_words_lane = 1;   // tuning key 16: 1 = lane-per-record word kernels where eligible
+static int g_words_lane = 2;   // tuning key 16: 0 word-map, 1 lane-per-record, 2 LDS-staged lane (default)
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -743,7 +743,7 @@ int set_tuning(int key, long long value) {
     case 3: if (value < 0) return -1; g_stream_blocks_per_cu = (int)value; return 0;
     case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12: case 13: return set_rec_tuning(key, value);
     case 14: if (value < 0 || value > 2) return -1; g_framed_kernel = (int)value; return 0;
-    case 16: if (value < 0 || value > 1) return -1; g_words_lane = (int)value; return 0;
+    case 16: if (value < 0 || value > 2) return -1; g_words_lane = (int)value; return 0;
     default: return -1;
     }
 }
@@ -857,6 +857,127 @@ __global__ __launch_bounds__(256) void k_words_lane_dec(const WordMapArgs a) {
     }
 }
 
+// LDS-staged form of the lane kernels: the block's 256 records sit in LDS as
+// rows of kRowPad (odd) words, so a lane's row writes / reads hit distinct
+// banks, and the block's XDR span — contiguous, 16-byte aligned because it
+// starts at record 256*blockIdx.x of a 16-byte-aligned stream — moves as
+// coalesced 16-byte accesses whatever the record size (the lane kernels' own
+// record stores stride wt*4 bytes per lane: 9-word framed records took
+// scalar stores, 1.95 ms on config 2).
+constexpr int kRowPad = kLaneWords + 1;
+
+__device__ __forceinline__ uint32_t lds_word(const uint32_t *t, uint32_t j, uint32_t wt) {
+    const uint32_t rr = j / wt;
+    return t[rr * kRowPad + (j - rr * wt)];
+}
+
+// Column side, for both directions: quad q of the block is word w = q / 64 of
+// records 4*(q % 64) .. +3 — w is wave-uniform, so its WordOp is a scalar
+// load and a dense 4-byte column (stride 4, 16-byte aligned run) moves as one
+// 16-byte access per lane; other strides take four 4-byte accesses.
+__device__ __forceinline__ void wave_op(const WordMapArgs &a, uint32_t w, uint32_t &op, uint32_t &col, uint32_t &off) {
+    const uint64_t raw = *(const uint64_t *)&a.ops[__builtin_amdgcn_readfirstlane(w)];
+    op = (uint32_t)(raw & 0xff);
+    col = (uint32_t)((raw >> 8) & 0xff);
+    off = (uint32_t)(raw >> 32) + (op == OP_HYPER_HI ? 4u : 0u);
+}
+
+__device__ __forceinline__ uint32_t enc_xform(uint32_t op, uint32_t x) {
+    return op == OP_OPAQUE ? x : bswap32(op == OP_FLOAT ? canon_f32(x) : x);   // Xdr.java:545, :674
+}
+
+__global__ __launch_bounds__(256) void k_words_lds_enc(const WordMapArgs a) {
+    __shared__ uint32_t t[256 * kRowPad];
+    const uint64_t r0 = (uint64_t)blockIdx.x * 256;
+    const uint32_t wt = a.wt;
+    const uint32_t nr = (uint32_t)min<uint64_t>(256, a.n - r0);
+    for (uint32_t q = threadIdx.x; q < 64 * wt; q += 256) {
+        const uint32_t w = q >> 6, i = 4 * (q & 63);
+        uint32_t op, col, off;
+        wave_op(a, w, op, col, off);
+        uint32_t *row = t + i * kRowPad + w;
+        if (op == OP_MARK) {   // GrizzlyRpcTransport.java:103-110
+            row[0] = row[kRowPad] = row[2 * kRowPad] = row[3 * kRowPad] = a.mark_le;
+            continue;
+        }
+        const int64_t st = a.stride[col];
+        const uint8_t *p = a.base[col] + (int64_t)(r0 + i) * st + off;
+        if (i + 4 <= nr && st == 4 && ((uintptr_t)p & 15) == 0) {
+            const u32x4 x = __builtin_nontemporal_load((const u32x4 *)p);
+            row[0] = enc_xform(op, x.x); row[kRowPad] = enc_xform(op, x.y);
+            row[2 * kRowPad] = enc_xform(op, x.z); row[3 * kRowPad] = enc_xform(op, x.w);
+        } else {
+            for (uint32_t k = 0; k < 4 && i + k < nr; ++k) row[k * kRowPad] = enc_xform(op, *(const uint32_t *)(p + k * st));
+        }
+    }
+    __syncthreads();
+    const uint32_t words = nr * wt, quads = words >> 2;
+    uint8_t *dst = a.xdr + r0 * wt * 4;
+    for (uint32_t q = threadIdx.x; q < quads; q += 256) {
+        u32x4 o;
+        o.x = lds_word(t, 4 * q, wt); o.y = lds_word(t, 4 * q + 1, wt);
+        o.z = lds_word(t, 4 * q + 2, wt); o.w = lds_word(t, 4 * q + 3, wt);
+        __builtin_nontemporal_store(o, (u32x4 *)(dst + 16 * q));
+    }
+    for (uint32_t j = 4 * quads + threadIdx.x; j < words; j += 256) *(uint32_t *)(dst + 4 * j) = lds_word(t, j, wt);
+}
+
+__global__ __launch_bounds__(256) void k_words_lds_dec(const WordMapArgs a) {
+    __shared__ uint32_t t[256 * kRowPad];
+    const uint64_t r0 = (uint64_t)blockIdx.x * 256;
+    const uint32_t wt = a.wt;
+    // records wholly inside xdr_len; the first one that is not is the host's SHORT key
+    const uint64_t whole = a.xdr_len / ((uint64_t)wt * 4);
+    const uint64_t lim = min<uint64_t>(a.n, whole);
+    if (r0 >= lim) return;   // block-uniform
+    const uint32_t nr = (uint32_t)min<uint64_t>(256, lim - r0);
+    const uint32_t words = nr * wt, quads = words >> 2;
+    const uint8_t *src = a.xdr + r0 * wt * 4;
+    for (uint32_t q = threadIdx.x; q < quads; q += 256) {
+        const u32x4 x = __builtin_nontemporal_load((const u32x4 *)(src + 16 * q));
+        const uint32_t j = 4 * q;
+        uint32_t rr = j / wt, c = j - rr * wt;
+        t[rr * kRowPad + c] = x.x; if (++c == wt) { c = 0; ++rr; }
+        t[rr * kRowPad + c] = x.y; if (++c == wt) { c = 0; ++rr; }
+        t[rr * kRowPad + c] = x.z; if (++c == wt) { c = 0; ++rr; }
+        t[rr * kRowPad + c] = x.w;
+    }
+    for (uint32_t j = 4 * quads + threadIdx.x; j < words; j += 256) {
+        const uint32_t rr = j / wt;
+        t[rr * kRowPad + (j - rr * wt)] = *(const uint32_t *)(src + 4 * j);
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < 64 * wt; q += 256) {
+        const uint32_t w = q >> 6, i = 4 * (q & 63);
+        if (i >= nr) continue;
+        uint32_t op, col, off;
+        wave_op(a, w, op, col, off);
+        const uint32_t *row = t + i * kRowPad + w;
+        if (op == OP_MARK) {   // RpcMessageParserTCP.java:63-99; the min key is the first bad record
+            for (uint32_t k = 0; k < 4 && i + k < nr; ++k)
+                if (row[k * kRowPad] != a.mark_le) {
+                    atomicMin(a.errkey, err_key(r0 + i + k, w, XDRG_E_FRAME));
+                    break;
+                }
+            continue;
+        }
+        // decode keeps raw float bits (Xdr.java:255-257); opaque bytes as they are
+        const int64_t st = a.stride[col];
+        uint8_t *p = a.base[col] + (int64_t)(r0 + i) * st + off;
+        if (i + 4 <= nr && st == 4 && ((uintptr_t)p & 15) == 0) {
+            u32x4 o;
+            o.x = row[0]; o.y = row[kRowPad]; o.z = row[2 * kRowPad]; o.w = row[3 * kRowPad];
+            if (op != OP_OPAQUE) { o.x = bswap32(o.x); o.y = bswap32(o.y); o.z = bswap32(o.z); o.w = bswap32(o.w); }
+            __builtin_nontemporal_store(o, (u32x4 *)p);
+        } else {
+            for (uint32_t k = 0; k < 4 && i + k < nr; ++k) {
+                const uint32_t v = row[k * kRowPad];
+                *(uint32_t *)(p + k * st) = op == OP_OPAQUE ? v : bswap32(v);
+            }
+        }
+    }
+}
+
 bool words_lane_ok(const WordOp *ops, uint32_t nops) {
     if (!nops || nops > (uint32_t)kLaneWords) return false;
     for (uint32_t w = 0; w < nops; ++w) {
@@ -874,6 +995,11 @@ int launch_words_lane(const WordMapArgs &a, bool decode, bool v16, void *stream)
     if (!a.n) return hipSuccess;
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((unsigned)((a.n + 255) / 256));
+    if (g_words_lane == 2 && ((uintptr_t)a.xdr & 15) == 0) {
+        if (decode) hipLaunchKernelGGL(k_words_lds_dec, grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(k_words_lds_enc, grid, dim3(256), 0, st, a);
+        return (int)hipGetLastError();
+    }
     if (decode) {
         if (v16) hipLaunchKernelGGL(k_words_lane_dec<true>, grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL(k_words_lane_dec<false>, grid, dim3(256), 0, st, a);

@@ -444,7 +444,7 @@ def test_big_records(gpu_ctx, name, framed):
 
 
 # ---- lane-per-record word kernels (kernels_fixed.hip k_words_lane_*, tuning key 16)
-@pytest.mark.parametrize("lane_kernel", [1, 0], ids=["lane", "wordmap"])
+@pytest.mark.parametrize("lane_kernel", [2, 1, 0], ids=["lds", "lane", "wordmap"])
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("name,fields", [
     ("ints8", [(I, SC, 0)] * 8),
@@ -502,4 +502,4 @@ def test_words_lane(gpu_ctx, lane_kernel, framed, name, fields):
             g = gpu_decode(gpu_ctx, fields, bytes(bad), n, None, {}, True, use_offsets=False)
             assert g[:3] == oracle_decode(fields, bytes(bad), n, None, {}, True)[:3] == (abi.E_FRAME, n // 2, abi.E_FRAME)
     finally:
-        _tune(16, 1)
+        _tune(16, 2)

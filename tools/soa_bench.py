@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--records", type=int, default=64 << 20)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--framed", action="store_true")
+    ap.add_argument("--lane-kernel", type=int, default=None, help="tuning key 16 (0 word-map, 1 lane, 2 LDS-staged lane)")
     args = ap.parse_args()
     import torch
     from oncrpc4j_amd import abi, engine
@@ -41,6 +42,11 @@ def main():
 
     cin, cout = cols(cols_in), cols(cols_out)
     ctx = engine.Context(0, timing=True)
+    if args.lane_kernel is not None:
+        import ctypes
+        L = engine.lib()
+        L.xdrg_internal_tune.argtypes = [ctypes.c_int, ctypes.c_longlong]
+        assert L.xdrg_internal_tune(16, args.lane_kernel) == 0
     ctx.set_stream(torch.cuda.current_stream())
     ctx.encode(sch, cin, n, xdr, xdr.numel(), framed=args.framed, async_=True)
     ctx.decode(sch, xdr, xdr.numel(), n, cout, framed=args.framed, async_=True)
@@ -63,6 +69,7 @@ def main():
     enc, dec = enc / args.reps, dec / args.reps
     per_launch = n * (32 + rec)
     print(json.dumps({"workload": f"{n} x 8 int32, struct-of-arrays columns" + (", framed" if args.framed else ""),
+                      "lane_kernel": args.lane_kernel,
                       "encode_ms": round(enc, 4), "decode_ms": round(dec, 4),
                       "encode_GBps": round(per_launch / enc / 1e6, 1),
                       "decode_GBps": round(per_launch / dec / 1e6, 1)}), flush=True)
