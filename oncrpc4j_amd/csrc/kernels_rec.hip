@@ -1910,6 +1910,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
     if (a.framed)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
         for (uint32_t j = tid; j < nrec; j += kRecThreads)
             *(uint32_t *)(out + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
+    if (a.probe_skip & 8) return;
     // ---- sub-batches
     uint32_t js = 0;
     uint32_t k1 = enc_fit(a, base, srel, js, nrec);
@@ -1935,7 +1936,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
             cb[d + 1] += stage_chunks(f.data + (base[d] + srel[d * RS + js]) * esz,
                                       f.data + (base[d] + srel[d * RS + je]) * esz, &a0[d]);
         }
-        stage_copy(tile, a0, cb, a.ndyn);
+        if (!(a.probe_skip & 4)) stage_copy(tile, a0, cb, a.ndyn);
         __syncthreads();
         // scatter, field-major; field k of record j sits at
         // soff[j] + (fixed bytes before k) + (dynamic bytes before k)
@@ -1946,7 +1947,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
             const VField &f = a.f[k];
             if (f.kind != XDRG_K_DYNAMIC) {
                 const uint32_t nw = f.xbytes >> 2;
-                if (nw) {
+                if (nw && !(a.probe_skip & 2)) {
                     const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
                     const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
                     for (uint32_t j = js + tid / G; j < je; j += ng) {
@@ -1957,6 +1958,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
                 fpre += f.xbytes;
                 continue;
             }
+            if (a.probe_skip & 1) { ++d; continue; }
             const bool bytes = f.xsz == 1;
             const uint64_t esz = bytes ? 1 : f.nsz;
             const uint32_t *rel = srel + d * RS;
@@ -2129,6 +2131,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
         for (uint32_t j = 0; j < nlive; ++j) dec_record_block(a, rb + j, sstart[j], supto[j]);
         return;
     }
+    if (a.probe_skip & 8) return;
     // ---- sub-batches
     uint32_t js = 0;
     uint32_t k1 = nlive ? dec_fit(a, sstart, snrel, js, nlive) : 0;
@@ -2143,7 +2146,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
         const uint8_t *a0[kMaxDynLds] = {nullptr, nullptr, nullptr, nullptr};
         uint32_t cb[kMaxDynLds + 1] = {0, 0, 0, 0, 0};
         cb[1] = stage_chunks(in + sstart[js], in + sstart[je - 1] + fx + dyn_before(a, snrel, je - 1, a.ndyn), &a0[0]);
-        stage_copy(tile, a0, cb, 1);
+        if (!(a.probe_skip & 4)) stage_copy(tile, a0, cb, 1);
         __syncthreads();
         const int64_t lds0 = -(int64_t)(a0[0] - in);   // tile offset of stream offset x: lds0 + x
         uint32_t fpre = 0;
@@ -2153,7 +2156,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
             const VField &f = a.f[k];
             if (f.kind != XDRG_K_DYNAMIC) {
                 const uint32_t nw = f.xbytes >> 2;
-                if (nw) {
+                if (nw && !(a.probe_skip & 2)) {
                     const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
                     const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
                     for (uint32_t j = js + tid / G; j < je; j += ng) {
@@ -2166,8 +2169,22 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
                 fpre += f.xbytes;
                 continue;
             }
+            if (a.probe_skip & 1) { ++d; continue; }
             const bool bytes = f.xsz == 1;
             const uint64_t esz = bytes ? 1 : f.nsz;
+            if (a.probe_skip & 16) {   // probe: aligned flat stores over the column range, no gather
+                uint8_t *cb0 = f.data + a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x] * esz;
+                const uint32_t *rl = snrel + d * RS;
+                const uintptr_t X0 = ((uintptr_t)(cb0 + (uint64_t)rl[js] * esz) + 15) & ~(uintptr_t)15;
+                const uintptr_t X1 = (uintptr_t)(cb0 + (uint64_t)rl[je] * esz) & ~(uintptr_t)15;
+                for (uintptr_t x = X0 + 16 * (uintptr_t)tid; x < X1; x += 16 * kRecThreads) {
+                    const uint32_t *w = (const uint32_t *)(tile + ((x - X0) & 0x3ff0));
+                    u32x4n v; v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3];
+                    *(u32x4n *)x = v;
+                }
+                ++d;
+                continue;
+            }
             const uint32_t *rel = snrel + d * RS;
             const uint64_t base = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x];
             const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
@@ -2264,7 +2281,16 @@ static int g_rec_kernel = 4;   // 4 = staged (default), 0 = group per record, 3 
 static uint32_t g_tile_bytes = 16384;
 static uint32_t g_big_rec = 1024;   // XDR bytes per record from which blocks take the group kernel
 static uint32_t g_lane_bytes_enc = 32, g_lane_bytes_dec = 32;
+static uint32_t g_probe_skip = 0;
 int set_rec_tuning(int key, long long value) {
+    if (key == 17) {   // probe only (tools/probe_stage_parts.py): the staged kernels skip parts
+                       // (bit0 dynamic scatter, bit1 fixed scatter, bit2 stage loads, bit3 all after
+                       // the prologue; bit4 decode writes its dynamic columns' ranges with aligned
+                       // flat stores, no gather); outputs are wrong under a mask
+        if (value < 0 || value > 31) return -1;
+        g_probe_skip = (uint32_t)value;
+        return 0;
+    }
     if (key == 13) {   // staged kernels: group-kernel split (average XDR bytes per record; 0 = never)
         if (value < 0 || value > (1ll << 31)) return -1;
         g_big_rec = (uint32_t)value;
@@ -2306,6 +2332,7 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
     a.lane_bytes_dec = g_lane_bytes_dec;
     a.tile_bytes = g_tile_bytes;
     a.big_rec = 0;
+    a.probe_skip = g_probe_skip;
     if (phase == REC_DEC_SIZES && getenv("XDRG_DEBUG"))
         hipLaunchKernelGGL(k_debug_recargs, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
     hipStream_t st = (hipStream_t)stream;

@@ -134,7 +134,7 @@ struct RecArgs {
                                // kernels, the others the staged ones (0: one kernel for all)
     uint32_t ncond;            // conditional fields in the schema (0: every record has all fields)
     uint32_t byref;            // 0, or 1 + the field encoded by reference / decoded as a view
-    uint32_t rsv2;
+    uint32_t probe_skip;       // probe only (tuning key 17): parts of the staged kernels skipped
     uint64_t *ref_pos;         // byref: encode splice[n] / decode payload_pos[n]
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];

@@ -503,3 +503,46 @@ def test_words_lane(gpu_ctx, lane_kernel, framed, name, fields):
             assert g[:3] == oracle_decode(fields, bytes(bad), n, None, {}, True)[:3] == (abi.E_FRAME, n // 2, abi.E_FRAME)
     finally:
         _tune(16, 2)
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+@pytest.mark.parametrize("name", ["cfg4_int_string_intvec", "cfg1_int_int_string", "dyn_vectors"])
+def test_decode_packed_bytes_unaligned_base(gpu_ctx, rec_kernel, name, shift):
+    """Packed byte columns (string<> / opaque<>) decoded at every base
+    misalignment: the staged kernel writes each whole word of a sub-batch's
+    column range once (composing the next records' bytes) and byte-stores
+    only the words shared with neighbouring sub-batches.  Short (0..5 byte)
+    and long strings mixed; guard bytes around the column stay untouched."""
+    fields = SCHEMAS[name]
+    n = 5000
+    hb = random_batch(fields, n, seed=zlib.crc32(f"pack/{name}/{shift}".encode()), dyn_len=(0, 5))
+    rng = np.random.default_rng(shift)
+    for k, (t, kind, _) in enumerate(fields):   # every 7th record long, so sub-batches split
+        if kind == DY and t in (O, STR):
+            vals, offs = hb.arrays[k]
+            lens = np.diff(offs.astype(np.int64))
+            lens[::7] = rng.integers(6, 300, size=lens[::7].size)
+            no = np.zeros(n + 1, dtype=offs.dtype)
+            no[1:] = np.cumsum(lens)
+            hb.arrays[k] = (rng.integers(0, 256, size=int(no[-1]), dtype=np.uint8).astype(vals.dtype), no)
+    rc, want, want_offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total(False), framed=False)
+    assert rc == 0
+    caps = hb.dyn_caps()
+    db = DeviceBatch.empty(fields, n, caps)
+    guard = {}
+    for k, (t, kind, _) in enumerate(fields):
+        if kind == DY and t in (O, STR):
+            tv, to = db.tensors[k]
+            big = torch.full((tv.numel() + 8,), 0x5A, dtype=tv.dtype, device="cuda")
+            guard[k] = big
+            db.tensors[k] = (big[shift:shift + tv.numel()], to)
+    buf = torch.from_numpy(np.frombuffer(want, dtype=np.uint8).copy()).cuda()
+    ro = torch.from_numpy(np.asarray(want_offs, dtype=np.uint64).view(np.int64)).cuda()
+    rc, fb, err = gpu_ctx.decode(engine.Schema(fields), buf, len(want), n, db.columns(), rec_offsets=ro,
+                                 raise_on_error=False)
+    o = oracle_decode(fields, want, n, want_offs, caps)
+    assert (rc, fb, err) == o[:3] == (0, n, 0)
+    for k, big in guard.items():
+        g = big.cpu().numpy().view(np.uint8)
+        assert (g[:shift] == 0x5A).all() and (g[shift + db.tensors[k][0].numel():] == 0x5A).all()
+    assert db.to_host().equal(o[3])
