@@ -2000,9 +2000,12 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
 }
 
 // ---- decode -------------------------------------------------------------------
-// LDS: sstart[RPB + 1] u64 | snrel[ND][RPB + 1] u32 | supto[RPB] u32 | tile[tile_bytes + slack]
+// LDS: sstart[RPB + 1] u32 (record start - the block's first start) | snrel[ND][RPB + 1] u32 |
+// supto[RPB] u8 | tile[tile_bytes + slack]: 29.4 KB with two dynamic fields, so
+// five blocks fit a CU (the u64 starts and u32 field limits of the first
+// version held it at four)
 __host__ __device__ constexpr size_t dec_stage_meta(uint32_t nd) {
-    return ((size_t)(kRecPerBlock + 1) * 8 + (size_t)nd * (kRecPerBlock + 1) * 4 + (size_t)kRecPerBlock * 4 +
+    return ((size_t)(kRecPerBlock + 1) * 4 + (size_t)nd * (kRecPerBlock + 1) * 4 + (size_t)kRecPerBlock +
             15) & ~(size_t)15;
 }
 
@@ -2038,24 +2041,24 @@ __device__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uin
 }
 
 // As enc_fit, over the XDR stream range of records [js, js + 1 + t).
-__device__ __forceinline__ uint32_t dec_fit(const RecArgs &a, const uint64_t *sstart, const uint32_t *snrel,
-                                            uint32_t js, uint32_t nlive) {
+__device__ __forceinline__ uint32_t dec_fit(const RecArgs &a, const uint32_t *sstart, uint64_t sb,
+                                            const uint32_t *snrel, uint32_t js, uint32_t nlive) {
     const uint32_t je = js + 1 + threadIdx.x;
     bool fits = false;
     if (je <= nlive) {
         const uint8_t *a0;
-        const uint64_t e = sstart[je - 1] + (a.fixed_xdr - (a.framed ? 4 : 0)) + dyn_before(a, snrel, je - 1, a.ndyn);
-        fits = 16 * stage_chunks(a.xdr + sstart[js], a.xdr + e, &a0) <= a.tile_bytes;
+        const uint64_t e = sb + sstart[je - 1] + (a.fixed_xdr - (a.framed ? 4 : 0)) + dyn_before(a, snrel, je - 1, a.ndyn);
+        fits = 16 * stage_chunks(a.xdr + sb + sstart[js], a.xdr + e, &a0) <= a.tile_bytes;
     }
     return (uint32_t)__syncthreads_count(fits);
 }
 
-__global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
+__global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;
-    uint64_t *sstart = (uint64_t *)smem;
-    uint32_t *snrel = (uint32_t *)(sstart + RS);
-    uint32_t *supto = snrel + (size_t)a.ndyn * RS;
+    uint32_t *sstart = (uint32_t *)smem;
+    uint32_t *snrel = sstart + RS;
+    uint8_t *supto = (uint8_t *)(snrel + (size_t)a.ndyn * RS);
     uint8_t *tile = smem + dec_stage_meta(a.ndyn);
     __shared__ uint32_t s_wide;
     if (a.big_rec && block_is_big(a, true)) return;   // the group kernel's block
@@ -2067,14 +2070,19 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
     const uint32_t nlive = bad > rb ? (uint32_t)(bad - rb < (uint64_t)nrec ? bad - rb : (uint64_t)nrec) : 0;
     if (tid == 0) s_wide = 0;
     // ---- prologue: counts, native offsets (written to the columns), capacity, extents
+    const uint64_t sb = nlive ? rec_extent(a, rb).a + (a.framed ? 4 : 0) : 0;   // stream offset of sstart 0
     uint32_t upto[kRecPerThread];
+    bool wide = false;
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) {
         const bool live = t0 + j < nlive;
         upto[j] = live ? a.nf : 0u;
-        if (live) sstart[t0 + j] = rec_extent(a, rb + t0 + j).a + (a.framed ? 4 : 0);
+        if (live) {
+            const uint64_t st = rec_extent(a, rb + t0 + j).a + (a.framed ? 4 : 0);
+            wide |= st < sb || st - sb >= (1ull << 31);   // out of order or beyond 31 bits: direct path
+            sstart[t0 + j] = (uint32_t)(st - sb);
+        }
     }
-    bool wide = false;
 #pragma unroll
     for (int d = 0; d < kMaxDynLds; ++d) {
         if ((uint32_t)d >= a.ndyn) continue;
@@ -2109,7 +2117,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
         if (blockIdx.x == 0 && tid == 0) f.offsets[a.n] = a.totals[d];
     }
 #pragma unroll
-    for (int j = 0; j < kRecPerThread; ++j) supto[t0 + j] = upto[j];
+    for (int j = 0; j < kRecPerThread; ++j) supto[t0 + j] = (uint8_t)upto[j];
     __syncthreads();
     // staging needs every record's fields to end where the next begins or
     // before (records in stream order); otherwise the block goes direct
@@ -2128,27 +2136,29 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
     const uint8_t *in = a.xdr;
 
     if (wide) {
-        for (uint32_t j = 0; j < nlive; ++j) dec_record_block(a, rb + j, sstart[j], supto[j]);
+        for (uint32_t j = 0; j < nlive; ++j)
+            dec_record_block(a, rb + j, rec_extent(a, rb + j).a + (a.framed ? 4 : 0), supto[j]);
         return;
     }
     if (a.probe_skip & 8) return;
     // ---- sub-batches
     uint32_t js = 0;
-    uint32_t k1 = nlive ? dec_fit(a, sstart, snrel, js, nlive) : 0;
+    uint32_t k1 = nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
     while (js < nlive) {
         if (k1 == 0) {   // too large for the tile: the whole block decodes record js
-            dec_record_block(a, rb + js, sstart[js], supto[js]);
+            dec_record_block(a, rb + js, sb + sstart[js], supto[js]);
             ++js;
-            k1 = js < nlive ? dec_fit(a, sstart, snrel, js, nlive) : 0;
+            k1 = js < nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
             continue;
         }
         const uint32_t je = js + k1;
         const uint8_t *a0[kMaxDynLds] = {nullptr, nullptr, nullptr, nullptr};
         uint32_t cb[kMaxDynLds + 1] = {0, 0, 0, 0, 0};
-        cb[1] = stage_chunks(in + sstart[js], in + sstart[je - 1] + fx + dyn_before(a, snrel, je - 1, a.ndyn), &a0[0]);
+        cb[1] = stage_chunks(in + sb + sstart[js], in + sb + sstart[je - 1] + fx + dyn_before(a, snrel, je - 1, a.ndyn),
+                             &a0[0]);
         if (!(a.probe_skip & 4)) stage_copy(tile, a0, cb, 1);
         __syncthreads();
-        const int64_t lds0 = -(int64_t)(a0[0] - in);   // tile offset of stream offset x: lds0 + x
+        const int64_t lds0 = -(int64_t)(a0[0] - (in + sb));   // tile offset of sstart value x: lds0 + x
         uint32_t fpre = 0;
         uint32_t d = 0;
         const uint32_t m = je - js;
@@ -2224,7 +2234,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_stage(const RecArgs a) {
             ++d;
         }
         js = je;
-        k1 = js < nlive ? dec_fit(a, sstart, snrel, js, nlive) : 0;   // its barrier ends the tile's use
+        k1 = js < nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;   // its barrier ends the tile's use
     }
 }
 

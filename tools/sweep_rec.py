@@ -27,8 +27,9 @@ DEFAULTS = {9: engine.DEFAULT_REC_KERNEL, 4: 2, 5: 2, 10: 1, 11: 1, 7: 32, 8: 32
 
 VARIANTS = {
     3: [(f"u{u}r{r}", {4: u, 5: u, 10: r, 11: r}) for u in (1, 2, 4) for r in (1, 2)],
-    4: [(f"tile{t}", {12: t}) for t in (4096, 8192, 12288, 16384, 24576)] +
-       [(f"lanebytes{b}", {7: b, 8: b}) for b in (16, 64, 128, 256)],
+    4: [(f"tile{t}", {12: t}) for t in (int(x) for x in os.environ.get(
+        "TILES", "4096,8192,12288,16384,24576").split(","))] +
+       ([] if os.environ.get("TILES") else [(f"lanebytes{b}", {7: b, 8: b}) for b in (16, 64, 128, 256)]),
 }
 
 
