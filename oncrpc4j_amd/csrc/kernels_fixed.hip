@@ -741,7 +741,7 @@ int set_tuning(int key, long long value) {
         return 0;
     case 2: g_stream_nt = (int)(value & 3); return 0;
     case 3: if (value < 0) return -1; g_stream_blocks_per_cu = (int)value; return 0;
-    case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12: case 13: case 17: return set_rec_tuning(key, value);
+    case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12: case 13: case 17: case 18: return set_rec_tuning(key, value);
     case 14: if (value < 0 || value > 2) return -1; g_framed_kernel = (int)value; return 0;
     case 16: if (value < 0 || value > 2) return -1; g_words_lane = (int)value; return 0;
     default: return -1;

@@ -1227,6 +1227,14 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_place_g(const RecArgs a) {
         }
         const uint32_t *cn = scnt + (size_t)d * kRecPerBlock;
         const uint64_t *sr = ssrc + (size_t)d * kRecPerBlock;
+        if (a.payk == d + 1) {   // k_enc_payload moves this field: hand over its position
+            for (uint32_t j = tid; j < nrec; j += kRecThreads) a.pay_pos[rb + j] = soff[j] + fixed_delta;
+            __syncthreads();
+            for (uint32_t j = tid; j < nrec; j += kRecThreads) soff[j] += dyn_xdr_bytes(f, cn[j]);
+            __syncthreads();
+            ++d;
+            continue;
+        }
         uint64_t ps = 0;
         for (uint32_t j = tid; j < nrec; j += kRecThreads) ps += cn[j];
         const uint64_t fbytes = block_sum(ps) * (f.xsz == 1 ? 1 : f.xsz) + 4 * nrec;
@@ -1361,6 +1369,15 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
         }
         const uint32_t *cn = scnt + (size_t)d * kRecPerBlock;
         const uint64_t *no = snoff + (size_t)d * kRecPerBlock;
+        if (a.payk == d + 1) {   // k_dec_payload moves this field (records the walk passed only)
+            for (uint32_t j = tid; j < nrec; j += kRecThreads)
+                a.pay_pos[rb + j] = k < supto[j] ? sstart[j] + fixed_delta : ~0ull;
+            __syncthreads();
+            for (uint32_t j = tid; j < nrec; j += kRecThreads) sstart[j] += dyn_xdr_bytes(f, cn[j]);
+            __syncthreads();
+            ++d;
+            continue;
+        }
         uint64_t ps = 0;
         for (uint32_t j = tid; j < nrec; j += kRecThreads) ps += cn[j];
         const uint64_t fbytes = block_sum(ps) * (f.xsz == 1 ? 1 : f.xsz) + 4 * nrec;
@@ -1404,6 +1421,109 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
         __syncthreads();
         ++d;
     }
+}
+
+// ---- payload kernels (large byte payloads of the group kernels' blocks) -----
+// Config 3's payload copy bound (tools/probes/record_copy.hip,
+// profiles/r01_configs/record_copy_probe.txt): a block that owns 1024
+// consecutive 4 KiB records keeps the records in flight at any moment 4 MB
+// apart (28-31 ms per 64 GiB copy); only grids whose neighbouring blocks
+// copy neighbouring records reach 23.5 ms.  The group kernels compute every
+// record's placement (block scan) and write the other fields; for one dynamic
+// byte field (opaque<> / string<>) they only store the field's stream
+// position (pay_pos), and these kernels move it: a wave per record, four
+// consecutive records per block, a one-pass grid, 16-byte accesses with
+// four in flight per lane.  Same bytes as enc_blob_bytes / dec_bytes
+// (Xdr.java:765-800 length, bytes, zero pad; :341-383 decode).
+__device__ __forceinline__ bool payload_block(const RecArgs &a, uint64_t r, bool decode) {
+    return !a.big_rec || block_is_big_at(a, r / kRecPerBlock, decode);
+}
+template <uint32_t LPR, bool NT>
+__device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
+    if (r >= a.n || a.totals[0] > a.xdr_cap || !payload_block(a, r, false)) return;
+    const VField &f = a.f[a.dyn_idx[a.payk - 1]];
+    const uint64_t e0 = f.offsets[r], cnt = f.offsets[r + 1] - e0;
+    uint8_t *dst = a.xdr + a.pay_pos[r];
+    const uint8_t *src = f.data + e0;
+    const uint32_t lane = threadIdx.x % LPR;
+    if (lane == 0) *(uint32_t *)dst = bswap32r((uint32_t)cnt);
+    dst += 4;
+    const uint64_t nch = (cnt + 15) >> 4;
+    for (uint64_t c0 = lane; c0 < nch; c0 += 4 * LPR) {
+        u32x4a v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {   // full chunks: all loads in flight first
+            const uint64_t c = c0 + LPR * u;
+            if (16 * c + 16 <= cnt)
+                v[u] = NT ? __builtin_nontemporal_load((const u32x4u *)(src + 16 * c)) : *(const u32x4u *)(src + 16 * c);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t c = c0 + LPR * u;
+            if (c >= nch) continue;
+            if (16 * c + 16 <= cnt) {
+                if (NT) __builtin_nontemporal_store(v[u], (u32x4a *)(dst + 16 * c));
+                else *(u32x4a *)(dst + 16 * c) = v[u];
+                continue;
+            }
+            for (uint32_t i = 0; i < 4; ++i) {   // last chunk: words up to the zero-padded end
+                const uint64_t b = 16 * c + 4 * i;
+                if (b >= cnt) break;
+                const uint64_t k = cnt - b;
+                *(uint32_t *)(dst + b) = k >= 4 ? *(const u32u *)(src + b) : load_bytes(src + b, (uint32_t)k);
+            }
+        }
+    }
+}
+template <uint32_t LPR, bool NT>   // lanes per record: 64 (a wave) or 256 (the block); grid-strided; NT: nontemporal
+__global__ __launch_bounds__(256) void k_enc_payload(const RecArgs a) {
+    const uint64_t step = (uint64_t)gridDim.x * (256 / LPR);
+    for (uint64_t r = (uint64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; r < a.n; r += step)
+        enc_payload_rec<LPR, NT>(a, r);
+}
+template <uint32_t LPR, bool NT>
+__device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
+    if (r >= a.n || !payload_block(a, r, true)) return;
+    const uint64_t pos = a.pay_pos[r];
+    if (pos == ~0ull) return;
+    const uint32_t d = a.payk - 1;
+    const VField &f = a.f[a.dyn_idx[d]];
+    const uint64_t cnt = a.rec_cnt[(uint64_t)d * a.n + r];
+    const uint8_t *src = a.xdr + pos + 4;
+    uint8_t *dst = f.data + f.offsets[r];
+    const uint32_t lane = threadIdx.x % LPR;
+    const uint64_t nch = (cnt + 15) >> 4;
+    for (uint64_t c0 = lane; c0 < nch; c0 += 4 * LPR) {
+        u32x4a v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t c = c0 + LPR * u;
+            if (16 * c + 16 <= cnt)
+                v[u] = NT ? __builtin_nontemporal_load((const u32x4a *)(src + 16 * c)) : *(const u32x4a *)(src + 16 * c);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t c = c0 + LPR * u;
+            if (c >= nch) continue;
+            if (16 * c + 16 <= cnt) {
+                if (NT) __builtin_nontemporal_store(v[u], (u32x4u *)(dst + 16 * c));
+                else *(u32x4u *)(dst + 16 * c) = v[u];
+                continue;
+            }
+            for (uint64_t b = 16 * c; b < cnt; b += 4) {   // last chunk (stream words are 4-aligned)
+                const uint32_t w = *(const uint32_t *)(src + b);
+                const uint64_t k = cnt - b;
+                if (k >= 4) *(u32u *)(dst + b) = w;
+                else for (uint32_t i = 0; i < k; ++i) dst[b + i] = (uint8_t)(w >> (8 * i));
+            }
+        }
+    }
+}
+template <uint32_t LPR, bool NT>   // lanes per record: 64 (a wave) or 256 (the block); grid-strided; NT: nontemporal
+__global__ __launch_bounds__(256) void k_dec_payload(const RecArgs a) {
+    const uint64_t step = (uint64_t)gridDim.x * (256 / LPR);
+    for (uint64_t r = (uint64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; r < a.n; r += step)
+        dec_payload_rec<LPR, NT>(a, r);
 }
 
 // ===========================================================================
@@ -2292,7 +2412,13 @@ static uint32_t g_tile_bytes = 16384;
 static uint32_t g_big_rec = 1024;   // XDR bytes per record from which blocks take the group kernel
 static uint32_t g_lane_bytes_enc = 32, g_lane_bytes_dec = 32;
 static uint32_t g_probe_skip = 0;
+static uint32_t g_payload = 3;   // payload kernels (key 18): 0 off, 1 wave per record, 2 block, 3 wave + nontemporal
 int set_rec_tuning(int key, long long value) {
+    if (key == 18) {
+        if (value < 0 || value > 3) return -1;   // 0 off, 1 wave per record, 2 block per record, 3 = 1 + nontemporal
+        g_payload = (uint32_t)value;
+        return 0;
+    }
     if (key == 17) {   // probe only (tools/probe_stage_parts.py): the staged kernels skip parts
                        // (bit0 dynamic scatter, bit1 fixed scatter, bit2 stage loads, bit3 all after
                        // the prologue; bit4 decode writes its dynamic columns' ranges with aligned
@@ -2335,6 +2461,11 @@ int set_rec_tuning(int key, long long value) {
     return 0;
 }
 
+template <typename K>
+static void launch_payload(K wave, K wave_nt, K block, dim3 grid, hipStream_t st, const RecArgs &a) {
+    hipLaunchKernelGGL(g_payload == 2 ? block : g_payload == 3 ? wave_nt : wave, grid, dim3(256), 0, st, a);
+}
+
 int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
     RecArgs a = args;
     a.force_g = g_force_g;
@@ -2355,6 +2486,12 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
     bool stage = grp && g_rec_kernel == 4;
     for (uint32_t d = 0; d < a.ndyn && stage; ++d)
         stage = stage_type(a.f[a.dyn_idx[d]].type, a.f[a.dyn_idx[d]].xsz);
+    // one dynamic byte field, blocks on the group kernels: the payload kernels move it
+    const bool pay = g_payload && a.pay_pos && a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1 &&
+                     ((stage && g_big_rec) || (grp && !stage && g_rec_kernel == 0));
+    a.payk = pay ? 1u : 0u;
+    const uint64_t pblk = g_payload == 2 ? a.n : (a.n + 3) / 4;   // one record (group) per lane group
+    const dim3 pgrid((unsigned)(pblk < (1u << 22) ? pblk : (1u << 22)));
     switch (phase) {
     case REC_ENC_SIZES: hipLaunchKernelGGL(k_enc_sizes, dim3(nb), dim3(kRecThreads), 0, st, a); break;
     case REC_ENC_SCAN:
@@ -2366,10 +2503,12 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
             hipLaunchKernelGGL(k_enc_stage, dim3(nb), dim3(kRecThreads),
                                enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             if (a.big_rec) launch_ur<EncG>(g_enc_u, g_enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
+            if (a.big_rec && pay) launch_payload(k_enc_payload<64, false>, k_enc_payload<64, true>, k_enc_payload<256, false>, pgrid, st, a);
         } else if (lane || (grp && g_rec_kernel == 3)) {
             hipLaunchKernelGGL(k_enc_lane, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
             launch_ur<EncG>(g_enc_u, g_enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
+            if (pay) launch_payload(k_enc_payload<64, false>, k_enc_payload<64, true>, k_enc_payload<256, false>, pgrid, st, a);
         }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
@@ -2388,10 +2527,12 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
             hipLaunchKernelGGL(k_dec_stage, dim3(nb), dim3(kRecThreads),
                                dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             if (a.big_rec) launch_ur<DecG>(g_dec_u, g_dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
+            if (a.big_rec && pay) launch_payload(k_dec_payload<64, false>, k_dec_payload<64, true>, k_dec_payload<256, false>, pgrid, st, a);
         } else if (lane || (grp && g_rec_kernel == 3)) {
             hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
             launch_ur<DecG>(g_dec_u, g_dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
+            if (pay) launch_payload(k_dec_payload<64, false>, k_dec_payload<64, true>, k_dec_payload<256, false>, pgrid, st, a);
         }
         else hipLaunchKernelGGL(k_dec_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;

@@ -496,11 +496,14 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
     // block sums [rows][nblocks] | totals [rows] (+ pad) | per-record counts u32 [ndyn][n]
     const size_t sums_words = rows * a.nblocks + rows + 8;
     const size_t cnt_words = (a.ndyn * n + 1) / 2;
-    int rc = ensure_ws(c, sums_words + cnt_words);
+    // | per-record payload positions u64 [n] (one dynamic byte field: k_enc/dec_payload)
+    const size_t pay_words = (a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1) ? n : 0;
+    int rc = ensure_ws(c, sums_words + cnt_words + pay_words);
     if (rc) return rc;
     a.block_sums = c->d_ws;
     a.totals = c->d_ws + rows * a.nblocks;
     a.rec_cnt = (uint32_t *)(c->d_ws + sums_words);
+    a.pay_pos = pay_words ? c->d_ws + sums_words + cnt_words : nullptr;
     a.errkey = c->d_stat;
     return XDRG_OK;
 }

@@ -136,6 +136,11 @@ struct RecArgs {
     uint32_t byref;            // 0, or 1 + the field encoded by reference / decoded as a view
     uint32_t probe_skip;       // probe only (tuning key 17): parts of the staged kernels skipped
     uint64_t *ref_pos;         // byref: encode splice[n] / decode payload_pos[n]
+    uint32_t payk;             // 0, or 1 + the dynamic byte field the payload kernels move for the
+                               // group kernels' blocks (k_enc/dec_payload)
+    uint32_t rsv3;
+    uint64_t *pay_pos;         // payk: per record, stream offset of that field's length word
+                               // (decode: ~0 = not to be written)
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
     int32_t cvals[XDRG_MAX_CASES];  // case values of the conditional fields

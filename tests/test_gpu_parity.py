@@ -411,12 +411,22 @@ def test_cfg2_full_size_roundtrip(gpu_ctx):
 
 
 # ---- big records (blocks averaging >= 1 KiB: the group kernels) and mixed blocks
+@pytest.fixture(params=[3, 1, 2, 0], ids=["pay_wave_nt", "pay_wave", "pay_block", "pay_off"])
+def payload(request):
+    """Payload kernels for a single dynamic byte field on the group kernels'
+    blocks (kernels_rec.hip k_enc/dec_payload, tuning key 18)."""
+    _tune(18, request.param)
+    yield request.param
+    _tune(18, 3)
+
+
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("name", ["cfg3_6xint_opaque", "cfg4_int_string_intvec", "cfg1_int_int_string"])
-def test_big_records(gpu_ctx, name, framed):
+def test_big_records(gpu_ctx, rec_kernel, payload, name, framed):
     """Records of 1-6 KiB (every block big) and a mix of small and big blocks:
     bytes, offsets and values against the oracle; then error parity (cut
-    stream, negative / huge length) and a too-small native column."""
+    stream, negative / huge length) and a too-small native column.  Under
+    every record-path kernel and payload-kernel variant."""
     fields = SCHEMAS[name]
     for n, dyn in ((3000, (1000, 6000)), (5000, (0, 2600))):
         hb = random_batch(fields, n, seed=zlib.crc32(f"big/{name}/{framed}/{n}".encode()), dyn_len=dyn)
