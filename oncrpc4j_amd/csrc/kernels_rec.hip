@@ -1440,6 +1440,8 @@ __device__ __forceinline__ bool payload_block(const RecArgs &a, uint64_t r, bool
 }
 template <uint32_t LPR, bool NT>
 __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
+    // (the checks first: hoisting the metadata loads above them measured ~1 ms
+    // slower here, while it gains ~0.9 ms in dec_payload_rec)
     if (r >= a.n || a.totals[0] > a.xdr_cap || !payload_block(a, r, false)) return;
     const VField &f = a.f[a.dyn_idx[a.payk - 1]];
     const uint64_t e0 = f.offsets[r], cnt = f.offsets[r + 1] - e0;
@@ -1483,14 +1485,14 @@ __global__ __launch_bounds__(256) void k_enc_payload(const RecArgs a) {
 }
 template <uint32_t LPR, bool NT>
 __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
-    if (r >= a.n || !payload_block(a, r, true)) return;
-    const uint64_t pos = a.pay_pos[r];
-    if (pos == ~0ull) return;
+    if (r >= a.n) return;
     const uint32_t d = a.payk - 1;
     const VField &f = a.f[a.dyn_idx[d]];
-    const uint64_t cnt = a.rec_cnt[(uint64_t)d * a.n + r];
+    // metadata loads issued together, before the checks (one round trip ahead of the data)
+    const uint64_t pos = a.pay_pos[r], cnt = a.rec_cnt[(uint64_t)d * a.n + r], o = f.offsets[r];
+    if (pos == ~0ull || !payload_block(a, r, true)) return;
     const uint8_t *src = a.xdr + pos + 4;
-    uint8_t *dst = f.data + f.offsets[r];
+    uint8_t *dst = f.data + o;
     const uint32_t lane = threadIdx.x % LPR;
     const uint64_t nch = (cnt + 15) >> 4;
     for (uint64_t c0 = lane; c0 < nch; c0 += 4 * LPR) {
