@@ -1,25 +1,41 @@
 """bench.py — XDR encode+decode throughput on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): per GPU, 64 Mi records of 8 x int32
-(32 B native, 32 B XDR), seeded synthetic values, native records as an
-array of structs resident in HBM.  One step = xdrg_encode_batch of the whole
-batch (native -> XDR stream) + xdrg_decode_batch of that stream (XDR ->
-native), both through the C-ABI of libxdrgpu.so.  Weak scaling: every rank
-owns its own 64 Mi-record shard (records are independent, no data-path
-collective); with --gpus > 1 the RCCL all-gather that reassembles one
-contiguous stream (configs[4]) is timed separately and reported beside.
+Headline workload (BASELINE.json configs[1]): per GPU, 64 Mi records of
+8 x int32 (32 B native, 32 B XDR), seeded synthetic values, native records as
+an array of structs resident in HBM.  One step = xdrg_encode_batch of the
+whole batch (native -> XDR stream) + xdrg_decode_batch of that stream
+(XDR -> native), both through the C-ABI of libxdrgpu.so.
 
 value = algorithmic bytes of all ranks / max-over-ranks wall time, GiB/s:
 per record encode reads 32 B + writes 32 B, decode reads 32 + writes 32 B
-= 128 B.  roofline: the dominant kernel's launches timed by
-HIP events on the stream the engine launches on (xdrg_ctx_kernel_stats).
-cpu_baseline: the oracle (C restatement of the reference Xdr, "port") on a
-bounded sample on rank 0's host cores.
+= 128 B.  Weak scaling: every rank owns its own 64 Mi-record
+shard (records are independent, no data-path collective).
+
+`--gpus N` runs N ranks, one process per GPU: launched by torch.distributed.run
+(WORLD_SIZE set, must equal N), or, when WORLD_SIZE is unset, by this script
+itself, which spawns the N rank processes before anything touches a GPU.
+With N > 1 the line also carries encode-only and decode-only rates and the
+reassembly of one contiguous stream (configs[4]): RCCL all-gather for
+fixed-size records, size exchange + grouped send/recv for variable-size ones
+(oncrpc4j_amd/parallel.py), timed alone and together with the encode, and
+checked byte for byte against a 1-rank encode of all ranks' records.
+
+`extra_configs` (default run): configs[2] (6 x int32 + opaque<4096>),
+configs[3] (int32 + string<8..256> + int32<0..16>) and the record-marked
+configs[1], each with its own timing, dominant kernel and roofline fraction.
+
+roofline: the dominant kernel's launches timed by HIP events on the stream the
+engine launches on (xdrg_ctx_kernel_stats).  cpu_baseline: the oracle (C
+restatement of the reference Xdr, "port") on bounded samples on rank 0's host
+cores: configs[1] on all threads of the box's share and on one thread, and
+configs[0] (int, int, string[16]) on one thread.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,10 +45,11 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 HBM_COPY_GBS = 6290.0          # measured float4 copy ceiling (same table)
-BYTES_PER_RECORD = 128         # encode 32+32, decode 32+32
+SIZES = {2: 64 << 20, 3: 16 << 20, 4: 32 << 20}
+GATHER_MAX_BYTES = 80e9        # reassembled stream + its 1-rank reference must fit one GPU
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
@@ -42,85 +59,288 @@ def parse():
                         "opaque<4096>, 4 = int32 + string(8..256) + int32<0..16>")
     p.add_argument("--records", type=int, default=0, help="records per GPU (0 = the config's size)")
     p.add_argument("--framed", action="store_true", help="record-marked variant (36 B records)")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline budget (0 = skip)")
+    p.add_argument("--extra", type=int, default=-1,
+                   help="1 = also run the other BASELINE configs (default: on for the plain headline run)")
+    p.add_argument("--extra-steps", type=int, default=5)
+    p.add_argument("--gather-reps", type=int, default=3)
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="cpu_baseline budget (0 = skip)")
     p.add_argument("--no-host-inclusive", action="store_true")
-    return p.parse_args()
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    p.add_argument("--test-codec", default="",
+                   help="tests only: module providing make_workload() (CPU launcher test, gloo)")
+    a = p.parse_args(argv)
+    if a.extra < 0:
+        a.extra = int(a.config == 2 and not a.framed and not a.records and not a.test_codec)
+    return a
 
 
-def dist_setup(args):
-    import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
+# ---------------------------------------------------------------------------
+# launcher: one process per GPU
+# ---------------------------------------------------------------------------
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv):
+    """Spawn args.gpus rank processes of this script (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set) and return the first non-zero exit status.
+    Nothing in this process touches a GPU."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        if c and not rc:
+            rc = c
+    if rc:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+class Rank:
+    """This process's place in the job: world size, rank, collectives."""
+
+    def __init__(self, args):
+        import torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.cuda = not args.test_codec
+        if self.cuda:
+            torch.cuda.set_device(self.local)
+            self.device = torch.device("cuda", self.local)
+        else:
+            self.device = torch.device("cpu")
+        if self.world > 1:
+            import torch.distributed as dist
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.device)
+            else:
+                dist.init_process_group("gloo")
+
+    def sync(self):
+        if self.cuda:
+            import torch
+            torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank, local
+        t = torch.tensor([x], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(self, fn):
+        """Wall time of fn() bracketed by barrier + synchronize on both sides,
+        max over ranks."""
+        self.barrier()
+        self.sync()
+        t0 = time.perf_counter()
+        fn()
+        self.sync()
+        self.barrier()
+        return self.max(time.perf_counter() - t0)
+
+    def close(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
 
 
-def barrier(world):
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-
-
-def max_over_ranks(x, world):
-    if world == 1:
-        return x
+# ---------------------------------------------------------------------------
+# GPU workloads (one BASELINE config made concrete)
+# ---------------------------------------------------------------------------
+def _gen_shard(cfg, n, shard, dev):
+    """Seeded synthetic records of one shard (seed 0x0DCAC4E5 + cfg + 1000 x shard)."""
     import torch
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    g = torch.Generator(device=dev).manual_seed(0x0DCAC4E5 + cfg + 1000 * shard)
+    I32 = dict(dtype=torch.int32, device=dev, generator=g)
+    if cfg == 2:
+        return {"nat": torch.randint(-2**31, 2**31 - 1, (n, 8), **I32)}
+    if cfg == 3:
+        lens = torch.full((n,), 4096, dtype=torch.int64, device=dev)
+        hdr = torch.randint(-2**31, 2**31 - 1, (n, 6), **I32)
+        vals = torch.randint(0, 256, (n * 4096,), dtype=torch.uint8, device=dev, generator=g)
+        return {"hdr": hdr, "dyn": [(lens, vals)]}
+    lens = torch.randint(8, 257, (n,), dtype=torch.int64, device=dev, generator=g)
+    hdr = torch.randint(-2**31, 2**31 - 1, (n, 1), **I32)
+    vals = torch.randint(97, 123, (int(lens.sum()),), dtype=torch.uint8, device=dev, generator=g)
+    k = torch.randint(0, 17, (n,), dtype=torch.int64, device=dev, generator=g)
+    v2 = torch.randint(-2**31, 2**31 - 1, (int(k.sum()),), **I32)
+    return {"hdr": hdr, "dyn": [(lens, vals), (k, v2)]}
 
 
-def cpu_baseline(budget_s):
-    """Oracle (port of the reference Xdr semantics) on the host cores: encode +
-    decode of a bounded sample of the same workload, all threads of the box's
-    share (<= 16), repeated until the budget is spent."""
-    import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    from oncrpc4j_amd import abi
-    from oncrpc4j_amd.columns import HostBatch
-    L = oracle.lib()
-    threads = max(1, min(16, os.cpu_count() or 1))
-    n = 8 << 20
-    fields = [(abi.T_INT, abi.K_SCALAR, 0)] * 8
-    fa = oracle.fields_array(fields)
-    rng = np.random.default_rng(0x0DCAC4E5 + 2)
-    nat = rng.integers(-2**31, 2**31 - 1, size=(n, 8), dtype=np.int32)
-    back = np.zeros_like(nat)
-    xdr = np.zeros(n * 32, dtype=np.uint8)
+def _cat_shards(cfg, n, shards, dev):
+    """The records of several shards back to back (a 1-rank batch of them)."""
+    import torch
+    parts = [_gen_shard(cfg, n, s, dev) for s in shards]
+    if len(parts) == 1:
+        return parts[0]
+    if cfg == 2:
+        return {"nat": torch.cat([p["nat"] for p in parts])}
+    out = {"hdr": torch.cat([p["hdr"] for p in parts]), "dyn": []}
+    for j in range(len(parts[0]["dyn"])):
+        out["dyn"].append((torch.cat([p["dyn"][j][0] for p in parts]),
+                           torch.cat([p["dyn"][j][1] for p in parts])))
+    return out
 
-    def cols(a):
-        arr = (abi.Column * 8)()
-        for k in range(8):
-            arr[k].data = a.ctypes.data + 4 * k
-            arr[k].stride = 32
+
+class Workload:
+    """Device-resident native columns, the XDR stream, decode targets; one step
+    = encode batch + decode batch through the C-ABI."""
+
+    def __init__(self, ctx, cfg, n, framed, shards=(0,), decode_targets=True):
+        import torch
+        from oncrpc4j_amd import abi, engine
+        from oncrpc4j_amd.columns import aos_columns
+        self.ctx, self.cfg, self.framed = ctx, cfg, framed
+        self.n = n * len(shards)
+        n = self.n
+        I, SC, DY = abi.T_INT, abi.K_SCALAR, abi.K_DYNAMIC
+        dev = torch.device("cuda", torch.cuda.current_device())
+        d = _cat_shards(cfg, n // len(shards), list(shards), dev)
+        if cfg == 2:
+            self.fields = [(I, SC, 0)] * 8
+            rec = 36 if framed else 32
+            self.nat = d["nat"]
+            self.back = torch.empty_like(self.nat) if decode_targets else None
+            offs = [4 * k for k in range(8)]
+            self.cin = aos_columns(self.fields, self.nat.data_ptr(), 32, offs)
+            self.cout = aos_columns(self.fields, self.back.data_ptr(), 32, offs) if decode_targets else None
+            self.xlen = n * rec
+            self.native_bytes = n * 32
+            self.rec_offsets = None
+            self.kernels = ("k_stream_framed_enc/dec_lean" if framed else "k_stream_bswap",
+                            abi.KERNEL_FIXED_ENCODE, abi.KERNEL_FIXED_DECODE)
+            self.desc = ("configs[1]: 64 Mi fixed-schema records of 8 x int32 (32 B), encode+decode "
+                         "round trip, array-of-structs native records" if not framed else
+                         "configs[1] record-marked variant (36 B XDR records, one mark per record)")
+        else:
+            nh = 6 if cfg == 3 else 1
+            self.fields = ([(I, SC, 0)] * 6 + [(abi.T_OPAQUE, DY, 0)] if cfg == 3 else
+                           [(I, SC, 0), (abi.T_STRING, DY, 0), (I, DY, 0)])
+            self.hdr = d["hdr"]
+            self.hdr_back = torch.empty_like(self.hdr) if decode_targets else None
+            self.dyn = []       # (values, offsets, values_back, offsets_back) per dynamic field
+            for cnt, vals in d["dyn"]:
+                o = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+                torch.cumsum(cnt, 0, out=o[1:])
+                self.dyn.append((vals, o, torch.empty_like(vals) if decode_targets else None,
+                                 torch.empty_like(o) if decode_targets else None))
+            self.cin = self._cols(self.hdr, [(x[0], x[1]) for x in self.dyn], nh)
+            self.cout = self._cols(self.hdr_back, [(x[2], x[3]) for x in self.dyn], nh) \
+                if decode_targets else None
+            # XDR sizes: fixed part + per dynamic field 4 + payload (+pad)
+            size = torch.full((n,), 4 * nh + (4 if framed else 0), dtype=torch.int64, device=dev)
+            for (t, _, _), x in zip([f for f in self.fields if f[1] == DY], self.dyn):
+                cnt = x[1][1:] - x[1][:-1]
+                size += 4 + (cnt + ((4 - (cnt & 3)) & 3) if t in (abi.T_OPAQUE, abi.T_STRING) else 4 * cnt)
+            self.xlen = int(size.sum())
+            del size
+            self.rec_offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+            self.native_bytes = n * 4 * nh + sum(x[0].numel() * x[0].element_size() for x in self.dyn)
+            self.kernels = ("k_enc_place/k_dec_place (+payload)" if cfg == 3 else "k_enc_stage/k_dec_stage",
+                            abi.KERNEL_VAR_ENCODE, abi.KERNEL_VAR_DECODE)
+            self.desc = ("configs[2]: 16 Mi NFS-WRITE-shaped records, 6 x int32 + opaque<4096>"
+                         if cfg == 3 else
+                         "configs[3]: 32 Mi records int32 + string(8..256) + int32<0..16>")
+        self.xdr = torch.empty(self.xlen, dtype=torch.uint8, device=dev)
+        self.sch = engine.Schema(self.fields)
+        # encode reads native + writes XDR, decode the reverse
+        self.enc_bytes = self.native_bytes + self.xlen
+        self.bytes_per_step = 2 * self.enc_bytes
+
+    def _cols(self, hdr, dyn, nh):
+        from oncrpc4j_amd import abi
+        arr = (abi.Column * len(self.fields))()
+        for k in range(nh):
+            arr[k].data = hdr.data_ptr() + 4 * k
+            arr[k].stride = 4 * nh
+        for j, (v, o) in enumerate(dyn):
+            arr[nh + j].data = v.data_ptr()
+            arr[nh + j].offsets = o.data_ptr()
+            arr[nh + j].cap = v.numel()
+        arr._keep = (hdr, dyn)
         return arr
-    cin, cout = cols(nat), cols(back)
-    out_len = ctypes.c_uint64()
-    fb, err = ctypes.c_uint64(), ctypes.c_int()
-    t0 = time.perf_counter()
-    rounds = 0
-    while True:
-        rc = L.xo_encode_batch_mt(fa, 8, ctypes.addressof(cin), n, xdr.ctypes.data, xdr.size, 0,
-                                  ctypes.byref(out_len), threads)
-        rc |= L.xo_decode_batch_mt(fa, 8, xdr.ctypes.data, xdr.size, n, ctypes.addressof(cout), 0,
-                                   ctypes.byref(fb), ctypes.byref(err), threads)
-        assert rc == 0
-        rounds += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    assert np.array_equal(back, nat)
-    return {"value": round(rounds * n * BYTES_PER_RECORD / dt / GIB, 3), "unit": "GiB/s",
-            "cores": threads, "kind": "port",
-            "mrecords_per_s": round(rounds * n / dt / 1e6, 2),
-            "sample": f"{rounds} x (encode+decode of 8 Mi 8xint32 records), oracle/xdr_oracle.c "
-                      f"xo_*_batch_mt on {threads} threads, {dt:.1f} s"}
+
+    def encode(self):
+        self.ctx.encode(self.sch, self.cin, self.n, self.xdr, self.xlen, rec_offsets=self.rec_offsets,
+                        framed=self.framed, async_=True)
+
+    def decode(self):
+        self.ctx.decode(self.sch, self.xdr, self.xlen, self.n, self.cout, rec_offsets=self.rec_offsets,
+                        framed=self.framed, async_=True)
+
+    def step(self):
+        self.encode()
+        self.decode()
+
+    def xdr_view(self):
+        return self.xdr
+
+    def offsets_view(self):
+        return self.rec_offsets
+
+    def check(self):
+        import torch
+        if self.cfg == 2:
+            assert torch.equal(self.back, self.nat), "decode(encode(x)) != x"
+            if not self.framed:
+                m = min(self.n, 1 << 20) * 8
+                assert torch.equal(self.xdr.view(-1, 4)[:m], self.nat.view(torch.uint8).view(-1, 4)[:m].flip(1))
+            return
+        assert torch.equal(self.hdr_back, self.hdr), "header columns differ"
+        for v, o, vb, ob in self.dyn:
+            assert torch.equal(ob, o), "offsets differ"
+            assert torch.equal(vb, v), "values differ"
+
+    def reset_stats(self):
+        self.ctx.reset_stats()
+
+    def roofline(self, steps):
+        """Dominant kernel's average launch (HIP events, same stream) -> roofline dict."""
+        kname, kid_e, kid_d = self.kernels
+        ne, ms_e = self.ctx.kernel_stats(kid_e)
+        nd, ms_d = self.ctx.kernel_stats(kid_d)
+        launches = ne + nd
+        avg_ms = (ms_e + ms_d) / max(launches, 1)
+        per_launch = self.enc_bytes   # one side read, the other written
+        achieved = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        step_ms = {}
+        for kid, name in ((0, "fixed_encode"), (1, "fixed_decode"), (2, "var_size"), (3, "var_scan"),
+                          (4, "var_encode"), (5, "var_decode")):
+            c, ms = self.ctx.kernel_stats(kid)
+            if c:
+                step_ms[name] = round(ms / steps, 4)
+        roof = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
+                "traffic": load_traffic(kname, self.n),
+                "launches": launches, "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": per_launch}
+        return roof, step_ms
+
+    def gatherable(self, world):
+        return world * self.xlen <= GATHER_MAX_BYTES
+
+    def reference(self, world, n_per_rank):
+        """A 1-rank workload holding every rank's records (encode only)."""
+        return Workload(self.ctx, self.cfg, n_per_rank, self.framed, shards=range(world),
+                        decode_targets=False)
 
 
 def load_traffic(kernel, records):
@@ -139,12 +359,228 @@ def load_traffic(kernel, records):
     return None
 
 
-def host_inclusive(ctx, sch, cols_fn, n, rec_bytes):
+# ---------------------------------------------------------------------------
+# measurement legs
+# ---------------------------------------------------------------------------
+def gather_leg(R, wl, n_per_rank, reps):
+    """Reassemble one contiguous stream from every rank's shard (exact-size
+    exchange, parallel.py): timed alone and with the encode, checked against
+    a 1-rank encode of all ranks' records and by a checksum every rank agrees on."""
+    import torch
+    from oncrpc4j_amd import parallel
+    local, loffs = wl.xdr_view(), wl.offsets_view()
+    sizes = parallel.all_gather_ints(local.numel())
+    total = sum(sizes)
+    out = torch.empty(total, dtype=torch.uint8, device=local.device)
+    out_offs = torch.empty(wl.n * R.world + 1, dtype=torch.int64, device=local.device) \
+        if loffs is not None else None
+
+    def gather():
+        parallel.gather_stream(local, loffs, out=out, out_offsets=out_offs)
+
+    gather()
+    t_g = R.timed(lambda: [gather() for _ in range(reps)]) / reps
+
+    def enc_gather():
+        for _ in range(reps):
+            wl.encode()
+            gather()
+    t_eg = R.timed(enc_gather) / reps
+    h = parallel.stream_hash(out)
+    hashes = parallel.all_gather_ints(h)
+    equal = None
+    if R.rank == 0:
+        ref = wl.reference(R.world, n_per_rank)
+        ref.encode()
+        R.sync()
+        equal = bool(torch.equal(out, ref.xdr_view()))
+        if loffs is not None:
+            equal = equal and bool(torch.equal(out_offs, ref.offsets_view()))
+        del ref
+    R.barrier()
+    fixed = len(set(sizes)) == 1 and out.is_cuda
+    enc_all = wl.enc_bytes * R.world
+    res = {"ms": round(t_g * 1e3, 3), "encode_plus_gather_ms": round(t_eg * 1e3, 3),
+           "stream_bytes": total, "bytes_in_per_gpu": total - sizes[R.rank],
+           "GBps_in_per_gpu": round((total - sizes[R.rank]) / t_g / 1e9, 2),
+           "gather_inclusive_GiB_s": round(enc_all / t_eg / GIB, 3),
+           "gather_inclusive_stream_GiB_s": round(total / t_eg / GIB, 3),
+           "gather_inclusive_Mrec_s": round(wl.n * R.world / t_eg / 1e6, 2),
+           "collective": ("RCCL all_gather_into_tensor (equal shard sizes)" if fixed else
+                          "size all-gather + grouped send/recv (batch_isend_irecv), exact shard bytes"),
+           "check": {"equal_to_1rank_encode": equal, "checksum_ranks_agree": len(set(hashes)) == 1}}
+    del out, out_offs
+    return res
+
+
+def measure(R, args, make, cfg, framed, n, steps, warmup, with_gather):
+    """One config: encode+decode steps (the value), encode-only and decode-only
+    steps, the dominant kernel's roofline, and (N > 1) the stream reassembly."""
+    wl = make(cfg, n, framed)
+    for _ in range(warmup):
+        wl.step()
+    R.sync()
+    wl.check()   # correctness of the measured path, outside the timed region
+    wl.reset_stats()
+    dt = R.timed(lambda: [wl.step() for _ in range(steps)])
+    roof, step_ms = wl.roofline(steps)
+    t_enc = R.timed(lambda: [wl.encode() for _ in range(steps)])
+    t_dec = R.timed(lambda: [wl.decode() for _ in range(steps)])
+    R.sync()
+    wl.check()
+    recs = wl.n * R.world * steps
+    e = {"config": cfg, "framed": bool(framed), "workload": wl.desc, "records_per_gpu": wl.n,
+         "xdr_bytes_per_gpu": wl.xlen, "native_bytes_per_gpu": wl.native_bytes,
+         "bytes_per_step_per_gpu": wl.bytes_per_step, "steps": steps,
+         "ms_per_step": round(dt / steps * 1e3, 4),
+         "GiB_s": round(wl.bytes_per_step * R.world * steps / dt / GIB, 3),
+         "Mrec_s": round(recs / dt / 1e6, 2),
+         "encode_only": {"ms_per_step": round(t_enc / steps * 1e3, 4),
+                         "GiB_s": round(wl.enc_bytes * R.world * steps / t_enc / GIB, 3),
+                         "Mrec_s": round(recs / t_enc / 1e6, 2)},
+         "decode_only": {"ms_per_step": round(t_dec / steps * 1e3, 4),
+                         "GiB_s": round(wl.enc_bytes * R.world * steps / t_dec / GIB, 3),
+                         "Mrec_s": round(recs / t_dec / 1e6, 2)},
+         "roofline": roof, "kernel_ms_per_step": step_ms, "gather": None}
+    if R.world > 1 and with_gather:
+        if wl.gatherable(R.world):
+            e["gather"] = gather_leg(R, wl, n, args.gather_reps)
+        else:
+            e["gather"] = {"skipped": f"{R.world} x {wl.xlen} stream bytes do not fit one GPU "
+                                      "next to their 1-rank reference"}
+    return e, wl
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (oracle, rank 0, N = 1 only)
+# ---------------------------------------------------------------------------
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_threads():
+    """Threads of this process's CPU share: the affinity mask, capped by the
+    box's per-GPU share (OMP_NUM_THREADS is set to it on the GPU box)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS") or aff)
+    return max(1, min(aff, share)), aff
+
+
+def cpu_baseline(budget_s):
+    """Oracle (C restatement of the reference Xdr semantics) on the host
+    cores, bounded samples of the same workloads (oracle/xdr_oracle.c;
+    the reference's own harness is oncrpc4j-benchmark XdrBenchmark.java:17-59):
+    configs[1] on every thread of the share and on one thread, configs[0]
+    (int, int, string[16]) on one thread."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from oncrpc4j_amd import abi
+    L = oracle.lib()
+    threads, aff = _cpu_threads()
+    leg_s = budget_s / 3.0
+
+    def rounds_for(fn, seconds):
+        t0 = time.perf_counter()
+        r = 0
+        while True:
+            fn()
+            r += 1
+            if time.perf_counter() - t0 >= seconds:
+                return r, time.perf_counter() - t0
+
+    # configs[1]: 8 x int32 AoS, 128 B per record round trip
+    n2 = 8 << 20
+    f2 = [(abi.T_INT, abi.K_SCALAR, 0)] * 8
+    fa2 = oracle.fields_array(f2)
+    rng = np.random.default_rng(0x0DCAC4E5 + 2)
+    nat = rng.integers(-2**31, 2**31 - 1, size=(n2, 8), dtype=np.int32)
+    back = np.zeros_like(nat)
+    xdr = np.zeros(n2 * 32, dtype=np.uint8)
+
+    def cols(a):
+        arr = (abi.Column * 8)()
+        for k in range(8):
+            arr[k].data = a.ctypes.data + 4 * k
+            arr[k].stride = 32
+        return arr
+    cin, cout = cols(nat), cols(back)
+    out_len = ctypes.c_uint64()
+    fb, err = ctypes.c_uint64(), ctypes.c_int()
+
+    def cfg2(th):
+        def run():
+            rc = L.xo_encode_batch_mt(fa2, 8, ctypes.addressof(cin), n2, xdr.ctypes.data, xdr.size, 0,
+                                      ctypes.byref(out_len), th)
+            rc |= L.xo_decode_batch_mt(fa2, 8, xdr.ctypes.data, xdr.size, n2, ctypes.addressof(cout), 0,
+                                       ctypes.byref(fb), ctypes.byref(err), th)
+            assert rc == 0
+        r, dt = rounds_for(run, leg_s)
+        assert np.array_equal(back, nat)
+        back[:] = 0
+        return {"GiB_s": round(r * n2 * 128 / dt / GIB, 3), "Mrec_s": round(r * n2 / dt / 1e6, 2),
+                "threads": th, "sample": f"{r} x encode+decode of 8 Mi 8xint32 records, {dt:.1f} s"}
+
+    all_cores = cfg2(threads)
+    single = cfg2(1)
+
+    # configs[0]: (int a, int b, string s) with s 16 ASCII bytes, one thread;
+    # 104 B per record round trip (2 x (native 24 + XDR 28), SURVEY.md §8d)
+    n1 = 1 << 20
+    f1 = [(abi.T_INT, abi.K_SCALAR, 0), (abi.T_INT, abi.K_SCALAR, 0), (abi.T_STRING, abi.K_DYNAMIC, 0)]
+    rng1 = np.random.default_rng(0x0DCAC4E5 + 1)
+    a1 = rng1.integers(-2**31, 2**31 - 1, size=n1, dtype=np.int32)
+    b1 = rng1.integers(-2**31, 2**31 - 1, size=n1, dtype=np.int32)
+    s1 = rng1.integers(97, 123, size=16 * n1, dtype=np.uint8)
+    o1 = np.arange(0, 16 * (n1 + 1), 16, dtype=np.uint64)
+    ab, bb, sb, ob = np.zeros_like(a1), np.zeros_like(b1), np.zeros_like(s1), np.zeros_like(o1)
+
+    def cols1(a, b, s, o):
+        arr = (abi.Column * 3)()
+        arr[0].data, arr[1].data = a.ctypes.data, b.ctypes.data
+        arr[2].data, arr[2].offsets, arr[2].cap = s.ctypes.data, o.ctypes.data, s.size
+        return arr
+    c1in, c1out = cols1(a1, b1, s1, o1), cols1(ab, bb, sb, ob)
+    fa1 = oracle.fields_array(f1)
+    x1 = np.zeros(28 * n1, dtype=np.uint8)
+    ro1 = np.zeros(n1 + 1, dtype=np.uint64)
+
+    def run1():
+        rc = L.xo_encode_batch(fa1, 3, ctypes.addressof(c1in), n1, x1.ctypes.data, x1.size, ro1.ctypes.data, 0,
+                               ctypes.byref(out_len))
+        rc |= L.xo_decode_batch(fa1, 3, x1.ctypes.data, x1.size, ro1.ctypes.data, n1, ctypes.addressof(c1out), 0,
+                                ctypes.byref(fb), ctypes.byref(err))
+        assert rc == 0
+    r1, dt1 = rounds_for(run1, leg_s)
+    assert np.array_equal(ab, a1) and np.array_equal(bb, b1) and np.array_equal(sb, s1)
+    cfg1 = {"GiB_s": round(r1 * n1 * 104 / dt1 / GIB, 3), "Mrec_s": round(r1 * n1 / dt1 / 1e6, 2),
+            "threads": 1, "sample": f"{r1} x encode+decode of 1 Mi (int, int, string[16]) records, {dt1:.1f} s"}
+
+    return {"value": all_cores["GiB_s"], "unit": "GiB/s", "cores": threads, "kind": "port",
+            "mrecords_per_s": all_cores["Mrec_s"],
+            "sample": f"configs[1] {all_cores['sample']} on {threads} threads (oracle/xdr_oracle.c "
+                      f"xo_*_batch_mt)",
+            "cfg2_all_cores": all_cores, "cfg2_single_thread": single, "cfg1_single_thread": cfg1,
+            "nproc": os.cpu_count(), "affinity_cpus": aff, "threads_used": threads,
+            "cpu_model": _cpu_model(),
+            "note": "threads_used = the CPU share of one GPU on the box (OMP_NUM_THREADS); nproc counts "
+                    "the whole host"}
+
+
+def host_inclusive(ctx, sch, n):
     """H2D + encode + D2H, then H2D + decode + D2H, from pinned host buffers,
     pipelined in chunks over two streams (the path starts and ends in host
     NIO buffers)."""
     import torch
     from oncrpc4j_amd.columns import aos_columns
+    rec_bytes = 32
     nat_h = torch.randint(-2**31, 2**31 - 1, (n, 8), dtype=torch.int32).pin_memory()
     xdr_h = torch.empty(n * rec_bytes, dtype=torch.uint8).pin_memory()
     back_h = torch.empty_like(nat_h).pin_memory()
@@ -183,232 +619,97 @@ def host_inclusive(ctx, sch, cols_fn, n, rec_bytes):
     dt = time.perf_counter() - t0
     ok = torch.equal(back_h, nat_h)
     ctx.set_stream(torch.cuda.current_stream())
-    return {"value": round(n * BYTES_PER_RECORD / dt / GIB, 3), "unit": "GiB/s",
+    return {"value": round(n * 128 / dt / GIB, 3), "unit": "GiB/s",
             "ms": round(dt * 1e3, 3), "records": n, "pcie_bytes": 4 * n * 32, "roundtrip_ok": ok,
             "method": "pinned host, 4 Mi-record chunks, 2 streams, H2D/encode/D2H then H2D/decode/D2H"}
 
 
-class Workload:
-    """One BASELINE config made concrete: device-resident native columns, the
-    XDR stream, decode targets, and one step = encode batch + decode batch."""
-
-    def __init__(self, cfg, n, framed, rank):
-        import torch
-        from oncrpc4j_amd import abi, engine
-        from oncrpc4j_amd.columns import aos_columns
-        self.cfg, self.n, self.framed = cfg, n, framed
-        I, SC, DY = abi.T_INT, abi.K_SCALAR, abi.K_DYNAMIC
-        g = torch.Generator(device="cuda").manual_seed(0x0DCAC4E5 + cfg + 1000 * rank)
-        dev = "cuda"
-        if cfg == 2:
-            self.fields = [(I, SC, 0)] * 8
-            rec = 36 if framed else 32
-            self.nat = torch.randint(-2**31, 2**31 - 1, (n, 8), dtype=torch.int32, device=dev, generator=g)
-            self.back = torch.empty_like(self.nat)
-            offs = [4 * k for k in range(8)]
-            self.cin = aos_columns(self.fields, self.nat.data_ptr(), 32, offs)
-            self.cout = aos_columns(self.fields, self.back.data_ptr(), 32, offs)
-            self.xlen = n * rec
-            self.native_bytes = n * 32
-            self.rec_offsets = None
-            self.kernels = ("k_stream_framed_enc/dec" if framed else "k_stream_bswap",
-                            abi.KERNEL_FIXED_ENCODE, abi.KERNEL_FIXED_DECODE)
-            self.desc = ("configs[1]: 64 Mi fixed-schema records of 8 x int32 (32 B), encode+decode "
-                         "round trip, array-of-structs native records" if not framed else
-                         "configs[1] record-marked variant (36 B XDR records)")
-        else:
-            if cfg == 3:   # 6 x int32 header (AoS) + opaque<> of 4096 B
-                self.fields = [(I, SC, 0)] * 6 + [(abi.T_OPAQUE, DY, 0)]
-                nh = 6
-                lens = torch.full((n,), 4096, dtype=torch.int64, device=dev)
-            else:          # int32 + string(8..256) + int32<0..16>
-                self.fields = [(I, SC, 0), (abi.T_STRING, DY, 0), (I, DY, 0)]
-                nh = 1
-                lens = torch.randint(8, 257, (n,), dtype=torch.int64, device=dev, generator=g)
-            self.hdr = torch.randint(-2**31, 2**31 - 1, (n, nh), dtype=torch.int32, device=dev, generator=g)
-            self.hdr_back = torch.empty_like(self.hdr)
-            self.dyn = []       # (values, offsets, values_back, offsets_back) per dynamic field
-            offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-            torch.cumsum(lens, 0, out=offs[1:])
-            total = int(offs[-1])
-            if cfg == 3:
-                vals = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
-            else:
-                vals = torch.randint(97, 123, (total,), dtype=torch.uint8, device=dev, generator=g)
-            self.dyn.append((vals, offs, torch.empty_like(vals), torch.empty_like(offs)))
-            if cfg == 4:
-                k = torch.randint(0, 17, (n,), dtype=torch.int64, device=dev, generator=g)
-                o2 = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-                torch.cumsum(k, 0, out=o2[1:])
-                v2 = torch.randint(-2**31, 2**31 - 1, (int(o2[-1]),), dtype=torch.int32, device=dev,
-                                   generator=g)
-                self.dyn.append((v2, o2, torch.empty_like(v2), torch.empty_like(o2)))
-            self.cin = self._cols(self.hdr, [(d[0], d[1]) for d in self.dyn], nh)
-            self.cout = self._cols(self.hdr_back, [(d[2], d[3]) for d in self.dyn], nh)
-            # XDR sizes: fixed part + per dynamic field 4 + payload (+pad)
-            size = torch.full((n,), 4 * nh + (4 if framed else 0), dtype=torch.int64, device=dev)
-            for (t, kd, _), d in zip([f for f in self.fields if f[1] == DY], self.dyn):
-                cnt = d[1][1:] - d[1][:-1]
-                size += 4 + (cnt + ((4 - (cnt & 3)) & 3) if t in (abi.T_OPAQUE, abi.T_STRING) else 4 * cnt)
-            self.xlen = int(size.sum())
-            self.rec_offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-            self.native_bytes = n * 4 * nh + sum(d[0].numel() * d[0].element_size() for d in self.dyn)
-            self.kernels = ("k_enc_place/k_dec_place", abi.KERNEL_VAR_ENCODE, abi.KERNEL_VAR_DECODE)
-            self.desc = ("configs[2]: 16 Mi NFS-WRITE-shaped records, 6 x int32 + opaque<4096>"
-                         if cfg == 3 else
-                         "configs[3]: 32 Mi records int32 + string(8..256) + int32<0..16>")
-        self.xdr = torch.empty(self.xlen, dtype=torch.uint8, device=dev)
-        self.sch = engine.Schema(self.fields)
-        # per-record algorithmic bytes: encode reads native + writes XDR, decode the reverse
-        self.bytes_per_step = 2 * (self.native_bytes + self.xlen)
-
-    def _cols(self, hdr, dyn, nh):
-        from oncrpc4j_amd import abi
-        arr = (abi.Column * len(self.fields))()
-        for k in range(nh):
-            arr[k].data = hdr.data_ptr() + 4 * k
-            arr[k].stride = 4 * nh
-        for j, (v, o) in enumerate(dyn):
-            arr[nh + j].data = v.data_ptr()
-            arr[nh + j].offsets = o.data_ptr()
-            arr[nh + j].cap = v.numel()
-        arr._keep = (hdr, dyn)
-        return arr
-
-    def step(self, ctx):
-        ctx.encode(self.sch, self.cin, self.n, self.xdr, self.xlen, rec_offsets=self.rec_offsets,
-                   framed=self.framed, async_=True)
-        ctx.decode(self.sch, self.xdr, self.xlen, self.n, self.cout, rec_offsets=self.rec_offsets,
-                   framed=self.framed, async_=True)
-
-    def clear_outputs(self):
-        """Zero the XDR stream and every decode target (tools/tune_*.py: each
-        kernel variant must round-trip on its own writes)."""
-        self.xdr.zero_()
-        if self.cfg == 2:
-            self.back.zero_()
-            return
-        self.hdr_back.zero_()
-        for _, _, vb, ob in self.dyn:
-            vb.zero_()
-            ob.zero_()
-
-    def check(self):
-        import torch
-        if self.cfg == 2:
-            assert torch.equal(self.back, self.nat), "decode(encode(x)) != x"
-            if not self.framed:
-                m = min(self.n, 1 << 20) * 8
-                assert torch.equal(self.xdr.view(-1, 4)[:m], self.nat.view(torch.uint8).view(-1, 4)[:m].flip(1))
-            return
-        assert torch.equal(self.hdr_back, self.hdr), "header columns differ"
-        for v, o, vb, ob in self.dyn:
-            assert torch.equal(ob, o), "offsets differ"
-            assert torch.equal(vb, v), "values differ"
-
-
-def main():
-    args = parse()
+# ---------------------------------------------------------------------------
+def run_rank(args):
     import torch
-    from oncrpc4j_amd import engine
+    R = Rank(args)
+    if args.test_codec:
+        import importlib
+        codec = importlib.import_module(args.test_codec)
+        ctx = None
 
-    world, rank, local = dist_setup(args)
-    n = args.records if args.records else {2: 64 << 20, 3: 16 << 20, 4: 32 << 20}[args.config]
-    wl = Workload(args.config, n, args.framed, rank)
-    ctx = engine.Context(local, timing=True)
-    ctx.set_stream(torch.cuda.current_stream())
+        def make(cfg, n, framed):
+            return codec.make_workload(cfg, n, framed, R.rank)
+    else:
+        from oncrpc4j_amd import engine
+        ctx = engine.Context(R.local, timing=True)
+        ctx.set_stream(torch.cuda.current_stream())
 
-    for _ in range(args.warmup):
-        wl.step(ctx)
-    torch.cuda.synchronize()
-    wl.check()   # correctness of the measured path, outside the timed region
-    ctx.reset_stats()
+        def make(cfg, n, framed):
+            return Workload(ctx, cfg, n, framed, shards=(R.rank,))
 
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        wl.step(ctx)
-    torch.cuda.synchronize()
-    barrier(world)
-    dt = max_over_ranks(time.perf_counter() - t0, world)
+    n = args.records if args.records else SIZES[args.config]
+    head, wl = measure(R, args, make, args.config, args.framed, n, args.steps, args.warmup, with_gather=True)
+    hinc = None
+    if R.rank == 0 and R.world == 1 and args.config == 2 and not args.framed and not args.no_host_inclusive \
+            and ctx is not None:
+        hinc = host_inclusive(ctx, wl.sch, min(n, 64 << 20))
+    del wl
+    if R.cuda:
+        torch.cuda.empty_cache()
 
-    # dominant kernel(s): per-launch HIP-event durations, same stream, same region
-    kname, kid_e, kid_d = wl.kernels
-    ne, ms_e = ctx.kernel_stats(kid_e)
-    nd, ms_d = ctx.kernel_stats(kid_d)
-    launches = ne + nd
-    avg_ms = (ms_e + ms_d) / max(launches, 1)
-    per_launch_bytes = wl.native_bytes + wl.xlen   # one side read, the other written
-    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    step_kernel_ms = {}
-    for kid, name in ((0, "fixed_encode"), (1, "fixed_decode"), (2, "var_size"), (3, "var_scan"),
-                      (4, "var_encode"), (5, "var_decode")):
-        c, ms = ctx.kernel_stats(kid)
-        if c:
-            step_kernel_ms[name] = round(ms / args.steps, 4)
-
-    total_records = n * world * args.steps
-    value = wl.bytes_per_step * world * args.steps / dt / GIB
-
-    gather = None
-    if world > 1:
-        import torch.distributed as dist
-        xlen = wl.xlen
-        full = torch.empty(world * xlen, dtype=torch.uint8, device="cuda")
-        dist.all_gather_into_tensor(full, wl.xdr)
-        torch.cuda.synchronize()
-        barrier(world)
-        t1 = time.perf_counter()
-        reps = 3
-        for _ in range(reps):
-            dist.all_gather_into_tensor(full, wl.xdr)
-        torch.cuda.synchronize()
-        barrier(world)
-        gdt = max_over_ranks((time.perf_counter() - t1) / reps, world)
-        ok = torch.equal(full[rank * xlen:(rank + 1) * xlen], wl.xdr)
-        gather = {"ms": round(gdt * 1e3, 3), "bytes_in_per_gpu": (world - 1) * xlen,
-                  "GBps_in_per_gpu": round((world - 1) * xlen / gdt / 1e9, 2),
-                  "stream_bytes": world * xlen, "own_shard_ok": bool(ok),
-                  "collective": "RCCL all_gather_into_tensor (torch.distributed nccl)"}
-        del full
+    extra = []
+    if args.extra:
+        for cfg, framed in ((2, True), (3, False), (4, False)):
+            if (cfg, framed) == (args.config, bool(args.framed)):
+                continue
+            e, w = measure(R, args, make, cfg, framed, SIZES[cfg], args.extra_steps, 2,
+                           with_gather=(cfg == 4))
+            del w
+            if R.cuda:
+                torch.cuda.empty_cache()
+            extra.append(e)
 
     cpu = None
-    hinc = None
-    if rank == 0 and world == 1 and args.config == 2 and not args.framed:
-        if not args.no_host_inclusive:
-            hinc = host_inclusive(ctx, wl.sch, None, min(n, 64 << 20), 32)
-        if args.cpu_seconds > 0:
-            cpu = cpu_baseline(args.cpu_seconds)
+    if R.rank == 0 and R.world == 1 and args.cpu_seconds > 0 and not args.test_codec:
+        cpu = cpu_baseline(args.cpu_seconds)
 
-    if rank == 0:
+    if R.rank == 0:
         line = {
             "metric": "XDR encode+decode GiB/s (device-resident)",
-            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "value": head["GiB_s"], "unit": "GiB/s", "n_gpus": R.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
             "data": "synthetic (seeded uniform int32 / random bytes / [a-z] strings)",
-            "config": {"workload": wl.desc, "records_per_gpu": n, "xdr_bytes_per_gpu": wl.xlen,
-                       "native_bytes_per_gpu": wl.native_bytes, "bytes_per_step_per_gpu": wl.bytes_per_step,
-                       "framed": bool(args.framed),
-                       "parallelism": f"records sharded {world} ways" if world > 1 else "single GPU"},
-            "mrecords_per_s": round(total_records / dt / 1e6, 2),
-            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
-                         "traffic": load_traffic(kname, n),
-                         "launches": launches, "avg_launch_ms": round(avg_ms, 4),
-                         "bytes_per_launch": per_launch_bytes},
-            "kernel_ms_per_step": step_kernel_ms,
+            "config": {"workload": head["workload"], "records_per_gpu": head["records_per_gpu"],
+                       "xdr_bytes_per_gpu": head["xdr_bytes_per_gpu"],
+                       "native_bytes_per_gpu": head["native_bytes_per_gpu"],
+                       "bytes_per_step_per_gpu": head["bytes_per_step_per_gpu"],
+                       "framed": head["framed"],
+                       "parallelism": f"records sharded {R.world} ways, one process per GPU"
+                       if R.world > 1 else "single GPU"},
+            "mrecords_per_s": head["Mrec_s"],
+            "roofline": head["roofline"],
+            "kernel_ms_per_step": head["kernel_ms_per_step"],
+            "encode_only": head["encode_only"],
+            "decode_only": head["decode_only"],
+            "gather": head["gather"],
             "cpu_baseline": cpu,
             "host_inclusive": hinc,
-            "gather": gather,
+            "extra_configs": extra,
         }
         print(json.dumps(line), flush=True)
-    ctx.close()
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    if ctx is not None:
+        ctx.close()
+    R.close()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            sys.exit(launch(args, argv))
+    elif int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    run_rank(args)
 
 
 if __name__ == "__main__":

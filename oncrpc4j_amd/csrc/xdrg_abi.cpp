@@ -218,6 +218,21 @@ static int inval(xdrg_ctx *c, const char *what) {
         if (e_ != hipSuccess) return hip_fail(c, e_, #x);  \
     } while (0)
 
+// Every entry point that selects a device puts the caller thread's current
+// device back on every return path: a JVM or torch caller driving another
+// GPU must not find its device switched under it.
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
 static hipEvent_t ev_get(xdrg_ctx *c) {
     if (!c->pool.empty()) {
         hipEvent_t e = c->pool.back();
@@ -287,6 +302,7 @@ extern "C" int xdrg_ctx_create(int device, uint32_t flags, xdrg_ctx **out) {
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return XDRG_E_HIP;
+    DeviceGuard dg;
     if (hipSetDevice(device) != hipSuccess) return XDRG_E_HIP;
     xdrg_ctx *c = new (std::nothrow) xdrg_ctx();
     if (!c) return XDRG_E_NOMEM;
@@ -304,6 +320,7 @@ extern "C" int xdrg_ctx_create(int device, uint32_t flags, xdrg_ctx **out) {
 
 extern "C" int xdrg_ctx_destroy(xdrg_ctx *c) {
     if (!c) return XDRG_OK;
+    DeviceGuard dg;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     while (!c->pending.empty()) resolve_one(c);
@@ -324,6 +341,7 @@ extern "C" int xdrg_ctx_set_stream(xdrg_ctx *c, void *stream) {
 
 extern "C" int xdrg_ctx_kernel_stats(xdrg_ctx *c, int kernel, uint64_t *launches, double *total_ms) {
     if (!c || kernel < 0 || kernel >= XDRG_KERNEL_COUNT) return XDRG_E_INVAL;
+    DeviceGuard dg;
     (void)hipSetDevice(c->device);
     while (!c->pending.empty()) resolve_one(c);
     if (launches) *launches = c->launches[kernel];
@@ -333,6 +351,7 @@ extern "C" int xdrg_ctx_kernel_stats(xdrg_ctx *c, int kernel, uint64_t *launches
 
 extern "C" int xdrg_ctx_reset_stats(xdrg_ctx *c) {
     if (!c) return XDRG_E_INVAL;
+    DeviceGuard dg;
     (void)hipSetDevice(c->device);
     while (!c->pending.empty()) resolve_one(c);
     for (int k = 0; k < XDRG_KERNEL_COUNT; ++k) { c->launches[k] = 0; c->ms[k] = 0; }
@@ -516,6 +535,7 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
                        uint8_t *out, uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags,
                        uint64_t *out_len, uint32_t byref, uint64_t *ref_pos) {
     if (!c || !s) return XDRG_E_INVAL;
+    DeviceGuard dg;
     HIPCHK(c, hipSetDevice(c->device));
     const bool framed = flags & XDRG_FRAME_RM;
     const bool async = flags & XDRG_ASYNC;
@@ -691,6 +711,7 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
                        const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
                        uint64_t *first_bad, int *err, uint32_t byref, uint64_t *ref_pos) {
     if (!c || !s) return XDRG_E_INVAL;
+    DeviceGuard dg;
     HIPCHK(c, hipSetDevice(c->device));
     const bool framed = flags & XDRG_FRAME_RM;
     const bool async = flags & XDRG_ASYNC;
@@ -853,6 +874,7 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
     if (!c || !msg_offsets || !n_msgs) return XDRG_E_INVAL;
     if (len && !in) return inval(c, "stream is NULL");
     if (len >= (1ull << 34)) return inval(c, "stream longer than 16 GiB");
+    DeviceGuard dg;
     HIPCHK(c, hipSetDevice(c->device));
     *n_msgs = 0;
     if (consumed) *consumed = 0;
@@ -976,6 +998,7 @@ extern "C" int xdrg_encode_batch_multi(xdrg_ctx *const *ctxs, uint32_t nctx, con
                                        uint32_t flags, uint64_t *out_len) {
     int rc = multi_args(ctxs, nctx, s, counts, flags);
     if (rc) return rc;
+    DeviceGuard dg;
     if (!cols || !out) return inval(ctxs[0], "columns / outputs are NULL");
     const bool framed = flags & XDRG_FRAME_RM;
     // 1. shard sizes (all devices in flight, then one sync each)
@@ -1011,14 +1034,31 @@ extern "C" int xdrg_encode_batch_multi(xdrg_ctx *const *ctxs, uint32_t nctx, con
         rc = xdrg_encode_batch(c, s, cols[i], counts[i], out[i] + base[i], out_cap - base[i], ro,
                                (framed ? XDRG_FRAME_RM : 0) | XDRG_ASYNC, nullptr);
         if (rc) return rc;
-        if (ro) {
-            if (counts[i] == 0) HIPCHK(c, (hipError_t)launch_store_u64(ro, 0, c->stream));
-            HIPCHK(c, (hipError_t)launch_add_u64(ro, counts[i] + 1, base[i], c->stream));
-        }
     }
     for (uint32_t i = 0; i < nctx; ++i) {
         HIPCHK(ctxs[i], hipSetDevice(ctxs[i]->device));
         HIPCHK(ctxs[i], hipStreamSynchronize(ctxs[i]->stream));
+    }
+    // Rebase the shard-relative record offsets.  Shards sharing one offsets
+    // array both wrote entry first[i+1] (shard i its size, shard i+1 its 0),
+    // so that entry is stored, never read-modified: shard i stores base[i] at
+    // first[i] and base[i+1] at first[i+1] (the same value its neighbour
+    // stores) and adds base[i] only to its interior entries, which no other
+    // shard touches.  Every encode above has finished before these run.
+    if (rec_offsets) {
+        for (uint32_t i = 0; i < nctx; ++i) {
+            if (!rec_offsets[i]) continue;
+            xdrg_ctx *c = ctxs[i];
+            uint64_t *ro = rec_offsets[i] + first[i];
+            HIPCHK(c, hipSetDevice(c->device));
+            HIPCHK(c, (hipError_t)launch_store_u64(ro, base[i], c->stream));
+            HIPCHK(c, (hipError_t)launch_store_u64(ro + counts[i], base[i + 1], c->stream));
+            if (counts[i] > 1) HIPCHK(c, (hipError_t)launch_add_u64(ro + 1, counts[i] - 1, base[i], c->stream));
+        }
+        for (uint32_t i = 0; i < nctx; ++i) {
+            HIPCHK(ctxs[i], hipSetDevice(ctxs[i]->device));
+            HIPCHK(ctxs[i], hipStreamSynchronize(ctxs[i]->stream));
+        }
     }
     if (nctx == 1) return XDRG_OK;
     // 3. full-mesh all-gather: context i pulls every peer's shard (and offsets)
@@ -1059,6 +1099,7 @@ extern "C" int xdrg_decode_batch_multi(xdrg_ctx *const *ctxs, uint32_t nctx, con
                                        xdrg_column *const *cols, uint32_t flags, uint64_t *first_bad, int *err) {
     int rc = multi_args(ctxs, nctx, s, counts, flags);
     if (rc) return rc;
+    DeviceGuard dg;
     if (!cols || !in) return inval(ctxs[0], "columns / inputs are NULL");
     const bool framed = flags & XDRG_FRAME_RM;
     const uint64_t stride = s->fixed_size + (framed ? 4 : 0);

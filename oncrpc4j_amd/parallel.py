@@ -4,15 +4,20 @@ Records are independent (no cross-record state in org.dcache.oncrpc4j.xdr.Xdr;
 an XdrAble encodes into the stream in order), so a batch of N
 records shards into contiguous record ranges, rank r owning
 [r*N/G, (r+1)*N/G).  Encode and decode need no collective.  Reassembling
-one contiguous XDR stream (BASELINE configs[4]) is the only exchange:
+one contiguous XDR stream (BASELINE configs[4]) is the only exchange, and it
+moves exactly the shard bytes:
 
-* fixed-size records: every shard has the same byte count -> one rank-ordered
-  all-gather (RCCL `all_gather_into_tensor` over xGMI) is exactly the
-  single-GPU stream;
-* variable-size records: all-gather of the per-rank byte counts, then an
-  all-gather of shards padded to the largest, compacted in rank order (RCCL
-  has no all-gather-v).  Record offsets are rebased by the exclusive prefix of
-  the shard sizes.
+* the shard byte counts are all-gathered (G x u64) and prefix-summed: rank r's
+  shard lands at sum(sizes[:r]);
+* equal sizes (fixed-size records): one rank-ordered all-gather straight into
+  the output (RCCL `all_gather_into_tensor` over xGMI) is the single-GPU
+  stream;
+* unequal sizes (variable-size records): RCCL has no all-gather-v, so every
+  rank sends its shard to every peer and receives each peer's shard into its
+  exact slice, as one grouped batch of send/recv (`batch_isend_irecv`, which
+  the nccl backend issues inside one ncclGroupStart/End: the G-1 transfers
+  run concurrently over the point-to-point xGMI links, no padding moves).
+  Record offsets are rebased by the shard's prefix and exchanged the same way.
 
 The collectives run on the process group's backend: nccl (RCCL) on MI355X,
 gloo in the CPU tests.  The per-shard codec is passed in (the HIP engine in
@@ -33,55 +38,79 @@ def _coll_device(group=None):
         else torch.device("cpu")
 
 
-def _all_gather_sizes(x, group=None, dev=None):
+def all_gather_ints(x, group=None):
+    """All-gather one Python int per rank -> list in rank order."""
     world = dist.get_world_size(group)
-    dev = dev or _coll_device(group)
-    mine = torch.tensor([x], dtype=torch.int64, device=dev)
-    out = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(out, mine, group=group)
-    return [int(t.item()) for t in out]
+    dev = _coll_device(group)
+    mine = torch.tensor([int(x)], dtype=torch.int64, device=dev)
+    out = torch.zeros(world, dtype=torch.int64, device=dev)
+    if dev.type == "cuda":
+        dist.all_gather_into_tensor(out, mine, group=group)
+    else:
+        parts = list(out.split(1))
+        dist.all_gather(parts, mine, group=group)
+        out = torch.cat(parts)
+    return [int(v) for v in out.tolist()]
 
 
-def _all_gather_padded(local, size, group=None):
+def exchange_exact(local, sizes, out, group=None):
+    """Place every rank's `local` (sizes[r] elements) at its prefix offset of
+    `out` (sum(sizes) elements, same dtype), moving exactly the shard bytes."""
     world = dist.get_world_size(group)
-    if local.numel() < size:
-        pad = torch.zeros(size - local.numel(), dtype=local.dtype, device=local.device)
-        local = torch.cat([local, pad])
-    parts = [torch.empty(size, dtype=local.dtype, device=local.device) for _ in range(world)]
-    if local.is_cuda and hasattr(dist, "all_gather_into_tensor"):
-        flat = torch.empty(world * size, dtype=local.dtype, device=local.device)
-        dist.all_gather_into_tensor(flat, local, group=group)
-        return list(flat.view(world, size))
-    dist.all_gather(parts, local, group=group)
-    return parts
+    rank = dist.get_rank(group)
+    base = [0]
+    for s in sizes:
+        base.append(base[-1] + s)
+    assert local.numel() == sizes[rank] and out.numel() == base[-1], "shard sizes disagree"
+    if world == 1:
+        if out.data_ptr() != local.data_ptr():
+            out.copy_(local)
+        return out
+    if len(set(sizes)) == 1 and out.is_cuda:
+        if sizes[0]:
+            dist.all_gather_into_tensor(out, local, group=group)
+        return out
+    if sizes[rank]:
+        out[base[rank]:base[rank + 1]].copy_(local)
+    ops = []
+    for peer in range(world):
+        if peer == rank:
+            continue
+        gpeer = dist.get_global_rank(group, peer) if group is not None else peer
+        if sizes[rank]:
+            ops.append(dist.P2POp(dist.isend, local, gpeer, group))
+        if sizes[peer]:
+            ops.append(dist.P2POp(dist.irecv, out[base[peer]:base[peer + 1]], gpeer, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return out
 
 
-def gather_stream(local_xdr, local_offsets=None, group=None):
+def gather_stream(local_xdr, local_offsets=None, group=None, out=None, out_offsets=None):
     """Reassemble the rank-ordered concatenation of every rank's XDR shard.
 
     local_xdr: uint8 tensor (this rank's encoded records, exactly its bytes).
     local_offsets: optional int64 tensor [m+1] of record offsets inside the
-    shard.  Returns (stream, offsets) with offsets rebased to the full stream
-    (or None)."""
-    sizes = _all_gather_sizes(local_xdr.numel(), group)
-    big = max(sizes)
-    if big == 0:
-        stream = local_xdr.new_empty(0)
-    elif all(s == big for s in sizes):
-        stream = torch.cat(_all_gather_padded(local_xdr, big, group)) if len(sizes) > 1 else local_xdr
-    else:
-        parts = _all_gather_padded(local_xdr, big, group)
-        stream = torch.cat([p[:s] for p, s in zip(parts, sizes)])
+    shard.  out / out_offsets: optional preallocated results (sizes must
+    match).  Returns (stream, offsets) with offsets rebased to the full
+    stream (or None)."""
+    sizes = all_gather_ints(local_xdr.numel(), group)
+    total = sum(sizes)
+    if out is None:
+        out = local_xdr.new_empty(total)
+    stream = exchange_exact(local_xdr, sizes, out[:total], group)
     offs = None
     if local_offsets is not None:
-        counts = _all_gather_sizes(local_offsets.numel() - 1, group)
+        counts = all_gather_ints(local_offsets.numel() - 1, group)
         rank = dist.get_rank(group)
-        base = sum(sizes[:rank])
-        mine = (local_offsets[:-1] + base).to(torch.int64)
-        gathered = _all_gather_padded(mine, max(max(counts), 1), group)
-        pieces = [g[:c] for g, c in zip(gathered, counts)]
-        end = torch.tensor([sum(sizes)], dtype=torch.int64, device=local_offsets.device)
-        offs = torch.cat(pieces + [end])
+        n = sum(counts)
+        if out_offsets is None:
+            out_offsets = torch.empty(n + 1, dtype=torch.int64, device=local_offsets.device)
+        mine = local_offsets[:-1].to(torch.int64) + sum(sizes[:rank])
+        exchange_exact(mine, counts, out_offsets[:n], group)
+        out_offsets[n] = total
+        offs = out_offsets[:n + 1]
     return stream, offs
 
 
@@ -106,9 +135,24 @@ def decode_sharded(decode_shard, n, group=None):
     rank = dist.get_rank(group)
     lo, hi = shard_range(n, world, rank)
     status, first_bad, err = decode_shard(lo, hi)
-    key = first_bad * 16 + (err if status else 0) if status else n * 16
-    keys = _all_gather_sizes(key, group)
-    best = min(keys)
+    key = first_bad * 16 + err if status else n * 16
+    best = min(all_gather_ints(key, group))
     if best >= n * 16:
         return 0, n, 0
     return best % 16, best // 16, best % 16
+
+
+def stream_hash(t, chunk=1 << 24):
+    """Position-weighted checksum of a byte tensor (sum of 32-bit words times
+    their 1-based index, wrapping int64), chunked so the index vector stays
+    small; equal streams give equal values on every rank."""
+    n = t.numel()
+    h = torch.zeros((), dtype=torch.int64, device=t.device)
+    words = t[:n - n % 4].view(torch.int32)
+    w = torch.arange(1, chunk + 1, dtype=torch.int64, device=t.device)
+    for lo in range(0, words.numel(), chunk):
+        c = words[lo:lo + chunk].to(torch.int64)
+        h += (c * (w[:c.numel()] + lo)).sum()
+    for i in range(n - n % 4, n):
+        h += int(t[i]) * (i + 1)
+    return int(h)

@@ -126,6 +126,51 @@ def test_encode_multi_shared_output(ctxs):
     assert np.array_equal(ro.cpu().numpy().view(np.uint64), want_offs)
 
 
+@pytest.mark.parametrize("name", ["cfg4_int_string_intvec", "cfg2_8xint"])
+def test_encode_multi_shared_output_own_streams(name):
+    """Shared output and shared offsets array, every context on its own
+    stream: the shards' boundary offsets entries are written by two
+    contexts, so they must be stores of one value, never read-modify-writes."""
+    fields = SCHEMAS[name]
+    k = 4
+    streams = [torch.cuda.Stream() for _ in range(k)]
+    cs = [engine.Context(0) for _ in range(k)]
+    try:
+        for c, s in zip(cs, streams):
+            c.set_stream(s)
+        for rep, n in enumerate((4001, 20011, 7)):
+            hb = random_batch(fields, n, seed=100 + rep, dyn_len=(0, 60))
+            rc, want, want_offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total())
+            parts = _shards(n, k)
+            dbs = [DeviceBatch.from_host(hb.slice(lo, hi)) for lo, hi in parts]
+            out = torch.zeros(len(want) + 16, dtype=torch.uint8, device="cuda")
+            ro = torch.full((n + 1,), -1, dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            ln = engine.encode_multi(cs, engine.Schema(fields), [db.columns() for db in dbs],
+                                     [hi - lo for lo, hi in parts], [out] * k, out.numel(), rec_offsets=[ro] * k)
+            torch.cuda.synchronize()
+            assert ln == len(want)
+            assert out[:ln].cpu().numpy().tobytes() == want
+            assert np.array_equal(ro.cpu().numpy().view(np.uint64), want_offs), f"n={n}"
+    finally:
+        for c in cs:
+            c.close()
+
+
+def test_ctx_keeps_callers_device():
+    """Every entry point restores the caller thread's current device."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two devices to observe a device switch")
+    torch.cuda.set_device(1)
+    c = engine.Context(0)
+    assert torch.cuda.current_device() == 1
+    c.reset_stats()
+    assert torch.cuda.current_device() == 1
+    c.close()
+    assert torch.cuda.current_device() == 1
+    torch.cuda.set_device(0)
+
+
 def test_encode_multi_capacity(ctxs):
     fields = SCHEMAS["cfg2_8xint"]
     hb = random_batch(fields, 100, seed=1)

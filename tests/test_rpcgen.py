@@ -1,8 +1,10 @@
 """rpcgen .x -> engine field tapes (oncrpc4j_amd/rpcgen.py).
 
-Fixtures: the reference's rpcgen test inputs (oncrpc4j-rpcgen/src/test/xdr/
-Calculator.x, BlobStore.x — data files the reference's own tests hold) and
-tests/golden/rpcgen/batch_types.x.  The tape order is checked against an
+Fixtures: builder-written .x inputs with the constructs of the reference's
+rpcgen test inputs (oncrpc4j-rpcgen/src/test/xdr/Calculator.x, BlobStore.x):
+arith_service.x (constants in every literal form, a struct of hypers,
+procedures with two anonymous hyper arguments) and kv_store.x (bounded opaque
+key, bool union with a void arm), plus tests/golden/rpcgen/batch_types.x.  The tape order is checked against an
 independent per-declaration xdrlib packer that walks the parsed structs the
 way jrpcgen's generated xdrEncode does (jrpcgen.java:758-913: one call per
 declaration, nested structs through their own xdrEncode)."""
@@ -30,35 +32,34 @@ def spec(name):
     return rpcgen.parse_file(os.path.join(HERE, name))
 
 
-def test_calculator_consts_and_tapes():
-    s = spec("Calculator.x")
-    assert s.value("PLAIN_ZERO") == 0 and s.value("HEX_ZERO") == 0
-    assert s.value("SMALL_CONST") == 0xFF00
-    assert s.value("LARGE_CONST") == 0xFFF000000000
-    assert s.value("HUGE_CONST") == 0xFFF000000000000000000
-    assert s.value("UNSIGNED_LONG_HEX_CONST") == s.value("UNSIGNED_LONG_OCT_CONST") == \
-        s.value("UNSIGNED_LONG_DEC_CONST") == 2**64 - 1
-    assert s.value("UNSIGNED_INT_HEX_CONST") == s.value("UNSIGNED_INT_OCT_CONST") == 2**32 - 1
-    assert s.fields("CalculationResult") == [(H, SC, 0), (UH, SC, 0), (UH, SC, 0)]
+def test_arith_consts_and_tapes():
+    s = spec("arith_service.x")
+    assert s.value("ZERO_DEC") == 0 and s.value("ZERO_HEX") == 0
+    assert s.value("MASK_16") == 0xAB00
+    assert s.value("WIDE_48") == 0xABC000000000
+    assert s.value("BEYOND_64") == 0xABC000000000000000000
+    assert s.value("U64_MAX_HEX") == s.value("U64_MAX_OCT") == s.value("U64_MAX_DEC") == 2**64 - 1
+    assert s.value("U32_MAX_HEX") == s.value("U32_MAX_OCT") == s.value("U32_MAX_DEC") == 2**32 - 1
+    assert s.fields("arith_reply") == [(H, SC, 0), (UH, SC, 0), (UH, SC, 0)]
     procs = s.procedures()
-    assert {k: p.name for k, p in procs.items()} == {(117, 1, 1): "add", (117, 1, 2): "addSimple"}
-    assert s.args_fields(117, 1, 1) == [(H, SC, 0), (H, SC, 0)]   # add(hyper, hyper)
-    assert s.result_fields(117, 1, 1) == s.fields("CalculationResult")
-    assert s.result_fields(117, 1, 2) == [(H, SC, 0)]
+    assert {k: p.name for k, p in procs.items()} == {(400117, 1, 1): "SUM", (400117, 1, 2): "SUM_PLAIN"}
+    assert s.args_fields(400117, 1, 1) == [(H, SC, 0), (H, SC, 0)]   # SUM(hyper, hyper)
+    assert s.result_fields(400117, 1, 1) == s.fields("arith_reply")
+    assert s.result_fields(400117, 1, 2) == [(H, SC, 0)]
 
 
-def test_blobstore_union_is_not_one_tape():
-    s = spec("BlobStore.x")
-    assert s.fields("Key") == [(O, DY, 0)]
-    assert s.args_fields(118, 1, 2) == [(O, DY, 0)]                 # get(Key)
-    with pytest.raises(rpcgen.NotBatchable, match="union Value"):
-        s.fields("Value")
+def test_kv_union_is_not_one_tape():
+    s = spec("kv_store.x")
+    assert s.fields("kv_key") == [(O, DY, 0)]
+    assert s.args_fields(400118, 1, 2) == [(O, DY, 0)]              # FETCH(kv_key)
+    with pytest.raises(rpcgen.NotBatchable, match="union kv_value"):
+        s.fields("kv_value")
     with pytest.raises(rpcgen.NotBatchable):
-        s.args_fields(118, 1, 1)                                    # put(Key, Value)
-    u = s.types["Value"]
-    assert u.disc.name == "notNull" and u.disc.type == "bool"
+        s.args_fields(400118, 1, 1)                                 # STORE(kv_key, kv_value)
+    u = s.types["kv_value"]
+    assert u.disc.name == "present" and u.disc.type == "bool"
     assert [(v, d.kind, d.type) for v, d in u.arms] == [(["TRUE"], "dynamic", "opaque"), (["FALSE"], "void", "void")]
-    assert s.result_fields(118, 1, 1) == []                          # void put
+    assert s.result_fields(400118, 1, 1) == []                       # void STORE
 
 
 FATTR = [(E, SC, 0), (U, SC, 0), (U, SC, 0), (H, SC, 0), (UH, SC, 0), (U, SC, 0), (U, SC, 0),
@@ -162,10 +163,10 @@ def test_tape_matches_declaration_order(type_name):
 
 # ---- GPU: a call batch decoded with the tape of its procedure ----------------------
 @pytest.mark.gpu
-def test_calculator_calls_decode_with_generated_tape(gpu_ctx):
+def test_arith_calls_decode_with_generated_tape(gpu_ctx):
     import torch
     from oncrpc4j_amd import rpc
-    s = spec("Calculator.x")
+    s = spec("arith_service.x")
     rng = np.random.default_rng(117)
     n = 4000
     a = rng.integers(-2**63, 2**63, n, dtype=np.int64)
@@ -173,7 +174,7 @@ def test_calculator_calls_decode_with_generated_tape(gpu_ctx):
     stream, offs = b"", [0]
     for i in range(n):
         p = xdrlib.Packer()
-        for v in (i, rpc.CALL, rpc.RPCVERS, 117, 1, 1, rpc.AUTH_NONE):
+        for v in (i, rpc.CALL, rpc.RPCVERS, 400117, 1, 1, rpc.AUTH_NONE):
             p.pack_int(v)
         p.pack_opaque(b"")
         p.pack_int(rpc.AUTH_NONE)
@@ -189,7 +190,7 @@ def test_calculator_calls_decode_with_generated_tape(gpu_ctx):
     hdr, st = dec.decode_headers(dev, len(stream), n, ro)
     assert st == (0, n, 0)
     (key, idx), = rpc.CallDecoder.group_by_procedure(hdr).items()
-    assert key == (117, 1, 1, rpc.AUTH_NONE) and idx.numel() == n
+    assert key == (400117, 1, 1, rpc.AUTH_NONE) and idx.numel() == n
     args = s.args_fields(*key[:3])
     batch, st = dec.decode(rpc.AUTH_NONE, args, dev, len(stream), n, ro, {7: 16, 9: 16})
     assert st == (0, n, 0)
@@ -296,22 +297,23 @@ def test_conditional_tape_shapes():
         s.tape("optional_next")
 
 
-def test_blobstore_put_tape():
-    """The reference's own rpcgen input: put(Key, Value) with a bool union."""
-    s = spec("BlobStore.x")
-    f, c = s.args_tape(118, 1, 1)             # put
+def test_kv_store_tape():
+    """STORE(kv_key, kv_value): a bool union argument (the shape of the
+    reference's BlobStore.x put(Key, Value))."""
+    s = spec("kv_store.x")
+    f, c = s.args_tape(400118, 1, 1)          # STORE
     assert f == [(O, DY, 0), (B, SC, 0), (O, DY, 0)] and c == [(2, 1, False, [1])]
 
 
 @pytest.mark.gpu
-def test_gpu_blobstore_put_args(gpu_ctx):
-    """BlobStore put(Key, Value) argument batches through the engine with the
+def test_gpu_kv_store_args(gpu_ctx):
+    """STORE(kv_key, kv_value) argument batches through the engine with the
     conditional tape, checked against xdrlib packing of the generated order."""
     import torch
     from oncrpc4j_amd import engine
     from oncrpc4j_amd.columns import DeviceBatch, HostBatch
-    s = spec("BlobStore.x")
-    fields, conds = s.args_tape(118, 1, 1)
+    s = spec("kv_store.x")
+    fields, conds = s.args_tape(400118, 1, 1)
     n = 5000
     hb = _cond_batch(fields, conds, n, seed=118)
     want = b""
@@ -319,8 +321,8 @@ def test_gpu_blobstore_put_args(gpu_ctx):
     for i in range(n):
         p = xdrlib.Packer()
         vals = _record_values(fields, hb, i)
-        _walk(s, "Key", vals, True, p)
-        _walk(s, "Value", vals, True, p)
+        _walk(s, "kv_key", vals, True, p)
+        _walk(s, "kv_value", vals, True, p)
         want += p.get_buffer()
         offs.append(len(want))
     sch = engine.Schema(fields, conds)
