@@ -290,6 +290,18 @@ class Workload:
         self.encode()
         self.decode()
 
+    def clear_outputs(self):
+        """Zero the XDR stream and every decode target (tools/sweep_rec.py:
+        each kernel variant must round-trip on its own writes)."""
+        self.xdr.zero_()
+        if self.cfg == 2:
+            self.back.zero_()
+            return
+        self.hdr_back.zero_()
+        for _, _, vb, ob in self.dyn:
+            vb.zero_()
+            ob.zero_()
+
     def xdr_view(self):
         return self.xdr
 

@@ -128,6 +128,55 @@ private:
     int device_ = 0;
 };
 
+// ---- host staging buffer (Grizzly Buffer + GrizzlyMemoryManager) ------------
+// The socket-side host buffer an encoded batch lands in, with the reference's
+// growth semantics for callers that do not presize:
+//   Xdr.ensureCapacity (Xdr.java:1020-1026): when fewer than `size` bytes
+//     remain, newCapacity = max(capacity * 3 / 2 + 1, capacity + size);
+//   GrizzlyMemoryManager.reallocate (GrizzlyMemoryManager.java:46-53): a
+//     composite buffer appends a chunk of (newCapacity - capacity) bytes, any
+//     other buffer is reallocated with a copy.
+// position/limit/flip/clear/hasRemaining as the Grizzly Buffer the Xdr wraps.
+class XdrBuffer {
+public:
+    static constexpr size_t kInitialSize = 1024;   // Xdr.INITIAL_XDR_SIZE (Xdr.java:49)
+    explicit XdrBuffer(size_t capacity = kInitialSize, bool composite = false);
+
+    size_t capacity() const { return cap_; }
+    size_t position() const { return pos_; }
+    size_t limit() const { return lim_; }
+    size_t remaining() const { return lim_ - pos_; }
+    bool hasRemaining() const { return pos_ < lim_; }
+    bool isComposite() const { return composite_; }
+    size_t chunks() const { return chunks_.size(); }   // composite parts (1 when contiguous)
+    void clear() { pos_ = 0; lim_ = cap_; }            // beginEncoding (Xdr.java:137-140)
+    void flip() { lim_ = pos_; pos_ = 0; }             // endEncoding (Xdr.java:143-146)
+    void rewind() { pos_ = 0; }                        // begin/endDecoding (Xdr.java:122-134)
+
+    // Xdr.ensureCapacity: grow (per the policy above) so that `size` more bytes fit.
+    void ensureCapacity(size_t size);
+    // GrizzlyMemoryManager.reallocate to exactly newCapacity (>= capacity()).
+    void reallocate(size_t newCapacity);
+    // Append bytes at the position (growing as ensureCapacity does).
+    void put(const uint8_t *src, size_t len);
+    // Bytes [from, from + len) into dst (across composite chunks).
+    void get(size_t from, uint8_t *dst, size_t len) const;
+    // Copy of [position, limit) (Xdr.getBytes, Xdr.java:998-1006).
+    std::vector<uint8_t> bytes() const;
+
+private:
+    bool composite_;
+    size_t cap_ = 0, pos_ = 0, lim_ = 0;
+    std::vector<std::vector<uint8_t>> chunks_;
+};
+
+// A read-only view of bytes owned elsewhere (Xdr.asBuffer, Xdr.java:558-575:
+// the buffer that backs the message, no copy).
+struct BufferView {
+    const uint8_t *data = nullptr;
+    size_t size = 0;
+};
+
 // ---- batching encoder -------------------------------------------------------
 // One record = the calls between beginEncoding() and endEncoding(), as
 // RpcCall.acceptedReply drives one Xdr per message (RpcCall.java:323-343).
@@ -169,8 +218,23 @@ public:
     const std::vector<xdrg_field> &schema() const;
     // Encode every recorded record on the GPU into one XDR stream (record i
     // at offsets[i]); `framed` prepends one RFC 1831 record mark per record
-    // (GrizzlyRpcTransport.java:103-110).  Clears the batch.
+    // (GrizzlyRpcTransport.java:103-110).  Clears the batch.  The stream
+    // lands in this encoder's host XdrBuffer, which starts at
+    // XdrBuffer::kInitialSize and grows by the reference's policy when the
+    // engine reports the batch does not fit (XDRG_E_CAPACITY + needed size).
     std::vector<uint8_t> flush(bool framed = false, std::vector<uint64_t> *offsets = nullptr);
+
+    // Per-message access to the last flushed batch, the two ways the
+    // reference hands an encoded message on (RpcGssCall.java:111-131,
+    // GrizzlyRpcTransport.java:100): getBytes copies message i
+    // (Xdr.getBytes, Xdr.java:998-1006) and throws std::logic_error
+    // ("getBytes called while buffer in use", the reference's
+    // IllegalStateException) between beginEncoding() and endEncoding();
+    // asBuffer returns message i as a view of the stream (Xdr.asBuffer).
+    std::vector<uint8_t> getBytes(uint64_t i) const;
+    BufferView asBuffer(uint64_t i) const;
+    uint64_t messages() const;            // messages in the last flushed batch
+    const XdrBuffer &buffer() const;      // the stream's host buffer (growth history)
 
 private:
     struct Impl;
@@ -196,6 +260,9 @@ public:
 
     void beginDecoding() override;   // advances to the next record
     void endDecoding() override;
+    // Xdr.hasMoreData (Xdr.java:152-154): bytes of the current record not yet
+    // decoded (false before the first beginDecoding and past the last field).
+    bool hasMoreData() const;
     int32_t xdrDecodeInt() override;
     std::vector<int32_t> xdrDecodeIntVector() override;
     std::vector<int32_t> xdrDecodeIntFixedVector(int32_t length) override;

@@ -134,6 +134,9 @@ struct BatchXdrEncoder::Impl {
     bool have_tape = false, in_record = false;
     size_t field = 0;
     uint64_t n = 0;
+    XdrBuffer buf;                      // host staging of the flushed stream (grows, never shrinks)
+    std::vector<uint8_t> stream;        // the last flushed batch ...
+    std::vector<uint64_t> offs;         // ... and its message offsets
 
     Column &next(uint32_t t, uint32_t k, uint32_t c = 0) {
         if (!in_record) throw std::logic_error("xdrEncode* outside beginEncoding()/endEncoding()");
@@ -246,24 +249,13 @@ std::vector<uint8_t> BatchXdrEncoder::flush(bool framed, std::vector<uint64_t> *
     if (p_->in_record) throw std::logic_error("flush() inside a record");
     Impl &m = *p_;
     std::vector<uint8_t> out;
+    m.stream.clear();
+    m.offs.assign(1, 0);
     if (!m.n) {
         if (offsets) offsets->assign(1, 0);
         return out;
     }
     SchemaHandle sch(m.tape);
-    // XDR size of the batch (capacity for the engine; it computes the same)
-    uint64_t total = (framed ? 4 : 0) * m.n;
-    for (const Column &c : m.cols) {
-        if (c.f.kind == XDRG_K_DYNAMIC) {
-            for (uint64_t i = 0; i < m.n; ++i) {
-                const uint64_t cnt = c.offsets[i + 1] - c.offsets[i];
-                total += 4 + (xdr_size(c.f.type) == 1 ? cnt + pad4(cnt) : cnt * xdr_size(c.f.type));
-            }
-        } else {
-            const uint64_t cnt = c.f.kind == XDRG_K_FIXED ? c.f.count : 1;
-            total += m.n * (c.f.type == XDRG_T_OPAQUE ? cnt + pad4(cnt) : cnt * xdr_size(c.f.type));
-        }
-    }
     std::vector<DevBuf> bufs;
     std::vector<xdrg_column> cols(m.cols.size());
     for (size_t k = 0; k < m.cols.size(); ++k) {
@@ -280,22 +272,52 @@ std::vector<uint8_t> BatchXdrEncoder::flush(bool framed, std::vector<uint64_t> *
             cols[k].offsets = (uint64_t *)bufs.back().p;
         }
     }
-    DevBuf d_out(total), d_offs((m.n + 1) * 8);
+    // Encode into the staging buffer's capacity; when the batch does not fit
+    // the engine reports XDRG_E_CAPACITY and the bytes it needs, and the
+    // buffer grows as Xdr.ensureCapacity grows it (Xdr.java:1020-1026).
+    DevBuf d_offs((m.n + 1) * 8);
     uint64_t len = 0;
-    check(xdrg_encode_batch(m.eng->ctx(), sch.s, cols.data(), m.n, (uint8_t *)d_out.p, total,
-                            (uint64_t *)d_offs.p, framed ? XDRG_FRAME_RM : 0, &len),
-          m.eng->ctx());
-    out.resize(len);
-    d2h(out.data(), d_out.p, len);
-    if (offsets) {
-        offsets->resize(m.n + 1);
-        d2h(offsets->data(), d_offs.p, (m.n + 1) * 8);
+    m.buf.clear();
+    for (;;) {
+        DevBuf d_out(m.buf.remaining());
+        const int st = xdrg_encode_batch(m.eng->ctx(), sch.s, cols.data(), m.n, (uint8_t *)d_out.p,
+                                         m.buf.remaining(), (uint64_t *)d_offs.p, framed ? XDRG_FRAME_RM : 0, &len);
+        if (st == XDRG_E_CAPACITY && len > m.buf.remaining()) {
+            m.buf.ensureCapacity(len);
+            continue;
+        }
+        check(st, m.eng->ctx());
+        out.resize(len);
+        d2h(out.data(), d_out.p, len);
+        break;
     }
+    m.buf.put(out.data(), len);
+    m.buf.flip();   // endEncoding (Xdr.java:143-146)
+    m.offs.resize(m.n + 1);
+    d2h(m.offs.data(), d_offs.p, (m.n + 1) * 8);
+    if (offsets) *offsets = m.offs;
+    m.stream = out;
     m.cols.clear();
     m.tape.clear();
     m.have_tape = false;
     m.n = 0;
     return out;
+}
+
+uint64_t BatchXdrEncoder::messages() const { return p_->offs.size() - 1; }
+const XdrBuffer &BatchXdrEncoder::buffer() const { return p_->buf; }
+
+std::vector<uint8_t> BatchXdrEncoder::getBytes(uint64_t i) const {
+    // checkState(!_inUse, ...) (Xdr.java:999)
+    if (p_->in_record) throw std::logic_error("getBytes called while buffer in use");
+    if (i >= messages()) throw std::out_of_range("no such message in the last flushed batch");
+    return std::vector<uint8_t>(p_->stream.begin() + (ptrdiff_t)p_->offs[i],
+                                p_->stream.begin() + (ptrdiff_t)p_->offs[i + 1]);
+}
+
+BufferView BatchXdrEncoder::asBuffer(uint64_t i) const {
+    if (i >= messages()) throw std::out_of_range("no such message in the last flushed batch");
+    return BufferView{p_->stream.data() + p_->offs[i], (size_t)(p_->offs[i + 1] - p_->offs[i])};
 }
 
 // ---------------------------------------------------------------------------
@@ -416,6 +438,16 @@ void BatchXdrDecoder::beginDecoding() {
     if ((uint64_t)m.rec >= m.first_bad) fail(m.err, m.eng->ctx());   // what the reference throws
 }
 void BatchXdrDecoder::endDecoding() {}
+
+bool BatchXdrDecoder::hasMoreData() const {
+    const Impl &m = *p_;
+    if (m.rec < 0 || (uint64_t)m.rec >= m.n) return false;
+    for (size_t k = m.field; k < m.tape.size(); ++k) {   // any remaining field with XDR bytes
+        const xdrg_field &f = m.tape[k];
+        if (f.kind != XDRG_K_FIXED || f.count) return true;   // scalars and length words are >= 4 bytes
+    }
+    return false;
+}
 
 int32_t BatchXdrDecoder::xdrDecodeInt() { return p_->scalar<int32_t>(XDRG_T_INT); }
 std::vector<int32_t> BatchXdrDecoder::xdrDecodeIntVector() { return p_->dynamic<int32_t>(XDRG_T_INT); }

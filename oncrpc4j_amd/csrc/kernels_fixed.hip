@@ -24,8 +24,6 @@ namespace xdrg {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-static int g_words_lane = 2;   // tuning key 16: 0 word-map, 1 lane-per-record, 2 LDS-staged lane (default)
-
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // Float.floatToIntBits: every NaN -> 0x7fc00000 (Xdr.java:674-676).
@@ -151,108 +149,14 @@ __device__ __forceinline__ void divmod(uint64_t x, uint32_t d, double inv, uint6
     r = (uint32_t)rr;
 }
 
-__global__ __launch_bounds__(256) void k_stream_framed_enc(const StreamArgs a, uint64_t n, uint32_t mark_le,
-                                                           double inv_wt) {
-    __shared__ uint8_t sops[kMaxWords];
-    for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
-    __syncthreads();
-    const uint32_t W = a.w, Wt = a.w + 1;
-    const uint64_t total = n * Wt;                 // output words
-    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint64_t g0 = c * 4;
-    if (g0 >= total) return;
-    uint64_t r0; uint32_t w0;
-    divmod(g0, Wt, inv_wt, r0, w0);
-    const uint64_t nin = n * W;                    // input words
-    const uint64_t i0 = r0 * W + (w0 ? w0 - 1 : 0);
-    const uint32_t *src = (const uint32_t *)a.src;
-    uint32_t x0, x1, x2, x3, x4 = 0;
-    if (i0 + 5 <= nin) {
-        const u32x4w v = __builtin_nontemporal_load((const u32x4w *)(src + i0));
-        x0 = v.x; x1 = v.y; x2 = v.z; x3 = v.w;
-    } else {
-        x0 = i0 < nin ? src[i0] : 0u; x1 = i0 + 1 < nin ? src[i0 + 1] : 0u;
-        x2 = i0 + 2 < nin ? src[i0 + 2] : 0u; x3 = i0 + 3 < nin ? src[i0 + 3] : 0u;
-    }
-    (void)x4;
-    uint32_t o[4];
-    uint32_t k = 0, w = w0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (w == 0) {
-            o[j] = mark_le;
-        } else {
-            o[j] = word_op(sops[w - 1], pick5(x0, x1, x2, x3, x4, k));
-            ++k;
-        }
-        if (++w == Wt) w = 0;
-    }
-    u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
-    uint8_t *dst = a.dst + g0 * 4;
-    if (g0 + 4 <= total) {
-        __builtin_nontemporal_store(ov, (u32x4 *)dst);
-    } else {
-        for (uint64_t j = 0; g0 + j < total; ++j) ((uint32_t *)dst)[j] = o[j];
-    }
-}
-
-__global__ __launch_bounds__(256) void k_stream_framed_dec(const StreamArgs a, uint64_t n, uint32_t mark_le,
-                                                           double inv_w, unsigned long long *errkey) {
-    __shared__ uint8_t sops[kMaxWords];
-    for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
-    __syncthreads();
-    const uint32_t W = a.w, Wt = a.w + 1;
-    const uint64_t total = n * W;                  // native words
-    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint64_t n0 = c * 4;
-    if (n0 >= total) return;
-    uint64_t r0; uint32_t w0;
-    divmod(n0, W, inv_w, r0, w0);
-    const uint64_t x0i = r0 * Wt + 1 + w0;          // XDR word of native word n0
-    const uint64_t nx = n * Wt;
-    const uint32_t *src = (const uint32_t *)a.src;
-    uint32_t y0, y1, y2, y3, y4;
-    if (x0i + 5 <= nx) {
-        const u32x4w v = __builtin_nontemporal_load((const u32x4w *)(src + x0i));
-        y0 = v.x; y1 = v.y; y2 = v.z; y3 = v.w;
-        y4 = src[x0i + 4];
-    } else {
-        y0 = x0i < nx ? src[x0i] : 0u; y1 = x0i + 1 < nx ? src[x0i + 1] : 0u;
-        y2 = x0i + 2 < nx ? src[x0i + 2] : 0u; y3 = x0i + 3 < nx ? src[x0i + 3] : 0u;
-        y4 = x0i + 4 < nx ? src[x0i + 4] : 0u;
-    }
-    uint32_t o[4];
-    uint32_t k = 0, w = w0;
-    uint64_t r = r0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (n0 + j >= total) { o[j] = 0; continue; }
-        if (w == 0) {   // first word of record r: check its mark (the word before)
-            const uint32_t m = k == 0 ? src[x0i - 1] : pick5(y0, y1, y2, y3, y4, k - 1);
-            if (m != mark_le) atomicMin(errkey, err_key(r, 0, XDRG_E_FRAME));
-        }
-        o[j] = word_op(sops[w], pick5(y0, y1, y2, y3, y4, k));
-        ++k;
-        if (++w == W) { w = 0; ++r; ++k; }   // skip the next record's mark
-    }
-    u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
-    uint8_t *dst = a.dst + n0 * 4;
-    if (n0 + 4 <= total) {
-        __builtin_nontemporal_store(ov, (u32x4 *)dst);
-    } else {
-        for (uint64_t j = 0; n0 + j < total; ++j) ((uint32_t *)dst)[j] = o[j];
-    }
-}
-
-// ---- wave-local LDS transpose variant ----------------------------------------
-// The direct kernels above read 4-aligned (not 16-aligned) 16-byte windows:
-// every lane's load straddles two 16-byte sectors.  Here each wavefront owns
-// 256 consecutive destination words: it loads the source words they need as
-// 16-byte ALIGNED vectors (coalesced, one per lane, nontemporal) into its own
-// LDS slice, then every lane gathers its 4 destination words from LDS and
-// writes one aligned 16-byte vector.  Only the wave synchronises (no block
-// barrier after the op-table staging).
-constexpr int kFrEncWords = 4 * 66;      // encode: <= 256 + 3 source words per wave
+// ---- wave-local LDS transpose (decode of records under 3 words) --------------
+// Each wavefront owns 256 consecutive destination words: it loads the source
+// words they need as 16-byte ALIGNED vectors (coalesced, one per lane,
+// nontemporal) into its own LDS slice, then every lane gathers its 4
+// destination words from LDS and writes one aligned 16-byte vector.  Only
+// the wave synchronises (no block barrier after the op-table staging).  The
+// lean kernels below are faster; this one stays for records
+// whose 4 native words can span two marks.
 constexpr int kFrDecWords = 4 * 130;     // decode: <= 256 * (W+1)/W + 4 <= 516 source words
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -275,42 +179,6 @@ __device__ __forceinline__ void wave_stage(uint32_t *t, const uint32_t *src, uin
             x.z = wi + 2 < limit ? src[wi + 2] : 0u; x.w = 0u;
         }
         *(u32x4 *)(t + 4 * v) = x;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_stream_framed_enc_lds(const StreamArgs a, uint64_t n,
-                                                               uint32_t mark_le, double inv_wt) {
-    __shared__ uint8_t sops[kMaxWords];
-    __shared__ __attribute__((aligned(16))) uint32_t sbuf[4][kFrEncWords];
-    for (int t = threadIdx.x; t < (int)a.w; t += 256) sops[t] = a.ops[t];
-    __syncthreads();
-    const uint32_t W = a.w, Wt = a.w + 1, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t total = n * Wt;                          // XDR words
-    const uint64_t g_first = ((uint64_t)blockIdx.x * 4 + wid) * 256;
-    if (g_first >= total) return;
-    uint64_t r0; uint32_t j0;
-    divmod(g_first, Wt, inv_wt, r0, j0);
-    const uint64_t B = (r0 * W + (j0 ? j0 - 1 : 0)) & ~3ull;   // first native word needed, aligned
-    uint32_t *t = sbuf[wid];
-    wave_stage(t, (const uint32_t *)a.src, B, 65, n * W, lane);
-    wave_lds_sync();
-    const uint64_t g0 = g_first + 4 * (uint64_t)lane;
-    if (g0 >= total) return;
-    uint64_t r; uint32_t j;
-    divmod(g0, Wt, inv_wt, r, j);
-    uint32_t o[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        // word j of message r: its mark (GrizzlyRpcTransport.java:103-110) or native word j-1
-        o[k] = j == 0 ? mark_le : word_op(sops[j - 1], t[r * W + j - 1 - B]);
-        if (++j == Wt) { j = 0; ++r; }
-    }
-    uint8_t *dst = a.dst + g0 * 4;
-    if (g0 + 4 <= total) {
-        u32x4 ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
-        __builtin_nontemporal_store(ov, (u32x4 *)dst);
-    } else {
-        for (uint64_t k = 0; g0 + k < total; ++k) ((uint32_t *)dst)[k] = o[k];
     }
 }
 
@@ -359,9 +227,9 @@ __global__ __launch_bounds__(256) void k_stream_framed_dec_lds(const StreamArgs 
     }
 }
 
-// ---- lean variant ----------------------------------------------------------------
-// The direct kernels spend more VALU than memory time: a 64-bit double-
-// reciprocal divmod per lane, an LDS op-table read per word.  Here the
+// ---- lean kernels (default) ------------------------------------------------------
+// A per-lane 64-bit double-reciprocal divmod and an LDS op-table read per
+// word made the first direct kernels VALU-bound.  Here the
 // division happens once per wave on uniform values (scalar unit); a lane
 // only adds its 32-bit offset (4 * lane < 256 words) and splits it with a
 // float reciprocal; schemas of plain int/uint/enum words (ALLB) skip the op
@@ -482,47 +350,33 @@ __global__ __launch_bounds__(256) void k_stream_framed_dec_lean(const StreamArgs
     }
 }
 
-static int g_framed_kernel = 2;   // 0 = direct 4-aligned windows, 1 = wave-local LDS transpose, 2 = lean (default)
-
 int launch_stream_framed(const StreamArgs &a, uint64_t n, uint32_t mark_le, bool decode,
-                         unsigned long long *errkey, void *stream) {
+                         unsigned long long *errkey, const Tuning &t, void *stream) {
     if (!n || !a.w) return hipSuccess;
     hipStream_t st = (hipStream_t)stream;
-    const uint64_t words = decode ? n * a.w : n * (a.w + 1);
-    // the direct decode kernel holds 5 source words per lane: 4 native words
-    // of records of W < 3 words can span more (two marks), so those take the
-    // LDS variant whatever the knob says
-    if (g_framed_kernel == 1 || (decode && a.w < 3)) {
+    // the lean decode kernel holds 5 source words per lane: 4 native words of
+    // records of W < 3 words can span more (two marks), so those take the
+    // wave-LDS variant (tuning key 14 = 1 forces it for every decode)
+    if (decode && (t.framed == 1 || a.w < 3)) {
+        const uint64_t words = n * a.w;
         const uint64_t blocks = (words + 1023) / 1024;     // 4 waves x 256 words
-        if (decode)
-            hipLaunchKernelGGL(k_stream_framed_dec_lds, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
-                               1.0 / (double)a.w, errkey);
-        else
-            hipLaunchKernelGGL(k_stream_framed_enc_lds, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
-                               1.0 / (double)(a.w + 1));
-        return (int)hipGetLastError();
-    }
-    const uint64_t blocks = (((words + 3) >> 2) + 255) / 256;
-    if (g_framed_kernel == 2) {
-        if (decode) {
-            if (a.all_bswap)
-                hipLaunchKernelGGL(k_stream_framed_dec_lean<true>, dim3(blocks), dim3(256), 0, st, a, n, mark_le, errkey);
-            else
-                hipLaunchKernelGGL(k_stream_framed_dec_lean<false>, dim3(blocks), dim3(256), 0, st, a, n, mark_le, errkey);
-        } else {
-            if (a.all_bswap)
-                hipLaunchKernelGGL(k_stream_framed_enc_lean<true>, dim3(blocks), dim3(256), 0, st, a, n, mark_le);
-            else
-                hipLaunchKernelGGL(k_stream_framed_enc_lean<false>, dim3(blocks), dim3(256), 0, st, a, n, mark_le);
-        }
-        return (int)hipGetLastError();
-    }
-    if (decode)
-        hipLaunchKernelGGL(k_stream_framed_dec, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
+        hipLaunchKernelGGL(k_stream_framed_dec_lds, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
                            1.0 / (double)a.w, errkey);
-    else
-        hipLaunchKernelGGL(k_stream_framed_enc, dim3(blocks), dim3(256), 0, st, a, n, mark_le,
-                           1.0 / (double)(a.w + 1));
+        return (int)hipGetLastError();
+    }
+    const uint64_t words = decode ? n * a.w : n * (a.w + 1);
+    const uint64_t blocks = (((words + 3) >> 2) + 255) / 256;
+    if (decode) {
+        if (a.all_bswap)
+            hipLaunchKernelGGL(k_stream_framed_dec_lean<true>, dim3(blocks), dim3(256), 0, st, a, n, mark_le, errkey);
+        else
+            hipLaunchKernelGGL(k_stream_framed_dec_lean<false>, dim3(blocks), dim3(256), 0, st, a, n, mark_le, errkey);
+    } else {
+        if (a.all_bswap)
+            hipLaunchKernelGGL(k_stream_framed_enc_lean<true>, dim3(blocks), dim3(256), 0, st, a, n, mark_le);
+        else
+            hipLaunchKernelGGL(k_stream_framed_enc_lean<false>, dim3(blocks), dim3(256), 0, st, a, n, mark_le);
+    }
     return (int)hipGetLastError();
 }
 
@@ -688,64 +542,21 @@ static uint64_t grid_for(uint64_t work_items, uint64_t per_block, uint64_t max_b
     return b ? b : 1;
 }
 
-// Streaming-kernel tuning (defaults chosen by tools/tune_stream.py on MI355X;
-// see DESIGN.md).  Set through xdrg_internal_tune(), outside the C-ABI.
-static int g_stream_unroll = 1;         // 16-byte vectors in flight per lane
-static int g_stream_nt = 3;             // bit 0: nontemporal loads, bit 1: stores
-static int g_stream_blocks_per_cu = 0;  // grid = min(needed, CUs * this); 0 = one pass
-
-template <int U>
-static void launch_bswap_u(const u32x4 *src, u32x4 *dst, uint64_t nvec, uint64_t blocks, int nt,
-                           hipStream_t st) {
-    switch (nt & 3) {
-    case 0: hipLaunchKernelGGL((k_stream_bswap<U, false, false>), dim3(blocks), dim3(256), 0, st, src, dst, nvec); break;
-    case 1: hipLaunchKernelGGL((k_stream_bswap<U, true, false>), dim3(blocks), dim3(256), 0, st, src, dst, nvec); break;
-    case 2: hipLaunchKernelGGL((k_stream_bswap<U, false, true>), dim3(blocks), dim3(256), 0, st, src, dst, nvec); break;
-    default: hipLaunchKernelGGL((k_stream_bswap<U, true, true>), dim3(blocks), dim3(256), 0, st, src, dst, nvec); break;
-    }
-}
-
-int launch_stream_words(const StreamArgs &a, int variant, void *stream) {
-    (void)variant;
+// Streaming kernels: one 16-byte vector per lane, one pass over the batch
+// (no grid-stride loop), nontemporal loads and stores — the shape a sweep of
+// unroll x nontemporal x grid chose on MI355X.
+int launch_stream_words(const StreamArgs &a, void *stream) {
     if (!a.nvec) return hipSuccess;
     hipStream_t st = (hipStream_t)stream;
-    const int U = g_stream_unroll;
-    const uint64_t cap = g_stream_blocks_per_cu > 0 ? (uint64_t)num_cu() * g_stream_blocks_per_cu : ~0ull;
-    const uint64_t blocks = grid_for(a.nvec, 256 * (uint64_t)U, cap);
     if (a.all_bswap) {
-        const u32x4 *src = (const u32x4 *)a.src;
-        u32x4 *dst = (u32x4 *)a.dst;
-        switch (U) {
-        case 1: launch_bswap_u<1>(src, dst, a.nvec, blocks, g_stream_nt, st); break;
-        case 2: launch_bswap_u<2>(src, dst, a.nvec, blocks, g_stream_nt, st); break;
-        case 8: launch_bswap_u<8>(src, dst, a.nvec, blocks, g_stream_nt, st); break;
-        default: launch_bswap_u<4>(src, dst, a.nvec, blocks, g_stream_nt, st); break;
-        }
+        const uint64_t blocks = grid_for(a.nvec, 256, ~0ull);
+        hipLaunchKernelGGL((k_stream_bswap<1, true, true>), dim3(blocks), dim3(256), 0, st,
+                           (const u32x4 *)a.src, (u32x4 *)a.dst, a.nvec);
     } else {
-        const uint64_t b4 = grid_for(a.nvec, 256 * 4, cap);
-        if (g_stream_nt) hipLaunchKernelGGL((k_stream_ops<4, true>), dim3(b4), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((k_stream_ops<4, false>), dim3(b4), dim3(256), 0, st, a);
+        const uint64_t b4 = grid_for(a.nvec, 256 * 4, ~0ull);
+        hipLaunchKernelGGL((k_stream_ops<4, true>), dim3(b4), dim3(256), 0, st, a);
     }
     return (int)hipGetLastError();
-}
-
-// key 1: unroll (1/2/4/8), key 2: nontemporal bits, key 3: blocks per CU (0 = one pass),
-// keys 4/5: record-path encode/decode copy unroll (1/2/4), 6-9: record-path
-// group sizing / kernel choice, 10/11: record-path records per lane in flight,
-// 12: staged record kernels LDS tile bytes, 13: staged/group split (bytes per record)
-int set_tuning(int key, long long value) {
-    switch (key) {
-    case 1:
-        if (value != 1 && value != 2 && value != 4 && value != 8) return -1;
-        g_stream_unroll = (int)value;
-        return 0;
-    case 2: g_stream_nt = (int)(value & 3); return 0;
-    case 3: if (value < 0) return -1; g_stream_blocks_per_cu = (int)value; return 0;
-    case 4: case 5: case 6: case 7: case 8: case 9: case 10: case 11: case 12: case 13: case 17: case 18: return set_rec_tuning(key, value);
-    case 14: if (value < 0 || value > 2) return -1; g_framed_kernel = (int)value; return 0;
-    case 16: if (value < 0 || value > 2) return -1; g_words_lane = (int)value; return 0;
-    default: return -1;
-    }
 }
 
 static void wordmap_grid(WordMapArgs &a, uint64_t words, uint64_t *blocks) {
@@ -990,12 +801,12 @@ bool words_lane_ok(const WordOp *ops, uint32_t nops) {
     return true;
 }
 
-int launch_words_lane(const WordMapArgs &a, bool decode, bool v16, void *stream) {
-    if (!g_words_lane) return -1;   // the caller falls back to the word-map kernels
+int launch_words_lane(const WordMapArgs &a, bool decode, bool v16, const Tuning &t, void *stream) {
+    if (!t.words) return -1;   // the caller falls back to the word-map kernels
     if (!a.n) return hipSuccess;
     hipStream_t st = (hipStream_t)stream;
     const dim3 grid((unsigned)((a.n + 255) / 256));
-    if (g_words_lane == 2 && ((uintptr_t)a.xdr & 15) == 0) {
+    if (t.words == 2 && ((uintptr_t)a.xdr & 15) == 0) {
         if (decode) hipLaunchKernelGGL(k_words_lds_dec, grid, dim3(256), 0, st, a);
         else hipLaunchKernelGGL(k_words_lds_enc, grid, dim3(256), 0, st, a);
         return (int)hipGetLastError();

@@ -2032,7 +2032,6 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
     if (a.framed)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
         for (uint32_t j = tid; j < nrec; j += kRecThreads)
             *(uint32_t *)(out + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
-    if (a.probe_skip & 8) return;
     // ---- sub-batches
     uint32_t js = 0;
     uint32_t k1 = enc_fit(a, base, srel, js, nrec);
@@ -2058,7 +2057,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
             cb[d + 1] += stage_chunks(f.data + (base[d] + srel[d * RS + js]) * esz,
                                       f.data + (base[d] + srel[d * RS + je]) * esz, &a0[d]);
         }
-        if (!(a.probe_skip & 4)) stage_copy(tile, a0, cb, a.ndyn);
+        stage_copy(tile, a0, cb, a.ndyn);
         __syncthreads();
         // scatter, field-major; field k of record j sits at
         // soff[j] + (fixed bytes before k) + (dynamic bytes before k)
@@ -2069,7 +2068,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
             const VField &f = a.f[k];
             if (f.kind != XDRG_K_DYNAMIC) {
                 const uint32_t nw = f.xbytes >> 2;
-                if (nw && !(a.probe_skip & 2)) {
+                if (nw) {
                     const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
                     const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
                     for (uint32_t j = js + tid / G; j < je; j += ng) {
@@ -2080,7 +2079,6 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
                 fpre += f.xbytes;
                 continue;
             }
-            if (a.probe_skip & 1) { ++d; continue; }
             const bool bytes = f.xsz == 1;
             const uint64_t esz = bytes ? 1 : f.nsz;
             const uint32_t *rel = srel + d * RS;
@@ -2262,7 +2260,6 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
             dec_record_block(a, rb + j, rec_extent(a, rb + j).a + (a.framed ? 4 : 0), supto[j]);
         return;
     }
-    if (a.probe_skip & 8) return;
     // ---- sub-batches
     uint32_t js = 0;
     uint32_t k1 = nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
@@ -2278,7 +2275,7 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
         uint32_t cb[kMaxDynLds + 1] = {0, 0, 0, 0, 0};
         cb[1] = stage_chunks(in + sb + sstart[js], in + sb + sstart[je - 1] + fx + dyn_before(a, snrel, je - 1, a.ndyn),
                              &a0[0]);
-        if (!(a.probe_skip & 4)) stage_copy(tile, a0, cb, 1);
+        stage_copy(tile, a0, cb, 1);
         __syncthreads();
         const int64_t lds0 = -(int64_t)(a0[0] - (in + sb));   // tile offset of sstart value x: lds0 + x
         uint32_t fpre = 0;
@@ -2288,7 +2285,7 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
             const VField &f = a.f[k];
             if (f.kind != XDRG_K_DYNAMIC) {
                 const uint32_t nw = f.xbytes >> 2;
-                if (nw && !(a.probe_skip & 2)) {
+                if (nw) {
                     const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
                     const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
                     for (uint32_t j = js + tid / G; j < je; j += ng) {
@@ -2301,22 +2298,8 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
                 fpre += f.xbytes;
                 continue;
             }
-            if (a.probe_skip & 1) { ++d; continue; }
             const bool bytes = f.xsz == 1;
             const uint64_t esz = bytes ? 1 : f.nsz;
-            if (a.probe_skip & 16) {   // probe: aligned flat stores over the column range, no gather
-                uint8_t *cb0 = f.data + a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x] * esz;
-                const uint32_t *rl = snrel + d * RS;
-                const uintptr_t X0 = ((uintptr_t)(cb0 + (uint64_t)rl[js] * esz) + 15) & ~(uintptr_t)15;
-                const uintptr_t X1 = (uintptr_t)(cb0 + (uint64_t)rl[je] * esz) & ~(uintptr_t)15;
-                for (uintptr_t x = X0 + 16 * (uintptr_t)tid; x < X1; x += 16 * kRecThreads) {
-                    const uint32_t *w = (const uint32_t *)(tile + ((x - X0) & 0x3ff0));
-                    u32x4n v; v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3];
-                    *(u32x4n *)x = v;
-                }
-                ++d;
-                continue;
-            }
             const uint32_t *rel = snrel + d * RS;
             const uint64_t base = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x];
             const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
@@ -2363,40 +2346,6 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
 // ===========================================================================
 // Launchers
 // ===========================================================================
-__global__ void k_debug_recargs(const RecArgs a) {
-    if (threadIdx.x || blockIdx.x) return;
-    printf("RecArgs n=%llu nf=%u framed=%u fixed_xdr=%u ndyn=%u xdr=%p cap=%llu rec_in=%p stride=%llu "
-           "nblocks=%llu\n", (unsigned long long)a.n, a.nf, a.framed, a.fixed_xdr, a.ndyn, a.xdr,
-           (unsigned long long)a.xdr_cap, a.rec_in, (unsigned long long)a.rec_stride,
-           (unsigned long long)a.nblocks);
-    if (a.rec_in) printf("  rec_in[0..2]=%llu %llu %llu\n", (unsigned long long)a.rec_in[0],
-                         (unsigned long long)a.rec_in[1], (unsigned long long)a.rec_in[2]);
-    for (uint32_t k = 0; k < a.nf; ++k)
-        printf("  f%u type=%u kind=%u nsz=%u xsz=%u count=%u xbytes=%u data=%p off=%p cap=%llu\n", k,
-               a.f[k].type, a.f[k].kind, a.f[k].nsz, a.f[k].xsz, a.f[k].count, a.f[k].xbytes,
-               a.f[k].data, a.f[k].offsets, (unsigned long long)a.f[k].cap);
-    uint64_t c;
-    uint32_t sub;
-    const uint32_t e = walk_record(a, 0, a.ndyn ? a.dyn_idx[0] : 0, &c, &sub);
-    printf("  walk(0) -> err=%u sub=%u cnt=%llu\n", e, sub, (unsigned long long)c);
-    const uint32_t *w = (const uint32_t *)a.xdr;
-    printf("  xdr words: %08x %08x %08x %08x  be: %u %u %u\n", w[0], w[1], w[2], w[3], ld_be32(a.xdr),
-           ld_be32(a.xdr + 4), ld_be32(a.xdr + 8));
-    const Extent ex = rec_extent(a, 0);
-    uint64_t pos = ex.a + 8;
-    const int32_t len = (int32_t)ld_be32(a.xdr + pos);
-    pos += 4;
-    const uint64_t need = (uint64_t)len + pad4((uint64_t)len);
-    printf("  ext=[%llu,%llu) len=%d need=%llu room=%llu pad=%u\n", (unsigned long long)ex.a,
-           (unsigned long long)ex.b, len, (unsigned long long)need, (unsigned long long)(ex.b - pos),
-           pad4((uint64_t)len));
-}
-
-// copy unroll of the group kernels (tools/tune_rec.py; set_tuning keys 4 and
-// 5: chunks per record, 10 and 11: records per lane in flight)
-static int g_enc_u = 2, g_dec_u = 2;
-static int g_enc_r = 1, g_dec_r = 1;
-
 template <template <int, int> class K>
 static void launch_ur(int u, int r, dim3 grid, size_t lds, hipStream_t st, const RecArgs &a) {
 #define XDRG_UR(U_, R_) \
@@ -2408,76 +2357,14 @@ static void launch_ur(int u, int r, dim3 grid, size_t lds, hipStream_t st, const
 }
 template <int U, int R> struct EncG { static constexpr auto fn = k_enc_place_g<U, R>; };
 template <int U, int R> struct DecG { static constexpr auto fn = k_dec_place_g<U, R>; };
-static uint32_t g_force_g = 0;
-static int g_rec_kernel = 4;   // 4 = staged (default), 0 = group per record, 3 = lane per record
-static uint32_t g_tile_bytes = 16384;
-static uint32_t g_big_rec = 1024;   // XDR bytes per record from which blocks take the group kernel
-static uint32_t g_lane_bytes_enc = 32, g_lane_bytes_dec = 32;
-static uint32_t g_probe_skip = 0;
-static uint32_t g_payload = 3;   // payload kernels (key 18): 0 off, 1 wave per record, 2 block, 3 wave + nontemporal
-int set_rec_tuning(int key, long long value) {
-    if (key == 18) {
-        if (value < 0 || value > 3) return -1;   // 0 off, 1 wave per record, 2 block per record, 3 = 1 + nontemporal
-        g_payload = (uint32_t)value;
-        return 0;
-    }
-    if (key == 17) {   // probe only (tools/probe_stage_parts.py): the staged kernels skip parts
-                       // (bit0 dynamic scatter, bit1 fixed scatter, bit2 stage loads, bit3 all after
-                       // the prologue; bit4 decode writes its dynamic columns' ranges with aligned
-                       // flat stores, no gather); outputs are wrong under a mask
-        if (value < 0 || value > 31) return -1;
-        g_probe_skip = (uint32_t)value;
-        return 0;
-    }
-    if (key == 13) {   // staged kernels: group-kernel split (average XDR bytes per record; 0 = never)
-        if (value < 0 || value > (1ll << 31)) return -1;
-        g_big_rec = (uint32_t)value;
-        return 0;
-    }
-    if (key == 12) {   // staged kernels: LDS tile bytes per sub-batch
-        if (value < 1024 || value > 98304 || (value & 15)) return -1;
-        g_tile_bytes = (uint32_t)value;
-        return 0;
-    }
-    if (key == 9) {
-        if (value != 0 && value != 3 && value != 4) return -1;
-        g_rec_kernel = (int)value;
-        return 0;
-    }
-    if (key == 7 || key == 8) {   // target payload bytes per lane when sizing groups
-        if (value < 4 || value > 65536) return -1;
-        (key == 7 ? g_lane_bytes_enc : g_lane_bytes_dec) = (uint32_t)value;
-        return 0;
-    }
-    if (key == 6) {   // lanes per record: 0 = automatic, else a power of two <= 64
-        if (value < 0 || value > 64 || (value & (value - 1))) return -1;
-        g_force_g = (uint32_t)value;
-        return 0;
-    }
-    if (value != 1 && value != 2 && value != 4) return -1;
-    if (key == 4) g_enc_u = (int)value;
-    else if (key == 5) g_dec_u = (int)value;
-    else if (key == 10) g_enc_r = (int)value;
-    else if (key == 11) g_dec_r = (int)value;
-    else return -1;
-    return 0;
-}
 
-template <typename K>
-static void launch_payload(K wave, K wave_nt, K block, dim3 grid, hipStream_t st, const RecArgs &a) {
-    hipLaunchKernelGGL(g_payload == 2 ? block : g_payload == 3 ? wave_nt : wave, grid, dim3(256), 0, st, a);
-}
-
-int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
+int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stream) {
     RecArgs a = args;
-    a.force_g = g_force_g;
-    a.lane_bytes_enc = g_lane_bytes_enc;
-    a.lane_bytes_dec = g_lane_bytes_dec;
-    a.tile_bytes = g_tile_bytes;
+    a.force_g = t.force_g;
+    a.lane_bytes_enc = t.lane_bytes_enc;
+    a.lane_bytes_dec = t.lane_bytes_dec;
+    a.tile_bytes = t.tile_bytes;
     a.big_rec = 0;
-    a.probe_skip = g_probe_skip;
-    if (phase == REC_DEC_SIZES && getenv("XDRG_DEBUG"))
-        hipLaunchKernelGGL(k_debug_recargs, dim3(1), dim3(64), 0, (hipStream_t)stream, a);
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
     // conditional schemas (unions / optional data) and by-reference payloads take
@@ -2485,14 +2372,14 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
     const bool special = a.ncond || a.byref;
     const bool grp = a.ndyn <= (uint32_t)kMaxDynLds && !special;
     const bool lane = a.ndyn <= (uint32_t)kMaxDynLds && special;
-    bool stage = grp && g_rec_kernel == 4;
+    bool stage = grp && t.rec == 4;
     for (uint32_t d = 0; d < a.ndyn && stage; ++d)
         stage = stage_type(a.f[a.dyn_idx[d]].type, a.f[a.dyn_idx[d]].xsz);
     // one dynamic byte field, blocks on the group kernels: the payload kernels move it
-    const bool pay = g_payload && a.pay_pos && a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1 &&
-                     ((stage && g_big_rec) || (grp && !stage && g_rec_kernel == 0));
+    const bool pay = t.payload && a.pay_pos && a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1 &&
+                     ((stage && t.big_rec) || (grp && !stage && t.rec == 0));
     a.payk = pay ? 1u : 0u;
-    const uint64_t pblk = g_payload == 2 ? a.n : (a.n + 3) / 4;   // one record (group) per lane group
+    const uint64_t pblk = (a.n + 3) / 4;   // a wave per record, 4 records per block
     const dim3 pgrid((unsigned)(pblk < (1u << 22) ? pblk : (1u << 22)));
     switch (phase) {
     case REC_ENC_SIZES: hipLaunchKernelGGL(k_enc_sizes, dim3(nb), dim3(kRecThreads), 0, st, a); break;
@@ -2501,16 +2388,16 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
         break;
     case REC_ENC_PLACE:
         if (stage) {   // small-record blocks staged, large-record blocks by the group kernel
-            a.big_rec = g_big_rec;
+            a.big_rec = t.big_rec;
             hipLaunchKernelGGL(k_enc_stage, dim3(nb), dim3(kRecThreads),
                                enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
-            if (a.big_rec) launch_ur<EncG>(g_enc_u, g_enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
-            if (a.big_rec && pay) launch_payload(k_enc_payload<64, false>, k_enc_payload<64, true>, k_enc_payload<256, false>, pgrid, st, a);
-        } else if (lane || (grp && g_rec_kernel == 3)) {
+            if (a.big_rec) launch_ur<EncG>(t.enc_u, t.enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
+            if (a.big_rec && pay) hipLaunchKernelGGL((k_enc_payload<64, true>), pgrid, dim3(256), 0, st, a);
+        } else if (lane || (grp && t.rec == 3)) {
             hipLaunchKernelGGL(k_enc_lane, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
-            launch_ur<EncG>(g_enc_u, g_enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
-            if (pay) launch_payload(k_enc_payload<64, false>, k_enc_payload<64, true>, k_enc_payload<256, false>, pgrid, st, a);
+            launch_ur<EncG>(t.enc_u, t.enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
+            if (pay) hipLaunchKernelGGL((k_enc_payload<64, true>), pgrid, dim3(256), 0, st, a);
         }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
@@ -2525,16 +2412,16 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
         break;
     case REC_DEC_PLACE:
         if (stage) {
-            a.big_rec = g_big_rec;
+            a.big_rec = t.big_rec;
             hipLaunchKernelGGL(k_dec_stage, dim3(nb), dim3(kRecThreads),
                                dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
-            if (a.big_rec) launch_ur<DecG>(g_dec_u, g_dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
-            if (a.big_rec && pay) launch_payload(k_dec_payload<64, false>, k_dec_payload<64, true>, k_dec_payload<256, false>, pgrid, st, a);
-        } else if (lane || (grp && g_rec_kernel == 3)) {
+            if (a.big_rec) launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
+            if (a.big_rec && pay) hipLaunchKernelGGL((k_dec_payload<64, true>), pgrid, dim3(256), 0, st, a);
+        } else if (lane || (grp && t.rec == 3)) {
             hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
-            launch_ur<DecG>(g_dec_u, g_dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
-            if (pay) launch_payload(k_dec_payload<64, false>, k_dec_payload<64, true>, k_dec_payload<256, false>, pgrid, st, a);
+            launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
+            if (pay) hipLaunchKernelGGL((k_dec_payload<64, true>), pgrid, dim3(256), 0, st, a);
         }
         else hipLaunchKernelGGL(k_dec_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
@@ -2542,7 +2429,5 @@ int launch_rec_phase(const RecArgs &args, int phase, void *stream) {
     }
     return (int)hipGetLastError();
 }
-
-
 
 }  // namespace xdrg

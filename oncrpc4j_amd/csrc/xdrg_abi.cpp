@@ -198,6 +198,7 @@ struct xdrg_ctx {
     std::vector<hipEvent_t> pool;
     uint64_t launches[XDRG_KERNEL_COUNT] = {};
     double ms[XDRG_KERNEL_COUNT] = {};
+    Tuning tune;                // this context's kernel choices (xdrg_internal_tune)
 };
 
 static int hip_fail(xdrg_ctx *c, hipError_t e, const char *what) {
@@ -276,8 +277,33 @@ struct TimedLaunch {
 
 extern "C" int xdrg_abi_version(void) { return XDRG_ABI_VERSION; }
 
-// Not part of include/xdrg.h: kernel tuning knobs for tools/tune_stream.py.
-extern "C" int xdrg_internal_tune(int key, long long value) { return set_tuning(key, value); }
+int xdrg::set_tuning(Tuning &t, int key, long long v) {
+    auto in = [&](long long lo, long long hi) { return v >= lo && v <= hi; };
+    switch (key) {
+    case 4: case 5: case 10: case 11:
+        if (v != 1 && v != 2 && v != 4) return -1;
+        (key == 4 ? t.enc_u : key == 5 ? t.dec_u : key == 10 ? t.enc_r : t.dec_r) = (int32_t)v;
+        return 0;
+    case 6: if (!in(0, 64) || (v & (v - 1))) return -1; t.force_g = (uint32_t)v; return 0;
+    case 7: case 8: if (!in(4, 65536)) return -1; (key == 7 ? t.lane_bytes_enc : t.lane_bytes_dec) = (uint32_t)v; return 0;
+    case 9: if (v != 0 && v != 3 && v != 4) return -1; t.rec = (int32_t)v; return 0;
+    case 12: if (!in(1024, 98304) || (v & 15)) return -1; t.tile_bytes = (uint32_t)v; return 0;
+    case 13: if (!in(0, 1ll << 31)) return -1; t.big_rec = (uint32_t)v; return 0;
+    case 14: if (!in(1, 2)) return -1; t.framed = (int32_t)v; return 0;
+    case 16: if (!in(0, 2)) return -1; t.words = (int32_t)v; return 0;
+    case 18: if (!in(0, 1)) return -1; t.payload = (int32_t)v; return 0;
+    default: return -1;
+    }
+}
+
+// Not part of include/xdrg.h: per-context kernel choices (xdrg_internal.h
+// Tuning) for the parity tests, which force every production path, and for
+// tools/sweep_rec.py.  Key 0 restores the defaults.
+extern "C" int xdrg_internal_tune(xdrg_ctx *c, int key, long long value) {
+    if (!c) return XDRG_E_INVAL;
+    if (key == 0) { c->tune = Tuning(); return XDRG_OK; }
+    return set_tuning(c->tune, key, value) ? XDRG_E_INVAL : XDRG_OK;
+}
 
 extern "C" const char *xdrg_status_string(int status) {
     switch (status) {
@@ -567,7 +593,7 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
             a.w = s->nwords;
             fill_stream_ops(s, false, a);
             TimedLaunch t(c, XDRG_KERNEL_FIXED_ENCODE);
-            HIPCHK(c, (hipError_t)launch_stream_words(a, 0, c->stream));
+            HIPCHK(c, (hipError_t)launch_stream_words(a, c->stream));
         } else if (n && framed && framed_stream_eligible(s, cols, n, out, &base)) {
             StreamArgs a;
             memset(&a, 0, sizeof a);
@@ -577,7 +603,7 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
             fill_stream_ops(s, false, a);
             TimedLaunch t(c, XDRG_KERNEL_FIXED_ENCODE);
             HIPCHK(c, (hipError_t)launch_stream_framed(a, n, __builtin_bswap32((uint32_t)(s->fixed_size | kLastFrag)),
-                                                       false, nullptr, c->stream));
+                                                       false, nullptr, c->tune, c->stream));
         } else if (n && s->nwords + (framed ? 1 : 0) <= (uint32_t)kMaxWords && !s->ops.empty() &&
                    s->f.size() <= (size_t)kMaxCols) {
             WordMapArgs a;
@@ -587,7 +613,7 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
             TimedLaunch t(c, XDRG_KERNEL_FIXED_ENCODE);
             int lr = -1;
             if (words_lane_ok(a.ops, a.nops))
-                lr = launch_words_lane(a, false, aligned(out, 16) && (a.wt % 4) == 0, c->stream);
+                lr = launch_words_lane(a, false, aligned(out, 16) && (a.wt % 4) == 0, c->tune, c->stream);
             if (lr > 0) HIPCHK(c, (hipError_t)lr);
             if (lr < 0) HIPCHK(c, (hipError_t)launch_wordmap_encode(a, aligned(out, 16), c->stream));
         } else if (n && total) {
@@ -599,7 +625,7 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
             a.rec_out = nullptr;
             for (int ph = REC_ENC_SIZES; ph <= REC_ENC_PLACE; ++ph) {
                 TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE + ph);
-                HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+                HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->tune, c->stream));
             }
         }
         if (out_len) {
@@ -628,7 +654,7 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
     a.ref_pos = ref_pos;
     for (int ph = REC_ENC_SIZES; ph <= REC_ENC_PLACE; ++ph) {
         TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE + ph);
-        HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+        HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->tune, c->stream));
     }
     if (async) {
         if (out_len) HIPCHK(c, hipMemcpyAsync(out_len, a.totals, 8, hipMemcpyDeviceToDevice, c->stream));
@@ -744,7 +770,7 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
             a.w = s->nwords;
             fill_stream_ops(s, true, a);
             TimedLaunch t(c, XDRG_KERNEL_FIXED_DECODE);
-            HIPCHK(c, (hipError_t)launch_stream_words(a, 0, c->stream));
+            HIPCHK(c, (hipError_t)launch_stream_words(a, c->stream));
         } else if (n && framed && in_len >= total && framed_stream_eligible(s, cols, n, in, &base)) {
             StreamArgs a;
             memset(&a, 0, sizeof a);
@@ -756,7 +782,7 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
             HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
             TimedLaunch t(c, XDRG_KERNEL_FIXED_DECODE);
             HIPCHK(c, (hipError_t)launch_stream_framed(a, n, __builtin_bswap32((uint32_t)(s->fixed_size | kLastFrag)),
-                                                       true, c->d_stat, c->stream));
+                                                       true, c->d_stat, c->tune, c->stream));
         } else if (n && stride && s->nwords + (framed ? 1 : 0) <= (uint32_t)kMaxWords &&
                    !s->ops.empty() && s->f.size() <= (size_t)kMaxCols) {
             WordMapArgs a;
@@ -770,7 +796,7 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
             TimedLaunch t(c, XDRG_KERNEL_FIXED_DECODE);
             int lr = -1;
             if (words_lane_ok(a.ops, a.nops))
-                lr = launch_words_lane(a, true, aligned(in, 16) && (a.wt % 4) == 0, c->stream);
+                lr = launch_words_lane(a, true, aligned(in, 16) && (a.wt % 4) == 0, c->tune, c->stream);
             if (lr > 0) HIPCHK(c, (hipError_t)lr);
             if (lr < 0) HIPCHK(c, (hipError_t)launch_wordmap_decode(a, aligned(in, 16), c->stream));
         } else if (n && stride) {
@@ -785,7 +811,7 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
             dev_key = true;
             for (int ph = REC_DEC_SIZES; ph <= REC_DEC_PLACE; ++ph) {
                 TimedLaunch t(c, rec_dec_kernel_id(ph));
-                HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+                HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->tune, c->stream));
             }
         }
         return finish_decode(c, n, host_key, dev_key, async, first_bad, err);
@@ -808,7 +834,7 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
     HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
     for (int ph = REC_DEC_SIZES; ph <= REC_DEC_PLACE; ++ph) {
         TimedLaunch t(c, rec_dec_kernel_id(ph));
-        HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+        HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->tune, c->stream));
     }
     return finish_decode(c, n, kNoError, true, async, first_bad, err);
 }
@@ -986,7 +1012,7 @@ static int shard_size_launch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_colum
     RecArgs a;
     int rc = fill_rec(c, s, (xdrg_column *)cols, n, framed, a);
     if (rc) return rc;
-    for (int ph = REC_ENC_SIZES; ph <= REC_ENC_SCAN; ++ph) HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->stream));
+    for (int ph = REC_ENC_SIZES; ph <= REC_ENC_SCAN; ++ph) HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->tune, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, a.totals, 8, hipMemcpyDeviceToHost, c->stream));
     *on_device = true;
     return XDRG_OK;

@@ -134,7 +134,7 @@ struct RecArgs {
                                // kernels, the others the staged ones (0: one kernel for all)
     uint32_t ncond;            // conditional fields in the schema (0: every record has all fields)
     uint32_t byref;            // 0, or 1 + the field encoded by reference / decoded as a view
-    uint32_t probe_skip;       // probe only (tuning key 17): parts of the staged kernels skipped
+    uint32_t rsv2;
     uint64_t *ref_pos;         // byref: encode splice[n] / decode payload_pos[n]
     uint32_t payk;             // 0, or 1 + the dynamic byte field the payload kernels move for the
                                // group kernels' blocks (k_enc/dec_payload)
@@ -157,22 +157,42 @@ __host__ __device__ inline unsigned long long err_key(uint64_t rec, uint32_t sub
 }
 constexpr unsigned long long kNoError = ~0ull;
 
-// ---- launchers (kernels.hip) -------------------------------------------
+// ---- per-context kernel choices -----------------------------------------
+// Every value selects among production kernels (each of which some input
+// takes anyway) or sizes one; the defaults are the measured winners
+// (DESIGN.md §5).  A context owns its own copy (one context per thread), set
+// through xdrg_internal_tune() — not part of include/xdrg.h; the parity tests
+// force each path and tools/sweep_rec.py sweeps the sizes.
+struct Tuning {
+    int32_t words = 2;              // key 16: fixed 4-byte-word schemas: 2 LDS-staged, 1 lane per record, 0 word-map
+    int32_t framed = 2;             // key 14: record-marked AoS decode: 2 lean, 1 wave-LDS transpose
+    int32_t rec = 4;                // key 9: record path: 4 staged sub-batches, 0 group per record, 3 lane per record
+    int32_t payload = 1;            // key 18: one dynamic byte field on group-kernel blocks: 1 payload kernels, 0 in place
+    int32_t enc_u = 2, dec_u = 2;   // keys 4/5: group kernels, 16-byte chunks per lane in flight
+    int32_t enc_r = 1, dec_r = 1;   // keys 10/11: group kernels, records per lane in flight
+    uint32_t force_g = 0;           // key 6: lanes per record (0 = sized from the field)
+    uint32_t lane_bytes_enc = 32;   // keys 7/8: group sizing, XDR bytes per lane
+    uint32_t lane_bytes_dec = 32;
+    uint32_t tile_bytes = 16384;    // key 12: staged kernels, LDS tile per sub-batch
+    uint32_t big_rec = 1024;        // key 13: blocks averaging >= this many XDR bytes per record
+                                    // take the group kernels (0 = never)
+};
+int set_tuning(Tuning &t, int key, long long value);   // 0, or -1 for an unknown key / bad value
+
+// ---- launchers (kernels_*.hip) -----------------------------------------
 // All launches go on `stream`; each returns hipSuccess or the launch error.
-int launch_stream_words(const StreamArgs &a, int variant, void *stream);
-int set_tuning(int key, long long value);      // kernel knobs (tools/tune_*.py)
-int set_rec_tuning(int key, long long value);
+int launch_stream_words(const StreamArgs &a, void *stream);
 // record-marked AoS-dense stream (words: BSWAP / FLOAT / OPAQUE only)
 int launch_stream_framed(const StreamArgs &a, uint64_t n, uint32_t mark_le, bool decode,
-                         unsigned long long *errkey, void *stream);
+                         unsigned long long *errkey, const Tuning &t, void *stream);
 int launch_wordmap_encode(const WordMapArgs &a, bool aligned16, void *stream);
 // lane-per-record word kernels (every XDR word one 4-byte native word, <= 32
 // words per record incl. the mark); returns -1 when switched off (tuning)
 bool words_lane_ok(const WordOp *ops, uint32_t nops);
-int launch_words_lane(const WordMapArgs &a, bool decode, bool v16, void *stream);
+int launch_words_lane(const WordMapArgs &a, bool decode, bool v16, const Tuning &t, void *stream);
 int launch_wordmap_decode(const WordMapArgs &a, bool aligned16, void *stream);
 enum RecPhase { REC_ENC_SIZES, REC_ENC_SCAN, REC_ENC_PLACE, REC_DEC_SIZES, REC_DEC_SCAN, REC_DEC_PLACE };
-int launch_rec_phase(const RecArgs &a, int phase, void *stream);
+int launch_rec_phase(const RecArgs &a, int phase, const Tuning &t, void *stream);
 // *dst = value (stream-ordered)
 int launch_store_u64(uint64_t *dst, uint64_t value, void *stream);
 // rec_offsets[i] = i * stride for i in [0, n]

@@ -19,12 +19,6 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.s
 
 _LIB = None
 
-# record-path implementation the library starts with (kernels_rec.hip
-# g_rec_kernel: 4 = staged sub-batches, 0 = group per record, 3 = lane per record)
-DEFAULT_REC_KERNEL = 4
-# record-marked streaming kernel the library starts with (kernels_fixed.hip
-# g_framed_kernel: 0 = direct 4-aligned windows, 1 = wave-local LDS transpose, 2 = lean)
-DEFAULT_FRAMED_KERNEL = 2
 
 
 def lib():
@@ -35,6 +29,9 @@ def lib():
             raise RuntimeError(
                 "libxdrgpu.so is not built (run `python -c 'import __graft_entry__ as g; g.build()'`)")
         _LIB = abi.bind(ctypes.CDLL(LIB_PATH))
+        # not in include/xdrg.h: per-context kernel choices (xdrg_internal.h Tuning)
+        _LIB.xdrg_internal_tune.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong]
+        _LIB.xdrg_internal_tune.restype = ctypes.c_int
         v = _LIB.xdrg_abi_version()
         if v != abi.ABI_VERSION:
             raise RuntimeError(f"libxdrgpu.so ABI {v} != {abi.ABI_VERSION}")
@@ -246,6 +243,14 @@ class Context:
         if rc not in (abi.OK, abi.E_INCOMPLETE):
             _raise(rc, self._h)
         return nm.value, used.value
+
+    def tune(self, key, value=0):
+        """Force one of this context's kernel choices (xdrg_internal.h Tuning:
+        the parity tests run every production path; key 0 restores the
+        defaults).  Not part of the drop-in boundary."""
+        rc = lib().xdrg_internal_tune(self._h, int(key), int(value))
+        if rc:
+            raise ValueError(f"tuning key {key} = {value} rejected")
 
     def kernel_stats(self, kernel):
         """-> (launches, total_ms) for one XDRG_KERNEL_* id (needs timing=True)."""

@@ -2,6 +2,7 @@
 // C++ host mirror (include/xdrg_host.hpp) with the HIP engine behind it.
 // Each case names the reference test it follows (paths under /root/reference/
 // oncrpc4j-core/src/test/java/org/dcache/oncrpc4j/).  Needs a GPU.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -261,6 +262,65 @@ int main() {
         enc.beginEncoding(); enc.xdrEncodeInt(1); enc.endEncoding();
         enc.beginEncoding();
         EXPECT(throws<std::logic_error>([&] { enc.xdrEncodeLong(2); }));
+    });
+
+    // XdrTest.testGetBytes (ctest/xdr/XdrTest.java:360-376): bool true + long 17
+    // -> 12 bytes; getBytes while encoding -> IllegalStateException.
+    run("getBytes / asBuffer per message, IllegalStateException while in use", [&] {
+        BatchXdrEncoder enc(e);
+        for (int i = 0; i < 3; ++i) {
+            enc.beginEncoding();
+            enc.xdrEncodeBoolean(true);
+            enc.xdrEncodeLong(17 + i);
+            enc.endEncoding();
+        }
+        const auto all = enc.flush();
+        EXPECT(enc.messages() == 3 && all.size() == 36);
+        EXPECT(enc.getBytes(0) == hex("00000001" "0000000000000011"));
+        EXPECT(enc.getBytes(2) == hex("00000001" "0000000000000013"));
+        const BufferView v = enc.asBuffer(1);
+        EXPECT(v.size == 12 && std::memcmp(v.data, all.data() + 12, 12) == 0);
+        enc.beginEncoding();
+        EXPECT(throws<std::logic_error>([&] { (void)enc.getBytes(0); }));
+        enc.xdrEncodeBoolean(false);
+        enc.xdrEncodeLong(0);
+        enc.endEncoding();
+        EXPECT(enc.getBytes(0).size() == 12);   // not in use again: the last flushed batch
+        EXPECT(throws<std::out_of_range>([&] { (void)enc.getBytes(3); }));
+    });
+    // Xdr.ensureCapacity growth (Xdr.java:1020-1026) through the engine's
+    // capacity report: a 1 KiB initial buffer grows once to fit the batch.
+    run("flush grows the host buffer by the reference policy", [&] {
+        BatchXdrEncoder enc(e);
+        const std::vector<uint8_t> blob(3000, 0x5a);
+        for (int i = 0; i < 5; ++i) {
+            enc.beginEncoding();
+            enc.xdrEncodeInt(i);
+            enc.xdrEncodeDynamicOpaque(blob);
+            enc.endEncoding();
+        }
+        const size_t need = 5 * (4 + 4 + 3000);
+        const auto out = enc.flush();
+        EXPECT(out.size() == need);
+        const size_t want_cap = std::max<size_t>(XdrBuffer::kInitialSize * 3 / 2 + 1, XdrBuffer::kInitialSize + need);
+        EXPECT(enc.buffer().capacity() == want_cap);
+        EXPECT(enc.buffer().remaining() == need && enc.buffer().bytes() == out);
+    });
+    // Xdr.hasMoreData (Xdr.java:152-154) while a record's fields are replayed
+    run("hasMoreData over a record's fields", [&] {
+        BatchXdrEncoder enc(e);
+        enc.beginEncoding(); enc.xdrEncodeInt(7); enc.xdrEncodeString(std::string("ab")); enc.endEncoding();
+        std::vector<uint64_t> offs;
+        const auto bytes = enc.flush(false, &offs);
+        BatchXdrDecoder dec(e, {{XDRG_T_INT, XDRG_K_SCALAR, 0, 0}, {XDRG_T_STRING, XDRG_K_DYNAMIC, 0, 0}});
+        dec.load(bytes, 1, offs);
+        EXPECT(!dec.hasMoreData());
+        dec.beginDecoding();
+        EXPECT(dec.hasMoreData());
+        EXPECT(dec.xdrDecodeInt() == 7);
+        EXPECT(dec.hasMoreData());
+        EXPECT(dec.xdrDecodeString() == "ab");
+        EXPECT(!dec.hasMoreData());
     });
 
     if (g_fail) {

@@ -44,23 +44,11 @@ SCHEMAS = {
 REC_KERNELS = {"group": 0, "lane": 3, "staged": 4}
 
 
-def _tune(key, value):
-    import ctypes
-    L = engine.lib()
-    L.xdrg_internal_tune.argtypes = [ctypes.c_int, ctypes.c_longlong]
-    L.xdrg_internal_tune.restype = ctypes.c_int
-    assert L.xdrg_internal_tune(key, value) == 0
-
-
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
-def rec_kernel(request):
-    import ctypes
-    L = engine.lib()
-    L.xdrg_internal_tune.argtypes = [ctypes.c_int, ctypes.c_longlong]
-    L.xdrg_internal_tune.restype = ctypes.c_int
-    assert L.xdrg_internal_tune(9, REC_KERNELS[request.param]) == 0
+def rec_kernel(request, gpu_ctx):
+    gpu_ctx.tune(9, REC_KERNELS[request.param])
     yield request.param
-    L.xdrg_internal_tune(9, engine.DEFAULT_REC_KERNEL)
+    gpu_ctx.tune(0)
 
 
 # ---- helpers ----------------------------------------------------------------
@@ -164,17 +152,17 @@ AOS_EXTRA = {"float_words": [(F, SC, 0), (I, SC, 0), (O, FX, 4)] * 2,
              "one_word": [(I, SC, 0)], "wide_words": [(I, FX, 37)]}
 
 
-FRAMED_KERNELS = {"direct": 0, "lds": 1, "lean": 2}
+FRAMED_KERNELS = {"lds": 1, "lean": 2}
 
 
 @pytest.fixture(params=sorted(FRAMED_KERNELS))
-def framed_kernel(request):
-    """Record-marked streaming kernels (kernels_fixed.hip, tuning key 14):
-    direct 4-aligned windows, the wave-local LDS transpose, or the lean
-    variant (wave-uniform divmod, no op table for plain int words)."""
-    _tune(14, FRAMED_KERNELS[request.param])
+def framed_kernel(request, gpu_ctx):
+    """Record-marked streaming decode kernels (kernels_fixed.hip, tuning key
+    14): the wave-local LDS transpose (records under 3 words always take it)
+    or the lean kernels (wave-uniform divmod, no op table for plain int words)."""
+    gpu_ctx.tune(14, FRAMED_KERNELS[request.param])
     yield request.param
-    _tune(14, engine.DEFAULT_FRAMED_KERNEL)
+    gpu_ctx.tune(0)
 
 
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
@@ -287,9 +275,9 @@ def test_staged_tile_sizes(gpu_ctx, name, framed, tile):
     hb = random_batch(fields, n, seed=zlib.crc32(f"tile/{name}/{framed}/{tile}".encode()), dyn_len=(0, 3000))
     rc, want, want_offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total(framed) + 8, framed=framed)
     assert rc == 0
-    _tune(9, 4)
-    _tune(12, tile)
-    _tune(13, 0)   # every block staged (no split of large-record blocks to the group kernel)
+    gpu_ctx.tune(9, 4)
+    gpu_ctx.tune(12, tile)
+    gpu_ctx.tune(13, 0)   # every block staged (no split of large-record blocks to the group kernel)
     try:
         xdr, offs = gpu_encode(gpu_ctx, fields, hb, framed)
         assert xdr == want
@@ -300,9 +288,7 @@ def test_staged_tile_sizes(gpu_ctx, name, framed, tile):
         assert g[:3] == o[:3] == (0, n, 0)
         assert g[3].equal(o[3])
     finally:
-        _tune(12, 16384)
-        _tune(13, 1024)
-        _tune(9, engine.DEFAULT_REC_KERNEL)
+        gpu_ctx.tune(0)
 
 
 def test_decode_capacity(gpu_ctx, rec_kernel):
@@ -411,13 +397,14 @@ def test_cfg2_full_size_roundtrip(gpu_ctx):
 
 
 # ---- big records (blocks averaging >= 1 KiB: the group kernels) and mixed blocks
-@pytest.fixture(params=[3, 1, 2, 0], ids=["pay_wave_nt", "pay_wave", "pay_block", "pay_off"])
-def payload(request):
+@pytest.fixture(params=[1, 0], ids=["pay_wave_nt", "pay_off"])
+def payload(request, gpu_ctx):
     """Payload kernels for a single dynamic byte field on the group kernels'
-    blocks (kernels_rec.hip k_enc/dec_payload, tuning key 18)."""
-    _tune(18, request.param)
+    blocks (kernels_rec.hip k_enc/dec_payload, tuning key 18), or the group
+    kernels moving it in place."""
+    gpu_ctx.tune(18, request.param)
     yield request.param
-    _tune(18, 3)
+    gpu_ctx.tune(18, 1)
 
 
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
@@ -467,7 +454,7 @@ def test_words_lane(gpu_ctx, lane_kernel, framed, name, fields):
     """Struct-of-arrays and padded-stride columns of 4-byte words, raw and
     record-marked: bytes and values against the oracle, a cut stream and a
     corrupted mark against the oracle's first error."""
-    _tune(16, lane_kernel)
+    gpu_ctx.tune(16, lane_kernel)
     try:
         n = 70001
         hb = random_batch(fields, n, seed=zlib.crc32(f"lane/{name}/{framed}".encode()), special_floats=False)
@@ -512,7 +499,7 @@ def test_words_lane(gpu_ctx, lane_kernel, framed, name, fields):
             g = gpu_decode(gpu_ctx, fields, bytes(bad), n, None, {}, True, use_offsets=False)
             assert g[:3] == oracle_decode(fields, bytes(bad), n, None, {}, True)[:3] == (abi.E_FRAME, n // 2, abi.E_FRAME)
     finally:
-        _tune(16, 2)
+        gpu_ctx.tune(16, 2)
 
 
 @pytest.mark.parametrize("shift", [0, 1, 2, 3])

@@ -43,10 +43,7 @@ def main():
     cin, cout = cols(cols_in), cols(cols_out)
     ctx = engine.Context(0, timing=True)
     if args.lane_kernel is not None:
-        import ctypes
-        L = engine.lib()
-        L.xdrg_internal_tune.argtypes = [ctypes.c_int, ctypes.c_longlong]
-        assert L.xdrg_internal_tune(16, args.lane_kernel) == 0
+        ctx.tune(16, args.lane_kernel)
     ctx.set_stream(torch.cuda.current_stream())
     ctx.encode(sch, cin, n, xdr, xdr.numel(), framed=args.framed, async_=True)
     ctx.decode(sch, xdr, xdr.numel(), n, cout, framed=args.framed, async_=True)

@@ -8,7 +8,6 @@ line per variant and kernel class: median ms over rounds.
 
   CONFIGS=3,4 ROUNDS=5 python tools/sweep_rec.py
 """
-import ctypes
 import json
 import os
 import statistics
@@ -22,8 +21,6 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from oncrpc4j_amd import abi, engine  # noqa: E402
 
-# kernels_rec.hip defaults (set_rec_tuning)
-DEFAULTS = {9: engine.DEFAULT_REC_KERNEL, 4: 2, 5: 2, 10: 1, 11: 1, 7: 32, 8: 32, 12: 16384, 13: 1024}
 
 VARIANTS = {
     3: [(f"u{u}r{r}", {4: u, 5: u, 10: r, 11: r}) for u in (1, 2, 4) for r in (1, 2)],
@@ -34,23 +31,21 @@ VARIANTS = {
 
 
 def run(cfg, variants, rounds):
-    L = engine.lib()
-    L.xdrg_internal_tune.argtypes = [ctypes.c_int, ctypes.c_longlong]
-    L.xdrg_internal_tune.restype = ctypes.c_int
     n = {3: 16 << 20, 4: 32 << 20}[cfg]
-    wl = bench.Workload(cfg, n, False, 0)
     ctx = engine.Context(0, timing=True)
     ctx.set_stream(torch.cuda.current_stream())
+    wl = bench.Workload(ctx, cfg, n, False)
     res = {}
     try:
         for r in range(rounds):
             for name, knobs in variants:
-                for k, v in {**DEFAULTS, **knobs}.items():
-                    assert L.xdrg_internal_tune(k, v) == 0, (k, v)
+                ctx.tune(0)   # the defaults (xdrg_internal.h Tuning), then this variant's knobs
+                for k, v in knobs.items():
+                    ctx.tune(k, v)
                 if r == 0:
                     wl.clear_outputs()
                 ctx.reset_stats()
-                wl.step(ctx)
+                wl.step()
                 torch.cuda.synchronize()
                 if r == 0:
                     wl.check()
@@ -59,8 +54,7 @@ def run(cfg, variants, rounds):
                     c, ms = ctx.kernel_stats(kid)
                     res.setdefault((name, kn), []).append(ms)
     finally:
-        for k, v in DEFAULTS.items():
-            L.xdrg_internal_tune(k, v)
+        ctx.tune(0)
     per_launch = wl.native_bytes + wl.xlen
     for (name, kn), t in sorted(res.items()):
         med = statistics.median(t)
