@@ -583,6 +583,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_wave(const RecArgs a)
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
 typedef uint32_t u32u __attribute__((aligned(1)));
+typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));   // 16-byte aligned
 
 __device__ __forceinline__ bool is_word4(const VField &f) {
     return f.type == XDRG_T_INT || f.type == XDRG_T_UINT || f.type == XDRG_T_ENUM ||
@@ -1438,7 +1439,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
 __device__ __forceinline__ bool payload_block(const RecArgs &a, uint64_t r, bool decode) {
     return !a.big_rec || block_is_big_at(a, r / kRecPerBlock, decode);
 }
-template <uint32_t LPR, bool NT>
+template <uint32_t LPR, bool NT, bool NTS = NT>
 __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
     // (the checks first: hoisting the metadata loads above them measured ~1 ms
     // slower here, while it gains ~0.9 ms in dec_payload_rec)
@@ -1450,38 +1451,63 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
     const uint32_t lane = threadIdx.x % LPR;
     if (lane == 0) *(uint32_t *)dst = bswap32r((uint32_t)cnt);
     dst += 4;
-    const uint64_t nch = (cnt + 15) >> 4;
-    for (uint64_t c0 = lane; c0 < nch; c0 += 4 * LPR) {
+    // Output-aligned chunks: chunk c covers stream bytes [A + 16c, A + 16c + 16)
+    // with A = dst rounded down to 16, so every full chunk is one aligned
+    // 16-byte store (the stream offset of a payload is 4-aligned only: in a
+    // 4124-byte configs[2] record it sits 12 bytes off) and its source is a
+    // 4-aligned load.  The head chunk (shared with the length word) and the
+    // tail chunk (shared with the next record) go out as dwords, zero pad
+    // included (Xdr.java:776-781), by two lanes in the same pass as the full
+    // chunks' loads and stores.
+    const uint32_t sh = (uint32_t)((uintptr_t)dst & 15);
+    uint8_t *const A = dst - sh;
+    const uint64_t P = cnt + pad4(cnt);
+    const uint64_t cf = sh ? 1 : 0;                    // full chunks: [cf, cl)
+    const uint64_t cl = (sh + cnt) >> 4;
+    const uint64_t nch = (sh + P + 15) >> 4;
+    int64_t pc = -1;                                   // this lane's partial chunk
+    if (lane == LPR - 1 && sh) pc = 0;
+    if (lane == LPR - 2 && nch > cl && !(sh && cl == 0)) pc = (int64_t)cl;
+    uint32_t pw[4] = {0, 0, 0, 0};
+    if (pc >= 0) {
+        for (uint32_t i = 0; i < 4; ++i) {
+            const int64_t b = 16 * pc + 4 * i - (int64_t)sh;
+            if (b < 0 || (uint64_t)b >= P) continue;
+            const uint64_t k = cnt > (uint64_t)b ? cnt - (uint64_t)b : 0;
+            pw[i] = k >= 4 ? *(const u32u *)(src + b) : load_bytes(src + b, (uint32_t)k);
+        }
+    }
+    for (uint64_t c0 = cf + lane; c0 < cl || pc >= 0; c0 += 4 * LPR) {
         u32x4a v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {   // full chunks: all loads in flight first
             const uint64_t c = c0 + LPR * u;
-            if (16 * c + 16 <= cnt)
-                v[u] = NT ? __builtin_nontemporal_load((const u32x4u *)(src + 16 * c)) : *(const u32x4u *)(src + 16 * c);
+            if (c < cl) {
+                const u32x4a *p = (const u32x4a *)(src + 16 * c - sh);   // 4-aligned
+                v[u] = NT ? __builtin_nontemporal_load(p) : *p;
+            }
+        }
+        if (pc >= 0) {
+            for (uint32_t i = 0; i < 4; ++i) {
+                const int64_t b = 16 * pc + 4 * i - (int64_t)sh;
+                if (b >= 0 && (uint64_t)b < P) *(uint32_t *)(dst + b) = pw[i];
+            }
+            pc = -1;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint64_t c = c0 + LPR * u;
-            if (c >= nch) continue;
-            if (16 * c + 16 <= cnt) {
-                if (NT) __builtin_nontemporal_store(v[u], (u32x4a *)(dst + 16 * c));
-                else *(u32x4a *)(dst + 16 * c) = v[u];
-                continue;
-            }
-            for (uint32_t i = 0; i < 4; ++i) {   // last chunk: words up to the zero-padded end
-                const uint64_t b = 16 * c + 4 * i;
-                if (b >= cnt) break;
-                const uint64_t k = cnt - b;
-                *(uint32_t *)(dst + b) = k >= 4 ? *(const u32u *)(src + b) : load_bytes(src + b, (uint32_t)k);
-            }
+            if (c >= cl) continue;
+            if (NTS) __builtin_nontemporal_store(v[u], (u32x4n *)(A + 16 * c));
+            else *(u32x4n *)(A + 16 * c) = v[u];
         }
     }
 }
-template <uint32_t LPR, bool NT>   // lanes per record: 64 (a wave) or 256 (the block); grid-strided; NT: nontemporal
+template <uint32_t LPR, bool NT, bool NTS = NT>   // lanes per record; grid-strided; NT: nontemporal loads, NTS: stores
 __global__ __launch_bounds__(256) void k_enc_payload(const RecArgs a) {
     const uint64_t step = (uint64_t)gridDim.x * (256 / LPR);
     for (uint64_t r = (uint64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; r < a.n; r += step)
-        enc_payload_rec<LPR, NT>(a, r);
+        enc_payload_rec<LPR, NT, NTS>(a, r);
 }
 template <uint32_t LPR, bool NT>
 __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
@@ -1844,7 +1870,6 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
 // whole block straight between global buffers (enc/dec_record_block).
 // ===========================================================================
 constexpr uint32_t kStageSlack = 64;           // LDS bytes a chunk window may read past the tile
-typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));   // 16-byte aligned
 
 __host__ __device__ inline bool stage_type(uint32_t type, uint32_t xsz) {
     return xsz == 1 || type == XDRG_T_INT || type == XDRG_T_UINT || type == XDRG_T_ENUM || type == XDRG_T_FLOAT;
