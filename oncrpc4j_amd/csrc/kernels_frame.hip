@@ -6,27 +6,37 @@
 // `size` bytes remain; assembleXdr :109-140 concatenates the fragment
 // bodies; handleRead :44-61 repeats on the remainder.
 //
-// The marks form a linked list (mark at p -> next mark at p + 4 + size), so
-// the walk is a dependent chain.  On the GPU it becomes list ranking over
-// every 4-byte position of the stream (fragment sizes are multiples of 4 in
-// XDR traffic; a stream whose real chain meets another size falls back to
-// the exact serial walk):
-//   L1  k_frame_l1     per 16 KiB chunk, in LDS: every word position's exit =
-//                      first chain position at or past the chunk end (12
-//                      rounds of pointer jumping).
-//   L2  k_frame_l2 x6  per 1 MiB super-chunk, in HBM: pointer doubling of the
-//                      L1 exits (a hop crosses >= 1 chunk, so 6 rounds).
-//   L3  k_frame_fix    one lane hops super-chunk to super-chunk from offset 0
-//                      (<= len / 1 MiB dependent loads), k_frame_entries one
-//                      lane per super-chunk hops its chunks (<= 64), giving
-//                      every chunk's true entry; k_frame_count/emit walk each
-//                      chunk's own marks in parallel.
-// Fragments are then grouped into messages with two scans (rocPRIM) and the
-// bodies copied out by k_frame_copy.
-#include <cstring>
-
+// The marks form a chain (mark at word q -> next mark at q + 1 + size / 4),
+// so the walk is a dependent chain; every word of the stream may be the one
+// the chain enters a region at, so a region's "exit" (the first chain word
+// at or past its end) is computed for every word.  Fragment sizes of XDR
+// traffic are multiples of 4; a stream whose real chain meets another size
+// is walked serially (k_fr_serial), with the same result.
+//
+//   k_fr_exits  block per super-chunk (64 sub-chunks of 4096 words), sub-
+//               chunks from last to first: stage the words, point every word
+//               at its next mark, resolve pointers into later sub-chunks
+//               through their finished exits (LDS for the next one, HBM
+//               beyond), pointer-jump the pointers that stay inside (active
+//               words only) -> exitS[q] = first chain word at or past the
+//               super-chunk end.  One read of the stream, one write of exitS.
+//   k_fr_fix    one wave hops super-chunk to super-chunk from word 0 through
+//               exitS, from windows of the super-chunks' first words staged
+//               in LDS 64 at a time -> each super-chunk's true entry.
+//   k_fr_mark   block per super-chunk, sub-chunks first to last from its
+//               entry: stage, mark the chain by pointer doubling (round r
+//               marks the successors 2^r hops on, so round r covers hops
+//               < 2^(r+1)), count complete fragments and LAST flags, keep the
+//               two bitmaps and the in-super prefixes.
+//   k_fr_bases  one block: super-chunk prefixes, the last complete message.
+//   k_fr_emit   block per sub-chunk: message offsets (stream or payload
+//               coordinates) and, for xdrg_deframe, the fragment list.
+//   k_fr_copy   fragment bodies into the payload (marks stripped).
+// Chain fragments tile the stream from offset 0, so the payload offset of
+// fragment f at stream offset p is p - 4 f and its body size is the gap to
+// the next fragment minus 4: no scan over sizes is needed.
+// Word positions are 32-bit (streams < 16 GiB - 2 MiB, kFMaxLen).
 #include <hip/hip_runtime.h>
-#include <rocprim/rocprim.hpp>
 
 #include "xdrg_internal.h"
 
@@ -34,189 +44,543 @@ namespace xdrg {
 
 __device__ __forceinline__ uint32_t fr_bswap(uint32_t x) { return __builtin_bswap32(x); }
 
-// Next chain word index after the mark at word q (q < Q = len / 4), or a
-// terminal: kFStop (fragment not fully received), kFUnal (size % 4 != 0).
-__device__ __forceinline__ uint32_t frag_next(const uint32_t *w, uint64_t len, uint64_t q) {
-    const uint64_t p = 4 * q;
-    const uint32_t m = fr_bswap(w[q]);
-    const uint64_t size = m & kSizeMask;
-    if (size > len - p - 4) return kFStop;   // RpcMessageParserTCP.java:77-79
+// Next chain word after the mark m at word q < Q, or a terminal: kFStop
+// (fragment not fully received: size > remaining - 4, RpcMessageParserTCP.java
+// :77-79), kFUnal (size % 4 != 0).  The stream is 4Q + tb bytes (tb < 4).
+__device__ __forceinline__ uint32_t fr_next(uint32_t m, uint32_t q, uint32_t Q, uint32_t tb) {
+    const uint32_t size = m & kSizeMask;
+    const uint32_t R = Q - q;   // whole words left, >= 1
+    const bool fits = R >= (1u << 30) || size + 4 <= 4 * R + tb;
+    if (!fits) return kFStop;
     if (size & 3) return kFUnal;
-    return (uint32_t)((p + 4 + size) >> 2);
+    return q + 1 + (size >> 2);
 }
 
-// L1: exit of every word position of one chunk.
-__global__ __launch_bounds__(256) void k_frame_l1(const uint32_t *w, uint64_t len, uint64_t Q,
-                                                   uint32_t *exit1, uint32_t *exit2) {
-    __shared__ uint32_t J[kFChunk];
-    const uint64_t c0 = (uint64_t)blockIdx.x * kFChunk;
-    const uint64_t c1 = c0 + kFChunk;
-    for (uint32_t i = threadIdx.x; i < kFChunk; i += blockDim.x) {
-        const uint64_t q = c0 + i;
-        J[i] = q < Q ? frag_next(w, len, q) : kFStop;
-    }
-    __syncthreads();
-    for (int round = 0; round < kFChunkLog2; ++round) {   // chains inside a chunk have <= kFChunk hops
-        uint32_t v[kFChunk / 256];
+typedef uint32_t u32x4f __attribute__((ext_vector_type(4)));
+
+// The 16 words of sub-chunk `base` a thread owns: word 4*tid + 1024*k + c
+// (k, c < 4), as four 16-byte loads (a tail reads dword by dword, 0 past Q).
+__device__ __forceinline__ void fr_load16(const uint32_t *w, uint32_t Q, uint32_t base, uint32_t tid, uint32_t (&x)[16]) {
 #pragma unroll
-        for (int k = 0; k < kFChunk / 256; ++k) {
-            const uint32_t j = J[threadIdx.x + 256 * k];
-            v[k] = (j >= c0 && j < c1) ? J[j - c0] : j;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t q = base + 4 * tid + 1024 * k;
+        if (q + 4 <= Q) {
+            const u32x4f v = __builtin_nontemporal_load((const u32x4f *)(w + q));
+            x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) x[4 * k + c] = q + c < Q ? w[q + c] : 0u;
         }
-        __syncthreads();
+    }
+}
+__device__ __forceinline__ uint32_t fr_li(uint32_t tid, int i) { return 4 * tid + 1024 * (i >> 2) + (i & 3); }
+
+// Append this thread's flagged positions (mask bit i = position fr_li(tid, i))
+// to the block's list: a wave prefix of the counts, one LDS atomic per wave.
+__device__ __forceinline__ void fr_append16(uint32_t mask, uint32_t tid, uint16_t *list, uint32_t *count) {
+    const uint32_t lane = tid & 63;
+    const uint32_t c = __popc(mask);
+    uint32_t inc = c;   // inclusive wave scan
 #pragma unroll
-        for (int k = 0; k < kFChunk / 256; ++k) J[threadIdx.x + 256 * k] = v[k];
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += o;
+    }
+    const uint32_t tot = __shfl(inc, 63, 64);
+    uint32_t wbase = 0;
+    if (lane == 63 && tot) wbase = atomicAdd(count, tot);
+    wbase = __shfl(wbase, 63, 64);
+    uint32_t at = wbase + inc - c;
+    for (uint32_t m = mask; m; m &= m - 1) list[at++] = (uint16_t)fr_li(tid, __ffs(m) - 1);
+}
+
+// ---------------------------------------------------------------------------
+// k_fr_exits
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
+                                                   uint32_t *exitS) {
+    __shared__ __attribute__((aligned(16))) uint32_t J[2][kFChunk];
+    __shared__ uint16_t act[kFChunk];
+    __shared__ uint32_t nact;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t sbeg = blockIdx.x * kFSuper;
+    const uint32_t send = min(sbeg + kFSuper, Q);
+    const uint32_t sfin = sbeg + kFSuper;   // exits are chain words >= sfin (or == Q)
+    const uint32_t nsub = (send - sbeg + kFChunk - 1) / kFChunk;
+    uint32_t x[16], y[16];
+    fr_load16(w, Q, sbeg + (nsub - 1) * kFChunk, tid, x);
+    int cur = 0;
+    for (int j = (int)nsub - 1; j >= 0; --j) {
+        const uint32_t base = sbeg + (uint32_t)j * kFChunk;
+        const uint32_t bend = base + kFChunk;
+        if (j > 0) fr_load16(w, Q, base - kFChunk, tid, y);   // next sub-chunk's words in flight
+        uint32_t *Jc = J[cur];
+        const uint32_t *Jp = J[cur ^ 1];                       // exits of sub-chunk j + 1
+        if (tid == 0) nact = 0;
         __syncthreads();
-    }
-    for (uint32_t i = threadIdx.x; i < kFChunk; i += blockDim.x) {
-        const uint64_t q = c0 + i;
-        if (q < Q) { exit1[q] = J[i]; exit2[q] = J[i]; }
-    }
-}
-
-// L2: one doubling round of the super-chunk exits (in place: a value read
-// early is still a successor on the same chain, so rounds only get faster).
-__global__ __launch_bounds__(256) void k_frame_l2(uint32_t *exit2, uint64_t Q) {
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= Q) return;
-    const uint32_t v = exit2[q];
-    if (v < Q && v / kFSuper == q / kFSuper) exit2[q] = exit2[v];
-}
-
-// L3a: super-chunk entries along the real chain from offset 0.
-__global__ void k_frame_fix(const uint32_t *exit2, uint64_t Q, uint32_t *sentry, uint64_t *res) {
-    if (threadIdx.x || blockIdx.x) return;
-    uint64_t e = 0;
-    while (e < Q) {
-        sentry[e / kFSuper] = (uint32_t)e;
-        e = exit2[e];
-    }
-    res[0] = e;   // >= Q: ran to the end; kFStop / kFUnal: terminal met on the real chain
-}
-
-// L3b: chunk entries inside each super-chunk.
-__global__ void k_frame_entries(const uint32_t *exit1, uint64_t Q, uint64_t nsuper, const uint32_t *sentry,
-                                uint32_t *centry) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nsuper || sentry[s] == kFNone) return;
-    uint64_t e = sentry[s];
-    while (e < Q && e / kFSuper == s) {
-        centry[e / kFChunk] = (uint32_t)e;
-        e = exit1[e];
-    }
-}
-
-// Walk the real chain inside chunk c: count (emit == false) or write the
-// complete fragments (word index, raw mark).
-template <bool kEmit>
-__global__ void k_frame_walk(const uint32_t *w, uint64_t len, uint64_t Q, uint64_t nchunks,
-                             const uint32_t *centry, uint32_t *counts, const uint32_t *base,
-                             uint64_t *frag_pos, uint32_t *frag_mark) {
-    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nchunks) return;
-    uint32_t n = 0;
-    const uint32_t e = centry[c];
-    if (e != kFNone) {
-        const uint64_t c1 = (c + 1) * kFChunk;
-        uint64_t q = e;
-        const uint32_t b = kEmit ? base[c] : 0;
-        while (q < Q && q < c1) {
-            const uint32_t nx = frag_next(w, len, q);
-            if (nx == kFStop || nx == kFUnal) break;
-            if (kEmit) {
-                frag_pos[b + n] = 4 * q;
-                frag_mark[b + n] = fr_bswap(w[q]);
+        uint32_t t[16], mask = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t q = base + fr_li(tid, i);
+            uint32_t v = kFStop;
+            if (q < Q) {
+                v = fr_next(fr_bswap(x[i]), q, Q, tb);
+                if (v < sfin && v < Q) {   // a word (terminals are >= kFUnal > sfin)
+                    if (v >= bend) v = v < bend + kFChunk ? Jp[v - bend] : exitS[v];   // final exits
+                    else mask |= 1u << i;
+                }
             }
-            ++n;
-            q = nx;
+            t[i] = v;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            *(u32x4f *)&Jc[4 * tid + 1024 * k] = u32x4f{t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
+        fr_append16(mask, tid, act, &nact);
+        __syncthreads();
+        // pointer jumping over the words whose pointer stays inside (in place:
+        // a value read early is still a successor on the same chain)
+        const uint32_t na = nact;
+        for (;;) {
+            int mv = 0;
+            for (uint32_t a = tid; a < na; a += 256) {
+                const uint32_t li = act[a];
+                const uint32_t v = Jc[li];
+                if (v - base < kFChunk) {
+                    const uint32_t u = Jc[v - base];
+                    Jc[li] = u;
+                    mv |= u - base < kFChunk;
+                }
+            }
+            if (!__syncthreads_or(mv)) break;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t l0 = 4 * tid + 1024 * k;
+            const u32x4f v = *(const u32x4f *)&Jc[l0];
+            if (base + l0 + 4 <= Q) {
+                *(u32x4f *)(exitS + base + l0) = v;
+            } else {
+                if (base + l0 < Q) exitS[base + l0] = v.x;
+                if (base + l0 + 1 < Q) exitS[base + l0 + 1] = v.y;
+                if (base + l0 + 2 < Q) exitS[base + l0 + 2] = v.z;
+            }
+        }
+        cur ^= 1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = y[i];
+        __syncthreads();   // exitS of this sub-chunk visible to the block's later gathers
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fr_fix: super-chunk entries along the real chain from word 0.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kFixWin = 64;   // words per super-chunk window
+constexpr uint32_t kFixBatch = 64; // super-chunks per staged batch
+__global__ __launch_bounds__(64) void k_fr_fix(const uint32_t *exitS, uint64_t Q, uint64_t nsup,
+                                               uint32_t *sentry, uint64_t *res) {
+    __shared__ uint32_t win[kFixBatch][kFixWin];
+    const uint32_t lane = threadIdx.x;
+    uint64_t e = 0, b0 = ~0ull;
+    while (e < Q) {
+        const uint64_t s = e / kFSuper;
+        if (b0 == ~0ull || s >= b0 + kFixBatch) {   // stage windows of super-chunks [s, s + 64)
+            b0 = s;
+            uint32_t v[kFixBatch];
+#pragma unroll
+            for (uint32_t k = 0; k < kFixBatch; ++k) {   // every load in flight before the LDS writes
+                const uint64_t q = (b0 + k) * kFSuper + lane;
+                v[k] = exitS[q < Q ? q : Q - 1];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kFixBatch; ++k) {
+                const uint64_t q = (b0 + k) * kFSuper + lane;
+                win[k][lane] = (b0 + k < nsup && q < Q) ? v[k] : kFStop;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (lane == 0) sentry[s] = (uint32_t)e;
+        const uint64_t d = e - s * kFSuper;
+        const uint32_t t = d < kFixWin ? win[s - b0][d] : exitS[e];   // a deep entry: one HBM load
+        e = t;
+        if (t >= kFUnal) break;
+    }
+    if (lane == 0) res[0] = e;   // >= Q: ran to the end; kFStop / kFUnal: terminal met on the real chain
+}
+
+// ---------------------------------------------------------------------------
+// k_fr_mark: per sub-chunk bitmaps of the complete chain fragments and their
+// LAST flags, counts and in-super prefixes.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fr_mark(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
+                                                  const uint32_t *sentry, const uint64_t *res, FrameSub *sub,
+                                                  uint32_t *fbits, uint32_t *lbits, FrameSuper *sup) {
+    __shared__ __attribute__((aligned(16))) uint32_t J[2][kFChunk];
+    __shared__ __attribute__((aligned(16))) uint8_t on[kFChunk];
+    __shared__ __attribute__((aligned(16))) uint8_t fl[kFChunk];   // bit 0: complete fragment, bit 1: LAST
+    __shared__ uint16_t act[kFChunk];
+    __shared__ uint32_t fbw[kFChunk / 32], lbw[kFChunk / 32];
+    __shared__ uint32_t nact, red[3][4];
+    __shared__ uint32_t e_next, lastpos;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t s = blockIdx.x;
+    const uint32_t sbeg = s * kFSuper;
+    const uint32_t send = min(sbeg + kFSuper, Q);
+    const uint32_t nsub = (send - sbeg + kFChunk - 1) / kFChunk;
+    const uint64_t sub0 = (uint64_t)s * (kFSuper / kFChunk);
+    uint32_t e = res[0] == kFUnal ? kFNone : sentry[s];   // kFNone: no chain word in this super-chunk
+    uint32_t pre_f = 0, pre_l = 0, tail = 2;   // tail: LAST flag of the super's last fragment (2 = none yet)
+    uint32_t lastlast = 0, has_ll = 0;         // in-super count up to and including its last LAST fragment
+    uint32_t x[16], y[16];
+    uint32_t held = ~0u;                       // sub-chunk whose words x holds
+    for (uint32_t j = 0; j < nsub; ++j) {
+        const uint32_t base = sbeg + j * kFChunk;
+        const uint32_t bend = base + kFChunk;
+        FrameSub info;
+        info.pre_frag = pre_f;
+        info.pre_last = pre_l;
+        info.prev_tail = tail;
+        info.nfrag = info.nlast = info.upto_ll = info.has_ll = info.rsv = 0;
+        if (e >= bend || e >= Q) {   // the chain skips this sub-chunk (or has ended)
+            if (tid == 0) sub[sub0 + j] = info;
+            if (tid < kFChunk / 32) { fbits[(sub0 + j) * 128 + tid] = 0; lbits[(sub0 + j) * 128 + tid] = 0; }
+            continue;
+        }
+        if (held != j) fr_load16(w, Q, base, tid, x);
+        if (j + 1 < nsub) { fr_load16(w, Q, bend, tid, y); held = j + 1; }   // next sub-chunk in flight
+        if (tid == 0) { nact = 0; e_next = kFStop; lastpos = 0; }
+        __syncthreads();
+        uint32_t t[16], mask = 0, fo[4] = {0, 0, 0, 0}, ff[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t q = base + fr_li(tid, i);
+            uint32_t v = kFStop, f = 0;
+            if (q < Q) {
+                const uint32_t m = fr_bswap(x[i]);
+                v = fr_next(m, q, Q, tb);
+                f = (v < kFUnal ? 1u : 0u) | ((m >> 31) << 1);
+                if (v < bend) mask |= 1u << i;   // v < bend < kFUnal: a word inside
+                if (q == e && (v >= kFUnal || v >= bend)) e_next = v;   // the entry itself leaves at once
+            }
+            t[i] = v;
+            ff[i >> 2] |= f << (8 * (i & 3));
+            fo[i >> 2] |= (q == e ? 1u : 0u) << (8 * (i & 3));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t l0 = 4 * tid + 1024 * k;
+            const u32x4f v{t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
+            *(u32x4f *)&J[0][l0] = v;
+            *(u32x4f *)&J[1][l0] = v;
+            *(uint32_t *)&on[l0] = fo[k];
+            *(uint32_t *)&fl[l0] = ff[k];
+        }
+        fr_append16(mask, tid, act, &nact);
+        __syncthreads();
+        // pointer doubling with marking: round r marks the nodes 2^r hops past
+        // every marked node, so after round r every chain node < 2^(r+1) hops
+        // from e is marked (double-buffered pointers: round r reads next^(2^r))
+        const uint32_t na = nact;
+        int cur = 0;
+        for (;;) {
+            int mv = 0;
+            const uint32_t *Jc = J[cur];
+            uint32_t *Jn = J[cur ^ 1];
+            for (uint32_t a = tid; a < na; a += 256) {
+                const uint32_t li = act[a];
+                const uint32_t v = Jc[li];
+                if (v - base < kFChunk) {
+                    if (on[li]) on[v - base] = 1;
+                    const uint32_t u = Jc[v - base];
+                    Jn[li] = u;
+                    mv |= u - base < kFChunk;
+                } else {
+                    Jn[li] = v;
+                }
+            }
+            cur ^= 1;
+            if (!__syncthreads_or(mv)) break;
+        }
+        // bitmaps (word k = words 32k .. 32k+31), counts, the last LAST fragment
+        uint32_t cf = 0, cl = 0;
+        if (tid < kFChunk / 32) {
+            uint32_t fb = 0, lb = 0;
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t o = *(const uint32_t *)&on[32 * tid + 4 * g];
+                const uint32_t f = *(const uint32_t *)&fl[32 * tid + 4 * g] & (o * 3u);   // only marked words
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint32_t v = (f >> (8 * c)) & 3u;
+                    fb |= (v & 1u) << (4 * g + c);
+                    lb |= ((v >> 1) & v & 1u) << (4 * g + c);
+                }
+            }
+            fbw[tid] = fb;
+            lbw[tid] = lb;
+            fbits[(sub0 + j) * 128 + tid] = fb;
+            lbits[(sub0 + j) * 128 + tid] = lb;
+            cf = __popc(fb);
+            cl = __popc(lb);
+            if (lb) atomicMax(&lastpos, 32 * tid + (31 - __clz(lb)) + 1);
+        }
+        // the chain's exit: the marked node whose own next leaves the sub-chunk
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t li = fr_li(tid, i);
+            const uint32_t q = base + li;
+            if (q < Q && q != e && on[li]) {
+                const uint32_t v = fr_next(fr_bswap(x[i]), q, Q, tb);
+                if (v >= kFUnal || v >= bend) e_next = v;
+            }
+        }
+        for (int d = 32; d > 0; d >>= 1) {
+            cf += __shfl_xor(cf, d, 64);
+            cl += __shfl_xor(cl, d, 64);
+        }
+        if (lane == 0) { red[0][wv] = cf; red[1][wv] = cl; }
+        __syncthreads();
+        const uint32_t nf = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        const uint32_t nl = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        const uint32_t lp = lastpos;
+        // fragments up to and including the last LAST one (for the incomplete-tail cut)
+        uint32_t upto = 0;
+        if (lp && tid < kFChunk / 32) {
+            const uint32_t fb = fbw[tid];
+            const uint32_t lo = 32 * tid;
+            if (lo + 32 <= lp) upto = __popc(fb);
+            else if (lo < lp) upto = __popc(fb & (0xffffffffu >> (32 - (lp - lo))));
+        }
+        for (int d = 32; d > 0; d >>= 1) upto += __shfl_xor(upto, d, 64);
+        if (lane == 0) red[2][wv] = upto;
+        // LAST flag of the last complete fragment (from the LDS bitmaps)
+        uint32_t tl = tail;
+        if (nf) {
+            for (int k = kFChunk / 32 - 1; k >= 0; --k) {
+                const uint32_t fb = fbw[k];
+                if (fb) {
+                    tl = (lbw[k] >> (31 - __clz(fb))) & 1u;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        info.nfrag = nf;
+        info.nlast = nl;
+        if (lp) {
+            info.has_ll = 1;
+            info.upto_ll = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+            has_ll = 1;
+            lastlast = pre_f + info.upto_ll;
+        }
+        tail = tl;
+        if (tid == 0) sub[sub0 + j] = info;
+        pre_f += nf;
+        pre_l += nl;
+        e = e_next;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = y[i];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        FrameSuper v;
+        v.nfrag = pre_f;
+        v.nlast = pre_l;
+        v.tail = tail;
+        v.has_ll = has_ll;
+        v.upto_ll = lastlast;
+        sup[s] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fr_bases: super-chunk exclusive prefixes (fragments, LAST flags, the LAST
+// flag of the fragment before each super-chunk) and the batch totals:
+// res[1] = complete fragments (through the last LAST one), res[4] = complete
+// messages, res[5] = fragments of the first `cap` messages (k_fr_emit lowers
+// it), res[3] = consumed stream bytes (set by k_fr_emit).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64_t nsup, FrameBase *bases,
+                                                    uint64_t *res) {
+    __shared__ uint64_t sf[1024], sl[1024];
+    __shared__ uint32_t st[1024];
+    __shared__ uint64_t carry_f, carry_l, fc;
+    __shared__ uint32_t carry_t;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) { carry_f = 0; carry_l = 0; carry_t = 1; fc = 0; }   // fragment 0 starts a message
+    __syncthreads();
+    if (res[0] == kFUnal) return;
+    for (uint64_t b = 0; b < nsup; b += 1024) {
+        const uint64_t s = b + tid;
+        FrameSuper v{};
+        if (s < nsup) v = sup[s];
+        sf[tid] = v.nfrag;
+        sl[tid] = v.nlast;
+        st[tid] = v.nfrag ? v.tail : 2u;
+        __syncthreads();
+        // inclusive Hillis-Steele scans (sums; "last non-empty tail")
+        for (uint32_t d = 1; d < 1024; d <<= 1) {
+            const uint64_t af = tid >= d ? sf[tid - d] : 0, al = tid >= d ? sl[tid - d] : 0;
+            const uint32_t at = tid >= d ? st[tid - d] : 2u;
+            __syncthreads();
+            sf[tid] += af;
+            sl[tid] += al;
+            if (st[tid] == 2u) st[tid] = at;
+            __syncthreads();
+        }
+        if (s < nsup) {
+            FrameBase o;
+            o.frag = carry_f + sf[tid] - v.nfrag;
+            o.last = carry_l + sl[tid] - v.nlast;
+            const uint32_t prev = tid ? st[tid - 1] : 2u;
+            o.prev_tail = prev != 2u ? prev : carry_t;
+            bases[s] = o;
+            if (v.has_ll) atomicMax((unsigned long long *)&fc, (unsigned long long)(o.frag + v.upto_ll));
+        }
+        __syncthreads();
+        if (tid == 0) {
+            carry_f += sf[1023];
+            carry_l += sl[1023];
+            if (st[1023] != 2u) carry_t = st[1023];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        res[1] = fc;          // complete fragments: through the last LAST fragment
+        res[4] = carry_l;     // complete messages
+        res[5] = fc;
+        res[3] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fr_emit: block (128 threads) per sub-chunk, thread t owns bitmap word t.
+// frag_pos (xdrg_deframe only): stream offset of every fragment of the first
+// `cap` messages, plus the entry after the last one (the next fragment's
+// offset, or the end of the last complete message) so k_fr_copy reads body
+// sizes as gaps.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w, uint32_t Q, const FrameSub *sub,
+                                                  const FrameBase *bases, const uint32_t *fbits,
+                                                  const uint32_t *lbits, uint64_t cap, int stream_offsets,
+                                                  uint64_t *msg_offsets, uint64_t *frag_pos, uint64_t *res) {
+    __shared__ uint32_t pf[128], pl[128], tl[128];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t k = blockIdx.x;                 // sub-chunk
+    const uint64_t s = k / (kFSuper / kFChunk);
+    if (res[0] == kFUnal || k * kFChunk >= Q) return;
+    const FrameSub info = sub[k];
+    if (!info.nfrag) return;
+    const FrameBase b = bases[s];
+    const uint64_t F = res[1], M = res[4];
+    const uint64_t fb0 = b.frag + info.pre_frag, lb0 = b.last + info.pre_last;
+    if (fb0 >= F) return;                          // past the last complete message
+    const uint32_t in_tail = info.prev_tail != 2u ? info.prev_tail : b.prev_tail;
+    const uint32_t fw = fbits[k * 128 + tid], lw = lbits[k * 128 + tid];
+    // exclusive prefixes over the block's words, and the LAST flag of the
+    // fragment before each word ("last non-empty" scan)
+    pf[tid] = __popc(fw);
+    pl[tid] = __popc(lw);
+    tl[tid] = fw ? (lw >> (31 - __clz(fw))) & 1 : 2u;
+    __syncthreads();
+    for (uint32_t d = 1; d < 128; d <<= 1) {
+        const uint32_t a = tid >= d ? pf[tid - d] : 0, c = tid >= d ? pl[tid - d] : 0;
+        const uint32_t t = tid >= d ? tl[tid - d] : 2u;
+        __syncthreads();
+        pf[tid] += a;
+        pl[tid] += c;
+        if (tl[tid] == 2u) tl[tid] = t;
+        __syncthreads();
+    }
+    uint64_t f = fb0 + pf[tid] - __popc(fw);
+    uint64_t m = lb0 + pl[tid] - __popc(lw);
+    uint32_t prev_last = tid ? (tl[tid - 1] != 2u ? tl[tid - 1] : in_tail) : in_tail;
+    const uint64_t base = k * kFChunk;
+    for (uint32_t bits = fw; bits; bits &= bits - 1) {
+        if (f >= F) break;
+        const uint32_t bt = __ffs(bits) - 1;
+        const uint64_t p = 4 * (base + 32 * tid + bt);
+        const bool last = (lw >> bt) & 1;
+        const bool first = f == 0 || prev_last;
+        if (first && m <= cap) {
+            if (m < M) msg_offsets[m] = stream_offsets ? p : p - 4 * f;   // payload: fragments tile the stream
+            if (m == cap) { res[3] = p; res[5] = f; }   // handleRead's split point (:57-60)
+        }
+        if (frag_pos && m <= cap) frag_pos[f] = p;
+        if (f + 1 == F) {   // the last LAST fragment closes the last complete message
+            const uint64_t size = fr_bswap(w[p >> 2]) & kSizeMask;
+            if (m + 1 <= cap) msg_offsets[m + 1] = stream_offsets ? p + 4 + size : p - 4 * f + size;
+            if (M <= cap) {
+                res[3] = p + 4 + size;
+                if (frag_pos) frag_pos[F] = p + 4 + size;
+            }
+        }
+        prev_last = last;
+        m += last;
+        ++f;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Exact serial walk (any fragment sizes): the fallback.  Same results as the
+// parallel path (fragment list with its end entry, message offsets).
+// ---------------------------------------------------------------------------
+__global__ void k_fr_serial(const uint8_t *in, uint64_t len, uint64_t cap, int stream_offsets,
+                            uint64_t *msg_offsets, uint64_t *frag_pos, uint64_t *res) {
+    if (threadIdx.x || blockIdx.x) return;
+    uint64_t p = 0, n = 0, F = 0, M = 0, endF = 0;
+    while (len - p >= 4) {
+        const uint32_t mk = ((uint32_t)in[p] << 24) | ((uint32_t)in[p + 1] << 16) | ((uint32_t)in[p + 2] << 8) | in[p + 3];
+        const uint64_t size = mk & kSizeMask;
+        if (size > len - p - 4) break;
+        frag_pos[n++] = p;
+        p += 4 + size;
+        if (mk & kLastFrag) { F = n; ++M; endF = p; }
+    }
+    frag_pos[n] = p;
+    // messages of the complete fragments (isAllFragmentsArrived :82-85)
+    uint64_t m = 0, body = 0, consumed = 0, fcap = F;
+    bool first = true;
+    for (uint64_t f = 0; f < F; ++f) {
+        const uint64_t pos = frag_pos[f], size = frag_pos[f + 1] - pos - 4;
+        if (first && m <= cap) {
+            if (m < M) msg_offsets[m] = stream_offsets ? pos : body;
+            if (m == cap) { consumed = pos; fcap = f; }
+        }
+        body += size;
+        const uint32_t mk = ((uint32_t)in[pos] << 24);
+        first = (mk & kLastFrag) != 0;
+        if (first) {
+            ++m;
+            if (m <= cap) msg_offsets[m] = stream_offsets ? pos + 4 + size : body;
         }
     }
-    if (!kEmit) counts[c] = n;
+    if (M <= cap) consumed = endF;
+    res[1] = F;
+    res[3] = consumed;
+    res[4] = M;
+    res[5] = fcap;
 }
 
-// Exact serial walk (any fragment sizes): the fallback.  res[0] = fragments.
-__global__ void k_frame_serial(const uint8_t *in, uint64_t len, uint64_t *frag_pos, uint32_t *frag_mark,
-                               uint64_t *res) {
-    if (threadIdx.x || blockIdx.x) return;
-    uint64_t p = 0, n = 0;
-    while (len - p >= 4) {
-        const uint32_t m = ((uint32_t)in[p] << 24) | ((uint32_t)in[p + 1] << 16) | ((uint32_t)in[p + 2] << 8) | in[p + 3];
-        const uint64_t size = m & kSizeMask;
-        if (size > len - p - 4) break;
-        frag_pos[n] = p;
-        frag_mark[n] = m;
-        ++n;
-        p += 4 + size;
-    }
-    res[0] = n;
-}
-
-// Complete fragments end with the last LAST mark: res[1] = its index + 1
-// (grid-stride max, one atomic per block).
-__global__ __launch_bounds__(256) void k_frame_lastmsg(const uint32_t *frag_mark, uint64_t nfrag,
-                                                        unsigned long long *res) {
-    __shared__ unsigned long long wmax[4];
-    unsigned long long m = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nfrag; i += (uint64_t)gridDim.x * blockDim.x)
-        if (frag_mark[i] & kLastFrag) m = i + 1;
-    for (int d = 32; d > 0; d >>= 1) {
-        const unsigned long long o = __shfl_down(m, d, 64);
-        m = o > m ? o : m;
-    }
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < 4; ++w) m = wmax[w] > m ? wmax[w] : m;
-        if (m) atomicMax(res, m);
-    }
-}
-
-// Per-fragment scan inputs: body size and last flag.
-__global__ void k_frame_prep(const uint32_t *frag_mark, uint64_t nf, uint64_t *size, uint32_t *last) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nf) return;
-    size[i] = frag_mark[i] & kSizeMask;
-    last[i] = frag_mark[i] >> 31;
-}
-
-// Message i's first fragment writes msg_offsets[i] (payload or stream
-// offset); the tail entry is the end of message `cap` (or of the last).
-// consumed[0] = stream bytes of messages < cap (handleRead's split point).
-__global__ void k_frame_msgs(const uint64_t *frag_pos, const uint32_t *frag_mark, uint64_t nf,
-                             const uint32_t *msg_id, const uint64_t *pay_off, uint64_t cap, bool stream_offsets,
-                             uint64_t *msg_offsets, uint64_t *consumed) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nf) return;
-    const bool first = i == 0 || (frag_mark[i - 1] & kLastFrag);
-    const uint64_t m = msg_id[i];
-    const uint64_t v = stream_offsets ? frag_pos[i] : pay_off[i];
-    if (first && m <= cap) msg_offsets[m] = v;
-    if (first && m == cap) consumed[0] = frag_pos[i];
-    if (i + 1 == nf && m + 1 <= cap) {   // end of the last message
-        const uint64_t sz = frag_mark[i] & kSizeMask;
-        msg_offsets[m + 1] = stream_offsets ? frag_pos[i] + 4 + sz : pay_off[i] + sz;
-        consumed[0] = frag_pos[i] + 4 + sz;
-    }
-}
-
-// A group of G lanes per fragment copies its body (G sized by the host from
-// the average fragment): 16-byte accesses (dword-aligned, so unaligned
-// vectors on gfx950) with a dword tail; byte copies on the fallback path.
-typedef uint32_t u32x4f __attribute__((ext_vector_type(4), aligned(4)));
-__global__ __launch_bounds__(256) void k_frame_copy(const uint8_t *in, const uint64_t *frag_pos,
-                                                     const uint32_t *frag_mark, const uint64_t *pay_off,
-                                                     const uint32_t *msg_id, uint64_t nf, uint64_t cap,
-                                                     uint32_t G, uint8_t *payload) {
+// A group of G lanes per fragment copies its body (the gap to the next
+// fragment minus the mark) to payload[p - 4 f): 16-byte accesses (dword-
+// aligned, so unaligned vectors on gfx950) with a dword tail; byte copies
+// when a body is not a 4-multiple (serial path).
+typedef uint32_t u32x4c __attribute__((ext_vector_type(4), aligned(4)));
+__global__ __launch_bounds__(256) void k_fr_copy(const uint8_t *in, const uint64_t *frag_pos, uint64_t nf, uint32_t G,
+                                                 uint8_t *payload) {
     const uint32_t gl = threadIdx.x & (G - 1);
     const uint64_t ngroups = (uint64_t)gridDim.x * (blockDim.x / G);
     for (uint64_t f = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; f < nf; f += ngroups) {
-        if (msg_id[f] >= cap) return;   // fragments are in message order
-        const uint8_t *src = in + frag_pos[f] + 4;
-        uint8_t *dst = payload + pay_off[f];
-        const uint64_t n = frag_mark[f] & kSizeMask;
+        const uint64_t p = frag_pos[f];
+        const uint64_t n = frag_pos[f + 1] - p - 4;
+        const uint8_t *src = in + p + 4;
+        uint8_t *dst = payload + (p - 4 * f);
         if ((((uintptr_t)src | (uintptr_t)dst | n) & 3) == 0) {
             const uint64_t nv = n >> 4;
-            for (uint64_t i = gl; i < nv; i += G) *(u32x4f *)(dst + 16 * i) = *(const u32x4f *)(src + 16 * i);
+            for (uint64_t i = gl; i < nv; i += G) *(u32x4c *)(dst + 16 * i) = *(const u32x4c *)(src + 16 * i);
             for (uint64_t i = 4 * nv + gl; i < n / 4; i += G) ((uint32_t *)dst)[i] = ((const uint32_t *)src)[i];
         } else {
             for (uint64_t i = gl; i < n; i += G) dst[i] = src[i];
@@ -225,80 +589,39 @@ __global__ __launch_bounds__(256) void k_frame_copy(const uint8_t *in, const uin
 }
 
 // ---- launchers -------------------------------------------------------------------
-static inline dim3 grid1(uint64_t n, uint32_t t) { return dim3((uint32_t)((n + t - 1) / t)); }
-
-int frame_levels(const uint8_t *in, uint64_t len, FrameWs &ws, void *stream) {
+int frame_parallel(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+                   uint64_t *msg_offsets, bool frag_list, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     const uint32_t *w = (const uint32_t *)in;
-    const uint64_t Q = len / 4, nch = (Q + kFChunk - 1) / kFChunk, nsup = (Q + kFSuper - 1) / kFSuper;
-    hipLaunchKernelGGL(k_frame_l1, dim3((uint32_t)nch), dim3(256), 0, st, w, len, Q, ws.exit1, ws.exit2);
-    for (uint32_t r = 0; r < kFSuperLog2; ++r) hipLaunchKernelGGL(k_frame_l2, grid1(Q, 256), dim3(256), 0, st, ws.exit2, Q);
+    const uint32_t Q = (uint32_t)(len / 4), tb = (uint32_t)(len & 3);
+    const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
+    hipLaunchKernelGGL(k_fr_exits, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitS);
     if (hipMemsetAsync(ws.sentry, 0xff, nsup * 4, st) != hipSuccess) return (int)hipErrorUnknown;
-    if (hipMemsetAsync(ws.centry, 0xff, nch * 4, st) != hipSuccess) return (int)hipErrorUnknown;
-    hipLaunchKernelGGL(k_frame_fix, dim3(1), dim3(64), 0, st, ws.exit2, Q, ws.sentry, ws.res);
-    hipLaunchKernelGGL(k_frame_entries, grid1(nsup, 64), dim3(64), 0, st, ws.exit1, Q, nsup, ws.sentry, ws.centry);
-    hipLaunchKernelGGL(k_frame_walk<false>, grid1(nch, 64), dim3(64), 0, st, w, len, Q, nch, ws.centry, ws.counts,
-                       nullptr, nullptr, nullptr);
-    // fragment base per chunk; res[2] = fragments
-    size_t tb = ws.tmp_bytes;
-    if (rocprim::exclusive_scan(ws.tmp, tb, ws.counts, ws.base, 0u, nch, rocprim::plus<uint32_t>(), st) != hipSuccess)
-        return (int)hipErrorUnknown;
-    hipLaunchKernelGGL(k_frame_walk<true>, grid1(nch, 64), dim3(64), 0, st, w, len, Q, nch, ws.centry, nullptr,
-                       ws.base, ws.frag_pos, ws.frag_mark);
+    hipLaunchKernelGGL(k_fr_fix, dim3(1), dim3(64), 0, st, ws.exitS, (uint64_t)Q, nsup, ws.sentry, ws.res);
+    hipLaunchKernelGGL(k_fr_mark, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.sub,
+                       ws.fbits, ws.lbits, ws.sup);
+    hipLaunchKernelGGL(k_fr_bases, dim3(1), dim3(1024), 0, st, ws.sup, nsup, ws.bases, ws.res);
+    hipLaunchKernelGGL(k_fr_emit, dim3((uint32_t)nsub), dim3(128), 0, st, w, Q, ws.sub, ws.bases, ws.fbits,
+                       ws.lbits, cap, stream_offsets ? 1 : 0, msg_offsets, frag_list ? ws.frag_pos : nullptr, ws.res);
     return (int)hipGetLastError();
 }
 
-size_t frame_scan_tmp_bytes(uint64_t n) {
-    size_t a = 0, b = 0;
-    (void)rocprim::exclusive_scan(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u, n,
-                                  rocprim::plus<uint32_t>());
-    (void)rocprim::exclusive_scan(nullptr, b, (const uint64_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0, n,
-                                  rocprim::plus<uint64_t>());
-    return (a > b ? a : b) + 256;
-}
-
-int frame_serial(const uint8_t *in, uint64_t len, FrameWs &ws, void *stream) {
-    hipLaunchKernelGGL(k_frame_serial, dim3(1), dim3(64), 0, (hipStream_t)stream, in, len, ws.frag_pos, ws.frag_mark,
-                       ws.res + 2);
+int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+                 uint64_t *msg_offsets, void *stream) {
+    hipLaunchKernelGGL(k_fr_serial, dim3(1), dim3(64), 0, (hipStream_t)stream, in, len, cap, stream_offsets ? 1 : 0,
+                       msg_offsets, ws.frag_pos, ws.res);
     return (int)hipGetLastError();
 }
 
-int frame_last(FrameWs &ws, uint64_t nfrag, void *stream) {
-    hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(ws.res + 1, 0, 8, st) != hipSuccess) return (int)hipErrorUnknown;
-    uint64_t blocks = (nfrag + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    if (nfrag) hipLaunchKernelGGL(k_frame_lastmsg, dim3((uint32_t)blocks), dim3(256), 0, st, ws.frag_mark, nfrag,
-                                  (unsigned long long *)ws.res + 1);
-    return (int)hipGetLastError();
-}
-
-int frame_messages(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, bool stream_offsets,
-                   uint64_t *msg_offsets, void *stream) {
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_frame_prep, grid1(nf, 256), dim3(256), 0, st, ws.frag_mark, nf, ws.size, ws.last);
-    size_t tb = ws.tmp_bytes;
-    if (rocprim::exclusive_scan(ws.tmp, tb, ws.last, ws.msg_id, 0u, nf, rocprim::plus<uint32_t>(), st) != hipSuccess)
-        return (int)hipErrorUnknown;
-    tb = ws.tmp_bytes;
-    if (rocprim::exclusive_scan(ws.tmp, tb, ws.size, ws.pay_off, (uint64_t)0, nf, rocprim::plus<uint64_t>(), st) !=
-        hipSuccess)
-        return (int)hipErrorUnknown;
-    hipLaunchKernelGGL(k_frame_msgs, grid1(nf, 256), dim3(256), 0, st, ws.frag_pos, ws.frag_mark, nf, ws.msg_id,
-                       ws.pay_off, cap, stream_offsets, msg_offsets, ws.res + 3);
-    (void)in;
-    return (int)hipGetLastError();
-}
-
-int frame_copy(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, uint64_t payload_bytes, uint8_t *payload,
+int frame_copy(const uint8_t *in, const FrameWs &ws, uint64_t nf, uint64_t payload_bytes, uint8_t *payload,
                void *stream) {
+    if (!nf) return hipSuccess;
     uint32_t G = 1;   // lanes per fragment: ~16 bytes per lane for the average fragment
     while (G < 64 && 16ull * G * nf < payload_bytes) G <<= 1;
     uint64_t blocks = (nf + 256 / G - 1) / (256 / G);
     if (blocks > 65536) blocks = 65536;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_frame_copy, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, in, ws.frag_pos,
-                       ws.frag_mark, ws.pay_off, ws.msg_id, nf, cap, G, payload);
+    hipLaunchKernelGGL(k_fr_copy, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, in, ws.frag_pos, nf, G,
+                       payload);
     return (int)hipGetLastError();
 }
 

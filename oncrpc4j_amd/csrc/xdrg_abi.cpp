@@ -858,18 +858,16 @@ extern "C" int xdrg_decode_batch_view(xdrg_ctx *c, const xdrg_schema *s, const u
 // ---------------------------------------------------------------------------
 // framing
 // ---------------------------------------------------------------------------
-// Carve the frame-walk workspace for a stream of Q words (upper bound on
-// fragments: one per word).
+// Carve the frame-walk workspace for a stream of Q words (the fragment list:
+// one entry per word at most).
 static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
-    const uint64_t nch = (Q + kFChunk - 1) / kFChunk + 1, nsup = (Q + kFSuper - 1) / kFSuper + 1;
-    const uint64_t F = Q + 1;
-    const size_t tmp = frame_scan_tmp_bytes(F > nch ? F : nch);
+    const uint64_t nsup = (Q + kFSuper - 1) / kFSuper + 1, nsub = nsup * (kFSuper / kFChunk);
+    const uint64_t F = Q + 2;
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_e1 = take(4 * Q), o_e2 = take(4 * Q), o_se = take(4 * nsup), o_ce = take(4 * nch),
-                 o_cn = take(4 * nch), o_ba = take(4 * nch), o_fp = take(8 * F), o_fm = take(4 * F),
-                 o_sz = take(8 * F), o_po = take(8 * F), o_la = take(4 * F), o_mi = take(4 * F), o_re = take(64),
-                 o_tm = take(tmp);
+    const size_t o_ex = take(4 * Q), o_se = take(4 * nsup), o_sb = take(sizeof(FrameSub) * nsub),
+                 o_fb = take(512 * nsub), o_lb = take(512 * nsub), o_su = take(sizeof(FrameSuper) * nsup),
+                 o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_re = take(64);
     if (off > c->fws_bytes) {
         if (c->d_fws) {
             HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -881,81 +879,75 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
         c->fws_bytes = off;
     }
     uint8_t *b = (uint8_t *)c->d_fws;
-    ws.exit1 = (uint32_t *)(b + o_e1); ws.exit2 = (uint32_t *)(b + o_e2);
-    ws.sentry = (uint32_t *)(b + o_se); ws.centry = (uint32_t *)(b + o_ce);
-    ws.counts = (uint32_t *)(b + o_cn); ws.base = (uint32_t *)(b + o_ba);
-    ws.frag_pos = (uint64_t *)(b + o_fp); ws.frag_mark = (uint32_t *)(b + o_fm);
-    ws.size = (uint64_t *)(b + o_sz); ws.pay_off = (uint64_t *)(b + o_po);
-    ws.last = (uint32_t *)(b + o_la); ws.msg_id = (uint32_t *)(b + o_mi);
+    ws.exitS = (uint32_t *)(b + o_ex);
+    ws.sentry = (uint32_t *)(b + o_se);
+    ws.sub = (FrameSub *)(b + o_sb);
+    ws.fbits = (uint32_t *)(b + o_fb);
+    ws.lbits = (uint32_t *)(b + o_lb);
+    ws.sup = (FrameSuper *)(b + o_su);
+    ws.bases = (FrameBase *)(b + o_ba);
+    ws.frag_pos = (uint64_t *)(b + o_fp);
     ws.res = (uint64_t *)(b + o_re);
-    ws.tmp = b + o_tm;
-    ws.tmp_bytes = tmp;
     return XDRG_OK;
 }
 
 // RpcMessageParserTCP.handleRead over a whole buffer: the complete messages
 // (at most cap) as stream offsets (payload == NULL) or assembled bodies.
+// One host round trip for xdrg_frame_scan (two for xdrg_deframe: the payload
+// size is checked before the bodies move).
 static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *payload, uint64_t payload_cap,
                       uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs, uint64_t *consumed) {
     if (!c || !msg_offsets || !n_msgs) return XDRG_E_INVAL;
     if (len && !in) return inval(c, "stream is NULL");
-    if (len >= (1ull << 34)) return inval(c, "stream longer than 16 GiB");
+    if (len > kFMaxLen) return inval(c, "stream longer than 16 GiB");
     DeviceGuard dg;
     HIPCHK(c, hipSetDevice(c->device));
     *n_msgs = 0;
     if (consumed) *consumed = 0;
     TimedLaunch t(c, XDRG_KERNEL_FRAME_SCAN);
     HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));
-    const uint64_t Q = len / 4, nch = (Q + kFChunk - 1) / kFChunk;
+    const uint64_t Q = len / 4;
     FrameWs ws;
     int rc = frame_ws(c, Q, ws);
     if (rc) return rc;
-    uint64_t nfrag = 0;
+    const bool stream_offsets = payload == nullptr;
     bool serial = !aligned(in, 4) || Q == 0;
     if (!serial) {   // parallel walk; a real chain meeting a size % 4 != 0 goes serial
-        HIPCHK(c, (hipError_t)frame_levels(in, len, ws, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync((uint32_t *)(c->h_stat + 3), ws.base + nch - 1, 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync((uint32_t *)(c->h_stat + 3) + 1, ws.counts + nch - 1, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, (hipError_t)frame_parallel(in, len, ws, cap, stream_offsets, msg_offsets, !stream_offsets, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 48, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (c->h_stat[2] == kFUnal) serial = true;
-        else nfrag = (uint64_t)((uint32_t *)(c->h_stat + 3))[0] + ((uint32_t *)(c->h_stat + 3))[1];
     }
-    if (serial && len >= 4) {
-        HIPCHK(c, (hipError_t)frame_serial(in, len, ws, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res + 2, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        nfrag = c->h_stat[2];
+    if (serial) {
+        if (len < 4) {
+            c->h_stat[2 + 1] = c->h_stat[2 + 3] = c->h_stat[2 + 4] = c->h_stat[2 + 5] = 0;
+        } else {
+            HIPCHK(c, (hipError_t)frame_serial(in, len, ws, cap, stream_offsets, msg_offsets, c->stream));
+            HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 48, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+        }
     }
-    // complete fragments: up to the last LAST mark (isAllFragmentsArrived :82-85)
-    uint64_t nf = 0;
-    if (nfrag) {
-        HIPCHK(c, (hipError_t)frame_last(ws, nfrag, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res + 1, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        nf = c->h_stat[2];
-    }
-    if (nf == 0) return XDRG_E_INCOMPLETE;   // NextAction STOP (RpcMessageParserTCP.java:51-53)
-    HIPCHK(c, (hipError_t)frame_messages(in, ws, nf, cap, payload == nullptr, msg_offsets, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.msg_id + nf - 1, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_stat + 3, ws.res + 3, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    const uint64_t total = (uint64_t)(uint32_t)c->h_stat[2] + 1;   // the last complete fragment ends a message
-    const uint64_t nout = total < cap ? total : cap;
+    // h_stat[2 + k] = res[k]: [1] complete fragments, [3] consumed, [4] complete messages,
+    // [5] fragments of the first cap messages
+    const uint64_t M = c->h_stat[2 + 4];
+    const uint64_t nout = M < cap ? M : cap;
+    if (nout == 0) return XDRG_E_INCOMPLETE;   // NextAction STOP (RpcMessageParserTCP.java:51-53)
     *n_msgs = nout;
-    if (consumed) *consumed = c->h_stat[3];
+    if (consumed) *consumed = c->h_stat[2 + 3];
     if (payload) {
-        HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, msg_offsets + nout, 8, hipMemcpyDeviceToHost, c->stream));
+        const uint64_t nfc = c->h_stat[2 + 5];
+        HIPCHK(c, hipMemcpyAsync(c->h_stat + 1, msg_offsets + nout, 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (c->h_stat[2] > payload_cap) {
+        const uint64_t bytes = c->h_stat[1];
+        if (bytes > payload_cap) {
             c->err = "payload buffer too small";
-            if (consumed) *consumed = c->h_stat[2];
+            if (consumed) *consumed = bytes;
             return XDRG_E_CAPACITY;
         }
-        HIPCHK(c, (hipError_t)frame_copy(in, ws, nf, cap, c->h_stat[2], payload, c->stream));
+        HIPCHK(c, (hipError_t)frame_copy(in, ws, nfc, bytes, payload, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    return nout ? XDRG_OK : XDRG_E_INCOMPLETE;
+    return XDRG_OK;
 }
 
 extern "C" int xdrg_frame_scan(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint64_t *msg_offsets,

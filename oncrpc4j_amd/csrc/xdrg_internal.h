@@ -204,35 +204,49 @@ int launch_finalize(const unsigned long long *errkey, unsigned long long extra_k
 
 // ---- parallel record-mark walk (kernels_frame.hip) ------------------------
 constexpr uint32_t kFChunkLog2 = 12;
-constexpr uint32_t kFChunk = 1u << kFChunkLog2;      // words per level-1 chunk (16 KiB of stream)
-constexpr uint32_t kFSuperLog2 = 6;                  // level-1 chunks per super-chunk, log2
+constexpr uint32_t kFChunk = 1u << kFChunkLog2;      // words per sub-chunk (16 KiB of stream)
+constexpr uint32_t kFSuperLog2 = 6;                  // sub-chunks per super-chunk, log2
 constexpr uint32_t kFSuper = kFChunk << kFSuperLog2; // words per super-chunk (1 MiB)
 constexpr uint32_t kFStop = 0xffffffffu;      // chain ends: fragment not fully received
 constexpr uint32_t kFUnal = 0xfffffffeu;      // chain meets a size % 4 != 0 (serial fallback)
 constexpr uint32_t kFNone = 0xffffffffu;      // no entry
-struct FrameWs {                              // device workspace of one walk
-    uint32_t *exit1, *exit2;                  // [Q] word-position exits (L1 chunk, L2 super-chunk)
-    uint32_t *sentry, *centry;                // [nsuper], [nchunks] chain entries
-    uint32_t *counts, *base;                  // [nchunks] fragments per chunk, exclusive scan
-    uint64_t *frag_pos;                       // [nfrag] stream offset of each fragment's mark
-    uint32_t *frag_mark;                      // [nfrag] the raw mark (size | LAST)
-    uint64_t *size, *pay_off;                 // [nfrag] body sizes, body offsets in the payload
-    uint32_t *last, *msg_id;                  // [nfrag] LAST flags, message index
-    uint64_t *res;                            // [0] chain terminal [1] complete fragments
-                                              // [2] fragments (serial) [3] consumed stream bytes
-    void *tmp;                                // rocPRIM scan storage
-    size_t tmp_bytes;
+constexpr uint64_t kFMaxLen = (1ull << 34) - (1ull << 21);   // 32-bit word positions below the terminals
+struct FrameSub {                             // one sub-chunk's share of the real chain
+    uint32_t nfrag, nlast;                    // complete fragments starting in it, LAST flags among them
+    uint32_t pre_frag, pre_last;              // exclusive prefixes inside its super-chunk
+    uint32_t prev_tail;                       // LAST flag of the super's previous fragment (2: none)
+    uint32_t upto_ll, has_ll, rsv;            // fragments through its last LAST one
 };
-size_t frame_scan_tmp_bytes(uint64_t n);
-int frame_levels(const uint8_t *in, uint64_t len, FrameWs &ws, void *stream);
-int frame_serial(const uint8_t *in, uint64_t len, FrameWs &ws, void *stream);
-int frame_last(FrameWs &ws, uint64_t nfrag, void *stream);
-// msg_offsets[0..min(n, cap)] of the messages formed by the first nf
-// (complete) fragments: stream offsets of their marks, or offsets in the
-// payload (bodies back to back); res[3] = stream bytes of messages < cap.
-int frame_messages(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, bool stream_offsets,
-                   uint64_t *msg_offsets, void *stream);
-int frame_copy(const uint8_t *in, FrameWs &ws, uint64_t nf, uint64_t cap, uint64_t payload_bytes, uint8_t *payload,
+struct FrameSuper {
+    uint32_t nfrag, nlast, tail, has_ll;      // tail: LAST flag of its last fragment
+    uint64_t upto_ll;                         // in-super fragments through its last LAST one
+};
+struct FrameBase {                            // super-chunk exclusive prefixes
+    uint64_t frag, last;
+    uint32_t prev_tail, rsv;                  // LAST flag of the fragment before it
+};
+struct FrameWs {                              // device workspace of one walk
+    uint32_t *exitS;                          // [Q] first chain word at or past the super-chunk end
+    uint32_t *sentry;                         // [nsup] super-chunk entries on the real chain
+    FrameSub *sub;                            // [nsub]
+    uint32_t *fbits, *lbits;                  // [nsub][128] complete-fragment / LAST bitmaps
+    FrameSuper *sup;                          // [nsup]
+    FrameBase *bases;                         // [nsup]
+    uint64_t *frag_pos;                       // [Q + 2] stream offset of each complete fragment's mark
+                                              // (xdrg_deframe; one entry past the last copied fragment)
+    uint64_t *res;                            // [0] chain terminal [1] complete fragments (through the
+                                              // last LAST one) [3] consumed bytes [4] complete messages
+                                              // [5] fragments of the first `cap` messages
+};
+// Parallel walk: every result in ws.res / msg_offsets (stream or payload
+// offsets); the fragment list too when frag_list.  res[0] == kFUnal: the
+// real chain met a size % 4 != 0 — run frame_serial instead.
+int frame_parallel(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+                   uint64_t *msg_offsets, bool frag_list, void *stream);
+int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+                 uint64_t *msg_offsets, void *stream);
+// Bodies of the first nf fragments into payload (marks stripped).
+int frame_copy(const uint8_t *in, const FrameWs &ws, uint64_t nf, uint64_t payload_bytes, uint8_t *payload,
                void *stream);
 
 // ---- multi-GPU exchange (kernels_multi.hip) -------------------------------
