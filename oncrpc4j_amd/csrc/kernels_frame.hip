@@ -20,9 +20,10 @@
 //               beyond), pointer-jump the pointers that stay inside (active
 //               words only) -> exitS[q] = first chain word at or past the
 //               super-chunk end.  One read of the stream, one write of exitS.
-//   k_fr_fix    one wave hops super-chunk to super-chunk from word 0 through
-//               exitS, from windows of the super-chunks' first words staged
-//               in LDS 64 at a time -> each super-chunk's true entry.
+//   k_fr_fix_* each super-chunk's true entry: groups of 64 super-chunks
+//               resolve the exit of every entry in their first words in
+//               parallel (windows of exitS in LDS), one wave hops group to
+//               group from word 0, each group fills in its super-chunks.
 //   k_fr_mark   block per super-chunk, sub-chunks first to last from its
 //               entry: stage, mark the chain by pointer doubling (round r
 //               marks the successors 2^r hops on, so round r covers hops
@@ -175,39 +176,88 @@ __global__ __launch_bounds__(256) void k_fr_exits(const uint32_t *__restrict__ w
 // ---------------------------------------------------------------------------
 // k_fr_fix: super-chunk entries along the real chain from word 0.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kFixWin = 64;   // words per super-chunk window
-constexpr uint32_t kFixBatch = 64; // super-chunks per staged batch
-__global__ __launch_bounds__(64) void k_fr_fix(const uint32_t *exitS, uint64_t Q, uint64_t nsup,
-                                               uint32_t *sentry, uint64_t *res) {
-    __shared__ uint32_t win[kFixBatch][kFixWin];
-    const uint32_t lane = threadIdx.x;
-    uint64_t e = 0, b0 = ~0ull;
-    while (e < Q) {
-        const uint64_t s = e / kFSuper;
-        if (b0 == ~0ull || s >= b0 + kFixBatch) {   // stage windows of super-chunks [s, s + 64)
-            b0 = s;
-            uint32_t v[kFixBatch];
+// Two levels: a group is 64 consecutive super-chunks.
+//   k_fr_fix_grp   block per group: the group's exit for every entry word in
+//                  the first kFixWin words of its first super-chunk (a lane
+//                  per entry hops super-chunk to super-chunk through windows
+//                  of exitS staged in LDS; an entry deeper than the window
+//                  reads exitS from HBM);
+//   k_fr_fix_top   one wave hops group to group from word 0 (a deep group
+//                  entry walks that group's super-chunks through exitS);
+//   k_fr_fix_fill  block per group: from its true entry, every super-chunk
+//                  entry of the group (sentry).
+constexpr uint32_t kFixWin = 256;   // entry words per super-chunk window
+constexpr uint32_t kFixGrp = 64;    // super-chunks per group
+__device__ __forceinline__ void fix_stage(const uint32_t *exitS, uint32_t Q, uint32_t nsup, uint32_t g, uint32_t *win) {
+    for (uint32_t k = threadIdx.x / 64; k < kFixGrp; k += blockDim.x / 64) {   // a wave per super-chunk
+        const uint32_t s = g * kFixGrp + k;
 #pragma unroll
-            for (uint32_t k = 0; k < kFixBatch; ++k) {   // every load in flight before the LDS writes
-                const uint64_t q = (b0 + k) * kFSuper + lane;
-                v[k] = exitS[q < Q ? q : Q - 1];
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kFixBatch; ++k) {
-                const uint64_t q = (b0 + k) * kFSuper + lane;
-                win[k][lane] = (b0 + k < nsup && q < Q) ? v[k] : kFStop;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t c = 0; c < kFixWin / 64; ++c) {
+            const uint64_t q = (uint64_t)s * kFSuper + 64 * c + (threadIdx.x & 63);
+            win[k * kFixWin + 64 * c + (threadIdx.x & 63)] = (s < nsup && q < Q) ? exitS[q] : kFStop;
         }
-        if (lane == 0) sentry[s] = (uint32_t)e;
-        const uint64_t d = e - s * kFSuper;
-        const uint32_t t = d < kFixWin ? win[s - b0][d] : exitS[e];   // a deep entry: one HBM load
-        e = t;
-        if (t >= kFUnal) break;
     }
-    if (lane == 0) res[0] = e;   // >= Q: ran to the end; kFStop / kFUnal: terminal met on the real chain
+    __syncthreads();
+}
+// One hop from chain word e inside group g: the exit of e's super-chunk.
+__device__ __forceinline__ uint32_t fix_hop(const uint32_t *exitS, const uint32_t *win, uint32_t g, uint32_t e) {
+    const uint32_t s = e >> (kFChunkLog2 + kFSuperLog2), d = e & (kFSuper - 1);
+    return d < kFixWin ? win[(s - g * kFixGrp) * kFixWin + d] : exitS[e];
+}
+
+__global__ __launch_bounds__(256) void k_fr_fix_grp(const uint32_t *exitS, uint32_t Q, uint32_t nsup, uint32_t *gexit) {
+    __shared__ uint32_t win[kFixGrp * kFixWin];
+    const uint32_t g = blockIdx.x;
+    fix_stage(exitS, Q, nsup, g, win);
+    const uint64_t gend64 = (uint64_t)(g + 1) * kFixGrp * kFSuper;
+    const uint32_t gend = gend64 < Q ? (uint32_t)gend64 : Q;
+    uint32_t e = g * kFixGrp * kFSuper + threadIdx.x;   // this lane's entry word
+    if (e < gend) {
+        while (e < gend) {
+            e = fix_hop(exitS, win, g, e);
+            if (e >= kFUnal) break;
+        }
+    } else {
+        e = kFStop;
+    }
+    gexit[(uint64_t)g * kFixWin + threadIdx.x] = e;
+}
+
+__global__ __launch_bounds__(64) void k_fr_fix_top(const uint32_t *exitS, const uint32_t *gexit, uint32_t Q,
+                                                   uint32_t *gentry, uint64_t *res) {
+    uint32_t e = 0;
+    while (e < Q) {
+        const uint32_t g = e / (kFixGrp * kFSuper), d = e - g * kFixGrp * kFSuper;
+        gentry[g] = e;   // one address for the whole wave
+        if (d < kFixWin) {
+            e = gexit[(uint64_t)g * kFixWin + d];
+        } else {         // a deep group entry: walk its super-chunks through exitS
+            const uint64_t gend = (uint64_t)(g + 1) * kFixGrp * kFSuper;
+            while (e < Q && e < gend) {
+                e = exitS[e];
+                if (e >= kFUnal) break;
+            }
+        }
+        if (e >= kFUnal) break;
+    }
+    if (threadIdx.x == 0) res[0] = e;   // >= Q: ran to the end; kFStop / kFUnal: terminal met on the real chain
+}
+
+__global__ __launch_bounds__(256) void k_fr_fix_fill(const uint32_t *exitS, const uint32_t *gentry, uint32_t Q,
+                                                     uint32_t nsup, uint32_t *sentry) {
+    __shared__ uint32_t win[kFixGrp * kFixWin];
+    const uint32_t g = blockIdx.x;
+    uint32_t e = gentry[g];
+    if (e == kFNone) return;   // the chain skips this group (block-uniform)
+    fix_stage(exitS, Q, nsup, g, win);
+    if (threadIdx.x) return;
+    const uint64_t gend64 = (uint64_t)(g + 1) * kFixGrp * kFSuper;
+    const uint32_t gend = gend64 < Q ? (uint32_t)gend64 : Q;
+    while (e < gend) {
+        sentry[e >> (kFChunkLog2 + kFSuperLog2)] = e;
+        e = fix_hop(exitS, win, g, e);
+        if (e >= kFUnal) break;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -262,7 +312,6 @@ __global__ __launch_bounds__(256) void k_fr_mark(const uint32_t *__restrict__ w,
                 v = fr_next(m, q, Q, tb);
                 f = (v < kFUnal ? 1u : 0u) | ((m >> 31) << 1);
                 if (v < bend) mask |= 1u << i;   // v < bend < kFUnal: a word inside
-                if (q == e && (v >= kFUnal || v >= bend)) e_next = v;   // the entry itself leaves at once
             }
             t[i] = v;
             ff[i >> 2] |= f << (8 * (i & 3));
@@ -328,13 +377,12 @@ __global__ __launch_bounds__(256) void k_fr_mark(const uint32_t *__restrict__ w,
         }
         // the chain's exit: the marked node whose own next leaves the sub-chunk
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t li = fr_li(tid, i);
-            const uint32_t q = base + li;
-            if (q < Q && q != e && on[li]) {
-                const uint32_t v = fr_next(fr_bswap(x[i]), q, Q, tb);
-                if (v >= kFUnal || v >= bend) e_next = v;
-            }
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t o = *(const uint32_t *)&on[4 * tid + 1024 * k];
+            if (!o) continue;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (((o >> (8 * c)) & 1u) && t[4 * k + c] >= bend) e_next = t[4 * k + c];   // terminals too
         }
         for (int d = 32; d > 0; d >>= 1) {
             cf += __shfl_xor(cf, d, 64);
@@ -596,8 +644,13 @@ int frame_parallel(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t 
     const uint32_t Q = (uint32_t)(len / 4), tb = (uint32_t)(len & 3);
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
     hipLaunchKernelGGL(k_fr_exits, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitS);
+    const uint64_t ngrp = (nsup + kFixGrp - 1) / kFixGrp;
     if (hipMemsetAsync(ws.sentry, 0xff, nsup * 4, st) != hipSuccess) return (int)hipErrorUnknown;
-    hipLaunchKernelGGL(k_fr_fix, dim3(1), dim3(64), 0, st, ws.exitS, (uint64_t)Q, nsup, ws.sentry, ws.res);
+    if (hipMemsetAsync(ws.gentry, 0xff, ngrp * 4, st) != hipSuccess) return (int)hipErrorUnknown;
+    hipLaunchKernelGGL(k_fr_fix_grp, dim3((uint32_t)ngrp), dim3(kFixWin), 0, st, ws.exitS, Q, (uint32_t)nsup, ws.gexit);
+    hipLaunchKernelGGL(k_fr_fix_top, dim3(1), dim3(64), 0, st, ws.exitS, ws.gexit, Q, ws.gentry, ws.res);
+    hipLaunchKernelGGL(k_fr_fix_fill, dim3((uint32_t)ngrp), dim3(256), 0, st, ws.exitS, ws.gentry, Q, (uint32_t)nsup,
+                       ws.sentry);
     hipLaunchKernelGGL(k_fr_mark, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.sub,
                        ws.fbits, ws.lbits, ws.sup);
     hipLaunchKernelGGL(k_fr_bases, dim3(1), dim3(1024), 0, st, ws.sup, nsup, ws.bases, ws.res);

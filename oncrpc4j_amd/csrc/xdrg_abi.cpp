@@ -862,10 +862,11 @@ extern "C" int xdrg_decode_batch_view(xdrg_ctx *c, const xdrg_schema *s, const u
 // one entry per word at most).
 static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper + 1, nsub = nsup * (kFSuper / kFChunk);
+    const uint64_t ngrp = nsup / 64 + 2;
     const uint64_t F = Q + 2;
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_ex = take(4 * Q), o_se = take(4 * nsup), o_sb = take(sizeof(FrameSub) * nsub),
+    const size_t o_ex = take(4 * Q), o_se = take(4 * nsup), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
                  o_fb = take(512 * nsub), o_lb = take(512 * nsub), o_su = take(sizeof(FrameSuper) * nsup),
                  o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_re = take(64);
     if (off > c->fws_bytes) {
@@ -881,6 +882,8 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     uint8_t *b = (uint8_t *)c->d_fws;
     ws.exitS = (uint32_t *)(b + o_ex);
     ws.sentry = (uint32_t *)(b + o_se);
+    ws.gexit = (uint32_t *)(b + o_ge);
+    ws.gentry = (uint32_t *)(b + o_gn);
     ws.sub = (FrameSub *)(b + o_sb);
     ws.fbits = (uint32_t *)(b + o_fb);
     ws.lbits = (uint32_t *)(b + o_lb);

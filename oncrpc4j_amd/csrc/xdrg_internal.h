@@ -205,8 +205,8 @@ int launch_finalize(const unsigned long long *errkey, unsigned long long extra_k
 // ---- parallel record-mark walk (kernels_frame.hip) ------------------------
 constexpr uint32_t kFChunkLog2 = 12;
 constexpr uint32_t kFChunk = 1u << kFChunkLog2;      // words per sub-chunk (16 KiB of stream)
-constexpr uint32_t kFSuperLog2 = 6;                  // sub-chunks per super-chunk, log2
-constexpr uint32_t kFSuper = kFChunk << kFSuperLog2; // words per super-chunk (1 MiB)
+constexpr uint32_t kFSuperLog2 = 4;                  // sub-chunks per super-chunk, log2
+constexpr uint32_t kFSuper = kFChunk << kFSuperLog2; // words per super-chunk (256 KiB)
 constexpr uint32_t kFStop = 0xffffffffu;      // chain ends: fragment not fully received
 constexpr uint32_t kFUnal = 0xfffffffeu;      // chain meets a size % 4 != 0 (serial fallback)
 constexpr uint32_t kFNone = 0xffffffffu;      // no entry
@@ -228,6 +228,8 @@ struct FrameBase {                            // super-chunk exclusive prefixes
 struct FrameWs {                              // device workspace of one walk
     uint32_t *exitS;                          // [Q] first chain word at or past the super-chunk end
     uint32_t *sentry;                         // [nsup] super-chunk entries on the real chain
+    uint32_t *gexit;                          // [ngrp][256] group exits of the first super's first words
+    uint32_t *gentry;                         // [ngrp] group entries on the real chain
     FrameSub *sub;                            // [nsub]
     uint32_t *fbits, *lbits;                  // [nsub][128] complete-fragment / LAST bitmaps
     FrameSuper *sup;                          // [nsup]
