@@ -2154,10 +2154,12 @@ __host__ __device__ constexpr size_t dec_stage_meta(uint32_t nd) {
             15) & ~(size_t)15;
 }
 
-// The whole block decodes fields [0, upto) of record r whose first field
-// starts at stream offset pos (records too large for the tile).  Native
-// offsets come from the columns' offsets arrays this block just wrote.
-__device__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uint32_t upto) {
+// The whole block decodes fields [0, upto) of record r (the block's record
+// j) whose first field starts at stream offset pos (records too large for the
+// tile).  Counts come from the block's relative native offsets snrel, native
+// offsets from the columns' offsets arrays this block just wrote.
+__device__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uint32_t upto,
+                                 const uint32_t *snrel, uint32_t j) {
     const uint32_t tid = threadIdx.x;
     const uint8_t *in = a.xdr;
     const Span sp = make_span(in, in + a.xdr_cap, (const uint8_t *)a.block_sums);
@@ -2171,7 +2173,8 @@ __device__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uin
             continue;
         }
         const bool bytes = f.xsz == 1;
-        const uint64_t cnt1 = a.rec_cnt[(uint64_t)d * a.n + r];
+        const uint32_t *rel = snrel + (size_t)d * (kRecPerBlock + 1);
+        const uint64_t cnt1 = rel[j + 1] - rel[j];
         uint8_t *dst[1] = {f.data + f.offsets[r] * (bytes ? 1 : f.nsz)};
         const uint8_t *src[1] = {in + pos + 4};
         const uint64_t cnt[1] = {cnt1};
@@ -2198,6 +2201,115 @@ __device__ __forceinline__ uint32_t dec_fit(const RecArgs &a, const uint32_t *ss
     return (uint32_t)__syncthreads_count(fits);
 }
 
+// ---- decoupled look-back: the staged decode with the sizes walk folded in ----
+// Each block walks its own records' length words (k_dec_sizes_g's checks),
+// publishes its count totals, and learns the native offset of its first
+// element per dynamic field from its predecessors: one status word per block
+// and word w (w < ndyn: counts of dynamic field w; w = ndyn: the first record
+// a walk check failed, a.n = none): flag in bits 62-63 (1 = the block's own
+// value, 2 = the inclusive prefix over blocks [0, b]: sum, or min for the
+// failed record) | value.  Flag and value share one 8-byte word, stored and
+// polled with agent-scope relaxed atomics (L2, not the CU's L1), a tagged
+// granule that needs no fence (MI355X_MICROARCH.md, inter-workgroup
+// visibility).  Blocks take tickets in start order, so every block waited on
+// is already running and publishes its own value without waiting.
+constexpr uint64_t kLbOwn = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = kLbOwn - 1;
+
+__device__ __forceinline__ void lb_put(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_get(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        const uint64_t t = __shfl_xor(v, o, 64);
+        v = t < v ? t : v;
+    }
+    return v;
+}
+
+// Wave 0 of block b (totals agg, own first failing record lbad): publish,
+// look back over the predecessors 64 at a time down to the nearest inclusive
+// prefix, publish the block's inclusive prefix.  Leaves s_base[d] = the
+// exclusive prefix of field d's counts and *s_bad = the first failing record
+// over blocks [0, b]; the last block also writes the totals and each
+// column's offsets[n].
+__device__ __forceinline__ void lb_resolve(const RecArgs &a, uint64_t b, const uint64_t (&agg)[kMaxDynLds + 1], uint64_t lbad,
+                           uint64_t *s_base, unsigned long long *s_bad) {
+    const uint32_t lane = threadIdx.x & 63, nd = a.ndyn;
+    const uint64_t nb = a.nblocks;
+    uint64_t *st = a.lb_state;
+    if (lane == 0) {
+        const uint64_t fl = b ? kLbOwn : kLbIncl;
+#pragma unroll
+        for (int w = 0; w < kMaxDynLds; ++w)
+            if ((uint32_t)w < nd) lb_put(st + (uint64_t)w * nb + b, fl | agg[w]);
+        lb_put(st + (uint64_t)nd * nb + b, fl | lbad);
+    }
+    // Every word is its own chain: a predecessor may be seen with some words
+    // already inclusive and others still its own value.
+    uint64_t pre[kMaxDynLds + 1] = {0, 0, 0, 0, 0};
+    uint64_t pbad = a.n;
+    uint32_t done = 0;
+    const uint32_t all = (2u << nd) - 1;
+    int64_t p = (int64_t)b - 1 - (int64_t)lane;
+    while (b && done != all) {
+        uint64_t v[kMaxDynLds + 1];
+        for (;;) {
+            bool ready = true;
+#pragma unroll
+            for (int w = 0; w <= kMaxDynLds; ++w) {
+                if ((uint32_t)w > nd) continue;
+                const uint64_t x = p >= 0 ? lb_get(st + (uint64_t)w * nb + (uint64_t)p)
+                                          : (kLbIncl | ((uint32_t)w == nd ? a.n : 0));
+                v[w] = x;
+                ready = ready && (x >> 62) != 0;
+            }
+            if (__all(ready)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+#pragma unroll
+        for (int w = 0; w <= kMaxDynLds; ++w) {
+            if ((uint32_t)w > nd || ((done >> w) & 1)) continue;
+            const uint64_t pm = __ballot((v[w] >> 62) == 2);
+            const uint32_t first = pm ? (uint32_t)__builtin_ctzll(pm) : 63u;   // nearest inclusive predecessor
+            const bool take = lane <= first;
+            const uint64_t x = v[w] & kLbVal;
+            if ((uint32_t)w < nd) {
+                pre[w] += wave_sum64(take ? x : 0);
+            } else {
+                const uint64_t m = wave_min64(take ? x : a.n);
+                pbad = m < pbad ? m : pbad;
+            }
+            if (pm) done |= 1u << w;
+        }
+        p -= 64;
+    }
+    if (lane == 0) {
+        const uint64_t bad = pbad < lbad ? pbad : lbad;
+#pragma unroll
+        for (int w = 0; w < kMaxDynLds; ++w) {
+            if ((uint32_t)w >= nd) continue;
+            if (b) lb_put(st + (uint64_t)w * nb + b, kLbIncl | (pre[w] + agg[w]));
+            s_base[w] = pre[w];
+            if (b + 1 == nb) {
+                a.totals[w] = pre[w] + agg[w];
+                a.f[a.dyn_idx[w]].offsets[a.n] = pre[w] + agg[w];
+            }
+        }
+        if (b) lb_put(st + (uint64_t)nd * nb + b, kLbIncl | bad);
+        *s_bad = bad;
+    }
+}
+
+template <bool LB>
 __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;
@@ -2206,12 +2318,68 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
     uint8_t *supto = (uint8_t *)(snrel + (size_t)a.ndyn * RS);
     uint8_t *tile = smem + dec_stage_meta(a.ndyn);
     __shared__ uint32_t s_wide;
-    if (a.big_rec && block_is_big(a, true)) return;   // the group kernel's block
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    __shared__ uint64_t s_base[kMaxDynLds];   // native offset of the block's first element, per dynamic field
+    __shared__ unsigned long long s_b, s_bad;
     const uint32_t tid = threadIdx.x, t0 = tid * kRecPerThread;
-    const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
-    const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
+    const uint64_t nb = a.nblocks;
+    uint64_t bid = blockIdx.x, bad;
+    uint64_t agg[kMaxDynLds + 1] = {0, 0, 0, 0, 0};   // LB: the block's count totals
+    if (LB) {   // blocks take tickets in start order: every block waited on is running
+        if (tid == 0) {
+            s_b = atomicAdd(a.lb_ticket, 1ull);
+            s_bad = a.n;
+        }
+        __syncthreads();
+        bid = s_b;
+    } else if (a.big_rec && block_is_big_at(a, bid, true)) {
+        return;   // the group kernel's block
+    }
+    const uint64_t rb = bid * kRecPerBlock;
     const uint32_t nrec = (uint32_t)(a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0);
+    uint32_t *lcnt = (uint32_t *)tile;   // LB: walked counts [ndyn][kRecPerBlock], consumed before staging
+    if (LB) {
+        // ---- k_dec_sizes_g's walk (same checks, order and dead-record rule)
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j)
+            for (uint32_t d = 0; d < a.ndyn; ++d) lcnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
+        const uint32_t nj = t0 < nrec ? (nrec - t0 < (uint32_t)kRecPerThread ? nrec - t0 : (uint32_t)kRecPerThread) : 0u;
+        uint32_t err[kRecPerThread], sub[kRecPerThread];
+        walk_counts_lockstep(a, rb + t0, nj, lcnt + t0, err, sub);
+        bool dead = false;
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            if (!dead && err[j]) {
+                atomicMin(a.errkey, err_key(rb + t0 + j, sub[j], err[j]));
+                atomicMin(&s_bad, (unsigned long long)(rb + t0 + j));
+                dead = true;
+            }
+            if (dead)
+                for (uint32_t d = 0; d < a.ndyn; ++d) lcnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
+        }
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d) {
+            if ((uint32_t)d >= a.ndyn) continue;
+            uint64_t sv = 0;
+#pragma unroll
+            for (int j = 0; j < kRecPerThread; ++j) sv += lcnt[(size_t)d * kRecPerBlock + t0 + j];
+            agg[d] = block_sum(sv);   // its barriers also publish s_bad
+        }
+        if (tid < 64) lb_resolve(a, bid, agg, (uint64_t)s_bad, s_base, &s_bad);
+        __syncthreads();
+        bad = s_bad;
+        if (a.big_rec && block_is_big_at(a, bid, true)) {
+            // the group kernel's block: leave what k_dec_sizes_g + k_scan_rows would
+            for (uint32_t d = 0; d < a.ndyn; ++d)
+                for (uint32_t i = tid; i < nrec; i += kRecThreads)
+                    a.rec_cnt[(uint64_t)d * a.n + rb + i] = lcnt[(size_t)d * kRecPerBlock + i];
+            if (tid < a.ndyn) a.block_sums[(uint64_t)tid * nb + bid] = s_base[tid];
+            return;
+        }
+    } else {
+        const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
+        bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
+        if (tid < a.ndyn) s_base[tid] = a.block_sums[(uint64_t)tid * nb + bid];
+    }
     const uint32_t nlive = bad > rb ? (uint32_t)(bad - rb < (uint64_t)nrec ? bad - rb : (uint64_t)nrec) : 0;
     if (tid == 0) s_wide = 0;
     // ---- prologue: counts, native offsets (written to the columns), capacity, extents
@@ -2238,11 +2406,11 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {
             const uint64_t r = rb + t0 + j;
-            c[j] = t0 + j < nlive ? a.rec_cnt[(uint64_t)d * a.n + r] : 0u;
+            c[j] = t0 + j < nlive ? (LB ? lcnt[(size_t)d * kRecPerBlock + t0 + j] : a.rec_cnt[(uint64_t)d * a.n + r]) : 0u;
             s += c[j];
         }
         uint64_t btot;
-        const uint64_t base = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x];
+        const uint64_t base = LB ? s_base[d] : a.block_sums[(uint64_t)d * nb + bid];
         uint64_t off = base + block_excl_scan(s, &btot);
         wide |= btot * (f.xsz == 1 ? 1 : f.nsz) >= (1ull << 31);
 #pragma unroll
@@ -2259,7 +2427,7 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
             off += c[j];
         }
         if (tid == kRecThreads - 1) snrel[d * RS + kRecPerBlock] = (uint32_t)(off - base);
-        if (blockIdx.x == 0 && tid == 0) f.offsets[a.n] = a.totals[d];
+        if (!LB && tid == 0 && bid == 0) f.offsets[a.n] = a.totals[d];   // LB: lb_resolve
     }
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) supto[t0 + j] = (uint8_t)upto[j];
@@ -2282,7 +2450,7 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
 
     if (wide) {
         for (uint32_t j = 0; j < nlive; ++j)
-            dec_record_block(a, rb + j, rec_extent(a, rb + j).a + (a.framed ? 4 : 0), supto[j]);
+            dec_record_block(a, rb + j, rec_extent(a, rb + j).a + (a.framed ? 4 : 0), supto[j], snrel, j);
         return;
     }
     // ---- sub-batches
@@ -2290,7 +2458,7 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
     uint32_t k1 = nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
     while (js < nlive) {
         if (k1 == 0) {   // too large for the tile: the whole block decodes record js
-            dec_record_block(a, rb + js, sb + sstart[js], supto[js]);
+            dec_record_block(a, rb + js, sb + sstart[js], supto[js], snrel, js);
             ++js;
             k1 = js < nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
             continue;
@@ -2326,7 +2494,7 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
             const bool bytes = f.xsz == 1;
             const uint64_t esz = bytes ? 1 : f.nsz;
             const uint32_t *rel = snrel + d * RS;
-            const uint64_t base = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x];
+            const uint64_t base = s_base[d];
             const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
             const uint32_t G = a.force_g ? a.force_g : pow2_lanes(fbytes / m, a.lane_bytes_dec);
             const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
@@ -2404,6 +2572,9 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     const bool pay = t.payload && a.pay_pos && a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1 &&
                      ((stage && t.big_rec) || (grp && !stage && t.rec == 0));
     a.payk = pay ? 1u : 0u;
+    // staged decode: the sizes walk runs inside the place kernel (its counts
+    // borrow the tile until staging starts)
+    const bool lb = stage && t.dec_lb && a.ndyn && (size_t)a.ndyn * kRecPerBlock * 4 <= a.tile_bytes;
     const uint64_t pblk = (a.n + 3) / 4;   // a wave per record, 4 records per block
     const dim3 pgrid((unsigned)(pblk < (1u << 22) ? pblk : (1u << 22)));
     switch (phase) {
@@ -2427,19 +2598,22 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SIZES:
+        if (lb) return (int)hipMemsetAsync(a.lb_state, 0, ((uint64_t)(a.ndyn + 1) * nb + 1) * 8, st);
         if (grp || lane) hipLaunchKernelGGL(k_dec_sizes_g, dim3(nb), dim3(kRecThreads),
                                     (size_t)a.ndyn * kRecPerBlock * 4, st, a);
         else hipLaunchKernelGGL(k_dec_sizes_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SCAN:
-        if (a.ndyn)
+        if (a.ndyn && !lb)
             hipLaunchKernelGGL(k_scan_rows, dim3(a.ndyn), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_DEC_PLACE:
         if (stage) {
             a.big_rec = t.big_rec;
-            hipLaunchKernelGGL(k_dec_stage, dim3(nb), dim3(kRecThreads),
-                               dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            if (lb) hipLaunchKernelGGL(k_dec_stage<true>, dim3(nb), dim3(kRecThreads),
+                                       dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            else hipLaunchKernelGGL(k_dec_stage<false>, dim3(nb), dim3(kRecThreads),
+                                    dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             if (a.big_rec) launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
             if (a.big_rec && pay) hipLaunchKernelGGL((k_dec_payload<64, true>), pgrid, dim3(256), 0, st, a);
         } else if (lane || (grp && t.rec == 3)) {

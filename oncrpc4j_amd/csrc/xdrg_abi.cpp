@@ -292,6 +292,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 14: if (!in(1, 2)) return -1; t.framed = (int32_t)v; return 0;
     case 16: if (!in(0, 2)) return -1; t.words = (int32_t)v; return 0;
     case 18: if (!in(0, 1)) return -1; t.payload = (int32_t)v; return 0;
+    case 19: if (!in(0, 1)) return -1; t.dec_lb = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -543,12 +544,16 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
     const size_t cnt_words = (a.ndyn * n + 1) / 2;
     // | per-record payload positions u64 [n] (one dynamic byte field: k_enc/dec_payload)
     const size_t pay_words = (a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1) ? n : 0;
-    int rc = ensure_ws(c, sums_words + cnt_words + pay_words);
+    // | look-back status words [ndyn + 1][nblocks] | ticket (staged decode)
+    const size_t lb_words = (a.ndyn + 1) * a.nblocks + 1;
+    int rc = ensure_ws(c, sums_words + cnt_words + pay_words + lb_words);
     if (rc) return rc;
     a.block_sums = c->d_ws;
     a.totals = c->d_ws + rows * a.nblocks;
     a.rec_cnt = (uint32_t *)(c->d_ws + sums_words);
     a.pay_pos = pay_words ? c->d_ws + sums_words + cnt_words : nullptr;
+    a.lb_state = c->d_ws + sums_words + cnt_words + pay_words;
+    a.lb_ticket = (unsigned long long *)(a.lb_state + (a.ndyn + 1) * a.nblocks);
     a.errkey = c->d_stat;
     return XDRG_OK;
 }

@@ -141,6 +141,8 @@ struct RecArgs {
     uint32_t rsv3;
     uint64_t *pay_pos;         // payk: per record, stream offset of that field's length word
                                // (decode: ~0 = not to be written)
+    uint64_t *lb_state;        // staged decode with look-back: [ndyn + 1][nblocks] status words
+    unsigned long long *lb_ticket;   // and the block ticket (both zeroed before the launch)
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
     int32_t cvals[XDRG_MAX_CASES];  // case values of the conditional fields
@@ -168,6 +170,8 @@ struct Tuning {
     int32_t framed = 2;             // key 14: record-marked AoS decode: 2 lean, 1 wave-LDS transpose
     int32_t rec = 4;                // key 9: record path: 4 staged sub-batches, 0 group per record, 3 lane per record
     int32_t payload = 1;            // key 18: one dynamic byte field on group-kernel blocks: 1 payload kernels, 0 in place
+    int32_t dec_lb = 0;             // key 19: staged record-path decode: 1 counts walked in the place kernel
+                                    // (decoupled look-back), 0 separate sizes walk + scan kernels
     int32_t enc_u = 2, dec_u = 2;   // keys 4/5: group kernels, 16-byte chunks per lane in flight
     int32_t enc_r = 1, dec_r = 1;   // keys 10/11: group kernels, records per lane in flight
     uint32_t force_g = 0;           // key 6: lanes per record (0 = sized from the field)

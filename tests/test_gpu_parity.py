@@ -38,15 +38,18 @@ SCHEMAS = {
 }
 
 
-# Record-path implementations (kernels_rec.hip launch_rec_phase): 4 = staged
-# (sub-batches through an LDS tile, the default), 0 = group per record,
-# 3 = lane per record.  Tests taking `rec_kernel` run under each.
-REC_KERNELS = {"group": 0, "lane": 3, "staged": 4}
+# Record-path implementations (kernels_rec.hip launch_rec_phase), as tuning
+# (key, value) pairs: key 9 = 4 staged (sub-batches through an LDS tile, the
+# default), with key 19 = 1 the staged decode walking the counts itself
+# (decoupled look-back, no sizes / scan kernels); key 9 = 0 group per record,
+# 3 lane per record.  Tests taking `rec_kernel` run under each.
+REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),), "staged_lb": ((9, 4), (19, 1))}
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
 def rec_kernel(request, gpu_ctx):
-    gpu_ctx.tune(9, REC_KERNELS[request.param])
+    for k, v in REC_KERNELS[request.param]:
+        gpu_ctx.tune(k, v)
     yield request.param
     gpu_ctx.tune(0)
 

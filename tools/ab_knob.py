@@ -32,8 +32,10 @@ def main():
     p.add_argument("--key", type=int, required=True)
     p.add_argument("--values", required=True)
     p.add_argument("--rounds", type=int, default=7)
+    p.add_argument("--base", default="", help="key=value,... applied before each variant")
     a = p.parse_args()
     values = [int(v) for v in a.values.split(",")]
+    basek = [tuple(int(x) for x in kv.split("=")) for kv in a.base.split(",") if kv]
     ctx = engine.Context(0, timing=True)
     ctx.set_stream(torch.cuda.current_stream())
     n = a.records or bench.SIZES[a.config]
@@ -41,6 +43,8 @@ def main():
     res = {}
     for v in values:   # correctness of every variant on its own writes
         ctx.tune(0)
+        for k, x in basek:
+            ctx.tune(k, x)
         ctx.tune(a.key, v)
         wl.clear_outputs()
         wl.step()
@@ -49,6 +53,8 @@ def main():
     for _ in range(a.rounds):
         for v in values:
             ctx.tune(0)
+            for k, x in basek:
+                ctx.tune(k, x)
             ctx.tune(a.key, v)
             ctx.reset_stats()
             wl.step()
@@ -59,7 +65,7 @@ def main():
                     res.setdefault((v, name), []).append(ms)
     ctx.tune(0)
     for (v, name), t in sorted(res.items()):
-        print(json.dumps({"config": a.config, "framed": a.framed, "key": a.key, "value": v, "kernel": name,
+        print(json.dumps({"config": a.config, "framed": a.framed, "base": a.base, "key": a.key, "value": v, "kernel": name,
                           "median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4)}), flush=True)
     ctx.close()
 
