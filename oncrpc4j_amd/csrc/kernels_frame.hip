@@ -57,119 +57,119 @@ __device__ __forceinline__ uint32_t fr_next(uint32_t m, uint32_t q, uint32_t Q, 
     return q + 1 + (size >> 2);
 }
 
+// Word layout of a sub-chunk (kFChunk = 4096 words, 256 threads): thread t
+// owns the 16 consecutive words [16 t, 16 t + 16) — four 16-byte loads, one
+// 16-byte LDS access per 4 words, and its per-word bits form one 16-bit
+// piece of the sub-chunk's bitmaps.
 typedef uint32_t u32x4f __attribute__((ext_vector_type(4)));
 
-// The 16 words of sub-chunk `base` a thread owns: word 4*tid + 1024*k + c
-// (k, c < 4), as four 16-byte loads (a tail reads dword by dword, 0 past Q).
-__device__ __forceinline__ void fr_load16(const uint32_t *w, uint32_t Q, uint32_t base, uint32_t tid, uint32_t (&x)[16]) {
+__device__ __forceinline__ void fr_load(const uint32_t *w, uint32_t Q, uint32_t base, uint32_t tid, uint32_t (&x)[16]) {
+    const uint32_t q0 = base + 16 * tid;
+    if (q0 + 16 <= Q) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t q = base + 4 * tid + 1024 * k;
-        if (q + 4 <= Q) {
-            const u32x4f v = __builtin_nontemporal_load((const u32x4f *)(w + q));
+        for (int k = 0; k < 4; ++k) {
+            const u32x4f v = __builtin_nontemporal_load((const u32x4f *)(w + q0 + 4 * k));
             x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
-        } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) x[4 * k + c] = q + c < Q ? w[q + c] : 0u;
         }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = q0 + i < Q ? w[q0 + i] : 0u;
     }
 }
-__device__ __forceinline__ uint32_t fr_li(uint32_t tid, int i) { return 4 * tid + 1024 * (i >> 2) + (i & 3); }
 
-// Append this thread's flagged positions (mask bit i = position fr_li(tid, i))
-// to the block's list: a wave prefix of the counts, one LDS atomic per wave.
-__device__ __forceinline__ void fr_append16(uint32_t mask, uint32_t tid, uint16_t *list, uint32_t *count) {
-    const uint32_t lane = tid & 63;
-    const uint32_t c = __popc(mask);
-    uint32_t inc = c;   // inclusive wave scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(inc, d, 64);
-        if (lane >= (uint32_t)d) inc += o;
-    }
-    const uint32_t tot = __shfl(inc, 63, 64);
-    uint32_t wbase = 0;
-    if (lane == 63 && tot) wbase = atomicAdd(count, tot);
-    wbase = __shfl(wbase, 63, 64);
-    uint32_t at = wbase + inc - c;
-    for (uint32_t m = mask; m; m &= m - 1) list[at++] = (uint16_t)fr_li(tid, __ffs(m) - 1);
+// Block-wide "any" with one barrier: each wave's ballot lands in one of two
+// alternating flag rows (a row is rewritten only two rounds later, after
+// every thread has read it).
+struct FrAny {
+    uint32_t f[2][4];
+};
+__device__ __forceinline__ bool fr_block_any(bool p, FrAny &a, uint32_t &par) {
+    const bool w = __ballot(p) != 0;
+    a.f[par][threadIdx.x >> 6] = w ? 1u : 0u;   // every lane of the wave stores the same value
+    __syncthreads();
+    const u32x4f v = *(const u32x4f *)a.f[par];
+    par ^= 1u;
+    return (v.x | v.y | v.z | v.w) != 0;
 }
 
 // ---------------------------------------------------------------------------
 // k_fr_exits
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
-                                                   uint32_t *exitS) {
-    __shared__ __attribute__((aligned(16))) uint32_t J[2][kFChunk];
-    __shared__ uint16_t act[kFChunk];
-    __shared__ uint32_t nact;
+// Sub-chunks from last to first.  A word whose next mark stays inside the
+// sub-chunk is active: its LDS pointer jumps (in place: a value read early is
+// still a successor on the same chain) until it leaves.  A pointer into a
+// later sub-chunk of the super-chunk resolves through that sub-chunk's exits,
+// which this block already wrote to exitS (L2; never read before, so no
+// stale L1 line).  16 KiB of LDS, so several blocks share a CU.  Here thread
+// t owns words 4 t + 1024 k + c (k, c < 4): every 16-byte load and store of
+// a wave covers 1 KiB contiguously, and the pointer rounds' own-word LDS
+// accesses of neighbouring lanes fall in neighbouring banks.
+__device__ __forceinline__ uint32_t fr_cw(uint32_t tid, int i) { return 4 * tid + 1024 * (i >> 2) + (i & 3); }
+
+__global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
+                                                      uint32_t *exitS) {
+    __shared__ __attribute__((aligned(16))) uint32_t J[kFChunk];
+    __shared__ __attribute__((aligned(16))) FrAny any;
     const uint32_t tid = threadIdx.x;
     const uint32_t sbeg = blockIdx.x * kFSuper;
     const uint32_t send = min(sbeg + kFSuper, Q);
     const uint32_t sfin = sbeg + kFSuper;   // exits are chain words >= sfin (or == Q)
     const uint32_t nsub = (send - sbeg + kFChunk - 1) / kFChunk;
+    uint32_t par = 0;
     uint32_t x[16], y[16];
-    fr_load16(w, Q, sbeg + (nsub - 1) * kFChunk, tid, x);
-    int cur = 0;
+    auto load = [&](uint32_t base, uint32_t (&r)[16]) {
+        if (base + kFChunk <= Q) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const u32x4f v = __builtin_nontemporal_load((const u32x4f *)(w + base + 4 * tid + 1024 * k));
+                r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) r[i] = base + fr_cw(tid, i) < Q ? w[base + fr_cw(tid, i)] : 0u;
+        }
+    };
+    load(sbeg + (nsub - 1) * kFChunk, x);
     for (int j = (int)nsub - 1; j >= 0; --j) {
         const uint32_t base = sbeg + (uint32_t)j * kFChunk;
         const uint32_t bend = base + kFChunk;
-        if (j > 0) fr_load16(w, Q, base - kFChunk, tid, y);   // next sub-chunk's words in flight
-        uint32_t *Jc = J[cur];
-        const uint32_t *Jp = J[cur ^ 1];                       // exits of sub-chunk j + 1
-        if (tid == 0) nact = 0;
-        __syncthreads();
-        uint32_t t[16], mask = 0;
+        if (j > 0) load(base - kFChunk, y);   // next sub-chunk's words in flight
+        uint32_t t[16], act = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const uint32_t q = base + fr_li(tid, i);
-            uint32_t v = kFStop;
-            if (q < Q) {
-                v = fr_next(fr_bswap(x[i]), q, Q, tb);
-                if (v < sfin && v < Q) {   // a word (terminals are >= kFUnal > sfin)
-                    if (v >= bend) v = v < bend + kFChunk ? Jp[v - bend] : exitS[v];   // final exits
-                    else mask |= 1u << i;
-                }
-            }
+            const uint32_t q = base + fr_cw(tid, i);
+            const uint32_t v = q < Q ? fr_next(fr_bswap(x[i]), q, Q, tb) : kFStop;
+            act |= (v < bend ? 1u : 0u) << i;   // v < bend: a word inside (terminals are >= kFUnal)
             t[i] = v;
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            *(u32x4f *)&Jc[4 * tid + 1024 * k] = u32x4f{t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
-        fr_append16(mask, tid, act, &nact);
-        __syncthreads();
-        // pointer jumping over the words whose pointer stays inside (in place:
-        // a value read early is still a successor on the same chain)
-        const uint32_t na = nact;
-        for (;;) {
-            int mv = 0;
-            for (uint32_t a = tid; a < na; a += 256) {
-                const uint32_t li = act[a];
-                const uint32_t v = Jc[li];
-                if (v - base < kFChunk) {
-                    const uint32_t u = Jc[v - base];
-                    Jc[li] = u;
-                    mv |= u - base < kFChunk;
-                }
-            }
-            if (!__syncthreads_or(mv)) break;
-        }
+        for (int i = 0; i < 16; ++i)   // final exits of later sub-chunks' words
+            if (t[i] >= bend && t[i] < sfin && t[i] < Q) t[i] = exitS[t[i]];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t l0 = 4 * tid + 1024 * k;
-            const u32x4f v = *(const u32x4f *)&Jc[l0];
-            if (base + l0 + 4 <= Q) {
-                *(u32x4f *)(exitS + base + l0) = v;
-            } else {
-                if (base + l0 < Q) exitS[base + l0] = v.x;
-                if (base + l0 + 1 < Q) exitS[base + l0 + 1] = v.y;
-                if (base + l0 + 2 < Q) exitS[base + l0 + 2] = v.z;
+        for (int k = 0; k < 4; ++k)
+            *(u32x4f *)&J[4 * tid + 1024 * k] = u32x4f{t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
+        __syncthreads();
+        for (;;) {
+            for (uint32_t m = act; m; m &= m - 1) {
+                const int i = __ffs(m) - 1;
+                const uint32_t li = fr_cw(tid, i);
+                const uint32_t u = J[J[li] - base];
+                J[li] = u;
+                if (u - base >= kFChunk) act &= ~(1u << i);
             }
+            if (!fr_block_any(act != 0, any, par)) break;
         }
-        cur ^= 1;
+        if (base + kFChunk <= Q) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                *(u32x4f *)(exitS + base + 4 * tid + 1024 * k) = *(const u32x4f *)&J[4 * tid + 1024 * k];
+        } else {
+            for (int i = 0; i < 16; ++i)
+                if (base + fr_cw(tid, i) < Q) exitS[base + fr_cw(tid, i)] = J[fr_cw(tid, i)];
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = y[i];
-        __syncthreads();   // exitS of this sub-chunk visible to the block's later gathers
+        __syncthreads();   // this sub-chunk's exitS visible to the block; J free again
     }
 }
 
@@ -264,16 +264,41 @@ __global__ __launch_bounds__(256) void k_fr_fix_fill(const uint32_t *exitS, cons
 // k_fr_mark: per sub-chunk bitmaps of the complete chain fragments and their
 // LAST flags, counts and in-super prefixes.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_fr_mark(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
-                                                  const uint32_t *sentry, const uint64_t *res, FrameSub *sub,
-                                                  uint32_t *fbits, uint32_t *lbits, FrameSuper *sup) {
-    __shared__ __attribute__((aligned(16))) uint32_t J[2][kFChunk];
-    __shared__ __attribute__((aligned(16))) uint8_t on[kFChunk];
-    __shared__ __attribute__((aligned(16))) uint8_t fl[kFChunk];   // bit 0: complete fragment, bit 1: LAST
-    __shared__ uint16_t act[kFChunk];
-    __shared__ uint32_t fbw[kFChunk / 32], lbw[kFChunk / 32];
-    __shared__ uint32_t nact, red[3][4];
-    __shared__ uint32_t e_next, lastpos;
+// Marking by pointer doubling over sub-chunk-local u16 pointers (kFOut = the
+// pointer leaves the sub-chunk), double-buffered: round r reads J^(2^r) and
+// marks the node 2^r hops past every marked node, so after round r every
+// chain node < 2^(r+1) hops from the entry is marked.  A word whose pointer
+// left copies the sentinel into the other buffer once more before it drops
+// out, so both buffers agree on it.  Thread t's 16 marks are one 16-byte LDS
+// read; its 16-bit masks are the bitmaps' u16 piece t.
+constexpr uint32_t kFOut = 0xffffu;
+struct FrWaveStat {
+    uint32_t cnt;         // complete fragments | LAST ones << 16
+    uint32_t lastpos;     // 1 + sub-chunk position of its last LAST fragment (0: none)
+    uint32_t upto;        // complete fragments through that one
+    uint32_t tail;        // 1 + (position << 1 | LAST flag) of its last complete fragment (0: none)
+};
+__device__ __forceinline__ uint32_t fr_wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t fr_wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+    return v;
+}
+// bytes b0..b3 of w, each 0 or 1, as bits 0..3
+__device__ __forceinline__ uint32_t fr_bytes01(uint32_t w) { return (w * 0x01020408u) >> 24 & 0xfu; }
+
+__global__ __launch_bounds__(256, 6) void k_fr_mark(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
+                                                     const uint32_t *sentry, const uint64_t *res, FrameSub *sub,
+                                                     uint32_t *fbits, uint32_t *lbits, FrameSuper *sup) {
+    __shared__ __attribute__((aligned(16))) uint16_t J[2][kFChunk];
+    __shared__ __attribute__((aligned(16))) uint8_t on[kFChunk + 64];   // + one dummy byte per lane
+    __shared__ __attribute__((aligned(16))) FrAny any;
+    __shared__ FrWaveStat ws[4];
+    __shared__ uint32_t e_next;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t s = blockIdx.x;
     const uint32_t sbeg = s * kFSuper;
@@ -283,154 +308,119 @@ __global__ __launch_bounds__(256) void k_fr_mark(const uint32_t *__restrict__ w,
     uint32_t e = res[0] == kFUnal ? kFNone : sentry[s];   // kFNone: no chain word in this super-chunk
     uint32_t pre_f = 0, pre_l = 0, tail = 2;   // tail: LAST flag of the super's last fragment (2 = none yet)
     uint32_t lastlast = 0, has_ll = 0;         // in-super count up to and including its last LAST fragment
+    uint32_t par = 0;
     uint32_t x[16], y[16];
     uint32_t held = ~0u;                       // sub-chunk whose words x holds
     for (uint32_t j = 0; j < nsub; ++j) {
         const uint32_t base = sbeg + j * kFChunk;
         const uint32_t bend = base + kFChunk;
+        const uint32_t q0 = base + 16 * tid;
         FrameSub info;
         info.pre_frag = pre_f;
         info.pre_last = pre_l;
         info.prev_tail = tail;
         info.nfrag = info.nlast = info.upto_ll = info.has_ll = info.rsv = 0;
+        uint16_t *fb16 = (uint16_t *)fbits + (sub0 + j) * (kFChunk / 16);
+        uint16_t *lb16 = (uint16_t *)lbits + (sub0 + j) * (kFChunk / 16);
         if (e >= bend || e >= Q) {   // the chain skips this sub-chunk (or has ended)
             if (tid == 0) sub[sub0 + j] = info;
-            if (tid < kFChunk / 32) { fbits[(sub0 + j) * 128 + tid] = 0; lbits[(sub0 + j) * 128 + tid] = 0; }
+            fb16[tid] = 0;
+            lb16[tid] = 0;
             continue;
         }
-        if (held != j) fr_load16(w, Q, base, tid, x);
-        if (j + 1 < nsub) { fr_load16(w, Q, bend, tid, y); held = j + 1; }   // next sub-chunk in flight
-        if (tid == 0) { nact = 0; e_next = kFStop; lastpos = 0; }
-        __syncthreads();
-        uint32_t t[16], mask = 0, fo[4] = {0, 0, 0, 0}, ff[4] = {0, 0, 0, 0};
+        if (held != j) fr_load(w, Q, base, tid, x);
+        if (j + 1 < nsub) { fr_load(w, Q, bend, tid, y); held = j + 1; }   // next sub-chunk in flight
+        uint32_t act = 0, cf = 0, lf = 0, lv = 0;   // per word: active / complete fragment / LAST / next leaves
+        uint32_t p[8];                              // local pointers, two u16 per register
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const uint32_t q = base + fr_li(tid, i);
-            uint32_t v = kFStop, f = 0;
-            if (q < Q) {
-                const uint32_t m = fr_bswap(x[i]);
-                v = fr_next(m, q, Q, tb);
-                f = (v < kFUnal ? 1u : 0u) | ((m >> 31) << 1);
-                if (v < bend) mask |= 1u << i;   // v < bend < kFUnal: a word inside
-            }
-            t[i] = v;
-            ff[i >> 2] |= f << (8 * (i & 3));
-            fo[i >> 2] |= (q == e ? 1u : 0u) << (8 * (i & 3));
+            const uint32_t q = q0 + i;
+            const uint32_t m = fr_bswap(x[i]);
+            const uint32_t v = q < Q ? fr_next(m, q, Q, tb) : kFStop;
+            cf |= (v < kFUnal ? 1u : 0u) << i;
+            lf |= (q < Q ? m >> 31 : 0u) << i;
+            lv |= (v >= bend ? 1u : 0u) << i;       // v < bend: a word inside (v > q >= base)
+            const uint32_t pi = v < bend ? v - base : kFOut;
+            if (i & 1) p[i >> 1] |= pi << 16; else p[i >> 1] = pi;
         }
+        act = ~lv & 0xffffu;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t l0 = 4 * tid + 1024 * k;
-            const u32x4f v{t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
-            *(u32x4f *)&J[0][l0] = v;
-            *(u32x4f *)&J[1][l0] = v;
-            *(uint32_t *)&on[l0] = fo[k];
-            *(uint32_t *)&fl[l0] = ff[k];
+        for (int b = 0; b < 2; ++b) {
+            *(u32x4f *)&J[b][16 * tid] = u32x4f{p[0], p[1], p[2], p[3]};
+            *(u32x4f *)&J[b][16 * tid + 8] = u32x4f{p[4], p[5], p[6], p[7]};
         }
-        fr_append16(mask, tid, act, &nact);
+        {   // the entry's mark
+            const uint32_t d = e - q0;
+            uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[k] = d >> 2 == (uint32_t)k ? 1u << (8 * (d & 3)) : 0u;
+            *(u32x4f *)&on[16 * tid] = u32x4f{o[0], o[1], o[2], o[3]};
+        }
         __syncthreads();
-        // pointer doubling with marking: round r marks the nodes 2^r hops past
-        // every marked node, so after round r every chain node < 2^(r+1) hops
-        // from e is marked (double-buffered pointers: round r reads next^(2^r))
-        const uint32_t na = nact;
-        int cur = 0;
+        if (tid == 0) e_next = kFStop;   // every thread read the previous value before this barrier
+        uint32_t cur = 0;
         for (;;) {
-            int mv = 0;
-            const uint32_t *Jc = J[cur];
-            uint32_t *Jn = J[cur ^ 1];
-            for (uint32_t a = tid; a < na; a += 256) {
-                const uint32_t li = act[a];
+            bool mv = false;
+            const uint16_t *Jc = J[cur];
+            uint16_t *Jn = J[cur ^ 1];
+            for (uint32_t m = act; m; m &= m - 1) {
+                const uint32_t i = __ffs(m) - 1;
+                const uint32_t li = 16 * tid + i;
                 const uint32_t v = Jc[li];
-                if (v - base < kFChunk) {
-                    if (on[li]) on[v - base] = 1;
-                    const uint32_t u = Jc[v - base];
-                    Jn[li] = u;
-                    mv |= u - base < kFChunk;
-                } else {
-                    Jn[li] = v;
-                }
+                const bool in = v != kFOut;
+                const uint32_t vv = in ? v : li;
+                const bool o = on[li] != 0;
+                on[in && o ? v : kFChunk + lane] = 1;
+                const uint32_t u = Jc[vv];
+                Jn[li] = (uint16_t)(in ? u : kFOut);
+                act &= in ? ~0u : ~(1u << i);
+                mv |= in && u != kFOut;
             }
             cur ^= 1;
-            if (!__syncthreads_or(mv)) break;
+            if (!fr_block_any(mv, any, par)) break;
         }
-        // bitmaps (word k = words 32k .. 32k+31), counts, the last LAST fragment
-        uint32_t cf = 0, cl = 0;
-        if (tid < kFChunk / 32) {
-            uint32_t fb = 0, lb = 0;
-#pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                const uint32_t o = *(const uint32_t *)&on[32 * tid + 4 * g];
-                const uint32_t f = *(const uint32_t *)&fl[32 * tid + 4 * g] & (o * 3u);   // only marked words
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const uint32_t v = (f >> (8 * c)) & 3u;
-                    fb |= (v & 1u) << (4 * g + c);
-                    lb |= ((v >> 1) & v & 1u) << (4 * g + c);
-                }
-            }
-            fbw[tid] = fb;
-            lbw[tid] = lb;
-            fbits[(sub0 + j) * 128 + tid] = fb;
-            lbits[(sub0 + j) * 128 + tid] = lb;
-            cf = __popc(fb);
-            cl = __popc(lb);
-            if (lb) atomicMax(&lastpos, 32 * tid + (31 - __clz(lb)) + 1);
+        // this thread's marks -> bitmaps, counts, the chain's exit
+        const u32x4f ob = *(const u32x4f *)&on[16 * tid];
+        const uint32_t om = fr_bytes01(ob.x) | fr_bytes01(ob.y) << 4 | fr_bytes01(ob.z) << 8 | fr_bytes01(ob.w) << 12;
+        const uint32_t oc = om & cf, ol = oc & lf;
+        fb16[tid] = (uint16_t)oc;
+        lb16[tid] = (uint16_t)ol;
+        if (om & lv) {   // the marked node whose next leaves the sub-chunk (terminals too): one thread
+            const uint32_t q = q0 + __ffs(om & lv) - 1;
+            e_next = q < Q ? fr_next(fr_bswap(w[q]), q, Q, tb) : kFStop;
         }
-        // the chain's exit: the marked node whose own next leaves the sub-chunk
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t o = *(const uint32_t *)&on[4 * tid + 1024 * k];
-            if (!o) continue;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (((o >> (8 * c)) & 1u) && t[4 * k + c] >= bend) e_next = t[4 * k + c];   // terminals too
-        }
-        for (int d = 32; d > 0; d >>= 1) {
-            cf += __shfl_xor(cf, d, 64);
-            cl += __shfl_xor(cl, d, 64);
-        }
-        if (lane == 0) { red[0][wv] = cf; red[1][wv] = cl; }
+        const uint32_t cnt = fr_wave_sum(__popc(oc) | __popc(ol) << 16);
+        const uint32_t lastpos = fr_wave_max(ol ? 16 * tid + (32 - __clz(ol)) : 0u);
+        const uint32_t k = lastpos > 16 * tid ? min(lastpos - 16 * tid, 16u) : 0u;
+        const uint32_t upto = fr_wave_sum(__popc(oc & ((1u << k) - 1u)));
+        const uint32_t hb = 31 - __clz(oc);
+        const uint32_t tl_w = fr_wave_max(oc ? 1 + ((16 * tid + hb) << 1 | ((ol >> hb) & 1u)) : 0u);
+        if (lane == 0) ws[wv] = FrWaveStat{cnt, lastpos, upto, tl_w};
         __syncthreads();
-        const uint32_t nf = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-        const uint32_t nl = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-        const uint32_t lp = lastpos;
-        // fragments up to and including the last LAST one (for the incomplete-tail cut)
-        uint32_t upto = 0;
-        if (lp && tid < kFChunk / 32) {
-            const uint32_t fb = fbw[tid];
-            const uint32_t lo = 32 * tid;
-            if (lo + 32 <= lp) upto = __popc(fb);
-            else if (lo < lp) upto = __popc(fb & (0xffffffffu >> (32 - (lp - lo))));
+        uint32_t tnf = 0, tnl = 0, tl = tail, up = 0, lp = 0;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const FrWaveStat st = ws[v];
+            if (st.lastpos) { lp = st.lastpos; up = tnf + st.upto; }
+            tnf += st.cnt & 0xffffu;
+            tnl += st.cnt >> 16;
+            if (st.tail) tl = (st.tail - 1) & 1u;
         }
-        for (int d = 32; d > 0; d >>= 1) upto += __shfl_xor(upto, d, 64);
-        if (lane == 0) red[2][wv] = upto;
-        // LAST flag of the last complete fragment (from the LDS bitmaps)
-        uint32_t tl = tail;
-        if (nf) {
-            for (int k = kFChunk / 32 - 1; k >= 0; --k) {
-                const uint32_t fb = fbw[k];
-                if (fb) {
-                    tl = (lbw[k] >> (31 - __clz(fb))) & 1u;
-                    break;
-                }
-            }
-        }
-        __syncthreads();
-        info.nfrag = nf;
-        info.nlast = nl;
+        info.nfrag = tnf;
+        info.nlast = tnl;
         if (lp) {
             info.has_ll = 1;
-            info.upto_ll = red[2][0] + red[2][1] + red[2][2] + red[2][3];
+            info.upto_ll = up;
             has_ll = 1;
-            lastlast = pre_f + info.upto_ll;
+            lastlast = pre_f + up;
         }
-        tail = tl;
         if (tid == 0) sub[sub0 + j] = info;
-        pre_f += nf;
-        pre_l += nl;
         e = e_next;
+        tail = tl;
+        pre_f += tnf;
+        pre_l += tnl;
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = y[i];
-        __syncthreads();
     }
     if (tid == 0) {
         FrameSuper v;
