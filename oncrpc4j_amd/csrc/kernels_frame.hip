@@ -58,22 +58,22 @@ __device__ __forceinline__ uint32_t fr_next(uint32_t m, uint32_t q, uint32_t Q, 
 }
 
 // Word layout of a sub-chunk (kFChunk = 4096 words, 256 threads): thread t
-// owns the 16 consecutive words [16 t, 16 t + 16) — four 16-byte loads, one
-// 16-byte LDS access per 4 words, and its per-word bits form one 16-bit
-// piece of the sub-chunk's bitmaps.
+// owns words 4 t + 1024 k + c (k, c < 4), so every 16-byte load and store of
+// a wave covers 1 KiB contiguously and the own-word LDS accesses of
+// neighbouring lanes fall in neighbouring banks.  (Sixteen consecutive words
+// per thread measured slower: 16-byte accesses 64 bytes apart.)
 typedef uint32_t u32x4f __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void fr_load(const uint32_t *w, uint32_t Q, uint32_t base, uint32_t tid, uint32_t (&x)[16]) {
-    const uint32_t q0 = base + 16 * tid;
-    if (q0 + 16 <= Q) {
+__device__ __forceinline__ uint32_t fr_cw(uint32_t tid, int i) { return 4 * tid + 1024 * (i >> 2) + (i & 3); }
+__device__ __forceinline__ void fr_cload(const uint32_t *w, uint32_t Q, uint32_t base, uint32_t tid, uint32_t (&r)[16]) {
+    if (base + kFChunk <= Q) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const u32x4f v = __builtin_nontemporal_load((const u32x4f *)(w + q0 + 4 * k));
-            x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+            const u32x4f v = __builtin_nontemporal_load((const u32x4f *)(w + base + 4 * tid + 1024 * k));
+            r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) x[i] = q0 + i < Q ? w[q0 + i] : 0u;
+        for (int i = 0; i < 16; ++i) r[i] = base + fr_cw(tid, i) < Q ? w[base + fr_cw(tid, i)] : 0u;
     }
 }
 
@@ -100,12 +100,7 @@ __device__ __forceinline__ bool fr_block_any(bool p, FrAny &a, uint32_t &par) {
 // still a successor on the same chain) until it leaves.  A pointer into a
 // later sub-chunk of the super-chunk resolves through that sub-chunk's exits,
 // which this block already wrote to exitS (L2; never read before, so no
-// stale L1 line).  16 KiB of LDS, so several blocks share a CU.  Here thread
-// t owns words 4 t + 1024 k + c (k, c < 4): every 16-byte load and store of
-// a wave covers 1 KiB contiguously, and the pointer rounds' own-word LDS
-// accesses of neighbouring lanes fall in neighbouring banks.
-__device__ __forceinline__ uint32_t fr_cw(uint32_t tid, int i) { return 4 * tid + 1024 * (i >> 2) + (i & 3); }
-
+// stale L1 line).  16 KiB of LDS, so several blocks share a CU.
 __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
                                                       uint32_t *exitS) {
     __shared__ __attribute__((aligned(16))) uint32_t J[kFChunk];
@@ -117,23 +112,11 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
     const uint32_t nsub = (send - sbeg + kFChunk - 1) / kFChunk;
     uint32_t par = 0;
     uint32_t x[16], y[16];
-    auto load = [&](uint32_t base, uint32_t (&r)[16]) {
-        if (base + kFChunk <= Q) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const u32x4f v = __builtin_nontemporal_load((const u32x4f *)(w + base + 4 * tid + 1024 * k));
-                r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) r[i] = base + fr_cw(tid, i) < Q ? w[base + fr_cw(tid, i)] : 0u;
-        }
-    };
-    load(sbeg + (nsub - 1) * kFChunk, x);
+    fr_cload(w, Q, sbeg + (nsub - 1) * kFChunk, tid, x);
     for (int j = (int)nsub - 1; j >= 0; --j) {
         const uint32_t base = sbeg + (uint32_t)j * kFChunk;
         const uint32_t bend = base + kFChunk;
-        if (j > 0) load(base - kFChunk, y);   // next sub-chunk's words in flight
+        if (j > 0) fr_cload(w, Q, base - kFChunk, tid, y);   // next sub-chunk's words in flight
         uint32_t t[16], act = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -264,19 +247,19 @@ __global__ __launch_bounds__(256) void k_fr_fix_fill(const uint32_t *exitS, cons
 // k_fr_mark: per sub-chunk bitmaps of the complete chain fragments and their
 // LAST flags, counts and in-super prefixes.
 // ---------------------------------------------------------------------------
-// Marking by pointer doubling over sub-chunk-local u16 pointers (kFOut = the
-// pointer leaves the sub-chunk), double-buffered: round r reads J^(2^r) and
-// marks the node 2^r hops past every marked node, so after round r every
-// chain node < 2^(r+1) hops from the entry is marked.  A word whose pointer
-// left copies the sentinel into the other buffer once more before it drops
-// out, so both buffers agree on it.  Thread t's 16 marks are one 16-byte LDS
-// read; its 16-bit masks are the bitmaps' u16 piece t.
+// The chain inside a sub-chunk, from its entry: by pruning (below), or by
+// pointer doubling over sub-chunk-local u16 pointers (kFOut = the pointer
+// leaves the sub-chunk) when pruning has not settled in kFPruneRounds.  The
+// bitmaps are written as 16-bit pieces (16 consecutive words), each
+// assembled from 4 lanes' nibbles.
 constexpr uint32_t kFOut = 0xffffu;
-struct FrWaveStat {
+constexpr int kFPruneRounds = 4;   // then pointer doubling
+struct FrWaveStat {       // wave v's words: bands [1024 k + 256 v, +256), k < 4
     uint32_t cnt;         // complete fragments | LAST ones << 16
     uint32_t lastpos;     // 1 + sub-chunk position of its last LAST fragment (0: none)
-    uint32_t upto;        // complete fragments through that one
+    uint32_t upto;        // its complete fragments before lastpos
     uint32_t tail;        // 1 + (position << 1 | LAST flag) of its last complete fragment (0: none)
+    uint32_t band[2];     // complete fragments per band k (u16 each)
 };
 __device__ __forceinline__ uint32_t fr_wave_sum(uint32_t v) {
 #pragma unroll
@@ -291,11 +274,12 @@ __device__ __forceinline__ uint32_t fr_wave_max(uint32_t v) {
 // bytes b0..b3 of w, each 0 or 1, as bits 0..3
 __device__ __forceinline__ uint32_t fr_bytes01(uint32_t w) { return (w * 0x01020408u) >> 24 & 0xfu; }
 
-__global__ __launch_bounds__(256, 6) void k_fr_mark(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
+__global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
                                                      const uint32_t *sentry, const uint64_t *res, FrameSub *sub,
                                                      uint32_t *fbits, uint32_t *lbits, FrameSuper *sup) {
     __shared__ __attribute__((aligned(16))) uint16_t J[2][kFChunk];
     __shared__ __attribute__((aligned(16))) uint8_t on[kFChunk + 64];   // + one dummy byte per lane
+    __shared__ __attribute__((aligned(16))) uint8_t pred[kFChunk];
     __shared__ __attribute__((aligned(16))) FrAny any;
     __shared__ FrWaveStat ws[4];
     __shared__ uint32_t e_next;
@@ -314,7 +298,6 @@ __global__ __launch_bounds__(256, 6) void k_fr_mark(const uint32_t *__restrict__
     for (uint32_t j = 0; j < nsub; ++j) {
         const uint32_t base = sbeg + j * kFChunk;
         const uint32_t bend = base + kFChunk;
-        const uint32_t q0 = base + 16 * tid;
         FrameSub info;
         info.pre_frag = pre_f;
         info.pre_last = pre_l;
@@ -328,13 +311,13 @@ __global__ __launch_bounds__(256, 6) void k_fr_mark(const uint32_t *__restrict__
             lb16[tid] = 0;
             continue;
         }
-        if (held != j) fr_load(w, Q, base, tid, x);
-        if (j + 1 < nsub) { fr_load(w, Q, bend, tid, y); held = j + 1; }   // next sub-chunk in flight
+        if (held != j) fr_cload(w, Q, base, tid, x);
+        if (j + 1 < nsub) { fr_cload(w, Q, bend, tid, y); held = j + 1; }   // next sub-chunk in flight
         uint32_t act = 0, cf = 0, lf = 0, lv = 0;   // per word: active / complete fragment / LAST / next leaves
         uint32_t p[8];                              // local pointers, two u16 per register
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const uint32_t q = q0 + i;
+            const uint32_t q = base + fr_cw(tid, i);
             const uint32_t m = fr_bswap(x[i]);
             const uint32_t v = q < Q ? fr_next(m, q, Q, tb) : kFStop;
             cf |= (v < kFUnal ? 1u : 0u) << i;
@@ -344,68 +327,145 @@ __global__ __launch_bounds__(256, 6) void k_fr_mark(const uint32_t *__restrict__
             if (i & 1) p[i >> 1] |= pi << 16; else p[i >> 1] = pi;
         }
         act = ~lv & 0xffffu;
+        typedef uint32_t u32x2f __attribute__((ext_vector_type(2)));
+        uint32_t eb = 0;   // the entry among this thread's words
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            *(u32x4f *)&J[b][16 * tid] = u32x4f{p[0], p[1], p[2], p[3]};
-            *(u32x4f *)&J[b][16 * tid + 8] = u32x4f{p[4], p[5], p[6], p[7]};
-        }
-        {   // the entry's mark
-            const uint32_t d = e - q0;
-            uint32_t o[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) o[k] = d >> 2 == (uint32_t)k ? 1u << (8 * (d & 3)) : 0u;
-            *(u32x4f *)&on[16 * tid] = u32x4f{o[0], o[1], o[2], o[3]};
+        for (int kk = 0; kk < 4; ++kk) {
+            const uint32_t li = 4 * tid + 1024 * kk;
+            const uint32_t d = e - base - li;
+            eb |= (d < 4 ? 1u << d : 0u) << (4 * kk);
+            *(u32x2f *)&J[0][li] = u32x2f{p[2 * kk], p[2 * kk + 1]};
+            *(uint32_t *)&on[li] = d < 4 ? 1u << (8 * d) : 0u;
+            *(uint32_t *)&pred[li] = 0;
         }
         __syncthreads();
         if (tid == 0) e_next = kFStop;   // every thread read the previous value before this barrier
-        uint32_t cur = 0;
-        for (;;) {
-            bool mv = false;
-            const uint16_t *Jc = J[cur];
-            uint16_t *Jn = J[cur ^ 1];
-            for (uint32_t m = act; m; m &= m - 1) {
-                const uint32_t i = __ffs(m) - 1;
-                const uint32_t li = 16 * tid + i;
-                const uint32_t v = Jc[li];
-                const bool in = v != kFOut;
-                const uint32_t vv = in ? v : li;
-                const bool o = on[li] != 0;
-                on[in && o ? v : kFChunk + lane] = 1;
-                const uint32_t u = Jc[vv];
-                Jn[li] = (uint16_t)(in ? u : kFOut);
-                act &= in ? ~0u : ~(1u << i);
-                mv |= in && u != kFOut;
+        // S = the entry and every inside target; then drop the nodes with no
+        // predecessor in S until nothing changes.  Every node left reaches back
+        // to the entry (positions fall along predecessors), every chain node
+        // stays: S is the chain.  Rounds = the longest false chain + 1.
+        for (uint32_t m = act; m; m &= m - 1) on[J[0][fr_cw(tid, __ffs(m) - 1)]] = 1;
+        __syncthreads();
+        uint32_t om = 0;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) om |= fr_bytes01(*(const uint32_t *)&on[4 * tid + 1024 * kk]) << (4 * kk);
+        bool settled = false;
+        for (int r = 0; r < kFPruneRounds; ++r) {
+            for (uint32_t m = om & act; m; m &= m - 1) pred[J[0][fr_cw(tid, __ffs(m) - 1)]] = 1;
+            __syncthreads();
+            uint32_t pm = 0;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const uint32_t li = 4 * tid + 1024 * kk;
+                pm |= fr_bytes01(*(const uint32_t *)&pred[li]) << (4 * kk);
+                *(uint32_t *)&pred[li] = 0;   // pushes of the next round come after the barrier below
             }
-            cur ^= 1;
-            if (!fr_block_any(mv, any, par)) break;
+            const uint32_t nm = om & (pm | eb);
+            const bool ch = nm != om;
+            om = nm;
+            if (!fr_block_any(ch, any, par)) { settled = true; break; }
         }
-        // this thread's marks -> bitmaps, counts, the chain's exit
-        const u32x4f ob = *(const u32x4f *)&on[16 * tid];
-        const uint32_t om = fr_bytes01(ob.x) | fr_bytes01(ob.y) << 4 | fr_bytes01(ob.z) << 8 | fr_bytes01(ob.w) << 12;
+        if (!settled) {
+            // long false chains (bodies full of small integers): pointer
+            // doubling with marking, double-buffered: round r reads J^(2^r) and
+            // marks the node 2^r hops past every marked node, so after round r
+            // every chain node < 2^(r+1) hops from the entry is marked.  A word
+            // whose pointer left copies the sentinel into the other buffer once
+            // more before it drops out, so both buffers agree on it.
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const uint32_t li = 4 * tid + 1024 * kk;
+                *(u32x2f *)&J[1][li] = *(const u32x2f *)&J[0][li];
+                const uint32_t d = e - base - li;
+                *(uint32_t *)&on[li] = d < 4 ? 1u << (8 * d) : 0u;
+            }
+            __syncthreads();
+            uint32_t cur = 0;
+            for (;;) {
+                bool mv = false;
+                const uint16_t *Jc = J[cur];
+                uint16_t *Jn = J[cur ^ 1];
+                for (uint32_t m = act; m; m &= m - 1) {
+                    const int i = __ffs(m) - 1;
+                    const uint32_t li = fr_cw(tid, i);
+                    const uint32_t v = Jc[li];
+                    const bool in = v != kFOut;
+                    const uint32_t vv = in ? v : li;
+                    const bool o = on[li] != 0;
+                    on[in && o ? v : kFChunk + lane] = 1;
+                    const uint32_t u = Jc[vv];
+                    Jn[li] = (uint16_t)(in ? u : kFOut);
+                    act &= in ? ~0u : ~(1u << i);
+                    mv |= in && u != kFOut;
+                }
+                cur ^= 1;
+                if (!fr_block_any(mv, any, par)) break;
+            }
+            om = 0;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) om |= fr_bytes01(*(const uint32_t *)&on[4 * tid + 1024 * kk]) << (4 * kk);
+        }
+        // this thread's chain words -> bitmaps, counts, the chain's exit
         const uint32_t oc = om & cf, ol = oc & lf;
-        fb16[tid] = (uint16_t)oc;
-        lb16[tid] = (uint16_t)ol;
+        {   // bitmap piece (16 words) k = lane & 3 of lane group g = lane >> 2: nibble k of lanes 4g..4g+3
+            const uint32_t g4 = lane & ~3u, kk = lane & 3u;
+            uint32_t pc = 0, pl = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                pc |= ((__shfl(oc, g4 + c, 64) >> (4 * kk)) & 0xfu) << (4 * c);
+                pl |= ((__shfl(ol, g4 + c, 64) >> (4 * kk)) & 0xfu) << (4 * c);
+            }
+            const uint32_t pi = 64 * kk + 16 * wv + (lane >> 2);   // words [16 pi, 16 pi + 16)
+            fb16[pi] = (uint16_t)pc;
+            lb16[pi] = (uint16_t)pl;
+        }
         if (om & lv) {   // the marked node whose next leaves the sub-chunk (terminals too): one thread
-            const uint32_t q = q0 + __ffs(om & lv) - 1;
+            const uint32_t q = base + fr_cw(tid, __ffs(om & lv) - 1);
             e_next = q < Q ? fr_next(fr_bswap(w[q]), q, Q, tb) : kFStop;
         }
         const uint32_t cnt = fr_wave_sum(__popc(oc) | __popc(ol) << 16);
-        const uint32_t lastpos = fr_wave_max(ol ? 16 * tid + (32 - __clz(ol)) : 0u);
-        const uint32_t k = lastpos > 16 * tid ? min(lastpos - 16 * tid, 16u) : 0u;
-        const uint32_t upto = fr_wave_sum(__popc(oc & ((1u << k) - 1u)));
+        const uint32_t b01 = fr_wave_sum(__popc(oc & 0xfu) | __popc(oc & 0xf0u) << 16);
+        const uint32_t b23 = fr_wave_sum(__popc(oc & 0xf00u) | __popc(oc & 0xf000u) << 16);
+        const uint32_t lastpos = fr_wave_max(ol ? fr_cw(tid, 31 - __clz(ol)) + 1 : 0u);
+        uint32_t below = 0;   // words of this thread before lastpos
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const uint32_t p0 = 4 * tid + 1024 * kk;
+            const uint32_t nb = lastpos > p0 ? min(lastpos - p0, 4u) : 0u;
+            below |= ((1u << nb) - 1u) << (4 * kk);
+        }
+        const uint32_t upto = fr_wave_sum(__popc(oc & below));
         const uint32_t hb = 31 - __clz(oc);
-        const uint32_t tl_w = fr_wave_max(oc ? 1 + ((16 * tid + hb) << 1 | ((ol >> hb) & 1u)) : 0u);
-        if (lane == 0) ws[wv] = FrWaveStat{cnt, lastpos, upto, tl_w};
+        const uint32_t tl_w = fr_wave_max(oc ? 1 + (fr_cw(tid, hb) << 1 | ((ol >> hb) & 1u)) : 0u);
+        if (lane == 0) ws[wv] = FrWaveStat{cnt, lastpos, upto, tl_w, {b01, b23}};
         __syncthreads();
-        uint32_t tnf = 0, tnl = 0, tl = tail, up = 0, lp = 0;
+        // combine in position order: the last LAST fragment lies in band k* of
+        // wave v* (the wave with the largest lastpos); the other waves' complete
+        // fragments before it are their bands k < k*, plus band k* if v < v*
+        uint32_t tnf = 0, tnl = 0, tlp = 0, lp = 0, vs = 0;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const FrWaveStat st = ws[v];
-            if (st.lastpos) { lp = st.lastpos; up = tnf + st.upto; }
             tnf += st.cnt & 0xffffu;
             tnl += st.cnt >> 16;
-            if (st.tail) tl = (st.tail - 1) & 1u;
+            tlp = max(tlp, st.tail);
+            if (st.lastpos > lp) { lp = st.lastpos; vs = v; }
         }
+        uint32_t up = 0;
+        if (lp) {
+            const uint32_t ks = (lp - 1) >> 10;
+            up = ws[vs].upto;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                if ((uint32_t)v == vs) continue;
+                const uint32_t b[4] = {ws[v].band[0] & 0xffffu, ws[v].band[0] >> 16, ws[v].band[1] & 0xffffu,
+                                       ws[v].band[1] >> 16};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if ((uint32_t)k < ks || ((uint32_t)k == ks && (uint32_t)v < vs)) up += b[k];
+            }
+        }
+        const uint32_t tl = tlp ? (tlp - 1) & 1u : tail;
         info.nfrag = tnf;
         info.nlast = tnl;
         if (lp) {
@@ -494,7 +554,8 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
 }
 
 // ---------------------------------------------------------------------------
-// k_fr_emit: block (128 threads) per sub-chunk, thread t owns bitmap word t.
+// k_fr_emit: block (128 threads, two waves) per sub-chunk, thread t owns
+// bitmap word t.
 // frag_pos (xdrg_deframe only): stream offset of every fragment of the first
 // `cap` messages, plus the entry after the last one (the next fragment's
 // offset, or the end of the last complete message) so k_fr_copy reads body
@@ -504,8 +565,8 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
                                                   const FrameBase *bases, const uint32_t *fbits,
                                                   const uint32_t *lbits, uint64_t cap, int stream_offsets,
                                                   uint64_t *msg_offsets, uint64_t *frag_pos, uint64_t *res) {
-    __shared__ uint32_t pf[128], pl[128], tl[128];
-    const uint32_t tid = threadIdx.x;
+    __shared__ uint32_t wsum[2][2], wtail[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t k = blockIdx.x;                 // sub-chunk
     const uint64_t s = k / (kFSuper / kFChunk);
     if (res[0] == kFUnal || k * kFChunk >= Q) return;
@@ -517,24 +578,24 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
     if (fb0 >= F) return;                          // past the last complete message
     const uint32_t in_tail = info.prev_tail != 2u ? info.prev_tail : b.prev_tail;
     const uint32_t fw = fbits[k * 128 + tid], lw = lbits[k * 128 + tid];
-    // exclusive prefixes over the block's words, and the LAST flag of the
-    // fragment before each word ("last non-empty" scan)
-    pf[tid] = __popc(fw);
-    pl[tid] = __popc(lw);
-    tl[tid] = fw ? (lw >> (31 - __clz(fw))) & 1 : 2u;
-    __syncthreads();
-    for (uint32_t d = 1; d < 128; d <<= 1) {
-        const uint32_t a = tid >= d ? pf[tid - d] : 0, c = tid >= d ? pl[tid - d] : 0;
-        const uint32_t t = tid >= d ? tl[tid - d] : 2u;
-        __syncthreads();
-        pf[tid] += a;
-        pl[tid] += c;
-        if (tl[tid] == 2u) tl[tid] = t;
-        __syncthreads();
+    // exclusive prefixes over the block's words (wave scans + one barrier),
+    // and the LAST flag of the fragment before each word ("last non-empty")
+    uint32_t cf = __popc(fw), cl = __popc(lw);
+    uint32_t lt = fw ? 1 + (tid << 1 | ((lw >> (31 - __clz(fw))) & 1u)) : 0u;   // max = the latest
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t a1 = __shfl_up(cf, d, 64), a2 = __shfl_up(cl, d, 64), a3 = __shfl_up(lt, d, 64);
+        if (lane >= (uint32_t)d) { cf += a1; cl += a2; lt = max(lt, a3); }
     }
-    uint64_t f = fb0 + pf[tid] - __popc(fw);
-    uint64_t m = lb0 + pl[tid] - __popc(lw);
-    uint32_t prev_last = tid ? (tl[tid - 1] != 2u ? tl[tid - 1] : in_tail) : in_tail;
+    if (lane == 63) { wsum[wv][0] = cf; wsum[wv][1] = cl; wtail[wv] = lt; }
+    __syncthreads();
+    const uint32_t pf_incl = cf + (wv ? wsum[0][0] : 0u), pl_incl = cl + (wv ? wsum[0][1] : 0u);
+    uint32_t lt_excl = __shfl_up(lt, 1, 64);
+    if (lane == 0) lt_excl = 0;
+    if (wv) lt_excl = max(lt_excl, wtail[0]);
+    uint64_t f = fb0 + pf_incl - __popc(fw);
+    uint64_t m = lb0 + pl_incl - __popc(lw);
+    uint32_t prev_last = lt_excl ? (lt_excl - 1) & 1u : in_tail;
     const uint64_t base = k * kFChunk;
     for (uint32_t bits = fw; bits; bits &= bits - 1) {
         if (f >= F) break;
