@@ -58,6 +58,10 @@ extern "C" {
 #define XDRG_E_NOMEM      8  /* allocation failed */
 #define XDRG_E_INCOMPLETE 9  /* frame scan: not all fragments arrived -> NextAction STOP
                                 (RpcMessageParserTCP.java:51-53) */
+#define XDRG_E_NEG_SIZE   10 /* NegativeArraySizeException: a negative element count of an
+                                array of structs, which jrpcgen decodes as
+                                `new T[xdr.xdrDecodeInt()]` with no checkArraySize
+                                (oncrpc4j-rpcgen .../jrpcgen/jrpcgen.java:886-906) */
 
 /* ---- schema vocabulary (rpcgen) ------------------------------------------ */
 /* Base types.  Native element sizes: INT/UINT/ENUM/FLOAT 4, HYPER/UHYPER/
@@ -78,19 +82,41 @@ extern "C" {
 #define XDRG_T_BYTE   10   /* sign-extend / truncate   Xdr.java:919 / :485               */
 #define XDRG_T_OPAQUE 11   /* opaque x[N] / x<>        Xdr.java:776, :797 / :341, :374     */
 #define XDRG_T_STRING 12   /* string s<> as UTF-8 bytes Xdr.java:760 / :392              */
+#define XDRG_T_GROUP  13   /* a repeated group of member fields (array of structs / linked
+                              list); see "Repeated groups" below                     */
 
 /* Declaration kinds (JrpcgenDeclaration.java:64-81).                         */
 #define XDRG_K_SCALAR  0   /* one element                                              */
 #define XDRG_K_FIXED   1   /* T x[count]: count elements, no length word               */
 #define XDRG_K_DYNAMIC 2   /* T x<count?>: 4-byte BE length word + elements (count = max,
                               0 = unbounded; the reference never enforces a max)       */
+#define XDRG_K_LIST    3   /* XDRG_T_GROUP only: a recursive list `T *x` with
+                              struct T { ...; T *next; }: BE(1) before every element,
+                              BE(0) after the last (INDIRECTION, jrpcgen.java:835-851;
+                              portmap/pmaplist.java:50-69, rpcb_list.java:55-78)     */
 
 typedef struct xdrg_field {
     uint32_t type;      /* XDRG_T_* */
     uint32_t kind;      /* XDRG_K_* */
     uint32_t count;     /* FIXED: element count; DYNAMIC: max (0 = none); SCALAR: ignored */
-    uint32_t reserved;  /* must be 0 */
+    uint32_t reserved;  /* XDRG_T_GROUP: number of member fields that follow; else 0 */
 } xdrg_field;
+
+/* Repeated groups (arrays of structs, linked lists).  rpcgen encodes
+ * `T x<>` / `T x[N]` for a struct T as a count word (dynamic only) and then
+ * each element's fields (jrpcgen.java:856-906), and a recursive optional list
+ * (struct T { ...; T *next; }, used as `T *x`) as BE(1) + element for every
+ * element and a closing BE(0).  On the tape a group is one field
+ * {XDRG_T_GROUP, kind FIXED / DYNAMIC / LIST, count, reserved = m} followed
+ * by its m member fields (SCALAR, FIXED or DYNAMIC of the base types; no
+ * nested groups, no conditions in a schema with groups).  Columns: the
+ * group's own column has offsets[n + 1] (DYNAMIC / LIST: record i owns
+ * elements [offsets[i], offsets[i+1]); FIXED: element i*count + j, offsets
+ * unused) and, on decode, cap = element capacity; data is unused.  A member's
+ * column is indexed by ELEMENT: fixed members at data + e*stride, dynamic
+ * members own [offsets[e], offsets[e+1]) (offsets has elements + 1 entries).
+ * Decode errors keep the reference's order: the count / list bools / member
+ * checks as the element loop meets them; a negative count is XDRG_E_NEG_SIZE. */
 
 /* One native column.  Fixed-size fields (SCALAR / FIXED): record i's first
  * element is at  data + i*stride  (stride 0 = packed = elem_size*count), so

@@ -18,19 +18,22 @@ E_INVAL = 6
 E_HIP = 7
 E_NOMEM = 8
 E_INCOMPLETE = 9
+E_NEG_SIZE = 10
 
 STATUS_NAMES = {
     OK: "OK", E_SHORT: "SHORT", E_CORRUPT: "CORRUPT", E_FIXED_LEN: "FIXED_LEN",
     E_CAPACITY: "CAPACITY", E_FRAME: "FRAME", E_INVAL: "INVAL", E_HIP: "HIP",
-    E_NOMEM: "NOMEM", E_INCOMPLETE: "INCOMPLETE",
+    E_NOMEM: "NOMEM", E_INCOMPLETE: "INCOMPLETE", E_NEG_SIZE: "NEG_SIZE",
 }
 
 # base types (rpcgen baseTypes, jrpcgen.java:608-618)
 T_INT, T_UINT, T_ENUM, T_BOOL, T_HYPER, T_UHYPER = 1, 2, 3, 4, 5, 6
 T_FLOAT, T_DOUBLE, T_SHORT, T_BYTE, T_OPAQUE, T_STRING = 7, 8, 9, 10, 11, 12
+T_GROUP = 13   # repeated group: the next `reserved` fields are its members
 
 # declaration kinds (JrpcgenDeclaration.java:64-81)
 K_SCALAR, K_FIXED, K_DYNAMIC = 0, 1, 2
+K_LIST = 3     # XDRG_T_GROUP only: recursive optional list (BE(1) + element ..., BE(0))
 
 # flags
 FRAME_RM = 0x1

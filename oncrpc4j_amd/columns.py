@@ -9,6 +9,13 @@ engine works on a batch of N records of one schema laid out as columns
 * dynamic field (T<> / opaque<> / string<>): (values, offsets[n+1]) —
   record i owns values[offsets[i]:offsets[i+1]].
 
+* repeated group (array of structs / linked list, include/xdrg.h): the field
+  tuple is (T_GROUP, kind, count, members) and the next `members` fields are
+  its members; the group's array is offsets[n+1] (element ranges; None for
+  a FIXED group: record i owns elements i*count ...), and every member array
+  is indexed by ELEMENT (fixed: (E,) / (E, count); dynamic: (values,
+  offsets[E+1])).
+
 HostBatch holds numpy arrays (fixtures, the oracle's host pointers);
 DeviceBatch holds torch tensors in HBM (the engine's device pointers).
 torch is only the device-memory allocator here.
@@ -31,6 +38,30 @@ _BITS = {4: np.uint32, 8: np.uint64, 2: np.uint16, 1: np.uint8}
 
 def pad4(n):
     return (4 - (n & 3)) & 3
+
+
+def parents(fields):
+    """parent[k] = index of the group field k is a member of, or -1."""
+    par = [-1] * len(fields)
+    k = 0
+    while k < len(fields):
+        f = fields[k]
+        if f[0] == abi.T_GROUP:
+            for j in range(1, f[3] + 1):
+                par[k + j] = k
+            k += f[3] + 1
+        else:
+            k += 1
+    return par
+
+
+def _is_group(f):
+    return f[0] == abi.T_GROUP
+
+
+def _counted(f):
+    """Fields whose array carries offsets: dynamic fields, DYNAMIC / LIST groups."""
+    return f[1] == abi.K_DYNAMIC or (_is_group(f) and f[1] == abi.K_LIST)
 
 
 def field_xdr_bytes(field, cnt=None):
@@ -56,59 +87,119 @@ class HostBatch:
         self.fields = [tuple(f) for f in fields]
         self.n = int(n)
         self.arrays = arrays
+        self.parent = parents(self.fields)
+
+    # ---- element bookkeeping of repeated groups ----------------------------
+    def elems(self, g, upto=None):
+        """Elements of group g in records [0, upto)."""
+        f = self.fields[g]
+        n = self.n if upto is None else upto
+        if f[1] == abi.K_FIXED:
+            return n * f[2]
+        return int(self.arrays[g][n])
+
+    def rows(self, k):
+        """Rows of field k's array: records, or its group's elements."""
+        g = self.parent[k]
+        return self.n if g < 0 else self.elems(g)
+
+    def _elem_cap(self, g):
+        m = self.arrays[g + 1]
+        return (len(m[1]) - 1) if self.fields[g + 1][1] == abi.K_DYNAMIC else m.shape[0]
 
     # ---- construction ----------------------------------------------------
     @classmethod
     def empty(cls, fields, n, dyn_caps=None):
-        """Zeroed output columns for a decode; dyn_caps[k] = element capacity."""
+        """Zeroed output columns for a decode; dyn_caps[k] = element capacity
+        (of a dynamic field, of a group, or of a group's dynamic member)."""
+        fields = [tuple(f) for f in fields]
+        par = parents(fields)
+        caps = dyn_caps or {}
         arrays = []
-        for k, (t, kind, c) in enumerate(fields):
+        for k, f in enumerate(fields):
+            t, kind, c = f[0], f[1], f[2]
+            rows = n if par[k] < 0 else (n * fields[par[k]][2] if fields[par[k]][1] == abi.K_FIXED
+                                          else caps.get(par[k], 0))
+            if _is_group(f):
+                arrays.append(None if kind == abi.K_FIXED else np.zeros(n + 1, dtype=np.uint64))
+                continue
             dt = NP_DTYPE[t]
             if kind == abi.K_DYNAMIC:
-                cap = (dyn_caps or {}).get(k, 0)
-                arrays.append((np.zeros(max(cap, 1), dtype=dt), np.zeros(n + 1, dtype=np.uint64)))
+                cap = caps.get(k, 0)
+                arrays.append((np.zeros(max(cap, 1), dtype=dt), np.zeros(rows + 1, dtype=np.uint64)))
             elif kind == abi.K_FIXED:
-                arrays.append(np.zeros((n, c), dtype=dt))
+                arrays.append(np.zeros((max(rows, 1), c), dtype=dt))
             else:
-                arrays.append(np.zeros(n, dtype=dt))
+                arrays.append(np.zeros(max(rows, 1), dtype=dt))
         return cls(fields, n, arrays)
 
     def columns(self):
         """ctypes xdrg_column array with HOST pointers (for the oracle)."""
         arr = (abi.Column * len(self.fields))()
-        for k, (t, kind, c) in enumerate(self.fields):
-            if kind == abi.K_DYNAMIC:
+        for k, f in enumerate(self.fields):
+            kind = f[1]
+            arr[k].stride = 0
+            if _is_group(f):
+                offs = self.arrays[k]
+                arr[k].data = None
+                arr[k].offsets = None if offs is None else offs.ctypes.data
+                arr[k].cap = self._elem_cap(k)
+            elif kind == abi.K_DYNAMIC:
                 vals, offs = self.arrays[k]
                 arr[k].data = vals.ctypes.data
                 arr[k].offsets = offs.ctypes.data
                 arr[k].cap = vals.size
-                arr[k].stride = 0
             else:
                 a = self.arrays[k]
                 arr[k].data = a.ctypes.data
-                arr[k].stride = 0
                 arr[k].offsets = None
                 arr[k].cap = 0
         arr._keep = self.arrays  # keep the numpy buffers alive with the array
         return arr
 
     def dyn_caps(self):
-        return {k: int(self.arrays[k][1][-1]) for k, f in enumerate(self.fields)
-                if f[1] == abi.K_DYNAMIC}
+        caps = {}
+        for k, f in enumerate(self.fields):
+            if _is_group(f):
+                caps[k] = self.elems(k)
+            elif f[1] == abi.K_DYNAMIC:
+                caps[k] = int(self.arrays[k][1][self.rows(k)])
+        return caps
+
+    def _field_sizes(self, k, rows):
+        """XDR bytes of field k for each of its `rows` rows (numpy uint64)."""
+        f = self.fields[k]
+        if f[1] == abi.K_DYNAMIC:
+            offs = self.arrays[k][1][:rows + 1].astype(np.uint64)
+            cnt = offs[1:] - offs[:-1]
+            if abi.XDR_SIZE[f[0]] == 1:
+                return 4 + cnt + ((4 - (cnt & 3)) & 3)
+            return 4 + cnt * abi.XDR_SIZE[f[0]]
+        return np.full(rows, field_xdr_bytes(f[:3]), dtype=np.uint64)
 
     def xdr_sizes(self, framed=False):
         """Per-record XDR size (numpy uint64)."""
         s = np.full(self.n, 4 if framed else 0, dtype=np.uint64)
-        for k, f in enumerate(self.fields):
-            if f[1] == abi.K_DYNAMIC:
-                offs = self.arrays[k][1].astype(np.uint64)
-                cnt = offs[1:] - offs[:-1]
-                if abi.XDR_SIZE[f[0]] == 1:
-                    s += 4 + cnt + ((4 - (cnt & 3)) & 3)
-                else:
-                    s += 4 + cnt * abi.XDR_SIZE[f[0]]
+        k = 0
+        while k < len(self.fields):
+            f = self.fields[k]
+            if not _is_group(f):
+                s += self._field_sizes(k, self.n)
+                k += 1
+                continue
+            E = self.elems(k)
+            es = np.full(E, 4 if f[1] == abi.K_LIST else 0, dtype=np.uint64)
+            for j in range(k + 1, k + 1 + f[3]):
+                es += self._field_sizes(j, E)
+            ce = np.zeros(E + 1, dtype=np.uint64)
+            np.cumsum(es, out=ce[1:])
+            if f[1] == abi.K_FIXED:
+                bounds = np.arange(self.n + 1, dtype=np.uint64) * f[2]
             else:
-                s += field_xdr_bytes(f)
+                bounds = self.arrays[k][:self.n + 1].astype(np.uint64)
+            s += ce[bounds[1:]] - ce[bounds[:-1]]
+            s += {abi.K_DYNAMIC: 4, abi.K_LIST: 4, abi.K_FIXED: 0}[f[1]]
+            k += 1 + f[3]
         return s
 
     def xdr_total(self, framed=False):
@@ -118,15 +209,19 @@ class HostBatch:
         """Algorithmic native bytes of the batch (values actually present)."""
         tot = 0
         for k, f in enumerate(self.fields):
-            if f[1] == abi.K_DYNAMIC:
+            if _is_group(f):
+                if self.arrays[k] is not None:
+                    tot += 8 * self.n
+            elif f[1] == abi.K_DYNAMIC:
                 vals, offs = self.arrays[k]
-                tot += int(offs[-1]) * vals.dtype.itemsize
+                tot += int(offs[self.rows(k)]) * vals.dtype.itemsize
             else:
-                tot += self.arrays[k].nbytes
+                a = self.arrays[k]
+                tot += a[:self.rows(k)].nbytes
         return tot
 
     def record(self, i, k):
-        """Value(s) of field k of record i."""
+        """Value(s) of top-level field k of record i."""
         f = self.fields[k]
         if f[1] == abi.K_DYNAMIC:
             vals, offs = self.arrays[k]
@@ -134,49 +229,84 @@ class HostBatch:
         return self.arrays[k][i]
 
     def slice(self, lo, hi):
-        """Records [lo, hi) as a new batch (dynamic offsets rebased)."""
+        """Records [lo, hi) as a new batch (offsets rebased)."""
         arrays = []
+        rng = {}
         for k, f in enumerate(self.fields):
-            if f[1] == abi.K_DYNAMIC:
+            g = self.parent[k]
+            a, b = (lo, hi) if g < 0 else rng[g]
+            if _is_group(f):
+                if f[1] == abi.K_FIXED:
+                    arrays.append(None)
+                    rng[k] = (lo * f[2], hi * f[2])
+                else:
+                    offs = self.arrays[k]
+                    arrays.append((offs[lo:hi + 1] - offs[lo]).astype(np.uint64))
+                    rng[k] = (int(offs[lo]), int(offs[hi]))
+            elif f[1] == abi.K_DYNAMIC:
                 vals, offs = self.arrays[k]
-                a, b = int(offs[lo]), int(offs[hi])
-                arrays.append((vals[a:b].copy(), (offs[lo:hi + 1] - offs[lo]).astype(np.uint64)))
+                x, y = int(offs[a]), int(offs[b])
+                arrays.append((vals[x:y].copy(), (offs[a:b + 1] - offs[a]).astype(np.uint64)))
             else:
-                arrays.append(self.arrays[k][lo:hi].copy())
+                arrays.append(self.arrays[k][a:b].copy())
         return HostBatch(self.fields, hi - lo, arrays)
 
     def equal(self, other, upto=None):
         """Bit-exact equality of the first `upto` records (floats by bits)."""
         n = self.n if upto is None else upto
         for k, f in enumerate(self.fields):
-            if f[1] == abi.K_DYNAMIC:
+            g = self.parent[k]
+            rows = n if g < 0 else self.elems(g, n)
+            if _is_group(f):
+                if f[1] != abi.K_FIXED and not np.array_equal(self.arrays[k][:n + 1],
+                                                                other.arrays[k][:n + 1]):
+                    return False
+            elif f[1] == abi.K_DYNAMIC:
                 va, oa = self.arrays[k]
                 vb, ob = other.arrays[k]
-                if not np.array_equal(oa[:n + 1], ob[:n + 1]):
+                if not np.array_equal(oa[:rows + 1], ob[:rows + 1]):
                     return False
-                e = int(oa[n])
+                e = int(oa[rows])
                 if not np.array_equal(_bits(va[:e]), _bits(vb[:e])):
                     return False
             else:
-                if not np.array_equal(_bits(self.arrays[k][:n]), _bits(other.arrays[k][:n])):
+                if not np.array_equal(_bits(self.arrays[k][:rows]), _bits(other.arrays[k][:rows])):
                     return False
         return True
 
 
 # ---- synthetic batches (seeded) -------------------------------------------
 def random_batch(fields, n, seed, dyn_len=(0, 16), string_alphabet=b"abcdefghijklmnopqrstuvwxyz",
-                 special_floats=True):
+                 special_floats=True, group_len=(0, 4)):
     """Seeded synthetic batch: ints uniform over their full range, floats as
     random bit patterns (NaNs with payloads included), bools 0/1/other
-    non-zero bytes, dynamic lengths uniform in dyn_len (inclusive)."""
+    non-zero bytes, dynamic lengths uniform in dyn_len, DYNAMIC / LIST group
+    element counts uniform in group_len (both inclusive)."""
     rng = np.random.default_rng(seed)
+    fields = [tuple(f) for f in fields]
+    par = parents(fields)
     arrays = []
-    for t, kind, c in fields:
+    elems = {}
+    for k, f in enumerate(fields):
+        t, kind, c = f[0], f[1], f[2]
+        rows = n if par[k] < 0 else elems[par[k]]
+        if t == abi.T_GROUP:
+            if kind == abi.K_FIXED:
+                arrays.append(None)
+                elems[k] = n * c
+            else:
+                lo, hi = group_len
+                cnt = rng.integers(lo, hi + 1, size=n, dtype=np.uint64)
+                offs = np.zeros(n + 1, dtype=np.uint64)
+                np.cumsum(cnt, out=offs[1:])
+                arrays.append(offs)
+                elems[k] = int(offs[-1])
+            continue
         dt = np.dtype(NP_DTYPE[t])
         if kind == abi.K_DYNAMIC:
             lo, hi = dyn_len
-            cnt = rng.integers(lo, hi + 1, size=n, dtype=np.uint64)
-            offs = np.zeros(n + 1, dtype=np.uint64)
+            cnt = rng.integers(lo, hi + 1, size=rows, dtype=np.uint64)
+            offs = np.zeros(rows + 1, dtype=np.uint64)
             np.cumsum(cnt, out=offs[1:])
             total = int(offs[-1])
             if t == abi.T_STRING:
@@ -186,7 +316,7 @@ def random_batch(fields, n, seed, dyn_len=(0, 16), string_alphabet=b"abcdefghijk
                 vals = _random_values(rng, dt, total, t, special_floats)
             arrays.append((vals, offs))
         else:
-            shape = (n, c) if kind == abi.K_FIXED else (n,)
+            shape = (rows, c) if kind == abi.K_FIXED else (rows,)
             size = int(np.prod(shape))
             arrays.append(_random_values(rng, dt, size, t, special_floats).reshape(shape))
     return HostBatch(fields, n, arrays)
@@ -243,13 +373,19 @@ class DeviceBatch:
         self.n = int(n)
         self.tensors = tensors
         self._np = np_dtypes
+        self.parent = parents(self.fields)
 
     @classmethod
     def from_host(cls, hb, device="cuda"):
         import torch
         tensors, dts = [], []
         for k, f in enumerate(hb.fields):
-            if f[1] == abi.K_DYNAMIC:
+            if _is_group(f):
+                offs = hb.arrays[k]
+                tensors.append(None if offs is None else
+                               torch.from_numpy(offs.astype(np.uint64).view(np.int64)).to(device))
+                dts.append(None)
+            elif f[1] == abi.K_DYNAMIC:
                 vals, offs = hb.arrays[k]
                 tv = torch.from_numpy(_signed_view(vals if vals.size else np.zeros(1, vals.dtype)))
                 to = torch.from_numpy(offs.astype(np.uint64).view(np.int64))
@@ -257,41 +393,60 @@ class DeviceBatch:
                 dts.append(vals.dtype)
             else:
                 a = hb.arrays[k]
-                tensors.append(torch.from_numpy(_signed_view(a)).to(device))
+                tensors.append(torch.from_numpy(_signed_view(a if a.size else
+                                                             np.zeros((1,) + a.shape[1:], a.dtype))).to(device))
                 dts.append(a.dtype)
         return cls(hb.fields, hb.n, tensors, dts)
 
     @classmethod
     def empty(cls, fields, n, dyn_caps=None, device="cuda"):
         import torch
+        fields = [tuple(f) for f in fields]
+        par = parents(fields)
+        caps = dyn_caps or {}
         tensors, dts = [], []
-        for k, (t, kind, c) in enumerate(fields):
+        for k, f in enumerate(fields):
+            t, kind, c = f[0], f[1], f[2]
+            rows = n if par[k] < 0 else (n * fields[par[k]][2] if fields[par[k]][1] == abi.K_FIXED
+                                          else caps.get(par[k], 0))
+            if _is_group(f):
+                tensors.append(None if kind == abi.K_FIXED else
+                               torch.zeros(n + 1, dtype=torch.int64, device=device))
+                dts.append(None)
+                continue
             dt = np.dtype(NP_DTYPE[t])
             tdt = _torch_dtype(dt)
             if kind == abi.K_DYNAMIC:
-                cap = max((dyn_caps or {}).get(k, 0), 1)
+                cap = max(caps.get(k, 0), 1)
                 tensors.append((torch.zeros(cap, dtype=tdt, device=device),
-                                torch.zeros(n + 1, dtype=torch.int64, device=device)))
+                                torch.zeros(rows + 1, dtype=torch.int64, device=device)))
             elif kind == abi.K_FIXED:
-                tensors.append(torch.zeros((n, c), dtype=tdt, device=device))
+                tensors.append(torch.zeros((max(rows, 1), c), dtype=tdt, device=device))
             else:
-                tensors.append(torch.zeros(n, dtype=tdt, device=device))
+                tensors.append(torch.zeros(max(rows, 1), dtype=tdt, device=device))
             dts.append(dt)
         return cls(fields, n, tensors, dts)
+
+    def _elem_cap(self, g):
+        m = self.tensors[g + 1]
+        return (m[1].numel() - 1) if self.fields[g + 1][1] == abi.K_DYNAMIC else m.shape[0]
 
     def columns(self):
         """ctypes xdrg_column array with DEVICE pointers."""
         arr = (abi.Column * len(self.fields))()
         for k, f in enumerate(self.fields):
-            if f[1] == abi.K_DYNAMIC:
+            arr[k].stride = 0
+            if _is_group(f):
+                arr[k].data = None
+                arr[k].offsets = None if self.tensors[k] is None else self.tensors[k].data_ptr()
+                arr[k].cap = self._elem_cap(k)
+            elif f[1] == abi.K_DYNAMIC:
                 tv, to = self.tensors[k]
                 arr[k].data = tv.data_ptr()
                 arr[k].offsets = to.data_ptr()
                 arr[k].cap = tv.numel()
-                arr[k].stride = 0
             else:
                 arr[k].data = self.tensors[k].data_ptr()
-                arr[k].stride = 0
                 arr[k].offsets = None
                 arr[k].cap = 0
         arr._keep = self.tensors
@@ -301,7 +456,10 @@ class DeviceBatch:
         arrays = []
         for k, f in enumerate(self.fields):
             dt = self._np[k]
-            if f[1] == abi.K_DYNAMIC:
+            if _is_group(f):
+                arrays.append(None if self.tensors[k] is None else
+                              self.tensors[k].cpu().numpy().view(np.uint64))
+            elif f[1] == abi.K_DYNAMIC:
                 tv, to = self.tensors[k]
                 vals = tv.cpu().numpy().view(dt)
                 offs = to.cpu().numpy().view(np.uint64)

@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "libxdr_oracle.so")
 # mirrors include/xdrg.h (kept local so the oracle does not import the product)
 OK, E_SHORT, E_CORRUPT, E_FIXED_LEN, E_CAPACITY, E_FRAME, E_INVAL = 0, 1, 2, 3, 4, 5, 6
 E_INCOMPLETE = 9
+E_NEG_SIZE = 10
 FRAME_RM = 0x1
 
 
@@ -116,9 +117,11 @@ def lib():
 
 
 def fields_array(fields):
+    """[(type, kind, count)] or, for a repeated group, (T_GROUP, kind, count, members)."""
     arr = (Field * len(fields))()
-    for i, (t, k, c) in enumerate(fields):
-        arr[i].type, arr[i].kind, arr[i].count, arr[i].reserved = t, k, c, 0
+    for i, f in enumerate(fields):
+        arr[i].type, arr[i].kind, arr[i].count = f[0], f[1], f[2]
+        arr[i].reserved = f[3] if len(f) > 3 else 0
     return arr
 
 

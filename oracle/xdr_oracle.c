@@ -380,6 +380,7 @@ static size_t native_size(uint32_t t) {
  * (jrpcgen.java:661-739): no boolean vectors, strings only as string<>,
  * opaque only as opaque[N] / opaque<>.                                       */
 static int field_valid(const xdrg_field *f) {
+    if (f->type == XDRG_T_GROUP) return 0;   /* checked by check_schema with its members */
     if (!native_size(f->type) || f->kind > XDRG_K_DYNAMIC || f->reserved) return 0;
     if (f->type == XDRG_T_BOOL && f->kind != XDRG_K_SCALAR) return 0;
     if (f->type == XDRG_T_STRING && f->kind != XDRG_K_DYNAMIC) return 0;
@@ -405,9 +406,11 @@ static inline const uint8_t *fixed_ptr(const xdrg_field *f, const xdrg_column *c
  * points at field k's condition or is NULL.                                 */
 typedef struct { const xdrg_cond *cond_of[64]; } xo_conds;
 
+static int has_group(const xdrg_field *fs, size_t nf);
 static int cond_table(const xdrg_field *fs, size_t nf, const xdrg_cond *conds, size_t nc,
                       xo_conds *t) {
     memset(t, 0, sizeof *t);
+    if (nc && has_group(fs, nf)) return XDRG_E_INVAL;   /* no conditions with repeated groups */
     if (nf > 64) return nc ? XDRG_E_INVAL : XDRG_OK;
     for (size_t i = 0; i < nc; i++) {
         const xdrg_cond *c = &conds[i];
@@ -428,6 +431,80 @@ static int present(const xo_conds *t, size_t k, const int *pres, const int32_t *
     int in = 0;
     for (uint32_t j = 0; j < c->nvalues; j++) in |= c->values[j] == val[c->disc];
     return in != (c->negate != 0);
+}
+
+/* Field f of row i of its column — a record for a top-level field, an
+ * element for a group member — through the stream encoders. */
+static int encode_field(xo_stream *s, const xdrg_field *f, const xdrg_column *c, uint64_t i) {
+    int rc = XDRG_OK;
+    if (f->kind == XDRG_K_DYNAMIC) {
+        uint64_t a = c->offsets[i], b = c->offsets[i + 1];
+        const uint8_t *base = (const uint8_t *)c->data + a * native_size(f->type);
+        size_t n = (size_t)(b - a);
+        switch (f->type) {
+        case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM:
+            rc = xo_encode_int_vector(s, (const int32_t *)base, n); break;
+        case XDRG_T_HYPER: case XDRG_T_UHYPER:
+            rc = xo_encode_long_vector(s, (const int64_t *)base, n); break;
+        case XDRG_T_FLOAT:  rc = xo_encode_float_vector(s, (const float *)base, n); break;
+        case XDRG_T_DOUBLE: rc = xo_encode_double_vector(s, (const double *)base, n); break;
+        case XDRG_T_SHORT:  rc = xo_encode_short_vector(s, (const int16_t *)base, n); break;
+        case XDRG_T_BYTE:   rc = xo_encode_byte_vector(s, (const int8_t *)base, n); break;
+        case XDRG_T_OPAQUE: rc = xo_encode_dynamic_opaque(s, base, n); break;
+        case XDRG_T_STRING: rc = xo_encode_string(s, base, n); break;
+        default: rc = XDRG_E_INVAL;
+        }
+    } else if (f->kind == XDRG_K_FIXED) {
+        const uint8_t *p = fixed_ptr(f, c, i);
+        size_t n = f->count; int32_t len = (int32_t)f->count;
+        switch (f->type) {
+        case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM:
+            rc = xo_encode_int_fixed_vector(s, (const int32_t *)p, n, len); break;
+        case XDRG_T_HYPER: case XDRG_T_UHYPER:
+            rc = xo_encode_long_fixed_vector(s, (const int64_t *)p, n, len); break;
+        case XDRG_T_FLOAT:  rc = xo_encode_float_fixed_vector(s, (const float *)p, n, len); break;
+        case XDRG_T_DOUBLE: rc = xo_encode_double_fixed_vector(s, (const double *)p, n, len); break;
+        case XDRG_T_SHORT:  rc = xo_encode_short_fixed_vector(s, (const int16_t *)p, n, len); break;
+        case XDRG_T_BYTE:   rc = xo_encode_byte_fixed_vector(s, (const int8_t *)p, n, len); break;
+        case XDRG_T_OPAQUE: rc = xo_encode_opaque(s, p, 0, n); break;
+        default: rc = XDRG_E_INVAL;
+        }
+    } else {
+        const uint8_t *p = fixed_ptr(f, c, i);
+        switch (f->type) {
+        case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: {
+            int32_t v; memcpy(&v, p, 4); rc = xo_encode_int(s, v); break; }
+        case XDRG_T_HYPER: case XDRG_T_UHYPER: {
+            int64_t v; memcpy(&v, p, 8); rc = xo_encode_long(s, v); break; }
+        case XDRG_T_FLOAT:  { float v; memcpy(&v, p, 4); rc = xo_encode_float(s, v); break; }
+        case XDRG_T_DOUBLE: { double v; memcpy(&v, p, 8); rc = xo_encode_double(s, v); break; }
+        case XDRG_T_BOOL:   rc = xo_encode_boolean(s, *p != 0); break;
+        case XDRG_T_SHORT:  { int16_t v; memcpy(&v, p, 2); rc = xo_encode_short(s, v); break; }
+        case XDRG_T_BYTE:   rc = xo_encode_byte(s, (int8_t)*p); break;
+        default: rc = XDRG_E_INVAL;
+        }
+    }
+    return rc;
+}
+
+/* A repeated group (include/xdrg.h): rpcgen's array-of-structs loop
+ * `xdrEncodeInt($size); for (...) x[$idx].xdrEncode(xdr)` (jrpcgen.java:
+ * 856-880; no count for T x[N]), or a recursive list: xdrEncodeBoolean(true)
+ * and the element while there is one, then xdrEncodeBoolean(false)
+ * (portmap/pmaplist.java:63-70).  g[0] is the group, g[1..m] its members. */
+static int encode_group(xo_stream *s, const xdrg_field *g, const xdrg_column *gc, uint64_t i) {
+    const uint32_t m = g->reserved;
+    uint64_t e0, cnt;
+    if (g->kind == XDRG_K_FIXED) { e0 = i * g->count; cnt = g->count; }
+    else { e0 = gc->offsets[i]; cnt = gc->offsets[i + 1] - e0; }
+    int rc = XDRG_OK;
+    if (g->kind == XDRG_K_DYNAMIC) rc = xo_encode_int(s, (int32_t)cnt);
+    for (uint64_t e = e0; !rc && e < e0 + cnt; e++) {
+        if (g->kind == XDRG_K_LIST) rc = xo_encode_boolean(s, 1);
+        for (uint32_t j = 1; !rc && j <= m; j++) rc = encode_field(s, &g[j], &gc[j], e);
+    }
+    if (!rc && g->kind == XDRG_K_LIST) rc = xo_encode_boolean(s, 0);
+    return rc;
 }
 
 /* shallow >= 0: that dynamic opaque/string field is encoded by reference
@@ -461,53 +538,13 @@ static int encode_record_ex(xo_stream *s, const xdrg_field *fs, size_t nf, const
             *chunk_len = b - a;
             continue;
         }
-        if (f->kind == XDRG_K_DYNAMIC) {
-            uint64_t a = c->offsets[i], b = c->offsets[i + 1];
-            const uint8_t *base = (const uint8_t *)c->data + a * native_size(f->type);
-            size_t n = (size_t)(b - a);
-            switch (f->type) {
-            case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM:
-                rc = xo_encode_int_vector(s, (const int32_t *)base, n); break;
-            case XDRG_T_HYPER: case XDRG_T_UHYPER:
-                rc = xo_encode_long_vector(s, (const int64_t *)base, n); break;
-            case XDRG_T_FLOAT:  rc = xo_encode_float_vector(s, (const float *)base, n); break;
-            case XDRG_T_DOUBLE: rc = xo_encode_double_vector(s, (const double *)base, n); break;
-            case XDRG_T_SHORT:  rc = xo_encode_short_vector(s, (const int16_t *)base, n); break;
-            case XDRG_T_BYTE:   rc = xo_encode_byte_vector(s, (const int8_t *)base, n); break;
-            case XDRG_T_OPAQUE: rc = xo_encode_dynamic_opaque(s, base, n); break;
-            case XDRG_T_STRING: rc = xo_encode_string(s, base, n); break;
-            default: rc = XDRG_E_INVAL;
-            }
-        } else if (f->kind == XDRG_K_FIXED) {
-            const uint8_t *p = fixed_ptr(f, c, i);
-            size_t n = f->count; int32_t len = (int32_t)f->count;
-            switch (f->type) {
-            case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM:
-                rc = xo_encode_int_fixed_vector(s, (const int32_t *)p, n, len); break;
-            case XDRG_T_HYPER: case XDRG_T_UHYPER:
-                rc = xo_encode_long_fixed_vector(s, (const int64_t *)p, n, len); break;
-            case XDRG_T_FLOAT:  rc = xo_encode_float_fixed_vector(s, (const float *)p, n, len); break;
-            case XDRG_T_DOUBLE: rc = xo_encode_double_fixed_vector(s, (const double *)p, n, len); break;
-            case XDRG_T_SHORT:  rc = xo_encode_short_fixed_vector(s, (const int16_t *)p, n, len); break;
-            case XDRG_T_BYTE:   rc = xo_encode_byte_fixed_vector(s, (const int8_t *)p, n, len); break;
-            case XDRG_T_OPAQUE: rc = xo_encode_opaque(s, p, 0, n); break;
-            default: rc = XDRG_E_INVAL;
-            }
-        } else {
-            const uint8_t *p = fixed_ptr(f, c, i);
-            switch (f->type) {
-            case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: {
-                int32_t v; memcpy(&v, p, 4); rc = xo_encode_int(s, v); break; }
-            case XDRG_T_HYPER: case XDRG_T_UHYPER: {
-                int64_t v; memcpy(&v, p, 8); rc = xo_encode_long(s, v); break; }
-            case XDRG_T_FLOAT:  { float v; memcpy(&v, p, 4); rc = xo_encode_float(s, v); break; }
-            case XDRG_T_DOUBLE: { double v; memcpy(&v, p, 8); rc = xo_encode_double(s, v); break; }
-            case XDRG_T_BOOL:   rc = xo_encode_boolean(s, *p != 0); break;
-            case XDRG_T_SHORT:  { int16_t v; memcpy(&v, p, 2); rc = xo_encode_short(s, v); break; }
-            case XDRG_T_BYTE:   rc = xo_encode_byte(s, (int8_t)*p); break;
-            default: rc = XDRG_E_INVAL;
-            }
+        if (f->type == XDRG_T_GROUP) {
+            rc = encode_group(s, fs + k, cols + k, i);
+            if (rc) return rc;
+            k += f->reserved;   /* its members */
+            continue;
         }
+        rc = encode_field(s, f, c, i);
         if (rc) return rc;
     }
     return XDRG_OK;
@@ -519,9 +556,34 @@ static int encode_record(xo_stream *s, const xdrg_field *fs, size_t nf, const xd
     return encode_record_ex(s, fs, nf, cols, i, cc, -1, &at, &len);
 }
 
+/* Repeated groups (include/xdrg.h): the group field, then `reserved` member
+ * fields of the base types; no nested groups; an element that encodes to at
+ * least one byte (list elements carry their bool). */
+static int has_group(const xdrg_field *fs, size_t nf) {
+    for (size_t k = 0; k < nf; k++) if (fs[k].type == XDRG_T_GROUP) return 1;
+    return 0;
+}
 static int check_schema(const xdrg_field *fs, size_t nf) {
-    if (!fs || !nf) return XDRG_E_INVAL;
-    for (size_t k = 0; k < nf; k++) if (!field_valid(&fs[k])) return XDRG_E_INVAL;
+    if (!fs || !nf || nf > 64) return XDRG_E_INVAL;
+    for (size_t k = 0; k < nf; k++) {
+        const xdrg_field *g = &fs[k];
+        if (g->type != XDRG_T_GROUP) {
+            if (!field_valid(g)) return XDRG_E_INVAL;
+            continue;
+        }
+        const uint32_t m = g->reserved;
+        if (g->kind < XDRG_K_FIXED || g->kind > XDRG_K_LIST || m == 0 || m > nf - 1 - k) return XDRG_E_INVAL;
+        if ((g->kind == XDRG_K_FIXED && g->count > 0x7fffffffu) || (g->kind == XDRG_K_LIST && g->count))
+            return XDRG_E_INVAL;
+        int sized = g->kind == XDRG_K_LIST;
+        for (uint32_t j = 1; j <= m; j++) {
+            const xdrg_field *f = &g[j];
+            if (!field_valid(f)) return XDRG_E_INVAL;
+            sized |= f->kind == XDRG_K_DYNAMIC || f->kind == XDRG_K_SCALAR || f->count > 0;
+        }
+        if (!sized) return XDRG_E_INVAL;
+        k += m;
+    }
     return XDRG_OK;
 }
 
@@ -570,6 +632,7 @@ int xo_encode_batch_shallow(const xdrg_field *fs, size_t nf, const xdrg_cond *co
                             uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len,
                             uint32_t field, uint64_t *splice) {
     int rc = check_schema(fs, nf); if (rc) return rc;
+    if (has_group(fs, nf)) return XDRG_E_INVAL;
     if (field >= nf || fs[field].kind != XDRG_K_DYNAMIC ||
         (fs[field].type != XDRG_T_OPAQUE && fs[field].type != XDRG_T_STRING)) return XDRG_E_INVAL;
     xo_conds cc;
@@ -594,6 +657,148 @@ int xo_encode_batch_shallow(const xdrg_field *fs, size_t nf, const xdrg_cond *co
     }
     if (rec_offsets) rec_offsets[n] = pos;
     if (out_len) *out_len = pos;
+    return XDRG_OK;
+}
+
+/* Field f of row i of its column (a record, or an element of a group)
+ * through the stream decoders; dynamic fields append at offsets[i]. */
+static int decode_field(xo_stream *s, const xdrg_field *f, xdrg_column *c, uint64_t i) {
+    int rc = XDRG_OK;
+    if (f->kind == XDRG_K_DYNAMIC) {
+        size_t es = native_size(f->type);
+        uint64_t a = c->offsets[i];
+        uint8_t *base = (uint8_t *)c->data + a * es;
+        size_t cap = c->cap > a ? (size_t)(c->cap - a) : 0, got = 0;
+        switch (f->type) {
+        case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM:
+            rc = xo_decode_int_vector(s, (int32_t *)base, cap, &got); break;
+        case XDRG_T_HYPER: case XDRG_T_UHYPER:
+            rc = xo_decode_long_vector(s, (int64_t *)base, cap, &got); break;
+        case XDRG_T_FLOAT:  rc = xo_decode_float_vector(s, (float *)base, cap, &got); break;
+        case XDRG_T_DOUBLE: rc = xo_decode_double_vector(s, (double *)base, cap, &got); break;
+        case XDRG_T_SHORT:  rc = xo_decode_short_vector(s, (int16_t *)base, cap, &got); break;
+        case XDRG_T_BYTE:   rc = xo_decode_byte_vector(s, (int8_t *)base, cap, &got); break;
+        case XDRG_T_OPAQUE: case XDRG_T_STRING: {
+            const uint8_t *p; size_t len;
+            rc = f->type == XDRG_T_OPAQUE ? xo_decode_dynamic_opaque(s, &p, &len)
+                                          : xo_decode_string(s, &p, &len);
+            if (!rc && len > cap) rc = XDRG_E_CAPACITY;
+            if (!rc) { memcpy(base, p, len); got = len; }
+            break; }
+        default: rc = XDRG_E_INVAL;
+        }
+        if (rc) return rc;
+        c->offsets[i + 1] = a + got;
+    } else {
+        size_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
+        uint8_t *p = (uint8_t *)fixed_ptr(f, c, i);
+        if (f->type == XDRG_T_OPAQUE) return xo_decode_opaque(s, p, cnt);
+        for (size_t e = 0; e < cnt && !rc; e++) {
+            switch (f->type) {
+            case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: {
+                int32_t v; rc = xo_decode_int(s, &v); if (!rc) memcpy(p + 4 * e, &v, 4); break; }
+            case XDRG_T_FLOAT: {
+                float v; rc = xo_decode_float(s, &v); if (!rc) memcpy(p + 4 * e, &v, 4); break; }
+            case XDRG_T_HYPER: case XDRG_T_UHYPER: {
+                int64_t v; rc = xo_decode_long(s, &v); if (!rc) memcpy(p + 8 * e, &v, 8); break; }
+            case XDRG_T_DOUBLE: {
+                double v; rc = xo_decode_double(s, &v); if (!rc) memcpy(p + 8 * e, &v, 8); break; }
+            case XDRG_T_BOOL: { int v; rc = xo_decode_boolean(s, &v); if (!rc) p[e] = (uint8_t)v; break; }
+            case XDRG_T_SHORT: {
+                int16_t v; rc = xo_decode_short(s, &v); if (!rc) memcpy(p + 2 * e, &v, 2); break; }
+            case XDRG_T_BYTE: { int8_t v; rc = xo_decode_byte(s, &v); if (!rc) p[e] = (uint8_t)v; break; }
+            default: rc = XDRG_E_INVAL;
+            }
+        }
+        if (rc) return rc;
+    }
+    return XDRG_OK;
+}
+
+/* Count of a repeated group's elements as its decoder meets them: rpcgen's
+ * `int $size = xdr.xdrDecodeInt(); x = new T[$size]` — no checkArraySize, so
+ * a negative count is NegativeArraySizeException (jrpcgen.java:886-906) —
+ * or a list's `xdrDecodeBoolean()` before every element (pmaplist.java:
+ * 52-61).  The first pass walks the group with every member's checks on a
+ * copy of the stream (walk errors come first, in the reference's order);
+ * then the element and member capacities; then the second pass decodes.   */
+static int walk_group(xo_stream *s, const xdrg_field *g, uint64_t *cnt_out, uint64_t *mcnt) {
+    const uint32_t m = g->reserved;
+    for (uint32_t j = 1; j <= m; j++) mcnt[j] = 0;
+    uint64_t cnt = 0;
+    int rc = XDRG_OK;
+    if (g->kind == XDRG_K_DYNAMIC) {
+        int32_t v;
+        rc = xo_decode_int(s, &v);
+        if (rc) return rc;
+        if (v < 0) return XDRG_E_NEG_SIZE;
+        cnt = (uint64_t)v;
+    } else if (g->kind == XDRG_K_FIXED) {
+        cnt = g->count;
+    }
+    for (uint64_t e = 0;; e++) {
+        if (g->kind == XDRG_K_LIST) {
+            int more;
+            rc = xo_decode_boolean(s, &more);
+            if (rc) return rc;
+            if (!more) break;
+        } else if (e == cnt) {
+            break;
+        }
+        for (uint32_t j = 1; j <= m; j++) {
+            const xdrg_field *f = &g[j];
+            if (f->kind == XDRG_K_DYNAMIC) {
+                int32_t len;
+                rc = xo_decode_int(s, &len);
+                if (rc) return rc;
+                size_t need;
+                if (f->type == XDRG_T_OPAQUE || f->type == XDRG_T_STRING) {
+                    if (len == 0) continue;                       /* Xdr.java:376-378 */
+                    if (len < 0) return XDRG_E_CORRUPT;           /* checkArraySize :1034-1037 */
+                    need = (size_t)len + pad4((size_t)len);
+                } else {
+                    if (len < 0) return XDRG_E_CORRUPT;
+                    need = (size_t)len * (native_size(f->type) == 8 ? 8 : 4);
+                }
+                rc = ensure_bytes(s, need);
+                if (rc) return rc;
+                s->pos += need;
+                mcnt[j] += (uint64_t)len;
+            } else {
+                size_t n = f->kind == XDRG_K_FIXED ? f->count : 1;
+                size_t need = f->type == XDRG_T_OPAQUE ? n + pad4(n)
+                            : n * ((f->type == XDRG_T_HYPER || f->type == XDRG_T_UHYPER || f->type == XDRG_T_DOUBLE) ? 8 : 4);
+                rc = ensure_bytes(s, need);
+                if (rc) return rc;
+                s->pos += need;
+            }
+        }
+        if (g->kind == XDRG_K_LIST) cnt++;
+    }
+    *cnt_out = cnt;
+    return XDRG_OK;
+}
+
+static int decode_group(xo_stream *s, const xdrg_field *g, xdrg_column *gc, uint64_t i) {
+    const uint32_t m = g->reserved;
+    uint64_t mcnt[64], cnt = 0;
+    xo_stream w = *s;
+    int rc = walk_group(&w, g, &cnt, mcnt);
+    if (rc) return rc;
+    const uint64_t e0 = g->kind == XDRG_K_FIXED ? i * g->count : gc->offsets[i];
+    if (g->kind != XDRG_K_FIXED && e0 + cnt > gc->cap) return XDRG_E_CAPACITY;
+    for (uint32_t j = 1; j <= m; j++)
+        if (g[j].kind == XDRG_K_DYNAMIC && gc[j].offsets[e0] + mcnt[j] > gc[j].cap) return XDRG_E_CAPACITY;
+    if (g->kind == XDRG_K_DYNAMIC) s->pos += 4;
+    for (uint64_t e = e0; e < e0 + cnt; e++) {
+        if (g->kind == XDRG_K_LIST) s->pos += 4;
+        for (uint32_t j = 1; j <= m; j++) {
+            rc = decode_field(s, &g[j], &gc[j], e);
+            if (rc) return rc;
+        }
+    }
+    if (g->kind == XDRG_K_LIST) s->pos += 4;
+    if (g->kind != XDRG_K_FIXED) gc->offsets[i + 1] = e0 + cnt;
     return XDRG_OK;
 }
 
@@ -632,60 +837,21 @@ static int decode_record(xo_stream *s, const xdrg_field *fs, size_t nf, xdrg_col
             c->offsets[i + 1] = c->offsets[i] + len;
             continue;
         }
-        if (f->kind == XDRG_K_DYNAMIC) {
-            size_t es = native_size(f->type);
-            uint64_t a = c->offsets[i];
-            uint8_t *base = (uint8_t *)c->data + a * es;
-            size_t cap = c->cap > a ? (size_t)(c->cap - a) : 0, got = 0;
-            switch (f->type) {
-            case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM:
-                rc = xo_decode_int_vector(s, (int32_t *)base, cap, &got); break;
-            case XDRG_T_HYPER: case XDRG_T_UHYPER:
-                rc = xo_decode_long_vector(s, (int64_t *)base, cap, &got); break;
-            case XDRG_T_FLOAT:  rc = xo_decode_float_vector(s, (float *)base, cap, &got); break;
-            case XDRG_T_DOUBLE: rc = xo_decode_double_vector(s, (double *)base, cap, &got); break;
-            case XDRG_T_SHORT:  rc = xo_decode_short_vector(s, (int16_t *)base, cap, &got); break;
-            case XDRG_T_BYTE:   rc = xo_decode_byte_vector(s, (int8_t *)base, cap, &got); break;
-            case XDRG_T_OPAQUE: case XDRG_T_STRING: {
-                const uint8_t *p; size_t len;
-                rc = f->type == XDRG_T_OPAQUE ? xo_decode_dynamic_opaque(s, &p, &len)
-                                              : xo_decode_string(s, &p, &len);
-                if (!rc && len > cap) rc = XDRG_E_CAPACITY;
-                if (!rc) { memcpy(base, p, len); got = len; }
-                break; }
-            default: rc = XDRG_E_INVAL;
-            }
+        if (f->type == XDRG_T_GROUP) {
+            rc = decode_group(s, fs + k, cols + k, i);
             if (rc) return rc;
-            c->offsets[i + 1] = a + got;
-        } else {
-            size_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
-            uint8_t *p = (uint8_t *)fixed_ptr(f, c, i);
-            if (f->type == XDRG_T_OPAQUE) { rc = xo_decode_opaque(s, p, cnt); if (rc) return rc; continue; }
-            for (size_t e = 0; e < cnt && !rc; e++) {
-                switch (f->type) {
-                case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: {
-                    int32_t v; rc = xo_decode_int(s, &v); if (!rc) memcpy(p + 4 * e, &v, 4); break; }
-                case XDRG_T_FLOAT: {
-                    float v; rc = xo_decode_float(s, &v); if (!rc) memcpy(p + 4 * e, &v, 4); break; }
-                case XDRG_T_HYPER: case XDRG_T_UHYPER: {
-                    int64_t v; rc = xo_decode_long(s, &v); if (!rc) memcpy(p + 8 * e, &v, 8); break; }
-                case XDRG_T_DOUBLE: {
-                    double v; rc = xo_decode_double(s, &v); if (!rc) memcpy(p + 8 * e, &v, 8); break; }
-                case XDRG_T_BOOL: { int v; rc = xo_decode_boolean(s, &v); if (!rc) p[e] = (uint8_t)v; break; }
-                case XDRG_T_SHORT: {
-                    int16_t v; rc = xo_decode_short(s, &v); if (!rc) memcpy(p + 2 * e, &v, 2); break; }
-                case XDRG_T_BYTE: { int8_t v; rc = xo_decode_byte(s, &v); if (!rc) p[e] = (uint8_t)v; break; }
-                default: rc = XDRG_E_INVAL;
-                }
-            }
-            if (rc) return rc;
+            k += f->reserved;   /* its members */
+            continue;
         }
+        rc = decode_field(s, f, c, i);
+        if (rc) return rc;
     }
     return XDRG_OK;
 }
 
 static uint64_t schema_fixed_size(const xdrg_field *fs, size_t nf) {
     uint64_t sz = 0;
+    if (has_group(fs, nf)) return 0;   /* repeated groups: record offsets, like dynamic fields */
     for (size_t k = 0; k < nf; k++) {
         const xdrg_field *f = &fs[k];
         if (f->kind == XDRG_K_DYNAMIC) return 0;
@@ -719,6 +885,7 @@ int xo_decode_batch_view(const xdrg_field *fs, size_t nf, const xdrg_cond *conds
                          int *err, uint32_t field, uint64_t *view_pos) {
     int rc = check_schema(fs, nf); if (rc) return rc;
     const int view = field < nf ? (int)field : -1;
+    if (view >= 0 && has_group(fs, nf)) return XDRG_E_INVAL;
     if (field != UINT32_MAX && (view < 0 || fs[field].kind != XDRG_K_DYNAMIC || !view_pos ||
         (fs[field].type != XDRG_T_OPAQUE && fs[field].type != XDRG_T_STRING))) return XDRG_E_INVAL;
     xo_conds cc;
@@ -729,7 +896,8 @@ int xo_decode_batch_view(const xdrg_field *fs, size_t nf, const xdrg_cond *conds
     for (size_t k = 0; k < nf; k++)
         if (fs[k].kind != XDRG_K_DYNAMIC && cols[k].stride == XDRG_STRIDE_CONST) return XDRG_E_INVAL;
     for (size_t k = 0; k < nf; k++)
-        if (fs[k].kind == XDRG_K_DYNAMIC && n) cols[k].offsets[0] = 0;
+        if ((fs[k].kind == XDRG_K_DYNAMIC || (fs[k].type == XDRG_T_GROUP && fs[k].kind == XDRG_K_LIST)) && n)
+            cols[k].offsets[0] = 0;
     const uint64_t stride = fixed + (framed ? 4 : 0);
     for (uint64_t i = 0; i < n; i++) {
         uint64_t a, b;

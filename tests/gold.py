@@ -5,7 +5,7 @@ import os
 import numpy as np
 
 from oncrpc4j_amd import abi
-from oncrpc4j_amd.columns import NP_DTYPE, HostBatch
+from oncrpc4j_amd.columns import NP_DTYPE, HostBatch, parents
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -24,29 +24,49 @@ def _arr(t, vals):
 
 
 def batch_from_records(fields, records):
-    """records[i][k] -> HostBatch (floats given as bit patterns, bytes as hex)."""
+    """records[i][k] -> HostBatch (floats given as bit patterns, bytes as hex).
+    A repeated group's slot holds its elements (each a list of member values)
+    and its members' slots are None (tests/golden/make_golden.py)."""
     fields = [tuple(f) for f in fields]
     n = len(records)
+    par = parents(fields)
     arrays = []
-    for k, (t, kind, c) in enumerate(fields):
-        col = [r[k] for r in records]
-        if t in (abi.T_OPAQUE, abi.T_STRING):
-            bs = [bytes.fromhex(v) for v in col]
+    for k, f in enumerate(fields):
+        t, kind, c = f[0], f[1], f[2]
+        if t == abi.T_GROUP:
+            lens = [len(r[k]) for r in records]
             if kind == abi.K_FIXED:
-                arrays.append(np.frombuffer(b"".join(bs), dtype=np.uint8).reshape(n, c).copy())
-                continue
-            vals = np.frombuffer(b"".join(bs), dtype=np.uint8).copy()
-            lens = [len(b) for b in bs]
-        elif kind == abi.K_SCALAR:
-            arrays.append(_arr(t, col))
+                arrays.append(None)
+            else:
+                offs = np.zeros(n + 1, dtype=np.uint64)
+                np.cumsum(np.array(lens, dtype=np.uint64), out=offs[1:])
+                arrays.append(offs)
             continue
-        elif kind == abi.K_FIXED:
-            arrays.append(_arr(t, col).reshape(n, c) if n else np.zeros((0, c), NP_DTYPE[t]))
-            continue
+        if par[k] >= 0:   # member j of group g: one row per element
+            g = par[k]
+            col = [e[k - g - 1] for r in records for e in r[g]]
         else:
-            vals = _arr(t, [x for v in col for x in v])
-            lens = [len(v) for v in col]
-        offs = np.zeros(n + 1, dtype=np.uint64)
-        np.cumsum(np.array(lens, dtype=np.uint64), out=offs[1:])
-        arrays.append((vals, offs))
+            col = [r[k] for r in records]
+        n_rows = len(col)
+        arrays.append(_column(t, kind, c, col, n_rows))
     return HostBatch(fields, n, arrays)
+
+
+def _column(t, kind, c, col, n):
+    """One field's array from its n row values."""
+    if t in (abi.T_OPAQUE, abi.T_STRING):
+        bs = [bytes.fromhex(v) for v in col]
+        if kind == abi.K_FIXED:
+            return np.frombuffer(b"".join(bs), dtype=np.uint8).reshape(n, c).copy()
+        vals = np.frombuffer(b"".join(bs), dtype=np.uint8).copy()
+        lens = [len(b) for b in bs]
+    elif kind == abi.K_SCALAR:
+        return _arr(t, col)
+    elif kind == abi.K_FIXED:
+        return _arr(t, col).reshape(n, c) if n else np.zeros((0, c), NP_DTYPE[t])
+    else:
+        vals = _arr(t, [x for v in col for x in v])
+        lens = [len(v) for v in col]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(np.array(lens, dtype=np.uint64), out=offs[1:])
+    return (vals, offs)

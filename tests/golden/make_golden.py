@@ -290,6 +290,97 @@ def cond_vectors(seed=0xC0ED):
     return out
 
 
+# ---- repeated groups (arrays of structs, recursive lists) -----------------------
+# A group field is [T_GROUP, kind, count, members] followed by its members.
+# rpcgen encodes `T x<>` as the count and each element (jrpcgen.java:856-880),
+# `T x[N]` without the count, and a recursive list `T *x` (struct T { ...;
+# T *next; }) as TRUE + element for every element, then FALSE (INDIRECTION,
+# jrpcgen.java:835-851; the reference's own portmap/pmaplist.java:63-70 and
+# rpcb_list.java:68-78 write the same bytes).
+T_GROUP, K_LIST = 13, 3
+GROUP_SCHEMAS = {
+    # portmap DUMP reply body: pmaplist of mapping {prog, vers, prot, port}
+    "pmaplist": [[T_GROUP, K_LIST, 0, 4], [T_INT, K_SCALAR, 0], [T_INT, K_SCALAR, 0],
+                 [T_INT, K_SCALAR, 0], [T_INT, K_SCALAR, 0]],
+    # rpcbind DUMP reply body: rpcb_list of rpcb {prog, vers, netid, addr, owner}
+    "rpcb_list": [[T_GROUP, K_LIST, 0, 5], [T_UINT, K_SCALAR, 0], [T_UINT, K_SCALAR, 0],
+                  [T_STRING, K_DYNAMIC, 0], [T_STRING, K_DYNAMIC, 0], [T_STRING, K_DYNAMIC, 0]],
+    # READDIR-shaped: struct dirlist { entry *entries; bool eof; }
+    #                 struct entry { hyper fileid; string name<>; hyper cookie; entry *next; }
+    "dirlist": [[T_GROUP, K_LIST, 0, 3], [T_HYPER, K_SCALAR, 0], [T_STRING, K_DYNAMIC, 0],
+                [T_HYPER, K_SCALAR, 0], [T_BOOL, K_SCALAR, 0]],
+    # struct { int id; item items<>; int tail; }  item = { int a; float f; opaque o<>; }
+    "array_of_structs": [[T_INT, K_SCALAR, 0], [T_GROUP, K_DYNAMIC, 0, 3], [T_INT, K_SCALAR, 0],
+                         [T_FLOAT, K_SCALAR, 0], [T_OPAQUE, K_DYNAMIC, 0], [T_INT, K_SCALAR, 0]],
+    # struct { pair p[3]; hyper h; }  pair = { short s; int v<>; }
+    "fixed_array_of_structs": [[T_GROUP, K_FIXED, 3, 2], [T_SHORT, K_SCALAR, 0],
+                               [T_INT, K_DYNAMIC, 0], [T_HYPER, K_SCALAR, 0]],
+    # two groups: struct { tag tags<>; kv *attrs; }  tag = { unsigned id; string name<>; },
+    # kv = { bool set; double d; opaque o[5]; kv *next; }
+    "two_groups": [[T_GROUP, K_DYNAMIC, 0, 2], [T_UINT, K_SCALAR, 0], [T_STRING, K_DYNAMIC, 0],
+                   [T_GROUP, K_LIST, 0, 3], [T_BOOL, K_SCALAR, 0], [T_DOUBLE, K_SCALAR, 0],
+                   [T_OPAQUE, K_FIXED, 5]],
+}
+
+
+def group_vectors(seed=0x6A0F):
+    rng = random.Random(seed)
+    out = {"source": "CPython 3.10 stdlib xdrlib (RFC 1014), arrays of structs and recursive "
+                     "lists in the order jrpcgen emits them", "seed": seed, "batches": []}
+    for name, fields in GROUP_SCHEMAS.items():
+        for framed in (False, True):
+            n = 16
+            records, chunks = [], []
+            for i in range(n):
+                rec, k = [], 0
+                while k < len(fields):
+                    f = fields[k]
+                    if f[0] != T_GROUP:
+                        rec.append(rand_value(rng, f[0], f[1], f[2]))
+                        k += 1
+                        continue
+                    mem = fields[k + 1:k + 1 + f[3]]
+                    ne = f[2] if f[1] == K_FIXED else rng.choice([0, 0, 1, 2, 3, 5, 8])
+                    rec.append([[rand_value(rng, t, kd, c) for t, kd, c in mem] for _ in range(ne)])
+                    rec.extend([None] * f[3])
+                    k += 1 + f[3]
+                p = xdrlib.Packer()
+                k = 0
+                while k < len(fields):
+                    f = fields[k]
+                    if f[0] != T_GROUP:
+                        pack_value(p, f[0], f[1], f[2], rec[k])
+                        k += 1
+                        continue
+                    mem = fields[k + 1:k + 1 + f[3]]
+
+                    def pack_elem(e, mem=mem):
+                        for (t, kd, c), v in zip(mem, e):
+                            pack_value(p, t, kd, c, v)
+                    if f[1] == K_DYNAMIC:
+                        p.pack_array(rec[k], pack_elem)
+                    elif f[1] == K_FIXED:
+                        p.pack_farray(f[2], rec[k], pack_elem)
+                    else:
+                        for e in rec[k]:
+                            p.pack_bool(True)
+                            pack_elem(e)
+                        p.pack_bool(False)
+                    k += 1 + f[3]
+                body = p.get_buffer()
+                if framed:
+                    body = struct.pack(">I", len(body) | 0x80000000) + body
+                chunks.append(body)
+                records.append(rec)
+            offs = [0]
+            for ch in chunks:
+                offs.append(offs[-1] + len(ch))
+            out["batches"].append({"name": name, "framed": framed, "fields": fields, "n": n,
+                                   "records": records, "xdr": b"".join(chunks).hex(),
+                                   "rec_offsets": offs})
+    return out
+
+
 # ---- framing -----------------------------------------------------------------
 def call_message(xid, args_string):
     """RpcMessageParserTCPTest.XdrStreamBuilder.build (:127-142): CALL header,
@@ -433,7 +524,7 @@ def main():
     for name, obj in (("kat_reference.json", kat_reference()), ("kat_jdk_nan.json", kat_jdk_nan()),
                       ("xdrlib_vectors.json", xdrlib_vectors()), ("framing.json", framing()),
                       ("rpc_vectors.json", rpc_vectors()),
-                      ("cond_vectors.json", cond_vectors())):
+                      ("cond_vectors.json", cond_vectors()), ("group_vectors.json", group_vectors())):
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1)
             f.write("\n")
