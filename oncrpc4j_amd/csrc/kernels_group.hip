@@ -1,0 +1,506 @@
+// kernels_group.hip — repeated groups: arrays of structs and recursive
+// lists (include/xdrg.h "Repeated groups").
+//
+// rpcgen encodes `T x<>` of a struct T as xdrEncodeInt(x.length) and then
+// each element's fields, `T x[N]` without the count, and decodes with
+// `new T[xdr.xdrDecodeInt()]` and no checkArraySize
+// (oncrpc4j-rpcgen .../jrpcgen/jrpcgen.java:856-906).  A recursive list
+// `T *x` (struct T { ...; T *next; }) is xdrEncodeBoolean(true) + element
+// while there is one, then xdrEncodeBoolean(false) (INDIRECTION,
+// jrpcgen.java:835-851; oncrpc4j-core portmap/pmaplist.java:50-69).
+//
+// Encode: k_grp_enc_sizes (a lane per record sums its fields, elements
+// included) -> k_scan_rows -> k_grp_enc_place (a wave per record; elements
+// of fixed size go a lane per element at computed positions, others a lane
+// per element after a wave scan of their sizes).
+// Decode: k_grp_dec_walk (a lane per record walks every count, list bool
+// and member length in the reference's order and reports the first failing
+// check) -> k_scan_rows over the counted columns -> k_grp_dec_offsets
+// (native offsets, capacity) -> k_grp_dec_place (a wave per record walks
+// again in lockstep, lanes move payload words).
+#include <hip/hip_runtime.h>
+
+#include "xdrg_device.h"
+#include "xdrg_internal.h"
+
+namespace xdrg {
+
+typedef uint32_t u32g __attribute__((aligned(1)));
+
+__device__ __forceinline__ uint64_t g_dyn_bytes(const GField &f, uint64_t cnt) {
+    return 4 + (f.xsz == 1 ? cnt + pad4(cnt) : cnt * f.xsz);
+}
+__device__ __forceinline__ uint32_t g_ld(const uint8_t *p) { return bswap32r(*(const uint32_t *)p); }
+
+// Elements [e0, e0 + cnt) of group g in record r (DYNAMIC / LIST: its
+// offsets; FIXED: r * count on).
+__device__ __forceinline__ void g_range(const GField &g, uint64_t r, uint64_t &e0, uint64_t &cnt) {
+    if (g.kind == XDRG_K_FIXED) {
+        e0 = r * g.count;
+        cnt = g.count;
+    } else {
+        e0 = g.offsets[r];
+        cnt = g.offsets[r + 1] - e0;
+    }
+}
+
+// XDR word w of fixed field f at row i (a record, or an element of a group).
+__device__ __forceinline__ uint32_t g_fixed_word(const GField &f, uint64_t i, uint32_t w) {
+    const uint8_t *base = f.data + (int64_t)i * f.stride;
+    if (f.type == XDRG_T_OPAQUE) {   // bytes + zero pad (Xdr.java:776-781)
+        const uint32_t rem = f.count - 4 * w;
+        return load_bytes(base + 4 * w, rem < 4 ? rem : 4);
+    }
+    if (f.xsz == 8) return enc_elem(f.type, base + (uint64_t)(w >> 1) * 8, w & 1);
+    return enc_elem(f.type, base + (uint64_t)w * f.nsz, 0);
+}
+__device__ __forceinline__ void g_fixed_store(const GField &f, uint64_t i, uint32_t w, uint32_t v) {
+    uint8_t *base = f.data + (int64_t)i * f.stride;
+    if (f.type == XDRG_T_OPAQUE) {   // pad skipped unchecked (Xdr.java:341-349)
+        const uint32_t rem = f.count - 4 * w, kb = rem < 4 ? rem : 4;
+        if (kb == 4) *(u32g *)(base + 4 * w) = v;
+        else for (uint32_t b = 0; b < kb; ++b) base[4 * w + b] = (uint8_t)(v >> (8 * b));
+        return;
+    }
+    if (f.xsz == 8) dec_elem(f.type, base + (uint64_t)(w >> 1) * 8, w & 1, v);
+    else dec_elem(f.type, base + (uint64_t)w * f.nsz, 0, v);
+}
+// Payload word w (after the length word) of a dynamic field whose row owns
+// elements [e0, e0 + cnt).
+__device__ __forceinline__ uint32_t g_dyn_word(const GField &f, uint64_t e0, uint64_t cnt, uint64_t w) {
+    if (f.xsz == 1) {
+        const uint64_t b = 4 * w;
+        const uint8_t *src = f.data + e0 + b;
+        return cnt - b >= 4 ? *(const u32g *)src : load_bytes(src, (uint32_t)(cnt - b));
+    }
+    if (f.xsz == 8) return enc_elem(f.type, f.data + (e0 + (w >> 1)) * 8, (uint32_t)(w & 1));
+    return enc_elem(f.type, f.data + (e0 + w) * f.nsz, 0);
+}
+__device__ __forceinline__ void g_dyn_store(const GField &f, uint64_t e0, uint64_t cnt, uint64_t w, uint32_t v) {
+    if (f.xsz == 1) {
+        const uint64_t b = 4 * w;
+        uint8_t *dst = f.data + e0 + b;
+        if (cnt - b >= 4) *(u32g *)dst = v;
+        else for (uint64_t i = 0; i < cnt - b; ++i) dst[i] = (uint8_t)(v >> (8 * i));
+        return;
+    }
+    if (f.xsz == 8) dec_elem(f.type, f.data + (e0 + (w >> 1)) * 8, (uint32_t)(w & 1), v);
+    else dec_elem(f.type, f.data + (e0 + w) * f.nsz, 0, v);
+}
+__device__ __forceinline__ uint64_t g_dyn_words(const GField &f, uint64_t cnt) {
+    return f.xsz == 1 ? (cnt + 3) >> 2 : cnt * (f.xsz >> 2);
+}
+
+// XDR bytes of element e of group g (its list bool included).
+__device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g, uint64_t e) {
+    uint64_t s = a.f[g].efix;
+    for (uint32_t j = 1; j <= a.f[g].nmem; ++j) {
+        const GField &m = a.f[g + j];
+        if (m.kind == XDRG_K_DYNAMIC) s += g_dyn_bytes(m, m.offsets[e + 1] - m.offsets[e]);
+    }
+    return s;
+}
+
+// ===========================================================================
+// Encode
+// ===========================================================================
+__device__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
+    uint64_t s = a.framed ? 4 : 0;
+    for (uint32_t k = 0; k < a.nf;) {
+        const GField &f = a.f[k];
+        if (f.type == XDRG_T_GROUP) {
+            uint64_t e0, cnt;
+            g_range(f, r, e0, cnt);
+            s += f.kind == XDRG_K_FIXED ? 0 : 4;   // the count, or a list's closing bool
+            if (f.ndm) for (uint64_t e = e0; e < e0 + cnt; ++e) s += g_elem_bytes(a, k, e);
+            else s += cnt * f.efix;
+            k += 1 + f.nmem;
+            continue;
+        }
+        s += f.kind == XDRG_K_DYNAMIC ? g_dyn_bytes(f, f.offsets[r + 1] - f.offsets[r]) : (uint64_t)f.xbytes;
+        ++k;
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a) {
+    const uint64_t r0 = (uint64_t)blockIdx.x * kRecPerBlock + (uint64_t)threadIdx.x * kRecPerThread;
+    uint64_t s = 0;
+    for (int j = 0; j < kRecPerThread; ++j) {
+        const uint64_t r = r0 + j;
+        if (r >= a.n) break;
+        const uint64_t z = g_rec_size(a, r);
+        a.rec_size[r] = z;
+        s += z;
+    }
+    const uint64_t tot = block_sum(s);
+    if (threadIdx.x == 0) a.block_sums[blockIdx.x] = tot;
+}
+
+// One lane writes element e of group g at stream byte p.
+__device__ void g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t p) {
+    uint8_t *out = a.xdr;
+    if (a.f[g].kind == XDRG_K_LIST) {   // xdrEncodeBoolean(true) (pmaplist.java:65-67)
+        *(uint32_t *)(out + p) = bswap32r(1u);
+        p += 4;
+    }
+    for (uint32_t j = 1; j <= a.f[g].nmem; ++j) {
+        const GField &m = a.f[g + j];
+        if (m.kind != XDRG_K_DYNAMIC) {
+            for (uint32_t w = 0; w < m.xbytes >> 2; ++w) *(uint32_t *)(out + p + 4 * w) = g_fixed_word(m, e, w);
+            p += m.xbytes;
+            continue;
+        }
+        const uint64_t e0 = m.offsets[e], cnt = m.offsets[e + 1] - e0;
+        *(uint32_t *)(out + p) = bswap32r((uint32_t)cnt);
+        const uint64_t nw = g_dyn_words(m, cnt);
+        for (uint64_t w = 0; w < nw; ++w) *(uint32_t *)(out + p + 4 + 4 * w) = g_dyn_word(m, e0, cnt, w);
+        p += 4 + 4 * nw;
+    }
+}
+
+// One wavefront writes record r at stream byte pos.
+__device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint64_t size) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint8_t *out = a.xdr;
+    if (a.framed) {   // GrizzlyRpcTransport.java:103-110
+        if (lane == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
+        pos += 4;
+    }
+    for (uint32_t k = 0; k < a.nf;) {
+        const GField &f = a.f[k];
+        if (f.type == XDRG_T_GROUP) {
+            uint64_t e0, cnt;
+            g_range(f, r, e0, cnt);
+            if (f.kind == XDRG_K_DYNAMIC) {   // xdrEncodeInt($size) (jrpcgen.java:866-876)
+                if (lane == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)cnt);
+                pos += 4;
+            }
+            if (!f.ndm) {   // elements of one size: a lane per element
+                for (uint64_t i = lane; i < cnt; i += 64) g_enc_elem(a, k, e0 + i, pos + i * f.efix);
+                pos += cnt * f.efix;
+            } else {        // a lane per element at its scanned position
+                for (uint64_t b = 0; b < cnt; b += 64) {
+                    const uint64_t i = b + lane;
+                    const uint64_t z = i < cnt ? g_elem_bytes(a, k, e0 + i) : 0;
+                    const uint64_t incl = wave_incl_scan(z);
+                    if (i < cnt) g_enc_elem(a, k, e0 + i, pos + incl - z);
+                    pos += __shfl(incl, 63, 64);
+                }
+            }
+            if (f.kind == XDRG_K_LIST) {   // xdrEncodeBoolean(false): the list ends
+                if (lane == 0) *(uint32_t *)(out + pos) = 0;
+                pos += 4;
+            }
+            k += 1 + f.nmem;
+            continue;
+        }
+        if (f.kind != XDRG_K_DYNAMIC) {
+            for (uint32_t w = lane; w < f.xbytes >> 2; w += 64) *(uint32_t *)(out + pos + 4 * w) = g_fixed_word(f, r, w);
+            pos += f.xbytes;
+        } else {
+            const uint64_t e0 = f.offsets[r], cnt = f.offsets[r + 1] - e0;
+            if (lane == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)cnt);
+            const uint64_t nw = g_dyn_words(f, cnt);
+            for (uint64_t w = lane; w < nw; w += 64) *(uint32_t *)(out + pos + 4 + 4 * w) = g_dyn_word(f, e0, cnt, w);
+            pos += 4 + 4 * nw;
+        }
+        ++k;
+    }
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a) {
+    __shared__ uint64_t soff[kRecPerBlock + 1];
+    const uint64_t total = a.totals[0];
+    if (total > a.xdr_cap) return;   // XDRG_E_CAPACITY: write nothing
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t t0 = threadIdx.x * kRecPerThread;
+    uint64_t sz[kRecPerThread], s = 0;
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        sz[j] = rb + t0 + j < a.n ? a.rec_size[rb + t0 + j] : 0;
+        s += sz[j];
+    }
+    uint64_t btot;
+    uint64_t off = a.block_sums[blockIdx.x] + block_excl_scan(s, &btot);
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        soff[t0 + j] = off;
+        if (a.rec_out && rb + t0 + j < a.n) a.rec_out[rb + t0 + j] = off;
+        off += sz[j];
+    }
+    if (threadIdx.x == kRecThreads - 1) soff[kRecPerBlock] = off;
+    if (a.rec_out && blockIdx.x == 0 && threadIdx.x == 0) a.rec_out[a.n] = total;
+    __syncthreads();
+    const uint64_t nrec = a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock;
+    for (uint32_t j = threadIdx.x >> 6; j < nrec; j += kRecThreads / 64)
+        g_enc_record(a, rb + j, soff[j], soff[j + 1] - soff[j]);
+}
+
+// ===========================================================================
+// Decode
+// ===========================================================================
+struct GExtent { uint64_t a, b; };
+__device__ __forceinline__ GExtent g_extent(const GroupArgs &a, uint64_t r) {
+    GExtent e{a.rec_in[r], a.rec_in[r + 1]};
+    if (e.b > a.xdr_cap) e.b = a.xdr_cap;
+    if (e.a > e.b) e.a = e.b;
+    return e;
+}
+
+// A dynamic field's length word at pos, then its payload: the reference's
+// check order (Xdr.java:171-175 length, :374-383 / :392-401 len == 0 first,
+// checkArraySize :1034-1037, ensureBytes :1028-1032).  Returns 0 or an error.
+__device__ __forceinline__ uint32_t g_walk_dyn(const GField &f, const uint8_t *in, uint64_t end, uint64_t &pos,
+                                               uint32_t &len_out) {
+    if (end - pos < 4) return XDRG_E_SHORT;
+    const int32_t len = (int32_t)g_ld(in + pos);
+    pos += 4;
+    uint64_t need;
+    if (f.xsz == 1) {
+        if (len == 0) { len_out = 0; return 0; }
+        if (len < 0) return XDRG_E_CORRUPT;
+        need = (uint64_t)len + pad4((uint64_t)len);
+    } else {
+        if (len < 0) return XDRG_E_CORRUPT;
+        need = (uint64_t)len * f.xsz;
+    }
+    if (end - pos < need) return XDRG_E_SHORT;
+    pos += need;
+    len_out = (uint32_t)len;
+    return 0;
+}
+
+// Walk record r; cnt[s] = the record's count of counted column s.
+__device__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxSlots], uint32_t *sub) {
+    const GExtent e = g_extent(a, r);
+    const uint8_t *in = a.xdr;
+    uint64_t pos = e.a;
+    *sub = 0;
+    if (a.framed) {   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
+        if (e.b - pos < 4) return XDRG_E_SHORT;
+        const uint32_t m = g_ld(in + pos);
+        if (!(m & kLastFrag) || (uint64_t)(m & kSizeMask) != e.b - pos - 4) return XDRG_E_FRAME;
+        pos += 4;
+    }
+    for (uint32_t k = 0; k < a.nf;) {
+        const GField &f = a.f[k];
+        *sub = 2 * k + 1;
+        if (f.type == XDRG_T_GROUP) {
+            uint64_t n;
+            if (f.kind == XDRG_K_DYNAMIC) {   // int $size = xdr.xdrDecodeInt(); new T[$size]
+                if (e.b - pos < 4) return XDRG_E_SHORT;
+                const int32_t c = (int32_t)g_ld(in + pos);
+                pos += 4;
+                if (c < 0) return XDRG_E_NEG_SIZE;
+                n = (uint64_t)c;
+            } else {
+                n = f.kind == XDRG_K_FIXED ? f.count : ~0ull;
+            }
+            if (!f.ndm && f.kind != XDRG_K_LIST) {   // elements of one size
+                if ((e.b - pos) / f.efix < n) return XDRG_E_SHORT;
+                pos += n * f.efix;
+            } else {
+                uint64_t i = 0;
+                for (;; ++i) {
+                    if (f.kind == XDRG_K_LIST) {   // xdrDecodeBoolean(): any non-zero = another
+                        if (e.b - pos < 4) return XDRG_E_SHORT;
+                        const uint32_t more = g_ld(in + pos);
+                        pos += 4;
+                        if (!more) break;
+                    } else if (i == n) {
+                        break;
+                    }
+                    for (uint32_t j = 1; j <= f.nmem; ++j) {
+                        const GField &m = a.f[k + j];
+                        if (m.kind != XDRG_K_DYNAMIC) {
+                            if (e.b - pos < m.xbytes) return XDRG_E_SHORT;
+                            pos += m.xbytes;
+                        } else {
+                            uint32_t len = 0;
+                            const uint32_t err = g_walk_dyn(m, in, e.b, pos, len);
+                            if (err) return err;
+                            cnt[m.slot - 1] += len;
+                        }
+                    }
+                }
+                n = i;
+            }
+            if (f.slot) cnt[f.slot - 1] = (uint32_t)n;
+            k += 1 + f.nmem;
+            continue;
+        }
+        if (f.kind != XDRG_K_DYNAMIC) {
+            if (e.b - pos < f.xbytes) return XDRG_E_SHORT;   // ensureBytes (Xdr.java:1028-1032)
+            pos += f.xbytes;
+        } else {
+            uint32_t len = 0;
+            const uint32_t err = g_walk_dyn(f, in, e.b, pos, len);
+            if (err) return err;
+            cnt[f.slot - 1] = len;
+        }
+        ++k;
+    }
+    return 0;
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a) {
+    const uint64_t r0 = (uint64_t)blockIdx.x * kRecPerBlock + (uint64_t)threadIdx.x * kRecPerThread;
+    uint64_t sums[kMaxSlots];
+    for (uint32_t s = 0; s < a.nslot; ++s) sums[s] = 0;
+    for (int j = 0; j < kRecPerThread; ++j) {
+        const uint64_t r = r0 + j;
+        if (r >= a.n) break;
+        uint32_t cnt[kMaxSlots];
+        for (uint32_t s = 0; s < a.nslot; ++s) cnt[s] = 0;
+        uint32_t sub;
+        const uint32_t err = g_walk(a, r, cnt, &sub);
+        if (err) {
+            atomicMin(a.errkey, err_key(r, sub, err));
+            for (uint32_t s = 0; s < a.nslot; ++s) cnt[s] = 0;   // a failed record owns nothing
+        }
+        for (uint32_t s = 0; s < a.nslot; ++s) {
+            a.rec_cnt[(uint64_t)s * a.n + r] = cnt[s];
+            sums[s] += cnt[s];
+        }
+    }
+    for (uint32_t s = 0; s < a.nslot; ++s) {
+        const uint64_t tot = block_sum(sums[s]);
+        if (threadIdx.x == 0) a.block_sums[(uint64_t)s * a.nblocks + blockIdx.x] = tot;
+    }
+}
+
+// Native offsets of every counted column (the columns' offsets arrays for
+// top-level fields and groups, rec_base for all), capacity per record.
+__global__ __launch_bounds__(kRecThreads) void k_grp_dec_offsets(const GroupArgs a) {
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t t0 = threadIdx.x * kRecPerThread;
+    for (uint32_t s = 0; s < a.nslot; ++s) {
+        const uint32_t k = a.slot_field[s];
+        const GField &f = a.f[k];
+        uint32_t c[kRecPerThread];
+        uint64_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            const uint64_t r = rb + t0 + j;
+            c[j] = r < a.n ? a.rec_cnt[(uint64_t)s * a.n + r] : 0u;
+            sum += c[j];
+        }
+        uint64_t btot;
+        uint64_t off = a.block_sums[(uint64_t)s * a.nblocks + blockIdx.x] + block_excl_scan(sum, &btot);
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            const uint64_t r = rb + t0 + j;
+            if (r < a.n) {
+                a.rec_base[(uint64_t)s * a.n + r] = off;
+                if (!f.grp) f.offsets[r] = off;   // members: per element, by the place kernel
+                if (off + c[j] > f.cap) atomicMin(a.errkey, err_key(r, 2 * f.top + 2, XDRG_E_CAPACITY));
+            }
+            off += c[j];
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) {   // offsets[rows] = the column's total
+            if (!f.grp) {
+                f.offsets[a.n] = a.totals[s];
+            } else {
+                const GField &g = a.f[f.grp - 1];
+                const uint64_t rows = g.kind == XDRG_K_FIXED ? a.n * g.count : a.totals[g.slot - 1];
+                if (a.totals[s] <= f.cap && (g.kind == XDRG_K_FIXED || rows <= g.cap)) f.offsets[rows] = a.totals[s];
+            }
+        }
+    }
+}
+
+// One wavefront decodes record r (walked clean, capacity checked).
+__device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint8_t *in = a.xdr;
+    uint64_t pos = a.rec_in[r] + (a.framed ? 4 : 0);
+    for (uint32_t k = 0; k < a.nf;) {
+        const GField &f = a.f[k];
+        if (f.type == XDRG_T_GROUP) {
+            const uint64_t e0 = f.kind == XDRG_K_FIXED ? r * f.count : a.rec_base[(uint64_t)(f.slot - 1) * a.n + r];
+            const uint64_t cnt = f.kind == XDRG_K_FIXED ? f.count : a.rec_cnt[(uint64_t)(f.slot - 1) * a.n + r];
+            if (f.kind == XDRG_K_DYNAMIC) pos += 4;
+            const uint32_t lb = f.kind == XDRG_K_LIST ? 4 : 0;   // each list element's bool
+            if (!f.ndm) {   // elements of one size: a lane per element
+                for (uint64_t i = lane; i < cnt; i += 64) {
+                    uint64_t p = pos + i * f.efix + lb;
+                    for (uint32_t j = 1; j <= f.nmem; ++j) {
+                        const GField &m = a.f[k + j];
+                        for (uint32_t w = 0; w < m.xbytes >> 2; ++w) g_fixed_store(m, e0 + i, w, *(const uint32_t *)(in + p + 4 * w));
+                        p += m.xbytes;
+                    }
+                }
+                pos += cnt * f.efix;
+            } else {        // element by element; lanes move each member's words
+                uint64_t mb[kMaxFields];
+                for (uint32_t j = 1; j <= f.nmem; ++j) {
+                    const GField &m = a.f[k + j];
+                    mb[j - 1] = m.kind == XDRG_K_DYNAMIC ? a.rec_base[(uint64_t)(m.slot - 1) * a.n + r] : 0;
+                }
+                for (uint64_t i = 0; i < cnt; ++i) {
+                    pos += lb;
+                    const uint64_t e = e0 + i;
+                    for (uint32_t j = 1; j <= f.nmem; ++j) {
+                        const GField &m = a.f[k + j];
+                        if (m.kind != XDRG_K_DYNAMIC) {
+                            for (uint32_t w = lane; w < m.xbytes >> 2; w += 64) g_fixed_store(m, e, w, *(const uint32_t *)(in + pos + 4 * w));
+                            pos += m.xbytes;
+                            continue;
+                        }
+                        const uint64_t len = g_ld(in + pos);
+                        if (lane == 0) m.offsets[e] = mb[j - 1];
+                        const uint64_t nw = g_dyn_words(m, len);
+                        for (uint64_t w = lane; w < nw; w += 64) g_dyn_store(m, mb[j - 1], len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
+                        mb[j - 1] += len;
+                        pos += 4 + 4 * nw;
+                    }
+                }
+                // the entry after the record's last element (the next record
+                // writes the same value; a failed next record does not run)
+                if (lane == 0)
+                    for (uint32_t j = 1; j <= f.nmem; ++j)
+                        if (a.f[k + j].kind == XDRG_K_DYNAMIC) a.f[k + j].offsets[e0 + cnt] = mb[j - 1];
+            }
+            if (f.kind == XDRG_K_LIST) pos += 4;
+            k += 1 + f.nmem;
+            continue;
+        }
+        if (f.kind != XDRG_K_DYNAMIC) {
+            for (uint32_t w = lane; w < f.xbytes >> 2; w += 64) g_fixed_store(f, r, w, *(const uint32_t *)(in + pos + 4 * w));
+            pos += f.xbytes;
+        } else {
+            const uint64_t len = g_ld(in + pos);
+            const uint64_t e0 = a.rec_base[(uint64_t)(f.slot - 1) * a.n + r];
+            const uint64_t nw = g_dyn_words(f, len);
+            for (uint64_t w = lane; w < nw; w += 64) g_dyn_store(f, e0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
+            pos += 4 + 4 * nw;
+        }
+        ++k;
+    }
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_grp_dec_place(const GroupArgs a) {
+    const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
+    const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    uint64_t nrec = bad > rb ? bad - rb : 0;
+    if (nrec > kRecPerBlock) nrec = kRecPerBlock;
+    for (uint32_t j = threadIdx.x >> 6; j < nrec; j += kRecThreads / 64) g_dec_record(a, rb + j);
+}
+
+int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((uint32_t)a.nblocks), block(kRecThreads);
+    switch (phase) {
+    case GRP_ENC_SIZES: hipLaunchKernelGGL(k_grp_enc_sizes, grid, block, 0, st, a); break;
+    case GRP_ENC_PLACE: hipLaunchKernelGGL(k_grp_enc_place, grid, block, 0, st, a); break;
+    case GRP_DEC_WALK: hipLaunchKernelGGL(k_grp_dec_walk, grid, block, 0, st, a); break;
+    case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
+    case GRP_DEC_PLACE: hipLaunchKernelGGL(k_grp_dec_place, grid, block, 0, st, a); break;
+    default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+
+}  // namespace xdrg

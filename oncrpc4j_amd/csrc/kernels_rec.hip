@@ -27,20 +27,10 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "xdrg_device.h"
 #include "xdrg_internal.h"
 
 namespace xdrg {
-
-__device__ __forceinline__ uint32_t bswap32r(uint32_t x) { return __builtin_bswap32(x); }
-__device__ __forceinline__ uint32_t pad4(uint64_t n) { return (uint32_t)((4 - (n & 3)) & 3); }
-
-__device__ __forceinline__ uint32_t canon_f32r(uint32_t u) {
-    return ((u & 0x7fffffffu) > 0x7f800000u) ? 0x7fc00000u : u;
-}
-__device__ __forceinline__ void canon_f64r(uint32_t &hi, uint32_t &lo) {
-    const uint32_t h = hi & 0x7fffffffu;
-    if (h > 0x7ff00000u || (h == 0x7ff00000u && lo != 0)) { hi = 0x7ff80000u; lo = 0; }
-}
 
 // XDR bytes of a dynamic field holding `cnt` elements (length word included).
 __device__ __forceinline__ uint64_t dyn_xdr_bytes(const VField &f, uint64_t cnt) {
@@ -88,84 +78,6 @@ __device__ __forceinline__ void cond_mark(const VField &f, uint32_t k, int32_t x
 __device__ __forceinline__ int32_t disc_native(const VField &f, uint64_t r) {
     const uint8_t *p = f.data + (int64_t)r * f.stride;
     return f.type == XDRG_T_BOOL ? (int32_t)(*p != 0) : *(const int32_t *)p;
-}
-
-// ---- element words ---------------------------------------------------------
-// XDR word `half` (0 = first) of one native element at p.
-__device__ __forceinline__ uint32_t enc_elem(uint32_t type, const uint8_t *p, uint32_t half) {
-    switch (type) {
-    case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: return bswap32r(*(const uint32_t *)p);
-    case XDRG_T_FLOAT: return bswap32r(canon_f32r(*(const uint32_t *)p));
-    case XDRG_T_HYPER: case XDRG_T_UHYPER: return bswap32r(*(const uint32_t *)(p + (half ? 0 : 4)));
-    case XDRG_T_DOUBLE: {
-        uint32_t lo = *(const uint32_t *)p, hi = *(const uint32_t *)(p + 4);
-        canon_f64r(hi, lo);
-        return bswap32r(half ? lo : hi);
-    }
-    case XDRG_T_BOOL: return *p ? 0x01000000u : 0u;
-    case XDRG_T_SHORT: return bswap32r((uint32_t)(int32_t)*(const int16_t *)p);
-    case XDRG_T_BYTE: return bswap32r((uint32_t)(int32_t)*(const int8_t *)p);
-    default: return 0;
-    }
-}
-__device__ __forceinline__ void dec_elem(uint32_t type, uint8_t *p, uint32_t half, uint32_t v) {
-    switch (type) {
-    case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: case XDRG_T_FLOAT:
-        *(uint32_t *)p = bswap32r(v); break;
-    case XDRG_T_HYPER: case XDRG_T_UHYPER: case XDRG_T_DOUBLE:
-        *(uint32_t *)(p + (half ? 0 : 4)) = bswap32r(v); break;
-    case XDRG_T_BOOL: *p = v != 0; break;
-    case XDRG_T_SHORT: *(uint16_t *)p = (uint16_t)bswap32r(v); break;
-    case XDRG_T_BYTE: *p = (uint8_t)bswap32r(v); break;
-    default: break;
-    }
-}
-
-// k (1..4) bytes starting at an arbitrarily aligned p, as they sit in memory
-// (little-endian word).  Only dwords that hold a requested byte are read, so
-// no access leaves the page of a valid byte.
-__device__ __forceinline__ uint32_t load_bytes(const uint8_t *p, uint32_t k) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t *q = (const uint32_t *)(a - sh);
-    const uint32_t lo = q[0];
-    const uint32_t hi = (sh + k > 4) ? q[1] : 0u;
-    uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
-    if (k < 4) v &= (1u << (8 * k)) - 1u;
-    return v;
-}
-
-// ---- block-wide exclusive scan (256 threads = 4 waves of 64) ----------------
-__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
-// Returns the exclusive prefix of v over the block; *total = block sum.
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *total) {
-    __shared__ uint64_t wsum[kRecThreads / 64];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t incl = wave_incl_scan(v);
-    if (lane == 63) wsum[wid] = incl;
-    __syncthreads();
-    uint64_t before = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kRecThreads / 64; ++w) {
-        if (w < wid) before += wsum[w];
-        tot += wsum[w];
-    }
-    __syncthreads();
-    *total = tot;
-    return before + incl - v;
-}
-__device__ __forceinline__ uint64_t block_sum(uint64_t v) {
-    uint64_t tot;
-    (void)block_excl_scan(v, &tot);
-    return tot;
 }
 
 // ---- scan of per-block sums: one block (1024 threads) per row ---------------
@@ -2550,6 +2462,12 @@ static void launch_ur(int u, int r, dim3 grid, size_t lds, hipStream_t st, const
 }
 template <int U, int R> struct EncG { static constexpr auto fn = k_enc_place_g<U, R>; };
 template <int U, int R> struct DecG { static constexpr auto fn = k_dec_place_g<U, R>; };
+
+int launch_scan_rows(uint64_t *sums, uint64_t nblocks, uint64_t *totals, uint32_t rows, void *stream) {
+    if (!rows) return hipSuccess;
+    hipLaunchKernelGGL(k_scan_rows, dim3(rows), dim3(1024), 0, (hipStream_t)stream, sums, nblocks, totals);
+    return (int)hipGetLastError();
+}
 
 int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stream) {
     RecArgs a = args;

@@ -38,6 +38,10 @@ struct xdrg_schema {
     uint32_t ncond = 0;
     bool stream_types = true;       // every field is word-for-word (int/float/hyper/double/opaque%4)
     uint32_t nwords = 0;
+    // repeated groups (include/xdrg.h): grp[k] = its group's index + 1 for a
+    // member, 0 otherwise; such schemas take the group kernels
+    std::vector<uint32_t> grp;
+    uint32_t ngroups = 0;
 };
 
 static uint32_t native_size(uint32_t t) {
@@ -86,8 +90,38 @@ extern "C" int xdrg_schema_create_cond(const xdrg_field *fields, size_t nfields,
     xdrg_schema *s = new (std::nothrow) xdrg_schema();
     if (!s) return XDRG_E_NOMEM;
     uint64_t words = 0;
+    // repeated groups: {XDRG_T_GROUP, FIXED / DYNAMIC / LIST, count, m} and m
+    // member fields of the base types, an element of at least one XDR word
+    s->grp.assign(nfields, 0);
+    for (size_t k = 0; k < nfields; ++k) {
+        const xdrg_field &g = fields[k];
+        if (g.type != XDRG_T_GROUP) continue;
+        const uint32_t m = g.reserved;
+        bool ok = g.kind >= XDRG_K_FIXED && g.kind <= XDRG_K_LIST && m >= 1 && (size_t)m < nfields - k &&
+                  !(g.kind == XDRG_K_FIXED && g.count > 0x7fffffffu) && !(g.kind == XDRG_K_LIST && g.count);
+        bool sized = g.kind == XDRG_K_LIST;
+        for (uint32_t j = 1; ok && j <= m; ++j) {
+            const xdrg_field &f = fields[k + j];
+            ok = field_valid(f);
+            sized |= f.kind != XDRG_K_FIXED || f.count > 0;
+            s->grp[k + j] = (uint32_t)k + 1;
+        }
+        if (!ok || !sized || nconds) { delete s; return XDRG_E_INVAL; }   // no conditions with groups
+        ++s->ngroups;
+        k += m;
+    }
     for (size_t k = 0; k < nfields; ++k) {
         const xdrg_field &f = fields[k];
+        if (f.type == XDRG_T_GROUP) {   // a record's elements: counted on the device
+            s->f.push_back(f);
+            s->nsz.push_back(0);
+            s->xsz.push_back(0);
+            s->wpos.push_back((uint32_t)words);
+            s->xbytes.push_back(0);
+            s->var_size = true;
+            s->stream_types = false;
+            continue;
+        }
         if (!field_valid(f)) { delete s; return XDRG_E_INVAL; }
         s->f.push_back(f);
         s->nsz.push_back(native_size(f.type));
@@ -318,6 +352,7 @@ extern "C" const char *xdrg_status_string(int status) {
     case XDRG_E_HIP: return "HIP runtime error";
     case XDRG_E_NOMEM: return "out of memory";
     case XDRG_E_INCOMPLETE: return "not all fragments arrived";
+    case XDRG_E_NEG_SIZE: return "negative array size";   // NegativeArraySizeException
     default: return "unknown status";
     }
 }
@@ -416,6 +451,11 @@ static int check_columns(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *c
     if (!cols) return inval(c, "columns are NULL");
     for (size_t k = 0; k < s->f.size(); ++k) {
         const xdrg_field &f = s->f[k];
+        if (f.type == XDRG_T_GROUP) {
+            if (f.kind != XDRG_K_FIXED && !cols[k].offsets) return inval(c, "group column without offsets");
+            continue;
+        }
+        if (s->grp[k] && f.kind != XDRG_K_DYNAMIC && !cols[k].data) return inval(c, "group member data is NULL");
         const uint32_t al = s->nsz[k] >= 4 ? 4 : s->nsz[k];
         if (f.kind == XDRG_K_DYNAMIC) {
             if (!cols[k].offsets) return inval(c, "dynamic column without offsets");
@@ -558,6 +598,107 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
     return XDRG_OK;
 }
 
+// Kernel arguments and workspace of a schema with repeated groups.
+static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool framed,
+                      bool decode, GroupArgs &a) {
+    memset(&a, 0, sizeof a);
+    a.n = n;
+    a.nf = (uint32_t)s->f.size();
+    a.framed = framed;
+    for (size_t k = 0; k < s->f.size(); ++k) {
+        GField &v = a.f[k];
+        const xdrg_field &f = s->f[k];
+        v.type = f.type;
+        v.kind = f.kind;
+        v.nsz = s->nsz[k];
+        v.xsz = s->xsz[k];
+        v.count = f.count;
+        v.xbytes = s->xbytes[k];
+        v.grp = s->grp[k];
+        v.top = v.grp ? v.grp - 1 : (uint32_t)k;
+        v.data = (uint8_t *)cols[k].data;
+        v.stride = (f.kind == XDRG_K_DYNAMIC || f.type == XDRG_T_GROUP) ? 0 : eff_stride(s, k, cols[k]);
+        v.offsets = cols[k].offsets;
+        v.cap = cols[k].cap;
+        const bool counted = (f.type == XDRG_T_GROUP && f.kind != XDRG_K_FIXED) ||
+                             (f.type != XDRG_T_GROUP && f.kind == XDRG_K_DYNAMIC);
+        if (counted) {
+            if (a.nslot == (uint32_t)kMaxSlots) return inval(c, "too many counted columns in a group schema");
+            a.slot_field[a.nslot] = (uint32_t)k;
+            v.slot = ++a.nslot;
+        }
+        if (f.type == XDRG_T_GROUP) {
+            v.nmem = f.reserved;
+            v.efix = f.kind == XDRG_K_LIST ? 4 : 0;
+            for (uint32_t j = 1; j <= f.reserved; ++j) {
+                if (s->f[k + j].kind == XDRG_K_DYNAMIC) ++v.ndm;
+                else v.efix += s->xbytes[k + j];
+            }
+        }
+    }
+    a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;
+    if (!a.nblocks) a.nblocks = 1;
+    const size_t rows = a.nslot ? a.nslot : 1;
+    // block sums [rows][nblocks] | totals [rows] | encode: sizes [n] / decode: counts u32 [nslot][n]
+    // and native offsets [nslot][n]
+    const size_t sums = rows * a.nblocks + rows + 8;
+    const size_t per_rec = decode ? (a.nslot * n + 1) / 2 + a.nslot * n : n;
+    int rc = ensure_ws(c, sums + per_rec + 1);
+    if (rc) return rc;
+    a.block_sums = c->d_ws;
+    a.totals = c->d_ws + rows * a.nblocks;
+    if (decode) {
+        a.rec_cnt = (uint32_t *)(c->d_ws + sums);
+        a.rec_base = c->d_ws + sums + (a.nslot * n + 1) / 2;
+    } else {
+        a.rec_size = c->d_ws + sums;
+    }
+    a.errkey = c->d_stat;
+    return XDRG_OK;
+}
+
+static int group_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, uint8_t *out,
+                        uint64_t out_cap, uint64_t *rec_offsets, bool framed, bool async, uint64_t *out_len) {
+    if (n == 0) {
+        if (rec_offsets) HIPCHK(c, hipMemsetAsync(rec_offsets, 0, 8, c->stream));
+        if (out_len && !async) *out_len = 0;
+        if (out_len && async) HIPCHK(c, (hipError_t)launch_store_u64(out_len, 0, c->stream));
+        if (!async) HIPCHK(c, hipStreamSynchronize(c->stream));
+        return XDRG_OK;
+    }
+    GroupArgs a;
+    int rc = fill_group(c, s, cols, n, framed, false, a);
+    if (rc) return rc;
+    a.xdr = out;
+    a.xdr_cap = out_cap;
+    a.rec_out = rec_offsets;
+    {
+        TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE);
+        HIPCHK(c, (hipError_t)launch_group_phase(a, GRP_ENC_SIZES, c->stream));
+    }
+    {
+        TimedLaunch t(c, XDRG_KERNEL_VAR_SCAN);
+        HIPCHK(c, (hipError_t)launch_scan_rows(a.block_sums, a.nblocks, a.totals, 1, c->stream));
+    }
+    {
+        TimedLaunch t(c, XDRG_KERNEL_VAR_ENCODE);
+        HIPCHK(c, (hipError_t)launch_group_phase(a, GRP_ENC_PLACE, c->stream));
+    }
+    if (async) {
+        if (out_len) HIPCHK(c, hipMemcpyAsync(out_len, a.totals, 8, hipMemcpyDeviceToDevice, c->stream));
+        return XDRG_OK;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->h_stat, a.totals, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t total = c->h_stat[0];
+    if (out_len) *out_len = total;
+    if (total > out_cap) {
+        c->err = "output buffer too small";
+        return XDRG_E_CAPACITY;
+    }
+    return XDRG_OK;
+}
+
 // ---------------------------------------------------------------------------
 // encode
 // ---------------------------------------------------------------------------
@@ -574,6 +715,10 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
     if (n && !out) return inval(c, "XDR buffer is NULL");
     int rc = check_columns(c, s, cols, n, false);
     if (rc) return rc;
+    if (s->ngroups) {
+        if (byref) return inval(c, "by-reference payloads in a schema with repeated groups");
+        return group_encode(c, s, cols, n, out, out_cap, rec_offsets, framed, async, out_len);
+    }
 
     if (!s->var_size) {
         const uint64_t stride = s->fixed_size + (framed ? 4 : 0);
@@ -751,6 +896,35 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
     if (s->var_size && !rec_offsets) return inval(c, "variable-size schema needs record offsets");
     int rc = check_columns(c, s, cols, n, true);
     if (rc) return rc;
+    if (s->ngroups) {
+        if (byref) return inval(c, "payload views in a schema with repeated groups");
+        GroupArgs a;
+        rc = fill_group(c, s, cols, n, framed, true, a);
+        if (rc) return rc;
+        if (n == 0) {
+            for (uint32_t q = 0; q < a.nslot; ++q)
+                if (!a.f[a.slot_field[q]].grp) HIPCHK(c, hipMemsetAsync(cols[a.slot_field[q]].offsets, 0, 8, c->stream));
+            return finish_decode(c, n, kNoError, false, async, first_bad, err);
+        }
+        a.xdr = (uint8_t *)in;
+        a.xdr_cap = in_len;
+        a.rec_in = rec_offsets;
+        HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
+        {
+            TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE);
+            HIPCHK(c, (hipError_t)launch_group_phase(a, GRP_DEC_WALK, c->stream));
+        }
+        {
+            TimedLaunch t(c, XDRG_KERNEL_VAR_SCAN);
+            HIPCHK(c, (hipError_t)launch_scan_rows(a.block_sums, a.nblocks, a.totals, a.nslot, c->stream));
+        }
+        {
+            TimedLaunch t(c, XDRG_KERNEL_VAR_DECODE);
+            HIPCHK(c, (hipError_t)launch_group_phase(a, GRP_DEC_OFFSETS, c->stream));
+            HIPCHK(c, (hipError_t)launch_group_phase(a, GRP_DEC_PLACE, c->stream));
+        }
+        return finish_decode(c, n, kNoError, true, async, first_bad, err);
+    }
 
     if (!s->var_size && !rec_offsets) {
         const uint64_t stride = s->fixed_size + (framed ? 4 : 0);
@@ -996,6 +1170,7 @@ static int multi_args(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *s
     for (uint32_t i = 0; i < nctx; ++i)
         if (!ctxs[i]) return XDRG_E_INVAL;
     if (flags & ~XDRG_FRAME_RM) return inval(ctxs[0], "multi-GPU calls are synchronous (no XDRG_ASYNC)");
+    if (s->ngroups) return inval(ctxs[0], "multi-GPU calls take schemas without repeated groups");
     return XDRG_OK;
 }
 

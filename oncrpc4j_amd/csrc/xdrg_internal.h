@@ -267,6 +267,54 @@ struct GatherArgs {             // copy bytes[s] from src[s] (a peer's HBM) to d
 int launch_gather(const GatherArgs &a, void *stream);
 int launch_add_u64(uint64_t *p, uint64_t n, uint64_t delta, void *stream);   // p[0..n) += delta
 
+// ---- repeated groups (kernels_group.hip) --------------------------------
+// Arrays of structs and recursive lists (include/xdrg.h "Repeated groups").
+// A counted column ("slot") is one whose per-record element count the decode
+// walk reports and a scan turns into native offsets: a top-level dynamic
+// field, a DYNAMIC / LIST group (its elements) or a group's dynamic member
+// (its values over the record's elements).
+constexpr int kMaxSlots = 16;
+struct GField {
+    uint32_t type, kind, nsz, xsz;
+    uint32_t count;   // FIXED count (of a field's elements or a group's)
+    uint32_t xbytes;  // fixed field: XDR bytes (incl. pad)
+    uint32_t grp;     // member: its group's field index + 1; top level: 0
+    uint32_t nmem;    // group: member fields that follow it
+    uint32_t efix;    // group: XDR bytes of an element's fixed members (+ 4: a list's bool)
+    uint32_t ndm;     // group: dynamic members
+    uint32_t slot;    // counted column: slot + 1, else 0
+    uint32_t top;     // top-level field index that owns it (the group for a member)
+    uint8_t *data;
+    int64_t stride;
+    uint64_t *offsets;
+    uint64_t cap;
+};
+struct GroupArgs {
+    uint64_t n;
+    uint32_t nf;
+    uint32_t framed;
+    uint32_t nslot;
+    uint32_t rsv;
+    uint8_t *xdr;
+    uint64_t xdr_cap;            // encode: out_cap; decode: in_len
+    const uint64_t *rec_in;      // decode: record extents (n+1)
+    uint64_t *rec_out;           // encode: record offsets (n+1), nullable
+    uint64_t *rec_size;          // encode workspace [n]: record sizes
+    uint64_t *block_sums;        // [max(nslot, 1)][nblocks]
+    uint64_t nblocks;
+    uint64_t *totals;            // [max(nslot, 1)]
+    uint32_t *rec_cnt;           // decode workspace [nslot][n]: counts per record
+    uint64_t *rec_base;          // decode workspace [nslot][n]: native offset per record
+    unsigned long long *errkey;
+    uint32_t slot_field[kMaxSlots];
+    GField f[kMaxFields];
+};
+static_assert(sizeof(GroupArgs) <= 4096, "GroupArgs must fit the kernel-argument segment");
+enum GroupPhase { GRP_ENC_SIZES, GRP_ENC_PLACE, GRP_DEC_WALK, GRP_DEC_OFFSETS, GRP_DEC_PLACE };
+int launch_group_phase(const GroupArgs &a, int phase, void *stream);
+// exclusive scan of `rows` rows of nblocks block sums each (k_scan_rows)
+int launch_scan_rows(uint64_t *sums, uint64_t nblocks, uint64_t *totals, uint32_t rows, void *stream);
+
 constexpr int kRecThreads = 256;   // record path: threads per block
 constexpr int kRecPerThread = 4;   // records per thread in the size/scan pass
 constexpr int kRecPerBlock = kRecThreads * kRecPerThread;

@@ -55,6 +55,11 @@ class CapacityError(XdrgError):
     pass
 
 
+class NegativeArraySizeException(XdrgError):
+    """java.lang.NegativeArraySizeException: an array of structs decoded with a
+    negative count (rpcgen's `new T[xdr.xdrDecodeInt()]`, jrpcgen.java:886-906)."""
+
+
 def _raise(code, ctx=None, first_bad=None):
     L = lib()
     msg = L.xdrg_status_string(code).decode()
@@ -66,6 +71,8 @@ def _raise(code, ctx=None, first_bad=None):
         raise BadXdrOncRpcException(code, msg, first_bad)
     if code == abi.E_FIXED_LEN:
         raise ValueError(msg)
+    if code == abi.E_NEG_SIZE:
+        raise NegativeArraySizeException(code, msg, first_bad)
     if code == abi.E_CAPACITY:
         raise CapacityError(code, msg, first_bad)
     raise XdrgError(code, msg, first_bad)
@@ -83,8 +90,9 @@ class Schema:
         self.conds = [(int(f), int(d), int(n), [int(v) for v in vals])
                       for f, d, n, vals in (conds or ())]
         arr = (abi.Field * len(self.fields))()
-        for i, (t, k, c) in enumerate(self.fields):
-            arr[i].type, arr[i].kind, arr[i].count, arr[i].reserved = t, k, c, 0
+        for i, f in enumerate(self.fields):   # (type, kind, count[, members of a group])
+            arr[i].type, arr[i].kind, arr[i].count = f[0], f[1], f[2]
+            arr[i].reserved = f[3] if len(f) > 3 else 0
         h = ctypes.c_void_p()
         if self.conds:
             ca = (abi.Cond * len(self.conds))()
@@ -113,7 +121,7 @@ class Schema:
 
     @property
     def is_fixed(self):
-        return not self.conds and all(k != abi.K_DYNAMIC for _, k, _ in self.fields)
+        return not self.conds and all(f[1] != abi.K_DYNAMIC and f[0] != abi.T_GROUP for f in self.fields)
 
     def __del__(self):
         h = getattr(self, "_h", None)

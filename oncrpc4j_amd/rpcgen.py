@@ -24,8 +24,17 @@ conditions (include/xdrg.h xdrg_cond: field k present iff its discriminant
 field is present and the discriminant's value is / is not in a case list),
 which the engine batches directly (engine.Schema(fields, conds)).
 Spec.fields() keeps the plain-tape contract and raises NotBatchable for
-them.  Still not one tape: arrays of structs / unions (a repeated group)
-and recursive types (linked lists through `T *next`).
+them.
+
+Arrays of structs `T x<>` / `T x[N]` (jrpcgen.java:856-906: the count, then
+each element's xdrEncode) and recursive lists — a struct whose last
+declaration is `T *next`, used as `T *x` or `T x` (INDIRECTION,
+jrpcgen.java:835-851: TRUE + element while there is one, then FALSE; the
+reference's own portmap/pmaplist.java:50-69) — become repeated groups
+(include/xdrg.h: a (T_GROUP, kind, count, members) field and the element's
+flattened fields as members).  Still not one tape: unions / optional data
+inside group elements, arrays of structs inside elements, and recursion
+anywhere but a struct's last declaration.
 """
 import re
 
@@ -297,8 +306,49 @@ class _Tape:
         if u.default is not None:
             self.decl(u.default, where, (k, True, every), stack)
 
+    # ---- repeated groups ---------------------------------------------------------
+    def _struct_of(self, t):
+        """The Struct a (typedef'd) type name resolves to, or None."""
+        d = self.s.types.get(t) if isinstance(t, str) else None
+        while isinstance(d, Decl) and d.kind == SCALAR:
+            d = self.s.types.get(d.type) if isinstance(d.type, str) else None
+        return d if isinstance(d, Struct) else None
+
+    def _list_struct(self, st):
+        """Is struct st a list node: its last declaration `st *next`?"""
+        return bool(st.decls) and st.decls[-1].kind == OPTIONAL and self._struct_of(st.decls[-1].type) is st
+
+    def group(self, kind, count, st, decls, where, guard, stack):
+        """Group field + the element's flattened fields as its members."""
+        if guard is not None:
+            raise NotBatchable(f"{where}: a repeated group inside a union arm or optional value")
+        sub = _Tape(self.s)
+        for d in decls:
+            sub.decl(d, f"{where}.{d.name}", None, stack + (st.name,))
+        fields, conds = sub.result()
+        if conds or any(f[0] == abi.T_GROUP for f in fields):
+            raise NotBatchable(f"{where}: elements of {st.name} hold unions, optional data or arrays "
+                               f"of structs (no one-level group)")
+        if not fields:
+            raise NotBatchable(f"{where}: elements of {st.name} have no fields")
+        self.add((abi.T_GROUP, kind, count, len(fields)), None)
+        for f in fields:
+            self.add(f, None)
+
     def decl(self, decl, where, guard, stack):
         if decl.kind == VOID:
+            return
+        st = self._struct_of(decl.type) if decl.kind != SCALAR else None
+        if decl.kind == OPTIONAL and st is not None and self._list_struct(st):
+            # `T *x` of a list node T: TRUE + element while there is one, then FALSE
+            self.group(abi.K_LIST, 0, st, st.decls[:-1], where, guard, stack)
+            return
+        if decl.kind in (FIXED, DYNAMIC) and st is not None:
+            # `T x<>` / `T x[N]` of a struct: the count (dynamic), then the elements
+            if self._list_struct(st):
+                raise NotBatchable(f"{where}: an array of list heads {st.name}")
+            self.group(abi.K_FIXED if decl.kind == FIXED else abi.K_DYNAMIC,
+                       self.s.value(decl.size) if decl.kind == FIXED else 0, st, st.decls, where, guard, stack)
             return
         if decl.kind == OPTIONAL:
             # T *x: xdrEncodeBoolean(x != null), then x (JrpcgenDeclaration.INDIRECTION)

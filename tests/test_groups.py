@@ -138,3 +138,154 @@ def test_oracle_group_random_roundtrip():
         hb2 = HostBatch(hb.fields, hb.n, list(hb.arrays))
         hb2.arrays[6] = (want != 0).astype(np.uint8)
         assert out.equal(hb2)
+
+
+# ---- the HIP engine (GPU) -------------------------------------------------------------
+def _engine():
+    torch = pytest.importorskip("torch")
+    from oncrpc4j_amd import engine
+    from oncrpc4j_amd.columns import DeviceBatch
+    return torch, engine, DeviceBatch
+
+
+def gpu_encode(ctx, fields, hb, framed):
+    torch, engine, DeviceBatch = _engine()
+    sch = engine.Schema(fields)
+    assert sch.fixed_size == 0 and not sch.is_fixed
+    db = DeviceBatch.from_host(hb)
+    cap = hb.xdr_total(framed)
+    out = torch.zeros(cap + 64, dtype=torch.uint8, device="cuda")
+    offs = torch.zeros(hb.n + 1, dtype=torch.int64, device="cuda")
+    ln = ctx.encode(sch, db.columns(), hb.n, out, cap, rec_offsets=offs, framed=framed)
+    assert not out[ln:].any(), "engine wrote past the stream end"
+    return out[:ln].cpu().numpy().tobytes(), offs.cpu().numpy().view(np.uint64)
+
+
+def gpu_decode(ctx, fields, xdr, n, offs, caps, framed):
+    torch, engine, DeviceBatch = _engine()
+    sch = engine.Schema(fields)
+    db = DeviceBatch.empty(fields, n, caps)
+    buf = torch.from_numpy(np.frombuffer(xdr, dtype=np.uint8).copy()).cuda() if xdr else \
+        torch.zeros(4, dtype=torch.uint8, device="cuda")
+    ro = torch.from_numpy(np.asarray(offs, dtype=np.uint64).view(np.int64)).cuda()
+    rc, fb, err = ctx.decode(sch, buf, len(xdr), n, db.columns(), rec_offsets=ro, framed=framed,
+                             raise_on_error=False)
+    return rc, fb, err, db.to_host()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b", BATCHES, ids=_ids)
+def test_gpu_group_fixture(gpu_ctx, b):
+    fields = _fields(b)
+    hb = gold.batch_from_records(fields, b["records"])
+    xdr, offs = gpu_encode(gpu_ctx, fields, hb, b["framed"])
+    assert xdr.hex() == b["xdr"]
+    assert offs.tolist() == b["rec_offsets"]
+    rc, fb, err, out = gpu_decode(gpu_ctx, fields, xdr, hb.n, offs, hb.dyn_caps(), b["framed"])
+    assert (rc, fb, err) == (0, hb.n, 0)
+    assert out.equal(hb)
+
+
+SHAPES = {
+    "pmaplist": PMAP,
+    "items": ITEMS,
+    "dirlist": [(G, LS, 0, 3), (H, SC, 0), (STR, DY, 0), (H, SC, 0), (B, SC, 0)],
+    "fixed_pairs": [(I, SC, 0), (G, FX, 3, 2), (abi.T_SHORT, SC, 0), (I, DY, 0), (H, SC, 0)],
+    "two_groups": [(G, DY, 0, 2), (U, SC, 0), (STR, DY, 0), (G, LS, 0, 3), (B, SC, 0),
+                   (abi.T_DOUBLE, SC, 0), (O, FX, 5), (O, DY, 0)],
+    "fixed_members_only": [(O, DY, 0), (G, DY, 0, 3), (I, SC, 0), (abi.T_BYTE, FX, 3), (H, SC, 0)],
+}
+
+
+def _sane(hb):
+    """Values the codec maps one to one: bools 0/1, no NaN payloads."""
+    for k, f in enumerate(hb.fields):
+        if f[0] == B:
+            hb.arrays[k] = (hb.arrays[k] != 0).astype(np.uint8)
+        if f[0] in (F, abi.T_DOUBLE) and f[1] != DY:
+            a = hb.arrays[k]
+            a[np.isnan(a)] = 0
+    return hb
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+@pytest.mark.parametrize("shape", list(SHAPES), ids=list(SHAPES))
+def test_gpu_group_vs_oracle(gpu_ctx, shape, framed):
+    fields = SHAPES[shape]
+    for n, glen in ((1, (0, 3)), (3000, (0, 9)), (20000, (0, 3)), (900, (60, 140))):
+        hb = _sane(random_batch(fields, n, seed=n + len(shape), dyn_len=(0, 21), group_len=glen))
+        rc, want, woffs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total(framed), framed=framed)
+        assert rc == 0
+        xdr, offs = gpu_encode(gpu_ctx, fields, hb, framed)
+        assert xdr == want, f"n={n}: encode differs from the oracle"
+        assert offs.tolist() == woffs.tolist()
+        rc, fb, err, out = gpu_decode(gpu_ctx, fields, xdr, n, offs, hb.dyn_caps(), framed)
+        assert (rc, fb, err) == (0, n, 0)
+        assert out.equal(hb)
+
+
+def _corrupt_cases():
+    """(name, fields, record index, how to break its bytes)"""
+    return [
+        ("neg_count", ITEMS, lambda b: b[:4] + bytes.fromhex("fffffffe") + b[8:]),
+        ("short_tail", ITEMS, lambda b: b[:-4]),
+        ("corrupt_string", [(G, DY, 0, 1), (STR, DY, 0)],
+         lambda b: b[:4] + bytes.fromhex("80000000") + b[8:] if len(b) > 8 else b[:-4]),
+        ("list_cut", PMAP, lambda b: b[:-4]),
+        ("list_bool_nonzero", PMAP, lambda b: bytes.fromhex("00000009") + b[4:]),
+    ]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", _corrupt_cases(), ids=lambda c: c[0])
+def test_gpu_group_errors_first_bad(gpu_ctx, case):
+    """Every record is its own message; one broken record in the middle: the
+    engine reports the oracle's (first_bad, code) and decodes every record
+    before it."""
+    name, fields, brk = case
+    hb = _sane(random_batch(fields, 4000, seed=7, dyn_len=(1, 9), group_len=(1, 5)))
+    rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), hb.n, hb.xdr_total(False))
+    assert rc == 0
+    recs = [xdr[int(offs[i]):int(offs[i + 1])] for i in range(hb.n)]
+    bad = 2345
+    recs[bad] = brk(recs[bad])
+    stream = b"".join(recs)
+    o = np.zeros(hb.n + 1, np.uint64)
+    np.cumsum([len(r) for r in recs], out=o[1:])
+    want = HostBatch.empty(fields, hb.n, hb.dyn_caps())
+    wrc, wfb, werr = oracle.decode_batch(fields, stream, o, hb.n, want.columns())
+    rc, fb, err, out = gpu_decode(gpu_ctx, fields, stream, hb.n, o, hb.dyn_caps(), False)
+    assert (rc, fb, err) == (wrc, wfb, werr)
+    if wrc:
+        assert wfb == bad
+        assert out.equal(want, upto=bad)
+
+
+@pytest.mark.gpu
+def test_gpu_group_capacity(gpu_ctx):
+    fields = ITEMS
+    hb = random_batch(fields, 500, seed=3, dyn_len=(0, 9), group_len=(0, 5))
+    rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), hb.n, hb.xdr_total(False))
+    caps = hb.dyn_caps()
+    for k in (1, 3):   # too few element slots / too few string bytes
+        small = dict(caps)
+        small[k] = caps[k] // 2
+        want = HostBatch.empty(fields, hb.n, small)
+        wrc, wfb, werr = oracle.decode_batch(fields, xdr, offs, hb.n, want.columns())
+        rc, fb, err, out = gpu_decode(gpu_ctx, fields, xdr, hb.n, offs, small, False)
+        assert (rc, fb, err) == (wrc, wfb, werr) and wrc == abi.E_CAPACITY
+        assert out.equal(want, upto=wfb)
+
+
+@pytest.mark.gpu
+def test_gpu_group_encode_capacity(gpu_ctx):
+    torch, engine, DeviceBatch = _engine()
+    hb = random_batch(PMAP, 100, seed=5)
+    sch = engine.Schema(PMAP)
+    db = DeviceBatch.from_host(hb)
+    need = hb.xdr_total(False)
+    out = torch.zeros(need, dtype=torch.uint8, device="cuda")
+    with pytest.raises(engine.CapacityError):
+        gpu_ctx.encode(sch, db.columns(), hb.n, out, need - 4)
+    assert not out.any()

@@ -26,6 +26,7 @@ HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rpcge
 I, U, E, B, H, UH = abi.T_INT, abi.T_UINT, abi.T_ENUM, abi.T_BOOL, abi.T_HYPER, abi.T_UHYPER
 F, D, S, BY, O, STR = abi.T_FLOAT, abi.T_DOUBLE, abi.T_SHORT, abi.T_BYTE, abi.T_OPAQUE, abi.T_STRING
 SC, FX, DY = abi.K_SCALAR, abi.K_FIXED, abi.K_DYNAMIC
+G, LS = abi.T_GROUP, abi.K_LIST
 
 
 def spec(name):
@@ -76,10 +77,10 @@ def test_batch_types_tapes():
     assert s.result_fields(400123, 1, 4) == FATTR
     assert s.args_fields(400123, 1, 5) == [(O, FX, 32), (U, SC, 0)]
     assert s.result_fields(400123, 1, 5) == [(STR, DY, 0)]
-    with pytest.raises(rpcgen.NotBatchable, match="optional"):
-        s.fields("optional_next")
-    with pytest.raises(rpcgen.NotBatchable, match="array"):
-        s.fields("with_array_of_structs")
+    # a list node (last declaration `optional_next *next`) and an array of
+    # structs are repeated groups (include/xdrg.h)
+    assert s.fields("optional_next") == [(I, SC, 0), (G, LS, 0, 1), (I, SC, 0)]
+    assert s.fields("with_array_of_structs") == [(G, DY, 0, 2), (U, SC, 0), (U, SC, 0)]
 
 
 def test_syntax_errors():
@@ -293,8 +294,8 @@ def test_conditional_tape_shapes():
                  (5, 4, True, [0]), (6, 4, True, [0]), (7, 0, True, [1, 5, 2])]
     f, c = s.args_tape(400123, 1, 7)           # LIST(fhandle, kind_res): arguments back to back
     assert f[0] == (O, FX, 32) and c[0] == (2, 1, False, [1, 5])
-    with pytest.raises(rpcgen.NotBatchable, match="contains itself"):
-        s.tape("optional_next")
+    f, c = s.tape("optional_next")           # a list node: a repeated group, no conditions
+    assert f == [(I, SC, 0), (G, LS, 0, 1), (I, SC, 0)] and c == []
 
 
 def test_kv_store_tape():
@@ -339,3 +340,121 @@ def test_gpu_kv_store_args(gpu_ctx):
     assert oracle.decode_batch(fields, want, np.array(offs, np.uint64), n, ref.columns(),
                                conds=conds) == (0, n, 0)
     assert back.to_host().equal(ref)
+
+
+# ---- repeated groups: arrays of structs and recursive lists ---------------------------
+MAPPING = [(U, SC, 0)] * 4
+DIRENT = [(UH, SC, 0), (STR, DY, 0), (UH, SC, 0)]
+LIST_TAPES = {
+    "dump_res": [(G, LS, 0, 4)] + MAPPING,
+    "dir_list": [(G, LS, 0, 3)] + DIRENT + [(B, SC, 0)],
+    "readdir_ok": [(O, FX, 8), (G, LS, 0, 3)] + DIRENT + [(B, SC, 0)],
+    "tagged": [(I, SC, 0), (G, DY, 0, 2), (U, SC, 0), (U, SC, 0), (G, FX, 2, 2), (U, SC, 0), (U, SC, 0),
+               (STR, DY, 0)],
+    # `map_node first` (not a pointer): its fields, then its `next` chain
+    "chain_head": [(I, SC, 0)] + MAPPING + [(G, LS, 0, 4)] + MAPPING,
+}
+
+
+def test_group_tapes():
+    s = spec("list_types.x")
+    for t, want in LIST_TAPES.items():
+        assert s.fields(t) == want, t
+    assert s.result_fields(400124, 1, 4) == LIST_TAPES["dump_res"]        # DUMP
+    assert s.args_fields(400124, 1, 16) == LIST_TAPES["dir_list"]         # READDIR(dir_list)
+    bad = rpcgen.parse("struct u { int a; }; union v switch (int d) { case 1: int x; default: void; };"
+                       "struct w { v items<>; }; struct n { int a; n *next; int b; };")
+    with pytest.raises(rpcgen.NotBatchable):
+        bad.fields("w")                      # union elements: no one-level group
+    with pytest.raises(rpcgen.NotBatchable, match="contains itself"):
+        bad.fields("n")                      # recursion that is not the last declaration
+
+
+def _pack_tape(p, fields, hb, i):
+    """xdrlib, driven by the tape: a group packs its count (dynamic) / TRUE
+    before each element and FALSE after (list) and each element's members."""
+    def one(k, row):
+        t, kind = fields[k][0], fields[k][1]
+        a = hb.arrays[k]
+        if kind == DY:
+            vals, offs = a
+            v = vals[int(offs[row]):int(offs[row + 1])]
+            if t in (O, STR):
+                p.pack_opaque(bytes(np.asarray(v, np.uint8)))
+            else:
+                p.pack_array([int(x) for x in v], p.pack_int if t != U else p.pack_uint)
+            return
+        if t == O:
+            p.pack_fopaque(fields[k][2], bytes(np.asarray(a[row], np.uint8)))
+            return
+        pk = {I: p.pack_int, U: p.pack_uint, B: p.pack_bool, H: p.pack_hyper, UH: p.pack_uhyper}[t]
+        pk(int(a[row]))
+    k = 0
+    while k < len(fields):
+        f = fields[k]
+        if f[0] != G:
+            one(k, i)
+            k += 1
+            continue
+        e0, e1 = (i * f[2], (i + 1) * f[2]) if f[1] == FX else (int(hb.arrays[k][i]), int(hb.arrays[k][i + 1]))
+        if f[1] == DY:
+            p.pack_uint(e1 - e0)
+        for e in range(e0, e1):
+            if f[1] == LS:
+                p.pack_bool(True)
+            for j in range(1, f[3] + 1):
+                one(k + j, e)
+        if f[1] == LS:
+            p.pack_bool(False)
+        k += 1 + f[3]
+
+
+def _group_batch(fields, n, seed):
+    hb = random_batch(fields, n, seed=seed, dyn_len=(0, 11), group_len=(0, 7), special_floats=False)
+    for k, f in enumerate(fields):
+        if f[0] == B:
+            hb.arrays[k] = (hb.arrays[k] != 0).astype(np.uint8)
+    return hb
+
+
+@pytest.mark.parametrize("type_name", list(LIST_TAPES))
+def test_group_tape_matches_xdrlib(type_name):
+    fields = LIST_TAPES[type_name]
+    n = 300
+    hb = _group_batch(fields, n, seed=len(type_name))
+    rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total())
+    assert rc == 0
+    for i in range(n):
+        p = xdrlib.Packer()
+        _pack_tape(p, fields, hb, i)
+        assert xdr[offs[i]:offs[i + 1]] == p.get_buffer(), f"record {i}"
+
+
+@pytest.mark.gpu
+def test_gpu_portmap_dump_and_readdir(gpu_ctx):
+    """DUMP reply bodies (mapping lists) encoded on the GPU with the generated
+    tape equal xdrlib's; READDIR(dir_list) arguments decode like the oracle."""
+    import torch
+    from oncrpc4j_amd import engine
+    from oncrpc4j_amd.columns import DeviceBatch, HostBatch
+    s = spec("list_types.x")
+    for fields, n in ((s.result_fields(400124, 1, 4), 20000), (s.args_fields(400124, 1, 16), 8000)):
+        hb = _group_batch(fields, n, seed=n)
+        want, offs = b"", [0]
+        for i in range(n):
+            p = xdrlib.Packer()
+            _pack_tape(p, fields, hb, i)
+            want += p.get_buffer()
+            offs.append(len(want))
+        sch = engine.Schema(fields)
+        db = DeviceBatch.from_host(hb)
+        out = torch.zeros(len(want), dtype=torch.uint8, device="cuda")
+        ro = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+        ln = gpu_ctx.encode(sch, db.columns(), n, out, len(want), rec_offsets=ro)
+        assert out[:ln].cpu().numpy().tobytes() == want
+        assert ro.cpu().tolist() == offs
+        back = DeviceBatch.empty(fields, n, hb.dyn_caps())
+        assert gpu_ctx.decode(sch, out, ln, n, back.columns(), rec_offsets=ro) == (0, n, 0)
+        ref = HostBatch.empty(fields, n, hb.dyn_caps())
+        assert oracle.decode_batch(fields, want, np.array(offs, np.uint64), n, ref.columns()) == (0, n, 0)
+        assert back.to_host().equal(ref) and ref.equal(hb)
