@@ -16,8 +16,8 @@
 // Decode: k_grp_dec_walk (a lane per record walks every count, list bool
 // and member length in the reference's order and reports the first failing
 // check) -> k_scan_rows over the counted columns -> k_grp_dec_offsets
-// (native offsets, capacity) -> k_grp_dec_place (a wave per record walks
-// again in lockstep, lanes move payload words).
+// (native offsets, capacity) -> k_grp_dec_place (a lane per record walks
+// it again and stores every value).
 #include <hip/hip_runtime.h>
 
 #include "xdrg_device.h"
@@ -410,9 +410,10 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_offsets(const GroupArgs
     }
 }
 
-// One wavefront decodes record r (walked clean, capacity checked).
+// One lane decodes record r (walked clean, capacity checked), field by
+// field in stream order: a wave keeps 64 records' loads in flight instead of
+// one record's chain of dependent length words.
 __device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
-    const uint32_t lane = threadIdx.x & 63;
     const uint8_t *in = a.xdr;
     uint64_t pos = a.rec_in[r] + (a.framed ? 4 : 0);
     for (uint32_t k = 0; k < a.nf;) {
@@ -421,59 +422,39 @@ __device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
             const uint64_t e0 = f.kind == XDRG_K_FIXED ? r * f.count : a.rec_base[(uint64_t)(f.slot - 1) * a.n + r];
             const uint64_t cnt = f.kind == XDRG_K_FIXED ? f.count : a.rec_cnt[(uint64_t)(f.slot - 1) * a.n + r];
             if (f.kind == XDRG_K_DYNAMIC) pos += 4;
-            const uint32_t lb = f.kind == XDRG_K_LIST ? 4 : 0;   // each list element's bool
-            if (!f.ndm) {   // elements of one size: a lane per element
-                for (uint64_t i = lane; i < cnt; i += 64) {
-                    uint64_t p = pos + i * f.efix + lb;
-                    for (uint32_t j = 1; j <= f.nmem; ++j) {
-                        const GField &m = a.f[k + j];
-                        for (uint32_t w = 0; w < m.xbytes >> 2; ++w) g_fixed_store(m, e0 + i, w, *(const uint32_t *)(in + p + 4 * w));
-                        p += m.xbytes;
-                    }
-                }
-                pos += cnt * f.efix;
-            } else {        // element by element; lanes move each member's words
-                uint64_t mb[kMaxFields];
+            for (uint32_t j = 1; j <= f.nmem; ++j) {   // each dynamic member's first value
+                const GField &m = a.f[k + j];
+                if (m.kind == XDRG_K_DYNAMIC) m.offsets[e0] = a.rec_base[(uint64_t)(m.slot - 1) * a.n + r];
+            }
+            for (uint64_t e = e0; e < e0 + cnt; ++e) {
+                if (f.kind == XDRG_K_LIST) pos += 4;   // its TRUE
                 for (uint32_t j = 1; j <= f.nmem; ++j) {
                     const GField &m = a.f[k + j];
-                    mb[j - 1] = m.kind == XDRG_K_DYNAMIC ? a.rec_base[(uint64_t)(m.slot - 1) * a.n + r] : 0;
-                }
-                for (uint64_t i = 0; i < cnt; ++i) {
-                    pos += lb;
-                    const uint64_t e = e0 + i;
-                    for (uint32_t j = 1; j <= f.nmem; ++j) {
-                        const GField &m = a.f[k + j];
-                        if (m.kind != XDRG_K_DYNAMIC) {
-                            for (uint32_t w = lane; w < m.xbytes >> 2; w += 64) g_fixed_store(m, e, w, *(const uint32_t *)(in + pos + 4 * w));
-                            pos += m.xbytes;
-                            continue;
-                        }
-                        const uint64_t len = g_ld(in + pos);
-                        if (lane == 0) m.offsets[e] = mb[j - 1];
-                        const uint64_t nw = g_dyn_words(m, len);
-                        for (uint64_t w = lane; w < nw; w += 64) g_dyn_store(m, mb[j - 1], len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
-                        mb[j - 1] += len;
-                        pos += 4 + 4 * nw;
+                    if (m.kind != XDRG_K_DYNAMIC) {
+                        for (uint32_t w = 0; w < m.xbytes >> 2; ++w) g_fixed_store(m, e, w, *(const uint32_t *)(in + pos + 4 * w));
+                        pos += m.xbytes;
+                        continue;
                     }
+                    const uint64_t len = g_ld(in + pos);
+                    const uint64_t v0 = m.offsets[e];   // written for the element before (or above)
+                    m.offsets[e + 1] = v0 + len;
+                    const uint64_t nw = g_dyn_words(m, len);
+                    for (uint64_t w = 0; w < nw; ++w) g_dyn_store(m, v0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
+                    pos += 4 + 4 * nw;
                 }
-                // the entry after the record's last element (the next record
-                // writes the same value; a failed next record does not run)
-                if (lane == 0)
-                    for (uint32_t j = 1; j <= f.nmem; ++j)
-                        if (a.f[k + j].kind == XDRG_K_DYNAMIC) a.f[k + j].offsets[e0 + cnt] = mb[j - 1];
             }
-            if (f.kind == XDRG_K_LIST) pos += 4;
+            if (f.kind == XDRG_K_LIST) pos += 4;   // its FALSE
             k += 1 + f.nmem;
             continue;
         }
         if (f.kind != XDRG_K_DYNAMIC) {
-            for (uint32_t w = lane; w < f.xbytes >> 2; w += 64) g_fixed_store(f, r, w, *(const uint32_t *)(in + pos + 4 * w));
+            for (uint32_t w = 0; w < f.xbytes >> 2; ++w) g_fixed_store(f, r, w, *(const uint32_t *)(in + pos + 4 * w));
             pos += f.xbytes;
         } else {
             const uint64_t len = g_ld(in + pos);
             const uint64_t e0 = a.rec_base[(uint64_t)(f.slot - 1) * a.n + r];
             const uint64_t nw = g_dyn_words(f, len);
-            for (uint64_t w = lane; w < nw; w += 64) g_dyn_store(f, e0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
+            for (uint64_t w = 0; w < nw; ++w) g_dyn_store(f, e0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
             pos += 4 + 4 * nw;
         }
         ++k;
@@ -483,10 +464,8 @@ __device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place(const GroupArgs a) {
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
     const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
-    uint64_t nrec = bad > rb ? bad - rb : 0;
-    if (nrec > kRecPerBlock) nrec = kRecPerBlock;
-    for (uint32_t j = threadIdx.x >> 6; j < nrec; j += kRecThreads / 64) g_dec_record(a, rb + j);
+    const uint64_t r = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x;
+    if (r < bad) g_dec_record(a, r);
 }
 
 int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
@@ -497,7 +476,9 @@ int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
     case GRP_ENC_PLACE: hipLaunchKernelGGL(k_grp_enc_place, grid, block, 0, st, a); break;
     case GRP_DEC_WALK: hipLaunchKernelGGL(k_grp_dec_walk, grid, block, 0, st, a); break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
-    case GRP_DEC_PLACE: hipLaunchKernelGGL(k_grp_dec_place, grid, block, 0, st, a); break;
+    case GRP_DEC_PLACE:   // a lane per record
+        hipLaunchKernelGGL(k_grp_dec_place, dim3((uint32_t)((a.n + kRecThreads - 1) / kRecThreads)), block, 0, st, a);
+        break;
     default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
