@@ -1106,6 +1106,10 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_place_g(const RecArgs a) {
     if (nrec > kRecPerBlock) nrec = kRecPerBlock;
     uint8_t *out = a.xdr;
     const uint32_t tid = threadIdx.x;
+    if (a.payk) {   // k_enc_payload writes these records whole: hand over the payload positions
+        for (uint32_t j = tid; j < nrec; j += kRecThreads) a.pay_pos[rb + j] = soff[j] + a.pay_fb;
+        return;
+    }
     if (a.framed) {   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
         for (uint32_t j = tid; j < nrec; j += kRecThreads)
             *(uint32_t *)(out + soff[j]) = bswap32r((uint32_t)(soff[j + 1] - soff[j] - 4) | kLastFrag);
@@ -1351,60 +1355,60 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
 __device__ __forceinline__ bool payload_block(const RecArgs &a, uint64_t r, bool decode) {
     return !a.big_rec || block_is_big_at(a, r / kRecPerBlock, decode);
 }
+// XDR word at byte o (4-aligned) of record r in a schema whose one dynamic
+// field is the byte field f (cnt bytes at src): the mark, the fixed fields
+// before f, f's length word, its payload and zero pad (Xdr.java:776-800),
+// the fixed fields after f.
+__device__ uint32_t payload_rec_word(const RecArgs &a, uint64_t r, uint64_t o, uint64_t size, const uint8_t *src,
+                                     uint64_t cnt) {
+    const uint64_t fb = a.pay_fb, P = cnt + pad4(cnt);
+    if (a.framed && o == 0) return bswap32r((uint32_t)(size - 4) | kLastFrag);   // GrizzlyRpcTransport:103-110
+    if (o >= fb && o < fb + 4) return bswap32r((uint32_t)cnt);
+    if (o >= fb + 4 && o < fb + 4 + P) {
+        const uint64_t b = o - fb - 4;
+        return b >= cnt ? 0u : (cnt - b >= 4 ? *(const u32u *)(src + b) : load_bytes(src + b, (uint32_t)(cnt - b)));
+    }
+    uint64_t q = a.framed ? 4 : 0;   // a fixed field's word
+    if (o >= fb) o -= 4 + P;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind == XDRG_K_DYNAMIC) continue;
+        if (o < q + f.xbytes) return fixed_word(f, r, o - q);
+        q += f.xbytes;
+    }
+    return 0;
+}
+
+// A wave writes record r whole — mark, fixed fields, length word, payload,
+// zero pad, trailing fixed fields.  Chunk c covers stream bytes
+// [A + 16c, A + 16c + 16), A = the record start rounded down to 16; chunks
+// inside the payload are one aligned 16-byte store from a 4-aligned load,
+// the record's other words go out a dword per lane after them (the edge
+// lines are shared with the neighbouring records, whose waves run alongside
+// and complete them in L2).  One pass over each line: the group kernel only
+// hands over the payload positions (pay_pos).
 template <uint32_t LPR, bool NT, bool NTS = NT>
 __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
-    // (the checks first: hoisting the metadata loads above them measured ~1 ms
-    // slower here, while it gains ~0.9 ms in dec_payload_rec)
     if (r >= a.n || a.totals[0] > a.xdr_cap || !payload_block(a, r, false)) return;
     const VField &f = a.f[a.dyn_idx[a.payk - 1]];
     const uint64_t e0 = f.offsets[r], cnt = f.offsets[r + 1] - e0;
-    uint8_t *dst = a.xdr + a.pay_pos[r];
+    const uint64_t R = a.pay_pos[r] - a.pay_fb;   // record start
+    const uint64_t P = cnt + pad4(cnt), size = a.fixed_xdr + 4 + P;
     const uint8_t *src = f.data + e0;
     const uint32_t lane = threadIdx.x % LPR;
-    if (lane == 0) *(uint32_t *)dst = bswap32r((uint32_t)cnt);
-    dst += 4;
-    // Output-aligned chunks: chunk c covers stream bytes [A + 16c, A + 16c + 16)
-    // with A = dst rounded down to 16, so every full chunk is one aligned
-    // 16-byte store (the stream offset of a payload is 4-aligned only: in a
-    // 4124-byte configs[2] record it sits 12 bytes off) and its source is a
-    // 4-aligned load.  The head chunk (shared with the length word) and the
-    // tail chunk (shared with the next record) go out as dwords, zero pad
-    // included (Xdr.java:776-781), by two lanes in the same pass as the full
-    // chunks' loads and stores.
-    const uint32_t sh = (uint32_t)((uintptr_t)dst & 15);
-    uint8_t *const A = dst - sh;
-    const uint64_t P = cnt + pad4(cnt);
-    const uint64_t cf = sh ? 1 : 0;                    // full chunks: [cf, cl)
-    const uint64_t cl = (sh + cnt) >> 4;
-    const uint64_t nch = (sh + P + 15) >> 4;
-    int64_t pc = -1;                                   // this lane's partial chunk
-    if (lane == LPR - 1 && sh) pc = 0;
-    if (lane == LPR - 2 && nch > cl && !(sh && cl == 0)) pc = (int64_t)cl;
-    uint32_t pw[4] = {0, 0, 0, 0};
-    if (pc >= 0) {
-        for (uint32_t i = 0; i < 4; ++i) {
-            const int64_t b = 16 * pc + 4 * i - (int64_t)sh;
-            if (b < 0 || (uint64_t)b >= P) continue;
-            const uint64_t k = cnt > (uint64_t)b ? cnt - (uint64_t)b : 0;
-            pw[i] = k >= 4 ? *(const u32u *)(src + b) : load_bytes(src + b, (uint32_t)k);
-        }
-    }
-    for (uint64_t c0 = cf + lane; c0 < cl || pc >= 0; c0 += 4 * LPR) {
+    uint8_t *const A = a.xdr + (R & ~(uint64_t)15);
+    const uint64_t sh = R & 15;                    // record start inside chunk 0
+    const uint64_t p0 = sh + a.pay_fb + 4;         // payload start, chunk coordinates
+    const uint64_t cf = (p0 + 15) >> 4, cl = (p0 + cnt) >> 4;   // payload-only chunks: [cf, cl)
+    for (uint64_t c0 = cf + lane; c0 < cl; c0 += 4 * LPR) {   // payload-only chunks
         u32x4a v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {   // full chunks: all loads in flight first
+        for (int u = 0; u < 4; ++u) {   // all loads in flight first
             const uint64_t c = c0 + LPR * u;
             if (c < cl) {
-                const u32x4a *p = (const u32x4a *)(src + 16 * c - sh);   // 4-aligned
+                const u32x4a *p = (const u32x4a *)(src + 16 * c - p0);   // 4-aligned
                 v[u] = NT ? __builtin_nontemporal_load(p) : *p;
             }
-        }
-        if (pc >= 0) {
-            for (uint32_t i = 0; i < 4; ++i) {
-                const int64_t b = 16 * pc + 4 * i - (int64_t)sh;
-                if (b >= 0 && (uint64_t)b < P) *(uint32_t *)(dst + b) = pw[i];
-            }
-            pc = -1;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1413,6 +1417,16 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
             if (NTS) __builtin_nontemporal_store(v[u], (u32x4n *)(A + 16 * c));
             else *(u32x4n *)(A + 16 * c) = v[u];
         }
+    }
+    // the record's words outside those chunks (mark, fixed fields, length,
+    // the payload's first and last bytes, pad, trailing fixed fields): a word
+    // per lane, their loads in parallel
+    const uint64_t hw = cl > cf ? (16 * cf - sh) >> 2 : (size >> 2);   // head words
+    const uint64_t tw0 = cl > cf ? (16 * cl - sh) >> 2 : (size >> 2);  // first tail word
+    const uint64_t nslow = hw + (size >> 2) - tw0;
+    for (uint64_t i = lane; i < nslow; i += LPR) {
+        const uint64_t wi = i < hw ? i : tw0 + (i - hw);
+        *(uint32_t *)(a.xdr + R + 4 * wi) = payload_rec_word(a, r, 4 * wi, size, src, cnt);
     }
 }
 template <uint32_t LPR, bool NT, bool NTS = NT>   // lanes per record; grid-strided; NT: nontemporal loads, NTS: stores

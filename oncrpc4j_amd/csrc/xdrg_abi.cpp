@@ -573,7 +573,9 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
         v.cnum = s->cnum[k];
         v.slot = s->slot[k];
         if (f.kind == XDRG_K_DYNAMIC) a.dyn_idx[a.ndyn++] = (uint32_t)k;
+        else if (!a.ndyn) a.pay_fb += s->xbytes[k];
     }
+    a.pay_fb += framed ? 4 : 0;   // bytes before the first dynamic field (the payload kernels' field)
     a.ncond = s->ncond;
     for (size_t i = 0; i < s->cvals.size(); ++i) a.cvals[i] = s->cvals[i];
     a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;

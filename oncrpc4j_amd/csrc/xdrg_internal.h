@@ -138,7 +138,7 @@ struct RecArgs {
     uint64_t *ref_pos;         // byref: encode splice[n] / decode payload_pos[n]
     uint32_t payk;             // 0, or 1 + the dynamic byte field the payload kernels move for the
                                // group kernels' blocks (k_enc/dec_payload)
-    uint32_t rsv3;
+    uint32_t pay_fb;           // payk: XDR bytes before that field in a record (mark + fixed fields)
     uint64_t *pay_pos;         // payk: per record, stream offset of that field's length word
                                // (decode: ~0 = not to be written)
     uint64_t *lb_state;        // staged decode with look-back: [ndyn + 1][nblocks] status words
