@@ -1389,10 +1389,14 @@ __device__ uint32_t payload_rec_word(const RecArgs &a, uint64_t r, uint64_t o, u
 // hands over the payload positions (pay_pos).
 template <uint32_t LPR, bool NT, bool NTS = NT>
 __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
-    if (r >= a.n || a.totals[0] > a.xdr_cap || !payload_block(a, r, false)) return;
+    if (r >= a.n) return;
     const VField &f = a.f[a.dyn_idx[a.payk - 1]];
-    const uint64_t e0 = f.offsets[r], cnt = f.offsets[r + 1] - e0;
-    const uint64_t R = a.pay_pos[r] - a.pay_fb;   // record start
+    // every metadata load issued together, before the checks that use them
+    const uint64_t total = a.totals[0], e0 = f.offsets[r], e1 = f.offsets[r + 1], pp = a.pay_pos[r];
+    const bool mine = payload_block(a, r, false);
+    if (total > a.xdr_cap || !mine) return;
+    const uint64_t cnt = e1 - e0;
+    const uint64_t R = pp - a.pay_fb;   // record start
     const uint64_t P = cnt + pad4(cnt), size = a.fixed_xdr + 4 + P;
     const uint8_t *src = f.data + e0;
     const uint32_t lane = threadIdx.x % LPR;
