@@ -2084,13 +2084,12 @@ __host__ __device__ constexpr size_t dec_stage_meta(uint32_t nd) {
             15) & ~(size_t)15;
 }
 
-// The whole block decodes fields [0, upto) of record r (the block's record
-// j) whose first field starts at stream offset pos (records too large for the
-// tile).  Counts come from the block's relative native offsets snrel, native
+// Threads tid < nthr of the block decode fields [0, upto) of record r (the
+// block's record j) whose first field starts at stream offset pos (records
+// too large for the tile).  Counts come from the block's relative native offsets snrel, native
 // offsets from the columns' offsets arrays this block just wrote.
-__device__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uint32_t upto,
-                                 const uint32_t *snrel, uint32_t j) {
-    const uint32_t tid = threadIdx.x;
+__device__ __forceinline__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uint32_t upto,
+                                 const uint32_t *snrel, uint32_t j, uint32_t tid, uint32_t nthr) {
     const uint8_t *in = a.xdr;
     const Span sp = make_span(in, in + a.xdr_cap, (const uint8_t *)a.block_sums);
     uint32_t d = 0;
@@ -2098,7 +2097,7 @@ __device__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uin
         const VField &f = a.f[k];
         if (f.kind != XDRG_K_DYNAMIC) {
             const uint32_t nw = f.xbytes >> 2;
-            for (uint32_t i = tid; i < nw; i += kRecThreads) fixed_store(f, r, 4 * i, *(const uint32_t *)(in + pos + 4 * i));
+            for (uint32_t i = tid; i < nw; i += nthr) fixed_store(f, r, 4 * i, *(const uint32_t *)(in + pos + 4 * i));
             pos += f.xbytes;
             continue;
         }
@@ -2111,9 +2110,163 @@ __device__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uin
         const uint32_t sh = (uint32_t)((uintptr_t)dst[0] & 3);
         const uint64_t nd = bytes ? (sh + cnt1 + 3) >> 2 : cnt1;
         const uint64_t nch[1] = {cnt1 ? (nd + 3) >> 2 : 0};
-        if (bytes) dec_bytes<2, 1>(dst, src, cnt, nch, sp, kRecThreads, tid);
-        else dec_words4<2, 1>(dst, src, cnt, nch, sp, kRecThreads, tid);
+        if (bytes) dec_bytes<2, 1>(dst, src, cnt, nch, sp, nthr, tid);
+        else dec_words4<2, 1>(dst, src, cnt, nch, sp, nthr, tid);
         pos += dyn_xdr_bytes(f, cnt1);
+        ++d;
+    }
+}
+
+// Unaligned dword of the tile at byte offset o.
+__device__ __forceinline__ uint32_t tile_word(const uint8_t *tile, int64_t o) {
+    const uint32_t *w = (const uint32_t *)(tile + (o & ~(int64_t)3));
+    const uint32_t s = (uint32_t)(o & 3);
+    return s ? __builtin_amdgcn_alignbyte(w[1], w[0], s) : w[0];
+}
+// XDR bytes of record j's dynamic fields before d (xs: their element sizes).
+__device__ __forceinline__ uint32_t dyn_before_xs(const uint32_t (&xs)[kMaxDynLds], const uint32_t *rel,
+                                                  uint32_t j, uint32_t d) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int e = 0; e < kMaxDynLds - 1; ++e) {
+        if ((uint32_t)e >= d) continue;
+        const uint32_t *r = rel + e * (kRecPerBlock + 1);
+        const uint32_t c = r[j + 1] - r[j];
+        s += 4 + (xs[e] == 1 ? (c + 3) & ~3u : c * xs[e]);
+    }
+    return s;
+}
+// Byte field of one staged record, lean form (tuning key 20): cnt bytes
+// at tile offset L (4-aligned) to dst (any alignment), chunk c of the
+// 4-aligned da = dst - sh by lane c % G.  The dword a record boundary falls
+// in is written once, whole, by the later record's first lane when both
+// records fill their side of it (own_head: hv is the composed dword; the
+// earlier record then skips it, skip_tail); otherwise each side byte-stores
+// its own bytes.  Every other store is a whole dword or 16 bytes.
+__device__ __forceinline__ void dec_bytes_lean(uint8_t *dst, const uint8_t *tile, uint32_t L, uint32_t cnt,
+                                               bool own_head, uint32_t hv, bool skip_tail, uint32_t gl, uint32_t G) {
+    const uint32_t sh = (uint32_t)((uintptr_t)dst & 3), end = sh + cnt, nch = (end + 15) >> 4;
+    uint8_t *da = dst - sh;
+    const uint32_t rs = (4 - sh) & 3;   // source misalignment of dest dwords
+    for (uint32_t c = gl; c < nch; c += G) {
+        const uint32_t b0 = 16 * c;
+        const uint32_t *w = (const uint32_t *)(tile + (L + b0 - sh - rs));   // 4-aligned
+        const uint32_t q0 = w[0], q1 = w[1], q2 = w[2], q3 = w[3], q4 = w[4];
+        uint32_t v[4];
+        v[0] = rs ? __builtin_amdgcn_alignbyte(q1, q0, rs) : q0;
+        v[1] = rs ? __builtin_amdgcn_alignbyte(q2, q1, rs) : q1;
+        v[2] = rs ? __builtin_amdgcn_alignbyte(q3, q2, rs) : q2;
+        v[3] = rs ? __builtin_amdgcn_alignbyte(q4, q3, rs) : q3;
+        const bool head = c == 0 && sh != 0;
+        if (head && own_head) v[0] = hv;
+        uint8_t *d = da + b0;
+        if ((!head || own_head) && b0 + 16 <= end) {
+            u32x4a o; o.x = v[0]; o.y = v[1]; o.z = v[2]; o.w = v[3];
+            *(u32x4a *)d = o;
+            continue;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t lo = b0 + 4 * k;
+            if (lo >= end) continue;
+            const bool hd = lo < sh, tl = lo + 4 > end;
+            if ((!hd || own_head) && !tl) { *(uint32_t *)(d + 4 * k) = v[k]; continue; }
+            if (tl && skip_tail) continue;
+            const uint32_t bs = hd ? sh : 0u, be = tl ? end - lo : 4u;
+            uint8_t *p = d + 4 * k;
+            if (bs == 0 && be > 0) p[0] = (uint8_t)v[k];
+            if (bs <= 1 && be > 1) p[1] = (uint8_t)(v[k] >> 8);
+            if (bs <= 2 && be > 2) p[2] = (uint8_t)(v[k] >> 16);
+            if (be > 3) p[3] = (uint8_t)(v[k] >> 24);
+        }
+    }
+}
+
+// Records [js, je) of a staged decode sub-batch, whose XDR bytes the tile
+// holds (stream offset sb + x at tile offset lds0 + x), decoded by threads
+// ctid < nthr: every field by groups of lanes per record; byte fields of
+// error-free blocks with whole boundary dwords (dec_bytes_lean).
+__device__ __forceinline__ void dec_stage_batch(const RecArgs &a, const uint8_t *tile, int64_t lds0, uint64_t rb,
+                                                uint32_t js, uint32_t je, const uint32_t *sstart,
+                                                const uint32_t *snrel, const uint8_t *supto, const uint64_t *s_base,
+                                                const uint32_t (&xs)[kMaxDynLds], bool lean, uint32_t ctid,
+                                                uint32_t nthr) {
+    constexpr uint32_t RS = kRecPerBlock + 1;
+    uint32_t fpre = 0;
+    uint32_t d = 0;
+    const uint32_t m = je - js;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind != XDRG_K_DYNAMIC) {
+            const uint32_t nw = f.xbytes >> 2;
+            if (nw) {
+                const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
+                const uint32_t gl = ctid & (G - 1), ng = nthr / G;
+                for (uint32_t j = js + ctid / G; j < je; j += ng) {
+                    if (k >= supto[j]) continue;
+                    const uint32_t *w = (const uint32_t *)(tile + (lds0 + (int64_t)(sstart[j] + fpre +
+                                                                               dyn_before(a, snrel, j, d))));
+                    for (uint32_t i = gl; i < nw; i += G) fixed_store(f, rb + j, 4 * i, w[i]);
+                }
+            }
+            fpre += f.xbytes;
+            continue;
+        }
+        const bool bytes = f.xsz == 1;
+        const uint64_t esz = bytes ? 1 : f.nsz;
+        const uint32_t *rel = snrel + d * RS;
+        const uint64_t base = s_base[d];
+        const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
+        const uint32_t G = a.force_g ? a.force_g : pow2_lanes(fbytes / m, a.lane_bytes_dec);
+        const uint32_t gl = ctid & (G - 1), ng = nthr / G;
+        for (uint32_t j = js + ctid / G; j < je; j += ng) {
+            if (k >= supto[j]) continue;
+            const uint64_t cnt = rel[j + 1] - rel[j];
+            if (!cnt) continue;
+            // tile offset of the payload (after the length word)
+            const int64_t L = lds0 + (int64_t)(sstart[j] + fpre + dyn_before(a, snrel, j, d) + 4);
+            uint8_t *dst = f.data + (base + rel[j]) * esz;
+            if (bytes && lean) {
+                // the boundary dwords with records j - 1 and j + 1 (within the sub-batch)
+                const uint32_t sh = (uint32_t)((uintptr_t)dst & 3);
+                const uint32_t tb = (sh + (uint32_t)cnt) & 3;   // record j's bytes in its last dword
+                bool own = false, skip = false;
+                uint32_t hv = 0;
+                if (sh && j > js) {
+                    const uint32_t cp = rel[j] - rel[j - 1];
+                    if (cp >= sh && cnt >= 4 - sh) {
+                        own = true;
+                        const int64_t Lp = lds0 + (int64_t)(sstart[j - 1] + fpre + dyn_before_xs(xs, snrel, j - 1, d) + 4);
+                        const uint32_t pw = tile_word(tile, Lp + cp - sh), hw = tile_word(tile, L);
+                        hv = (pw & ((1u << (8 * sh)) - 1u)) | (hw << (8 * sh));
+                    }
+                }
+                if (tb && j + 1 < je && cnt >= tb && rel[j + 2] - rel[j + 1] >= 4 - tb) skip = true;
+                dec_bytes_lean(dst, tile, (uint32_t)L, (uint32_t)cnt, own, hv, skip, gl, G);
+            } else if (bytes) {
+                const uint32_t sh = (uint32_t)((uintptr_t)dst & 3);
+                const uint64_t nch = (((sh + cnt + 3) >> 2) + 3) >> 2;
+                for (uint64_t c = gl; c < nch; c += G) {
+                    const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c - 4));
+                    Chunk5 q;
+                    q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = w[4];
+                    dec_store(dst - sh, q, c, cnt, sh);
+                }
+            } else {
+                const uint64_t nch = (cnt + 3) >> 2;
+                for (uint64_t c = gl; c < nch; c += G) {
+                    const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c));
+                    uint32_t *o = (uint32_t *)(dst + 16 * c);
+                    if (4 * c + 4 <= cnt) {
+                        u32x4a v;
+                        v.x = bswap32r(w[0]); v.y = bswap32r(w[1]); v.z = bswap32r(w[2]); v.w = bswap32r(w[3]);
+                        *(u32x4a *)o = v;
+                    } else {
+                        for (uint64_t e = 0; 4 * c + e < cnt; ++e) o[e] = bswap32r(w[e]);
+                    }
+                }
+            }
+        }
         ++d;
     }
 }
@@ -2239,8 +2392,11 @@ __device__ __forceinline__ void lb_resolve(const RecArgs &a, uint64_t b, const u
     }
 }
 
+#ifndef XDRG_DEC_STAGE_OCC
+#define XDRG_DEC_STAGE_OCC 5   // blocks per CU the register budget is sized for
+#endif
 template <bool LB>
-__global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
+__global__ __launch_bounds__(kRecThreads, XDRG_DEC_STAGE_OCC) void k_dec_stage(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;
     uint32_t *sstart = (uint32_t *)smem;
@@ -2267,6 +2423,9 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
     const uint64_t rb = bid * kRecPerBlock;
     const uint32_t nrec = (uint32_t)(a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0);
     uint32_t *lcnt = (uint32_t *)tile;   // LB: walked counts [ndyn][kRecPerBlock], consumed before staging
+    uint32_t xs[kMaxDynLds];             // XDR element size per dynamic field (1: padded bytes)
+#pragma unroll
+    for (int e = 0; e < kMaxDynLds; ++e) xs[e] = (uint32_t)e < a.ndyn ? a.f[a.dyn_idx[e]].xsz : 0u;
     if (LB) {
         // ---- k_dec_sizes_g's walk (same checks, order and dead-record rule)
 #pragma unroll
@@ -2361,7 +2520,10 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) supto[t0 + j] = (uint8_t)upto[j];
-    __syncthreads();
+    bool full = true;   // every live record decodes every field: byte fields take dec_bytes_lean
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) full &= t0 + j >= nlive || upto[j] == a.nf;
+    const bool lean = __syncthreads_and(full) && a.dec_lean;
     // staging needs every record's fields to end where the next begins or
     // before (records in stream order); otherwise the block goes direct
     const uint32_t fx = a.fixed_xdr - (a.framed ? 4 : 0);   // fixed XDR bytes of the fields
@@ -2380,7 +2542,7 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
 
     if (wide) {
         for (uint32_t j = 0; j < nlive; ++j)
-            dec_record_block(a, rb + j, rec_extent(a, rb + j).a + (a.framed ? 4 : 0), supto[j], snrel, j);
+            dec_record_block(a, rb + j, rec_extent(a, rb + j).a + (a.framed ? 4 : 0), supto[j], snrel, j, tid, kRecThreads);
         return;
     }
     // ---- sub-batches
@@ -2388,7 +2550,7 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
     uint32_t k1 = nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
     while (js < nlive) {
         if (k1 == 0) {   // too large for the tile: the whole block decodes record js
-            dec_record_block(a, rb + js, sb + sstart[js], supto[js], snrel, js);
+            dec_record_block(a, rb + js, sb + sstart[js], supto[js], snrel, js, tid, kRecThreads);
             ++js;
             k1 = js < nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
             continue;
@@ -2401,66 +2563,7 @@ __global__ __launch_bounds__(kRecThreads, 5) void k_dec_stage(const RecArgs a) {
         stage_copy(tile, a0, cb, 1);
         __syncthreads();
         const int64_t lds0 = -(int64_t)(a0[0] - (in + sb));   // tile offset of sstart value x: lds0 + x
-        uint32_t fpre = 0;
-        uint32_t d = 0;
-        const uint32_t m = je - js;
-        for (uint32_t k = 0; k < a.nf; ++k) {
-            const VField &f = a.f[k];
-            if (f.kind != XDRG_K_DYNAMIC) {
-                const uint32_t nw = f.xbytes >> 2;
-                if (nw) {
-                    const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
-                    const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-                    for (uint32_t j = js + tid / G; j < je; j += ng) {
-                        if (k >= supto[j]) continue;
-                        const uint32_t *w = (const uint32_t *)(tile + (lds0 + (int64_t)(sstart[j] + fpre +
-                                                                                   dyn_before(a, snrel, j, d))));
-                        for (uint32_t i = gl; i < nw; i += G) fixed_store(f, rb + j, 4 * i, w[i]);
-                    }
-                }
-                fpre += f.xbytes;
-                continue;
-            }
-            const bool bytes = f.xsz == 1;
-            const uint64_t esz = bytes ? 1 : f.nsz;
-            const uint32_t *rel = snrel + d * RS;
-            const uint64_t base = s_base[d];
-            const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
-            const uint32_t G = a.force_g ? a.force_g : pow2_lanes(fbytes / m, a.lane_bytes_dec);
-            const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-            for (uint32_t j = js + tid / G; j < je; j += ng) {
-                if (k >= supto[j]) continue;
-                const uint64_t cnt = rel[j + 1] - rel[j];
-                if (!cnt) continue;
-                // tile offset of the payload (after the length word)
-                const int64_t L = lds0 + (int64_t)(sstart[j] + fpre + dyn_before(a, snrel, j, d) + 4);
-                uint8_t *dst = f.data + (base + rel[j]) * esz;
-                if (bytes) {
-                    const uint32_t sh = (uint32_t)((uintptr_t)dst & 3);
-                    const uint64_t nch = (((sh + cnt + 3) >> 2) + 3) >> 2;
-                    for (uint64_t c = gl; c < nch; c += G) {
-                        const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c - 4));
-                        Chunk5 q;
-                        q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = w[4];
-                        dec_store(dst - sh, q, c, cnt, sh);
-                    }
-                } else {
-                    const uint64_t nch = (cnt + 3) >> 2;
-                    for (uint64_t c = gl; c < nch; c += G) {
-                        const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c));
-                        uint32_t *o = (uint32_t *)(dst + 16 * c);
-                        if (4 * c + 4 <= cnt) {
-                            u32x4a v;
-                            v.x = bswap32r(w[0]); v.y = bswap32r(w[1]); v.z = bswap32r(w[2]); v.w = bswap32r(w[3]);
-                            *(u32x4a *)o = v;
-                        } else {
-                            for (uint64_t e = 0; 4 * c + e < cnt; ++e) o[e] = bswap32r(w[e]);
-                        }
-                    }
-                }
-            }
-            ++d;
-        }
+        dec_stage_batch(a, tile, lds0, rb, js, je, sstart, snrel, supto, s_base, xs, lean, tid, kRecThreads);
         js = je;
         k1 = js < nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;   // its barrier ends the tile's use
     }
@@ -2493,6 +2596,7 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     a.lane_bytes_enc = t.lane_bytes_enc;
     a.lane_bytes_dec = t.lane_bytes_dec;
     a.tile_bytes = t.tile_bytes;
+    a.dec_lean = (uint32_t)t.dec_lean;
     a.big_rec = 0;
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;

@@ -134,7 +134,7 @@ struct RecArgs {
                                // kernels, the others the staged ones (0: one kernel for all)
     uint32_t ncond;            // conditional fields in the schema (0: every record has all fields)
     uint32_t byref;            // 0, or 1 + the field encoded by reference / decoded as a view
-    uint32_t rsv2;
+    uint32_t dec_lean;         // staged decode: byte fields of error-free blocks by dec_bytes_lean
     uint64_t *ref_pos;         // byref: encode splice[n] / decode payload_pos[n]
     uint32_t payk;             // 0, or 1 + the dynamic byte field the payload kernels move for the
                                // group kernels' blocks (k_enc/dec_payload)
@@ -172,6 +172,8 @@ struct Tuning {
     int32_t payload = 1;            // key 18: one dynamic byte field on group-kernel blocks: 1 payload kernels, 0 in place
     int32_t dec_lb = 0;             // key 19: staged record-path decode: 1 counts walked in the place kernel
                                     // (decoupled look-back), 0 separate sizes walk + scan kernels
+    int32_t dec_lean = 1;           // key 20: staged decode, byte fields of error-free blocks: 1 whole
+                                    // boundary dwords (dec_bytes_lean), 0 byte-stored record edges
     int32_t enc_u = 2, dec_u = 2;   // keys 4/5: group kernels, 16-byte chunks per lane in flight
     int32_t enc_r = 1, dec_r = 1;   // keys 10/11: group kernels, records per lane in flight
     uint32_t force_g = 0;           // key 6: lanes per record (0 = sized from the field)

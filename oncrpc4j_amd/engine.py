@@ -15,7 +15,9 @@ import os
 
 from . import abi
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libxdrgpu.so")
+# XDRG_LIBRARY: another build of the same C-ABI (measurement tools A/B kernel variants)
+LIB_PATH = os.environ.get("XDRG_LIBRARY") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                          "libxdrgpu.so")
 
 _LIB = None
 

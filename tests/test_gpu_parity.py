@@ -41,9 +41,12 @@ SCHEMAS = {
 # Record-path implementations (kernels_rec.hip launch_rec_phase), as tuning
 # (key, value) pairs: key 9 = 4 staged (sub-batches through an LDS tile, the
 # default), with key 19 = 1 the staged decode walking the counts itself
-# (decoupled look-back, no sizes / scan kernels); key 9 = 0 group per record,
-# 3 lane per record.  Tests taking `rec_kernel` run under each.
-REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),), "staged_lb": ((9, 4), (19, 1))}
+# (decoupled look-back, no sizes / scan kernels), key 20 = 0 its byte
+# fields' record edges byte-stored instead of written as whole dwords;
+# key 9 = 0 group per record, 3 lane per record.  Tests taking `rec_kernel`
+# run under each.
+REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),), "staged_lb": ((9, 4), (19, 1)),
+               "staged_edges": ((9, 4), (20, 0))}
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
@@ -264,11 +267,12 @@ def test_error_parity(gpu_ctx, rec_kernel, name, framed):
             assert g2[:3] == o2[:3], desc
 
 
+@pytest.mark.parametrize("lean", [1, 0], ids=["lean", "edges"])
 @pytest.mark.parametrize("tile", [1024, 4096])
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("name", ["cfg1_int_int_string", "cfg3_6xint_opaque", "cfg4_int_string_intvec",
                                   "dyn_vectors"])
-def test_staged_tile_sizes(gpu_ctx, name, framed, tile):
+def test_staged_tile_sizes(gpu_ctx, name, framed, tile, lean):
     """Staged place kernels with small LDS tiles: records whose staged bytes
     exceed the tile take the whole-block direct path, the others form
     sub-batches of every size (dyn_vectors has non-stageable vector types and
@@ -281,6 +285,7 @@ def test_staged_tile_sizes(gpu_ctx, name, framed, tile):
     gpu_ctx.tune(9, 4)
     gpu_ctx.tune(12, tile)
     gpu_ctx.tune(13, 0)   # every block staged (no split of large-record blocks to the group kernel)
+    gpu_ctx.tune(20, lean)
     try:
         xdr, offs = gpu_encode(gpu_ctx, fields, hb, framed)
         assert xdr == want

@@ -1,6 +1,9 @@
 """Per-kernel counter table from tools/prof_rec.sh output directories.
 
-  python tools/pmc_table.py gpurun_out/p_c4      (prefix of the *_fetch, *_sq ... dirs)
+  python tools/pmc_table.py gpurun_out/p_c4 [--grid]   (prefix of the *_fetch, *_sq ... dirs)
+
+--grid keys the table by kernel and grid size (one tool launching a kernel
+on several workloads).
 
 Median over dispatches of every counter, per xdrg kernel; FETCH_SIZE is
 doubled (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md)."""
@@ -13,12 +16,15 @@ import sys
 
 def main():
     pre = sys.argv[1]
+    by_grid = "--grid" in sys.argv[2:]
     vals = {}
     for path in glob.glob(pre + "_*/run_counter_collection.csv"):
         for r in csv.DictReader(open(path)):
             if "xdrg::" not in r["Kernel_Name"]:
                 continue
             k = r["Kernel_Name"].replace("void ", "").replace("xdrg::", "").split("(")[0]
+            if by_grid:
+                k += " grid " + r["Grid_Size"]
             d = vals.setdefault(k, {})
             d.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
             d.setdefault("_vgpr", []).append(float(r["VGPR_Count"]))
