@@ -565,7 +565,8 @@ __host__ __device__ constexpr size_t enc_lds_bytes(uint32_t nd) {
 // Walk record r (known valid) and store each dynamic field's count at
 // cnt_row[d * kRecPerBlock]; returns the record's first payload byte.
 __device__ __forceinline__ uint32_t walk_counts(const RecArgs &a, uint64_t r, uint32_t *cnt_row,
-                                                uint32_t *sub, uint64_t *start, uint64_t *bytes) {
+                                                uint32_t *sub, uint64_t *start, uint64_t *bytes,
+                                                uint32_t stride = kRecPerBlock) {
     const Extent e = rec_extent(a, r);
     uint64_t pos = e.a;
     *start = e.a;
@@ -609,7 +610,7 @@ __device__ __forceinline__ uint32_t walk_counts(const RecArgs &a, uint64_t r, ui
         }
         if (e.b - pos < need) return XDRG_E_SHORT;
         pos += need;
-        cnt_row[(size_t)d * kRecPerBlock] = (uint32_t)len;
+        cnt_row[(size_t)d * stride] = (uint32_t)len;
         ++d;
     }
     return 0;
@@ -1841,12 +1842,13 @@ __device__ __forceinline__ void stage_copy(uint8_t *tile, const uint8_t *const (
 
 // XDR bytes of record j's dynamic fields d < nd (counts from a rel table:
 // row d holds element offsets relative to the block's first record).
-__device__ __forceinline__ uint64_t dyn_before(const RecArgs &a, const uint32_t *rel, uint32_t j, uint32_t nd) {
+__device__ __forceinline__ uint64_t dyn_before(const RecArgs &a, const uint32_t *rel, uint32_t j, uint32_t nd,
+                                               uint32_t rs = kRecPerBlock + 1) {
     uint64_t s = 0;
 #pragma unroll
     for (int d = 0; d < kMaxDynLds; ++d) {
         if ((uint32_t)d >= nd) continue;
-        const uint32_t *r = rel + d * (kRecPerBlock + 1);
+        const uint32_t *r = rel + d * rs;
         s += dyn_xdr_bytes(a.f[a.dyn_idx[d]], r[j + 1] - r[j]);
     }
     return s;
@@ -2089,7 +2091,8 @@ __host__ __device__ constexpr size_t dec_stage_meta(uint32_t nd) {
 // too large for the tile).  Counts come from the block's relative native offsets snrel, native
 // offsets from the columns' offsets arrays this block just wrote.
 __device__ __forceinline__ void dec_record_block(const RecArgs &a, uint64_t r, uint64_t pos, uint32_t upto,
-                                 const uint32_t *snrel, uint32_t j, uint32_t tid, uint32_t nthr) {
+                                 const uint32_t *snrel, uint32_t j, uint32_t tid, uint32_t nthr,
+                                 uint32_t rs = kRecPerBlock + 1) {
     const uint8_t *in = a.xdr;
     const Span sp = make_span(in, in + a.xdr_cap, (const uint8_t *)a.block_sums);
     uint32_t d = 0;
@@ -2102,7 +2105,7 @@ __device__ __forceinline__ void dec_record_block(const RecArgs &a, uint64_t r, u
             continue;
         }
         const bool bytes = f.xsz == 1;
-        const uint32_t *rel = snrel + (size_t)d * (kRecPerBlock + 1);
+        const uint32_t *rel = snrel + (size_t)d * rs;
         const uint64_t cnt1 = rel[j + 1] - rel[j];
         uint8_t *dst[1] = {f.data + f.offsets[r] * (bytes ? 1 : f.nsz)};
         const uint8_t *src[1] = {in + pos + 4};
@@ -2125,12 +2128,12 @@ __device__ __forceinline__ uint32_t tile_word(const uint8_t *tile, int64_t o) {
 }
 // XDR bytes of record j's dynamic fields before d (xs: their element sizes).
 __device__ __forceinline__ uint32_t dyn_before_xs(const uint32_t (&xs)[kMaxDynLds], const uint32_t *rel,
-                                                  uint32_t j, uint32_t d) {
+                                                  uint32_t j, uint32_t d, uint32_t rs = kRecPerBlock + 1) {
     uint32_t s = 0;
 #pragma unroll
     for (int e = 0; e < kMaxDynLds - 1; ++e) {
         if ((uint32_t)e >= d) continue;
-        const uint32_t *r = rel + e * (kRecPerBlock + 1);
+        const uint32_t *r = rel + e * rs;
         const uint32_t c = r[j + 1] - r[j];
         s += 4 + (xs[e] == 1 ? (c + 3) & ~3u : c * xs[e]);
     }
@@ -2186,12 +2189,12 @@ __device__ __forceinline__ void dec_bytes_lean(uint8_t *dst, const uint8_t *tile
 // holds (stream offset sb + x at tile offset lds0 + x), decoded by threads
 // ctid < nthr: every field by groups of lanes per record; byte fields of
 // error-free blocks with whole boundary dwords (dec_bytes_lean).
+template <uint32_t RS>
 __device__ __forceinline__ void dec_stage_batch(const RecArgs &a, const uint8_t *tile, int64_t lds0, uint64_t rb,
                                                 uint32_t js, uint32_t je, const uint32_t *sstart,
                                                 const uint32_t *snrel, const uint8_t *supto, const uint64_t *s_base,
                                                 const uint32_t (&xs)[kMaxDynLds], bool lean, uint32_t ctid,
                                                 uint32_t nthr) {
-    constexpr uint32_t RS = kRecPerBlock + 1;
     uint32_t fpre = 0;
     uint32_t d = 0;
     const uint32_t m = je - js;
@@ -2205,7 +2208,7 @@ __device__ __forceinline__ void dec_stage_batch(const RecArgs &a, const uint8_t 
                 for (uint32_t j = js + ctid / G; j < je; j += ng) {
                     if (k >= supto[j]) continue;
                     const uint32_t *w = (const uint32_t *)(tile + (lds0 + (int64_t)(sstart[j] + fpre +
-                                                                               dyn_before(a, snrel, j, d))));
+                                                                               dyn_before(a, snrel, j, d, RS))));
                     for (uint32_t i = gl; i < nw; i += G) fixed_store(f, rb + j, 4 * i, w[i]);
                 }
             }
@@ -2224,7 +2227,7 @@ __device__ __forceinline__ void dec_stage_batch(const RecArgs &a, const uint8_t 
             const uint64_t cnt = rel[j + 1] - rel[j];
             if (!cnt) continue;
             // tile offset of the payload (after the length word)
-            const int64_t L = lds0 + (int64_t)(sstart[j] + fpre + dyn_before(a, snrel, j, d) + 4);
+            const int64_t L = lds0 + (int64_t)(sstart[j] + fpre + dyn_before(a, snrel, j, d, RS) + 4);
             uint8_t *dst = f.data + (base + rel[j]) * esz;
             if (bytes && lean) {
                 // the boundary dwords with records j - 1 and j + 1 (within the sub-batch)
@@ -2236,7 +2239,7 @@ __device__ __forceinline__ void dec_stage_batch(const RecArgs &a, const uint8_t 
                     const uint32_t cp = rel[j] - rel[j - 1];
                     if (cp >= sh && cnt >= 4 - sh) {
                         own = true;
-                        const int64_t Lp = lds0 + (int64_t)(sstart[j - 1] + fpre + dyn_before_xs(xs, snrel, j - 1, d) + 4);
+                        const int64_t Lp = lds0 + (int64_t)(sstart[j - 1] + fpre + dyn_before_xs(xs, snrel, j - 1, d, RS) + 4);
                         const uint32_t pw = tile_word(tile, Lp + cp - sh), hw = tile_word(tile, L);
                         hv = (pw & ((1u << (8 * sh)) - 1u)) | (hw << (8 * sh));
                     }
@@ -2563,9 +2566,158 @@ __global__ __launch_bounds__(kRecThreads, XDRG_DEC_STAGE_OCC) void k_dec_stage(c
         stage_copy(tile, a0, cb, 1);
         __syncthreads();
         const int64_t lds0 = -(int64_t)(a0[0] - (in + sb));   // tile offset of sstart value x: lds0 + x
-        dec_stage_batch(a, tile, lds0, rb, js, je, sstart, snrel, supto, s_base, xs, lean, tid, kRecThreads);
+        dec_stage_batch<RS>(a, tile, lds0, rb, js, je, sstart, snrel, supto, s_base, xs, lean, tid, kRecThreads);
         js = je;
         k1 = js < nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;   // its barrier ends the tile's use
+    }
+}
+
+// ---- one-pass staged decode: LDS-resident blocks ------------------------------
+// Blocks of kResRec records whose XDR extents lie in one range of at most
+// tile_bytes (small-record batches; the launcher checks the average).  The
+// block stages the range once, walks its records' length words in LDS (the
+// checks and order of walk_counts), publishes its count totals and learns
+// its native offsets by decoupled look-back (lb_resolve), then decodes every
+// record from the same tile: the stream is read once, no sizes/scan kernels.
+// A block whose range does not fit walks from HBM and decodes record by
+// record (dec_record_block).
+__host__ __device__ constexpr size_t dec_res_meta(uint32_t nd) {
+    return ((size_t)(kResRec + 1) * 4 * (1 + nd) + kResRec + 15) & ~(size_t)15;
+}
+
+// walk_counts over a staged record whose XDR bytes [p, e) are at those tile
+// offsets; e_len = the record's extent length (the framed mark's check).
+__device__ __forceinline__ uint32_t walk_counts_tile(const RecArgs &a, const uint8_t *tile, uint32_t p, uint32_t e,
+                                                     uint32_t (&cnt)[kMaxDynLds], uint32_t *sub) {
+    *sub = 0;
+    if (a.framed) {
+        if (e - p < 4) return XDRG_E_SHORT;
+        const uint32_t m = bswap32r(tile_word(tile, p));
+        const uint64_t want_len = a.rec_in ? (uint64_t)(e - p - 4) : a.rec_stride - 4;
+        if (!(m & kLastFrag) || (uint64_t)(m & kSizeMask) != want_len) return XDRG_E_FRAME;
+        p += 4;
+    }
+    uint32_t d = 0;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        *sub = 2 * k + 1;
+        if (f.kind != XDRG_K_DYNAMIC) {
+            if (e - p < f.xbytes) return XDRG_E_SHORT;
+            p += f.xbytes;
+            continue;
+        }
+        if (e - p < 4) return XDRG_E_SHORT;
+        const int32_t len = (int32_t)bswap32r(tile_word(tile, p));
+        p += 4;
+        uint64_t need;
+        if (f.xsz == 1) {
+            if (len == 0) need = 0;
+            else if (len < 0) return XDRG_E_CORRUPT;
+            else need = (uint64_t)len + pad4((uint64_t)len);
+        } else {
+            if (len < 0) return XDRG_E_CORRUPT;
+            need = (uint64_t)len * f.xsz;
+        }
+        if ((uint64_t)(e - p) < need) return XDRG_E_SHORT;
+        p += (uint32_t)need;
+        cnt[d++] = (uint32_t)len;
+    }
+    return 0;
+}
+
+__global__ __launch_bounds__(kRecThreads, 4) void k_dec_res(const RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr uint32_t RS = kResRec + 1;
+    uint32_t *sstart = (uint32_t *)smem;
+    uint32_t *snrel = sstart + RS;
+    uint8_t *supto = (uint8_t *)(snrel + (size_t)a.ndyn * RS);
+    uint8_t *tile = smem + dec_res_meta(a.ndyn);
+    __shared__ uint64_t s_base[kMaxDynLds];
+    __shared__ unsigned long long s_b, s_bad;
+    __shared__ uint64_t s_range[2];
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {   // blocks take tickets in start order: every block waited on is running
+        s_b = atomicAdd(a.lb_ticket, 1ull);
+        s_bad = a.n;
+    }
+    __syncthreads();
+    const uint64_t bid = s_b, rb = bid * kResRec;
+    const uint32_t nrec = (uint32_t)(a.n - rb < (uint64_t)kResRec ? a.n - rb : (uint64_t)kResRec);
+    uint32_t xs[kMaxDynLds];
+#pragma unroll
+    for (int e = 0; e < kMaxDynLds; ++e) xs[e] = (uint32_t)e < a.ndyn ? a.f[a.dyn_idx[e]].xsz : 0u;
+    // ---- extents; the block's range [x0, x1) and whether the tile holds it
+    const bool mine = tid < nrec;
+    const Extent ex = mine ? rec_extent(a, rb + tid) : Extent{0, 0};
+    if (tid == 0) s_range[0] = ex.a;
+    if (tid == nrec - 1) s_range[1] = ex.b;
+    __syncthreads();
+    const uint64_t x0 = s_range[0] & ~(uint64_t)15, x1 = s_range[1];
+    const bool inside = !mine || (ex.a >= x0 && ex.b <= x1);
+    const bool res = __syncthreads_and(inside) && x1 >= x0 && x1 - x0 <= a.tile_bytes;
+    if (res) {
+        const uint8_t *a0[kMaxDynLds] = {a.xdr + x0, nullptr, nullptr, nullptr};
+        const uint32_t cb[kMaxDynLds + 1] = {0, (uint32_t)((x1 - x0 + 15) >> 4), 0, 0, 0};
+        stage_copy(tile, a0, cb, 1);
+    }
+    __syncthreads();
+    // ---- walk
+    uint32_t cnt[kMaxDynLds] = {0, 0, 0, 0};
+    uint32_t err = 0, sub = 0;
+    if (mine) {
+        if (res) {
+            err = walk_counts_tile(a, tile, (uint32_t)(ex.a - x0), (uint32_t)(ex.b - x0), cnt, &sub);
+        } else {
+            uint64_t st, by;
+            err = walk_counts(a, rb + tid, cnt, &sub, &st, &by, 1);
+        }
+        if (err) {
+            atomicMin(a.errkey, err_key(rb + tid, sub, err));
+            atomicMin(&s_bad, (unsigned long long)(rb + tid));
+#pragma unroll
+            for (int d = 0; d < kMaxDynLds; ++d) cnt[d] = 0;
+        }
+    }
+    uint64_t agg[kMaxDynLds + 1] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int d = 0; d < kMaxDynLds; ++d)
+        if ((uint32_t)d < a.ndyn) agg[d] = block_sum(cnt[d]);   // its barriers also publish s_bad
+    if (tid < 64) lb_resolve(a, bid, agg, (uint64_t)s_bad, s_base, &s_bad);
+    __syncthreads();
+    const uint64_t bad = s_bad;
+    const uint32_t nlive = bad > rb ? (uint32_t)(bad - rb < (uint64_t)nrec ? bad - rb : (uint64_t)nrec) : 0;
+    // ---- native offsets, capacity, record starts
+    const bool live = tid < nlive;
+    uint32_t upto = live ? a.nf : 0u;
+#pragma unroll
+    for (int d = 0; d < kMaxDynLds; ++d) {
+        if ((uint32_t)d >= a.ndyn) continue;
+        const uint32_t k = a.dyn_idx[d];
+        const VField &f = a.f[k];
+        const uint32_t c = live ? cnt[d] : 0u;
+        uint64_t btot;
+        const uint64_t rel = block_excl_scan(c, &btot);
+        const uint64_t off = s_base[d] + rel;
+        if (tid < RS) snrel[d * RS + tid] = (uint32_t)rel;   // [nrec] = the block's total
+        if (mine) {
+            f.offsets[rb + tid] = off;
+            if (live && off + c > f.cap) {   // native column too small
+                atomicMin(a.errkey, err_key(rb + tid, 2 * k + 2, XDRG_E_CAPACITY));
+                if (upto > k) upto = k;
+            }
+        }
+    }
+    const uint32_t fr = a.framed ? 4u : 0u;
+    if (mine) {
+        sstart[tid] = (uint32_t)(res ? ex.a + fr - x0 : 0u);
+        supto[tid] = (uint8_t)upto;
+    }
+    const bool lean = __syncthreads_and(!live || upto == a.nf) && a.dec_lean;
+    if (res) {
+        dec_stage_batch<RS>(a, tile, 0, rb, 0, nlive, sstart, snrel, supto, s_base, xs, lean, tid, kRecThreads);
+    } else {
+        for (uint32_t j = 0; j < nlive; ++j)
+            dec_record_block(a, rb + j, rec_extent(a, rb + j).a + fr, supto[j], snrel, j, tid, kRecThreads, RS);
     }
 }
 
@@ -2615,6 +2767,10 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     // staged decode: the sizes walk runs inside the place kernel (its counts
     // borrow the tile until staging starts)
     const bool lb = stage && t.dec_lb && a.ndyn && (size_t)a.ndyn * kRecPerBlock * 4 <= a.tile_bytes;
+    // one-pass LDS-resident decode: small records (the average block range fits the tile with margin)
+    const uint64_t nb_res = (a.n + kResRec - 1) / kResRec;
+    const bool res = stage && !lb && t.dec_res && a.ndyn && a.n &&
+                     (a.xdr_cap / a.n + 1) * kResRec * 5 / 4 <= (uint64_t)t.res_tile;
     const uint64_t pblk = (a.n + 3) / 4;   // a wave per record, 4 records per block
     const dim3 pgrid((unsigned)(pblk < (1u << 22) ? pblk : (1u << 22)));
     switch (phase) {
@@ -2637,18 +2793,25 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
         }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
-    case REC_DEC_SIZES:
-        if (lb) return (int)hipMemsetAsync(a.lb_state, 0, ((uint64_t)(a.ndyn + 1) * nb + 1) * 8, st);
+    case REC_DEC_SIZES:   // (the ticket word precedes the status words)
+        if (lb || res)
+            return (int)hipMemsetAsync(a.lb_ticket, 0, ((uint64_t)(a.ndyn + 1) * (res ? nb_res : nb) + 1) * 8, st);
         if (grp || lane) hipLaunchKernelGGL(k_dec_sizes_g, dim3(nb), dim3(kRecThreads),
                                     (size_t)a.ndyn * kRecPerBlock * 4, st, a);
         else hipLaunchKernelGGL(k_dec_sizes_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SCAN:
-        if (a.ndyn && !lb)
+        if (a.ndyn && !lb && !res)
             hipLaunchKernelGGL(k_scan_rows, dim3(a.ndyn), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_DEC_PLACE:
-        if (stage) {
+        if (res) {
+            RecArgs ar = a;
+            ar.nblocks = nb_res;
+            ar.tile_bytes = t.res_tile;
+            hipLaunchKernelGGL(k_dec_res, dim3((unsigned)nb_res), dim3(kRecThreads),
+                               dec_res_meta(a.ndyn) + t.res_tile + kStageSlack, st, ar);
+        } else if (stage) {
             a.big_rec = t.big_rec;
             if (lb) hipLaunchKernelGGL(k_dec_stage<true>, dim3(nb), dim3(kRecThreads),
                                        dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);

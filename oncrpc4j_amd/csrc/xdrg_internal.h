@@ -142,7 +142,7 @@ struct RecArgs {
     uint64_t *pay_pos;         // payk: per record, stream offset of that field's length word
                                // (decode: ~0 = not to be written)
     uint64_t *lb_state;        // staged decode with look-back: [ndyn + 1][nblocks] status words
-    unsigned long long *lb_ticket;   // and the block ticket (both zeroed before the launch)
+    unsigned long long *lb_ticket;   // and the block ticket just before them (both zeroed before the launch)
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
     int32_t cvals[XDRG_MAX_CASES];  // case values of the conditional fields
@@ -172,6 +172,9 @@ struct Tuning {
     int32_t payload = 1;            // key 18: one dynamic byte field on group-kernel blocks: 1 payload kernels, 0 in place
     int32_t dec_lb = 0;             // key 19: staged record-path decode: 1 counts walked in the place kernel
                                     // (decoupled look-back), 0 separate sizes walk + scan kernels
+    int32_t dec_res = 0;            // key 22: staged decode of small records: 1 one pass, blocks of 128
+                                    // records decoded from their LDS-resident range (k_dec_res)
+    uint32_t res_tile = 32768;      // key 23: k_dec_res, LDS bytes for a block's range
     int32_t dec_lean = 1;           // key 20: staged decode, byte fields of error-free blocks: 1 whole
                                     // boundary dwords (dec_bytes_lean), 0 byte-stored record edges
     int32_t enc_u = 2, dec_u = 2;   // keys 4/5: group kernels, 16-byte chunks per lane in flight
@@ -320,6 +323,7 @@ int launch_scan_rows(uint64_t *sums, uint64_t nblocks, uint64_t *totals, uint32_
 constexpr int kRecThreads = 256;   // record path: threads per block
 constexpr int kRecPerThread = 4;   // records per thread in the size/scan pass
 constexpr int kRecPerBlock = kRecThreads * kRecPerThread;
+constexpr int kResRec = 128;       // records per block of the one-pass staged decode (k_dec_res)
 constexpr int kMaxDynLds = 4;      // dynamic fields whose per-record metadata is staged in LDS
 
 }  // namespace xdrg

@@ -42,11 +42,13 @@ SCHEMAS = {
 # (key, value) pairs: key 9 = 4 staged (sub-batches through an LDS tile, the
 # default), with key 19 = 1 the staged decode walking the counts itself
 # (decoupled look-back, no sizes / scan kernels), key 20 = 0 its byte
-# fields' record edges byte-stored instead of written as whole dwords;
+# fields' record edges byte-stored instead of written as whole dwords,
+# key 22 = 1 the one-pass decode of small records (blocks of 128 records
+# decoded from their LDS-resident stream range, k_dec_res);
 # key 9 = 0 group per record, 3 lane per record.  Tests taking `rec_kernel`
 # run under each.
 REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),), "staged_lb": ((9, 4), (19, 1)),
-               "staged_edges": ((9, 4), (20, 0))}
+               "staged_edges": ((9, 4), (20, 0)), "staged_res": ((9, 4), (22, 1))}
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
@@ -551,3 +553,45 @@ def test_decode_packed_bytes_unaligned_base(gpu_ctx, rec_kernel, name, shift):
         g = big.cpu().numpy().view(np.uint8)
         assert (g[:shift] == 0x5A).all() and (g[shift + db.tensors[k][0].numel():] == 0x5A).all()
     assert db.to_host().equal(o[3])
+
+
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+@pytest.mark.parametrize("name", ["cfg4_int_string_intvec", "cfg1_int_int_string", "dyn_vectors", "cfg3_6xint_opaque"])
+def test_resident_decode_fallback_blocks(gpu_ctx, name, framed):
+    """One-pass decode (k_dec_res): small records, except a run of 14
+    records of ~3000 bytes whose block range exceeds the 32 KiB tile, so that
+    block walks from HBM and decodes record by record while its neighbours
+    stay resident; a second pass plants a corrupt length word in a resident
+    block (first-bad record, error code and the records before it)."""
+    fields = SCHEMAS[name]
+    n = 3000
+    hb = random_batch(fields, n, seed=zlib.crc32(f"res/{name}/{framed}".encode()), dyn_len=(0, 24))
+    rng = np.random.default_rng(7)
+    for k, (t, kind, _) in enumerate(fields):
+        if kind == DY and t in (O, STR):
+            vals, offs = hb.arrays[k]
+            lens = np.diff(offs.astype(np.int64))
+            lens[1300:1314] = rng.integers(2900, 3100, size=14)
+            no = np.zeros(n + 1, dtype=offs.dtype)
+            no[1:] = np.cumsum(lens)
+            hb.arrays[k] = (rng.integers(0, 256, size=int(no[-1]), dtype=np.uint8).astype(vals.dtype), no)
+    rc, want, want_offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total(framed), framed=framed)
+    assert rc == 0
+    caps = hb.dyn_caps()
+    gpu_ctx.tune(9, 4)
+    gpu_ctx.tune(22, 1)
+    try:
+        g = gpu_decode(gpu_ctx, fields, want, n, want_offs, caps, framed)
+        o = oracle_decode(fields, want, n, want_offs, caps, framed)
+        assert g[:3] == o[:3] == (0, n, 0)
+        assert g[3].equal(o[3])
+        bad = bytearray(want)
+        p = int(want_offs[2000]) + (4 if framed else 0) + 4 * sum(
+            f[2] if f[1] == FX else 1 for f in fields[:next(i for i, f in enumerate(fields) if f[1] == DY)])
+        bad[p:p + 4] = (0x7FFFFFF0).to_bytes(4, "big")   # first dynamic length word of record 2000
+        g = gpu_decode(gpu_ctx, fields, bytes(bad), n, want_offs, caps, framed)
+        o = oracle_decode(fields, bytes(bad), n, want_offs, caps, framed)
+        assert g[:3] == o[:3] and o[1] == 2000
+        assert g[3].equal(o[3], upto=2000)   # records before first_bad decoded
+    finally:
+        gpu_ctx.tune(0)
