@@ -616,7 +616,7 @@ __device__ __forceinline__ uint32_t walk_counts(const RecArgs &a, uint64_t r, ui
     return 0;
 }
 
-// The kRecPerThread records of a thread walked in lockstep, field by field
+// The kRecPerThread records r0 + j * rs of a thread walked in lockstep, field by field
 // (schemas without conditional fields): their length words are independent
 // loads, issued together (clamped addresses, no per-load guard) before any
 // is used, so a thread waits once per dynamic field instead of once per
@@ -626,7 +626,7 @@ __device__ __forceinline__ uint32_t walk_counts(const RecArgs &a, uint64_t r, ui
 // counts are stored for the dynamic fields the walk passed.
 __device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t r0, uint32_t nj,
                                                      uint32_t *cnt_row, uint32_t (&err)[kRecPerThread],
-                                                     uint32_t (&sub)[kRecPerThread]) {
+                                                     uint32_t (&sub)[kRecPerThread], uint32_t rs = 1) {
     constexpr uint32_t kNone = 0xffu;                         // slot past the batch end
     const uint8_t *dummy = (const uint8_t *)a.block_sums;     // any 4 readable bytes
     uint64_t pos[kRecPerThread], end[kRecPerThread];
@@ -634,7 +634,7 @@ __device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t 
     for (int j = 0; j < kRecPerThread; ++j) {
         sub[j] = 0;
         if ((uint32_t)j < nj) {
-            const Extent e = rec_extent(a, r0 + j);
+            const Extent e = rec_extent(a, r0 + (uint64_t)j * rs);
             pos[j] = e.a; end[j] = e.b; err[j] = 0;
         } else {
             pos[j] = end[j] = 0; err[j] = kNone;
@@ -694,7 +694,7 @@ __device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t 
             }
             if (end[j] - pos[j] < need) { err[j] = XDRG_E_SHORT; continue; }
             pos[j] += need;
-            cnt_row[(size_t)d * kRecPerBlock + j] = (uint32_t)len;
+            cnt_row[(size_t)d * kRecPerBlock + j * rs] = (uint32_t)len;
         }
         ++d;
     }
@@ -712,22 +712,27 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_sizes_g(const RecArgs a) {
     const uint32_t t0 = threadIdx.x * kRecPerThread;
     bool dead = false;
     if (!a.ncond) {
+        // thread t walks records rb + t + 256 j: each length-word load of a
+        // wave covers 64 consecutive records, so neighbouring records' words
+        // share cache lines inside one instruction (one line fetch each)
+        const uint32_t t = threadIdx.x;
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j)
-            for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
-        const uint64_t r0 = rb + t0;
-        const uint32_t nj = r0 < a.n ? (uint32_t)(a.n - r0 < (uint64_t)kRecPerThread ? a.n - r0 : (uint64_t)kRecPerThread)
+            for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t + j * kRecThreads] = 0;
+        const uint64_t r0 = rb + t;
+        const uint32_t nj = r0 < a.n ? (uint32_t)((a.n - r0 + kRecThreads - 1) / kRecThreads < (uint64_t)kRecPerThread
+                                                  ? (a.n - r0 + kRecThreads - 1) / kRecThreads : (uint64_t)kRecPerThread)
                                      : 0u;
         uint32_t err[kRecPerThread], sub[kRecPerThread];
-        walk_counts_lockstep(a, r0, nj, scnt + t0, err, sub);
+        walk_counts_lockstep(a, r0, nj, scnt + t, err, sub, kRecThreads);
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {
             if (!dead && err[j]) {
-                atomicMin(a.errkey, err_key(r0 + j, sub[j], err[j]));
+                atomicMin(a.errkey, err_key(r0 + (uint64_t)j * kRecThreads, sub[j], err[j]));
                 dead = true;   // later records of this thread are past the error
             }
             if (dead)
-                for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
+                for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t + j * kRecThreads] = 0;
         }
     }
     for (int j = 0; a.ncond && j < kRecPerThread; ++j) {   // conditional schemas: serial walk
