@@ -342,7 +342,7 @@ class Workload:
         roof = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
-                "traffic": load_traffic(kname, self.n),
+                "traffic": load_traffic(self.cfg, self.framed, self.n),
                 "launches": launches, "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": per_launch}
         return roof, step_ms
 
@@ -355,15 +355,18 @@ class Workload:
                         decode_targets=False)
 
 
-def load_traffic(kernel, records):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary
-    (profiles/pmc_traffic.json, collected with separate FETCH_SIZE and
-    WRITE_SIZE passes, FETCH doubled per the gfx950 correction)."""
+def load_traffic(cfg, framed, records):
+    """HBM bytes per launch of the dominant kernel(s) from the committed
+    rocprofv3 --pmc summary (profiles/pmc_traffic.json, tools/pmc_summary.py:
+    separate FETCH_SIZE and WRITE_SIZE passes over bench.py, FETCH doubled per
+    the gfx950 correction; record configs average their encode and decode
+    place kernels, as `achieved` does), or None when the summary was taken on
+    another record count."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        e = d["kernels"][kernel]
+        e = d["configs"][f"{cfg}{'f' if framed else ''}"]
         if e.get("records") == records:
             return e["bytes_per_launch"]
     except (OSError, KeyError, ValueError):

@@ -6,7 +6,10 @@
 * FETCH_SIZE / WRITE_SIZE passes (separate runs, MI355X_MICROARCH.md §HBM):
   per-dispatch KB; FETCH doubled (gfx950 reports half of a wide streaming
   read), WRITE exact for 16-B streaming stores -> profiles/pmc_traffic.json
-  bytes_per_launch per kernel (median over dispatches).
+  bytes_per_launch per kernel and grid (median over dispatches), and per
+  bench.py config the bytes of its dominant launch (CONFIGS below: the place
+  kernels of one direction summed, encode and decode averaged, as bench.py's
+  roofline `achieved` averages their launches).
 """
 import csv
 import json
@@ -29,6 +32,26 @@ def per_kernel(path, counter):
             continue
         out.setdefault(short(r["Kernel_Name"]), []).append(float(r["Counter_Value"]))
     return out
+
+
+# bench.py config -> (records, encode kernels, decode kernels) as (name, grid)
+CONFIGS = {
+    "2": (67108864, [("k_stream_bswap", "134217728")], [("k_stream_bswap", "134217728")]),
+    "2f": (67108864, [("k_stream_framed_enc_lean", "150994944")], [("k_stream_framed_dec_lean", "134217728")]),
+    "3": (16777216, [("k_enc_place_g", "4194304"), ("k_enc_payload", "1073741824")],
+          [("k_dec_place_g", "4194304"), ("k_dec_payload", "1073741824")]),
+    "4": (33554432, [("k_enc_stage", "8388608"), ("k_enc_place_g", "8388608")],
+          [("k_dec_stage", "8388608"), ("k_dec_place_g", "8388608")]),
+}
+
+
+def by_grid(path, counter):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        if "xdrg::" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
+            continue
+        out.setdefault((short(r["Kernel_Name"]).split("<")[0], r["Grid_Size"]), []).append(float(r["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in out.items()}
 
 
 def main():
@@ -60,6 +83,23 @@ def main():
                                 "fetch_kb_raw": fkb, "write_kb": wkb,
                                 "bytes_per_launch": int(round((2 * fkb + wkb) * 1024)),
                                 "dispatches": len(fe[k])}
+    fg = by_grid(os.path.join(fetch, "run_counter_collection.csv"), "FETCH_SIZE")
+    wg = by_grid(os.path.join(write, "run_counter_collection.csv"), "WRITE_SIZE")
+    doc["configs"] = {}
+    for key, (recs, enc, dec) in CONFIGS.items():
+        sides = []
+        for ks in (enc, dec):
+            if not all(k in fg and k in wg for k in ks):
+                break
+            f_b = sum(2 * fg[k] * 1024 for k in ks)
+            w_b = sum(wg[k] * 1024 for k in ks)
+            sides.append((f_b, w_b))
+        if len(sides) == 2:
+            doc["configs"][key] = {"records": recs, "tag": tag, "encode": [k[0] for k in enc],
+                                   "decode": [k[0] for k in dec],
+                                   "fetch_bytes": [int(x[0]) for x in sides],
+                                   "write_bytes": [int(x[1]) for x in sides],
+                                   "bytes_per_launch": int(round(sum(x[0] + x[1] for x in sides) / 2))}
     with open(path, "w") as f:
         json.dump(doc, f, indent=1)
         f.write("\n")
