@@ -1393,14 +1393,22 @@ __device__ uint32_t payload_rec_word(const RecArgs &a, uint64_t r, uint64_t o, u
 // lines are shared with the neighbouring records, whose waves run alongside
 // and complete them in L2).  One pass over each line: the group kernel only
 // hands over the payload positions (pay_pos).
-template <uint32_t LPR, bool NT, bool NTS = NT>
+template <uint32_t LPR, bool NT, bool NTS = NT, bool H = true>
 __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
     if (r >= a.n) return;
     const VField &f = a.f[a.dyn_idx[a.payk - 1]];
-    // every metadata load issued together, before the checks that use them
-    const uint64_t total = a.totals[0], e0 = f.offsets[r], e1 = f.offsets[r + 1], pp = a.pay_pos[r];
-    const bool mine = payload_block(a, r, false);
-    if (total > a.xdr_cap || !mine) return;
+    // H: every metadata load issued together, before the checks that use them
+    // (else the checks first; tuning key 24 A/Bs the two in one run)
+    uint64_t total, e0, e1, pp;
+    if (H) {
+        total = a.totals[0]; e0 = f.offsets[r]; e1 = f.offsets[r + 1]; pp = a.pay_pos[r];
+        const bool mine = payload_block(a, r, false);
+        if (total > a.xdr_cap || !mine) return;
+    } else {
+        total = a.totals[0];
+        if (total > a.xdr_cap || !payload_block(a, r, false)) return;
+        e0 = f.offsets[r]; e1 = f.offsets[r + 1]; pp = a.pay_pos[r];
+    }
     const uint64_t cnt = e1 - e0;
     const uint64_t R = pp - a.pay_fb;   // record start
     const uint64_t P = cnt + pad4(cnt), size = a.fixed_xdr + 4 + P;
@@ -1439,20 +1447,28 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
         *(uint32_t *)(a.xdr + R + 4 * wi) = payload_rec_word(a, r, 4 * wi, size, src, cnt);
     }
 }
-template <uint32_t LPR, bool NT, bool NTS = NT>   // lanes per record; grid-strided; NT: nontemporal loads, NTS: stores
+template <uint32_t LPR, bool NT, bool NTS = NT, bool H = true>   // lanes per record; grid-strided; NT: nontemporal loads, NTS: stores; H: hoisted metadata loads
 __global__ __launch_bounds__(256) void k_enc_payload(const RecArgs a) {
     const uint64_t step = (uint64_t)gridDim.x * (256 / LPR);
     for (uint64_t r = (uint64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; r < a.n; r += step)
-        enc_payload_rec<LPR, NT, NTS>(a, r);
+        enc_payload_rec<LPR, NT, NTS, H>(a, r);
 }
-template <uint32_t LPR, bool NT>
+template <uint32_t LPR, bool NT, bool H = true>
 __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
     if (r >= a.n) return;
     const uint32_t d = a.payk - 1;
     const VField &f = a.f[a.dyn_idx[d]];
-    // metadata loads issued together, before the checks (one round trip ahead of the data)
-    const uint64_t pos = a.pay_pos[r], cnt = a.rec_cnt[(uint64_t)d * a.n + r], o = f.offsets[r];
-    if (pos == ~0ull || !payload_block(a, r, true)) return;
+    // H: metadata loads issued together, before the checks (one round trip ahead of the data)
+    uint64_t pos, cnt, o;
+    if (H) {
+        pos = a.pay_pos[r]; cnt = a.rec_cnt[(uint64_t)d * a.n + r]; o = f.offsets[r];
+        if (pos == ~0ull || !payload_block(a, r, true)) return;
+    } else {
+        if (!payload_block(a, r, true)) return;
+        pos = a.pay_pos[r];
+        if (pos == ~0ull) return;
+        cnt = a.rec_cnt[(uint64_t)d * a.n + r]; o = f.offsets[r];
+    }
     const uint8_t *src = a.xdr + pos + 4;
     uint8_t *dst = f.data + o;
     const uint32_t lane = threadIdx.x % LPR;
@@ -1483,11 +1499,11 @@ __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
         }
     }
 }
-template <uint32_t LPR, bool NT>   // lanes per record: 64 (a wave) or 256 (the block); grid-strided; NT: nontemporal
+template <uint32_t LPR, bool NT, bool H = true>   // lanes per record: 64 (a wave) or 256 (the block); grid-strided; NT: nontemporal
 __global__ __launch_bounds__(256) void k_dec_payload(const RecArgs a) {
     const uint64_t step = (uint64_t)gridDim.x * (256 / LPR);
     for (uint64_t r = (uint64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; r < a.n; r += step)
-        dec_payload_rec<LPR, NT>(a, r);
+        dec_payload_rec<LPR, NT, H>(a, r);
 }
 
 // ===========================================================================
@@ -2747,6 +2763,15 @@ int launch_scan_rows(uint64_t *sums, uint64_t nblocks, uint64_t *totals, uint32_
     return (int)hipGetLastError();
 }
 
+static void launch_enc_payload(int hoist, dim3 grid, hipStream_t st, const RecArgs &a) {
+    if (hoist) hipLaunchKernelGGL((k_enc_payload<64, true, true, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_enc_payload<64, true, true, false>), grid, dim3(256), 0, st, a);
+}
+static void launch_dec_payload(int hoist, dim3 grid, hipStream_t st, const RecArgs &a) {
+    if (hoist) hipLaunchKernelGGL((k_dec_payload<64, true, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_dec_payload<64, true, false>), grid, dim3(256), 0, st, a);
+}
+
 int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stream) {
     RecArgs a = args;
     a.force_g = t.force_g;
@@ -2789,12 +2814,12 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
             hipLaunchKernelGGL(k_enc_stage, dim3(nb), dim3(kRecThreads),
                                enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             if (a.big_rec) launch_ur<EncG>(t.enc_u, t.enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
-            if (a.big_rec && pay) hipLaunchKernelGGL((k_enc_payload<64, true>), pgrid, dim3(256), 0, st, a);
+            if (a.big_rec && pay) launch_enc_payload(t.pay_hoist, pgrid, st, a);
         } else if (lane || (grp && t.rec == 3)) {
             hipLaunchKernelGGL(k_enc_lane, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
             launch_ur<EncG>(t.enc_u, t.enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
-            if (pay) hipLaunchKernelGGL((k_enc_payload<64, true>), pgrid, dim3(256), 0, st, a);
+            if (pay) launch_enc_payload(t.pay_hoist, pgrid, st, a);
         }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
@@ -2823,12 +2848,12 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
             else hipLaunchKernelGGL(k_dec_stage<false>, dim3(nb), dim3(kRecThreads),
                                     dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             if (a.big_rec) launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
-            if (a.big_rec && pay) hipLaunchKernelGGL((k_dec_payload<64, true>), pgrid, dim3(256), 0, st, a);
+            if (a.big_rec && pay) launch_dec_payload(t.pay_hoist, pgrid, st, a);
         } else if (lane || (grp && t.rec == 3)) {
             hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
             launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
-            if (pay) hipLaunchKernelGGL((k_dec_payload<64, true>), pgrid, dim3(256), 0, st, a);
+            if (pay) launch_dec_payload(t.pay_hoist, pgrid, st, a);
         }
         else hipLaunchKernelGGL(k_dec_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;

@@ -169,6 +169,8 @@ struct Tuning {
     int32_t words = 2;              // key 16: fixed 4-byte-word schemas: 2 LDS-staged, 1 lane per record, 0 word-map
     int32_t framed = 2;             // key 14: record-marked AoS decode: 2 lean, 1 wave-LDS transpose
     int32_t rec = 4;                // key 9: record path: 4 staged sub-batches, 0 group per record, 3 lane per record
+    int32_t pay_hoist = 1;          // key 24: payload kernels: 1 metadata loads issued before the block
+                                    // checks, 0 checks first (A/B)
     int32_t payload = 1;            // key 18: one dynamic byte field on group-kernel blocks: 1 payload kernels, 0 in place
     int32_t dec_lb = 0;             // key 19: staged record-path decode: 1 counts walked in the place kernel
                                     // (decoupled look-back), 0 separate sizes walk + scan kernels

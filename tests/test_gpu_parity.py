@@ -407,14 +407,17 @@ def test_cfg2_full_size_roundtrip(gpu_ctx):
 
 
 # ---- big records (blocks averaging >= 1 KiB: the group kernels) and mixed blocks
-@pytest.fixture(params=[1, 0], ids=["pay_wave_nt", "pay_off"])
+@pytest.fixture(params=[(1, 1), (1, 0), (0, 1)], ids=["pay_wave_nt", "pay_checks_first", "pay_off"])
 def payload(request, gpu_ctx):
     """Payload kernels for a single dynamic byte field on the group kernels'
-    blocks (kernels_rec.hip k_enc/dec_payload, tuning key 18), or the group
-    kernels moving it in place."""
-    gpu_ctx.tune(18, request.param)
+    blocks (kernels_rec.hip k_enc/dec_payload, tuning key 18; key 24 = 0 their
+    block checks before the metadata loads), or the group kernels moving it
+    in place."""
+    gpu_ctx.tune(18, request.param[0])
+    gpu_ctx.tune(24, request.param[1])
     yield request.param
     gpu_ctx.tune(18, 1)
+    gpu_ctx.tune(24, 1)
 
 
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
