@@ -590,53 +590,88 @@ def cpu_baseline(budget_s):
 
 
 def host_inclusive(ctx, sch, n):
-    """H2D + encode + D2H, then H2D + decode + D2H, from pinned host buffers,
-    pipelined in chunks over two streams (the path starts and ends in host
-    NIO buffers)."""
+    """Both directions of a server at once, from pinned host buffers: replies
+    (native records H2D -> encode -> XDR D2H) and requests (received XDR H2D
+    -> decode -> native D2H), chunk by chunk on their own streams, so the
+    PCIe link carries H2D and D2H traffic concurrently (full duplex).  The
+    request stream is the records' own encoding, made before timing; both
+    outputs are checked."""
     import torch
     from oncrpc4j_amd.columns import aos_columns
     rec_bytes = 32
     nat_h = torch.randint(-2**31, 2**31 - 1, (n, 8), dtype=torch.int32).pin_memory()
-    xdr_h = torch.empty(n * rec_bytes, dtype=torch.uint8).pin_memory()
+    xdr_h = torch.empty(n * rec_bytes, dtype=torch.uint8).pin_memory()      # replies out
+    req_h = torch.empty(n * rec_bytes, dtype=torch.uint8).pin_memory()      # requests in
     back_h = torch.empty_like(nat_h).pin_memory()
     chunk = 4 << 20
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    bufs = [(torch.empty((chunk, 8), dtype=torch.int32, device="cuda"),
-             torch.empty(chunk * rec_bytes, dtype=torch.uint8, device="cuda")) for _ in streams]
+    nslot = 2                                                               # chunks in flight per direction
+    enc_s = [torch.cuda.Stream() for _ in range(nslot)]
+    dec_s = [torch.cuda.Stream() for _ in range(nslot)]
+    enc_b = [(torch.empty((chunk, 8), dtype=torch.int32, device="cuda"),
+              torch.empty(chunk * rec_bytes, dtype=torch.uint8, device="cuda")) for _ in range(nslot)]
+    dec_b = [(torch.empty((chunk, 8), dtype=torch.int32, device="cuda"),
+              torch.empty(chunk * rec_bytes, dtype=torch.uint8, device="cuda")) for _ in range(nslot)]
     fields = sch.fields
     offs = [4 * k for k in range(8)]
 
+    def enc_chunk(i, lo, m, out_h):
+        s, (dn, dx) = enc_s[i % nslot], enc_b[i % nslot]
+        with torch.cuda.stream(s):
+            dn[:m].copy_(nat_h[lo:lo + m], non_blocking=True)
+            ctx.set_stream(s)
+            ctx.encode(sch, aos_columns(fields, dn.data_ptr(), 32, offs), m, dx, m * rec_bytes, async_=True)
+            out_h[lo * rec_bytes:(lo + m) * rec_bytes].copy_(dx[:m * rec_bytes], non_blocking=True)
+
+    def dec_chunk(i, lo, m):
+        s, (dn, dx) = dec_s[i % nslot], dec_b[i % nslot]
+        with torch.cuda.stream(s):
+            dx[:m * rec_bytes].copy_(req_h[lo * rec_bytes:(lo + m) * rec_bytes], non_blocking=True)
+            ctx.set_stream(s)
+            ctx.decode(sch, dx, m * rec_bytes, m, aos_columns(fields, dn.data_ptr(), 32, offs), async_=True)
+            back_h[lo:lo + m].copy_(dn[:m], non_blocking=True)
+
+    chunks = [(i, lo, min(chunk, n - lo)) for i, lo in enumerate(range(0, n, chunk))]
+    for i, lo, m in chunks:   # the request stream (what a peer would send)
+        enc_chunk(i, lo, m, req_h)
+    torch.cuda.synchronize()
+
     def run():
-        for i, lo in enumerate(range(0, n, chunk)):
-            m = min(chunk, n - lo)
-            s = streams[i & 1]
-            dn, dx = bufs[i & 1]
-            with torch.cuda.stream(s):
-                dn[:m].copy_(nat_h[lo:lo + m], non_blocking=True)
-                ctx.set_stream(s)
-                ctx.encode(sch, aos_columns(fields, dn.data_ptr(), 32, offs), m, dx, m * rec_bytes,
-                           async_=True)
-                xdr_h[lo * rec_bytes:(lo + m) * rec_bytes].copy_(dx[:m * rec_bytes], non_blocking=True)
-        for i, lo in enumerate(range(0, n, chunk)):
-            m = min(chunk, n - lo)
-            s = streams[i & 1]
-            dn, dx = bufs[i & 1]
-            with torch.cuda.stream(s):
-                dx[:m * rec_bytes].copy_(xdr_h[lo * rec_bytes:(lo + m) * rec_bytes], non_blocking=True)
-                ctx.set_stream(s)
-                ctx.decode(sch, dx, m * rec_bytes, m, aos_columns(fields, dn.data_ptr(), 32, offs),
-                           async_=True)
-                back_h[lo:lo + m].copy_(dn[:m], non_blocking=True)
+        for i, lo, m in chunks:
+            enc_chunk(i, lo, m, xdr_h)
+            dec_chunk(i, lo, m)
         torch.cuda.synchronize()
-    run()
-    t0 = time.perf_counter()
-    run()
-    dt = time.perf_counter() - t0
-    ok = torch.equal(back_h, nat_h)
+    def run_mapped():
+        # the kernels read and write the pinned host buffers themselves (mapped
+        # host memory over PCIe): encode and decode run at once on two streams
+        with torch.cuda.stream(enc_s[0]):
+            ctx.set_stream(enc_s[0])
+            ctx.encode(sch, aos_columns(fields, nat_h.data_ptr(), 32, offs), n, xdr_h.data_ptr(), n * rec_bytes,
+                       async_=True)
+        with torch.cuda.stream(dec_s[0]):
+            ctx.set_stream(dec_s[0])
+            ctx.decode(sch, req_h.data_ptr(), n * rec_bytes, n, aos_columns(fields, back_h.data_ptr(), 32, offs),
+                       async_=True)
+        torch.cuda.synchronize()
+
+    res = {}
+    for name, fn in (("staged", run), ("mapped", run_mapped)):
+        back_h.zero_()
+        xdr_h.zero_()
+        fn()
+        t0 = time.perf_counter()
+        fn()
+        dt = time.perf_counter() - t0
+        ok = bool(torch.equal(back_h, nat_h)) and bool(torch.equal(xdr_h, req_h))
+        res[name] = {"GiB_s": round(n * 128 / dt / GIB, 3), "ms": round(dt * 1e3, 3),
+                     "pcie_GBps": round(4 * n * 32 / dt / 1e9, 2), "roundtrip_ok": ok}
     ctx.set_stream(torch.cuda.current_stream())
-    return {"value": round(n * 128 / dt / GIB, 3), "unit": "GiB/s",
-            "ms": round(dt * 1e3, 3), "records": n, "pcie_bytes": 4 * n * 32, "roundtrip_ok": ok,
-            "method": "pinned host, 4 Mi-record chunks, 2 streams, H2D/encode/D2H then H2D/decode/D2H"}
+    best = max((k for k in res if res[k]["roundtrip_ok"]), key=lambda k: res[k]["GiB_s"], default="staged")
+    return {"value": res[best]["GiB_s"], "unit": "GiB/s", "ms": res[best]["ms"], "records": n,
+            "pcie_bytes": 4 * n * 32, "pcie_GBps": res[best]["pcie_GBps"],
+            "roundtrip_ok": all(r["roundtrip_ok"] for r in res.values()), "best": best, "legs": res,
+            "method": "pinned host buffers; replies (native -> XDR) and requests (XDR -> native) at once. "
+                      "staged: 4 Mi-record chunks H2D / kernel / D2H on 2 + 2 streams; mapped: the kernels "
+                      "read and write the pinned buffers over PCIe on 2 streams"}
 
 
 # ---------------------------------------------------------------------------
