@@ -2104,7 +2104,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
 // version held it at four)
 __host__ __device__ constexpr size_t dec_stage_meta(uint32_t nd) {
     return ((size_t)(kRecPerBlock + 1) * 4 + (size_t)nd * (kRecPerBlock + 1) * 4 + (size_t)kRecPerBlock +
-            15) & ~(size_t)15;
+            16 + 15) & ~(size_t)15;   // + 16: the sweep's meta sentinels after supto (kSweepMetaPad words)
 }
 
 // Threads tid < nthr of the block decode fields [0, upto) of record r (the
@@ -2295,6 +2295,267 @@ __device__ __forceinline__ void dec_stage_batch(const RecArgs &a, const uint8_t 
     }
 }
 
+// ---- output-stationary sweep of a staged sub-batch (tuning key 20 = 2) --------
+// The dynamic fields of an error-free sub-batch are written by destination
+// chunks instead of by records: lane q writes the q-th 16-byte chunk of the
+// sub-batch's column range (aligned in global memory: one coalesced store per
+// lane, no partial lines) and composes it from the records whose bytes it
+// holds.  Before the stage barrier every record lane describes its record in
+// meta (start, end and tile offset: one word, read as consecutive words) and
+// writes its index into the chunk map for the chunks whose first element it
+// holds (about length / 16 byte stores per record).  A chunk reads its owner
+// from the map and the next records' words in one go, so the common chunks
+// (inside one record, or across one record edge) are straight-line code with
+// no dependent LDS round trips beyond map -> meta -> tile; the per-record
+// control flow of groups of lanes (what bounds dec_stage_batch, DESIGN.md
+// §5.3) is gone.  Byte fields: Xdr.java:760-763 / :797-800 (bytes, pad
+// skipped); int vectors: Xdr.java:607-613 (one bswap per element).
+#ifndef XDRG_SW_PROBE
+#define XDRG_SW_PROBE 0   // experiment builds only: parts of the sweep switched off (wrong output)
+#endif
+constexpr uint32_t kSweepMetaPad = 4;   // meta sentinels after the sub-batch's last record
+
+// LDS the sweep adds after the tile: the second field's meta and the chunk
+// map of both fields (their chunks together cover at most the tile's bytes).
+__host__ __device__ constexpr size_t dec_sweep_extra(uint32_t tile_bytes) {
+    return (((size_t)kRecThreads + kSweepMetaPad) * 4 + 15 & ~(size_t)15) +
+           (((size_t)(tile_bytes >> 4) + 32 + 15) & ~(size_t)15);
+}
+
+// Record lanes of the sub-batch [js, js + m): meta[t] = (start - x0) | tile
+// offset << 16 (elements relative to chunk 0, which starts at x0),
+// meta[m .. m + pad) = the end (empty records); map[c] = the record holding
+// chunk c's first element, for every c in [1, nq) (chunk 0: record 0 or the
+// first non-empty one after it).
+template <uint32_t RS>
+__device__ __forceinline__ void sweep_build(uint32_t *meta, uint8_t *map, const uint32_t *rel,
+                                            const uint32_t *sstart, const uint32_t *snrel,
+                                            const uint32_t (&xs)[kMaxDynLds], uint32_t d, int32_t tb, int32_t x0,
+                                            uint32_t cs, uint32_t js, uint32_t m, uint32_t nq) {
+    const uint32_t t = threadIdx.x;
+    if (t >= m) return;
+    const uint32_t j = js + t;
+    const uint32_t lo = (uint32_t)((int32_t)rel[j] - x0), hi = (uint32_t)((int32_t)rel[j + 1] - x0);
+    const uint32_t T = (uint32_t)(tb + (int32_t)(sstart[j] + dyn_before_xs(xs, snrel, j, d, RS)));
+    meta[t] = lo | T << 16;
+    if (t + 1 == m)
+#pragma unroll
+        for (uint32_t k = 0; k < kSweepMetaPad; ++k) meta[m + k] = hi;
+    const uint32_t r = (1u << cs) - 1;
+    const uint32_t c1 = min((hi + r) >> cs, nq);
+    for (uint32_t c = (lo + r) >> cs; c < c1; ++c) map[c] = (uint8_t)t;
+}
+
+// Byte mask of bytes [lo, hi) (clamped to 0..4) of a dword.
+__device__ __forceinline__ uint32_t byte_mask(int32_t lo, int32_t hi) {
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > 4 ? 4 : hi;
+    return hi > lo ? (uint32_t)((1ull << (8 * hi)) - (1ull << (8 * lo))) : 0u;
+}
+
+// Bytes [lo, hi) of the aligned 16-byte chunk at g (g + 4 k: dword k = v[k]),
+// by whole dwords where a dword is covered and byte stores at the ends.
+__device__ __forceinline__ void store_chunk_part(uint8_t *g, const uint32_t (&v)[4], int32_t lo, int32_t hi) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int32_t b0 = lo - 4 * k < 0 ? 0 : lo - 4 * k, b1 = hi - 4 * k > 4 ? 4 : hi - 4 * k;
+        if (b1 <= b0) continue;
+        uint8_t *p = g + 4 * k;
+        if (b0 == 0 && b1 == 4) { *(uint32_t *)p = v[k]; continue; }
+        for (int32_t b = b0; b < b1; ++b) p[b] = (uint8_t)(v[k] >> (8 * b));
+    }
+}
+
+// The 16 tile bytes from tile offset w (any alignment; the tile's slack and
+// the meta region before it make every such window readable).
+__device__ __forceinline__ void tile16(const uint8_t *tile, int32_t w, uint32_t (&u)[4]) {
+    const uint32_t *p = (const uint32_t *)(tile + (w & ~3));
+    const uint32_t s = (uint32_t)w & 3u;
+    const uint32_t q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3], q4 = p[4];
+    u[0] = __builtin_amdgcn_alignbyte(q1, q0, s);
+    u[1] = __builtin_amdgcn_alignbyte(q2, q1, s);
+    u[2] = __builtin_amdgcn_alignbyte(q3, q2, s);
+    u[3] = __builtin_amdgcn_alignbyte(q4, q3, s);
+}
+
+// Byte field: col = the column at block-relative element 0, chunk q = bytes
+// [x0 + 16 q, + 16) with col + x0 16-aligned, [xb, xe) = the sub-batch's bytes.
+__device__ __forceinline__ void sweep_bytes(uint8_t *col, const uint8_t *tile, const uint32_t *meta,
+                                            const uint8_t *map, int32_t x0, uint32_t nq, uint32_t m, int32_t xb,
+                                            int32_t xe) {
+    for (uint32_t q = threadIdx.x; q < nq; q += kRecThreads) {
+        const int32_t xr = 16 * (int32_t)q;   // chunk start relative to x0
+        uint32_t j = q ? map[q] : 0u;
+        uint32_t m0 = meta[j], m1 = meta[j + 1], m2 = meta[j + 2];
+        while ((int32_t)(m1 & 0xffffu) <= xr && j + 1 < m) {   // chunk 0: empty records first
+            ++j;
+            m0 = m1;
+            m1 = m2;
+            m2 = meta[j + 2];
+        }
+        // record A = j holds the chunk's first byte, record B = j + 1 starts where A ends
+        const int32_t loA = (int32_t)(m0 & 0xffffu), hiA = (int32_t)(m1 & 0xffffu), hiB = (int32_t)(m2 & 0xffffu);
+        uint32_t a[4], b[4], v[4];
+        tile16(tile, (int32_t)(m0 >> 16) + (xr - loA), a);
+        tile16(tile, (int32_t)(m1 >> 16) + (xr - hiA), b);
+        const int32_t sp = hiA - xr;   // chunk bytes [0, sp) from A, [sp, ..) from B
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int32_t o = sp - 4 * k;
+            const uint32_t mk = o >= 4 ? 0xffffffffu : (o <= 0 ? 0u : (1u << (8 * o)) - 1u);
+            v[k] = (a[k] & mk) | (b[k] & ~mk);
+        }
+        if (hiB < xr + 16) {   // a third record (or more) inside the chunk: B was short or empty
+            int32_t lo = hiB;
+            for (uint32_t jj = j + 2; lo < xr + 16 && jj < m; ++jj) {
+                const uint32_t e0 = meta[jj];
+                const int32_t hi = (int32_t)(meta[jj + 1] & 0xffffu);
+                if (hi > lo) {
+                    uint32_t c[4];
+                    tile16(tile, (int32_t)(e0 >> 16) + (xr - lo), c);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t mk = byte_mask(lo - xr - 4 * k, hi - xr - 4 * k);
+                        v[k] = (v[k] & ~mk) | (c[k] & mk);
+                    }
+                }
+                lo = hi;
+            }
+        }
+        const int32_t x = x0 + xr;
+        uint8_t *g = col + x;
+        if (x >= xb && x + 16 <= xe) {
+            u32x4n o;
+            o.x = v[0]; o.y = v[1]; o.z = v[2]; o.w = v[3];
+            *(u32x4n *)g = o;
+        } else {   // the sub-batch's first / last chunk: its neighbours own the other bytes
+            store_chunk_part(g, v, xb - x, xe - x);
+        }
+    }
+}
+
+// Word field (4-byte elements, XDR big-endian): chunk q = elements
+// [x0 + 4 q, + 4), col + x0 16-aligned; up to four records per chunk in
+// straight-line code.
+__device__ __forceinline__ void sweep_words(uint32_t *col, const uint8_t *tile, const uint32_t *meta,
+                                            const uint8_t *map, int32_t x0, uint32_t nq, uint32_t m, int32_t xb,
+                                            int32_t xe) {
+    for (uint32_t q = threadIdx.x; q < nq; q += kRecThreads) {
+        const int32_t xr = 4 * (int32_t)q;
+        uint32_t j = q ? map[q] : 0u;
+        uint32_t e[kSweepMetaPad + 1];
+#pragma unroll
+        for (uint32_t k = 0; k <= kSweepMetaPad; ++k) e[k] = meta[j + k];
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int32_t x = xr + k;
+            int32_t src = -1;
+#pragma unroll
+            for (int r = kSweepMetaPad - 1; r >= 0; --r) {   // the record among j .. j + 3 holding x
+                const int32_t lo = (int32_t)(e[r] & 0xffffu), hi = (int32_t)(e[r + 1] & 0xffffu);
+                if (x >= lo && x < hi) src = (int32_t)(e[r] >> 16) + 4 * (x - lo);
+            }
+            if (src < 0)   // beyond record j + 3 (short or empty records; rare)
+                for (uint32_t jj = j + kSweepMetaPad; jj < m; ++jj) {
+                    const uint32_t f0 = meta[jj];
+                    const int32_t lo = (int32_t)(f0 & 0xffffu), hi = (int32_t)(meta[jj + 1] & 0xffffu);
+                    if (x >= lo && x < hi) { src = (int32_t)(f0 >> 16) + 4 * (x - lo); break; }
+                    if (lo > x) break;
+                }
+            v[k] = src >= 0 ? bswap32r(*(const uint32_t *)(tile + src)) : 0u;
+        }
+        const int32_t x = x0 + xr;
+        uint32_t *g = col + x;
+        if (x >= xb && x + 4 <= xe) {
+            u32x4n o;
+            o.x = v[0]; o.y = v[1]; o.z = v[2]; o.w = v[3];
+            *(u32x4n *)g = o;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (x + k >= xb && x + k < xe) g[k] = v[k];
+        }
+    }
+}
+
+// Per dynamic field (at most two) of a sweep sub-batch: the column at
+// block-relative element 0, chunk 0's element x0, chunks, sub-batch range.
+struct SweepField {
+    uint8_t *col;
+    int32_t x0, xb, xe;
+    uint32_t nq, moff;   // chunks; the field's first entry in the shared chunk map
+};
+
+// Before the stage barrier: meta and chunk maps of the (at most two) dynamic
+// fields of records [js, je).  meta0 / meta1 hold kRecThreads + pad words.
+template <uint32_t RS>
+__device__ __forceinline__ void dec_sweep_prep(const RecArgs &a, int64_t lds0, uint32_t js, uint32_t je,
+                                               const uint32_t *sstart, const uint32_t *snrel,
+                                               const uint64_t *s_base, const uint32_t (&xs)[kMaxDynLds],
+                                               uint32_t *meta0, uint32_t *meta1, uint8_t *map,
+                                               SweepField *sf) {
+    uint32_t fpre = 0, d = 0, moff = 0;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind != XDRG_K_DYNAMIC) {
+            fpre += f.xbytes;
+            continue;
+        }
+        const uint32_t *rel = snrel + d * RS;
+        const bool bytes = f.xsz == 1;
+        SweepField s;
+        s.col = f.data + s_base[d] * (bytes ? 1 : 4);
+        const uint32_t cs = bytes ? 4u : 2u;   // log2 of a chunk's elements
+        s.xb = (int32_t)rel[js];
+        s.xe = (int32_t)rel[je];
+        s.x0 = bytes ? s.xb - (int32_t)((uintptr_t)(s.col + s.xb) & 15)
+                     : s.xb - (int32_t)(((uintptr_t)(s.col + 4 * (int64_t)s.xb) >> 2) & 3);
+        s.nq = s.xe > s.xb ? (uint32_t)(s.xe - s.x0 + (1 << cs) - 1) >> cs : 0u;
+        s.moff = moff;
+        sweep_build<RS>(d ? meta1 : meta0, map + moff, rel, sstart, snrel, xs, d, (int32_t)lds0 + (int32_t)fpre + 4,
+                        s.x0, cs, js, je - js, s.nq);
+        if (threadIdx.x == 0) sf[d] = s;   // read after the stage barrier
+        moff += s.nq;
+        ++d;
+    }
+}
+
+// After the stage barrier: every field of records [js, je), fixed fields by
+// groups of lanes per record as dec_stage_batch, dynamic fields by the sweep.
+template <uint32_t RS>
+__device__ __forceinline__ void dec_stage_sweep(const RecArgs &a, const uint8_t *tile, int64_t lds0, uint64_t rb,
+                                                uint32_t js, uint32_t je, const uint32_t *sstart,
+                                                const uint32_t *snrel, const uint32_t *meta0, const uint32_t *meta1,
+                                                const uint8_t *map, const SweepField *sf) {
+    const uint32_t tid = threadIdx.x, m = je - js;
+    uint32_t fpre = 0, d = 0;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind != XDRG_K_DYNAMIC) {
+            const uint32_t nw = f.xbytes >> 2;
+            if (nw && !(XDRG_SW_PROBE & 16)) {
+                const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
+                const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+                for (uint32_t j = js + tid / G; j < je; j += ng) {
+                    const uint32_t *w = (const uint32_t *)(tile + (lds0 + (int64_t)(sstart[j] + fpre +
+                                                                               dyn_before(a, snrel, j, d, RS))));
+                    for (uint32_t i = gl; i < nw; i += G) fixed_store(f, rb + j, 4 * i, w[i]);
+                }
+            }
+            fpre += f.xbytes;
+            continue;
+        }
+        const SweepField &s = sf[d];
+        if (f.xsz == 1) {
+            if (!(XDRG_SW_PROBE & 1)) sweep_bytes(s.col, tile, d ? meta1 : meta0, map + s.moff, s.x0, s.nq, m, s.xb, s.xe);
+        } else if (!(XDRG_SW_PROBE & 2)) {
+            sweep_words((uint32_t *)s.col, tile, d ? meta1 : meta0, map + s.moff, s.x0, s.nq, m, s.xb, s.xe);
+        }
+        ++d;
+    }
+}
+
 // As enc_fit, over the XDR stream range of records [js, js + 1 + t).
 __device__ __forceinline__ uint32_t dec_fit(const RecArgs &a, const uint32_t *sstart, uint64_t sb,
                                             const uint32_t *snrel, uint32_t js, uint32_t nlive) {
@@ -2419,8 +2680,8 @@ __device__ __forceinline__ void lb_resolve(const RecArgs &a, uint64_t b, const u
 #ifndef XDRG_DEC_STAGE_OCC
 #define XDRG_DEC_STAGE_OCC 5   // blocks per CU the register budget is sized for
 #endif
-template <bool LB>
-__global__ __launch_bounds__(kRecThreads, XDRG_DEC_STAGE_OCC) void k_dec_stage(const RecArgs a) {
+template <bool LB, bool SW>
+__device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;
     uint32_t *sstart = (uint32_t *)smem;
@@ -2548,6 +2809,14 @@ __global__ __launch_bounds__(kRecThreads, XDRG_DEC_STAGE_OCC) void k_dec_stage(c
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) full &= t0 + j >= nlive || upto[j] == a.nf;
     const bool lean = __syncthreads_and(full) && a.dec_lean;
+    // SW: the output-stationary sweep (key 20 = 2; the launcher checked the
+    // word columns' alignment and ndyn <= 2) for error-free blocks, record by
+    // record otherwise.  meta0 reuses supto (an error-free block's records all
+    // decode every field); meta1 and the chunk map follow the tile.
+    const bool sweep = SW && lean;
+    uint32_t *smeta1 = (uint32_t *)(tile + a.tile_bytes + kStageSlack);
+    uint8_t *smap = (uint8_t *)smeta1 + ((((size_t)kRecThreads + kSweepMetaPad) * 4 + 15) & ~(size_t)15);
+    __shared__ SweepField sf[2];
     // staging needs every record's fields to end where the next begins or
     // before (records in stream order); otherwise the block goes direct
     const uint32_t fx = a.fixed_xdr - (a.framed ? 4 : 0);   // fixed XDR bytes of the fields
@@ -2574,7 +2843,8 @@ __global__ __launch_bounds__(kRecThreads, XDRG_DEC_STAGE_OCC) void k_dec_stage(c
     uint32_t k1 = nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
     while (js < nlive) {
         if (k1 == 0) {   // too large for the tile: the whole block decodes record js
-            dec_record_block(a, rb + js, sb + sstart[js], supto[js], snrel, js, tid, kRecThreads);
+            // (an error-free block's every record decodes all fields; the sweep keeps its metadata in supto)
+            dec_record_block(a, rb + js, sb + sstart[js], sweep ? a.nf : supto[js], snrel, js, tid, kRecThreads);
             ++js;
             k1 = js < nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
             continue;
@@ -2584,13 +2854,30 @@ __global__ __launch_bounds__(kRecThreads, XDRG_DEC_STAGE_OCC) void k_dec_stage(c
         uint32_t cb[kMaxDynLds + 1] = {0, 0, 0, 0, 0};
         cb[1] = stage_chunks(in + sb + sstart[js], in + sb + sstart[je - 1] + fx + dyn_before(a, snrel, je - 1, a.ndyn),
                              &a0[0]);
-        stage_copy(tile, a0, cb, 1);
-        __syncthreads();
         const int64_t lds0 = -(int64_t)(a0[0] - (in + sb));   // tile offset of sstart value x: lds0 + x
-        dec_stage_batch<RS>(a, tile, lds0, rb, js, je, sstart, snrel, supto, s_base, xs, lean, tid, kRecThreads);
+        if (sweep && !(XDRG_SW_PROBE & 8))
+            dec_sweep_prep<RS>(a, lds0, js, je, sstart, snrel, s_base, xs, (uint32_t *)supto, smeta1, smap, sf);
+        if (!SW || !(XDRG_SW_PROBE & 32)) stage_copy(tile, a0, cb, 1);
+        __syncthreads();
+        if (!SW) dec_stage_batch<RS>(a, tile, lds0, rb, js, je, sstart, snrel, supto, s_base, xs, lean, tid, kRecThreads);
+        else if (sweep) dec_stage_sweep<RS>(a, tile, lds0, rb, js, je, sstart, snrel, (uint32_t *)supto, smeta1, smap, sf);
+        else
+            for (uint32_t j = js; j < je; ++j)
+                dec_record_block(a, rb + j, sb + sstart[j], supto[j], snrel, j, tid, kRecThreads);
         js = je;
         k1 = js < nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;   // its barrier ends the tile's use
     }
+}
+
+#ifndef XDRG_DEC_SWEEP_OCC
+#define XDRG_DEC_SWEEP_OCC 5   // blocks per CU the sweep kernel's register budget is sized for
+#endif
+template <bool LB>
+__global__ __launch_bounds__(kRecThreads, XDRG_DEC_STAGE_OCC) void k_dec_stage(const RecArgs a) {
+    dec_stage_body<LB, false>(a);
+}
+__global__ __launch_bounds__(kRecThreads, XDRG_DEC_SWEEP_OCC) void k_dec_sweep(const RecArgs a) {
+    dec_stage_body<false, true>(a);
 }
 
 // ---- one-pass staged decode: LDS-resident blocks ------------------------------
@@ -2843,10 +3130,17 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
                                dec_res_meta(a.ndyn) + t.res_tile + kStageSlack, st, ar);
         } else if (stage) {
             a.big_rec = t.big_rec;
-            if (lb) hipLaunchKernelGGL(k_dec_stage<true>, dim3(nb), dim3(kRecThreads),
-                                       dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
-            else hipLaunchKernelGGL(k_dec_stage<false>, dim3(nb), dim3(kRecThreads),
-                                    dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            const size_t lds = dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack +
+                               (t.dec_lean == 2 ? dec_sweep_extra(a.tile_bytes) : 0);
+            // the sweep writes word columns with 16-byte stores of 4-byte elements
+            bool sw = t.dec_lean == 2 && a.tile_bytes <= 32768 && a.ndyn <= 2;   // (16-bit tile offsets in meta)
+            for (uint32_t d = 0; d < a.ndyn && sw; ++d) {
+                const VField &f = a.f[a.dyn_idx[d]];
+                sw = f.xsz == 1 || (f.nsz == 4 && ((uintptr_t)f.data & 3) == 0);
+            }
+            if (lb) hipLaunchKernelGGL(k_dec_stage<true>, dim3(nb), dim3(kRecThreads), lds, st, a);
+            else if (sw) hipLaunchKernelGGL(k_dec_sweep, dim3(nb), dim3(kRecThreads), lds, st, a);
+            else hipLaunchKernelGGL(k_dec_stage<false>, dim3(nb), dim3(kRecThreads), lds, st, a);
             if (a.big_rec) launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
             if (a.big_rec && pay) launch_dec_payload(t.pay_hoist, pgrid, st, a);
         } else if (lane || (grp && t.rec == 3)) {

@@ -178,7 +178,8 @@ struct Tuning {
                                     // records decoded from their LDS-resident range (k_dec_res)
     uint32_t res_tile = 32768;      // key 23: k_dec_res, LDS bytes for a block's range
     int32_t dec_lean = 1;           // key 20: staged decode, byte fields of error-free blocks: 1 whole
-                                    // boundary dwords (dec_bytes_lean), 0 byte-stored record edges
+                                    // boundary dwords (dec_bytes_lean), 0 byte-stored record edges,
+                                    // 2 every dynamic field by the output-stationary sweep
     int32_t enc_u = 2, dec_u = 2;   // keys 4/5: group kernels, 16-byte chunks per lane in flight
     int32_t enc_r = 1, dec_r = 1;   // keys 10/11: group kernels, records per lane in flight
     uint32_t force_g = 0;           // key 6: lanes per record (0 = sized from the field)

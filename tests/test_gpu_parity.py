@@ -43,12 +43,15 @@ SCHEMAS = {
 # default), with key 19 = 1 the staged decode walking the counts itself
 # (decoupled look-back, no sizes / scan kernels), key 20 = 0 its byte
 # fields' record edges byte-stored instead of written as whole dwords,
+# key 20 = 2 every dynamic field of error-free blocks written by
+# destination chunks (the output-stationary sweep),
 # key 22 = 1 the one-pass decode of small records (blocks of 128 records
 # decoded from their LDS-resident stream range, k_dec_res);
 # key 9 = 0 group per record, 3 lane per record.  Tests taking `rec_kernel`
 # run under each.
 REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),), "staged_lb": ((9, 4), (19, 1)),
-               "staged_edges": ((9, 4), (20, 0)), "staged_res": ((9, 4), (22, 1))}
+               "staged_edges": ((9, 4), (20, 0)), "staged_res": ((9, 4), (22, 1)),
+               "staged_sweep": ((9, 4), (20, 2))}
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
@@ -269,7 +272,7 @@ def test_error_parity(gpu_ctx, rec_kernel, name, framed):
             assert g2[:3] == o2[:3], desc
 
 
-@pytest.mark.parametrize("lean", [1, 0], ids=["lean", "edges"])
+@pytest.mark.parametrize("lean", [1, 0, 2], ids=["lean", "edges", "sweep"])
 @pytest.mark.parametrize("tile", [1024, 4096])
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("name", ["cfg1_int_int_string", "cfg3_6xint_opaque", "cfg4_int_string_intvec",
