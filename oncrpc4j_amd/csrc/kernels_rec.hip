@@ -2680,7 +2680,7 @@ __device__ __forceinline__ void lb_resolve(const RecArgs &a, uint64_t b, const u
 #ifndef XDRG_DEC_STAGE_OCC
 #define XDRG_DEC_STAGE_OCC 5   // blocks per CU the register budget is sized for
 #endif
-template <bool LB, bool SW>
+template <bool SW>
 __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;
@@ -2690,70 +2690,18 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
     uint8_t *tile = smem + dec_stage_meta(a.ndyn);
     __shared__ uint32_t s_wide;
     __shared__ uint64_t s_base[kMaxDynLds];   // native offset of the block's first element, per dynamic field
-    __shared__ unsigned long long s_b, s_bad;
     const uint32_t tid = threadIdx.x, t0 = tid * kRecPerThread;
     const uint64_t nb = a.nblocks;
-    uint64_t bid = blockIdx.x, bad;
-    uint64_t agg[kMaxDynLds + 1] = {0, 0, 0, 0, 0};   // LB: the block's count totals
-    if (LB) {   // blocks take tickets in start order: every block waited on is running
-        if (tid == 0) {
-            s_b = atomicAdd(a.lb_ticket, 1ull);
-            s_bad = a.n;
-        }
-        __syncthreads();
-        bid = s_b;
-    } else if (a.big_rec && block_is_big_at(a, bid, true)) {
-        return;   // the group kernel's block
-    }
+    const uint64_t bid = blockIdx.x;
+    if (a.big_rec && block_is_big_at(a, bid, true)) return;   // the group kernel's block
     const uint64_t rb = bid * kRecPerBlock;
     const uint32_t nrec = (uint32_t)(a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0);
-    uint32_t *lcnt = (uint32_t *)tile;   // LB: walked counts [ndyn][kRecPerBlock], consumed before staging
     uint32_t xs[kMaxDynLds];             // XDR element size per dynamic field (1: padded bytes)
 #pragma unroll
     for (int e = 0; e < kMaxDynLds; ++e) xs[e] = (uint32_t)e < a.ndyn ? a.f[a.dyn_idx[e]].xsz : 0u;
-    if (LB) {
-        // ---- k_dec_sizes_g's walk (same checks, order and dead-record rule)
-#pragma unroll
-        for (int j = 0; j < kRecPerThread; ++j)
-            for (uint32_t d = 0; d < a.ndyn; ++d) lcnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
-        const uint32_t nj = t0 < nrec ? (nrec - t0 < (uint32_t)kRecPerThread ? nrec - t0 : (uint32_t)kRecPerThread) : 0u;
-        uint32_t err[kRecPerThread], sub[kRecPerThread];
-        walk_counts_lockstep(a, rb + t0, nj, lcnt + t0, err, sub);
-        bool dead = false;
-#pragma unroll
-        for (int j = 0; j < kRecPerThread; ++j) {
-            if (!dead && err[j]) {
-                atomicMin(a.errkey, err_key(rb + t0 + j, sub[j], err[j]));
-                atomicMin(&s_bad, (unsigned long long)(rb + t0 + j));
-                dead = true;
-            }
-            if (dead)
-                for (uint32_t d = 0; d < a.ndyn; ++d) lcnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
-        }
-#pragma unroll
-        for (int d = 0; d < kMaxDynLds; ++d) {
-            if ((uint32_t)d >= a.ndyn) continue;
-            uint64_t sv = 0;
-#pragma unroll
-            for (int j = 0; j < kRecPerThread; ++j) sv += lcnt[(size_t)d * kRecPerBlock + t0 + j];
-            agg[d] = block_sum(sv);   // its barriers also publish s_bad
-        }
-        if (tid < 64) lb_resolve(a, bid, agg, (uint64_t)s_bad, s_base, &s_bad);
-        __syncthreads();
-        bad = s_bad;
-        if (a.big_rec && block_is_big_at(a, bid, true)) {
-            // the group kernel's block: leave what k_dec_sizes_g + k_scan_rows would
-            for (uint32_t d = 0; d < a.ndyn; ++d)
-                for (uint32_t i = tid; i < nrec; i += kRecThreads)
-                    a.rec_cnt[(uint64_t)d * a.n + rb + i] = lcnt[(size_t)d * kRecPerBlock + i];
-            if (tid < a.ndyn) a.block_sums[(uint64_t)tid * nb + bid] = s_base[tid];
-            return;
-        }
-    } else {
-        const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
-        bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
-        if (tid < a.ndyn) s_base[tid] = a.block_sums[(uint64_t)tid * nb + bid];
-    }
+    const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
+    const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
+    if (tid < a.ndyn) s_base[tid] = a.block_sums[(uint64_t)tid * nb + bid];
     const uint32_t nlive = bad > rb ? (uint32_t)(bad - rb < (uint64_t)nrec ? bad - rb : (uint64_t)nrec) : 0;
     if (tid == 0) s_wide = 0;
     // ---- prologue: counts, native offsets (written to the columns), capacity, extents
@@ -2780,11 +2728,11 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {
             const uint64_t r = rb + t0 + j;
-            c[j] = t0 + j < nlive ? (LB ? lcnt[(size_t)d * kRecPerBlock + t0 + j] : a.rec_cnt[(uint64_t)d * a.n + r]) : 0u;
+            c[j] = t0 + j < nlive ? a.rec_cnt[(uint64_t)d * a.n + r] : 0u;
             s += c[j];
         }
         uint64_t btot;
-        const uint64_t base = LB ? s_base[d] : a.block_sums[(uint64_t)d * nb + bid];
+        const uint64_t base = a.block_sums[(uint64_t)d * nb + bid];
         uint64_t off = base + block_excl_scan(s, &btot);
         wide |= btot * (f.xsz == 1 ? 1 : f.nsz) >= (1ull << 31);
 #pragma unroll
@@ -2801,7 +2749,7 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
             off += c[j];
         }
         if (tid == kRecThreads - 1) snrel[d * RS + kRecPerBlock] = (uint32_t)(off - base);
-        if (!LB && tid == 0 && bid == 0) f.offsets[a.n] = a.totals[d];   // LB: lb_resolve
+        if (tid == 0 && bid == 0) f.offsets[a.n] = a.totals[d];
     }
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) supto[t0 + j] = (uint8_t)upto[j];
@@ -2870,14 +2818,14 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
 }
 
 #ifndef XDRG_DEC_SWEEP_OCC
-#define XDRG_DEC_SWEEP_OCC 5   // blocks per CU the sweep kernel's register budget is sized for
+#define XDRG_DEC_SWEEP_OCC 4   // blocks per CU the sweep kernel's register budget is sized for (5: 96 VGPRs
+                               // with spills, 3.71 ms vs 3.18 ms on config 4 at its best tile)
 #endif
-template <bool LB>
 __global__ __launch_bounds__(kRecThreads, XDRG_DEC_STAGE_OCC) void k_dec_stage(const RecArgs a) {
-    dec_stage_body<LB, false>(a);
+    dec_stage_body<false>(a);
 }
 __global__ __launch_bounds__(kRecThreads, XDRG_DEC_SWEEP_OCC) void k_dec_sweep(const RecArgs a) {
-    dec_stage_body<false, true>(a);
+    dec_stage_body<true>(a);
 }
 
 // ---- one-pass staged decode: LDS-resident blocks ------------------------------
@@ -3081,12 +3029,9 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     const bool pay = t.payload && a.pay_pos && a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1 &&
                      ((stage && t.big_rec) || (grp && !stage && t.rec == 0));
     a.payk = pay ? 1u : 0u;
-    // staged decode: the sizes walk runs inside the place kernel (its counts
-    // borrow the tile until staging starts)
-    const bool lb = stage && t.dec_lb && a.ndyn && (size_t)a.ndyn * kRecPerBlock * 4 <= a.tile_bytes;
     // one-pass LDS-resident decode: small records (the average block range fits the tile with margin)
     const uint64_t nb_res = (a.n + kResRec - 1) / kResRec;
-    const bool res = stage && !lb && t.dec_res && a.ndyn && a.n &&
+    const bool res = stage && t.dec_res && a.ndyn && a.n &&
                      (a.xdr_cap / a.n + 1) * kResRec * 5 / 4 <= (uint64_t)t.res_tile;
     const uint64_t pblk = (a.n + 3) / 4;   // a wave per record, 4 records per block
     const dim3 pgrid((unsigned)(pblk < (1u << 22) ? pblk : (1u << 22)));
@@ -3111,14 +3056,14 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SIZES:   // (the ticket word precedes the status words)
-        if (lb || res)
-            return (int)hipMemsetAsync(a.lb_ticket, 0, ((uint64_t)(a.ndyn + 1) * (res ? nb_res : nb) + 1) * 8, st);
+        if (res)
+            return (int)hipMemsetAsync(a.lb_ticket, 0, ((uint64_t)(a.ndyn + 1) * nb_res + 1) * 8, st);
         if (grp || lane) hipLaunchKernelGGL(k_dec_sizes_g, dim3(nb), dim3(kRecThreads),
                                     (size_t)a.ndyn * kRecPerBlock * 4, st, a);
         else hipLaunchKernelGGL(k_dec_sizes_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SCAN:
-        if (a.ndyn && !lb && !res)
+        if (a.ndyn && !res)
             hipLaunchKernelGGL(k_scan_rows, dim3(a.ndyn), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_DEC_PLACE:
@@ -3130,17 +3075,16 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
                                dec_res_meta(a.ndyn) + t.res_tile + kStageSlack, st, ar);
         } else if (stage) {
             a.big_rec = t.big_rec;
-            const size_t lds = dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack +
-                               (t.dec_lean == 2 ? dec_sweep_extra(a.tile_bytes) : 0);
             // the sweep writes word columns with 16-byte stores of 4-byte elements
-            bool sw = t.dec_lean == 2 && a.tile_bytes <= 32768 && a.ndyn <= 2;   // (16-bit tile offsets in meta)
+            bool sw = t.dec_lean == 2 && t.sweep_tile <= 32768 && a.ndyn <= 2;   // (16-bit tile offsets in meta)
             for (uint32_t d = 0; d < a.ndyn && sw; ++d) {
                 const VField &f = a.f[a.dyn_idx[d]];
                 sw = f.xsz == 1 || (f.nsz == 4 && ((uintptr_t)f.data & 3) == 0);
             }
-            if (lb) hipLaunchKernelGGL(k_dec_stage<true>, dim3(nb), dim3(kRecThreads), lds, st, a);
-            else if (sw) hipLaunchKernelGGL(k_dec_sweep, dim3(nb), dim3(kRecThreads), lds, st, a);
-            else hipLaunchKernelGGL(k_dec_stage<false>, dim3(nb), dim3(kRecThreads), lds, st, a);
+            if (sw) a.tile_bytes = t.sweep_tile;
+            const size_t lds = dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack + (sw ? dec_sweep_extra(a.tile_bytes) : 0);
+            if (sw) hipLaunchKernelGGL(k_dec_sweep, dim3(nb), dim3(kRecThreads), lds, st, a);
+            else hipLaunchKernelGGL(k_dec_stage, dim3(nb), dim3(kRecThreads), lds, st, a);
             if (a.big_rec) launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
             if (a.big_rec && pay) launch_dec_payload(t.pay_hoist, pgrid, st, a);
         } else if (lane || (grp && t.rec == 3)) {

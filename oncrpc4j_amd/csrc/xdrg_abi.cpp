@@ -326,10 +326,10 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 14: if (!in(1, 2)) return -1; t.framed = (int32_t)v; return 0;
     case 16: if (!in(0, 2)) return -1; t.words = (int32_t)v; return 0;
     case 18: if (!in(0, 1)) return -1; t.payload = (int32_t)v; return 0;
-    case 19: if (!in(0, 1)) return -1; t.dec_lb = (int32_t)v; return 0;
     case 20: if (!in(0, 2)) return -1; t.dec_lean = (int32_t)v; return 0;
     case 22: if (!in(0, 1)) return -1; t.dec_res = (int32_t)v; return 0;
     case 24: if (!in(0, 1)) return -1; t.pay_hoist = (int32_t)v; return 0;
+    case 25: if (!in(1024, 32768) || (v & 15)) return -1; t.sweep_tile = (uint32_t)v; return 0;
     case 23: if (!in(4096, 65536) || (v & 15)) return -1; t.res_tile = (uint32_t)v; return 0;
     default: return -1;
     }

@@ -172,12 +172,10 @@ struct Tuning {
     int32_t pay_hoist = 1;          // key 24: payload kernels: 1 metadata loads issued before the block
                                     // checks, 0 checks first (A/B)
     int32_t payload = 1;            // key 18: one dynamic byte field on group-kernel blocks: 1 payload kernels, 0 in place
-    int32_t dec_lb = 0;             // key 19: staged record-path decode: 1 counts walked in the place kernel
-                                    // (decoupled look-back), 0 separate sizes walk + scan kernels
     int32_t dec_res = 0;            // key 22: staged decode of small records: 1 one pass, blocks of 128
                                     // records decoded from their LDS-resident range (k_dec_res)
     uint32_t res_tile = 32768;      // key 23: k_dec_res, LDS bytes for a block's range
-    int32_t dec_lean = 1;           // key 20: staged decode, byte fields of error-free blocks: 1 whole
+    int32_t dec_lean = 2;           // key 20: staged decode, byte fields of error-free blocks: 1 whole
                                     // boundary dwords (dec_bytes_lean), 0 byte-stored record edges,
                                     // 2 every dynamic field by the output-stationary sweep
     int32_t enc_u = 2, dec_u = 2;   // keys 4/5: group kernels, 16-byte chunks per lane in flight
@@ -186,6 +184,7 @@ struct Tuning {
     uint32_t lane_bytes_enc = 32;   // keys 7/8: group sizing, XDR bytes per lane
     uint32_t lane_bytes_dec = 32;
     uint32_t tile_bytes = 16384;    // key 12: staged kernels, LDS tile per sub-batch
+    uint32_t sweep_tile = 21504;    // key 25: the sweep decode's LDS tile (k_dec_sweep, 4 blocks per CU)
     uint32_t big_rec = 1024;        // key 13: blocks averaging >= this many XDR bytes per record
                                     // take the group kernels (0 = never)
 };

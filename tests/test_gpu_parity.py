@@ -40,18 +40,18 @@ SCHEMAS = {
 
 # Record-path implementations (kernels_rec.hip launch_rec_phase), as tuning
 # (key, value) pairs: key 9 = 4 staged (sub-batches through an LDS tile, the
-# default), with key 19 = 1 the staged decode walking the counts itself
-# (decoupled look-back, no sizes / scan kernels), key 20 = 0 its byte
-# fields' record edges byte-stored instead of written as whole dwords,
-# key 20 = 2 every dynamic field of error-free blocks written by
-# destination chunks (the output-stationary sweep),
+# default), key 20 = 0 its byte fields' record edges byte-stored instead of
+# written as whole dwords,
+# key 20 = 1 the byte fields of error-free blocks written record by record
+# with whole boundary dwords instead of by the output-stationary sweep (the
+# default, 2),
 # key 22 = 1 the one-pass decode of small records (blocks of 128 records
 # decoded from their LDS-resident stream range, k_dec_res);
 # key 9 = 0 group per record, 3 lane per record.  Tests taking `rec_kernel`
 # run under each.
-REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),), "staged_lb": ((9, 4), (19, 1)),
+REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),),
                "staged_edges": ((9, 4), (20, 0)), "staged_res": ((9, 4), (22, 1)),
-               "staged_sweep": ((9, 4), (20, 2))}
+               "staged_lean": ((9, 4), (20, 1))}
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
@@ -289,6 +289,7 @@ def test_staged_tile_sizes(gpu_ctx, name, framed, tile, lean):
     assert rc == 0
     gpu_ctx.tune(9, 4)
     gpu_ctx.tune(12, tile)
+    gpu_ctx.tune(25, tile)   # the sweep decode's own tile
     gpu_ctx.tune(13, 0)   # every block staged (no split of large-record blocks to the group kernel)
     gpu_ctx.tune(20, lean)
     try:
