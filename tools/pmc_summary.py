@@ -40,9 +40,23 @@ CONFIGS = {
     "2f": (67108864, [("k_stream_framed_enc_lean", "150994944")], [("k_stream_framed_dec_lean", "134217728")]),
     "3": (16777216, [("k_enc_place_g", "4194304"), ("k_enc_payload", "1073741824")],
           [("k_dec_place_g", "4194304"), ("k_dec_payload", "1073741824")]),
-    "4": (33554432, [("k_enc_stage", "8388608"), ("k_enc_place_g", "8388608")],
-          [("k_dec_stage", "8388608"), ("k_dec_place_g", "8388608")]),
+    "4": (33554432, [("k_enc_sweep|k_enc_stage", "8388608"), ("k_enc_place_g", "8388608")],
+          [("k_dec_sweep|k_dec_stage", "8388608"), ("k_dec_place_g", "8388608")]),
 }
+# (a name "a|b" takes the first of the alternatives the profile holds: the
+# staged kernels' sweep variants replace them when the tuning selects them)
+
+
+def resolve(ks, table):
+    out = []
+    for name, grid in ks:
+        for alt in name.split("|"):
+            if (alt, grid) in table:
+                out.append((alt, grid))
+                break
+        else:
+            out.append((name, grid))
+    return out
 
 
 def by_grid(path, counter):
@@ -88,6 +102,7 @@ def main():
     doc["configs"] = {}
     for key, (recs, enc, dec) in CONFIGS.items():
         sides = []
+        enc, dec = resolve(enc, fg), resolve(dec, fg)
         for ks in (enc, dec):
             if not all(k in fg and k in wg for k in ks):
                 break
