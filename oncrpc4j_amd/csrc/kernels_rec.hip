@@ -2569,114 +2569,6 @@ __device__ __forceinline__ uint32_t dec_fit(const RecArgs &a, const uint32_t *ss
     return (uint32_t)__syncthreads_count(fits);
 }
 
-// ---- decoupled look-back: the staged decode with the sizes walk folded in ----
-// Each block walks its own records' length words (k_dec_sizes_g's checks),
-// publishes its count totals, and learns the native offset of its first
-// element per dynamic field from its predecessors: one status word per block
-// and word w (w < ndyn: counts of dynamic field w; w = ndyn: the first record
-// a walk check failed, a.n = none): flag in bits 62-63 (1 = the block's own
-// value, 2 = the inclusive prefix over blocks [0, b]: sum, or min for the
-// failed record) | value.  Flag and value share one 8-byte word, stored and
-// polled with agent-scope relaxed atomics (L2, not the CU's L1), a tagged
-// granule that needs no fence (MI355X_MICROARCH.md, inter-workgroup
-// visibility).  Blocks take tickets in start order, so every block waited on
-// is already running and publishes its own value without waiting.
-constexpr uint64_t kLbOwn = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = kLbOwn - 1;
-
-__device__ __forceinline__ void lb_put(uint64_t *p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t lb_get(const uint64_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o; o >>= 1) {
-        const uint64_t t = __shfl_xor(v, o, 64);
-        v = t < v ? t : v;
-    }
-    return v;
-}
-
-// Wave 0 of block b (totals agg, own first failing record lbad): publish,
-// look back over the predecessors 64 at a time down to the nearest inclusive
-// prefix, publish the block's inclusive prefix.  Leaves s_base[d] = the
-// exclusive prefix of field d's counts and *s_bad = the first failing record
-// over blocks [0, b]; the last block also writes the totals and each
-// column's offsets[n].
-__device__ __forceinline__ void lb_resolve(const RecArgs &a, uint64_t b, const uint64_t (&agg)[kMaxDynLds + 1], uint64_t lbad,
-                           uint64_t *s_base, unsigned long long *s_bad) {
-    const uint32_t lane = threadIdx.x & 63, nd = a.ndyn;
-    const uint64_t nb = a.nblocks;
-    uint64_t *st = a.lb_state;
-    if (lane == 0) {
-        const uint64_t fl = b ? kLbOwn : kLbIncl;
-#pragma unroll
-        for (int w = 0; w < kMaxDynLds; ++w)
-            if ((uint32_t)w < nd) lb_put(st + (uint64_t)w * nb + b, fl | agg[w]);
-        lb_put(st + (uint64_t)nd * nb + b, fl | lbad);
-    }
-    // Every word is its own chain: a predecessor may be seen with some words
-    // already inclusive and others still its own value.
-    uint64_t pre[kMaxDynLds + 1] = {0, 0, 0, 0, 0};
-    uint64_t pbad = a.n;
-    uint32_t done = 0;
-    const uint32_t all = (2u << nd) - 1;
-    int64_t p = (int64_t)b - 1 - (int64_t)lane;
-    while (b && done != all) {
-        uint64_t v[kMaxDynLds + 1];
-        for (;;) {
-            bool ready = true;
-#pragma unroll
-            for (int w = 0; w <= kMaxDynLds; ++w) {
-                if ((uint32_t)w > nd) continue;
-                const uint64_t x = p >= 0 ? lb_get(st + (uint64_t)w * nb + (uint64_t)p)
-                                          : (kLbIncl | ((uint32_t)w == nd ? a.n : 0));
-                v[w] = x;
-                ready = ready && (x >> 62) != 0;
-            }
-            if (__all(ready)) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-#pragma unroll
-        for (int w = 0; w <= kMaxDynLds; ++w) {
-            if ((uint32_t)w > nd || ((done >> w) & 1)) continue;
-            const uint64_t pm = __ballot((v[w] >> 62) == 2);
-            const uint32_t first = pm ? (uint32_t)__builtin_ctzll(pm) : 63u;   // nearest inclusive predecessor
-            const bool take = lane <= first;
-            const uint64_t x = v[w] & kLbVal;
-            if ((uint32_t)w < nd) {
-                pre[w] += wave_sum64(take ? x : 0);
-            } else {
-                const uint64_t m = wave_min64(take ? x : a.n);
-                pbad = m < pbad ? m : pbad;
-            }
-            if (pm) done |= 1u << w;
-        }
-        p -= 64;
-    }
-    if (lane == 0) {
-        const uint64_t bad = pbad < lbad ? pbad : lbad;
-#pragma unroll
-        for (int w = 0; w < kMaxDynLds; ++w) {
-            if ((uint32_t)w >= nd) continue;
-            if (b) lb_put(st + (uint64_t)w * nb + b, kLbIncl | (pre[w] + agg[w]));
-            s_base[w] = pre[w];
-            if (b + 1 == nb) {
-                a.totals[w] = pre[w] + agg[w];
-                a.f[a.dyn_idx[w]].offsets[a.n] = pre[w] + agg[w];
-            }
-        }
-        if (b) lb_put(st + (uint64_t)nd * nb + b, kLbIncl | bad);
-        *s_bad = bad;
-    }
-}
-
 #ifndef XDRG_DEC_STAGE_OCC
 #define XDRG_DEC_STAGE_OCC 5   // blocks per CU the register budget is sized for
 #endif
@@ -2828,155 +2720,6 @@ __global__ __launch_bounds__(kRecThreads, XDRG_DEC_SWEEP_OCC) void k_dec_sweep(c
     dec_stage_body<true>(a);
 }
 
-// ---- one-pass staged decode: LDS-resident blocks ------------------------------
-// Blocks of kResRec records whose XDR extents lie in one range of at most
-// tile_bytes (small-record batches; the launcher checks the average).  The
-// block stages the range once, walks its records' length words in LDS (the
-// checks and order of walk_counts), publishes its count totals and learns
-// its native offsets by decoupled look-back (lb_resolve), then decodes every
-// record from the same tile: the stream is read once, no sizes/scan kernels.
-// A block whose range does not fit walks from HBM and decodes record by
-// record (dec_record_block).
-__host__ __device__ constexpr size_t dec_res_meta(uint32_t nd) {
-    return ((size_t)(kResRec + 1) * 4 * (1 + nd) + kResRec + 15) & ~(size_t)15;
-}
-
-// walk_counts over a staged record whose XDR bytes [p, e) are at those tile
-// offsets; e_len = the record's extent length (the framed mark's check).
-__device__ __forceinline__ uint32_t walk_counts_tile(const RecArgs &a, const uint8_t *tile, uint32_t p, uint32_t e,
-                                                     uint32_t (&cnt)[kMaxDynLds], uint32_t *sub) {
-    *sub = 0;
-    if (a.framed) {
-        if (e - p < 4) return XDRG_E_SHORT;
-        const uint32_t m = bswap32r(tile_word(tile, p));
-        const uint64_t want_len = a.rec_in ? (uint64_t)(e - p - 4) : a.rec_stride - 4;
-        if (!(m & kLastFrag) || (uint64_t)(m & kSizeMask) != want_len) return XDRG_E_FRAME;
-        p += 4;
-    }
-    uint32_t d = 0;
-    for (uint32_t k = 0; k < a.nf; ++k) {
-        const VField &f = a.f[k];
-        *sub = 2 * k + 1;
-        if (f.kind != XDRG_K_DYNAMIC) {
-            if (e - p < f.xbytes) return XDRG_E_SHORT;
-            p += f.xbytes;
-            continue;
-        }
-        if (e - p < 4) return XDRG_E_SHORT;
-        const int32_t len = (int32_t)bswap32r(tile_word(tile, p));
-        p += 4;
-        uint64_t need;
-        if (f.xsz == 1) {
-            if (len == 0) need = 0;
-            else if (len < 0) return XDRG_E_CORRUPT;
-            else need = (uint64_t)len + pad4((uint64_t)len);
-        } else {
-            if (len < 0) return XDRG_E_CORRUPT;
-            need = (uint64_t)len * f.xsz;
-        }
-        if ((uint64_t)(e - p) < need) return XDRG_E_SHORT;
-        p += (uint32_t)need;
-        cnt[d++] = (uint32_t)len;
-    }
-    return 0;
-}
-
-__global__ __launch_bounds__(kRecThreads, 4) void k_dec_res(const RecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr uint32_t RS = kResRec + 1;
-    uint32_t *sstart = (uint32_t *)smem;
-    uint32_t *snrel = sstart + RS;
-    uint8_t *supto = (uint8_t *)(snrel + (size_t)a.ndyn * RS);
-    uint8_t *tile = smem + dec_res_meta(a.ndyn);
-    __shared__ uint64_t s_base[kMaxDynLds];
-    __shared__ unsigned long long s_b, s_bad;
-    __shared__ uint64_t s_range[2];
-    const uint32_t tid = threadIdx.x;
-    if (tid == 0) {   // blocks take tickets in start order: every block waited on is running
-        s_b = atomicAdd(a.lb_ticket, 1ull);
-        s_bad = a.n;
-    }
-    __syncthreads();
-    const uint64_t bid = s_b, rb = bid * kResRec;
-    const uint32_t nrec = (uint32_t)(a.n - rb < (uint64_t)kResRec ? a.n - rb : (uint64_t)kResRec);
-    uint32_t xs[kMaxDynLds];
-#pragma unroll
-    for (int e = 0; e < kMaxDynLds; ++e) xs[e] = (uint32_t)e < a.ndyn ? a.f[a.dyn_idx[e]].xsz : 0u;
-    // ---- extents; the block's range [x0, x1) and whether the tile holds it
-    const bool mine = tid < nrec;
-    const Extent ex = mine ? rec_extent(a, rb + tid) : Extent{0, 0};
-    if (tid == 0) s_range[0] = ex.a;
-    if (tid == nrec - 1) s_range[1] = ex.b;
-    __syncthreads();
-    const uint64_t x0 = s_range[0] & ~(uint64_t)15, x1 = s_range[1];
-    const bool inside = !mine || (ex.a >= x0 && ex.b <= x1);
-    const bool res = __syncthreads_and(inside) && x1 >= x0 && x1 - x0 <= a.tile_bytes;
-    if (res) {
-        const uint8_t *a0[kMaxDynLds] = {a.xdr + x0, nullptr, nullptr, nullptr};
-        const uint32_t cb[kMaxDynLds + 1] = {0, (uint32_t)((x1 - x0 + 15) >> 4), 0, 0, 0};
-        stage_copy(tile, a0, cb, 1);
-    }
-    __syncthreads();
-    // ---- walk
-    uint32_t cnt[kMaxDynLds] = {0, 0, 0, 0};
-    uint32_t err = 0, sub = 0;
-    if (mine) {
-        if (res) {
-            err = walk_counts_tile(a, tile, (uint32_t)(ex.a - x0), (uint32_t)(ex.b - x0), cnt, &sub);
-        } else {
-            uint64_t st, by;
-            err = walk_counts(a, rb + tid, cnt, &sub, &st, &by, 1);
-        }
-        if (err) {
-            atomicMin(a.errkey, err_key(rb + tid, sub, err));
-            atomicMin(&s_bad, (unsigned long long)(rb + tid));
-#pragma unroll
-            for (int d = 0; d < kMaxDynLds; ++d) cnt[d] = 0;
-        }
-    }
-    uint64_t agg[kMaxDynLds + 1] = {0, 0, 0, 0, 0};
-#pragma unroll
-    for (int d = 0; d < kMaxDynLds; ++d)
-        if ((uint32_t)d < a.ndyn) agg[d] = block_sum(cnt[d]);   // its barriers also publish s_bad
-    if (tid < 64) lb_resolve(a, bid, agg, (uint64_t)s_bad, s_base, &s_bad);
-    __syncthreads();
-    const uint64_t bad = s_bad;
-    const uint32_t nlive = bad > rb ? (uint32_t)(bad - rb < (uint64_t)nrec ? bad - rb : (uint64_t)nrec) : 0;
-    // ---- native offsets, capacity, record starts
-    const bool live = tid < nlive;
-    uint32_t upto = live ? a.nf : 0u;
-#pragma unroll
-    for (int d = 0; d < kMaxDynLds; ++d) {
-        if ((uint32_t)d >= a.ndyn) continue;
-        const uint32_t k = a.dyn_idx[d];
-        const VField &f = a.f[k];
-        const uint32_t c = live ? cnt[d] : 0u;
-        uint64_t btot;
-        const uint64_t rel = block_excl_scan(c, &btot);
-        const uint64_t off = s_base[d] + rel;
-        if (tid < RS) snrel[d * RS + tid] = (uint32_t)rel;   // [nrec] = the block's total
-        if (mine) {
-            f.offsets[rb + tid] = off;
-            if (live && off + c > f.cap) {   // native column too small
-                atomicMin(a.errkey, err_key(rb + tid, 2 * k + 2, XDRG_E_CAPACITY));
-                if (upto > k) upto = k;
-            }
-        }
-    }
-    const uint32_t fr = a.framed ? 4u : 0u;
-    if (mine) {
-        sstart[tid] = (uint32_t)(res ? ex.a + fr - x0 : 0u);
-        supto[tid] = (uint8_t)upto;
-    }
-    const bool lean = __syncthreads_and(!live || upto == a.nf) && a.dec_lean;
-    if (res) {
-        dec_stage_batch<RS>(a, tile, 0, rb, 0, nlive, sstart, snrel, supto, s_base, xs, lean, tid, kRecThreads);
-    } else {
-        for (uint32_t j = 0; j < nlive; ++j)
-            dec_record_block(a, rb + j, rec_extent(a, rb + j).a + fr, supto[j], snrel, j, tid, kRecThreads, RS);
-    }
-}
-
 // ===========================================================================
 // Launchers
 // ===========================================================================
@@ -3029,10 +2772,6 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     const bool pay = t.payload && a.pay_pos && a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1 &&
                      ((stage && t.big_rec) || (grp && !stage && t.rec == 0));
     a.payk = pay ? 1u : 0u;
-    // one-pass LDS-resident decode: small records (the average block range fits the tile with margin)
-    const uint64_t nb_res = (a.n + kResRec - 1) / kResRec;
-    const bool res = stage && t.dec_res && a.ndyn && a.n &&
-                     (a.xdr_cap / a.n + 1) * kResRec * 5 / 4 <= (uint64_t)t.res_tile;
     const uint64_t pblk = (a.n + 3) / 4;   // a wave per record, 4 records per block
     const dim3 pgrid((unsigned)(pblk < (1u << 22) ? pblk : (1u << 22)));
     switch (phase) {
@@ -3056,24 +2795,16 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SIZES:   // (the ticket word precedes the status words)
-        if (res)
-            return (int)hipMemsetAsync(a.lb_ticket, 0, ((uint64_t)(a.ndyn + 1) * nb_res + 1) * 8, st);
         if (grp || lane) hipLaunchKernelGGL(k_dec_sizes_g, dim3(nb), dim3(kRecThreads),
                                     (size_t)a.ndyn * kRecPerBlock * 4, st, a);
         else hipLaunchKernelGGL(k_dec_sizes_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SCAN:
-        if (a.ndyn && !res)
+        if (a.ndyn)
             hipLaunchKernelGGL(k_scan_rows, dim3(a.ndyn), dim3(1024), 0, st, a.block_sums, nb, a.totals);
         break;
     case REC_DEC_PLACE:
-        if (res) {
-            RecArgs ar = a;
-            ar.nblocks = nb_res;
-            ar.tile_bytes = t.res_tile;
-            hipLaunchKernelGGL(k_dec_res, dim3((unsigned)nb_res), dim3(kRecThreads),
-                               dec_res_meta(a.ndyn) + t.res_tile + kStageSlack, st, ar);
-        } else if (stage) {
+        if (stage) {
             a.big_rec = t.big_rec;
             // the sweep writes word columns with 16-byte stores of 4-byte elements
             bool sw = t.dec_lean == 2 && t.sweep_tile <= 32768 && a.ndyn <= 2;   // (16-bit tile offsets in meta)

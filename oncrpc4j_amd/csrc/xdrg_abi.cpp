@@ -327,10 +327,8 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 16: if (!in(0, 2)) return -1; t.words = (int32_t)v; return 0;
     case 18: if (!in(0, 1)) return -1; t.payload = (int32_t)v; return 0;
     case 20: if (!in(0, 2)) return -1; t.dec_lean = (int32_t)v; return 0;
-    case 22: if (!in(0, 1)) return -1; t.dec_res = (int32_t)v; return 0;
     case 24: if (!in(0, 1)) return -1; t.pay_hoist = (int32_t)v; return 0;
     case 25: if (!in(1024, 32768) || (v & 15)) return -1; t.sweep_tile = (uint32_t)v; return 0;
-    case 23: if (!in(4096, 65536) || (v & 15)) return -1; t.res_tile = (uint32_t)v; return 0;
     default: return -1;
     }
 }
@@ -590,17 +588,12 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
     const size_t cnt_words = (a.ndyn * n + 1) / 2;
     // | per-record payload positions u64 [n] (one dynamic byte field: k_enc/dec_payload)
     const size_t pay_words = (a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1) ? n : 0;
-    // | ticket | look-back status words [ndyn + 1][blocks] (staged decode; k_dec_res's blocks
-    // hold kResRec records, the others kRecPerBlock)
-    const size_t lb_words = (a.ndyn + 1) * ((n + kResRec - 1) / kResRec + 1) + 1;
-    int rc = ensure_ws(c, sums_words + cnt_words + pay_words + lb_words);
+    int rc = ensure_ws(c, sums_words + cnt_words + pay_words);
     if (rc) return rc;
     a.block_sums = c->d_ws;
     a.totals = c->d_ws + rows * a.nblocks;
     a.rec_cnt = (uint32_t *)(c->d_ws + sums_words);
     a.pay_pos = pay_words ? c->d_ws + sums_words + cnt_words : nullptr;
-    a.lb_ticket = (unsigned long long *)(c->d_ws + sums_words + cnt_words + pay_words);
-    a.lb_state = c->d_ws + sums_words + cnt_words + pay_words + 1;
     a.errkey = c->d_stat;
     return XDRG_OK;
 }

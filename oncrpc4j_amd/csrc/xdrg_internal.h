@@ -141,8 +141,6 @@ struct RecArgs {
     uint32_t pay_fb;           // payk: XDR bytes before that field in a record (mark + fixed fields)
     uint64_t *pay_pos;         // payk: per record, stream offset of that field's length word
                                // (decode: ~0 = not to be written)
-    uint64_t *lb_state;        // staged decode with look-back: [ndyn + 1][nblocks] status words
-    unsigned long long *lb_ticket;   // and the block ticket just before them (both zeroed before the launch)
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
     int32_t cvals[XDRG_MAX_CASES];  // case values of the conditional fields
@@ -172,9 +170,6 @@ struct Tuning {
     int32_t pay_hoist = 1;          // key 24: payload kernels: 1 metadata loads issued before the block
                                     // checks, 0 checks first (A/B)
     int32_t payload = 1;            // key 18: one dynamic byte field on group-kernel blocks: 1 payload kernels, 0 in place
-    int32_t dec_res = 0;            // key 22: staged decode of small records: 1 one pass, blocks of 128
-                                    // records decoded from their LDS-resident range (k_dec_res)
-    uint32_t res_tile = 32768;      // key 23: k_dec_res, LDS bytes for a block's range
     int32_t dec_lean = 2;           // key 20: staged decode, byte fields of error-free blocks: 1 whole
                                     // boundary dwords (dec_bytes_lean), 0 byte-stored record edges,
                                     // 2 every dynamic field by the output-stationary sweep
@@ -325,7 +320,6 @@ int launch_scan_rows(uint64_t *sums, uint64_t nblocks, uint64_t *totals, uint32_
 constexpr int kRecThreads = 256;   // record path: threads per block
 constexpr int kRecPerThread = 4;   // records per thread in the size/scan pass
 constexpr int kRecPerBlock = kRecThreads * kRecPerThread;
-constexpr int kResRec = 128;       // records per block of the one-pass staged decode (k_dec_res)
 constexpr int kMaxDynLds = 4;      // dynamic fields whose per-record metadata is staged in LDS
 
 }  // namespace xdrg

@@ -45,12 +45,10 @@ SCHEMAS = {
 # key 20 = 1 the byte fields of error-free blocks written record by record
 # with whole boundary dwords instead of by the output-stationary sweep (the
 # default, 2),
-# key 22 = 1 the one-pass decode of small records (blocks of 128 records
-# decoded from their LDS-resident stream range, k_dec_res);
 # key 9 = 0 group per record, 3 lane per record.  Tests taking `rec_kernel`
 # run under each.
 REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),),
-               "staged_edges": ((9, 4), (20, 0)), "staged_res": ((9, 4), (22, 1)),
+               "staged_edges": ((9, 4), (20, 0)),
                "staged_lean": ((9, 4), (20, 1))}
 
 
@@ -565,11 +563,11 @@ def test_decode_packed_bytes_unaligned_base(gpu_ctx, rec_kernel, name, shift):
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("name", ["cfg4_int_string_intvec", "cfg1_int_int_string", "dyn_vectors", "cfg3_6xint_opaque"])
 def test_resident_decode_fallback_blocks(gpu_ctx, name, framed):
-    """One-pass decode (k_dec_res): small records, except a run of 14
-    records of ~3000 bytes whose block range exceeds the 32 KiB tile, so that
-    block walks from HBM and decodes record by record while its neighbours
-    stay resident; a second pass plants a corrupt length word in a resident
-    block (first-bad record, error code and the records before it)."""
+    """Default decode over mixed blocks: small records, except a run of 14
+    records of ~3000 bytes whose block averages >= 1 KiB per record, so that
+    block goes to the group kernel while its neighbours take the staged sweep;
+    a second pass plants a corrupt length word in a staged block (first-bad
+    record, error code and the records before it)."""
     fields = SCHEMAS[name]
     n = 3000
     hb = random_batch(fields, n, seed=zlib.crc32(f"res/{name}/{framed}".encode()), dyn_len=(0, 24))
@@ -586,7 +584,6 @@ def test_resident_decode_fallback_blocks(gpu_ctx, name, framed):
     assert rc == 0
     caps = hb.dyn_caps()
     gpu_ctx.tune(9, 4)
-    gpu_ctx.tune(22, 1)
     try:
         g = gpu_decode(gpu_ctx, fields, want, n, want_offs, caps, framed)
         o = oracle_decode(fields, want, n, want_offs, caps, framed)
