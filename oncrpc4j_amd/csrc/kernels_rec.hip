@@ -1861,6 +1861,26 @@ __device__ __forceinline__ void stage_copy(uint8_t *tile, const uint8_t *const (
     }
 }
 
+// stage_copy by LDS-DMA (global_load_lds_dwordx4): chunk i lands at tile +
+// 16 i straight from memory, no registers, so the block can do other work
+// (the sweep's metadata) while the loads fly; the caller's barrier waits for
+// them.  A wave's 64 chunks are contiguous in the tile (the instruction's LDS
+// address is wave-uniform base + 16 * lane).
+__device__ __forceinline__ void stage_dma(uint8_t *tile, const uint8_t *const (&a0)[kMaxDynLds],
+                                          const uint32_t (&cb)[kMaxDynLds + 1], uint32_t nd) {
+    const uint32_t total = cb[nd], lane = threadIdx.x & 63;
+    for (uint32_t i0 = (threadIdx.x >> 6) * 64; i0 < total; i0 += kRecThreads) {
+        const uint32_t i = i0 + lane;
+        if (i >= total) continue;
+        const uint8_t *src = a0[0] + 16 * (uint64_t)i;
+#pragma unroll
+        for (int d = 1; d < kMaxDynLds; ++d)
+            if ((uint32_t)d < nd && i >= cb[d]) src = a0[d] + 16 * (uint64_t)(i - cb[d]);
+        __builtin_amdgcn_global_load_lds((const void *)src, (__attribute__((address_space(3))) void *)(tile + 16 * (size_t)i0),
+                                         16, 0, 0);
+    }
+}
+
 // XDR bytes of record j's dynamic fields d < nd (counts from a rel table:
 // row d holds element offsets relative to the block's first record).
 __device__ __forceinline__ uint64_t dyn_before(const RecArgs &a, const uint32_t *rel, uint32_t j, uint32_t nd,
@@ -2035,7 +2055,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
             cb[d + 1] += stage_chunks(f.data + (base[d] + srel[d * RS + js]) * esz,
                                       f.data + (base[d] + srel[d * RS + je]) * esz, &a0[d]);
         }
-        stage_copy(tile, a0, cb, a.ndyn);
+        stage_copy(tile, a0, cb, a.ndyn);   // (stage_dma measured 3.70 vs 3.62 ms here: nothing to overlap)
         __syncthreads();
         // scatter, field-major; field k of record j sits at
         // soff[j] + (fixed bytes before k) + (dynamic bytes before k)
@@ -2695,9 +2715,12 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
         cb[1] = stage_chunks(in + sb + sstart[js], in + sb + sstart[je - 1] + fx + dyn_before(a, snrel, je - 1, a.ndyn),
                              &a0[0]);
         const int64_t lds0 = -(int64_t)(a0[0] - (in + sb));   // tile offset of sstart value x: lds0 + x
-        if (sweep && !(XDRG_SW_PROBE & 8))
-            dec_sweep_prep<RS>(a, lds0, js, je, sstart, snrel, s_base, xs, (uint32_t *)supto, smeta1, smap, sf);
-        if (!SW || !(XDRG_SW_PROBE & 32)) stage_copy(tile, a0, cb, 1);
+        if (SW) {   // stage by LDS-DMA while the record lanes build the sweep's metadata
+            stage_dma(tile, a0, cb, 1);
+            if (sweep) dec_sweep_prep<RS>(a, lds0, js, je, sstart, snrel, s_base, xs, (uint32_t *)supto, smeta1, smap, sf);
+        } else {
+            stage_copy(tile, a0, cb, 1);
+        }
         __syncthreads();
         if (!SW) dec_stage_batch<RS>(a, tile, lds0, rb, js, je, sstart, snrel, supto, s_base, xs, lean, tid, kRecThreads);
         else if (sweep) dec_stage_sweep<RS>(a, tile, lds0, rb, js, je, sstart, snrel, (uint32_t *)supto, smeta1, smap, sf);
