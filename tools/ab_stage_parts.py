@@ -29,7 +29,8 @@ def main():
     for kv in filter(None, tune.split(",")):
         k, v = kv.split("=")
         ctx.tune(int(k), int(v))
-    wl = bench.Workload(ctx, 4, n, False)
+    cfg = int(os.environ.get("XDRG_CONFIG", "4"))
+    wl = bench.Workload(ctx, cfg, n, False)
     out = {"lib": os.path.basename(os.environ.get("XDRG_LIBRARY", "libxdrgpu.so")), "tune": tune, "records": n}
     for name, fn in (("encode", wl.encode), ("decode", wl.decode)):
         fn()
