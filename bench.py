@@ -93,15 +93,26 @@ def launch(args, argv):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    # poll every rank: the first one that fails ends the job, so survivors
+    # blocked in a rendezvous or a collective never hang the launcher
     rc = 0
-    for p in procs:
-        c = p.wait()
-        if c and not rc:
-            rc = c
-    if rc:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
+    live = list(procs)
+    while live and not rc:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c:
+                rc = c
+                break
+        if live and not rc:
+            time.sleep(0.05)
+    for p in live:
+        if p.poll() is None:
+            p.kill()
+    for p in live:
+        p.wait()
     return rc
 
 

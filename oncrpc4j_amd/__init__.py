@@ -8,4 +8,4 @@ this package is the Python host side above that ABI.
 """
 from . import abi  # noqa: F401
 
-__all__ = ["abi", "engine", "columns", "xdr", "parallel"]
+__all__ = ["abi", "engine", "columns", "parallel", "rpc", "rpcgen"]

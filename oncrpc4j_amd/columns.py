@@ -104,8 +104,13 @@ class HostBatch:
         return self.n if g < 0 else self.elems(g)
 
     def _elem_cap(self, g):
-        m = self.arrays[g + 1]
-        return (len(m[1]) - 1) if self.fields[g + 1][1] == abi.K_DYNAMIC else m.shape[0]
+        """Element capacity of group g: the smallest over its members (fixed
+        members are indexed by element with no capacity of their own)."""
+        caps = []
+        for j in range(1, self.fields[g][3] + 1):
+            m = self.arrays[g + j]
+            caps.append((len(m[1]) - 1) if self.fields[g + j][1] == abi.K_DYNAMIC else m.shape[0])
+        return min(caps)
 
     # ---- construction ----------------------------------------------------
     @classmethod
@@ -428,8 +433,12 @@ class DeviceBatch:
         return cls(fields, n, tensors, dts)
 
     def _elem_cap(self, g):
-        m = self.tensors[g + 1]
-        return (m[1].numel() - 1) if self.fields[g + 1][1] == abi.K_DYNAMIC else m.shape[0]
+        """Element capacity of group g: the smallest over its members."""
+        caps = []
+        for j in range(1, self.fields[g][3] + 1):
+            m = self.tensors[g + j]
+            caps.append((m[1].numel() - 1) if self.fields[g + j][1] == abi.K_DYNAMIC else m.shape[0])
+        return min(caps)
 
     def columns(self):
         """ctypes xdrg_column array with DEVICE pointers."""

@@ -2417,7 +2417,11 @@ __device__ __forceinline__ void sweep_bytes(uint8_t *col, const uint8_t *tile, c
         const int32_t loA = (int32_t)(m0 & 0xffffu), hiA = (int32_t)(m1 & 0xffffu), hiB = (int32_t)(m2 & 0xffffu);
         uint32_t a[4], b[4], v[4];
         tile16(tile, (int32_t)(m0 >> 16) + (xr - loA), a);
-        tile16(tile, (int32_t)(m1 >> 16) + (xr - hiA), b);
+        // B's window: when A is the sub-batch's last record (m1 is then the
+        // sentinel) or covers the whole chunk, B's bytes are masked out below;
+        // clamp the window so the read stays inside the block's LDS
+        const int32_t wb = (int32_t)(m1 >> 16) + (xr - hiA);
+        tile16(tile, wb < 0 ? 0 : wb, b);
         const int32_t sp = hiA - xr;   // chunk bytes [0, sp) from A, [sp, ..) from B
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -2716,8 +2720,15 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
                              &a0[0]);
         const int64_t lds0 = -(int64_t)(a0[0] - (in + sb));   // tile offset of sstart value x: lds0 + x
         if (SW) {   // stage by LDS-DMA while the record lanes build the sweep's metadata
-            stage_dma(tile, a0, cb, 1);
-            if (sweep) dec_sweep_prep<RS>(a, lds0, js, je, sstart, snrel, s_base, xs, (uint32_t *)supto, smeta1, smap, sf);
+            // (blocks that decode record by record from HBM below never read the tile)
+            if (sweep) {
+                stage_dma(tile, a0, cb, 1);
+                dec_sweep_prep<RS>(a, lds0, js, je, sstart, snrel, s_base, xs, (uint32_t *)supto, smeta1, smap, sf);
+                // LDS-DMA writes retire on vmcnt, not lgkmcnt: every wave waits for
+                // its own DMA before the barrier, so no wave reads a chunk that
+                // another wave's load has not landed yet
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
         } else {
             stage_copy(tile, a0, cb, 1);
         }

@@ -75,7 +75,7 @@ def _tokens(text):
 
 
 def _int_literal(s):
-    """C integer literal: decimal, 0x hex, leading-0 octal (Calculator.x consts)."""
+    """C integer literal: decimal, 0x hex, leading-0 octal (JrpcgenParser.cup constant forms)."""
     neg = s.startswith("-")
     t = s[1:] if neg else s
     if t[:2] in ("0x", "0X"):
@@ -144,7 +144,7 @@ class Spec:
             return 0
         if isinstance(v, int):
             return v
-        if v in ("TRUE", "FALSE"):    # bool union case labels (BlobStore.x)
+        if v in ("TRUE", "FALSE"):    # bool union case labels (RFC 4506 §4.4: TRUE / FALSE)
             return int(v == "TRUE")
         if re.fullmatch(r"-?(0[xX][0-9a-fA-F]+|\d+)", v):
             return _int_literal(v)

@@ -48,3 +48,12 @@ def test_world_size_mismatch_refused():
              env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "WORLD_SIZE" in p.stderr
+
+
+def test_launcher_ends_job_when_a_rank_dies():
+    """Rank 1 exits 3 while rank 0 waits in a barrier: the launcher returns 3
+    and kills rank 0 (it polls every rank, not rank 0 first)."""
+    p = _run(["--gpus", "2", "--backend", "gloo", "--test-codec", "bench_fail_codec", "--config", "2",
+              "--records", "100", "--steps", "1", "--warmup", "1"])
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert "rank 1 exits" in p.stderr

@@ -1,10 +1,10 @@
 """rpcgen .x -> engine field tapes (oncrpc4j_amd/rpcgen.py).
 
-Fixtures: builder-written .x inputs with the constructs of the reference's
-rpcgen test inputs (oncrpc4j-rpcgen/src/test/xdr/Calculator.x, BlobStore.x):
-arith_service.x (constants in every literal form, a struct of hypers,
-procedures with two anonymous hyper arguments) and kv_store.x (bounded opaque
-key, bool union with a void arm), plus tests/golden/rpcgen/batch_types.x.  The tape order is checked against an
+Fixtures: builder-designed .x inputs under tests/golden/rpcgen/:
+sensor_feed.x (constants in every literal form jrpcgen reads, an enum, a
+mixed-type struct, procedures with one / three / no arguments),
+lease_cache.x (an int-discriminated union with a multi-label arm and a void
+default as a procedure argument), batch_types.x and list_types.x.  The tape order is checked against an
 independent per-declaration xdrlib packer that walks the parsed structs the
 way jrpcgen's generated xdrEncode does (jrpcgen.java:758-913: one call per
 declaration, nested structs through their own xdrEncode)."""
@@ -33,34 +33,46 @@ def spec(name):
     return rpcgen.parse_file(os.path.join(HERE, name))
 
 
-def test_arith_consts_and_tapes():
-    s = spec("arith_service.x")
-    assert s.value("ZERO_DEC") == 0 and s.value("ZERO_HEX") == 0
-    assert s.value("MASK_16") == 0xAB00
-    assert s.value("WIDE_48") == 0xABC000000000
-    assert s.value("BEYOND_64") == 0xABC000000000000000000
-    assert s.value("U64_MAX_HEX") == s.value("U64_MAX_OCT") == s.value("U64_MAX_DEC") == 2**64 - 1
-    assert s.value("U32_MAX_HEX") == s.value("U32_MAX_OCT") == s.value("U32_MAX_DEC") == 2**32 - 1
-    assert s.fields("arith_reply") == [(H, SC, 0), (UH, SC, 0), (UH, SC, 0)]
+FEED = 0x2000F33D
+LEASE = 0x2000F33E
+
+
+def test_feed_consts_and_tapes():
+    s = spec("sensor_feed.x")
+    assert s.value("FEED_SLOTS") == 48 and s.value("FLAG_STALE") == 0x40
+    assert s.value("MODE_BITS") == 0o644
+    assert s.value("EPOCH_2023_NS") == 1672531200000000000
+    assert s.value("SEED_64") == 0x9E3779B97F4A7C15
+    assert s.value("TAG_80") == 0x7E57AB1E00000000000F
+    assert s.value("LIMIT_OCT_32") == s.value("LIMIT_HEX_32") == 2**31 - 1
+    assert s.types["unit_kind"].values == {"CELSIUS": 1, "PASCAL": 2, "VOLT": 3}
+    assert s.fields("reading") == [(U, SC, 0), (E, SC, 0), (H, SC, 0), (D, SC, 0), (F, FX, 2)]
     procs = s.procedures()
-    assert {k: p.name for k, p in procs.items()} == {(400117, 1, 1): "SUM", (400117, 1, 2): "SUM_PLAIN"}
-    assert s.args_fields(400117, 1, 1) == [(H, SC, 0), (H, SC, 0)]   # SUM(hyper, hyper)
-    assert s.result_fields(400117, 1, 1) == s.fields("arith_reply")
-    assert s.result_fields(400117, 1, 2) == [(H, SC, 0)]
+    assert {k: p.name for k, p in procs.items()} == {(FEED, 3, 1): "LATEST", (FEED, 3, 2): "WINDOW",
+                                                     (FEED, 3, 3): "FLUSH"}
+    assert s.args_fields(FEED, 3, 1) == [(U, SC, 0)]
+    assert s.result_fields(FEED, 3, 1) == s.fields("reading")
+    assert s.args_fields(FEED, 3, 2) == [(U, SC, 0), (H, SC, 0), (H, SC, 0)]   # WINDOW(unsigned, hyper, hyper)
+    assert s.result_fields(FEED, 3, 2) == [(H, SC, 0)]
+    assert s.args_fields(FEED, 3, 3) == [] and s.result_fields(FEED, 3, 3) == []   # void FLUSH(void)
 
 
-def test_kv_union_is_not_one_tape():
-    s = spec("kv_store.x")
-    assert s.fields("kv_key") == [(O, DY, 0)]
-    assert s.args_fields(400118, 1, 2) == [(O, DY, 0)]              # FETCH(kv_key)
-    with pytest.raises(rpcgen.NotBatchable, match="union kv_value"):
-        s.fields("kv_value")
+def test_lease_union_is_not_one_tape():
+    s = spec("lease_cache.x")
+    assert s.fields("lease_key") == [(UH, SC, 0), (STR, DY, 0)]
+    assert s.args_fields(LEASE, 1, 1) == [(UH, SC, 0), (STR, DY, 0), (U, SC, 0)]   # ACQUIRE(lease_key, unsigned)
+    with pytest.raises(rpcgen.NotBatchable, match="union lease_state"):
+        s.fields("lease_state")
     with pytest.raises(rpcgen.NotBatchable):
-        s.args_fields(400118, 1, 1)                                 # STORE(kv_key, kv_value)
-    u = s.types["kv_value"]
-    assert u.disc.name == "present" and u.disc.type == "bool"
-    assert [(v, d.kind, d.type) for v, d in u.arms] == [(["TRUE"], "dynamic", "opaque"), (["FALSE"], "void", "void")]
-    assert s.result_fields(400118, 1, 1) == []                       # void STORE
+        s.args_fields(LEASE, 1, 2)                                 # RELEASE(lease_key, lease_state)
+    with pytest.raises(rpcgen.NotBatchable):
+        s.result_fields(LEASE, 1, 1)                               # lease_state ACQUIRE
+    u = s.types["lease_state"]
+    assert u.disc.name == "code" and u.disc.type == "int"
+    assert [(v, d.kind, d.type) for v, d in u.arms] == [([0], "dynamic", "opaque"),
+                                                        ([1, 70], "scalar", ("unsigned", U))]
+    assert u.default.kind == "void"
+    assert s.result_fields(LEASE, 1, 2) == []                       # void RELEASE
 
 
 FATTR = [(E, SC, 0), (U, SC, 0), (U, SC, 0), (H, SC, 0), (UH, SC, 0), (U, SC, 0), (U, SC, 0),
@@ -164,22 +176,27 @@ def test_tape_matches_declaration_order(type_name):
 
 # ---- GPU: a call batch decoded with the tape of its procedure ----------------------
 @pytest.mark.gpu
-def test_arith_calls_decode_with_generated_tape(gpu_ctx):
+def test_feed_calls_decode_with_generated_tape(gpu_ctx):
     import torch
     from oncrpc4j_amd import rpc
-    s = spec("arith_service.x")
+    s = spec("sensor_feed.x")
     rng = np.random.default_rng(117)
     n = 4000
+    sensor = rng.integers(0, 2**32, n, dtype=np.uint32)
     a = rng.integers(-2**63, 2**63, n, dtype=np.int64)
     b = rng.integers(-2**63, 2**63, n, dtype=np.int64)
     stream, offs = b"", [0]
     for i in range(n):
         p = xdrlib.Packer()
-        for v in (i, rpc.CALL, rpc.RPCVERS, 400117, 1, 1, rpc.AUTH_NONE):
+        for v in (i, rpc.CALL, rpc.RPCVERS):
             p.pack_int(v)
+        for v in (FEED, 3, 2):
+            p.pack_uint(v)
+        p.pack_int(rpc.AUTH_NONE)
         p.pack_opaque(b"")
         p.pack_int(rpc.AUTH_NONE)
         p.pack_opaque(b"")
+        p.pack_uint(int(sensor[i]))
         p.pack_hyper(int(a[i]))
         p.pack_hyper(int(b[i]))
         m = p.get_buffer()
@@ -191,12 +208,13 @@ def test_arith_calls_decode_with_generated_tape(gpu_ctx):
     hdr, st = dec.decode_headers(dev, len(stream), n, ro)
     assert st == (0, n, 0)
     (key, idx), = rpc.CallDecoder.group_by_procedure(hdr).items()
-    assert key == (400117, 1, 1, rpc.AUTH_NONE) and idx.numel() == n
-    args = s.args_fields(*key[:3])
+    assert (key[0] & 0xffffffff, key[1], key[2], key[3]) == (FEED, 3, 2, rpc.AUTH_NONE) and idx.numel() == n
+    args = s.args_fields(FEED, 3, 2)
     batch, st = dec.decode(rpc.AUTH_NONE, args, dev, len(stream), n, ro, {7: 16, 9: 16})
     assert st == (0, n, 0)
     hb = batch.to_host()
-    assert np.array_equal(hb.arrays[10], a) and np.array_equal(hb.arrays[11], b)
+    assert np.array_equal(hb.arrays[10].view(np.uint32), sensor)
+    assert np.array_equal(hb.arrays[11], a) and np.array_equal(hb.arrays[12], b)
 
 
 # ---- conditional tapes: unions and optional data (Spec.tape) -------------------------
@@ -298,23 +316,25 @@ def test_conditional_tape_shapes():
     assert f == [(I, SC, 0), (G, LS, 0, 1), (I, SC, 0)] and c == []
 
 
-def test_kv_store_tape():
-    """STORE(kv_key, kv_value): a bool union argument (the shape of the
-    reference's BlobStore.x put(Key, Value))."""
-    s = spec("kv_store.x")
-    f, c = s.args_tape(400118, 1, 1)          # STORE
-    assert f == [(O, DY, 0), (B, SC, 0), (O, DY, 0)] and c == [(2, 1, False, [1])]
+def test_lease_release_tape():
+    """RELEASE(lease_key, lease_state): an int union argument; the two-label
+    arm carries both case values, the void default adds no field."""
+    s = spec("lease_cache.x")
+    f, c = s.args_tape(LEASE, 1, 2)
+    assert f == [(UH, SC, 0), (STR, DY, 0), (I, SC, 0), (O, DY, 0), (U, SC, 0)]
+    assert c == [(3, 2, False, [0]), (4, 2, False, [1, 70])]
 
 
 @pytest.mark.gpu
-def test_gpu_kv_store_args(gpu_ctx):
-    """STORE(kv_key, kv_value) argument batches through the engine with the
-    conditional tape, checked against xdrlib packing of the generated order."""
+def test_gpu_lease_release_args(gpu_ctx):
+    """RELEASE(lease_key, lease_state) argument batches through the engine
+    with the conditional tape, checked against xdrlib packing of the
+    generated order."""
     import torch
     from oncrpc4j_amd import engine
     from oncrpc4j_amd.columns import DeviceBatch, HostBatch
-    s = spec("kv_store.x")
-    fields, conds = s.args_tape(400118, 1, 1)
+    s = spec("lease_cache.x")
+    fields, conds = s.args_tape(LEASE, 1, 2)
     n = 5000
     hb = _cond_batch(fields, conds, n, seed=118)
     want = b""
@@ -322,8 +342,8 @@ def test_gpu_kv_store_args(gpu_ctx):
     for i in range(n):
         p = xdrlib.Packer()
         vals = _record_values(fields, hb, i)
-        _walk(s, "kv_key", vals, True, p)
-        _walk(s, "kv_value", vals, True, p)
+        _walk(s, "lease_key", vals, True, p)
+        _walk(s, "lease_state", vals, True, p)
         want += p.get_buffer()
         offs.append(len(want))
     sch = engine.Schema(fields, conds)
