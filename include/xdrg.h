@@ -28,7 +28,8 @@
  *     except its context's own device workspace;
  *   - a context is used by one thread at a time (mirrors Xdr's single-owner
  *     model, xdr/Xdr.java:56,71); use one context per worker thread;
- *   - all data pointers are DEVICE pointers (HBM) unless a call says otherwise.
+ *   - all data pointers are DEVICE pointers (HBM) unless a call says otherwise
+ *     or carries XDRG_HOST_PTRS (host memory through the staging ring).
  */
 #ifndef XDRG_H
 #define XDRG_H
@@ -148,6 +149,26 @@ typedef struct xdrg_column {
 /* out_len / first_bad / err are DEVICE pointers; the call does not
  * synchronise the stream (graph-capturable).                                  */
 #define XDRG_ASYNC         0x2u
+/* Host memory (SURVEY.md §8b HOST_PTRS): every pointer of an
+ * xdrg_encode_batch / xdrg_decode_batch call — column data and offsets, the
+ * stream, rec_offsets, out_len / first_bad / err — is a HOST pointer, as the
+ * reference's Xdr works on a host Grizzly buffer (xdr/Xdr.java:115-119,
+ * grizzly/GrizzlyMemoryManager.java:42-57) and sends from it
+ * (grizzly/GrizzlyRpcTransport.java:97-112).  The batch moves through the
+ * context's staging ring (xdrg_ctx_host_staging) in record chunks:
+ * H2D / kernels / D2H of consecutive chunks overlap on the context's own
+ * copy and compute streams; spans that are not pinned (xdrg_host_register,
+ * hipHostMalloc) pass through the ring's pinned bounce buffers.  The call
+ * is synchronous (XDRG_ASYNC is refused).  Results are those of the device
+ * call on the same records, except that a variable-size encode that
+ * overruns out_cap may have written the records before the overrun.
+ * Schemas with repeated groups take XDRG_HOST_MAPPED.                        */
+#define XDRG_HOST_PTRS     0x4u
+/* With XDRG_HOST_PTRS: no staging — the kernels read and write the host
+ * buffers in place over PCIe.  Every buffer must be registered
+ * (xdrg_host_register) or allocated pinned (hipHostMalloc); a variable-size
+ * decode then reads the stream twice over the link (sizes, then place).     */
+#define XDRG_HOST_MAPPED   0x8u
 
 /* ---- opaque handles ------------------------------------------------------- */
 typedef struct xdrg_ctx    xdrg_ctx;
@@ -178,6 +199,20 @@ int  xdrg_ctx_set_stream(xdrg_ctx *ctx, void *stream);
 #define XDRG_KERNEL_COUNT        7
 int  xdrg_ctx_kernel_stats(xdrg_ctx *ctx, int kernel, uint64_t *launches, double *total_ms);
 int  xdrg_ctx_reset_stats(xdrg_ctx *ctx);
+
+/* Staging ring of the XDRG_HOST_PTRS calls: `slots` (1..8) device slots of
+ * `slot_bytes` each, plus a pinned bounce mirror allocated on first use by
+ * a span that is not pinned.  Default 4 x 64 MiB.  A chunk is as many
+ * records as fit one slot (inputs, outputs and offsets together); a record
+ * larger than a slot grows the ring.  Takes effect at the next host call.  */
+int  xdrg_ctx_host_staging(xdrg_ctx *ctx, uint64_t slot_bytes, uint32_t slots);
+/* Pin a caller buffer for the DMA engines and map it for the kernels
+ * (hipHostRegister): the reference's direct / pooled Grizzly buffers
+ * (rpc/MemoryAllocator, grizzly/GrizzlyUtils.java:140-156) registered once
+ * and reused.  Registered spans skip the bounce copy and may take
+ * XDRG_HOST_MAPPED.  ctx may be NULL (current device).                      */
+int  xdrg_host_register(xdrg_ctx *ctx, void *ptr, uint64_t bytes);
+int  xdrg_host_unregister(xdrg_ctx *ctx, void *ptr);
 
 /* ---- schema ----------------------------------------------------------------- */
 /* Compile a field tape (rpcgen struct body, jrpcgen.java:758-913) into an

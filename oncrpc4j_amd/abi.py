@@ -38,6 +38,8 @@ K_LIST = 3     # XDRG_T_GROUP only: recursive optional list (BE(1) + element ...
 # flags
 FRAME_RM = 0x1
 ASYNC = 0x2
+HOST_PTRS = 0x4     # every pointer of the call is host memory (staging ring, include/xdrg.h)
+HOST_MAPPED = 0x8   # with HOST_PTRS: kernels access the registered host buffers in place
 STRIDE_CONST = -(1 << 63)   # XDRG_STRIDE_CONST: every record reads element run 0 (encode only)
 CTX_TIMING = 0x1
 
@@ -98,6 +100,9 @@ FUNCTIONS = {
     "xdrg_ctx_kernel_stats": (ctypes.c_int, [_P, ctypes.c_int, _PU64,
                                              ctypes.POINTER(ctypes.c_double)]),
     "xdrg_ctx_reset_stats": (ctypes.c_int, [_P]),
+    "xdrg_ctx_host_staging": (ctypes.c_int, [_P, _U64, ctypes.c_uint32]),
+    "xdrg_host_register": (ctypes.c_int, [_P, _P, _U64]),
+    "xdrg_host_unregister": (ctypes.c_int, [_P, _P]),
     "xdrg_schema_create": (ctypes.c_int, [ctypes.POINTER(Field), ctypes.c_size_t,
                                           ctypes.POINTER(_P)]),
     "xdrg_schema_create_cond": (ctypes.c_int, [ctypes.POINTER(Field), ctypes.c_size_t,

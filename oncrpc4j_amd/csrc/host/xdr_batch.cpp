@@ -4,7 +4,6 @@
 // BatchXdrEncoder records per-field calls into native columns (host staging,
 // the role Grizzly buffers play for the reference), BatchXdrDecoder replays
 // decoded columns; all XDR arithmetic runs in libxdrgpu.so on the GPU.
-#include <hip/hip_runtime.h>
 
 #include <cstring>
 #include <string>
@@ -44,25 +43,6 @@ uint32_t xdr_size(uint32_t t) {
     }
 }
 uint64_t pad4(uint64_t n) { return (4 - (n & 3)) & 3; }
-
-// Device buffer owned for the duration of one batch call.
-struct DevBuf {
-    void *p = nullptr;
-    DevBuf() = default;
-    explicit DevBuf(size_t bytes) {
-        if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) throw XdrgError(XDRG_E_NOMEM, "hipMalloc failed");
-    }
-    ~DevBuf() { if (p) (void)hipFree(p); }
-    DevBuf(DevBuf &&o) noexcept : p(o.p) { o.p = nullptr; }
-    DevBuf &operator=(DevBuf &&o) noexcept { std::swap(p, o.p); return *this; }
-    DevBuf(const DevBuf &) = delete;
-};
-void h2d(void *d, const void *h, size_t n) {
-    if (n && hipMemcpy(d, h, n, hipMemcpyHostToDevice) != hipSuccess) throw XdrgError(XDRG_E_HIP, "hipMemcpy H2D failed");
-}
-void d2h(void *h, const void *d, size_t n) {
-    if (n && hipMemcpy(h, d, n, hipMemcpyDeviceToHost) != hipSuccess) throw XdrgError(XDRG_E_HIP, "hipMemcpy D2H failed");
-}
 
 struct SchemaHandle {
     xdrg_schema *s = nullptr;
@@ -256,45 +236,36 @@ std::vector<uint8_t> BatchXdrEncoder::flush(bool framed, std::vector<uint64_t> *
         return out;
     }
     SchemaHandle sch(m.tape);
-    std::vector<DevBuf> bufs;
+    // Host columns straight into the engine (XDRG_HOST_PTRS: the context's
+    // staging ring moves them chunk by chunk); the stream lands in the
+    // XdrBuffer, grown as Xdr.ensureCapacity grows it (Xdr.java:1020-1026)
+    // when the engine reports XDRG_E_CAPACITY and the bytes it needs.
     std::vector<xdrg_column> cols(m.cols.size());
     for (size_t k = 0; k < m.cols.size(); ++k) {
-        const Column &c = m.cols[k];
-        bufs.emplace_back(c.data.size());
-        h2d(bufs.back().p, c.data.data(), c.data.size());
-        cols[k].data = bufs.back().p;
+        Column &c = m.cols[k];
+        if (c.data.empty()) c.data.resize(8);   // a valid pointer for empty columns
+        cols[k].data = c.data.data();
         cols[k].stride = 0;
         cols[k].cap = c.data.size() / native_size(c.f.type);
-        cols[k].offsets = nullptr;
-        if (c.f.kind == XDRG_K_DYNAMIC) {
-            bufs.emplace_back(c.offsets.size() * 8);
-            h2d(bufs.back().p, c.offsets.data(), c.offsets.size() * 8);
-            cols[k].offsets = (uint64_t *)bufs.back().p;
-        }
+        cols[k].offsets = c.f.kind == XDRG_K_DYNAMIC ? c.offsets.data() : nullptr;
     }
-    // Encode into the staging buffer's capacity; when the batch does not fit
-    // the engine reports XDRG_E_CAPACITY and the bytes it needs, and the
-    // buffer grows as Xdr.ensureCapacity grows it (Xdr.java:1020-1026).
-    DevBuf d_offs((m.n + 1) * 8);
+    m.offs.resize(m.n + 1);
     uint64_t len = 0;
     m.buf.clear();
     for (;;) {
-        DevBuf d_out(m.buf.remaining());
-        const int st = xdrg_encode_batch(m.eng->ctx(), sch.s, cols.data(), m.n, (uint8_t *)d_out.p,
-                                         m.buf.remaining(), (uint64_t *)d_offs.p, framed ? XDRG_FRAME_RM : 0, &len);
+        out.resize(m.buf.remaining());
+        const int st = xdrg_encode_batch(m.eng->ctx(), sch.s, cols.data(), m.n, out.data(), out.size(),
+                                         m.offs.data(), (framed ? XDRG_FRAME_RM : 0) | XDRG_HOST_PTRS, &len);
         if (st == XDRG_E_CAPACITY && len > m.buf.remaining()) {
             m.buf.ensureCapacity(len);
             continue;
         }
         check(st, m.eng->ctx());
         out.resize(len);
-        d2h(out.data(), d_out.p, len);
         break;
     }
     m.buf.put(out.data(), len);
     m.buf.flip();   // endEncoding (Xdr.java:143-146)
-    m.offs.resize(m.n + 1);
-    d2h(m.offs.data(), d_offs.p, (m.n + 1) * 8);
     if (offsets) *offsets = m.offs;
     m.stream = out;
     m.cols.clear();
@@ -368,8 +339,6 @@ void BatchXdrDecoder::load(const std::vector<uint8_t> &xdr, uint64_t n, const st
                            bool framed) {
     Impl &m = *p_;
     SchemaHandle sch(m.tape);
-    DevBuf d_in(xdr.size());
-    h2d(d_in.p, xdr.data(), xdr.size());
     // one record and no extents: the record is the whole buffer, as one Xdr
     // wraps one message (RpcMessageParserTCP.java:139)
     std::vector<uint64_t> one;
@@ -378,50 +347,39 @@ void BatchXdrDecoder::load(const std::vector<uint8_t> &xdr, uint64_t n, const st
         one = {0, (uint64_t)xdr.size()};
         ro = &one;
     }
-    DevBuf d_ro;
-    if (!ro->empty()) {
-        if (ro->size() != n + 1) throw std::invalid_argument("rec_offsets needs n + 1 entries");
-        d_ro = DevBuf(ro->size() * 8);
-        h2d(d_ro.p, ro->data(), ro->size() * 8);
-    }
-    std::vector<DevBuf> bufs;
+    if (!ro->empty() && ro->size() != n + 1) throw std::invalid_argument("rec_offsets needs n + 1 entries");
+    // host columns, filled by the engine through its staging ring (XDRG_HOST_PTRS)
     std::vector<xdrg_column> cols(m.tape.size());
     m.cols.assign(m.tape.size(), Column{});
     for (size_t k = 0; k < m.tape.size(); ++k) {
         const xdrg_field &f = m.tape[k];
-        m.cols[k].f = f;
+        Column &c = m.cols[k];
+        c.f = f;
         const uint32_t ns = native_size(f.type);
         if (f.kind == XDRG_K_DYNAMIC) {
             // a column cannot hold more elements than the stream has bytes
             const uint64_t cap = xdr.size() / (xdr_size(f.type) == 1 ? 1 : xdr_size(f.type)) + 1;
-            m.cols[k].data.resize(cap * ns);
-            m.cols[k].offsets.resize(n + 1);
-            bufs.emplace_back(cap * ns);
-            cols[k].data = bufs.back().p;
+            c.data.resize(cap * ns);
+            c.offsets.resize(n + 1);
             cols[k].cap = cap;
-            bufs.emplace_back((n + 1) * 8);
-            cols[k].offsets = (uint64_t *)bufs.back().p;
+            cols[k].offsets = c.offsets.data();
         } else {
             const uint64_t cnt = f.kind == XDRG_K_FIXED ? f.count : 1;
-            m.cols[k].data.resize(n * cnt * ns);
-            bufs.emplace_back(n * cnt * ns);
-            cols[k].data = bufs.back().p;
-            cols[k].offsets = nullptr;
+            c.data.resize(n * cnt * ns + 8);
             cols[k].cap = 0;
+            cols[k].offsets = nullptr;
         }
+        cols[k].data = c.data.data();
         cols[k].stride = 0;
     }
     uint64_t fb = 0;
     int err = 0;
-    const int st = xdrg_decode_batch(m.eng->ctx(), sch.s, (const uint8_t *)d_in.p, xdr.size(),
-                                     ro->empty() ? nullptr : (const uint64_t *)d_ro.p, n, cols.data(),
-                                     framed ? XDRG_FRAME_RM : 0, &fb, &err);
+    static const uint8_t empty4[4] = {0, 0, 0, 0};
+    const int st = xdrg_decode_batch(m.eng->ctx(), sch.s, xdr.empty() ? empty4 : xdr.data(), xdr.size(),
+                                     ro->empty() ? nullptr : ro->data(), n, cols.data(),
+                                     (framed ? XDRG_FRAME_RM : 0) | XDRG_HOST_PTRS, &fb, &err);
     if (st && st != XDRG_E_SHORT && st != XDRG_E_CORRUPT && st != XDRG_E_FRAME && st != XDRG_E_CAPACITY)
         fail(st, m.eng->ctx());
-    for (size_t k = 0; k < m.tape.size(); ++k) {
-        d2h(m.cols[k].data.data(), cols[k].data, m.cols[k].data.size());
-        if (cols[k].offsets) d2h(m.cols[k].offsets.data(), cols[k].offsets, (n + 1) * 8);
-    }
     m.n = n;
     m.first_bad = st ? fb : n;
     m.err = st ? err : 0;

@@ -11,10 +11,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
 
+#include "host_stage.h"
 #include "xdrg_internal.h"
 
 using namespace xdrg;
@@ -216,6 +219,24 @@ struct Timed {
     hipEvent_t a, b;
 };
 
+// Staging ring of the XDRG_HOST_PTRS calls (host_stage.h): device slots, a
+// pinned bounce mirror, the copy / compute streams and per-slot events and
+// status words.
+struct StageRing {
+    uint64_t want_slot = 64ull << 20;   // xdrg_ctx_host_staging
+    uint32_t want_n = 4;
+    uint8_t *dev = nullptr;
+    uint64_t slot = 0;                  // allocated bytes per slot
+    uint32_t n = 0;
+    uint8_t *bounce = nullptr;          // pinned, n * slot (first pageable span)
+    hipStream_t h2d = nullptr, d2h = nullptr, comp = nullptr;
+    hipEvent_t e_h2d[hs::kMaxSlots] = {}, e_kern[hs::kMaxSlots] = {}, e_d2h[hs::kMaxSlots] = {};
+    bool d2h_rec[hs::kMaxSlots] = {};
+    uint32_t nres[hs::kMaxSlots] = {};
+    uint64_t *d_res = nullptr, *h_res = nullptr;   // [kMaxSlots][kResWords]
+};
+constexpr uint32_t kResWords = 64;
+
 struct xdrg_ctx {
     int device = 0;
     uint32_t flags = 0;
@@ -233,6 +254,7 @@ struct xdrg_ctx {
     uint64_t launches[XDRG_KERNEL_COUNT] = {};
     double ms[XDRG_KERNEL_COUNT] = {};
     Tuning tune;                // this context's kernel choices (xdrg_internal_tune)
+    StageRing ring;             // XDRG_HOST_PTRS staging (allocated on first use)
 };
 
 static int hip_fail(xdrg_ctx *c, hipError_t e, const char *what) {
@@ -382,11 +404,14 @@ extern "C" int xdrg_ctx_create(int device, uint32_t flags, xdrg_ctx **out) {
     return XDRG_OK;
 }
 
+static void ring_free(xdrg_ctx *c);
+
 extern "C" int xdrg_ctx_destroy(xdrg_ctx *c) {
     if (!c) return XDRG_OK;
     DeviceGuard dg;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    ring_free(c);
     while (!c->pending.empty()) resolve_one(c);
     for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
     if (c->d_ws) (void)hipFree(c->d_ws);
@@ -821,9 +846,17 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
     return XDRG_OK;
 }
 
+static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, uint8_t *out,
+                       uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len);
+static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t in_len,
+                       const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
+                       uint64_t *first_bad, int *err);
+
 extern "C" int xdrg_encode_batch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols,
                                  uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_offsets,
                                  uint32_t flags, uint64_t *out_len) {
+    if (flags & XDRG_HOST_PTRS) return host_encode(c, s, cols, n, out, out_cap, rec_offsets, flags, out_len);
+    if (flags & XDRG_HOST_MAPPED) return inval(c, "XDRG_HOST_MAPPED without XDRG_HOST_PTRS");
     return encode_impl(c, s, cols, n, out, out_cap, rec_offsets, flags, out_len, 0, nullptr);
 }
 
@@ -1021,6 +1054,8 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
 extern "C" int xdrg_decode_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in,
                                  uint64_t in_len, const uint64_t *rec_offsets, uint64_t n,
                                  xdrg_column *cols, uint32_t flags, uint64_t *first_bad, int *err) {
+    if (flags & XDRG_HOST_PTRS) return host_decode(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err);
+    if (flags & XDRG_HOST_MAPPED) return inval(c, "XDRG_HOST_MAPPED without XDRG_HOST_PTRS");
     return decode_impl(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err, 0, nullptr);
 }
 
@@ -1032,6 +1067,373 @@ extern "C" int xdrg_decode_batch_view(xdrg_ctx *c, const xdrg_schema *s, const u
     if (rc) return rc;
     return decode_impl(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err, field + 1,
                        payload_pos);
+}
+
+// ---------------------------------------------------------------------------
+// host memory (XDRG_HOST_PTRS): registry, staging ring, executor
+// ---------------------------------------------------------------------------
+// Buffers pinned through xdrg_host_register: host base -> (bytes, device view).
+namespace {
+struct HostReg {
+    uint64_t bytes;
+    uint8_t *dev;
+};
+std::mutex g_reg_mu;
+std::map<uintptr_t, HostReg> g_reg;
+
+// The registration holding [p, p + n), or nullptr.
+bool reg_find(const void *p, uint64_t n, uintptr_t *base, HostReg *out) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    const uintptr_t a = (uintptr_t)p;
+    auto it = g_reg.upper_bound(a);
+    if (it == g_reg.begin()) return false;
+    --it;
+    if (a + n > it->first + it->second.bytes) return false;
+    if (base) *base = it->first;
+    if (out) *out = it->second;
+    return true;
+}
+
+// hipPointerGetAttributes: 1 pinned / mapped host memory, 2 device memory, 0 other
+int host_kind(const void *p) {
+    hipPointerAttribute_t a;
+    memset(&a, 0, sizeof a);
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    if (a.type == hipMemoryTypeHost) return 1;
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return 2;
+    return 0;
+}
+}  // namespace
+
+// A host span the DMA engines and kernels can reach without staging.
+static bool span_pinned(const void *p, uint64_t n) {
+    if (!n) return true;
+    if (reg_find(p, n, nullptr, nullptr)) return true;
+    return host_kind(p) == 1 && host_kind((const uint8_t *)p + n - 1) == 1;
+}
+
+// Device address of a pinned host span (XDRG_HOST_MAPPED), or nullptr.
+static void *span_device(const void *p, uint64_t n) {
+    if (!p) return nullptr;
+    uintptr_t base = 0;
+    HostReg r;
+    if (reg_find(p, n ? n : 1, &base, &r)) return r.dev + ((uintptr_t)p - base);
+    if (!span_pinned(p, n ? n : 1)) return nullptr;
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, (void *)p, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return d;
+}
+
+extern "C" int xdrg_host_register(xdrg_ctx *c, void *ptr, uint64_t bytes) {
+    if (!ptr || !bytes) return inval(c, "nothing to register");
+    DeviceGuard dg;
+    if (c) HIPCHK(c, hipSetDevice(c->device));
+    if (reg_find(ptr, 1, nullptr, nullptr)) return inval(c, "buffer already registered");
+    HIPCHK(c, hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+    void *d = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&d, ptr, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(ptr);
+        return hip_fail(c, e, "hipHostGetDevicePointer");
+    }
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[(uintptr_t)ptr] = HostReg{bytes, (uint8_t *)d};
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_host_unregister(xdrg_ctx *c, void *ptr) {
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto it = g_reg.find((uintptr_t)ptr);
+        if (it == g_reg.end()) return inval(c, "buffer not registered");
+        g_reg.erase(it);
+    }
+    DeviceGuard dg;
+    if (c) HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipHostUnregister(ptr));
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_ctx_host_staging(xdrg_ctx *c, uint64_t slot_bytes, uint32_t slots) {
+    if (!c) return XDRG_E_INVAL;
+    if (slots < 1 || slots > hs::kMaxSlots || slot_bytes < (1u << 16)) return inval(c, "staging: 1..8 slots of >= 64 KiB");
+    c->ring.want_slot = slot_bytes;
+    c->ring.want_n = slots;
+    return XDRG_OK;
+}
+
+static void ring_free(xdrg_ctx *c) {
+    StageRing &r = c->ring;
+    if (r.comp) (void)hipStreamSynchronize(r.comp);
+    if (r.h2d) (void)hipStreamSynchronize(r.h2d);
+    if (r.d2h) (void)hipStreamSynchronize(r.d2h);
+    if (r.dev) (void)hipFree(r.dev);
+    if (r.bounce) (void)hipHostFree(r.bounce);
+    r.dev = r.bounce = nullptr;
+    r.slot = 0;
+    r.n = 0;
+    for (uint32_t i = 0; i < hs::kMaxSlots; ++i) {
+        if (r.e_h2d[i]) (void)hipEventDestroy(r.e_h2d[i]);
+        if (r.e_kern[i]) (void)hipEventDestroy(r.e_kern[i]);
+        if (r.e_d2h[i]) (void)hipEventDestroy(r.e_d2h[i]);
+        r.e_h2d[i] = r.e_kern[i] = r.e_d2h[i] = nullptr;
+        r.d2h_rec[i] = false;
+    }
+    for (hipStream_t *st : {&r.h2d, &r.d2h, &r.comp})
+        if (*st) {
+            (void)hipStreamDestroy(*st);
+            *st = nullptr;
+        }
+    if (r.d_res) (void)hipFree(r.d_res);
+    if (r.h_res) (void)hipHostFree(r.h_res);
+    r.d_res = r.h_res = nullptr;
+}
+
+// Slots of `slot` bytes; streams, events and status words on first use.
+static int ring_ready(xdrg_ctx *c, uint64_t slot) {
+    StageRing &r = c->ring;
+    if (!r.comp) {
+        HIPCHK(c, hipStreamCreateWithFlags(&r.h2d, hipStreamNonBlocking));
+        HIPCHK(c, hipStreamCreateWithFlags(&r.d2h, hipStreamNonBlocking));
+        HIPCHK(c, hipStreamCreateWithFlags(&r.comp, hipStreamNonBlocking));
+        for (uint32_t i = 0; i < hs::kMaxSlots; ++i) {
+            HIPCHK(c, hipEventCreateWithFlags(&r.e_h2d[i], hipEventDisableTiming));
+            HIPCHK(c, hipEventCreateWithFlags(&r.e_kern[i], hipEventDisableTiming));
+            HIPCHK(c, hipEventCreateWithFlags(&r.e_d2h[i], hipEventDisableTiming));
+        }
+        HIPCHK(c, hipMalloc(&r.d_res, sizeof(uint64_t) * kResWords * hs::kMaxSlots));
+        HIPCHK(c, hipHostMalloc(&r.h_res, sizeof(uint64_t) * kResWords * hs::kMaxSlots, hipHostMallocDefault));
+    }
+    slot = hs::up(slot, 1 << 16);
+    if (r.dev && r.slot == slot && r.n == r.want_n) return XDRG_OK;
+    HIPCHK(c, hipStreamSynchronize(r.h2d));
+    HIPCHK(c, hipStreamSynchronize(r.d2h));
+    HIPCHK(c, hipStreamSynchronize(r.comp));
+    if (r.dev) HIPCHK(c, hipFree(r.dev));
+    if (r.bounce) HIPCHK(c, hipHostFree(r.bounce));
+    r.dev = r.bounce = nullptr;
+    for (uint32_t i = 0; i < hs::kMaxSlots; ++i) r.d2h_rec[i] = false;
+    r.n = r.want_n;
+    r.slot = slot;
+    const hipError_t e = hipMalloc(&r.dev, r.slot * r.n);
+    if (e != hipSuccess) {
+        r.dev = nullptr;
+        r.slot = 0;
+        return hip_fail(c, e, "staging ring hipMalloc");
+    }
+    return XDRG_OK;
+}
+
+// host_stage.h executor on one context: copies on the ring's H2D / D2H
+// streams, kernels on its compute stream, ordered by per-slot events.
+struct HipExec {
+    xdrg_ctx *c;
+    const xdrg_schema *s;
+    StageRing &r;
+    HipExec(xdrg_ctx *c_, const xdrg_schema *s_) : c(c_), s(s_), r(c_->ring) {}
+
+    uint32_t nslots() const { return r.n; }
+    uint64_t slot_bytes() const { return r.slot; }
+    uint8_t *slot(uint32_t i) const { return r.dev + (uint64_t)i * r.slot; }
+    uint8_t *bounce(uint32_t i) {
+        if (!r.bounce && hipHostMalloc(&r.bounce, r.slot * r.n, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            r.bounce = nullptr;
+            c->err = "staging bounce hipHostMalloc failed";
+            return nullptr;
+        }
+        return r.bounce + (uint64_t)i * r.slot;
+    }
+    bool pinned(const void *p, uint64_t n) const { return span_pinned(p, n); }
+    int wait_slot(uint32_t i) {
+        if (r.d2h_rec[i]) HIPCHK(c, hipEventSynchronize(r.e_d2h[i]));
+        return XDRG_OK;
+    }
+    int dma_h2d(uint8_t *dev, const void *host, uint64_t n) {
+        HIPCHK(c, hipMemcpyAsync(dev, host, n, hipMemcpyHostToDevice, r.h2d));
+        return XDRG_OK;
+    }
+    int h2d_done(uint32_t i) {
+        HIPCHK(c, hipEventRecord(r.e_h2d[i], r.h2d));
+        return XDRG_OK;
+    }
+    int kernel_begin(uint32_t i) {
+        HIPCHK(c, hipStreamWaitEvent(r.comp, r.e_h2d[i], 0));
+        HIPCHK(c, hipMemsetAsync(r.d_res + (uint64_t)i * kResWords, 0, 16, r.comp));
+        return XDRG_OK;
+    }
+    int add_u64(int on_d2h, uint64_t *p, uint64_t n, uint64_t delta) {
+        HIPCHK(c, (hipError_t)launch_add_u64(p, n, delta, on_d2h ? r.d2h : r.comp));
+        return XDRG_OK;
+    }
+    int encode(uint32_t i, const xdrg_column *dc, uint64_t m, uint8_t *out, uint64_t cap, uint64_t *rec,
+               uint32_t flags) {
+        hipStream_t keep = c->stream;
+        c->stream = r.comp;
+        const int rc = encode_impl(c, s, dc, m, out, cap, rec, flags | XDRG_ASYNC, r.d_res + (uint64_t)i * kResWords,
+                                   0, nullptr);
+        c->stream = keep;
+        return rc;
+    }
+    int decode(uint32_t i, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m, xdrg_column *dc,
+               uint32_t flags) {
+        hipStream_t keep = c->stream;
+        c->stream = r.comp;
+        uint64_t *w = r.d_res + (uint64_t)i * kResWords;
+        const int rc = decode_impl(c, s, in, len, rec, m, dc, flags | XDRG_ASYNC, w, (int *)(w + 1), 0, nullptr);
+        c->stream = keep;
+        return rc;
+    }
+    int kernel_end(uint32_t i, const uint64_t *const *extra, uint32_t nextra) {
+        if (nextra + 2 > kResWords) return inval(c, "too many dynamic fields for the staging status");
+        uint64_t *w = r.d_res + (uint64_t)i * kResWords;
+        for (uint32_t j = 0; j < nextra; ++j)
+            HIPCHK(c, hipMemcpyAsync(w + 2 + j, extra[j], 8, hipMemcpyDeviceToDevice, r.comp));
+        HIPCHK(c, hipMemcpyAsync(r.h_res + (uint64_t)i * kResWords, w, 8 * (2 + nextra), hipMemcpyDeviceToHost, r.comp));
+        r.nres[i] = 2 + nextra;
+        HIPCHK(c, hipEventRecord(r.e_kern[i], r.comp));
+        return XDRG_OK;
+    }
+    int wait_kernel(uint32_t i, uint64_t *w) {
+        HIPCHK(c, hipEventSynchronize(r.e_kern[i]));
+        memcpy(w, r.h_res + (uint64_t)i * kResWords, 8 * r.nres[i]);
+        w[1] &= 0xffffffffull;   // err is an int (the upper half was zeroed)
+        return XDRG_OK;
+    }
+    int d2h_begin(uint32_t i) {
+        HIPCHK(c, hipStreamWaitEvent(r.d2h, r.e_kern[i], 0));
+        return XDRG_OK;
+    }
+    int dma_d2h(void *host, const uint8_t *dev, uint64_t n) {
+        HIPCHK(c, hipMemcpyAsync(host, dev, n, hipMemcpyDeviceToHost, r.d2h));
+        return XDRG_OK;
+    }
+    int dma_d2h_2d(void *host, uint64_t hp, const uint8_t *dev, uint64_t dp, uint64_t w, uint64_t rows) {
+        HIPCHK(c, hipMemcpy2DAsync(host, hp, dev, dp, w, rows, hipMemcpyDeviceToHost, r.d2h));
+        return XDRG_OK;
+    }
+    int d2h_done(uint32_t i) {
+        HIPCHK(c, hipEventRecord(r.e_d2h[i], r.d2h));
+        r.d2h_rec[i] = true;
+        return XDRG_OK;
+    }
+    int grow(uint64_t slot) { return ring_ready(c, slot > r.slot ? slot : r.slot); }
+    // every copy and kernel of the call has finished (the caller's buffers are free again)
+    int finish() {
+        HIPCHK(c, hipStreamSynchronize(r.h2d));
+        HIPCHK(c, hipStreamSynchronize(r.comp));
+        HIPCHK(c, hipStreamSynchronize(r.d2h));
+        return XDRG_OK;
+    }
+};
+
+static void stage_schema(const xdrg_schema *s, hs::Schema &v) {
+    v.f.resize(s->f.size());
+    for (size_t k = 0; k < s->f.size(); ++k)
+        v.f[k] = hs::Field{s->f[k].type, s->f[k].kind, s->f[k].count, s->nsz[k], s->xsz[k], s->xbytes[k]};
+    v.fixed_part = s->fixed_part;
+    v.var_size = s->var_size;
+}
+
+// Device views of host columns (XDRG_HOST_MAPPED).
+static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
+                       std::vector<xdrg_column> &out) {
+    out.assign(cols, cols + s->f.size());
+    for (size_t k = 0; k < s->f.size(); ++k) {
+        xdrg_column &d = out[k];
+        if (d.offsets) {
+            d.offsets = (uint64_t *)span_device(cols[k].offsets, 8);
+            if (!d.offsets) return inval(c, "XDRG_HOST_MAPPED: column offsets not registered");
+        }
+        if (d.data) {
+            d.data = span_device(cols[k].data, 1);
+            if (!d.data) return inval(c, "XDRG_HOST_MAPPED: column data not registered");
+        }
+    }
+    (void)n;
+    return XDRG_OK;
+}
+
+static int host_common(xdrg_ctx *c, const xdrg_schema *s, uint32_t flags) {
+    if (!c || !s) return XDRG_E_INVAL;
+    if (flags & XDRG_ASYNC) return inval(c, "XDRG_HOST_PTRS calls are synchronous (no XDRG_ASYNC)");
+    return XDRG_OK;
+}
+
+static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, uint8_t *out,
+                       uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len) {
+    int rc = host_common(c, s, flags);
+    if (rc) return rc;
+    DeviceGuard dg;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!aligned(out, 4)) return inval(c, "XDR buffer not 4-byte aligned");
+    if (n && !out) return inval(c, "XDR buffer is NULL");
+    rc = check_columns(c, s, cols, n, false);
+    if (rc) return rc;
+    const uint32_t dflags = flags & XDRG_FRAME_RM;
+    if (flags & XDRG_HOST_MAPPED) {
+        std::vector<xdrg_column> dc;
+        rc = mapped_cols(c, s, cols, n, dc);
+        if (rc) return rc;
+        uint8_t *dout = n ? (uint8_t *)span_device(out, 1) : out;
+        uint64_t *drec = rec_offsets ? (uint64_t *)span_device(rec_offsets, 8) : nullptr;
+        if ((n && !dout) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
+        return encode_impl(c, s, dc.data(), n, dout, out_cap, drec, dflags, out_len, 0, nullptr);
+    }
+    if (s->ngroups) return inval(c, "repeated groups: XDRG_HOST_PTRS takes XDRG_HOST_MAPPED");
+    hs::Schema v;
+    stage_schema(s, v);
+    rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));   // the caller's earlier work on this context
+    HipExec x(c, s);
+    rc = hs::stage_encode(x, v, cols, n, out, out_cap, rec_offsets, dflags, out_len);
+    const int fr = x.finish();
+    if (rc == XDRG_E_CAPACITY) c->err = "output buffer too small";
+    else if (rc == XDRG_E_INVAL && c->err.empty()) c->err = "host columns: unsupported layout";
+    return rc ? rc : fr;
+}
+
+static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t in_len,
+                       const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
+                       uint64_t *first_bad, int *err) {
+    int rc = host_common(c, s, flags);
+    if (rc) return rc;
+    DeviceGuard dg;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!aligned(in, 4)) return inval(c, "XDR buffer not 4-byte aligned");
+    if (n && in_len && !in) return inval(c, "XDR buffer is NULL");
+    if (s->var_size && !rec_offsets) return inval(c, "variable-size schema needs record offsets");
+    rc = check_columns(c, s, cols, n, true);
+    if (rc) return rc;
+    const uint32_t dflags = flags & XDRG_FRAME_RM;
+    if (flags & XDRG_HOST_MAPPED) {
+        std::vector<xdrg_column> dc;
+        rc = mapped_cols(c, s, cols, n, dc);
+        if (rc) return rc;
+        const uint8_t *din = in_len ? (const uint8_t *)span_device(in, in_len) : in;
+        const uint64_t *drec = rec_offsets ? (const uint64_t *)span_device(rec_offsets, (n + 1) * 8) : nullptr;
+        if ((in_len && !din) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
+        return decode_impl(c, s, din, in_len, drec, n, dc.data(), dflags, first_bad, err, 0, nullptr);
+    }
+    if (s->ngroups) return inval(c, "repeated groups: XDRG_HOST_PTRS takes XDRG_HOST_MAPPED");
+    hs::Schema v;
+    stage_schema(s, v);
+    rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HipExec x(c, s);
+    rc = hs::stage_decode(x, v, in, in_len, rec_offsets, n, cols, dflags, first_bad, err);
+    const int fr = x.finish();
+    if (rc && rc != XDRG_E_INVAL && rc != XDRG_E_HIP && rc != XDRG_E_NOMEM) c->err = xdrg_status_string(rc);
+    else if (rc == XDRG_E_INVAL && c->err.empty()) c->err = "host columns: unsupported layout";
+    return rc ? rc : fr;
 }
 
 // ---------------------------------------------------------------------------

@@ -133,12 +133,29 @@ class Schema:
 
 
 def _ptr(x):
-    """Device/host address of a torch tensor, an int or None."""
+    """Address of a torch tensor, a numpy array, an int or None."""
     if x is None:
         return None
     if isinstance(x, int):
         return x
-    return x.data_ptr()
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+def host_register(ptr, nbytes, ctx=None):
+    """xdrg_host_register: pin (and map) a host buffer once, as a caller's
+    pooled direct buffers would be; registered spans skip the staging
+    ring's bounce copy and may take mapped=True."""
+    rc = lib().xdrg_host_register(ctx.handle if ctx is not None else None, _ptr(ptr), int(nbytes))
+    if rc:
+        _raise(rc, ctx.handle if ctx is not None else None)
+
+
+def host_unregister(ptr, ctx=None):
+    rc = lib().xdrg_host_unregister(ctx.handle if ctx is not None else None, _ptr(ptr))
+    if rc:
+        _raise(rc, ctx.handle if ctx is not None else None)
 
 
 def columns_array(cols):
@@ -176,10 +193,23 @@ class Context:
         if rc:
             _raise(rc, self._h)
 
+    def host_staging(self, slot_bytes, slots):
+        """xdrg_ctx_host_staging: the ring the host=True calls move through."""
+        rc = lib().xdrg_ctx_host_staging(self._h, int(slot_bytes), int(slots))
+        if rc:
+            _raise(rc, self._h)
+
+    @staticmethod
+    def _flags(framed, async_, host, mapped):
+        return ((abi.FRAME_RM if framed else 0) | (abi.ASYNC if async_ else 0) |
+                (abi.HOST_PTRS if host or mapped else 0) | (abi.HOST_MAPPED if mapped else 0))
+
     def encode(self, schema, cols, n, out, out_cap, rec_offsets=None, framed=False, async_=False,
-               out_len=None):
-        """xdrg_encode_batch -> bytes written (sync mode)."""
-        flags = (abi.FRAME_RM if framed else 0) | (abi.ASYNC if async_ else 0)
+               out_len=None, host=False, mapped=False):
+        """xdrg_encode_batch -> bytes written (sync mode).  host=True: every
+        pointer is host memory (XDRG_HOST_PTRS, the staging ring); mapped=True:
+        registered host memory accessed in place (XDRG_HOST_MAPPED)."""
+        flags = self._flags(framed, async_, host, mapped)
         carr = cols if isinstance(cols, ctypes.Array) else columns_array(cols)
         ol = ctypes.c_uint64(0)
         olp = _ptr(out_len) if async_ else ctypes.addressof(ol)
@@ -190,9 +220,10 @@ class Context:
         return None if async_ else ol.value
 
     def decode(self, schema, xdr, xdr_len, n, cols, rec_offsets=None, framed=False, async_=False,
-               first_bad=None, err=None, raise_on_error=True):
-        """xdrg_decode_batch -> (status, first_bad, err) in sync mode."""
-        flags = (abi.FRAME_RM if framed else 0) | (abi.ASYNC if async_ else 0)
+               first_bad=None, err=None, raise_on_error=True, host=False, mapped=False):
+        """xdrg_decode_batch -> (status, first_bad, err) in sync mode (host /
+        mapped as for encode)."""
+        flags = self._flags(framed, async_, host, mapped)
         carr = cols if isinstance(cols, ctypes.Array) else columns_array(cols)
         fb = ctypes.c_uint64(0)
         er = ctypes.c_int(0)

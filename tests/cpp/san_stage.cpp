@@ -1,0 +1,460 @@
+// san_stage.cpp — TEST INFRASTRUCTURE: the XDRG_HOST_PTRS staging pipeline
+// (oncrpc4j_amd/csrc/host_stage.h) under ASan + UBSan on the CPU, no GPU.
+//
+// CpuExec runs the pipeline's executor interface synchronously: the "device"
+// slots are a host arena (every copy is bounds-checked against it), pinned
+// spans are chosen pseudo-randomly so both the direct and the bounce paths
+// run, and the "kernels" are the oracle's batch codec (oracle/xdr_oracle.c,
+// the restatement of xdr/Xdr.java) on the slot-resident chunk.  Every batch
+// is checked against the oracle on the whole batch: stream bytes, record
+// offsets, out_len, CAPACITY, first_bad / error code and the decoded columns
+// of the records before first_bad.  Slots are a few KiB, so batches cut into
+// many chunks and some records outgrow a slot (the ring grows).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../../oncrpc4j_amd/csrc/host_stage.h"
+#include "../../oracle/xdr_oracle.h"
+
+#define CHECK(c)                                                                        \
+    do {                                                                                \
+        if (!(c)) {                                                                     \
+            std::fprintf(stderr, "%s:%d: check failed: %s\n", __FILE__, __LINE__, #c); \
+            std::exit(1);                                                               \
+        }                                                                               \
+    } while (0)
+
+using namespace xdrg;
+
+static uint32_t nsz_of(uint32_t t) {
+    switch (t) {
+    case XDRG_T_INT: case XDRG_T_UINT: case XDRG_T_ENUM: case XDRG_T_FLOAT: return 4;
+    case XDRG_T_HYPER: case XDRG_T_UHYPER: case XDRG_T_DOUBLE: return 8;
+    case XDRG_T_SHORT: return 2;
+    default: return 1;
+    }
+}
+static uint32_t xsz_of(uint32_t t) {
+    switch (t) {
+    case XDRG_T_HYPER: case XDRG_T_UHYPER: case XDRG_T_DOUBLE: return 8;
+    case XDRG_T_OPAQUE: case XDRG_T_STRING: return 1;
+    default: return 4;
+    }
+}
+
+struct CpuExec {
+    std::vector<uint8_t> arena, bnc;
+    uint32_t ns;
+    uint64_t sb;
+    int pin_mode;   // 0 none pinned, 1 all, 2 mixed
+    const xdrg_field *fields;
+    size_t nf;
+    const xdrg_cond *conds;
+    size_t nc;
+    uint64_t res[hs::kMaxSlots][66] = {};
+    uint32_t nres[hs::kMaxSlots] = {};
+    uint64_t grows = 0, bounced = 0, direct = 0;
+
+    uint32_t nslots() const { return ns; }
+    uint64_t slot_bytes() const { return sb; }
+    uint8_t *slot(uint32_t s) { return arena.data() + (uint64_t)s * sb; }
+    uint8_t *bounce(uint32_t s) {
+        if (bnc.size() != arena.size()) bnc.assign(arena.size(), 0xcd);
+        return bnc.data() + (uint64_t)s * sb;
+    }
+    bool pinned(const void *p, uint64_t n) const {
+        (void)n;
+        if (pin_mode < 2) return pin_mode == 1;
+        return (((uintptr_t)p >> 4) * 0x9E3779B97F4A7C15ull) >> 63;
+    }
+    bool in_arena(const uint8_t *p, uint64_t n) const {
+        const uint8_t *a = arena.data(), *b = bnc.data();
+        return (p >= a && p + n <= a + arena.size()) || (!bnc.empty() && p >= b && p + n <= b + bnc.size());
+    }
+    int wait_slot(uint32_t) { return XDRG_OK; }
+    int dma_h2d(uint8_t *dev, const void *host, uint64_t n) {
+        CHECK(dev >= arena.data() && dev + n <= arena.data() + arena.size());
+        std::memcpy(dev, host, n);
+        (in_arena((const uint8_t *)host, n) ? bounced : direct) += 1;
+        return XDRG_OK;
+    }
+    int h2d_done(uint32_t) { return XDRG_OK; }
+    int kernel_begin(uint32_t s) {
+        res[s][0] = res[s][1] = 0;
+        return XDRG_OK;
+    }
+    int add_u64(int, uint64_t *p, uint64_t n, uint64_t d) {
+        CHECK(in_arena((uint8_t *)p, n * 8));
+        for (uint64_t i = 0; i < n; ++i) p[i] += d;
+        return XDRG_OK;
+    }
+    int encode(uint32_t s, const xdrg_column *dc, uint64_t m, uint8_t *out, uint64_t cap, uint64_t *rec,
+               uint32_t flags) {
+        CHECK(in_arena(out, cap));
+        uint64_t len = 0;
+        const int rc = xo_encode_batch_cond(fields, nf, conds, nc, dc, m, out, cap, rec, flags, &len);
+        CHECK(rc == XDRG_OK);   // the slot span is sized to the chunk's bound
+        res[s][0] = len;
+        return XDRG_OK;
+    }
+    int decode(uint32_t s, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m, xdrg_column *dc,
+               uint32_t flags) {
+        CHECK(len == 0 || in_arena(in, len));
+        uint64_t fb = 0;
+        int err = 0;
+        (void)xo_decode_batch_cond(fields, nf, conds, nc, in, len, rec, m, dc, flags, &fb, &err);
+        res[s][0] = fb;
+        res[s][1] = (uint64_t)(uint32_t)err;
+        return XDRG_OK;
+    }
+    int kernel_end(uint32_t s, const uint64_t *const *extra, uint32_t ne) {
+        CHECK(ne <= 64);
+        for (uint32_t j = 0; j < ne; ++j) {
+            CHECK(in_arena((const uint8_t *)extra[j], 8));
+            res[s][2 + j] = *extra[j];
+        }
+        nres[s] = 2 + ne;
+        return XDRG_OK;
+    }
+    int wait_kernel(uint32_t s, uint64_t *w) {
+        std::memcpy(w, res[s], 8 * nres[s]);
+        return XDRG_OK;
+    }
+    int d2h_begin(uint32_t) { return XDRG_OK; }
+    int dma_d2h(void *host, const uint8_t *dev, uint64_t n) {
+        CHECK(dev >= arena.data() && dev + n <= arena.data() + arena.size());
+        std::memcpy(host, dev, n);
+        return XDRG_OK;
+    }
+    int dma_d2h_2d(void *host, uint64_t hp, const uint8_t *dev, uint64_t dp, uint64_t w, uint64_t rows) {
+        CHECK(dev >= arena.data() && dev + dp * (rows - 1) + w <= arena.data() + arena.size());
+        for (uint64_t r = 0; r < rows; ++r) std::memcpy((uint8_t *)host + r * hp, dev + r * dp, w);
+        return XDRG_OK;
+    }
+    int d2h_done(uint32_t) { return XDRG_OK; }
+    int grow(uint64_t bytes) {
+        if (bytes <= sb) return XDRG_OK;
+        sb = bytes;
+        arena.assign((uint64_t)ns * sb, 0xab);
+        bnc.clear();
+        ++grows;
+        return XDRG_OK;
+    }
+};
+
+// A random batch: columns owned by vectors, fixed fields in SoA, AoS (one
+// record struct with padding) or constant (encode only) layout.
+struct Batch {
+    std::vector<xdrg_field> f;
+    std::vector<xdrg_cond> c;
+    std::vector<int32_t> cvals{0};
+    uint64_t n = 0;
+    std::vector<std::vector<uint8_t>> data;   // per field
+    std::vector<std::vector<uint64_t>> offs;  // per dynamic field
+    std::vector<uint8_t> aos;                 // AoS record array (fixed fields)
+    uint64_t aos_stride = 0;
+    std::vector<uint64_t> aos_off;            // per field: byte offset in the AoS record (UINT64_MAX: SoA)
+    std::vector<xdrg_column> cols;
+    hs::Schema hs;
+};
+
+static void random_schema(std::mt19937_64 &g, Batch &b) {
+    static const uint32_t types[] = {XDRG_T_INT, XDRG_T_UINT, XDRG_T_ENUM, XDRG_T_BOOL, XDRG_T_HYPER,
+                                     XDRG_T_UHYPER, XDRG_T_FLOAT, XDRG_T_DOUBLE, XDRG_T_SHORT, XDRG_T_BYTE,
+                                     XDRG_T_OPAQUE, XDRG_T_STRING};
+    const size_t nf = 1 + g() % 7;
+    int disc = -1;
+    for (size_t k = 0; k < nf; ++k) {
+        xdrg_field x{types[g() % 12], 0, 0, 0};
+        if (x.type == XDRG_T_STRING) x.kind = XDRG_K_DYNAMIC;
+        else if (x.type == XDRG_T_BOOL) x.kind = XDRG_K_SCALAR;
+        else if (x.type == XDRG_T_OPAQUE) x.kind = 1 + g() % 2;
+        else x.kind = g() % 3;
+        if (x.kind == XDRG_K_FIXED) x.count = (uint32_t)(g() % 6);
+        b.f.push_back(x);
+        if (x.type == XDRG_T_BOOL && disc < 0) disc = (int)k;
+        else if (disc >= 0 && g() % 3 == 0) b.c.push_back({(uint32_t)k, (uint32_t)disc, 1, 1, nullptr});
+    }
+    for (auto &c : b.c) c.values = b.cvals.data();
+    uint64_t fixed = 0;
+    bool var = !b.c.empty();
+    for (auto &x : b.f) {
+        const uint32_t ns = nsz_of(x.type), xs = xsz_of(x.type);
+        uint32_t xb = 0;
+        if (x.kind != XDRG_K_DYNAMIC) {
+            const uint64_t cnt = x.kind == XDRG_K_FIXED ? x.count : 1;
+            xb = (uint32_t)(x.type == XDRG_T_OPAQUE ? cnt + ((4 - (cnt & 3)) & 3) : cnt * xs);
+            fixed += xb;
+        } else {
+            var = true;
+        }
+        b.hs.f.push_back({x.type, x.kind, x.count, ns, xs, xb});
+    }
+    b.hs.fixed_part = fixed;
+    b.hs.var_size = var;
+}
+
+static void random_values(std::mt19937_64 &g, Batch &b, bool for_encode) {
+    const size_t nf = b.f.size();
+    b.data.assign(nf, {});
+    b.offs.assign(nf, {});
+    b.aos_off.assign(nf, UINT64_MAX);
+    b.cols.assign(nf, xdrg_column{nullptr, 0, nullptr, 0});
+    // AoS record: the fixed fields that draw it, each aligned to its element size
+    uint64_t so = 0;
+    const bool aos = g() % 2;
+    for (size_t k = 0; k < nf; ++k) {
+        const auto &x = b.f[k];
+        if (x.kind == XDRG_K_DYNAMIC || !aos || g() % 4 == 0) continue;
+        const uint64_t e = hs::fixed_elem_bytes(b.hs.f[k]);
+        if (!e) continue;
+        const uint64_t al = nsz_of(x.type);   // natural alignment (the oracle loads elements in place)
+        so = (so + al - 1) / al * al + (g() % 3 == 0 ? al : 0);   // sometimes a gap (partial coverage)
+        b.aos_off[k] = so;
+        so += e;
+    }
+    b.aos_stride = (so + 7) / 8 * 8 + (g() % 2) * 8;
+    b.aos.assign(b.aos_stride * b.n + 1, 0);
+    for (auto &v : b.aos) v = (uint8_t)g();
+    for (size_t k = 0; k < nf; ++k) {
+        const auto &x = b.f[k];
+        xdrg_column &col = b.cols[k];
+        const uint32_t ns = nsz_of(x.type);
+        if (x.kind == XDRG_K_DYNAMIC) {
+            auto &o = b.offs[k];
+            o.assign(b.n + 1, 0);
+            for (uint64_t i = 0; i < b.n; ++i) o[i + 1] = o[i] + (g() % 8 == 0 ? g() % 300 : g() % 12);
+            b.data[k].assign(o[b.n] * ns + 8, 0);
+            for (auto &v : b.data[k]) v = (uint8_t)g();
+            col.data = b.data[k].data();
+            col.offsets = o.data();
+            col.cap = o[b.n];
+            continue;
+        }
+        const uint64_t e = hs::fixed_elem_bytes(b.hs.f[k]);
+        if (b.aos_off[k] != UINT64_MAX) {
+            col.data = b.aos.data() + b.aos_off[k];
+            col.stride = (int64_t)b.aos_stride;
+        } else if (for_encode && e && g() % 6 == 0) {
+            b.data[k].assign(e, 0);
+            for (auto &v : b.data[k]) v = (uint8_t)g();
+            col.data = b.data[k].data();
+            col.stride = XDRG_STRIDE_CONST;
+        } else {
+            b.data[k].assign(e * b.n + 8, 0);
+            for (auto &v : b.data[k]) v = (uint8_t)g();
+            col.data = b.data[k].data();
+            col.stride = 0;
+        }
+        if (x.type == XDRG_T_BOOL) {   // discriminants and bools: 0 / 1
+            for (uint64_t i = 0; i < (col.stride == XDRG_STRIDE_CONST ? 1 : b.n); ++i) {
+                uint8_t *p = (uint8_t *)col.data + (col.stride == XDRG_STRIDE_CONST ? 0 : i * (col.stride ? col.stride : 1));
+                *p = (uint8_t)(g() % 2);
+            }
+        }
+    }
+}
+
+// Empty decode targets with the same layout family as b.
+static void empty_like(std::mt19937_64 &g, const Batch &b, Batch &o, uint64_t slack) {
+    o.f = b.f;
+    o.c = b.c;
+    o.hs = b.hs;
+    o.n = b.n;
+    const size_t nf = b.f.size();
+    o.data.assign(nf, {});
+    o.offs.assign(nf, {});
+    o.aos_off = b.aos_off;
+    o.aos_stride = b.aos_stride;
+    o.aos.assign(b.aos.size(), 0x5a);
+    o.cols.assign(nf, xdrg_column{nullptr, 0, nullptr, 0});
+    for (size_t k = 0; k < nf; ++k) {
+        const auto &x = b.f[k];
+        xdrg_column &col = o.cols[k];
+        const uint32_t ns = nsz_of(x.type);
+        if (x.kind == XDRG_K_DYNAMIC) {
+            uint64_t cap = b.offs[k][b.n] + slack;
+            if (g() % 8 == 0 && cap) cap = g() % cap;   // too small: CAPACITY
+            o.offs[k].assign(b.n + 1, 0x77);
+            o.data[k].assign(cap * ns + 8, 0x33);
+            col.data = o.data[k].data();
+            col.offsets = o.offs[k].data();
+            col.cap = cap;
+            continue;
+        }
+        const uint64_t e = hs::fixed_elem_bytes(b.hs.f[k]);
+        if (o.aos_off[k] != UINT64_MAX) {
+            col.data = o.aos.data() + o.aos_off[k];
+            col.stride = (int64_t)o.aos_stride;
+        } else {
+            o.data[k].assign(e * b.n + 8, 0x44);
+            col.data = o.data[k].data();
+            col.stride = 0;
+        }
+    }
+}
+
+static void compare_prefix(const Batch &a, const Batch &b, uint64_t upto) {
+    for (size_t k = 0; k < a.f.size(); ++k) {
+        const auto &x = a.f[k];
+        const uint32_t ns = nsz_of(x.type);
+        if (x.kind == XDRG_K_DYNAMIC) {
+            // (for n = 0 the oracle leaves offsets[0] alone; the engine writes 0)
+            CHECK(a.n || a.offs[k][0] == 0);
+            for (uint64_t i = 0; i <= upto && a.n; ++i) {
+                if (a.offs[k][i] != b.offs[k][i])
+                    std::fprintf(stderr, "field %zu rec %llu: staged %llu whole %llu (upto %llu, n %llu)\n", k,
+                                 (unsigned long long)i, (unsigned long long)a.offs[k][i],
+                                 (unsigned long long)b.offs[k][i], (unsigned long long)upto, (unsigned long long)a.n);
+                CHECK(a.offs[k][i] == b.offs[k][i]);
+            }
+            if (a.n && std::memcmp(a.data[k].data(), b.data[k].data(), a.offs[k][upto] * ns) != 0) {
+                uint64_t j = 0;
+                while (a.data[k][j] == b.data[k][j]) ++j;
+                std::fprintf(stderr, "field %zu values differ at byte %llu of %llu (type %u)\n", k, (unsigned long long)j,
+                             (unsigned long long)(a.offs[k][upto] * ns), a.f[k].type);
+                CHECK(false);
+            }
+            continue;
+        }
+        const uint64_t e = hs::fixed_elem_bytes(a.hs.f[k]);
+        const int64_t st = a.cols[k].stride ? a.cols[k].stride : (int64_t)e;
+        for (uint64_t i = 0; i < upto; ++i)
+            CHECK(std::memcmp((const uint8_t *)a.cols[k].data + i * st, (const uint8_t *)b.cols[k].data + i * st, e) == 0);
+    }
+    // AoS bytes no field covers are the caller's: never written by a decode
+    if (!a.aos.empty()) {
+        std::vector<bool> cov(a.aos_stride, false);
+        for (size_t k = 0; k < a.f.size(); ++k)
+            if (a.aos_off[k] != UINT64_MAX)
+                for (uint64_t j = 0; j < hs::fixed_elem_bytes(a.hs.f[k]); ++j) cov[a.aos_off[k] + j] = true;
+        for (uint64_t i = 0; i < a.n; ++i)
+            for (uint64_t j = 0; j < a.aos_stride; ++j)
+                if (!cov[j]) CHECK(a.aos[i * a.aos_stride + j] == 0x5a);
+    }
+}
+
+static CpuExec make_exec(std::mt19937_64 &g, const Batch &b) {
+    CpuExec x;
+    x.ns = 1 + g() % 4;
+    x.sb = 2048 + (g() % 16) * 1024;
+    x.arena.assign((uint64_t)x.ns * x.sb, 0xab);
+    x.pin_mode = (int)(g() % 3);
+    x.fields = b.f.data();
+    x.nf = b.f.size();
+    x.conds = b.c.empty() ? nullptr : b.c.data();
+    x.nc = b.c.size();
+    return x;
+}
+
+int main(int argc, char **argv) {
+    const int rounds = argc > 1 ? std::atoi(argv[1]) : 300;
+    std::mt19937_64 g(0x0DCAC4E5);
+    uint64_t chunks_grown = 0, errs = 0, caps = 0, bounced = 0, direct = 0;
+    for (int r = 0; r < rounds; ++r) {
+        Batch b;
+        random_schema(g, b);
+        b.n = g() % 5 == 0 ? g() % 4 : g() % 1500;
+        random_values(g, b, true);
+        const uint32_t flags = g() % 2 ? XDRG_FRAME_RM : 0;
+        // whole-batch oracle
+        std::vector<uint8_t> want(1 << 22);
+        std::vector<uint64_t> wro(b.n + 1);
+        uint64_t wlen = 0;
+        int rc = xo_encode_batch_cond(b.f.data(), b.f.size(), b.c.empty() ? nullptr : b.c.data(), b.c.size(),
+                                      b.cols.data(), b.n, want.data(), want.size(), wro.data(), flags, &wlen);
+        CHECK(rc == XDRG_OK);
+        // staged encode
+        {
+            CpuExec x = make_exec(g, b);
+            const bool tight = g() % 6 == 0 && wlen > 0;
+            const uint64_t cap = tight ? g() % wlen : wlen + g() % 64;
+            std::vector<uint8_t> out(cap + 16, 0xee);
+            std::vector<uint64_t> ro(b.n + 1, 0x99);
+            uint64_t len = 0;
+            rc = hs::stage_encode(x, b.hs, b.cols.data(), b.n, out.data(), cap, g() % 4 ? ro.data() : nullptr, flags, &len);
+            chunks_grown += x.grows;
+            bounced += x.bounced;
+            direct += x.direct;
+            if (tight) {
+                if (!(rc == XDRG_E_CAPACITY && len == wlen))
+                    std::fprintf(stderr, "round %d: rc %d len %llu want %llu cap %llu var %d n %llu\n", r, rc,
+                                 (unsigned long long)len, (unsigned long long)wlen, (unsigned long long)cap,
+                                 (int)b.hs.var_size, (unsigned long long)b.n);
+                CHECK(rc == XDRG_E_CAPACITY && len == wlen);
+                ++caps;
+            } else {
+                if (!(rc == XDRG_OK && len == wlen)) {
+                    std::fprintf(stderr, "round %d rc %d len %llu want %llu flags %u n %llu nf %zu nc %zu\n", r, rc,
+                                 (unsigned long long)len, (unsigned long long)wlen, flags, (unsigned long long)b.n,
+                                 b.f.size(), b.c.size());
+                    for (size_t k = 0; k < b.f.size(); ++k)
+                        std::fprintf(stderr, "  f%zu t%u k%u c%u stride %lld\n", k, b.f[k].type, b.f[k].kind, b.f[k].count,
+                                     (long long)b.cols[k].stride);
+                    for (auto &c : b.c) std::fprintf(stderr, "  cond field %u disc %u\n", c.field, c.disc);
+                }
+                CHECK(rc == XDRG_OK && len == wlen);
+                CHECK(std::memcmp(out.data(), want.data(), wlen) == 0);
+                for (uint64_t i = wlen; i < out.size(); ++i) CHECK(out[i] == 0xee);
+            }
+            if (rc == XDRG_OK && ro[0] != 0x99) {   // record offsets asked for
+                for (uint64_t i = 0; i <= b.n; ++i) CHECK(ro[i] == wro[i]);
+            }
+        }
+        // staged decode (no constant columns on this side)
+        Batch src;
+        src.f = b.f;
+        src.c = b.c;
+        src.hs = b.hs;
+        src.n = b.n;
+        for (auto &c : src.c) c.values = b.cvals.data();
+        random_values(g, src, false);
+        for (auto &c : src.c) c.values = src.cvals.data();
+        rc = xo_encode_batch_cond(src.f.data(), src.f.size(), src.c.empty() ? nullptr : src.c.data(), src.c.size(),
+                                  src.cols.data(), src.n, want.data(), want.size(), wro.data(), flags, &wlen);
+        CHECK(rc == XDRG_OK);
+        std::vector<uint8_t> stream(want.begin(), want.begin() + (long)wlen);
+        uint64_t in_len = wlen;
+        const int mut = (int)(g() % 5);
+        if (mut == 1 && in_len) in_len = (g() % in_len) & ~3ull;                   // truncated
+        if (mut == 2 && b.n) {                                                     // a corrupted word
+            const uint64_t i = g() % b.n, o = wro[i] + ((g() % 4) * 4);
+            if (o + 4 <= wlen) { stream[o] = 0x80; stream[o + 1] = (uint8_t)g(); }
+        }
+        stream.resize(wlen + 16, 0);
+        const bool use_ro = b.hs.var_size || b.hs.fixed_part == 0 || g() % 2;   // (the oracle wants extents for 0-byte records)
+        Batch a, o;
+        std::mt19937_64 g2 = g;
+        empty_like(g, src, a, 0);
+        empty_like(g2, src, o, 0);   // same capacities as a
+        for (auto &c : a.c) c.values = src.cvals.data();
+        uint64_t fb_w = 0, fb = 0;
+        int err_w = 0, err = 0;
+        const int rc_w = xo_decode_batch_cond(src.f.data(), src.f.size(), src.c.empty() ? nullptr : src.c.data(),
+                                              src.c.size(), stream.data(), in_len, use_ro ? wro.data() : nullptr,
+                                              src.n, o.cols.data(), flags, &fb_w, &err_w);
+        CpuExec x = make_exec(g, src);
+        rc = hs::stage_decode(x, src.hs, stream.data(), in_len, use_ro ? wro.data() : nullptr, src.n, a.cols.data(),
+                              flags, &fb, &err);
+        if (getenv("VERB"))
+            std::fprintf(stderr, "round %d decode rc %d fb %llu err %d | whole %d %llu %d | n %llu in_len %llu/%llu ro %d mut %d slots %u x %llu\n",
+                         r, rc, (unsigned long long)fb, err, rc_w, (unsigned long long)fb_w, err_w,
+                         (unsigned long long)src.n, (unsigned long long)in_len, (unsigned long long)wlen, (int)use_ro, mut,
+                         x.ns, (unsigned long long)x.sb);
+        CHECK(rc == rc_w && fb == fb_w && err == err_w);
+        if (rc) ++errs;
+        compare_prefix(a, o, fb);
+        chunks_grown += x.grows;
+        bounced += x.bounced;
+        direct += x.direct;
+    }
+    CHECK(chunks_grown > 0 && errs > 0 && caps > 0 && bounced > 0 && direct > 0);
+    std::printf("san_stage: %d rounds ok (ring grown %llu times, %llu decode errors, %llu capacity, "
+                "%llu bounced / %llu direct copies)\n",
+                rounds, (unsigned long long)chunks_grown, (unsigned long long)errs, (unsigned long long)caps,
+                (unsigned long long)bounced, (unsigned long long)direct);
+    return 0;
+}

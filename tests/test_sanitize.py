@@ -28,3 +28,13 @@ def test_host_code_under_asan_ubsan():
     out = _build_and_run(os.path.join(ROOT, "oncrpc4j_amd", "csrc"),
                          os.path.join(ROOT, "oncrpc4j_amd", "csrc", "build", "san", "san_host"))
     assert "san_host: ok" in out
+
+
+def test_host_staging_pipeline_under_asan_ubsan():
+    """XDRG_HOST_PTRS bookkeeping (oncrpc4j_amd/csrc/host_stage.h): chunking,
+    slot layout, bounce copies, rebasing, ring growth, CAPACITY and first-bad
+    errors, run with the oracle as the kernels and checked against the oracle
+    on whole batches (tests/cpp/san_stage.cpp)."""
+    out = _build_and_run(os.path.join(ROOT, "oncrpc4j_amd", "csrc"),
+                         os.path.join(ROOT, "oncrpc4j_amd", "csrc", "build", "san", "san_stage"), ["400"])
+    assert "400 rounds ok" in out
