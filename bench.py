@@ -272,6 +272,8 @@ class Workload:
                          "configs[3]: 32 Mi records int32 + string(8..256) + int32<0..16>")
         self.xdr = torch.empty(self.xlen, dtype=torch.uint8, device=dev)
         self.sch = engine.Schema(self.fields)
+        # receive side of a record-marked stream: the mark walk's message offsets
+        self.scan_offs = torch.empty(n + 1, dtype=torch.int64, device=dev) if framed and decode_targets else None
         # encode reads native + writes XDR, decode the reverse
         self.enc_bytes = self.native_bytes + self.xlen
         self.bytes_per_step = 2 * self.enc_bytes
@@ -301,6 +303,16 @@ class Workload:
         self.encode()
         self.decode()
 
+    def receive(self):
+        """The receive pipeline of a record-marked stream (RpcMessageParserTCP
+        -> RpcProtocolFilter): xdrg_frame_scan walks the marks, then
+        xdrg_decode_batch(XDRG_FRAME_RM) decodes the messages at the offsets
+        the walk found (never the encoder's)."""
+        m = self.ctx.frame_scan(self.xdr, self.xlen, self.scan_offs, self.n)
+        assert m == self.n, f"frame scan found {m} of {self.n} messages"
+        self.ctx.decode(self.sch, self.xdr, self.xlen, self.n, self.cout, rec_offsets=self.scan_offs,
+                        framed=True, async_=True)
+
     def clear_outputs(self):
         """Zero the XDR stream and every decode target (tools/sweep_rec.py:
         each kernel variant must round-trip on its own writes)."""
@@ -318,6 +330,13 @@ class Workload:
 
     def offsets_view(self):
         return self.rec_offsets
+
+    def check_receive(self):
+        import torch
+        want = self.rec_offsets if self.rec_offsets is not None else \
+            torch.arange(self.n + 1, dtype=torch.int64, device=self.xdr.device) * (self.xlen // self.n)
+        assert torch.equal(self.scan_offs, want), "frame scan offsets differ from the stream's records"
+        self.check()
 
     def check(self):
         import torch
@@ -468,6 +487,8 @@ def measure(R, args, make, cfg, framed, n, steps, warmup, with_gather):
                          "GiB_s": round(wl.enc_bytes * R.world * steps / t_dec / GIB, 3),
                          "Mrec_s": round(recs / t_dec / 1e6, 2)},
          "roofline": roof, "kernel_ms_per_step": step_ms, "gather": None}
+    if framed and hasattr(wl, "receive") and wl.scan_offs is not None:
+        e["receive"] = receive_leg(R, wl, steps)
     if R.world > 1 and with_gather:
         if wl.gatherable(R.world):
             e["gather"] = gather_leg(R, wl, n, args.gather_reps)
@@ -475,6 +496,40 @@ def measure(R, args, make, cfg, framed, n, steps, warmup, with_gather):
             e["gather"] = {"skipped": f"{R.world} x {wl.xlen} stream bytes do not fit one GPU "
                                       "next to their 1-rank reference"}
     return e, wl
+
+
+def receive_leg(R, wl, steps):
+    """Receive pipeline on the bench clock: frame scan of the record-marked
+    stream, then the decode at the scan's offsets (RpcMessageParserTCP.java:
+    44-140 -> RpcProtocolFilter).  Bytes = the decode direction's (stream read,
+    native written); the walk's roofline = stream bytes read + 8 B of offsets
+    per message, over its average call (host round trips included)."""
+    from oncrpc4j_amd import abi
+    wl.receive()
+    R.sync()
+    wl.check_receive()
+    wl.reset_stats()
+    dt = R.timed(lambda: [wl.receive() for _ in range(steps)])
+    R.sync()
+    wl.check_receive()
+    ns, ms_s = wl.ctx.kernel_stats(abi.KERNEL_FRAME_SCAN)
+    walk_ms = ms_s / max(ns, 1)
+    walk_bytes = wl.xlen + 8 * (wl.n + 1)
+    walk_gbs = walk_bytes / (walk_ms * 1e-3) / 1e9 if walk_ms > 0 else 0.0
+    step_ms = {}
+    for kid, name in ((0, "fixed_encode"), (1, "fixed_decode"), (2, "var_size"), (3, "var_scan"),
+                      (4, "var_encode"), (5, "var_decode"), (6, "frame_scan")):
+        c, ms = wl.ctx.kernel_stats(kid)
+        if c:
+            step_ms[name] = round(ms / steps, 4)
+    return {"ms_per_step": round(dt / steps * 1e3, 4),
+            "GiB_s": round(wl.enc_bytes * R.world * steps / dt / GIB, 3),
+            "Mrec_s": round(wl.n * R.world * steps / dt / 1e6, 2),
+            "kernel_ms_per_step": step_ms,
+            "frame_scan": {"calls": ns, "avg_ms": round(walk_ms, 4), "bytes_per_call": walk_bytes,
+                           "achieved_GBps": round(walk_gbs, 1), "peak": HBM_PEAK_GBS,
+                           "frac": round(walk_gbs / HBM_PEAK_GBS, 4)},
+            "offsets": "the frame scan's (checked equal to the stream's record offsets)"}
 
 
 # ---------------------------------------------------------------------------
@@ -614,13 +669,15 @@ def _host_buffer(nbytes, register):
     return m, a, ptr
 
 
-def host_inclusive(device, sch, n, reps=3):
+def host_inclusive(device, sch, n, reps=3, slot_bytes=64 << 20, slots=4,
+                   legs=("staged", "staged_dma", "mapped", "staged_pageable")):
     """Host-resident batches through the C-ABI (XDRG_HOST_PTRS), configs[1]:
     a server's two directions at once, one context per thread (Xdr's single
     owner, Xdr.java:56,71) — replies encode native records from host memory
     into a host XDR stream, requests decode a received host stream into host
     records.  Legs: `staged` (the context's staging ring: chunked H2D /
-    kernels / D2H on its own streams) and `mapped` (XDRG_HOST_MAPPED: the
+    kernels / D2H on its own streams, the copies by copy kernels),
+    `staged_dma` (the same with the copies on the DMA engines) and `mapped` (XDRG_HOST_MAPPED: the
     kernels read and write the host buffers in place over PCIe), both on
     buffers pinned with xdrg_host_register; `staged_pageable` the same ring on
     unregistered memory (pinned bounce copies), on a quarter of the records.
@@ -640,7 +697,9 @@ def host_inclusive(device, sch, n, reps=3):
         nat.view(np.int32)[:] = rng.integers(-2**31, 2**31 - 1, m * 8, dtype=np.int32)
         ce, cd = engine.Context(device), engine.Context(device)
         for c in (ce, cd):
-            c.host_staging(64 << 20, 4)
+            c.host_staging(slot_bytes, slots)
+            if mode == "staged_dma":   # the ring's copies on the DMA engines instead of copy kernels
+                c.tune(26, 0)
         kw = {"mapped": True} if mode == "mapped" else {"host": True}
         # the request stream a peer sent: these records' encoding
         ce.encode(sch, aos_columns(fields, p_nat, 32, offs), m, p_req, m * 32, host=True)
@@ -670,22 +729,24 @@ def host_inclusive(device, sch, n, reps=3):
         for mm, _, ptr in bufs:
             if register:
                 engine.host_unregister(ptr)
-        del nat, xdr, req, back
-        for mm, _, _ in bufs:
-            mm.close()
+        del nat, xdr, req, back, bufs   # the mappings go with their last reference
         return {"GiB_s": round(m * 128 / dt / GIB, 3), "ms": round(dt * 1e3, 3), "records": m,
                 "pcie_GBps": round(4 * m * 32 / dt / 1e9, 2), "roundtrip_ok": ok}
 
-    res = {"staged": leg(n, True, "staged"), "mapped": leg(n, True, "mapped"),
-           "staged_pageable": leg(max(n // 4, 1), False, "staged")}
-    best = max((k for k in ("staged", "mapped") if res[k]["roundtrip_ok"]), key=lambda k: res[k]["GiB_s"],
+    res = {}
+    for name in legs:
+        res[name] = leg(max(n // 4, 1), False, "staged") if name == "staged_pageable" else \
+            leg(n, True, name)   # staged, staged_dma, mapped
+    best = max((k for k in ("staged", "staged_dma", "mapped") if k in res and res[k]["roundtrip_ok"]),
+               key=lambda k: res[k]["GiB_s"],
                default="staged")
     return {"value": res[best]["GiB_s"], "unit": "GiB/s", "ms": res[best]["ms"], "records": n,
             "pcie_bytes": 4 * n * 32, "pcie_GBps": res[best]["pcie_GBps"],
             "roundtrip_ok": all(r["roundtrip_ok"] for r in res.values()), "best": best, "legs": res,
+            "slots": [slots, slot_bytes],
             "method": "C-ABI xdrg_encode_batch / xdrg_decode_batch with XDRG_HOST_PTRS, replies and requests at "
-                      "once on two contexts (two threads); staged = the context's staging ring (4 x 64 MiB "
-                      "slots, chunked H2D / kernels / D2H on the context's copy and compute streams), mapped = "
+                      "once on two contexts (two threads); staged = the context's staging ring (slots x bytes "
+                      "above, chunked H2D / kernels / D2H on the context's copy and compute streams), mapped = "
                       "XDRG_HOST_MAPPED (kernels on the registered host buffers over PCIe); buffers pinned with "
                       "xdrg_host_register, staged_pageable on unregistered memory (bounce copies)"}
 
@@ -721,7 +782,7 @@ def run_rank(args):
 
     extra = []
     if args.extra:
-        for cfg, framed in ((2, True), (3, False), (4, False)):
+        for cfg, framed in ((2, True), (3, False), (4, False), (4, True)):
             if (cfg, framed) == (args.config, bool(args.framed)):
                 continue
             e, w = measure(R, args, make, cfg, framed, SIZES[cfg], args.extra_steps, 2,

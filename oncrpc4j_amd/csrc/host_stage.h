@@ -197,7 +197,7 @@ inline void enc_layout(const EncPlan &p, uint64_t lo, uint64_t m, Layout &L) {
         const uint64_t a = p.cols[k].offsets[lo], e = p.cols[k].offsets[lo + m];
         L.vcap[k] = e - a;
         L.val[k] = b.take((e - a) * s.f[k].nsz, (uintptr_t)((const uint8_t *)p.cols[k].data + a * s.f[k].nsz));
-        L.off[k] = b.take((m + 1) * 8);
+        L.off[k] = b.take((m + 1) * 8, (uintptr_t)(p.cols[k].offsets + lo));
     }
     L.xcap = bound_xdr(s, p.framed, m, p.cols, lo, lo + m);
     L.xdr = b.take(L.xcap);
@@ -481,7 +481,7 @@ inline void dec_layout(const DecPlan &p, uint64_t lo, uint64_t m, Layout &L) {
     L.m = m;
     dec_window(p, lo, m, L.win, L.wlen);
     L.xdr = b.take(L.wlen, (uintptr_t)(p.in + L.win));
-    L.rec = p.ro ? b.take((m + 1) * 8) : 0;
+    L.rec = p.ro ? b.take((m + 1) * 8, (uintptr_t)(p.ro + lo)) : 0;
     L.reg.assign(p.regs.size(), 0);
     for (size_t r = 0; r < p.regs.size(); ++r) {
         const Region &g = p.regs[r];

@@ -351,6 +351,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 20: if (!in(0, 2)) return -1; t.dec_lean = (int32_t)v; return 0;
     case 24: if (!in(0, 1)) return -1; t.pay_hoist = (int32_t)v; return 0;
     case 25: if (!in(1024, 32768) || (v & 15)) return -1; t.sweep_tile = (uint32_t)v; return 0;
+    case 26: if (!in(0, 1)) return -1; t.stage_copy = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -1255,7 +1256,15 @@ struct HipExec {
         if (r.d2h_rec[i]) HIPCHK(c, hipEventSynchronize(r.e_d2h[i]));
         return XDRG_OK;
     }
+    // the device's view of a host span when the copy kernels move it (tuning key 26)
+    const uint8_t *link_view(const void *host, uint64_t n) const {
+        return c->tune.stage_copy ? (const uint8_t *)span_device(host, n) : nullptr;
+    }
     int dma_h2d(uint8_t *dev, const void *host, uint64_t n) {
+        if (const uint8_t *v = link_view(host, n)) {
+            HIPCHK(c, (hipError_t)launch_copy_link(dev, v, n, r.h2d));
+            return XDRG_OK;
+        }
         HIPCHK(c, hipMemcpyAsync(dev, host, n, hipMemcpyHostToDevice, r.h2d));
         return XDRG_OK;
     }
@@ -1311,6 +1320,10 @@ struct HipExec {
         return XDRG_OK;
     }
     int dma_d2h(void *host, const uint8_t *dev, uint64_t n) {
+        if (const uint8_t *v = link_view(host, n)) {
+            HIPCHK(c, (hipError_t)launch_copy_link((uint8_t *)v, dev, n, r.d2h));
+            return XDRG_OK;
+        }
         HIPCHK(c, hipMemcpyAsync(host, dev, n, hipMemcpyDeviceToHost, r.d2h));
         return XDRG_OK;
     }

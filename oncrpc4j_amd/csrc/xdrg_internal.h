@@ -182,6 +182,8 @@ struct Tuning {
     uint32_t sweep_tile = 21504;    // key 25: the sweep decode's LDS tile (k_dec_sweep, 4 blocks per CU)
     uint32_t big_rec = 1024;        // key 13: blocks averaging >= this many XDR bytes per record
                                     // take the group kernels (0 = never)
+    int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
+                                    // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
 };
 int set_tuning(Tuning &t, int key, long long value);   // 0, or -1 for an unknown key / bad value
 
@@ -268,6 +270,8 @@ struct GatherArgs {             // copy bytes[s] from src[s] (a peer's HBM) to d
 };
 int launch_gather(const GatherArgs &a, void *stream);
 int launch_add_u64(uint64_t *p, uint64_t n, uint64_t delta, void *stream);   // p[0..n) += delta
+// dst[0..bytes) = src[0..bytes) by the CUs, one side host memory the device maps
+int launch_copy_link(uint8_t *dst, const uint8_t *src, uint64_t bytes, void *stream);
 
 // ---- repeated groups (kernels_group.hip) --------------------------------
 // Arrays of structs and recursive lists (include/xdrg.h "Repeated groups").

@@ -44,6 +44,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def hctx():
+    import torch
+    assert torch.cuda.is_available()   # torch's runtime first (its pinned allocator serves TorchPinned)
     c = engine.Context(0)
     c.host_staging(SLOT, 3)
     yield c
@@ -301,13 +303,14 @@ def test_host_aos_partial_coverage(hctx):
     aos = rng.integers(0, 256, n * rec, dtype=np.uint8)
     cols = aos_columns(fields, aos.ctypes.data, rec, offs)
     sch = engine.Schema(fields)
-    rc, want, _ = oracle.encode_batch(fields, cols, n, n * 32)
+    xb = n * sch.fixed_size   # 28 B records
+    rc, want, _ = oracle.encode_batch(fields, cols, n, xb)
     assert rc == 0
-    out = np.zeros(n * 32, np.uint8)
-    assert hctx.encode(sch, cols, n, out, n * 32, host=True) == n * 32
+    out = np.zeros(xb, np.uint8)
+    assert hctx.encode(sch, cols, n, out, xb, host=True) == xb
     assert out.tobytes() == want
     back = np.full(n * rec, 0xAB, np.uint8)
-    assert hctx.decode(sch, out, n * 32, n, aos_columns(fields, back.ctypes.data, rec, offs), host=True) == (0, n, 0)
+    assert hctx.decode(sch, out, xb, n, aos_columns(fields, back.ctypes.data, rec, offs), host=True) == (0, n, 0)
     b2, a2 = back.reshape(n, rec), aos.reshape(n, rec)
     covered = np.zeros(rec, bool)
     for o, w in zip(offs, [4, 4, 4, 4, 8, 4]):
