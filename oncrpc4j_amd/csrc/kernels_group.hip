@@ -91,12 +91,83 @@ __device__ __forceinline__ uint64_t g_dyn_words(const GField &f, uint64_t cnt) {
     return f.xsz == 1 ? (cnt + 3) >> 2 : cnt * (f.xsz >> 2);
 }
 
+// ---- conditions (unions / optional data) on their own level -------------------
+// A field's presence follows its discriminant (an earlier field of the same
+// level: top-level fields per record, a group's members per element), as the
+// generated xdrEncode / xdrDecode switch on it (jrpcgen.java:1240-1340).
+// pres: bit k = field k present; v: discriminant values by slot (uniform
+// slot indices, unrolled selects: no scratch).
+struct GDisc {
+    uint32_t pres;
+    int32_t v[XDRG_MAX_DISC];
+};
+__device__ __forceinline__ int32_t gd_get(const GDisc &d, uint32_t slot) {
+    int32_t r = 0;
+#pragma unroll
+    for (int j = 0; j < XDRG_MAX_DISC; ++j) r = slot == (uint32_t)j ? d.v[j] : r;
+    return r;
+}
+__device__ __forceinline__ bool g_present(const GroupArgs &a, const GField &f, const GDisc &d) {
+    if (!f.cond) return true;
+    const uint32_t dk = f.cond - 1;
+    if (!((d.pres >> dk) & 1u)) return false;
+    const int32_t v = gd_get(d, a.f[dk].dslot - 1);
+    bool in = false;
+    for (uint32_t j = 0; j < f.cnum; ++j) in |= a.cvals[f.cfirst + j] == v;
+    return in != (f.cneg != 0);
+}
+// Field k's presence (and its value when it is a discriminant) into d.
+__device__ __forceinline__ void g_note(GDisc &d, uint32_t k, const GField &f, bool present, int32_t val) {
+    d.pres = present ? (d.pres | (1u << k)) : (d.pres & ~(1u << k));
+    if (f.dslot) {
+#pragma unroll
+        for (int j = 0; j < XDRG_MAX_DISC; ++j)
+            if (f.dslot - 1 == (uint32_t)j) d.v[j] = present ? val : 0;
+    }
+}
+// A discriminant's value: from its native row (encode; bool as 0 / 1) or
+// from the word about to be decoded (any non-zero bool is true, Xdr.java:404-407).
+__device__ __forceinline__ int32_t g_enc_dval(const GField &f, uint64_t i) {
+    const uint8_t *p = f.data + (int64_t)i * f.stride;
+    return f.type == XDRG_T_BOOL ? (int32_t)(*p != 0) : *(const int32_t *)p;
+}
+__device__ __forceinline__ int32_t g_dec_dval(const GField &f, const uint8_t *in, uint64_t pos, uint64_t end) {
+    if (end - pos < 4) return 0;   // the field's own check fails first
+    const int32_t w = (int32_t)g_ld(in + pos);
+    return f.type == XDRG_T_BOOL ? (int32_t)(w != 0) : w;
+}
+// Presence of field k on encode at row i (notes it into d).
+__device__ __forceinline__ bool g_enc_field_present(const GroupArgs &a, uint32_t k, uint64_t i, GDisc &d) {
+    const GField &f = a.f[k];
+    if (!a.ncond) return true;
+    const bool p = g_present(a, f, d);
+    g_note(d, k, f, p, p && f.dslot ? g_enc_dval(f, i) : 0);
+    return p;
+}
+__device__ __forceinline__ bool g_dec_field_present(const GroupArgs &a, uint32_t k, const uint8_t *in, uint64_t pos,
+                                                    uint64_t end, GDisc &d) {
+    const GField &f = a.f[k];
+    if (!a.ncond) return true;
+    const bool p = g_present(a, f, d);
+    g_note(d, k, f, p, p && f.dslot ? g_dec_dval(f, in, pos, end) : 0);
+    return p;
+}
+
 // XDR bytes of element e of group g (its list bool included).
-__device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g, uint64_t e) {
-    uint64_t s = a.f[g].efix;
+__device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g, uint64_t e, GDisc d) {
+    if (!a.f[g].ncm) {
+        uint64_t s = a.f[g].efix;
+        for (uint32_t j = 1; j <= a.f[g].nmem; ++j) {
+            const GField &m = a.f[g + j];
+            if (m.kind == XDRG_K_DYNAMIC) s += g_dyn_bytes(m, m.offsets[e + 1] - m.offsets[e]);
+        }
+        return s;
+    }
+    uint64_t s = a.f[g].kind == XDRG_K_LIST ? 4 : 0;
     for (uint32_t j = 1; j <= a.f[g].nmem; ++j) {
         const GField &m = a.f[g + j];
-        if (m.kind == XDRG_K_DYNAMIC) s += g_dyn_bytes(m, m.offsets[e + 1] - m.offsets[e]);
+        if (!g_enc_field_present(a, g + j, e, d)) continue;
+        s += m.kind == XDRG_K_DYNAMIC ? g_dyn_bytes(m, m.offsets[e + 1] - m.offsets[e]) : (uint64_t)m.xbytes;
     }
     return s;
 }
@@ -106,13 +177,18 @@ __device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g,
 // ===========================================================================
 __device__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
     uint64_t s = a.framed ? 4 : 0;
+    GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
         const GField &f = a.f[k];
+        if (!g_enc_field_present(a, k, r, d)) {   // an absent field / array / list writes nothing
+            k += f.type == XDRG_T_GROUP ? 1 + f.nmem : 1;
+            continue;
+        }
         if (f.type == XDRG_T_GROUP) {
             uint64_t e0, cnt;
             g_range(f, r, e0, cnt);
             s += f.kind == XDRG_K_FIXED ? 0 : 4;   // the count, or a list's closing bool
-            if (f.ndm) for (uint64_t e = e0; e < e0 + cnt; ++e) s += g_elem_bytes(a, k, e);
+            if (f.ndm || f.ncm) for (uint64_t e = e0; e < e0 + cnt; ++e) s += g_elem_bytes(a, k, e, d);
             else s += cnt * f.efix;
             k += 1 + f.nmem;
             continue;
@@ -138,7 +214,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a
 }
 
 // One lane writes element e of group g at stream byte p.
-__device__ void g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t p) {
+__device__ void g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t p, GDisc d) {
     uint8_t *out = a.xdr;
     if (a.f[g].kind == XDRG_K_LIST) {   // xdrEncodeBoolean(true) (pmaplist.java:65-67)
         *(uint32_t *)(out + p) = bswap32r(1u);
@@ -146,6 +222,7 @@ __device__ void g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t 
     }
     for (uint32_t j = 1; j <= a.f[g].nmem; ++j) {
         const GField &m = a.f[g + j];
+        if (a.f[g].ncm && !g_enc_field_present(a, g + j, e, d)) continue;   // an element's absent arm
         if (m.kind != XDRG_K_DYNAMIC) {
             for (uint32_t w = 0; w < m.xbytes >> 2; ++w) *(uint32_t *)(out + p + 4 * w) = g_fixed_word(m, e, w);
             p += m.xbytes;
@@ -167,8 +244,13 @@ __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint6
         if (lane == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
         pos += 4;
     }
+    GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
         const GField &f = a.f[k];
+        if (!g_enc_field_present(a, k, r, d)) {   // the record's absent arm / optional value
+            k += f.type == XDRG_T_GROUP ? 1 + f.nmem : 1;
+            continue;
+        }
         if (f.type == XDRG_T_GROUP) {
             uint64_t e0, cnt;
             g_range(f, r, e0, cnt);
@@ -176,15 +258,15 @@ __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint6
                 if (lane == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)cnt);
                 pos += 4;
             }
-            if (!f.ndm) {   // elements of one size: a lane per element
-                for (uint64_t i = lane; i < cnt; i += 64) g_enc_elem(a, k, e0 + i, pos + i * f.efix);
+            if (!f.ndm && !f.ncm) {   // elements of one size: a lane per element
+                for (uint64_t i = lane; i < cnt; i += 64) g_enc_elem(a, k, e0 + i, pos + i * f.efix, d);
                 pos += cnt * f.efix;
             } else {        // a lane per element at its scanned position
                 for (uint64_t b = 0; b < cnt; b += 64) {
                     const uint64_t i = b + lane;
-                    const uint64_t z = i < cnt ? g_elem_bytes(a, k, e0 + i) : 0;
+                    const uint64_t z = i < cnt ? g_elem_bytes(a, k, e0 + i, d) : 0;
                     const uint64_t incl = wave_incl_scan(z);
-                    if (i < cnt) g_enc_elem(a, k, e0 + i, pos + incl - z);
+                    if (i < cnt) g_enc_elem(a, k, e0 + i, pos + incl - z, d);
                     pos += __shfl(incl, 63, 64);
                 }
             }
@@ -283,9 +365,14 @@ __device__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxS
         if (!(m & kLastFrag) || (uint64_t)(m & kSizeMask) != e.b - pos - 4) return XDRG_E_FRAME;
         pos += 4;
     }
+    GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
         const GField &f = a.f[k];
         *sub = 2 * k + 1;
+        if (!g_dec_field_present(a, k, in, pos, e.b, d)) {   // absent: nothing on the wire
+            k += f.type == XDRG_T_GROUP ? 1 + f.nmem : 1;
+            continue;
+        }
         if (f.type == XDRG_T_GROUP) {
             uint64_t n;
             if (f.kind == XDRG_K_DYNAMIC) {   // int $size = xdr.xdrDecodeInt(); new T[$size]
@@ -297,7 +384,7 @@ __device__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxS
             } else {
                 n = f.kind == XDRG_K_FIXED ? f.count : ~0ull;
             }
-            if (!f.ndm && f.kind != XDRG_K_LIST) {   // elements of one size
+            if (!f.ndm && !f.ncm && f.kind != XDRG_K_LIST) {   // elements of one size
                 if ((e.b - pos) / f.efix < n) return XDRG_E_SHORT;
                 pos += n * f.efix;
             } else {
@@ -313,6 +400,7 @@ __device__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxS
                     }
                     for (uint32_t j = 1; j <= f.nmem; ++j) {
                         const GField &m = a.f[k + j];
+                        if (f.ncm && !g_dec_field_present(a, k + j, in, pos, e.b, d)) continue;
                         if (m.kind != XDRG_K_DYNAMIC) {
                             if (e.b - pos < m.xbytes) return XDRG_E_SHORT;
                             pos += m.xbytes;
@@ -413,11 +501,43 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_offsets(const GroupArgs
 // One lane decodes record r (walked clean, capacity checked), field by
 // field in stream order: a wave keeps 64 records' loads in flight instead of
 // one record's chain of dependent length words.
+// The defaults of a freshly constructed rpcgen object for an absent fixed
+// field at row i: zeros.
+__device__ __forceinline__ void g_zero_fixed(const GField &f, uint64_t i) {
+    uint8_t *p = f.data + (int64_t)i * f.stride;
+    const uint64_t nb = (uint64_t)f.nsz * (f.kind == XDRG_K_FIXED ? f.count : 1);
+    for (uint64_t b = 0; b < nb; ++b) p[b] = 0;
+}
+
 __device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
     const uint8_t *in = a.xdr;
+    const uint64_t end = a.rec_in[r + 1];
     uint64_t pos = a.rec_in[r] + (a.framed ? 4 : 0);
+    GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
         const GField &f = a.f[k];
+        if (!g_dec_field_present(a, k, in, pos, end, d)) {
+            if (f.type != XDRG_T_GROUP) {
+                if (f.kind != XDRG_K_DYNAMIC) g_zero_fixed(f, r);   // dynamic: count 0 (offsets kernel)
+                ++k;
+                continue;
+            }
+            if (f.kind == XDRG_K_FIXED) {   // an absent T x[N]: N zero / empty elements
+                for (uint32_t j = 1; j <= f.nmem; ++j) {
+                    const GField &m = a.f[k + j];
+                    for (uint64_t e = r * f.count; e < (r + 1) * f.count; ++e) {
+                        if (m.kind != XDRG_K_DYNAMIC) {
+                            g_zero_fixed(m, e);
+                        } else {
+                            if (e == r * f.count) m.offsets[e] = a.rec_base[(uint64_t)(m.slot - 1) * a.n + r];
+                            m.offsets[e + 1] = m.offsets[e];
+                        }
+                    }
+                }
+            }
+            k += 1 + f.nmem;
+            continue;
+        }
         if (f.type == XDRG_T_GROUP) {
             const uint64_t e0 = f.kind == XDRG_K_FIXED ? r * f.count : a.rec_base[(uint64_t)(f.slot - 1) * a.n + r];
             const uint64_t cnt = f.kind == XDRG_K_FIXED ? f.count : a.rec_cnt[(uint64_t)(f.slot - 1) * a.n + r];
@@ -430,6 +550,11 @@ __device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
                 if (f.kind == XDRG_K_LIST) pos += 4;   // its TRUE
                 for (uint32_t j = 1; j <= f.nmem; ++j) {
                     const GField &m = a.f[k + j];
+                    if (f.ncm && !g_dec_field_present(a, k + j, in, pos, end, d)) {   // an element's absent arm
+                        if (m.kind != XDRG_K_DYNAMIC) g_zero_fixed(m, e);
+                        else m.offsets[e + 1] = m.offsets[e];
+                        continue;
+                    }
                     if (m.kind != XDRG_K_DYNAMIC) {
                         for (uint32_t w = 0; w < m.xbytes >> 2; ++w) g_fixed_store(m, e, w, *(const uint32_t *)(in + pos + 4 * w));
                         pos += m.xbytes;

@@ -109,7 +109,7 @@ extern "C" int xdrg_schema_create_cond(const xdrg_field *fields, size_t nfields,
             sized |= f.kind != XDRG_K_FIXED || f.count > 0;
             s->grp[k + j] = (uint32_t)k + 1;
         }
-        if (!ok || !sized || nconds) { delete s; return XDRG_E_INVAL; }   // no conditions with groups
+        if (!ok || !sized) { delete s; return XDRG_E_INVAL; }
         ++s->ngroups;
         k += m;
     }
@@ -179,6 +179,12 @@ extern "C" int xdrg_schema_create_cond(const xdrg_field *fields, size_t nfields,
         const xdrg_field &df = fields[d];
         if (df.kind != XDRG_K_SCALAR || (df.type != XDRG_T_INT && df.type != XDRG_T_UINT &&
                                          df.type != XDRG_T_ENUM && df.type != XDRG_T_BOOL)) {
+            delete s;
+            return XDRG_E_INVAL;
+        }
+        // with repeated groups a condition stays on its level: top-level on
+        // top-level, a member on an earlier member of its own group (per element)
+        if (s->grp[k] != s->grp[d]) {
             delete s;
             return XDRG_E_INVAL;
         }
@@ -659,9 +665,17 @@ static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols
             for (uint32_t j = 1; j <= f.reserved; ++j) {
                 if (s->f[k + j].kind == XDRG_K_DYNAMIC) ++v.ndm;
                 else v.efix += s->xbytes[k + j];
+                if (s->cond[k + j]) ++v.ncm;
             }
         }
+        v.cond = s->cond[k];
+        v.cneg = s->cneg[k];
+        v.cfirst = s->cfirst[k];
+        v.cnum = s->cnum[k];
+        v.dslot = s->slot[k];
     }
+    a.ncond = s->ncond;
+    for (size_t i = 0; i < s->cvals.size(); ++i) a.cvals[i] = s->cvals[i];
     a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;
     if (!a.nblocks) a.nblocks = 1;
     const size_t rows = a.nslot ? a.nslot : 1;

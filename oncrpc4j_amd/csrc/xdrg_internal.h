@@ -290,6 +290,13 @@ struct GField {
     uint32_t ndm;     // group: dynamic members
     uint32_t slot;    // counted column: slot + 1, else 0
     uint32_t top;     // top-level field index that owns it (the group for a member)
+    uint32_t ncm;     // group: conditional members (elements then differ in size)
+    // conditional fields (xdrg_cond) on their own level: a top-level field on
+    // an earlier top-level discriminant, a member on an earlier member of its
+    // group (per element): present iff field cond-1 is present and its value
+    // is (cneg = 0) / is not (cneg = 1) in cvals[cfirst, cfirst + cnum)
+    uint32_t cond, cneg, cfirst, cnum;
+    uint32_t dslot;   // 0, or 1 + this field's discriminant value slot
     uint8_t *data;
     int64_t stride;
     uint64_t *offsets;
@@ -313,6 +320,9 @@ struct GroupArgs {
     uint64_t *rec_base;          // decode workspace [nslot][n]: native offset per record
     unsigned long long *errkey;
     uint32_t slot_field[kMaxSlots];
+    uint32_t ncond;              // conditional fields (0: every record / element has all of them)
+    uint32_t rsv2;
+    int32_t cvals[XDRG_MAX_CASES];
     GField f[kMaxFields];
 };
 static_assert(sizeof(GroupArgs) <= 4096, "GroupArgs must fit the kernel-argument segment");

@@ -32,9 +32,11 @@ declaration is `T *next`, used as `T *x` or `T x` (INDIRECTION,
 jrpcgen.java:835-851: TRUE + element while there is one, then FALSE; the
 reference's own portmap/pmaplist.java:50-69) — become repeated groups
 (include/xdrg.h: a (T_GROUP, kind, count, members) field and the element's
-flattened fields as members).  Still not one tape: unions / optional data
-inside group elements, arrays of structs inside elements, and recursion
-anywhere but a struct's last declaration.
+flattened fields as members).  Unions and optional data inside an element
+become conditions between members of the same group (evaluated per
+element), and a group may itself sit in a union arm or behind optional data
+(a condition on the group field).  Still not one tape: arrays of structs
+inside elements, and recursion anywhere but a struct's last declaration.
 """
 import re
 
@@ -319,21 +321,27 @@ class _Tape:
         return bool(st.decls) and st.decls[-1].kind == OPTIONAL and self._struct_of(st.decls[-1].type) is st
 
     def group(self, kind, count, st, decls, where, guard, stack):
-        """Group field + the element's flattened fields as its members."""
-        if guard is not None:
-            raise NotBatchable(f"{where}: a repeated group inside a union arm or optional value")
+        """Group field + the element's flattened fields as its members.  The
+        group itself may sit under a guard (an array / list in a union arm or
+        behind optional data); its members may carry conditions on earlier
+        members of the same element (unions and optional data inside an
+        element, e.g. READDIRPLUS's post_op_attr).  Arrays of structs inside
+        an element are not one level of groups."""
         sub = _Tape(self.s)
         for d in decls:
             sub.decl(d, f"{where}.{d.name}", None, stack + (st.name,))
         fields, conds = sub.result()
-        if conds or any(f[0] == abi.T_GROUP for f in fields):
-            raise NotBatchable(f"{where}: elements of {st.name} hold unions, optional data or arrays "
-                               f"of structs (no one-level group)")
+        if any(f[0] == abi.T_GROUP for f in fields):
+            raise NotBatchable(f"{where}: elements of {st.name} hold arrays of structs or lists "
+                               f"(no one-level group)")
         if not fields:
             raise NotBatchable(f"{where}: elements of {st.name} have no fields")
-        self.add((abi.T_GROUP, kind, count, len(fields)), None)
+        g = self.add((abi.T_GROUP, kind, count, len(fields)), guard)
         for f in fields:
             self.add(f, None)
+        for k, d, neg, vals in conds:   # element-level conditions, in this tape's indices
+            self.conds.append((g + 1 + k, g + 1 + d, neg, list(vals)))
+        self.fields.reasons.extend(sub.fields.reasons)
 
     def decl(self, decl, where, guard, stack):
         if decl.kind == VOID:

@@ -407,14 +407,30 @@ static inline const uint8_t *fixed_ptr(const xdrg_field *f, const xdrg_column *c
 typedef struct { const xdrg_cond *cond_of[64]; } xo_conds;
 
 static int has_group(const xdrg_field *fs, size_t nf);
+/* grp_of[k] = index + 1 of the group field k is a member of, 0 at top level */
+static void group_of(const xdrg_field *fs, size_t nf, uint32_t *grp_of) {
+    for (size_t k = 0; k < nf; k++) grp_of[k] = 0;
+    for (size_t k = 0; k < nf; k++)
+        if (fs[k].type == XDRG_T_GROUP) {
+            for (uint32_t j = 1; j <= fs[k].reserved && k + j < nf; j++) grp_of[k + j] = (uint32_t)k + 1;
+            k += fs[k].reserved;
+        }
+}
+/* With repeated groups a condition stays on its level: a top-level field
+ * (a group included: the whole array / list present or not) on an earlier
+ * top-level discriminant, a member (a union or optional inside an element,
+ * e.g. READDIRPLUS's post_op_attr in entryplus3) on an earlier member of
+ * its own group, evaluated per element.                                      */
 static int cond_table(const xdrg_field *fs, size_t nf, const xdrg_cond *conds, size_t nc,
                       xo_conds *t) {
     memset(t, 0, sizeof *t);
-    if (nc && has_group(fs, nf)) return XDRG_E_INVAL;   /* no conditions with repeated groups */
     if (nf > 64) return nc ? XDRG_E_INVAL : XDRG_OK;
+    uint32_t grp_of[64];
+    group_of(fs, nf, grp_of);
     for (size_t i = 0; i < nc; i++) {
         const xdrg_cond *c = &conds[i];
         if (c->field >= nf || c->disc >= c->field || t->cond_of[c->field]) return XDRG_E_INVAL;
+        if (grp_of[c->field] != grp_of[c->disc]) return XDRG_E_INVAL;
         const xdrg_field *d = &fs[c->disc];
         if (d->kind != XDRG_K_SCALAR || !(d->type == XDRG_T_INT || d->type == XDRG_T_UINT ||
                                           d->type == XDRG_T_ENUM || d->type == XDRG_T_BOOL))
@@ -492,7 +508,21 @@ static int encode_field(xo_stream *s, const xdrg_field *f, const xdrg_column *c,
  * 856-880; no count for T x[N]), or a recursive list: xdrEncodeBoolean(true)
  * and the element while there is one, then xdrEncodeBoolean(false)
  * (portmap/pmaplist.java:63-70).  g[0] is the group, g[1..m] its members. */
-static int encode_group(xo_stream *s, const xdrg_field *g, const xdrg_column *gc, uint64_t i) {
+/* Presence and discriminant value of member / field k (absolute index gk)
+ * at row e, from the native columns (encode). */
+static void enc_presence(const xo_conds *cc, size_t gk, const xdrg_field *f, const xdrg_column *c, uint64_t e,
+                         int *pres, int32_t *val) {
+    pres[gk] = present(cc, gk, pres, val);
+    val[gk] = 0;
+    if (pres[gk] && f->kind == XDRG_K_SCALAR) {
+        const uint8_t *p = fixed_ptr(f, c, e);
+        if (f->type == XDRG_T_BOOL) val[gk] = *p != 0;
+        else if (native_size(f->type) == 4) memcpy(&val[gk], p, 4);
+    }
+}
+
+static int encode_group(xo_stream *s, const xdrg_field *g, const xdrg_column *gc, uint64_t i,
+                        const xo_conds *cc, size_t gk, int *pres, int32_t *val) {
     const uint32_t m = g->reserved;
     uint64_t e0, cnt;
     if (g->kind == XDRG_K_FIXED) { e0 = i * g->count; cnt = g->count; }
@@ -501,7 +531,12 @@ static int encode_group(xo_stream *s, const xdrg_field *g, const xdrg_column *gc
     if (g->kind == XDRG_K_DYNAMIC) rc = xo_encode_int(s, (int32_t)cnt);
     for (uint64_t e = e0; !rc && e < e0 + cnt; e++) {
         if (g->kind == XDRG_K_LIST) rc = xo_encode_boolean(s, 1);
-        for (uint32_t j = 1; !rc && j <= m; j++) rc = encode_field(s, &g[j], &gc[j], e);
+        for (uint32_t j = 1; !rc && j <= m; j++) {
+            /* an element's union arms / optional data (jrpcgen.java:1240-1340) */
+            enc_presence(cc, gk + j, &g[j], &gc[j], e, pres, val);
+            if (!pres[gk + j]) continue;
+            rc = encode_field(s, &g[j], &gc[j], e);
+        }
     }
     if (!rc && g->kind == XDRG_K_LIST) rc = xo_encode_boolean(s, 0);
     return rc;
@@ -521,7 +556,10 @@ static int encode_record_ex(xo_stream *s, const xdrg_field *fs, size_t nf, const
         int rc = XDRG_OK;
         if (k < 64) {
             pres[k] = present(cc, k, pres, val);
-            if (!pres[k]) continue;
+            if (!pres[k]) {
+                if (f->type == XDRG_T_GROUP) k += f->reserved;   /* nothing of the array / list */
+                continue;
+            }
             val[k] = 0;
             if (f->kind == XDRG_K_SCALAR) {
                 const uint8_t *p = fixed_ptr(f, c, i);
@@ -539,7 +577,7 @@ static int encode_record_ex(xo_stream *s, const xdrg_field *fs, size_t nf, const
             continue;
         }
         if (f->type == XDRG_T_GROUP) {
-            rc = encode_group(s, fs + k, cols + k, i);
+            rc = encode_group(s, fs + k, cols + k, i, cc, k, pres, val);
             if (rc) return rc;
             k += f->reserved;   /* its members */
             continue;
@@ -722,7 +760,20 @@ static int decode_field(xo_stream *s, const xdrg_field *f, xdrg_column *c, uint6
  * 52-61).  The first pass walks the group with every member's checks on a
  * copy of the stream (walk errors come first, in the reference's order);
  * then the element and member capacities; then the second pass decodes.   */
-static int walk_group(xo_stream *s, const xdrg_field *g, uint64_t *cnt_out, uint64_t *mcnt) {
+/* Presence and discriminant value of field k (absolute index gk) as a
+ * decoder meets it: the value is the word about to be decoded. */
+static void dec_presence(const xo_conds *cc, size_t gk, const xdrg_field *f, const xo_stream *s, int *pres,
+                         int32_t *val) {
+    pres[gk] = present(cc, gk, pres, val);
+    val[gk] = 0;
+    if (pres[gk] && f->kind == XDRG_K_SCALAR && xo_remaining(s) >= 4) {
+        const int32_t w = (int32_t)get_be32(s->buf + s->pos);
+        val[gk] = f->type == XDRG_T_BOOL ? (w != 0) : w;
+    }
+}
+
+static int walk_group(xo_stream *s, const xdrg_field *g, uint64_t *cnt_out, uint64_t *mcnt,
+                      const xo_conds *cc, size_t gk, int *pres, int32_t *val) {
     const uint32_t m = g->reserved;
     for (uint32_t j = 1; j <= m; j++) mcnt[j] = 0;
     uint64_t cnt = 0;
@@ -747,6 +798,8 @@ static int walk_group(xo_stream *s, const xdrg_field *g, uint64_t *cnt_out, uint
         }
         for (uint32_t j = 1; j <= m; j++) {
             const xdrg_field *f = &g[j];
+            dec_presence(cc, gk + j, f, s, pres, val);
+            if (!pres[gk + j]) continue;
             if (f->kind == XDRG_K_DYNAMIC) {
                 int32_t len;
                 rc = xo_decode_int(s, &len);
@@ -779,11 +832,22 @@ static int walk_group(xo_stream *s, const xdrg_field *g, uint64_t *cnt_out, uint
     return XDRG_OK;
 }
 
-static int decode_group(xo_stream *s, const xdrg_field *g, xdrg_column *gc, uint64_t i) {
+/* The defaults of a freshly constructed rpcgen object for an absent field
+ * at row e: zero, or an empty run (its offsets entry repeats). */
+static void absent_field(const xdrg_field *f, xdrg_column *c, uint64_t e) {
+    if (f->kind == XDRG_K_DYNAMIC) c->offsets[e + 1] = c->offsets[e];
+    else {
+        size_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
+        memset((uint8_t *)fixed_ptr(f, c, e), 0, cnt * native_size(f->type));
+    }
+}
+
+static int decode_group(xo_stream *s, const xdrg_field *g, xdrg_column *gc, uint64_t i,
+                        const xo_conds *cc, size_t gk, int *pres, int32_t *val) {
     const uint32_t m = g->reserved;
     uint64_t mcnt[64], cnt = 0;
     xo_stream w = *s;
-    int rc = walk_group(&w, g, &cnt, mcnt);
+    int rc = walk_group(&w, g, &cnt, mcnt, cc, gk, pres, val);
     if (rc) return rc;
     const uint64_t e0 = g->kind == XDRG_K_FIXED ? i * g->count : gc->offsets[i];
     if (g->kind != XDRG_K_FIXED && e0 + cnt > gc->cap) return XDRG_E_CAPACITY;
@@ -793,6 +857,11 @@ static int decode_group(xo_stream *s, const xdrg_field *g, xdrg_column *gc, uint
     for (uint64_t e = e0; e < e0 + cnt; e++) {
         if (g->kind == XDRG_K_LIST) s->pos += 4;
         for (uint32_t j = 1; j <= m; j++) {
+            dec_presence(cc, gk + j, &g[j], s, pres, val);
+            if (!pres[gk + j]) {
+                absent_field(&g[j], &gc[j], e);
+                continue;
+            }
             rc = decode_field(s, &g[j], &gc[j], e);
             if (rc) return rc;
         }
@@ -820,11 +889,17 @@ static int decode_record(xo_stream *s, const xdrg_field *fs, size_t nf, xdrg_col
             }
             if (!pres[k]) {   /* absent: the defaults of a new rpcgen object */
                 if ((int)k == view) view_pos[i] = UINT64_MAX;
-                if (f->kind == XDRG_K_DYNAMIC) c->offsets[i + 1] = c->offsets[i];
-                else {
-                    size_t cnt = f->kind == XDRG_K_FIXED ? f->count : 1;
-                    memset((uint8_t *)fixed_ptr(f, c, i), 0, cnt * native_size(f->type));
+                if (f->type == XDRG_T_GROUP) {   /* no elements (a FIXED group's are zero / empty) */
+                    if (f->kind != XDRG_K_FIXED) {
+                        c->offsets[i + 1] = c->offsets[i];
+                    } else {
+                        for (uint64_t e = i * f->count; e < (i + 1) * f->count; e++)
+                            for (uint32_t j = 1; j <= f->reserved; j++) absent_field(&f[j], &c[j], e);
+                    }
+                    k += f->reserved;
+                    continue;
                 }
+                absent_field(f, c, i);
                 continue;
             }
         }
@@ -838,7 +913,7 @@ static int decode_record(xo_stream *s, const xdrg_field *fs, size_t nf, xdrg_col
             continue;
         }
         if (f->type == XDRG_T_GROUP) {
-            rc = decode_group(s, fs + k, cols + k, i);
+            rc = decode_group(s, fs + k, cols + k, i, cc, k, pres, val);
             if (rc) return rc;
             k += f->reserved;   /* its members */
             continue;

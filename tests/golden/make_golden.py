@@ -19,6 +19,9 @@ fixtures are plain JSON data and travel, this script's inputs do not need to.
 4. rpc_vectors.json — record-marked accepted replies (RpcCall.acceptedReply)
    and AUTH_UNIX calls (RpcCall.callInternal + RpcAuthTypeUnix) packed by
    xdrlib in the reference's field order (oncrpc4j_amd/rpc.py batches them).
+5. cond_vectors.json / group_vectors.json / group_cond_vectors.json — union
+   and optional tapes, arrays of structs and lists, and unions inside list
+   elements (rpcgen/plus_types.x), packed by xdrlib.
 """
 import json
 import os
@@ -381,6 +384,97 @@ def group_vectors(seed=0x6A0F):
     return out
 
 
+# ---- unions inside list elements, a list inside a union arm --------------------
+# tests/golden/rpcgen/plus_types.x `plus_res`: READDIRPLUS-like replies packed
+# by xdrlib from the DECLARATIONS (status; the OK arm's optional directory
+# attributes, verifier, entry list with per-entry optional attributes and
+# optional handle, eof; the default arm's optional directory attributes) —
+# independently of the flattened tape the engine uses.  Each record is also
+# given in tape layout (absent fields as the zero / empty values a decode
+# returns), with the tape and its conditions from oncrpc4j_amd.rpcgen.
+def group_cond_vectors(seed=0x9D1F):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oncrpc4j_amd import rpcgen
+    spec = rpcgen.parse_file(os.path.join(HERE, "rpcgen", "plus_types.x"))
+    fields, conds = spec.tape("plus_res")
+    rng = random.Random(seed)
+    U64 = lambda: rng.getrandbits(64)   # noqa: E731
+    U32 = lambda: rng.getrandbits(32)   # noqa: E731
+
+    def dattr():
+        return [U32(), U32(), U64(), U64()]
+
+    def pack_attr(p, present, a):
+        p.pack_bool(present)
+        if present:
+            p.pack_uint(a[0]); p.pack_uint(a[1]); p.pack_uhyper(a[2]); p.pack_uhyper(a[3])
+
+    out = {"source": "CPython 3.10 stdlib xdrlib (RFC 1014) packing plus_types.x `plus_res` from its "
+                     "declarations (union arms, optional attributes inside `plus_entry *next` list "
+                     "elements, jrpcgen.java:835-906, 1240-1340)",
+           "seed": seed, "fields": [list(f) for f in fields], "conds": [list(c) for c in conds],
+           "batches": []}
+    for framed in (False, True):
+        n = 40
+        records, chunks = [], []
+        for i in range(n):
+            status = rng.choice([0, 0, 0, 0, 2, 5])
+            p = xdrlib.Packer()
+            p.pack_enum(status)
+            rec = [status] + [None] * (len(fields) - 1)
+            zero_attr = [0, 0, 0, 0]
+            if status == 0:
+                dpres = rng.random() < 0.7
+                da = dattr() if dpres else zero_attr
+                pack_attr(p, dpres, da)
+                verf = bytes(rng.getrandbits(8) for _ in range(8))
+                p.pack_fopaque(8, verf)
+                ents = []
+                for _ in range(rng.choice([0, 1, 2, 3, 5, 8])):
+                    name = bytes(rng.choice(b"abcdefghijklmnopqrstuvwxyz") for _ in range(rng.randrange(0, 21)))
+                    apres = rng.random() < 0.6
+                    a = dattr() if apres else zero_attr
+                    hpres = rng.random() < 0.5
+                    fh = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 65))) if hpres else b""
+                    fileid, cookie = U64(), U64()
+                    p.pack_bool(True)
+                    p.pack_uhyper(fileid); p.pack_string(name); p.pack_uhyper(cookie)
+                    pack_attr(p, apres, a)
+                    p.pack_bool(hpres)
+                    if hpres:
+                        p.pack_opaque(fh)
+                    ents.append([fileid, name.hex(), cookie, int(apres)] + a + [int(hpres), fh.hex()])
+                p.pack_bool(False)
+                eof = rng.randint(0, 1)
+                p.pack_bool(eof)
+                rec[1:7] = [int(dpres)] + da + [verf.hex()]
+                rec[7] = ents
+                rec[8:18] = [None] * 10
+                rec[18] = eof
+                rec[19:24] = [0, 0, 0, 0, 0]
+            else:
+                dpres = rng.random() < 0.5
+                da = dattr() if dpres else zero_attr
+                pack_attr(p, dpres, da)
+                rec[1:7] = [0, 0, 0, 0, 0, bytes(8).hex()]
+                rec[7] = []
+                rec[8:18] = [None] * 10
+                rec[18] = 0
+                rec[19:24] = [int(dpres)] + da
+            body = p.get_buffer()
+            if framed:
+                body = struct.pack(">I", len(body) | 0x80000000) + body
+            chunks.append(body)
+            records.append(rec)
+        offs = [0]
+        for ch in chunks:
+            offs.append(offs[-1] + len(ch))
+        out["batches"].append({"name": "plus_res", "framed": framed, "n": n, "records": records,
+                               "xdr": b"".join(chunks).hex(), "rec_offsets": offs})
+    return out
+
+
 # ---- framing -----------------------------------------------------------------
 def call_message(xid, args_string):
     """RpcMessageParserTCPTest.XdrStreamBuilder.build (:127-142): CALL header,
@@ -520,11 +614,16 @@ def rpc_vectors(seed=0x5EED):
                       "records": calls, "stream": stream.hex(), "rec_offsets": offs}}
 
 
-def main():
-    for name, obj in (("kat_reference.json", kat_reference()), ("kat_jdk_nan.json", kat_jdk_nan()),
-                      ("xdrlib_vectors.json", xdrlib_vectors()), ("framing.json", framing()),
-                      ("rpc_vectors.json", rpc_vectors()),
-                      ("cond_vectors.json", cond_vectors()), ("group_vectors.json", group_vectors())):
+GENERATORS = {"kat_reference.json": kat_reference, "kat_jdk_nan.json": kat_jdk_nan,
+              "xdrlib_vectors.json": xdrlib_vectors, "framing.json": framing, "rpc_vectors.json": rpc_vectors,
+              "cond_vectors.json": cond_vectors, "group_vectors.json": group_vectors,
+              "group_cond_vectors.json": group_cond_vectors}
+
+
+def main(names=None):
+    """Write every fixture, or the named ones (python make_golden.py group_cond_vectors.json)."""
+    for name in names or list(GENERATORS):
+        obj = GENERATORS[name]()
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(obj, f, indent=1)
             f.write("\n")
@@ -532,4 +631,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    main(sys.argv[1:])
