@@ -1955,7 +1955,89 @@ __device__ __forceinline__ uint32_t enc_fit(const RecArgs &a, const uint64_t (&b
     return (uint32_t)__syncthreads_count(fits);
 }
 
-__global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
+// Output-staged sub-batches (k_enc_ostage): records [js, je) whose OUTPUT
+// bytes, from the 16-byte line the first one starts in, fit the tile.
+__device__ __forceinline__ uint32_t enc_out_fit(const uint32_t *soff, uint32_t js, uint32_t nrec, uint32_t mis,
+                                                uint32_t cap) {
+    const uint32_t je = js + 1 + threadIdx.x;
+    const bool fits = je <= nrec && soff[je] - soff[js] + ((mis + soff[js]) & 15u) <= cap;
+    return (uint32_t)__syncthreads_count(fits);
+}
+
+// Compose the XDR bytes of records [js, je) into the LDS image `img` (image
+// byte 0 = the 16-byte aligned stream line record js starts in, `head`
+// bytes before it): marks, fixed words and length-prefixed dynamic fields,
+// read straight from the native columns (16-byte windows realigned in
+// registers), written to LDS at any 4-byte alignment.
+__device__ void enc_compose(const RecArgs &a, uint8_t *img, uint32_t head, uint64_t rb, uint32_t js, uint32_t je,
+                            const uint32_t *soff, const uint32_t *srel, const uint64_t (&base)[kMaxDynLds]) {
+    constexpr uint32_t RS = kRecPerBlock + 1;
+    const uint32_t tid = threadIdx.x;
+    uint8_t *const at = img + head - soff[js];   // image byte of block-relative stream offset x: at + x
+    if (a.framed)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
+        for (uint32_t j = js + tid; j < je; j += kRecThreads)
+            *(uint32_t *)(at + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
+    uint32_t fpre = a.framed ? 4 : 0;
+    uint32_t d = 0;
+    const uint32_t m = je - js;
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        const VField &f = a.f[k];
+        if (f.kind != XDRG_K_DYNAMIC) {
+            const uint32_t nw = f.xbytes >> 2;
+            if (nw) {
+                const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
+                const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+                for (uint32_t j = js + tid / G; j < je; j += ng) {
+                    uint8_t *dst = at + soff[j] + fpre + dyn_before(a, srel, j, d);
+                    for (uint32_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
+                }
+            }
+            fpre += f.xbytes;
+            continue;
+        }
+        const bool bytes = f.xsz == 1;
+        const uint64_t esz = bytes ? 1 : f.nsz;
+        const uint32_t *rel = srel + d * RS;
+        const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
+        const uint32_t G = a.force_g ? a.force_g : pow2_lanes(fbytes / m, a.lane_bytes_enc);
+        const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+        const Span sp = make_span(f.data + f.offsets[0] * esz, f.data + f.offsets[a.n] * esz,
+                                  (const uint8_t *)a.block_sums);
+        for (uint32_t j = js + tid / G; j < je; j += ng) {
+            const uint64_t cnt1 = rel[j + 1] - rel[j];
+            uint8_t *dst[1] = {at + soff[j] + fpre + dyn_before(a, srel, j, d)};
+            const uint8_t *src[1] = {f.data + (base[d] + rel[j]) * esz};
+            const uint64_t cnt[1] = {cnt1};
+            const uint64_t nwb = 1 + (bytes ? (cnt1 + 3) >> 2 : cnt1);
+            const uint64_t nch[1] = {(nwb + 3) >> 2};
+            if (bytes) enc_blob_bytes<2, 1>(dst, src, cnt, nch, sp, G, gl);
+            else enc_blob_words4<2, 1>(dst, src, cnt, nch, f.type == XDRG_T_FLOAT, sp, G, gl);
+        }
+        ++d;
+    }
+}
+
+// Write image bytes [head, nbytes) to the stream at A0 (16-byte aligned):
+// whole lines as aligned 16-byte stores, the first and last line's own
+// dwords only (the rest of those lines belong to the neighbouring records).
+__device__ __forceinline__ void enc_flush(const uint8_t *img, uint8_t *A0, uint32_t head, uint32_t nbytes) {
+    const uint32_t nch = (nbytes + 15) >> 4;
+    for (uint32_t i = threadIdx.x; i < nch; i += kRecThreads) {
+        const uint32_t lo = 16 * i;
+        const u32x4n v = *(const u32x4n *)(img + lo);
+        if (lo >= head && lo + 16 <= nbytes) {
+            __builtin_nontemporal_store(v, (u32x4n *)(A0 + lo));
+            continue;
+        }
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (lo + 4 * q >= head && lo + 4 * q + 4 <= nbytes) *(uint32_t *)(A0 + lo + 4 * q) = w[q];
+    }
+}
+
+template <bool OUT>
+__device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;   // row stride of soff / srel
     uint32_t *soff = (uint32_t *)smem;
@@ -2027,6 +2109,29 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
         return;
     }
     uint8_t *out = a.xdr + bbase;   // block-relative stream
+    if (OUT) {   // ---- output-staged sub-batches: compose in LDS, then whole lines out
+        const uint32_t mis = (uint32_t)((uintptr_t)out & 15);
+        uint32_t js = 0;
+        uint32_t k1 = enc_out_fit(soff, js, nrec, mis, a.tile_bytes);
+        while (js < nrec) {
+            if (k1 == 0) {   // too large for the tile: the whole block writes record js
+                if (a.framed && tid == 0)
+                    *(uint32_t *)(out + soff[js]) = bswap32r((soff[js + 1] - soff[js] - 4) | kLastFrag);
+                enc_record_block(a, rb + js, bbase + soff[js]);
+                ++js;
+                k1 = js < nrec ? enc_out_fit(soff, js, nrec, mis, a.tile_bytes) : 0;
+                continue;
+            }
+            const uint32_t je = js + k1;
+            const uint32_t head = (mis + soff[js]) & 15u;
+            enc_compose(a, tile, head, rb, js, je, soff, srel, base);
+            __syncthreads();
+            enc_flush(tile, out + soff[js] - head, head, head + soff[je] - soff[js]);
+            js = je;
+            k1 = js < nrec ? enc_out_fit(soff, js, nrec, mis, a.tile_bytes) : 0;   // its barrier ends the tile's use
+        }
+        return;
+    }
     if (a.framed)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
         for (uint32_t j = tid; j < nrec; j += kRecThreads)
             *(uint32_t *)(out + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
@@ -2116,6 +2221,8 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) {
         k1 = js < nrec ? enc_fit(a, base, srel, js, nrec) : 0;   // its barrier ends the tile's use
     }
 }
+__global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) { k_enc_stage_t<false>(a); }
+__global__ __launch_bounds__(kRecThreads) void k_enc_ostage(const RecArgs a) { k_enc_stage_t<true>(a); }
 
 // ---- decode -------------------------------------------------------------------
 // LDS: sstart[RPB + 1] u32 (record start - the block's first start) | snrel[ND][RPB + 1] u32 |
@@ -2816,8 +2923,12 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     case REC_ENC_PLACE:
         if (stage) {   // small-record blocks staged, large-record blocks by the group kernel
             a.big_rec = t.big_rec;
-            hipLaunchKernelGGL(k_enc_stage, dim3(nb), dim3(kRecThreads),
-                               enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            if (t.enc_out)   // output-staged sub-batches (tuning key 27)
+                hipLaunchKernelGGL(k_enc_ostage, dim3(nb), dim3(kRecThreads),
+                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            else
+                hipLaunchKernelGGL(k_enc_stage, dim3(nb), dim3(kRecThreads),
+                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             if (a.big_rec) launch_ur<EncG>(t.enc_u, t.enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
             if (a.big_rec && pay) launch_enc_payload(t.pay_hoist, pgrid, st, a);
         } else if (lane || (grp && t.rec == 3)) {

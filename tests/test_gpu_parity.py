@@ -49,7 +49,8 @@ SCHEMAS = {
 # run under each.
 REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),),
                "staged_edges": ((9, 4), (20, 0)),
-               "staged_lean": ((9, 4), (20, 1))}
+               "staged_lean": ((9, 4), (20, 1)),
+               "staged_out": ((9, 4), (27, 1))}   # output-staged encode (k_enc_ostage)
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
@@ -270,12 +271,13 @@ def test_error_parity(gpu_ctx, rec_kernel, name, framed):
             assert g2[:3] == o2[:3], desc
 
 
+@pytest.mark.parametrize("enc_out", [0, 1], ids=["enc_in", "enc_out"])
 @pytest.mark.parametrize("lean", [1, 0, 2], ids=["lean", "edges", "sweep"])
 @pytest.mark.parametrize("tile", [1024, 4096])
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("name", ["cfg1_int_int_string", "cfg3_6xint_opaque", "cfg4_int_string_intvec",
                                   "dyn_vectors"])
-def test_staged_tile_sizes(gpu_ctx, name, framed, tile, lean):
+def test_staged_tile_sizes(gpu_ctx, name, framed, tile, lean, enc_out):
     """Staged place kernels with small LDS tiles: records whose staged bytes
     exceed the tile take the whole-block direct path, the others form
     sub-batches of every size (dyn_vectors has non-stageable vector types and
@@ -290,6 +292,7 @@ def test_staged_tile_sizes(gpu_ctx, name, framed, tile, lean):
     gpu_ctx.tune(25, tile)   # the sweep decode's own tile
     gpu_ctx.tune(13, 0)   # every block staged (no split of large-record blocks to the group kernel)
     gpu_ctx.tune(20, lean)
+    gpu_ctx.tune(27, enc_out)
     try:
         xdr, offs = gpu_encode(gpu_ctx, fields, hb, framed)
         assert xdr == want
