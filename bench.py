@@ -369,10 +369,11 @@ class Workload:
             c, ms = self.ctx.kernel_stats(kid)
             if c:
                 step_ms[name] = round(ms / steps, 4)
+        traffic, traffic_src = load_traffic(self.cfg, self.framed, self.n)
         roof = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
-                "traffic": load_traffic(self.cfg, self.framed, self.n),
+                "traffic": traffic, "traffic_source": traffic_src,
                 "launches": launches, "avg_launch_ms": round(avg_ms, 4), "bytes_per_launch": per_launch}
         return roof, step_ms
 
@@ -386,22 +387,27 @@ class Workload:
 
 
 def load_traffic(cfg, framed, records):
-    """HBM bytes per launch of the dominant kernel(s) from the committed
-    rocprofv3 --pmc summary (profiles/pmc_traffic.json, tools/pmc_summary.py:
-    separate FETCH_SIZE and WRITE_SIZE passes over bench.py, FETCH doubled per
-    the gfx950 correction; record configs average their encode and decode
-    place kernels, as `achieved` does), or None when the summary was taken on
-    another record count."""
+    """(HBM bytes per launch of the dominant kernel(s), their source) from the
+    committed rocprofv3 --pmc summary (profiles/pmc_traffic.json,
+    tools/pmc_summary.py: separate FETCH_SIZE and WRITE_SIZE passes over
+    bench.py, FETCH doubled per the gfx950 correction; record configs average
+    their encode and decode place kernels, as `achieved` does), or (None,
+    reason) when the summary was taken on another record count.  The traffic
+    is not measured in this run: PMC counters need their own rocprofv3 pass."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    key = f"{cfg}{'f' if framed else ''}"
     try:
         with open(p) as f:
             d = json.load(f)
-        e = d["configs"][f"{cfg}{'f' if framed else ''}"]
+        e = d["configs"][key]
+        src = {"file": "profiles/pmc_traffic.json", "config_key": key, "tag": e.get("tag"),
+               "records": e.get("records"), "kernels": {"encode": e.get("encode"), "decode": e.get("decode")},
+               "measured_in_this_run": False}
         if e.get("records") == records:
-            return e["bytes_per_launch"]
+            return e["bytes_per_launch"], src
+        return None, dict(src, note="profiled on another record count")
     except (OSError, KeyError, ValueError):
-        pass
-    return None
+        return None, {"file": "profiles/pmc_traffic.json", "config_key": key, "note": "no entry"}
 
 
 # ---------------------------------------------------------------------------

@@ -2882,8 +2882,9 @@ int launch_scan_rows(uint64_t *sums, uint64_t nblocks, uint64_t *totals, uint32_
     return (int)hipGetLastError();
 }
 
-static void launch_enc_payload(int hoist, dim3 grid, hipStream_t st, const RecArgs &a) {
-    if (hoist) hipLaunchKernelGGL((k_enc_payload<64, true, true, true>), grid, dim3(256), 0, st, a);
+static void launch_enc_payload(int hoist, int nts, dim3 grid, hipStream_t st, const RecArgs &a) {
+    if (!nts) hipLaunchKernelGGL((k_enc_payload<64, true, false, true>), grid, dim3(256), 0, st, a);   // key 28 = 0
+    else if (hoist) hipLaunchKernelGGL((k_enc_payload<64, true, true, true>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_enc_payload<64, true, true, false>), grid, dim3(256), 0, st, a);
 }
 static void launch_dec_payload(int hoist, dim3 grid, hipStream_t st, const RecArgs &a) {
@@ -2930,12 +2931,12 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
                 hipLaunchKernelGGL(k_enc_stage, dim3(nb), dim3(kRecThreads),
                                    enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             if (a.big_rec) launch_ur<EncG>(t.enc_u, t.enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
-            if (a.big_rec && pay) launch_enc_payload(t.pay_hoist, pgrid, st, a);
+            if (a.big_rec && pay) launch_enc_payload(t.pay_hoist, t.pay_nts, pgrid, st, a);
         } else if (lane || (grp && t.rec == 3)) {
             hipLaunchKernelGGL(k_enc_lane, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
             launch_ur<EncG>(t.enc_u, t.enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
-            if (pay) launch_enc_payload(t.pay_hoist, pgrid, st, a);
+            if (pay) launch_enc_payload(t.pay_hoist, t.pay_nts, pgrid, st, a);
         }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;

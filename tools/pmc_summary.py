@@ -40,8 +40,10 @@ CONFIGS = {
     "2f": (67108864, [("k_stream_framed_enc_lean", "150994944")], [("k_stream_framed_dec_lean", "134217728")]),
     "3": (16777216, [("k_enc_place_g", "4194304"), ("k_enc_payload", "1073741824")],
           [("k_dec_place_g", "4194304"), ("k_dec_payload", "1073741824")]),
-    "4": (33554432, [("k_enc_sweep|k_enc_stage", "8388608"), ("k_enc_place_g", "8388608")],
+    "4": (33554432, [("k_enc_ostage|k_enc_stage", "8388608"), ("k_enc_place_g", "8388608")],
           [("k_dec_sweep|k_dec_stage", "8388608"), ("k_dec_place_g", "8388608")]),
+    "4f": (33554432, [("k_enc_ostage|k_enc_stage", "8388608"), ("k_enc_place_g", "8388608")],
+           [("k_dec_sweep|k_dec_stage", "8388608"), ("k_dec_place_g", "8388608")]),
 }
 # (a name "a|b" takes the first of the alternatives the profile holds: the
 # staged kernels' sweep variants replace them when the tuning selects them)
@@ -68,7 +70,61 @@ def by_grid(path, counter):
     return {k: statistics.median(v) for k, v in out.items()}
 
 
+def _trace_stats(path):
+    """rocprofv3 kernel stats rows of the xdrg kernels."""
+    return [r for r in csv.DictReader(open(path)) if "xdrg::" in r["Name"]]
+
+
+def per_config(tag, root):
+    """Per-config evidence (tools/profile_configs.sh): root/c<key>/{trace,fetch,write}
+    of one bench.py workload each -> profiles/<tag>_configs/c<key>_kernel_stats.csv
+    and pmc_traffic.json configs[key] from that config's own launches, with the
+    phase averages that reproduce bench.py's roofline fraction."""
+    prof = os.path.join(ROOT, "profiles")
+    out_dir = os.path.join(prof, f"{tag}_configs")
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(prof, "pmc_traffic.json")
+    doc = json.load(open(path))
+    for key, (recs, enc, dec) in CONFIGS.items():
+        d = os.path.join(root, f"c{key}")
+        tr = os.path.join(d, "trace", "run_kernel_stats.csv")
+        if not os.path.exists(tr):
+            print("no trace for", key)
+            continue
+        rows = _trace_stats(tr)
+        with open(os.path.join(out_dir, f"c{key}_kernel_stats.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "MinNs", "MaxNs"])
+            for r in rows:
+                w.writerow([short(r["Name"]), r["Calls"], r["TotalDurationNs"], r["AverageNs"], r["MinNs"], r["MaxNs"]])
+        avg = {short(r["Name"]).split("<")[0]: float(r["AverageNs"]) for r in rows}
+        fg = by_grid(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+        wg = by_grid(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+        enc, dec = resolve(enc, fg), resolve(dec, fg)
+        sides = []
+        for ks in (enc, dec):
+            if not all(k in fg and k in wg for k in ks):
+                break
+            sides.append((sum(2 * fg[k] * 1024 for k in ks), sum(wg[k] * 1024 for k in ks)))
+        # a phase's launch = its kernels back to back (bench.py times the phase)
+        phase_ns = [sum(avg.get(k[0], 0.0) for k in ks) for ks in (enc, dec)]
+        e = {"records": recs, "tag": tag, "encode": [k[0] for k in enc], "decode": [k[0] for k in dec],
+             "kernel_stats": os.path.relpath(os.path.join(out_dir, f"c{key}_kernel_stats.csv"), ROOT),
+             "phase_avg_ns": [round(x, 1) for x in phase_ns]}
+        if len(sides) == 2:
+            e.update({"fetch_bytes": [int(x[0]) for x in sides], "write_bytes": [int(x[1]) for x in sides],
+                      "bytes_per_launch": int(round(sum(x[0] + x[1] for x in sides) / 2))})
+        doc["configs"][key] = e
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
+        f.write("\n")
+    print(json.dumps(doc["configs"], indent=1))
+
+
 def main():
+    if sys.argv[1] == "--per-config":
+        per_config(sys.argv[2], sys.argv[3])
+        return
     tag, trace, fetch, write, records = sys.argv[1:6]
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
