@@ -1936,11 +1936,14 @@ __device__ void enc_record_block(const RecArgs &a, uint64_t r, uint64_t pos) {
 // one barrier (which also ends every use of the tile before it).  0 = record
 // js alone exceeds the tile.
 __device__ __forceinline__ uint32_t enc_fit(const RecArgs &a, const uint64_t (&base)[kMaxDynLds],
-                                            const uint32_t *srel, uint32_t js, uint32_t nrec) {
+                                            const uint32_t *srel, uint32_t js, uint32_t nrec,
+                                            const uint32_t *soff = nullptr, uint32_t mis = 0, uint32_t ocap = 0) {
     const uint32_t je = js + 1 + threadIdx.x;
     bool fits = false;
     if (je <= nrec) {
         uint32_t need = 0;
+        // output-imaged sub-batches: the output bytes from record js's line fit the image too
+        if (soff && soff[je] - soff[js] + ((mis + soff[js]) & 15u) > ocap) return (uint32_t)__syncthreads_count(false);
 #pragma unroll
         for (int d = 0; d < kMaxDynLds; ++d) {
             if ((uint32_t)d >= a.ndyn) continue;
@@ -2036,8 +2039,12 @@ __device__ __forceinline__ void enc_flush(const uint8_t *img, uint8_t *A0, uint3
     }
 }
 
-template <bool OUT>
+// MODE 0: input-staged (k_enc_stage); 1: output-imaged, inputs straight from
+// HBM (k_enc_ostage); 2: both tiles — inputs staged, output composed in an
+// LDS image, whole lines out (k_enc_iostage).
+template <int MODE>
 __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
+    constexpr bool OUT = MODE == 1;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;   // row stride of soff / srel
     uint32_t *soff = (uint32_t *)smem;
@@ -2132,20 +2139,32 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
         }
         return;
     }
-    if (a.framed)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
+    constexpr bool IMG = MODE == 2;
+    const uint32_t mis = (uint32_t)((uintptr_t)out & 15);
+    const uint32_t ocap = a.tile_bytes + (a.tile_bytes >> 3);   // the output image (MODE 2)
+    uint8_t *const img = tile + a.tile_bytes + kStageSlack;
+    if (a.framed && !IMG)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
         for (uint32_t j = tid; j < nrec; j += kRecThreads)
             *(uint32_t *)(out + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
     // ---- sub-batches
     uint32_t js = 0;
-    uint32_t k1 = enc_fit(a, base, srel, js, nrec);
+    uint32_t k1 = enc_fit(a, base, srel, js, nrec, IMG ? soff : nullptr, mis, ocap);
     while (js < nrec) {
         if (k1 == 0) {   // too large for the tile: the whole block writes record js
+            if (IMG && a.framed && tid == 0)
+                *(uint32_t *)(out + soff[js]) = bswap32r((soff[js + 1] - soff[js] - 4) | kLastFrag);
             enc_record_block(a, rb + js, bbase + soff[js]);
             ++js;
-            k1 = js < nrec ? enc_fit(a, base, srel, js, nrec) : 0;
+            k1 = js < nrec ? enc_fit(a, base, srel, js, nrec, IMG ? soff : nullptr, mis, ocap) : 0;
             continue;
         }
         const uint32_t je = js + k1;
+        const uint32_t head = (mis + soff[js]) & 15u;
+        // where field bytes go: the stream, or the image (byte 0 = record js's 16-byte line)
+        uint8_t *const wout = IMG ? img + head - soff[js] : out;
+        if (IMG && a.framed)
+            for (uint32_t j = js + tid; j < je; j += kRecThreads)
+                *(uint32_t *)(wout + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
         // stage every dynamic column's range of the sub-batch
         const uint8_t *a0[kMaxDynLds];
         uint32_t cb[kMaxDynLds + 1];
@@ -2175,7 +2194,7 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
                     const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
                     const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
                     for (uint32_t j = js + tid / G; j < je; j += ng) {
-                        uint8_t *dst = out + soff[j] + fpre + dyn_before(a, srel, j, d);
+                        uint8_t *dst = wout + soff[j] + fpre + dyn_before(a, srel, j, d);
                         for (uint32_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
                     }
                 }
@@ -2194,7 +2213,7 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
             for (uint32_t j = js + tid / G; j < je; j += ng) {
                 const uint64_t cnt = rel[j + 1] - rel[j];
                 const uint8_t *p = f.data + (base[d] + rel[j]) * esz;
-                uint8_t *dst = out + soff[j] + fpre + dyn_before(a, srel, j, d);
+                uint8_t *dst = wout + soff[j] + fpre + dyn_before(a, srel, j, d);
                 const int64_t L = lds0 + (int64_t)(uintptr_t)p;   // tile offset of p
                 if (bytes) {
                     const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
@@ -2217,12 +2236,17 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
             }
             ++d;
         }
+        if (IMG) {   // the image out as whole 16-byte lines
+            __syncthreads();
+            enc_flush(img, out + soff[js] - head, head, head + soff[je] - soff[js]);
+        }
         js = je;
-        k1 = js < nrec ? enc_fit(a, base, srel, js, nrec) : 0;   // its barrier ends the tile's use
+        k1 = js < nrec ? enc_fit(a, base, srel, js, nrec, IMG ? soff : nullptr, mis, ocap) : 0;   // its barrier ends the tiles' use
     }
 }
-__global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) { k_enc_stage_t<false>(a); }
-__global__ __launch_bounds__(kRecThreads) void k_enc_ostage(const RecArgs a) { k_enc_stage_t<true>(a); }
+__global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) { k_enc_stage_t<0>(a); }
+__global__ __launch_bounds__(kRecThreads) void k_enc_ostage(const RecArgs a) { k_enc_stage_t<1>(a); }
+__global__ __launch_bounds__(kRecThreads) void k_enc_iostage(const RecArgs a) { k_enc_stage_t<2>(a); }
 
 // ---- decode -------------------------------------------------------------------
 // LDS: sstart[RPB + 1] u32 (record start - the block's first start) | snrel[ND][RPB + 1] u32 |
@@ -2924,7 +2948,11 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     case REC_ENC_PLACE:
         if (stage) {   // small-record blocks staged, large-record blocks by the group kernel
             a.big_rec = t.big_rec;
-            if (t.enc_out)   // output-staged sub-batches (tuning key 27)
+            if (t.enc_out == 2)   // staged inputs, output image (tuning key 27)
+                hipLaunchKernelGGL(k_enc_iostage, dim3(nb), dim3(kRecThreads),
+                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack + a.tile_bytes +
+                                       (a.tile_bytes >> 3) + 32, st, a);
+            else if (t.enc_out)   // output-imaged sub-batches, inputs from HBM (tuning key 27)
                 hipLaunchKernelGGL(k_enc_ostage, dim3(nb), dim3(kRecThreads),
                                    enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
             else

@@ -183,8 +183,9 @@ struct Tuning {
     uint32_t big_rec = 1024;        // key 13: blocks averaging >= this many XDR bytes per record
                                     // take the group kernels (0 = never)
     int32_t pay_nts = 1;            // key 28: encode payload kernel: 1 nontemporal 16-byte stores, 0 plain
-    int32_t enc_out = 0;            // key 27: staged encode: 1 output-staged sub-batches (k_enc_ostage:
-                                    // composed in LDS, whole 16-byte lines out), 0 input-staged (k_enc_stage)
+    int32_t enc_out = 0;            // key 27: staged encode: 0 input-staged (k_enc_stage), 1 output image
+                                    // composed from HBM (k_enc_ostage), 2 input-staged + output image
+                                    // (k_enc_iostage); the image leaves as whole 16-byte lines
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
 };

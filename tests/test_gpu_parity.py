@@ -50,7 +50,8 @@ SCHEMAS = {
 REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),),
                "staged_edges": ((9, 4), (20, 0)),
                "staged_lean": ((9, 4), (20, 1)),
-               "staged_out": ((9, 4), (27, 1))}   # output-staged encode (k_enc_ostage)
+               "staged_out": ((9, 4), (27, 1)),    # output image from HBM inputs (k_enc_ostage)
+               "staged_io": ((9, 4), (27, 2))}     # staged inputs + output image (k_enc_iostage)
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
@@ -271,7 +272,7 @@ def test_error_parity(gpu_ctx, rec_kernel, name, framed):
             assert g2[:3] == o2[:3], desc
 
 
-@pytest.mark.parametrize("enc_out", [0, 1], ids=["enc_in", "enc_out"])
+@pytest.mark.parametrize("enc_out", [0, 1, 2], ids=["enc_in", "enc_out", "enc_io"])
 @pytest.mark.parametrize("lean", [1, 0, 2], ids=["lean", "edges", "sweep"])
 @pytest.mark.parametrize("tile", [1024, 4096])
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
