@@ -1940,10 +1940,10 @@ __device__ __forceinline__ uint32_t enc_fit(const RecArgs &a, const uint64_t (&b
                                             const uint32_t *soff = nullptr, uint32_t mis = 0, uint32_t ocap = 0) {
     const uint32_t je = js + 1 + threadIdx.x;
     bool fits = false;
-    if (je <= nrec) {
+    // output-imaged sub-batches: the output bytes from record js's line fit the image too
+    // (one barrier for every thread: the count below)
+    if (je <= nrec && (!soff || soff[je] - soff[js] + ((mis + soff[js]) & 15u) <= ocap)) {
         uint32_t need = 0;
-        // output-imaged sub-batches: the output bytes from record js's line fit the image too
-        if (soff && soff[je] - soff[js] + ((mis + soff[js]) & 15u) > ocap) return (uint32_t)__syncthreads_count(false);
 #pragma unroll
         for (int d = 0; d < kMaxDynLds; ++d) {
             if ((uint32_t)d >= a.ndyn) continue;

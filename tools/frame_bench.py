@@ -76,6 +76,30 @@ def main():
                 "frame_scan_ms": round(t * 1e3, 3), "frame_scan_GBps": round(len(s) / t / 1e9, 1),
                 "deframe_ms": round(t2 * 1e3, 3), "deframe_GBps": round(len(s) / t2 / 1e9, 1),
                 "cpu_serial_walk_GBps": round(len(s) / tc / 1e9, 2)})
+    del dev, offs, payload
+    # 3. the serial cliff: one fragment whose size is not a multiple of 4 on
+    # the chain (a peer's odd-sized opaque body) sends the whole walk to the
+    # one-lane k_fr_serial kernel (same results, measured bound)
+    parts = [oracle.fragment(b"abc", 4096)]
+    for i in range(20000):
+        body = rng.integers(0, 256, int(rng.integers(0, 1024)) * 4, dtype=np.uint8).tobytes()
+        parts.append(oracle.fragment(body, int(rng.choice([64, 512, 4096]))))
+    s = b"".join(parts)
+    dev = torch.from_numpy(np.frombuffer(s, dtype=np.uint8).copy()).cuda()
+    offs = torch.zeros(20002, dtype=torch.int64, device="cuda")
+    t = timed(lambda: ctx.frame_scan(dev, len(s), offs, 20001), reps=3)
+    assert ctx.frame_scan(dev, len(s), offs, 20001) == 20001
+    rc, want = oracle.frame_scan(s, 20001)
+    assert offs.cpu().numpy().astype(np.uint64)[:20002].tolist() == list(want)[:20002]
+    t0 = time.perf_counter()
+    oracle.frame_scan(s, 20001)
+    tc = time.perf_counter() - t0
+    frags = sum(len(p) for p in parts)
+    out.append({"stream": "20k messages 0..4 KiB after one 3-byte fragment (serial walk on the GPU)",
+                "bytes": len(s), "frame_scan_ms": round(t * 1e3, 3),
+                "frame_scan_GBps": round(len(s) / t / 1e9, 3), "cpu_serial_walk_GBps": round(len(s) / tc / 1e9, 2),
+                "note": "k_fr_serial: one lane hops mark to mark; the same stream without the odd fragment "
+                        "takes the parallel walk"})
     for o in out:
         print(json.dumps(o))
 
