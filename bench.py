@@ -307,11 +307,13 @@ class Workload:
         """The receive pipeline of a record-marked stream (RpcMessageParserTCP
         -> RpcProtocolFilter): xdrg_frame_scan walks the marks, then
         xdrg_decode_batch(XDRG_FRAME_RM) decodes the messages at the offsets
-        the walk found (never the encoder's)."""
+        the walk found (never the encoder's).  Fixed-size messages decode
+        synchronously: the engine checks the offsets for the fixed stride and
+        then takes the stride kernels (tuning key 29)."""
         m = self.ctx.frame_scan(self.xdr, self.xlen, self.scan_offs, self.n)
         assert m == self.n, f"frame scan found {m} of {self.n} messages"
         self.ctx.decode(self.sch, self.xdr, self.xlen, self.n, self.cout, rec_offsets=self.scan_offs,
-                        framed=True, async_=True)
+                        framed=True, async_=self.cfg != 2)
 
     def clear_outputs(self):
         """Zero the XDR stream and every decode target (tools/sweep_rec.py:

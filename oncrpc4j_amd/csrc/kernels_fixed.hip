@@ -868,6 +868,22 @@ int launch_finalize(const unsigned long long *errkey, unsigned long long extra_k
 }  // namespace xdrg
 
 namespace xdrg {
+// out[0] |= 1 when some record extent of ro (n + 1 offsets) is not `stride`
+// bytes; out[1] = ro[0].  Decides whether fixed-size records at explicit
+// extents (a frame scan's offsets) can take the fixed-stride kernels.
+__global__ void k_check_stride(const uint64_t *ro, uint64_t n, uint64_t stride, unsigned long long *out) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false;
+    for (uint64_t i = tid; i < n; i += (uint64_t)gridDim.x * blockDim.x) bad |= ro[i + 1] - ro[i] != stride;
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(out, 1ull);
+    if (tid == 0) out[1] = ro[0];
+}
+int launch_check_stride(const uint64_t *ro, uint64_t n, uint64_t stride, unsigned long long *out, void *stream) {
+    const uint64_t blocks = grid_for(n, 256, (uint64_t)num_cu() * 8);
+    hipLaunchKernelGGL(k_check_stride, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ro, n, stride, out);
+    return (int)hipGetLastError();
+}
+
 __global__ void k_store_u64(uint64_t *dst, uint64_t v) {
     if (threadIdx.x == 0 && blockIdx.x == 0) *dst = v;
 }

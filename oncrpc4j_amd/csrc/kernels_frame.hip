@@ -13,16 +13,18 @@
 // traffic are multiples of 4; a stream whose real chain meets another size
 // is walked serially (k_fr_serial), with the same result.
 //
-//   k_fr_exits  block per super-chunk (64 sub-chunks of 4096 words), sub-
+//   k_fr_exits  block per super-chunk (16 sub-chunks of 4096 words), sub-
 //               chunks from last to first: stage the words, point every word
 //               at its next mark, resolve pointers into later sub-chunks
-//               through their finished exits (LDS for the next one, HBM
-//               beyond), pointer-jump the pointers that stay inside (active
-//               words only) -> exitS[q] = first chain word at or past the
-//               super-chunk end.  One read of the stream, one write of exitS.
+//               through their finished results, pointer-jump the pointers
+//               that stay inside (active words, compacted) -> exitR[q] = the
+//               last chain word inside the super-chunk (16-bit, super-local);
+//               the super-chunk exit of q is that word's next mark, which the
+//               readers recompute (fr_exit).  One read of the stream, 2 B per
+//               word written.
 //   k_fr_fix_* each super-chunk's true entry: groups of 64 super-chunks
 //               resolve the exit of every entry in their first words in
-//               parallel (windows of exitS in LDS), one wave hops group to
+//               parallel (windows of exits in LDS), one wave hops group to
 //               group from word 0, each group fills in its super-chunks.
 //   k_fr_mark   block per super-chunk, sub-chunks first to last from its
 //               entry: stage, mark the chain by pointer doubling (round r
@@ -92,25 +94,52 @@ __device__ __forceinline__ bool fr_block_any(bool p, FrAny &a, uint32_t &par) {
     return (v.x | v.y | v.z | v.w) != 0;
 }
 
+// Next chain word on a full sub-chunk (every position < Q), R = whole words
+// left from q (>= 1): one compare of the size against R.  A size that is not
+// a multiple of 4 and reaches no further than the last whole word gives
+// kFUnal even when the fragment would end in the missing bytes of a partial
+// last word (fr_next says kFStop there): either way the real chain ending on
+// it leaves the word walk, and the exact walk settles it.
+__device__ __forceinline__ uint32_t fr_next_full(uint32_t m, uint32_t q, uint32_t R) {
+    const uint32_t sz4 = (m >> 2) & 0x1fffffffu;
+    return sz4 < R ? ((m & 3u) ? kFUnal : q + 1 + sz4) : kFStop;
+}
+
+// Inclusive prefix sum over the wave.
+__device__ __forceinline__ uint32_t fr_wave_incl(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t a = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += a;
+    }
+    return v;
+}
+
 // ---------------------------------------------------------------------------
 // k_fr_exits
 // ---------------------------------------------------------------------------
-// Sub-chunks from last to first.  A word whose next mark stays inside the
-// sub-chunk is active: its LDS pointer jumps (in place: a value read early is
-// still a successor on the same chain) until it leaves.  A pointer into a
-// later sub-chunk of the super-chunk resolves through that sub-chunk's exits,
-// which this block already wrote to exitS (L2; never read before, so no
-// stale L1 line).  16 KiB of LDS, so several blocks share a CU.
-__global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
-                                                      uint32_t *exitS) {
+// Sub-chunks from last to first.  J holds, per word, either a sub-chunk-local
+// pointer (< kFChunk: the word's chain goes on inside the sub-chunk) or a
+// result kFRes | r (r = super-local last chain word inside the super-chunk).
+// A word whose next mark stays inside the sub-chunk is active: its pointer
+// jumps (in place: a value read early is still a successor on the same chain)
+// until it holds a result.  The active words are compacted into a list first,
+// so every thread jumps ceil(active / 256) of them per round whatever the
+// layout of the marks.  A next mark in a later sub-chunk of the super-chunk
+// takes that word's result from exitR, which this block already wrote (L2;
+// never read before, so no stale L1 line).  24 KiB of LDS.  (The next sub-chunk's results kept in LDS instead measured slower:
+// 32 KiB, fewer blocks per CU.)
+constexpr uint32_t kFRes = 0x10000u;
+__global__ __launch_bounds__(256, 4) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
+                                                      uint16_t *exitR) {
     __shared__ __attribute__((aligned(16))) uint32_t J[kFChunk];
-    __shared__ __attribute__((aligned(16))) FrAny any;
-    const uint32_t tid = threadIdx.x;
+    __shared__ __attribute__((aligned(16))) uint16_t L[kFChunk];   // active positions (sub-chunk local)
+    __shared__ uint32_t wtot[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t sbeg = blockIdx.x * kFSuper;
-    const uint32_t send = min(sbeg + kFSuper, Q);
-    const uint32_t sfin = sbeg + kFSuper;   // exits are chain words >= sfin (or == Q)
+    const uint32_t send = min(sbeg + kFSuper, Q);   // chain words past it leave the super-chunk
     const uint32_t nsub = (send - sbeg + kFChunk - 1) / kFChunk;
-    uint32_t par = 0;
     uint32_t x[16], y[16];
     fr_cload(w, Q, sbeg + (nsub - 1) * kFChunk, tid, x);
     for (int j = (int)nsub - 1; j >= 0; --j) {
@@ -118,42 +147,96 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
         const uint32_t bend = base + kFChunk;
         if (j > 0) fr_cload(w, Q, base - kFChunk, tid, y);   // next sub-chunk's words in flight
         uint32_t t[16], act = 0;
+        if (bend <= Q) {
+            const uint32_t q0 = base + 4 * tid, R0 = Q - q0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t ci = 1024 * (i >> 2) + (i & 3);
+                t[i] = fr_next_full(fr_bswap(x[i]), q0 + ci, R0 - ci);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t q = base + fr_cw(tid, i);
+                t[i] = q < Q ? fr_next(fr_bswap(x[i]), q, Q, tb) : kFStop;
+            }
+        }
+        // J: a local pointer (next mark inside), the raw next mark when it lies
+        // in a later sub-chunk [bend, send) (looked up below), else the word
+        // itself as the last one
+        const uint32_t lim = send > bend ? send - bend : 0u;
+        const uint32_t own0 = kFRes | (base - sbeg + 4 * tid);
+        uint32_t look = 0;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const uint32_t q = base + fr_cw(tid, i);
-            const uint32_t v = q < Q ? fr_next(fr_bswap(x[i]), q, Q, tb) : kFStop;
-            act |= (v < bend ? 1u : 0u) << i;   // v < bend: a word inside (terminals are >= kFUnal)
-            t[i] = v;
+            const uint32_t v = t[i];
+            act |= (v < bend ? 1u : 0u) << i;   // a word inside (terminals are >= kFUnal)
+            const bool lk = v - bend < lim;
+            look |= (lk ? 1u : 0u) << i;
+            t[i] = v < bend ? v - base : lk ? v : own0 + 1024 * (i >> 2) + (i & 3);
         }
-#pragma unroll
-        for (int i = 0; i < 16; ++i)   // final exits of later sub-chunks' words
-            if (t[i] >= bend && t[i] < sfin && t[i] < Q) t[i] = exitS[t[i]];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             *(u32x4f *)&J[4 * tid + 1024 * k] = u32x4f{t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
-        __syncthreads();
-        for (;;) {
-            for (uint32_t m = act; m; m &= m - 1) {
-                const int i = __ffs(m) - 1;
-                const uint32_t li = fr_cw(tid, i);
-                const uint32_t u = J[J[li] - base];
-                J[li] = u;
-                if (u - base >= kFChunk) act &= ~(1u << i);
-            }
-            if (!fr_block_any(act != 0, any, par)) break;
+        for (uint32_t m = look; m; m &= m - 1) {   // own words: no barrier needed
+            const uint32_t li = fr_cw(tid, __ffs(m) - 1);
+            J[li] = kFRes | exitR[J[li]];
         }
-        if (base + kFChunk <= Q) {
+        const uint32_t cnt = __popc(act);
+        const uint32_t incl = fr_wave_incl(cnt);
+        if (lane == 63) wtot[wv] = incl;
+        __syncthreads();   // J, wtot
+        const uint32_t t0 = wtot[0], t1 = wtot[1], t2 = wtot[2], t3 = wtot[3];
+        const uint32_t A = t0 + t1 + t2 + t3;   // active words of the sub-chunk
+        uint32_t pos = incl - cnt + (wv > 0 ? t0 : 0u) + (wv > 1 ? t1 : 0u) + (wv > 2 ? t2 : 0u);
+        for (uint32_t m = act; m; m &= m - 1) L[pos++] = (uint16_t)fr_cw(tid, __ffs(m) - 1);
+        if (A) {
+            __syncthreads();   // L
+            // this thread's list entries: tid + 256 c, c < ceil((A - tid) / 256).
+            // Asynchronous pointer jumping: a thread jumps its own entries until
+            // they hold results, reading whatever the other threads have written
+            // meanwhile (LDS words are read and written whole, and every value a
+            // word ever holds is a successor on its chain), so no barrier per
+            // round.  Positions only grow, so a pointer resolves within kFChunk
+            // jumps (the bound is a guard).
+            const uint32_t mine = A > tid ? (A - tid - 1) / 256 + 1 : 0u;
+            uint32_t pend = mine >= 32 ? ~0u : (1u << mine) - 1u;
+            for (uint32_t it = 0; pend && it < kFChunk; ++it) {
+                for (uint32_t m = pend; m; m &= m - 1) {
+                    const uint32_t c = __ffs(m) - 1;
+                    const uint32_t li = L[tid + 256 * c];
+                    const uint32_t u = J[J[li]];
+                    J[li] = u;
+                    if (u >= kFRes) pend &= ~(1u << c);
+                }
+            }
+            __syncthreads();   // every entry holds its result
+        }
+        typedef uint16_t u16x4f __attribute__((ext_vector_type(4)));
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                *(u32x4f *)(exitS + base + 4 * tid + 1024 * k) = *(const u32x4f *)&J[4 * tid + 1024 * k];
-        } else {
-            for (int i = 0; i < 16; ++i)
-                if (base + fr_cw(tid, i) < Q) exitS[base + fr_cw(tid, i)] = J[fr_cw(tid, i)];
+        for (int k = 0; k < 4; ++k) {
+            const u32x4f v = *(const u32x4f *)&J[4 * tid + 1024 * k];
+            const u16x4f h = u16x4f{(uint16_t)v.x, (uint16_t)v.y, (uint16_t)v.z, (uint16_t)v.w};
+            if (bend <= Q) {
+                *(u16x4f *)(exitR + base + 4 * tid + 1024 * k) = h;
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (base + 4 * tid + 1024 * k + c < Q) exitR[base + 4 * tid + 1024 * k + c] = h[c];
+            }
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = y[i];
-        __syncthreads();   // this sub-chunk's exitS visible to the block; J free again
+        __syncthreads();   // this sub-chunk's exitR visible to the block; J, L, wtot free again
     }
+}
+
+// The super-chunk exit of word q < Q: the next mark after its chain's last
+// word inside the super-chunk (a word >= min(super end, Q), or a terminal).
+__device__ __forceinline__ uint32_t fr_exit(const uint32_t *w, const uint16_t *exitR, uint32_t Q, uint32_t tb,
+                                            uint32_t q) {
+    const uint32_t r = (q & ~(kFSuper - 1)) + exitR[q];
+    return fr_next(fr_bswap(w[r]), r, Q, tb);
 }
 
 // ---------------------------------------------------------------------------
@@ -163,41 +246,48 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
 //   k_fr_fix_grp   block per group: the group's exit for every entry word in
 //                  the first kFixWin words of its first super-chunk (a lane
 //                  per entry hops super-chunk to super-chunk through windows
-//                  of exitS staged in LDS; an entry deeper than the window
-//                  reads exitS from HBM);
+//                  of exits staged in LDS; an entry deeper than the window
+//                  recomputes its exit from exitR);
 //   k_fr_fix_top   one wave hops group to group from word 0 (a deep group
-//                  entry walks that group's super-chunks through exitS);
+//                  entry walks that group's super-chunks through fr_exit);
 //   k_fr_fix_fill  block per group: from its true entry, every super-chunk
 //                  entry of the group (sentry).
 constexpr uint32_t kFixWin = 256;   // entry words per super-chunk window
 constexpr uint32_t kFixGrp = 64;    // super-chunks per group
-__device__ __forceinline__ void fix_stage(const uint32_t *exitS, uint32_t Q, uint32_t nsup, uint32_t g, uint32_t *win) {
+struct FrExits {   // what fr_exit reads
+    const uint32_t *w;
+    const uint16_t *exitR;
+    uint32_t Q, tb;
+    __device__ __forceinline__ uint32_t operator()(uint32_t q) const { return fr_exit(w, exitR, Q, tb, q); }
+};
+__device__ __forceinline__ void fix_stage(const FrExits &ex, uint32_t nsup, uint32_t g, uint32_t *win) {
     for (uint32_t k = threadIdx.x / 64; k < kFixGrp; k += blockDim.x / 64) {   // a wave per super-chunk
         const uint32_t s = g * kFixGrp + k;
 #pragma unroll
         for (uint32_t c = 0; c < kFixWin / 64; ++c) {
             const uint64_t q = (uint64_t)s * kFSuper + 64 * c + (threadIdx.x & 63);
-            win[k * kFixWin + 64 * c + (threadIdx.x & 63)] = (s < nsup && q < Q) ? exitS[q] : kFStop;
+            win[k * kFixWin + 64 * c + (threadIdx.x & 63)] = (s < nsup && q < ex.Q) ? ex((uint32_t)q) : kFStop;
         }
     }
     __syncthreads();
 }
 // One hop from chain word e inside group g: the exit of e's super-chunk.
-__device__ __forceinline__ uint32_t fix_hop(const uint32_t *exitS, const uint32_t *win, uint32_t g, uint32_t e) {
+__device__ __forceinline__ uint32_t fix_hop(const FrExits &ex, const uint32_t *win, uint32_t g, uint32_t e) {
     const uint32_t s = e >> (kFChunkLog2 + kFSuperLog2), d = e & (kFSuper - 1);
-    return d < kFixWin ? win[(s - g * kFixGrp) * kFixWin + d] : exitS[e];
+    return d < kFixWin ? win[(s - g * kFixGrp) * kFixWin + d] : ex(e);
 }
 
-__global__ __launch_bounds__(256) void k_fr_fix_grp(const uint32_t *exitS, uint32_t Q, uint32_t nsup, uint32_t *gexit) {
+__global__ __launch_bounds__(256) void k_fr_fix_grp(FrExits ex, uint32_t nsup, uint32_t *gexit) {
     __shared__ uint32_t win[kFixGrp * kFixWin];
     const uint32_t g = blockIdx.x;
-    fix_stage(exitS, Q, nsup, g, win);
+    const uint32_t Q = ex.Q;
+    fix_stage(ex, nsup, g, win);
     const uint64_t gend64 = (uint64_t)(g + 1) * kFixGrp * kFSuper;
     const uint32_t gend = gend64 < Q ? (uint32_t)gend64 : Q;
     uint32_t e = g * kFixGrp * kFSuper + threadIdx.x;   // this lane's entry word
     if (e < gend) {
         while (e < gend) {
-            e = fix_hop(exitS, win, g, e);
+            e = fix_hop(ex, win, g, e);
             if (e >= kFUnal) break;
         }
     } else {
@@ -206,18 +296,19 @@ __global__ __launch_bounds__(256) void k_fr_fix_grp(const uint32_t *exitS, uint3
     gexit[(uint64_t)g * kFixWin + threadIdx.x] = e;
 }
 
-__global__ __launch_bounds__(64) void k_fr_fix_top(const uint32_t *exitS, const uint32_t *gexit, uint32_t Q,
-                                                   uint32_t *gentry, uint64_t *res) {
+__global__ __launch_bounds__(64) void k_fr_fix_top(FrExits ex, const uint32_t *gexit, uint32_t *gentry,
+                                                   uint64_t *res) {
+    const uint32_t Q = ex.Q;
     uint32_t e = 0;
     while (e < Q) {
         const uint32_t g = e / (kFixGrp * kFSuper), d = e - g * kFixGrp * kFSuper;
         gentry[g] = e;   // one address for the whole wave
         if (d < kFixWin) {
             e = gexit[(uint64_t)g * kFixWin + d];
-        } else {         // a deep group entry: walk its super-chunks through exitS
+        } else {         // a deep group entry: walk its super-chunks through fr_exit
             const uint64_t gend = (uint64_t)(g + 1) * kFixGrp * kFSuper;
             while (e < Q && e < gend) {
-                e = exitS[e];
+                e = ex(e);
                 if (e >= kFUnal) break;
             }
         }
@@ -226,19 +317,20 @@ __global__ __launch_bounds__(64) void k_fr_fix_top(const uint32_t *exitS, const 
     if (threadIdx.x == 0) res[0] = e;   // >= Q: ran to the end; kFStop / kFUnal: terminal met on the real chain
 }
 
-__global__ __launch_bounds__(256) void k_fr_fix_fill(const uint32_t *exitS, const uint32_t *gentry, uint32_t Q,
-                                                     uint32_t nsup, uint32_t *sentry) {
+__global__ __launch_bounds__(256) void k_fr_fix_fill(FrExits ex, const uint32_t *gentry, uint32_t nsup,
+                                                     uint32_t *sentry) {
     __shared__ uint32_t win[kFixGrp * kFixWin];
     const uint32_t g = blockIdx.x;
+    const uint32_t Q = ex.Q;
     uint32_t e = gentry[g];
     if (e == kFNone) return;   // the chain skips this group (block-uniform)
-    fix_stage(exitS, Q, nsup, g, win);
+    fix_stage(ex, nsup, g, win);
     if (threadIdx.x) return;
     const uint64_t gend64 = (uint64_t)(g + 1) * kFixGrp * kFSuper;
     const uint32_t gend = gend64 < Q ? (uint32_t)gend64 : Q;
     while (e < gend) {
         sentry[e >> (kFChunkLog2 + kFSuperLog2)] = e;
-        e = fix_hop(exitS, win, g, e);
+        e = fix_hop(ex, win, g, e);
         if (e >= kFUnal) break;
     }
 }
@@ -315,16 +407,28 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
         if (j + 1 < nsub) { fr_cload(w, Q, bend, tid, y); held = j + 1; }   // next sub-chunk in flight
         uint32_t act = 0, cf = 0, lf = 0, lv = 0;   // per word: active / complete fragment / LAST / next leaves
         uint32_t p[8];                              // local pointers, two u16 per register
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t q = base + fr_cw(tid, i);
-            const uint32_t m = fr_bswap(x[i]);
-            const uint32_t v = q < Q ? fr_next(m, q, Q, tb) : kFStop;
+        auto word = [&](int i, uint32_t m, uint32_t v) {
             cf |= (v < kFUnal ? 1u : 0u) << i;
-            lf |= (q < Q ? m >> 31 : 0u) << i;
+            lf |= (m >> 31) << i;
             lv |= (v >= bend ? 1u : 0u) << i;       // v < bend: a word inside (v > q >= base)
             const uint32_t pi = v < bend ? v - base : kFOut;
             if (i & 1) p[i >> 1] |= pi << 16; else p[i >> 1] = pi;
+        };
+        if (bend <= Q) {
+            const uint32_t q0 = base + 4 * tid, R0 = Q - q0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t ci = 1024 * (i >> 2) + (i & 3);
+                const uint32_t m = fr_bswap(x[i]);
+                word(i, m, fr_next_full(m, q0 + ci, R0 - ci));
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t q = base + fr_cw(tid, i);
+                const uint32_t m = q < Q ? fr_bswap(x[i]) : 0u;
+                word(i, m, q < Q ? fr_next(m, q, Q, tb) : kFStop);
+            }
         }
         act = ~lv & 0xffffu;
         typedef uint32_t u32x2f __attribute__((ext_vector_type(2)));
@@ -420,8 +524,12 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
             lb16[pi] = (uint16_t)pl;
         }
         if (om & lv) {   // the marked node whose next leaves the sub-chunk (terminals too): one thread
-            const uint32_t q = base + fr_cw(tid, __ffs(om & lv) - 1);
-            e_next = q < Q ? fr_next(fr_bswap(w[q]), q, Q, tb) : kFStop;
+            const uint32_t b = __ffs(om & lv) - 1;
+            uint32_t xm = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) xm = (uint32_t)i == b ? x[i] : xm;   // its word, from registers
+            const uint32_t q = base + fr_cw(tid, b);
+            e_next = q < Q ? fr_next(fr_bswap(xm), q, Q, tb) : kFStop;
         }
         const uint32_t cnt = fr_wave_sum(__popc(oc) | __popc(ol) << 16);
         const uint32_t b01 = fr_wave_sum(__popc(oc & 0xfu) | __popc(oc & 0xf0u) << 16);
@@ -694,13 +802,14 @@ int frame_parallel(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t 
     const uint32_t *w = (const uint32_t *)in;
     const uint32_t Q = (uint32_t)(len / 4), tb = (uint32_t)(len & 3);
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
-    hipLaunchKernelGGL(k_fr_exits, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitS);
+    hipLaunchKernelGGL(k_fr_exits, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitR);
     const uint64_t ngrp = (nsup + kFixGrp - 1) / kFixGrp;
     if (hipMemsetAsync(ws.sentry, 0xff, nsup * 4, st) != hipSuccess) return (int)hipErrorUnknown;
     if (hipMemsetAsync(ws.gentry, 0xff, ngrp * 4, st) != hipSuccess) return (int)hipErrorUnknown;
-    hipLaunchKernelGGL(k_fr_fix_grp, dim3((uint32_t)ngrp), dim3(kFixWin), 0, st, ws.exitS, Q, (uint32_t)nsup, ws.gexit);
-    hipLaunchKernelGGL(k_fr_fix_top, dim3(1), dim3(64), 0, st, ws.exitS, ws.gexit, Q, ws.gentry, ws.res);
-    hipLaunchKernelGGL(k_fr_fix_fill, dim3((uint32_t)ngrp), dim3(256), 0, st, ws.exitS, ws.gentry, Q, (uint32_t)nsup,
+    const FrExits ex{w, ws.exitR, Q, tb};
+    hipLaunchKernelGGL(k_fr_fix_grp, dim3((uint32_t)ngrp), dim3(kFixWin), 0, st, ex, (uint32_t)nsup, ws.gexit);
+    hipLaunchKernelGGL(k_fr_fix_top, dim3(1), dim3(64), 0, st, ex, ws.gexit, ws.gentry, ws.res);
+    hipLaunchKernelGGL(k_fr_fix_fill, dim3((uint32_t)ngrp), dim3(256), 0, st, ex, ws.gentry, (uint32_t)nsup,
                        ws.sentry);
     hipLaunchKernelGGL(k_fr_mark, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.sub,
                        ws.fbits, ws.lbits, ws.sup);

@@ -360,6 +360,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 26: if (!in(0, 1)) return -1; t.stage_copy = (int32_t)v; return 0;
     case 27: if (!in(0, 2)) return -1; t.enc_out = (int32_t)v; return 0;
     case 28: if (!in(0, 1)) return -1; t.pay_nts = (int32_t)v; return 0;
+    case 29: if (!in(0, 1)) return -1; t.stride_check = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -976,6 +977,25 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         return finish_decode(c, n, kNoError, true, async, first_bad, err);
     }
 
+    // Fixed-size records at explicit extents that turn out to be the fixed
+    // stride — a frame scan of uniform single-fragment messages, the receive
+    // side of GrizzlyRpcTransport's one mark per reply — take the stride
+    // kernels after one device check of the offsets (sync calls; one round
+    // trip).  Same records, same checks: record i is [ro[0] + i*stride, +stride).
+    if (!s->var_size && rec_offsets && n && !async && !byref && c->tune.stride_check) {
+        const uint64_t stride = s->fixed_size + (framed ? 4 : 0);
+        HIPCHK(c, hipMemsetAsync(c->d_stat + 6, 0, 16, c->stream));
+        HIPCHK(c, (hipError_t)launch_check_stride(rec_offsets, n, stride, c->d_stat + 6, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_stat + 6, c->d_stat + 6, 16, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const uint64_t o0 = c->h_stat[7];
+        if (!c->h_stat[6] && stride && o0 <= in_len && n * stride <= in_len - o0 && n * stride / n == stride &&
+            aligned(in + o0, 4)) {
+            in += o0;
+            in_len -= o0;
+            rec_offsets = nullptr;
+        }
+    }
     if (!s->var_size && !rec_offsets) {
         const uint64_t stride = s->fixed_size + (framed ? 4 : 0);
         const uint64_t total = n * stride;
@@ -1476,7 +1496,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     const uint64_t F = Q + 2;
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_ex = take(4 * Q), o_se = take(4 * nsup), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
+    const size_t o_ex = take(2 * Q), o_se = take(4 * nsup), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
                  o_fb = take(512 * nsub), o_lb = take(512 * nsub), o_su = take(sizeof(FrameSuper) * nsup),
                  o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_re = take(64);
     if (off > c->fws_bytes) {
@@ -1490,7 +1510,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
         c->fws_bytes = off;
     }
     uint8_t *b = (uint8_t *)c->d_fws;
-    ws.exitS = (uint32_t *)(b + o_ex);
+    ws.exitR = (uint16_t *)(b + o_ex);
     ws.sentry = (uint32_t *)(b + o_se);
     ws.gexit = (uint32_t *)(b + o_ge);
     ws.gentry = (uint32_t *)(b + o_gn);

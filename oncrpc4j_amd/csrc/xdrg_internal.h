@@ -182,6 +182,8 @@ struct Tuning {
     uint32_t sweep_tile = 21504;    // key 25: the sweep decode's LDS tile (k_dec_sweep, 4 blocks per CU)
     uint32_t big_rec = 1024;        // key 13: blocks averaging >= this many XDR bytes per record
                                     // take the group kernels (0 = never)
+    int32_t stride_check = 1;       // key 29: fixed-size decode at rec_offsets: 1 check for the fixed
+                                    // stride and take the stride kernels (sync calls), 0 the record path
     int32_t pay_nts = 1;            // key 28: encode payload kernel: 1 nontemporal 16-byte stores, 0 plain
     int32_t enc_out = 0;            // key 27: staged encode: 0 input-staged (k_enc_stage), 1 output image
                                     // composed from HBM (k_enc_ostage), 2 input-staged + output image
@@ -209,6 +211,8 @@ int launch_rec_phase(const RecArgs &a, int phase, const Tuning &t, void *stream)
 int launch_store_u64(uint64_t *dst, uint64_t value, void *stream);
 // rec_offsets[i] = i * stride for i in [0, n]
 int launch_iota(uint64_t *dst, uint64_t n, uint64_t stride, void *stream);
+// out[0] |= 1 if some extent ro[i+1] - ro[i] != stride (i < n); out[1] = ro[0]
+int launch_check_stride(const uint64_t *ro, uint64_t n, uint64_t stride, unsigned long long *out, void *stream);
 // Combine the device error key with a host-side key and write the public
 // results (async mode); any output pointer may be NULL.
 int launch_finalize(const unsigned long long *errkey, unsigned long long extra_key, uint64_t n,
@@ -219,6 +223,7 @@ constexpr uint32_t kFChunkLog2 = 12;
 constexpr uint32_t kFChunk = 1u << kFChunkLog2;      // words per sub-chunk (16 KiB of stream)
 constexpr uint32_t kFSuperLog2 = 4;                  // sub-chunks per super-chunk, log2
 constexpr uint32_t kFSuper = kFChunk << kFSuperLog2; // words per super-chunk (256 KiB)
+static_assert(kFSuper <= 65536, "super-local chain words are 16-bit (FrameWs::exitR)");
 constexpr uint32_t kFStop = 0xffffffffu;      // chain ends: fragment not fully received
 constexpr uint32_t kFUnal = 0xfffffffeu;      // chain meets a size % 4 != 0 (serial fallback)
 constexpr uint32_t kFNone = 0xffffffffu;      // no entry
@@ -238,7 +243,8 @@ struct FrameBase {                            // super-chunk exclusive prefixes
     uint32_t prev_tail, rsv;                  // LAST flag of the fragment before it
 };
 struct FrameWs {                              // device workspace of one walk
-    uint32_t *exitS;                          // [Q] first chain word at or past the super-chunk end
+    uint16_t *exitR;                          // [Q] last chain word inside the super-chunk (super-
+                                              // local): the exit is that word's next mark
     uint32_t *sentry;                         // [nsup] super-chunk entries on the real chain
     uint32_t *gexit;                          // [ngrp][256] group exits of the first super's first words
     uint32_t *gentry;                         // [ngrp] group entries on the real chain
