@@ -128,11 +128,15 @@ __device__ __forceinline__ uint32_t fr_wave_incl(uint32_t v) {
 // so every thread jumps ceil(active / 256) of them per round whatever the
 // layout of the marks.  A next mark in a later sub-chunk of the super-chunk
 // takes that word's result from exitR, which this block already wrote (L2;
-// never read before, so no stale L1 line).  24 KiB of LDS.  (The next sub-chunk's results kept in LDS instead measured slower:
-// 32 KiB, fewer blocks per CU.)
+// never read before, so no stale L1 line).  24 KiB of LDS.  (The next
+// sub-chunk's results kept in LDS instead measured slower: 32 KiB, fewer
+// blocks per CU.)  The compacted list goes out too, for k_fr_mark: per
+// sub-chunk alist[sub][k] = position | next << 12 | LAST << 24 of its active
+// words (complete fragments all), acnt[sub] of them.
 constexpr uint32_t kFRes = 0x10000u;
-__global__ __launch_bounds__(256, 4) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
-                                                      uint16_t *exitR) {
+constexpr uint32_t kFPtr = 0xfffu;     // the local pointer of a J value (bit 12: the word's LAST flag)
+__global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
+                                                      uint16_t *exitR, uint32_t *alist, uint32_t *acnt) {
     __shared__ __attribute__((aligned(16))) uint32_t J[kFChunk];
     __shared__ __attribute__((aligned(16))) uint16_t L[kFChunk];   // active positions (sub-chunk local)
     __shared__ uint32_t wtot[4];
@@ -146,41 +150,55 @@ __global__ __launch_bounds__(256, 4) void k_fr_exits(const uint32_t *__restrict_
         const uint32_t base = sbeg + (uint32_t)j * kFChunk;
         const uint32_t bend = base + kFChunk;
         if (j > 0) fr_cload(w, Q, base - kFChunk, tid, y);   // next sub-chunk's words in flight
-        uint32_t t[16], act = 0;
+        // J: a local pointer with the word's LAST flag (next mark inside), the
+        // next mark's offset past bend when it lies in a later sub-chunk
+        // [bend, send) (looked up below), else the word itself as the last one
+        // (next mark past the super-chunk, or a terminal)
+        const uint32_t lim = send > bend ? send - bend : 0u;
+        const uint32_t own0 = kFRes | (base - sbeg + 4 * tid);
+        uint32_t act = 0, look = 0;
         if (bend <= Q) {
-            const uint32_t q0 = base + 4 * tid, R0 = Q - q0;
+            // a full sub-chunk: d = local position of the next mark.  A size
+            // that is not a multiple of 4 ends the chain (terminal), and a
+            // fragment that does not fit reaches past Q >= send, so neither
+            // needs its own test here.  One band of 4 words at a time (few
+            // live registers: occupancy bounds this kernel)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const uint32_t ci = 1024 * (i >> 2) + (i & 3);
-                t[i] = fr_next_full(fr_bswap(x[i]), q0 + ci, R0 - ci);
+            for (int k = 0; k < 4; ++k) {
+                uint32_t t[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int i = 4 * k + c;
+                    const uint32_t m = fr_bswap(x[i]);
+                    const uint32_t d = ((m >> 2) & 0x1fffffffu) + 4 * tid + 1024 * k + c + 1;
+                    const bool al = (m & 3u) == 0;
+                    const bool in = al && d < kFChunk, lk = al && d - kFChunk < lim;
+                    act |= (in ? 1u : 0u) << i;
+                    look |= (lk ? 1u : 0u) << i;
+                    t[c] = in ? d | (x[i] & 0x80u) << 5 : lk ? d - kFChunk : own0 + 1024 * k + c;
+                }
+                *(u32x4f *)&J[4 * tid + 1024 * k] = u32x4f{t[0], t[1], t[2], t[3]};
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const uint32_t q = base + fr_cw(tid, i);
-                t[i] = q < Q ? fr_next(fr_bswap(x[i]), q, Q, tb) : kFStop;
+            for (int k = 0; k < 4; ++k) {
+                uint32_t t[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int i = 4 * k + c;
+                    const uint32_t q = base + fr_cw(tid, i);
+                    const uint32_t v = q < Q ? fr_next(fr_bswap(x[i]), q, Q, tb) : kFStop;
+                    act |= (v < bend ? 1u : 0u) << i;   // a word inside (terminals are >= kFUnal)
+                    const bool lk = v - bend < lim;
+                    look |= (lk ? 1u : 0u) << i;
+                    t[c] = v < bend ? (v - base) | (x[i] & 0x80u) << 5 : lk ? v - bend : own0 + 1024 * k + c;
+                }
+                *(u32x4f *)&J[4 * tid + 1024 * k] = u32x4f{t[0], t[1], t[2], t[3]};
             }
         }
-        // J: a local pointer (next mark inside), the raw next mark when it lies
-        // in a later sub-chunk [bend, send) (looked up below), else the word
-        // itself as the last one
-        const uint32_t lim = send > bend ? send - bend : 0u;
-        const uint32_t own0 = kFRes | (base - sbeg + 4 * tid);
-        uint32_t look = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t v = t[i];
-            act |= (v < bend ? 1u : 0u) << i;   // a word inside (terminals are >= kFUnal)
-            const bool lk = v - bend < lim;
-            look |= (lk ? 1u : 0u) << i;
-            t[i] = v < bend ? v - base : lk ? v : own0 + 1024 * (i >> 2) + (i & 3);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            *(u32x4f *)&J[4 * tid + 1024 * k] = u32x4f{t[4 * k], t[4 * k + 1], t[4 * k + 2], t[4 * k + 3]};
         for (uint32_t m = look; m; m &= m - 1) {   // own words: no barrier needed
             const uint32_t li = fr_cw(tid, __ffs(m) - 1);
-            J[li] = kFRes | exitR[J[li]];
+            J[li] = kFRes | exitR[bend + J[li]];
         }
         const uint32_t cnt = __popc(act);
         const uint32_t incl = fr_wave_incl(cnt);
@@ -189,9 +207,17 @@ __global__ __launch_bounds__(256, 4) void k_fr_exits(const uint32_t *__restrict_
         const uint32_t t0 = wtot[0], t1 = wtot[1], t2 = wtot[2], t3 = wtot[3];
         const uint32_t A = t0 + t1 + t2 + t3;   // active words of the sub-chunk
         uint32_t pos = incl - cnt + (wv > 0 ? t0 : 0u) + (wv > 1 ? t1 : 0u) + (wv > 2 ? t2 : 0u);
+        const uint64_t sub = (uint64_t)blockIdx.x * (kFSuper / kFChunk) + (uint32_t)j;
         for (uint32_t m = act; m; m &= m - 1) L[pos++] = (uint16_t)fr_cw(tid, __ffs(m) - 1);
+        if (tid == 0) acnt[sub] = A;
         if (A) {
             __syncthreads();   // L
+            // the list out (coalesced), before this thread's own entries jump
+            uint32_t *al = alist + sub * kFChunk;
+            for (uint32_t k = tid; k < A; k += 256) {
+                const uint32_t li = L[k];
+                al[k] = li | (J[li] & 0x1fffu) << 12;
+            }
             // this thread's list entries: tid + 256 c, c < ceil((A - tid) / 256).
             // Asynchronous pointer jumping: a thread jumps its own entries until
             // they hold results, reading whatever the other threads have written
@@ -205,7 +231,7 @@ __global__ __launch_bounds__(256, 4) void k_fr_exits(const uint32_t *__restrict_
                 for (uint32_t m = pend; m; m &= m - 1) {
                     const uint32_t c = __ffs(m) - 1;
                     const uint32_t li = L[tid + 256 * c];
-                    const uint32_t u = J[J[li]];
+                    const uint32_t u = J[J[li] & kFPtr];
                     J[li] = u;
                     if (u >= kFRes) pend &= ~(1u << c);
                 }
@@ -339,20 +365,25 @@ __global__ __launch_bounds__(256) void k_fr_fix_fill(FrExits ex, const uint32_t 
 // k_fr_mark: per sub-chunk bitmaps of the complete chain fragments and their
 // LAST flags, counts and in-super prefixes.
 // ---------------------------------------------------------------------------
-// The chain inside a sub-chunk, from its entry: by pruning (below), or by
-// pointer doubling over sub-chunk-local u16 pointers (kFOut = the pointer
-// leaves the sub-chunk) when pruning has not settled in kFPruneRounds.  The
-// bitmaps are written as 16-bit pieces (16 consecutive words), each
-// assembled from 4 lanes' nibbles.
+// Works on k_fr_exits' list of active words (the words whose next mark stays
+// inside the sub-chunk) instead of the stream: the chain inside a sub-chunk
+// is its entry, list entries, and one last word whose next mark leaves (or
+// ends the chain), read from the stream by one thread.  The chain is found by
+// pruning (below), or by pointer doubling over sub-chunk-local u16 pointers
+// (kFOut = no pointer inside) when pruning has not settled in kFPruneRounds.
+// Marks are LDS bitmaps (bit b of word k = position 32 k + b), written out
+// whole.
 constexpr uint32_t kFOut = 0xffffu;
 constexpr int kFPruneRounds = 4;   // then pointer doubling
-struct FrWaveStat {       // wave v's words: bands [1024 k + 256 v, +256), k < 4
-    uint32_t cnt;         // complete fragments | LAST ones << 16
-    uint32_t lastpos;     // 1 + sub-chunk position of its last LAST fragment (0: none)
-    uint32_t upto;        // its complete fragments before lastpos
+constexpr int kFMaxEnt = kFChunk / 256;   // list entries per thread (at most)
+struct FrWaveStat {       // waves 0 and 1 (bitmap words 64 v .. 64 v + 63)
+    uint32_t nfrag;       // complete fragments
+    uint32_t nlast;       // LAST ones among them
+    uint32_t cand;        // (1 + position of its last LAST fragment) << 16 | its complete fragments through it
     uint32_t tail;        // 1 + (position << 1 | LAST flag) of its last complete fragment (0: none)
-    uint32_t band[2];     // complete fragments per band k (u16 each)
 };
+// bytes b0..b3 of w, each 0 or 1, as bits 0..3
+__device__ __forceinline__ uint32_t fr_bytes01(uint32_t w) { return (w * 0x01020408u) >> 24 & 0xfu; }
 __device__ __forceinline__ uint32_t fr_wave_sum(uint32_t v) {
 #pragma unroll
     for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -363,18 +394,23 @@ __device__ __forceinline__ uint32_t fr_wave_max(uint32_t v) {
     for (int d = 32; d; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
     return v;
 }
-// bytes b0..b3 of w, each 0 or 1, as bits 0..3
-__device__ __forceinline__ uint32_t fr_bytes01(uint32_t w) { return (w * 0x01020408u) >> 24 & 0xfu; }
+__device__ __forceinline__ uint32_t fr_wave_min(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
+    return v;
+}
 
 __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
-                                                     const uint32_t *sentry, const uint64_t *res, FrameSub *sub,
+                                                     const uint32_t *sentry, const uint64_t *res,
+                                                     const uint32_t *alist, const uint32_t *acnt, FrameSub *sub,
                                                      uint32_t *fbits, uint32_t *lbits, FrameSuper *sup) {
     __shared__ __attribute__((aligned(16))) uint16_t J[2][kFChunk];
     __shared__ __attribute__((aligned(16))) uint8_t on[kFChunk + 64];   // + one dummy byte per lane
-    __shared__ __attribute__((aligned(16))) uint8_t pred[kFChunk];
+    __shared__ __attribute__((aligned(16))) uint8_t pred[kFChunk];      // round stamps (never cleared)
+    __shared__ __attribute__((aligned(16))) uint32_t fb[128], lb[128];
     __shared__ __attribute__((aligned(16))) FrAny any;
-    __shared__ FrWaveStat ws[4];
-    __shared__ uint32_t e_next;
+    __shared__ FrWaveStat ws[2];
+    __shared__ uint32_t wmax[4], e_next;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t s = blockIdx.x;
     const uint32_t sbeg = s * kFSuper;
@@ -385,113 +421,125 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
     uint32_t pre_f = 0, pre_l = 0, tail = 2;   // tail: LAST flag of the super's last fragment (2 = none yet)
     uint32_t lastlast = 0, has_ll = 0;         // in-super count up to and including its last LAST fragment
     uint32_t par = 0;
-    uint32_t x[16], y[16];
-    uint32_t held = ~0u;                       // sub-chunk whose words x holds
+    // empty state: J no pointers, on / pred / bitmaps clear
+    typedef uint32_t u32x4m __attribute__((ext_vector_type(4)));
+    const u32x4m z4 = {0u, 0u, 0u, 0u}, o4 = {~0u, ~0u, ~0u, ~0u};
+    *(u32x4m *)&J[0][8 * tid] = o4;
+    *(u32x4m *)&J[0][8 * tid + 2048] = o4;
+    *(u32x4m *)&on[16 * tid] = z4;
+    *(u32x4m *)&pred[16 * tid] = z4;
+    if (tid < 128) fb[tid] = 0; else lb[tid - 128] = 0;
+    __syncthreads();
+    // the next sub-chunk's list count and first two entries, loaded one ahead
+    uint32_t nA = acnt[sub0], n0 = alist[sub0 * kFChunk + tid], n1 = alist[sub0 * kFChunk + 256 + tid];
     for (uint32_t j = 0; j < nsub; ++j) {
         const uint32_t base = sbeg + j * kFChunk;
         const uint32_t bend = base + kFChunk;
+        const uint64_t sj = sub0 + j;
+        const uint32_t A = nA, p0 = n0, p1 = n1;
+        if (j + 1 < nsub) {
+            nA = acnt[sj + 1];
+            n0 = alist[(sj + 1) * kFChunk + tid];
+            n1 = alist[(sj + 1) * kFChunk + 256 + tid];
+        }
         FrameSub info;
         info.pre_frag = pre_f;
         info.pre_last = pre_l;
         info.prev_tail = tail;
         info.nfrag = info.nlast = info.upto_ll = info.has_ll = info.rsv = 0;
-        uint16_t *fb16 = (uint16_t *)fbits + (sub0 + j) * (kFChunk / 16);
-        uint16_t *lb16 = (uint16_t *)lbits + (sub0 + j) * (kFChunk / 16);
-        if (e >= bend || e >= Q) {   // the chain skips this sub-chunk (or has ended)
-            if (tid == 0) sub[sub0 + j] = info;
-            fb16[tid] = 0;
-            lb16[tid] = 0;
+        if (e >= bend || e >= Q) {   // the chain skips this sub-chunk (or has ended); state stays empty
+            if (tid == 0) sub[sj] = info;
+            if (tid < 128) fbits[sj * 128 + tid] = 0; else lbits[sj * 128 + tid - 128] = 0;
             continue;
         }
-        if (held != j) fr_cload(w, Q, base, tid, x);
-        if (j + 1 < nsub) { fr_cload(w, Q, bend, tid, y); held = j + 1; }   // next sub-chunk in flight
-        uint32_t act = 0, cf = 0, lf = 0, lv = 0;   // per word: active / complete fragment / LAST / next leaves
-        uint32_t p[8];                              // local pointers, two u16 per register
-        auto word = [&](int i, uint32_t m, uint32_t v) {
-            cf |= (v < kFUnal ? 1u : 0u) << i;
-            lf |= (m >> 31) << i;
-            lv |= (v >= bend ? 1u : 0u) << i;       // v < bend: a word inside (v > q >= base)
-            const uint32_t pi = v < bend ? v - base : kFOut;
-            if (i & 1) p[i >> 1] |= pi << 16; else p[i >> 1] = pi;
-        };
-        if (bend <= Q) {
-            const uint32_t q0 = base + 4 * tid, R0 = Q - q0;
+        const uint32_t el = e - base;   // the entry, sub-chunk local
+        const uint32_t Cmax = (A + 255) / 256;
+        const uint32_t *al = alist + sj * kFChunk;
+        uint32_t ent[kFMaxEnt], mine = 0;   // entries tid + 256 c: position | next << 12 | LAST << 24
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const uint32_t ci = 1024 * (i >> 2) + (i & 3);
-                const uint32_t m = fr_bswap(x[i]);
-                word(i, m, fr_next_full(m, q0 + ci, R0 - ci));
-            }
-        } else {
+        for (int c = 0; c < kFMaxEnt; ++c) {
+            if ((uint32_t)c >= Cmax) break;
+            const uint32_t k = tid + 256 * c;
+            ent[c] = c == 0 ? p0 : c == 1 ? p1 : k < A ? al[k] : 0u;
+            mine |= (k < A ? 1u : 0u) << c;
+        }
+        // S = the entry and every list target; the largest target (or the
+        // entry) is most likely the chain's last word: its stream word is
+        // loaded ahead of the pruning
+        uint32_t tmax = el;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const uint32_t q = base + fr_cw(tid, i);
-                const uint32_t m = q < Q ? fr_bswap(x[i]) : 0u;
-                word(i, m, q < Q ? fr_next(m, q, Q, tb) : kFStop);
+        for (int c = 0; c < kFMaxEnt; ++c) {
+            if ((uint32_t)c >= Cmax) break;
+            if ((mine >> c) & 1) {
+                const uint32_t pos = ent[c] & 0xfffu, nx = (ent[c] >> 12) & 0xfffu;
+                J[0][pos] = (uint16_t)nx;
+                on[nx] = 1;
+                tmax = max(tmax, nx);
             }
         }
-        act = ~lv & 0xffffu;
-        typedef uint32_t u32x2f __attribute__((ext_vector_type(2)));
-        uint32_t eb = 0;   // the entry among this thread's words
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const uint32_t li = 4 * tid + 1024 * kk;
-            const uint32_t d = e - base - li;
-            eb |= (d < 4 ? 1u << d : 0u) << (4 * kk);
-            *(u32x2f *)&J[0][li] = u32x2f{p[2 * kk], p[2 * kk + 1]};
-            *(uint32_t *)&on[li] = d < 4 ? 1u << (8 * d) : 0u;
-            *(uint32_t *)&pred[li] = 0;
+        tmax = fr_wave_max(tmax);
+        if (lane == 0) wmax[wv] = tmax;
+        if (tid == 0) on[el] = 1;
+        __syncthreads();
+        uint32_t guess = 0, gword = 0;
+        if (tid == 0) {
+            guess = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+            if (base + guess < Q) gword = w[base + guess];
         }
-        __syncthreads();
-        if (tid == 0) e_next = kFStop;   // every thread read the previous value before this barrier
-        // S = the entry and every inside target; then drop the nodes with no
-        // predecessor in S until nothing changes.  Every node left reaches back
-        // to the entry (positions fall along predecessors), every chain node
-        // stays: S is the chain.  Rounds = the longest false chain + 1.
-        for (uint32_t m = act; m; m &= m - 1) on[J[0][fr_cw(tid, __ffs(m) - 1)]] = 1;
-        __syncthreads();
-        uint32_t om = 0;
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) om |= fr_bytes01(*(const uint32_t *)&on[4 * tid + 1024 * kk]) << (4 * kk);
+        // drop the nodes with no predecessor in S until nothing changes; every
+        // node left reaches back to the entry (positions fall along
+        // predecessors), every chain node stays: S is the chain.  Rounds = the
+        // longest false chain + 1.  pred holds round stamps, so it is never
+        // cleared.
         bool settled = false;
         for (int r = 0; r < kFPruneRounds; ++r) {
-            for (uint32_t m = om & act; m; m &= m - 1) pred[J[0][fr_cw(tid, __ffs(m) - 1)]] = 1;
-            __syncthreads();
-            uint32_t pm = 0;
+            const uint8_t stamp = (uint8_t)(1 + j * kFPruneRounds + r);
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const uint32_t li = 4 * tid + 1024 * kk;
-                pm |= fr_bytes01(*(const uint32_t *)&pred[li]) << (4 * kk);
-                *(uint32_t *)&pred[li] = 0;   // pushes of the next round come after the barrier below
+            for (int c = 0; c < kFMaxEnt; ++c) {
+                if ((uint32_t)c >= Cmax) break;
+                if (((mine >> c) & 1) && on[ent[c] & 0xfffu]) pred[(ent[c] >> 12) & 0xfffu] = stamp;
             }
-            const uint32_t nm = om & (pm | eb);
-            const bool ch = nm != om;
-            om = nm;
+            __syncthreads();
+            bool ch = false;
+#pragma unroll
+            for (int c = 0; c < kFMaxEnt; ++c) {
+                if ((uint32_t)c >= Cmax) break;
+                const uint32_t nx = (ent[c] >> 12) & 0xfffu;
+                if (((mine >> c) & 1) && nx != el && on[nx] && pred[nx] != stamp) {
+                    on[nx] = 0;
+                    ch = true;
+                }
+            }
             if (!fr_block_any(ch, any, par)) { settled = true; break; }
         }
         if (!settled) {
             // long false chains (bodies full of small integers): pointer
             // doubling with marking, double-buffered: round r reads J^(2^r) and
             // marks the node 2^r hops past every marked node, so after round r
-            // every chain node < 2^(r+1) hops from the entry is marked.  A word
-            // whose pointer left copies the sentinel into the other buffer once
-            // more before it drops out, so both buffers agree on it.
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const uint32_t li = 4 * tid + 1024 * kk;
-                *(u32x2f *)&J[1][li] = *(const u32x2f *)&J[0][li];
-                const uint32_t d = e - base - li;
-                *(uint32_t *)&on[li] = d < 4 ? 1u << (8 * d) : 0u;
-            }
+            // every chain node < 2^(r+1) hops from the entry is marked.  An
+            // entry whose pointer left copies the sentinel into the other buffer
+            // once more before it drops out, so both buffers agree on it.
+            *(u32x4m *)&J[1][8 * tid] = o4;
+            *(u32x4m *)&J[1][8 * tid + 2048] = o4;
+            *(u32x4m *)&on[16 * tid] = z4;
             __syncthreads();
-            uint32_t cur = 0;
+#pragma unroll
+            for (int c = 0; c < kFMaxEnt; ++c) {
+                if ((uint32_t)c >= Cmax) break;
+                if ((mine >> c) & 1) J[1][ent[c] & 0xfffu] = (uint16_t)((ent[c] >> 12) & 0xfffu);
+            }
+            if (tid == 0) on[el] = 1;
+            __syncthreads();
+            uint32_t cur = 0, live = mine;
             for (;;) {
                 bool mv = false;
                 const uint16_t *Jc = J[cur];
                 uint16_t *Jn = J[cur ^ 1];
-                for (uint32_t m = act; m; m &= m - 1) {
-                    const int i = __ffs(m) - 1;
-                    const uint32_t li = fr_cw(tid, i);
+#pragma unroll
+                for (int c = 0; c < kFMaxEnt; ++c) {
+                    if ((uint32_t)c >= Cmax) break;
+                    if (!((live >> c) & 1)) continue;
+                    const uint32_t li = ent[c] & 0xfffu;
                     const uint32_t v = Jc[li];
                     const bool in = v != kFOut;
                     const uint32_t vv = in ? v : li;
@@ -499,80 +547,84 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
                     on[in && o ? v : kFChunk + lane] = 1;
                     const uint32_t u = Jc[vv];
                     Jn[li] = (uint16_t)(in ? u : kFOut);
-                    act &= in ? ~0u : ~(1u << i);
+                    live &= in ? ~0u : ~(1u << c);
                     mv |= in && u != kFOut;
                 }
                 cur ^= 1;
                 if (!fr_block_any(mv, any, par)) break;
             }
-            om = 0;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) om |= fr_bytes01(*(const uint32_t *)&on[4 * tid + 1024 * kk]) << (4 * kk);
+            // leave J[0] with no pointers for the next sub-chunk (J[1] is
+            // rewritten before use)
+            *(u32x4m *)&J[0][8 * tid] = o4;
+            *(u32x4m *)&J[0][8 * tid + 2048] = o4;
         }
-        // this thread's chain words -> bitmaps, counts, the chain's exit
-        const uint32_t oc = om & cf, ol = oc & lf;
-        {   // bitmap piece (16 words) k = lane & 3 of lane group g = lane >> 2: nibble k of lanes 4g..4g+3
-            const uint32_t g4 = lane & ~3u, kk = lane & 3u;
-            uint32_t pc = 0, pl = 0;
+        // marks of the chain's list words; its last word = the largest chain position
+        uint32_t lmax = el;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                pc |= ((__shfl(oc, g4 + c, 64) >> (4 * kk)) & 0xfu) << (4 * c);
-                pl |= ((__shfl(ol, g4 + c, 64) >> (4 * kk)) & 0xfu) << (4 * c);
-            }
-            const uint32_t pi = 64 * kk + 16 * wv + (lane >> 2);   // words [16 pi, 16 pi + 16)
-            fb16[pi] = (uint16_t)pc;
-            lb16[pi] = (uint16_t)pl;
-        }
-        if (om & lv) {   // the marked node whose next leaves the sub-chunk (terminals too): one thread
-            const uint32_t b = __ffs(om & lv) - 1;
-            uint32_t xm = 0;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) xm = (uint32_t)i == b ? x[i] : xm;   // its word, from registers
-            const uint32_t q = base + fr_cw(tid, b);
-            e_next = q < Q ? fr_next(fr_bswap(xm), q, Q, tb) : kFStop;
-        }
-        const uint32_t cnt = fr_wave_sum(__popc(oc) | __popc(ol) << 16);
-        const uint32_t b01 = fr_wave_sum(__popc(oc & 0xfu) | __popc(oc & 0xf0u) << 16);
-        const uint32_t b23 = fr_wave_sum(__popc(oc & 0xf00u) | __popc(oc & 0xf000u) << 16);
-        const uint32_t lastpos = fr_wave_max(ol ? fr_cw(tid, 31 - __clz(ol)) + 1 : 0u);
-        uint32_t below = 0;   // words of this thread before lastpos
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const uint32_t p0 = 4 * tid + 1024 * kk;
-            const uint32_t nb = lastpos > p0 ? min(lastpos - p0, 4u) : 0u;
-            below |= ((1u << nb) - 1u) << (4 * kk);
-        }
-        const uint32_t upto = fr_wave_sum(__popc(oc & below));
-        const uint32_t hb = 31 - __clz(oc);
-        const uint32_t tl_w = fr_wave_max(oc ? 1 + (fr_cw(tid, hb) << 1 | ((ol >> hb) & 1u)) : 0u);
-        if (lane == 0) ws[wv] = FrWaveStat{cnt, lastpos, upto, tl_w, {b01, b23}};
-        __syncthreads();
-        // combine in position order: the last LAST fragment lies in band k* of
-        // wave v* (the wave with the largest lastpos); the other waves' complete
-        // fragments before it are their bands k < k*, plus band k* if v < v*
-        uint32_t tnf = 0, tnl = 0, tlp = 0, lp = 0, vs = 0;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const FrWaveStat st = ws[v];
-            tnf += st.cnt & 0xffffu;
-            tnl += st.cnt >> 16;
-            tlp = max(tlp, st.tail);
-            if (st.lastpos > lp) { lp = st.lastpos; vs = v; }
-        }
-        uint32_t up = 0;
-        if (lp) {
-            const uint32_t ks = (lp - 1) >> 10;
-            up = ws[vs].upto;
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                if ((uint32_t)v == vs) continue;
-                const uint32_t b[4] = {ws[v].band[0] & 0xffffu, ws[v].band[0] >> 16, ws[v].band[1] & 0xffffu,
-                                       ws[v].band[1] >> 16};
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if ((uint32_t)k < ks || ((uint32_t)k == ks && (uint32_t)v < vs)) up += b[k];
+        for (int c = 0; c < kFMaxEnt; ++c) {
+            if ((uint32_t)c >= Cmax) break;
+            const uint32_t pos = ent[c] & 0xfffu;
+            if (((mine >> c) & 1) && on[pos]) {
+                atomicOr(&fb[pos >> 5], 1u << (pos & 31));
+                if ((ent[c] >> 24) & 1) atomicOr(&lb[pos >> 5], 1u << (pos & 31));
+                lmax = max(lmax, (ent[c] >> 12) & 0xfffu);
             }
         }
+        lmax = fr_wave_max(lmax);
+        if (lane == 0) wmax[wv] = lmax;   // (thread 0 read the previous values before the pruning's barriers)
+        __syncthreads();   // marks, wmax; on / J free again
+        const uint32_t last = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        // back to the empty state for the next sub-chunk (the list entries only)
+#pragma unroll
+        for (int c = 0; c < kFMaxEnt; ++c) {
+            if ((uint32_t)c >= Cmax) break;
+            if ((mine >> c) & 1) {
+                J[0][ent[c] & 0xfffu] = (uint16_t)kFOut;
+                on[(ent[c] >> 12) & 0xfffu] = 0;
+            }
+        }
+        if (tid == 0) {   // the last word: its next mark is the next sub-chunk's entry
+            const uint32_t q = base + last;
+            uint32_t v = kFStop;
+            if (q < Q) {
+                const uint32_t m = fr_bswap(last == guess ? gword : w[q]);
+                v = fr_next(m, q, Q, tb);
+                if (v < kFUnal) {
+                    atomicOr(&fb[last >> 5], 1u << (last & 31));
+                    if (m >> 31) atomicOr(&lb[last >> 5], 1u << (last & 31));
+                }
+            }
+            on[el] = 0;
+            e_next = v;
+        }
+        __syncthreads();   // bitmaps final, e_next
+        const uint32_t fw = tid < 128 ? fb[tid] : 0u, lw = tid < 128 ? lb[tid] : 0u;
+        if (tid < 128) fbits[sj * 128 + tid] = fw; else lbits[sj * 128 + tid - 128] = lb[tid - 128];
+        if (wv < 2) {   // bitmap word tid: counts, the last LAST fragment, the last fragment
+            const uint32_t pc = __popc(fw);
+            const uint32_t incl = fr_wave_incl(pc);
+            uint32_t cand = 0, tl = 0;
+            if (lw) {
+                const uint32_t hb = 31 - __clz(lw);
+                cand = (32 * tid + hb + 1) << 16 | (incl - pc + __popc(fw & ((2u << hb) - 1u)));
+            }
+            if (fw) {
+                const uint32_t hb = 31 - __clz(fw);
+                tl = 1 + ((32 * tid + hb) << 1 | ((lw >> hb) & 1u));
+            }
+            cand = fr_wave_max(cand);
+            tl = fr_wave_max(tl);
+            const uint32_t nl = fr_wave_sum(__popc(lw));
+            if (lane == 63) ws[wv] = FrWaveStat{incl, nl, cand, tl};
+        }
+        __syncthreads();   // ws; bitmaps read
+        if (tid < 128) fb[tid] = 0; else lb[tid - 128] = 0;
+        const FrWaveStat w0 = ws[0], w1 = ws[1];
+        const uint32_t tnf = w0.nfrag + w1.nfrag, tnl = w0.nlast + w1.nlast;
+        uint32_t lp = 0, up = 0;
+        if (w1.cand) { lp = w1.cand >> 16; up = (w1.cand & 0xffffu) + w0.nfrag; }
+        else if (w0.cand) { lp = w0.cand >> 16; up = w0.cand & 0xffffu; }
+        const uint32_t tlp = max(w0.tail, w1.tail);
         const uint32_t tl = tlp ? (tlp - 1) & 1u : tail;
         info.nfrag = tnf;
         info.nlast = tnl;
@@ -582,13 +634,11 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
             has_ll = 1;
             lastlast = pre_f + up;
         }
-        if (tid == 0) sub[sub0 + j] = info;
+        if (tid == 0) sub[sj] = info;
         e = e_next;
         tail = tl;
         pre_f += tnf;
         pre_l += tnl;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) x[i] = y[i];
     }
     if (tid == 0) {
         FrameSuper v;
@@ -610,52 +660,60 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64_t nsup, FrameBase *bases,
                                                     uint64_t *res) {
+    // thread t takes the run of super-chunks [t R, t R + R): its sums and
+    // "last non-empty tail" in registers, one block scan of the runs, then the
+    // run again with the carried prefix
     __shared__ uint64_t sf[1024], sl[1024];
     __shared__ uint32_t st[1024];
-    __shared__ uint64_t carry_f, carry_l, fc;
-    __shared__ uint32_t carry_t;
+    __shared__ uint64_t fc;
     const uint32_t tid = threadIdx.x;
-    if (tid == 0) { carry_f = 0; carry_l = 0; carry_t = 1; fc = 0; }   // fragment 0 starts a message
+    if (tid == 0) fc = 0;
+    if (res[0] == kFUnal) return;   // block-uniform
+    const uint64_t R = (nsup + 1023) / 1024;
+    const uint64_t s0 = tid * R, s1 = min(s0 + R, nsup);
+    uint64_t f = 0, l = 0;
+    uint32_t t = 2u;
+    for (uint64_t s = s0; s < s1; ++s) {
+        const FrameSuper v = sup[s];
+        f += v.nfrag;
+        l += v.nlast;
+        if (v.nfrag) t = v.tail;
+    }
+    sf[tid] = f;
+    sl[tid] = l;
+    st[tid] = t;
     __syncthreads();
-    if (res[0] == kFUnal) return;
-    for (uint64_t b = 0; b < nsup; b += 1024) {
-        const uint64_t s = b + tid;
-        FrameSuper v{};
-        if (s < nsup) v = sup[s];
-        sf[tid] = v.nfrag;
-        sl[tid] = v.nlast;
-        st[tid] = v.nfrag ? v.tail : 2u;
+    for (uint32_t d = 1; d < 1024; d <<= 1) {   // inclusive scans: sums, "last non-empty tail"
+        const uint64_t af = tid >= d ? sf[tid - d] : 0, al = tid >= d ? sl[tid - d] : 0;
+        const uint32_t at = tid >= d ? st[tid - d] : 2u;
         __syncthreads();
-        // inclusive Hillis-Steele scans (sums; "last non-empty tail")
-        for (uint32_t d = 1; d < 1024; d <<= 1) {
-            const uint64_t af = tid >= d ? sf[tid - d] : 0, al = tid >= d ? sl[tid - d] : 0;
-            const uint32_t at = tid >= d ? st[tid - d] : 2u;
-            __syncthreads();
-            sf[tid] += af;
-            sl[tid] += al;
-            if (st[tid] == 2u) st[tid] = at;
-            __syncthreads();
-        }
-        if (s < nsup) {
-            FrameBase o;
-            o.frag = carry_f + sf[tid] - v.nfrag;
-            o.last = carry_l + sl[tid] - v.nlast;
-            const uint32_t prev = tid ? st[tid - 1] : 2u;
-            o.prev_tail = prev != 2u ? prev : carry_t;
-            bases[s] = o;
-            if (v.has_ll) atomicMax((unsigned long long *)&fc, (unsigned long long)(o.frag + v.upto_ll));
-        }
-        __syncthreads();
-        if (tid == 0) {
-            carry_f += sf[1023];
-            carry_l += sl[1023];
-            if (st[1023] != 2u) carry_t = st[1023];
-        }
+        sf[tid] += af;
+        sl[tid] += al;
+        if (st[tid] == 2u) st[tid] = at;
         __syncthreads();
     }
+    uint64_t cf = sf[tid] - f, cl = sl[tid] - l;
+    uint32_t ct = tid ? st[tid - 1] : 2u;
+    if (ct == 2u) ct = 1u;   // fragment 0 starts a message
+    uint64_t best = 0;
+    for (uint64_t s = s0; s < s1; ++s) {
+        const FrameSuper v = sup[s];
+        FrameBase o;
+        o.frag = cf;
+        o.last = cl;
+        o.prev_tail = ct;
+        o.rsv = 0;
+        bases[s] = o;
+        if (v.has_ll) best = max(best, (uint64_t)(cf + v.upto_ll));
+        cf += v.nfrag;
+        cl += v.nlast;
+        if (v.nfrag) ct = v.tail;
+    }
+    if (best) atomicMax((unsigned long long *)&fc, (unsigned long long)best);
+    __syncthreads();
     if (tid == 0) {
-        res[1] = fc;          // complete fragments: through the last LAST fragment
-        res[4] = carry_l;     // complete messages
+        res[1] = fc;            // complete fragments: through the last LAST fragment
+        res[4] = sl[1023];      // complete messages
         res[5] = fc;
         res[3] = 0;
     }
@@ -802,7 +860,7 @@ int frame_parallel(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t 
     const uint32_t *w = (const uint32_t *)in;
     const uint32_t Q = (uint32_t)(len / 4), tb = (uint32_t)(len & 3);
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
-    hipLaunchKernelGGL(k_fr_exits, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitR);
+    hipLaunchKernelGGL(k_fr_exits, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitR, ws.alist, ws.acnt);
     const uint64_t ngrp = (nsup + kFixGrp - 1) / kFixGrp;
     if (hipMemsetAsync(ws.sentry, 0xff, nsup * 4, st) != hipSuccess) return (int)hipErrorUnknown;
     if (hipMemsetAsync(ws.gentry, 0xff, ngrp * 4, st) != hipSuccess) return (int)hipErrorUnknown;
@@ -811,8 +869,8 @@ int frame_parallel(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t 
     hipLaunchKernelGGL(k_fr_fix_top, dim3(1), dim3(64), 0, st, ex, ws.gexit, ws.gentry, ws.res);
     hipLaunchKernelGGL(k_fr_fix_fill, dim3((uint32_t)ngrp), dim3(256), 0, st, ex, ws.gentry, (uint32_t)nsup,
                        ws.sentry);
-    hipLaunchKernelGGL(k_fr_mark, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.sub,
-                       ws.fbits, ws.lbits, ws.sup);
+    hipLaunchKernelGGL(k_fr_mark, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.alist,
+                       ws.acnt, ws.sub, ws.fbits, ws.lbits, ws.sup);
     hipLaunchKernelGGL(k_fr_bases, dim3(1), dim3(1024), 0, st, ws.sup, nsup, ws.bases, ws.res);
     hipLaunchKernelGGL(k_fr_emit, dim3((uint32_t)nsub), dim3(128), 0, st, w, Q, ws.sub, ws.bases, ws.fbits,
                        ws.lbits, cap, stream_offsets ? 1 : 0, msg_offsets, frag_list ? ws.frag_pos : nullptr, ws.res);

@@ -1496,7 +1496,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     const uint64_t F = Q + 2;
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_ex = take(2 * Q), o_se = take(4 * nsup), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
+    const size_t o_ex = take(2 * Q), o_al = take(4 * (size_t)kFChunk * nsub), o_ac = take(4 * nsub), o_se = take(4 * nsup), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
                  o_fb = take(512 * nsub), o_lb = take(512 * nsub), o_su = take(sizeof(FrameSuper) * nsup),
                  o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_re = take(64);
     if (off > c->fws_bytes) {
@@ -1511,6 +1511,8 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     }
     uint8_t *b = (uint8_t *)c->d_fws;
     ws.exitR = (uint16_t *)(b + o_ex);
+    ws.alist = (uint32_t *)(b + o_al);
+    ws.acnt = (uint32_t *)(b + o_ac);
     ws.sentry = (uint32_t *)(b + o_se);
     ws.gexit = (uint32_t *)(b + o_ge);
     ws.gentry = (uint32_t *)(b + o_gn);

@@ -245,6 +245,8 @@ struct FrameBase {                            // super-chunk exclusive prefixes
 struct FrameWs {                              // device workspace of one walk
     uint16_t *exitR;                          // [Q] last chain word inside the super-chunk (super-
                                               // local): the exit is that word's next mark
+    uint32_t *alist, *acnt;                   // [nsub][kFChunk], [nsub]: active words of each sub-chunk
+                                              // (position | next << 12 | LAST << 24), their count
     uint32_t *sentry;                         // [nsup] super-chunk entries on the real chain
     uint32_t *gexit;                          // [ngrp][256] group exits of the first super's first words
     uint32_t *gentry;                         // [ngrp] group entries on the real chain
