@@ -286,15 +286,21 @@ struct FrExits {   // what fr_exit reads
     uint32_t Q, tb;
     __device__ __forceinline__ uint32_t operator()(uint32_t q) const { return fr_exit(w, exitR, Q, tb, q); }
 };
-__device__ __forceinline__ void fix_stage(const FrExits &ex, uint32_t nsup, uint32_t g, uint32_t *win) {
-    for (uint32_t k = threadIdx.x / 64; k < kFixGrp; k += blockDim.x / 64) {   // a wave per super-chunk
-        const uint32_t s = g * kFixGrp + k;
-#pragma unroll
-        for (uint32_t c = 0; c < kFixWin / 64; ++c) {
-            const uint64_t q = (uint64_t)s * kFSuper + 64 * c + (threadIdx.x & 63);
-            win[k * kFixWin + 64 * c + (threadIdx.x & 63)] = (s < nsup && q < ex.Q) ? ex((uint32_t)q) : kFStop;
-        }
-    }
+// k_fr_win: the window table, wtab[s][d] = exit of word d < kFixWin of
+// super-chunk s (kFStop past Q), every entry in parallel.
+__global__ __launch_bounds__(256) void k_fr_win(FrExits ex, uint32_t nsup, uint32_t *wtab) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (uint64_t)nsup * kFixWin) return;
+    const uint64_t q = (i / kFixWin) * kFSuper + i % kFixWin;
+    wtab[i] = q < ex.Q ? ex((uint32_t)q) : kFStop;
+}
+// Group g's windows from the table (kFStop past the last super-chunk).
+__device__ __forceinline__ void fix_stage(const uint32_t *wtab, uint32_t nsup, uint32_t g, uint32_t *win) {
+    typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
+    const uint64_t n = (uint64_t)min(kFixGrp, nsup - g * kFixGrp) * kFixWin;
+    const u32x4w *src = (const u32x4w *)(wtab + (uint64_t)g * kFixGrp * kFixWin);
+    for (uint32_t k = threadIdx.x; k < kFixGrp * kFixWin / 4; k += blockDim.x)
+        ((u32x4w *)win)[k] = 4 * (uint64_t)k < n ? src[k] : u32x4w{kFStop, kFStop, kFStop, kFStop};
     __syncthreads();
 }
 // One hop from chain word e inside group g: the exit of e's super-chunk.
@@ -303,39 +309,78 @@ __device__ __forceinline__ uint32_t fix_hop(const FrExits &ex, const uint32_t *w
     return d < kFixWin ? win[(s - g * kFixGrp) * kFixWin + d] : ex(e);
 }
 
-__global__ __launch_bounds__(256) void k_fr_fix_grp(FrExits ex, uint32_t nsup, uint32_t *gexit) {
-    __shared__ uint32_t win[kFixGrp * kFixWin];
-    const uint32_t g = blockIdx.x;
+// k_fr_fix_grp: per group, a backward sweep over its super-chunks gives, for
+// every window entry (k, d < kFixWin), the first chain word that is past the
+// group, a terminal, or a deep word (depth >= kFixWin) inside the group where
+// a walk must go on through fr_exit: gsx[g][k][d] (k_fr_fix_top uses it for
+// deep group entries).  Then the group exits of the first super-chunk's
+// window, gexit[g][d], resolved through the deep words.  128 KiB of LDS.
+__global__ __launch_bounds__(256) void k_fr_fix_grp(FrExits ex, const uint32_t *wtab, uint32_t nsup,
+                                                    uint32_t *gsx, uint32_t *gexit) {
+    __shared__ __attribute__((aligned(16))) uint32_t win[kFixGrp * kFixWin];
+    __shared__ __attribute__((aligned(16))) uint32_t sg[kFixGrp * kFixWin];
+    const uint32_t g = blockIdx.x, d = threadIdx.x;
     const uint32_t Q = ex.Q;
-    fix_stage(ex, nsup, g, win);
-    const uint64_t gend64 = (uint64_t)(g + 1) * kFixGrp * kFSuper;
+    fix_stage(wtab, nsup, g, win);
+    const uint32_t gbeg = g * kFixGrp * kFSuper;
+    const uint64_t gend64 = (uint64_t)gbeg + (uint64_t)kFixGrp * kFSuper;
     const uint32_t gend = gend64 < Q ? (uint32_t)gend64 : Q;
-    uint32_t e = g * kFixGrp * kFSuper + threadIdx.x;   // this lane's entry word
+    const uint32_t nk = min(kFixGrp, nsup - g * kFixGrp);
+    for (int k = (int)nk - 1; k >= 0; --k) {
+        uint32_t x = win[k * kFixWin + d];
+        if (x < gend) {   // inside the group, in a later super-chunk
+            const uint32_t k2 = (x - gbeg) >> (kFChunkLog2 + kFSuperLog2), d2 = (x - gbeg) & (kFSuper - 1);
+            if (d2 < kFixWin) x = sg[k2 * kFixWin + d2];
+        }
+        sg[k * kFixWin + d] = x;
+        __syncthreads();
+    }
+    uint32_t *out = gsx + (uint64_t)g * kFixGrp * kFixWin;
+    for (uint32_t k = 0; k < nk; ++k) out[k * kFixWin + d] = sg[k * kFixWin + d];
+    uint32_t e = gbeg + d;   // this lane's entry word
     if (e < gend) {
-        while (e < gend) {
-            e = fix_hop(ex, win, g, e);
-            if (e >= kFUnal) break;
+        e = sg[d];
+        while (e < gend) {   // a deep word: one super-chunk through fr_exit, then the table again
+            e = ex(e);
+            if (e >= gend) break;
+            const uint32_t k2 = (e - gbeg) >> (kFChunkLog2 + kFSuperLog2), d2 = (e - gbeg) & (kFSuper - 1);
+            if (d2 < kFixWin) e = sg[k2 * kFixWin + d2];
         }
     } else {
         e = kFStop;
     }
-    gexit[(uint64_t)g * kFixWin + threadIdx.x] = e;
+    gexit[(uint64_t)g * kFixWin + d] = e;
 }
 
-__global__ __launch_bounds__(64) void k_fr_fix_top(FrExits ex, const uint32_t *gexit, uint32_t *gentry,
-                                                   uint64_t *res) {
+// The group exits go through LDS when they fit (a stream up to kFTopLds
+// groups, 2.5 GiB): the hop chain then costs LDS latency per group.
+constexpr uint32_t kFTopLds = 160;
+__global__ __launch_bounds__(1024) void k_fr_fix_top(FrExits ex, const uint32_t *gsx, const uint32_t *gexit,
+                                                     uint32_t ngrp, uint32_t *gentry, uint64_t *res) {
+    __shared__ __attribute__((aligned(16))) uint32_t gl[kFTopLds * kFixWin];
     const uint32_t Q = ex.Q;
+    const bool lds = ngrp <= kFTopLds;
+    if (lds) {
+        typedef uint32_t u32x4w __attribute__((ext_vector_type(4)));
+        for (uint32_t k = threadIdx.x; k < ngrp * kFixWin / 4; k += blockDim.x)
+            ((u32x4w *)gl)[k] = ((const u32x4w *)gexit)[k];
+        __syncthreads();
+    }
+    if (threadIdx.x >= 64) return;
     uint32_t e = 0;
     while (e < Q) {
         const uint32_t g = e / (kFixGrp * kFSuper), d = e - g * kFixGrp * kFSuper;
         gentry[g] = e;   // one address for the whole wave
         if (d < kFixWin) {
-            e = gexit[(uint64_t)g * kFixWin + d];
-        } else {         // a deep group entry: walk its super-chunks through fr_exit
-            const uint64_t gend = (uint64_t)(g + 1) * kFixGrp * kFSuper;
+            e = lds ? gl[g * kFixWin + d] : gexit[(uint64_t)g * kFixWin + d];
+        } else {         // a deep group entry: fr_exit to the next super-chunk, then the sweep's table
+            const uint32_t gbeg = g * kFixGrp * kFSuper;
+            const uint64_t gend = (uint64_t)gbeg + (uint64_t)kFixGrp * kFSuper;
             while (e < Q && e < gend) {
                 e = ex(e);
-                if (e >= kFUnal) break;
+                if (e >= kFUnal || e >= Q || e >= gend) break;
+                const uint32_t k2 = (e - gbeg) >> (kFChunkLog2 + kFSuperLog2), d2 = (e - gbeg) & (kFSuper - 1);
+                if (d2 < kFixWin) e = gsx[((uint64_t)g * kFixGrp + k2) * kFixWin + d2];
             }
         }
         if (e >= kFUnal) break;
@@ -343,14 +388,14 @@ __global__ __launch_bounds__(64) void k_fr_fix_top(FrExits ex, const uint32_t *g
     if (threadIdx.x == 0) res[0] = e;   // >= Q: ran to the end; kFStop / kFUnal: terminal met on the real chain
 }
 
-__global__ __launch_bounds__(256) void k_fr_fix_fill(FrExits ex, const uint32_t *gentry, uint32_t nsup,
-                                                     uint32_t *sentry) {
-    __shared__ uint32_t win[kFixGrp * kFixWin];
+__global__ __launch_bounds__(256) void k_fr_fix_fill(FrExits ex, const uint32_t *wtab, const uint32_t *gentry,
+                                                     uint32_t nsup, uint32_t *sentry) {
+    __shared__ __attribute__((aligned(16))) uint32_t win[kFixGrp * kFixWin];
     const uint32_t g = blockIdx.x;
     const uint32_t Q = ex.Q;
     uint32_t e = gentry[g];
     if (e == kFNone) return;   // the chain skips this group (block-uniform)
-    fix_stage(ex, nsup, g, win);
+    fix_stage(wtab, nsup, g, win);
     if (threadIdx.x) return;
     const uint64_t gend64 = (uint64_t)(g + 1) * kFixGrp * kFSuper;
     const uint32_t gend = gend64 < Q ? (uint32_t)gend64 : Q;
@@ -865,9 +910,13 @@ int frame_parallel(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t 
     if (hipMemsetAsync(ws.sentry, 0xff, nsup * 4, st) != hipSuccess) return (int)hipErrorUnknown;
     if (hipMemsetAsync(ws.gentry, 0xff, ngrp * 4, st) != hipSuccess) return (int)hipErrorUnknown;
     const FrExits ex{w, ws.exitR, Q, tb};
-    hipLaunchKernelGGL(k_fr_fix_grp, dim3((uint32_t)ngrp), dim3(kFixWin), 0, st, ex, (uint32_t)nsup, ws.gexit);
-    hipLaunchKernelGGL(k_fr_fix_top, dim3(1), dim3(64), 0, st, ex, ws.gexit, ws.gentry, ws.res);
-    hipLaunchKernelGGL(k_fr_fix_fill, dim3((uint32_t)ngrp), dim3(256), 0, st, ex, ws.gentry, (uint32_t)nsup,
+    hipLaunchKernelGGL(k_fr_win, dim3((uint32_t)((nsup * kFixWin + 255) / 256)), dim3(256), 0, st, ex, (uint32_t)nsup,
+                       ws.wtab);
+    hipLaunchKernelGGL(k_fr_fix_grp, dim3((uint32_t)ngrp), dim3(kFixWin), 0, st, ex, ws.wtab, (uint32_t)nsup, ws.gsx,
+                       ws.gexit);
+    hipLaunchKernelGGL(k_fr_fix_top, dim3(1), dim3(1024), 0, st, ex, ws.gsx, ws.gexit, (uint32_t)ngrp, ws.gentry,
+                       ws.res);
+    hipLaunchKernelGGL(k_fr_fix_fill, dim3((uint32_t)ngrp), dim3(256), 0, st, ex, ws.wtab, ws.gentry, (uint32_t)nsup,
                        ws.sentry);
     hipLaunchKernelGGL(k_fr_mark, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.alist,
                        ws.acnt, ws.sub, ws.fbits, ws.lbits, ws.sup);

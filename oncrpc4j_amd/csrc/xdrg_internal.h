@@ -248,6 +248,8 @@ struct FrameWs {                              // device workspace of one walk
     uint32_t *alist, *acnt;                   // [nsub][kFChunk], [nsub]: active words of each sub-chunk
                                               // (position | next << 12 | LAST << 24), their count
     uint32_t *sentry;                         // [nsup] super-chunk entries on the real chain
+    uint32_t *wtab;                           // [nsup][256] super-chunk exits of each one's first words
+    uint32_t *gsx;                            // [nsup][256] walk from each window entry to the group end
     uint32_t *gexit;                          // [ngrp][256] group exits of the first super's first words
     uint32_t *gentry;                         // [ngrp] group entries on the real chain
     FrameSub *sub;                            // [nsub]
