@@ -449,9 +449,11 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
                                                      const uint32_t *sentry, const uint64_t *res,
                                                      const uint32_t *alist, const uint32_t *acnt, FrameSub *sub,
                                                      uint32_t *fbits, uint32_t *lbits, FrameSuper *sup) {
+    // J[1] (pointer doubling) and pred (pruning) are never live together: one
+    // buffer; a doubling pass clears it afterwards, as pred's stamps expect
     __shared__ __attribute__((aligned(16))) uint16_t J[2][kFChunk];
     __shared__ __attribute__((aligned(16))) uint8_t on[kFChunk + 64];   // + one dummy byte per lane
-    __shared__ __attribute__((aligned(16))) uint8_t pred[kFChunk];      // round stamps (never cleared)
+    uint8_t *const pred = (uint8_t *)J[1];                              // round stamps (else never cleared)
     __shared__ __attribute__((aligned(16))) uint32_t fb[128], lb[128];
     __shared__ __attribute__((aligned(16))) FrAny any;
     __shared__ FrWaveStat ws[2];
@@ -472,7 +474,8 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
     *(u32x4m *)&J[0][8 * tid] = o4;
     *(u32x4m *)&J[0][8 * tid + 2048] = o4;
     *(u32x4m *)&on[16 * tid] = z4;
-    *(u32x4m *)&pred[16 * tid] = z4;
+    *(u32x4m *)&J[1][8 * tid] = z4;
+    *(u32x4m *)&J[1][8 * tid + 2048] = z4;
     if (tid < 128) fb[tid] = 0; else lb[tid - 128] = 0;
     __syncthreads();
     // the next sub-chunk's list count and first two entries, loaded one ahead
@@ -598,10 +601,12 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
                 cur ^= 1;
                 if (!fr_block_any(mv, any, par)) break;
             }
-            // leave J[0] with no pointers for the next sub-chunk (J[1] is
-            // rewritten before use)
+            // leave J[0] with no pointers for the next sub-chunk, J[1] clear
+            // for pred's stamps
             *(u32x4m *)&J[0][8 * tid] = o4;
             *(u32x4m *)&J[0][8 * tid + 2048] = o4;
+            *(u32x4m *)&J[1][8 * tid] = z4;
+            *(u32x4m *)&J[1][8 * tid + 2048] = z4;
         }
         // marks of the chain's list words; its last word = the largest chain position
         uint32_t lmax = el;
@@ -776,7 +781,8 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
                                                   const FrameBase *bases, const uint32_t *fbits,
                                                   const uint32_t *lbits, uint64_t cap, int stream_offsets,
                                                   uint64_t *msg_offsets, uint64_t *frag_pos, uint64_t *res) {
-    __shared__ uint32_t wsum[2][2], wtail[2];
+    __shared__ uint32_t wsum[2][2], wtail[2], wlo[2], whi[2];
+    __shared__ uint16_t so[kFChunk + 1];           // staged message offsets
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t k = blockIdx.x;                 // sub-chunk
     const uint64_t s = k / (kFSuper / kFChunk);
@@ -808,16 +814,24 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
     uint64_t m = lb0 + pl_incl - __popc(lw);
     uint32_t prev_last = lt_excl ? (lt_excl - 1) & 1u : in_tail;
     const uint64_t base = k * kFChunk;
+    // message starts (m in [lb0, lb0 + LAST flags]) go through LDS as 16-bit
+    // offsets from the sub-chunk, then out coalesced
+    const uint64_t mlim = min(M, cap + 1);   // msg_offsets[m] is written for m < mlim
+    uint32_t klo = ~0u, khi = 0;
     for (uint32_t bits = fw; bits; bits &= bits - 1) {
         if (f >= F) break;
         const uint32_t bt = __ffs(bits) - 1;
-        const uint64_t p = 4 * (base + 32 * tid + bt);
+        const uint32_t lp = 32 * tid + bt;
+        const uint64_t p = 4 * (base + lp);
         const bool last = (lw >> bt) & 1;
         const bool first = f == 0 || prev_last;
-        if (first && m <= cap) {
-            if (m < M) msg_offsets[m] = stream_offsets ? p : p - 4 * f;   // payload: fragments tile the stream
-            if (m == cap) { res[3] = p; res[5] = f; }   // handleRead's split point (:57-60)
+        if (first && m < mlim) {   // payload offsets: fragments tile the stream (p - 4 f)
+            const uint32_t kk = (uint32_t)(m - lb0);
+            so[kk] = (uint16_t)(stream_offsets ? 4 * lp : 4 * (lp - (uint32_t)(f - fb0)));
+            klo = min(klo, kk);
+            khi = max(khi, kk + 1);
         }
+        if (first && m == cap) { res[3] = p; res[5] = f; }   // handleRead's split point (:57-60)
         if (frag_pos && m <= cap) frag_pos[f] = p;
         if (f + 1 == F) {   // the last LAST fragment closes the last complete message
             const uint64_t size = fr_bswap(w[p >> 2]) & kSizeMask;
@@ -831,6 +845,14 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
         m += last;
         ++f;
     }
+    klo = fr_wave_min(klo);
+    khi = fr_wave_max(khi);
+    if (lane == 0) { wlo[wv] = klo; whi[wv] = khi; }
+    __syncthreads();
+    klo = min(wlo[0], wlo[1]);
+    khi = max(whi[0], whi[1]);
+    const uint64_t vbase = stream_offsets ? 4 * base : 4 * (base - fb0);
+    for (uint32_t kk = klo + tid; kk < khi; kk += 128) msg_offsets[lb0 + kk] = vbase + so[kk];
 }
 
 // ---------------------------------------------------------------------------
