@@ -47,16 +47,46 @@ namespace xdrg {
 
 __device__ __forceinline__ uint32_t fr_bswap(uint32_t x) { return __builtin_bswap32(x); }
 
-// Next chain word after the mark m at word q < Q, or a terminal: kFStop
-// (fragment not fully received: size > remaining - 4, RpcMessageParserTCP.java
-// :77-79), kFUnal (size % 4 != 0).  The stream is 4Q + tb bytes (tb < 4).
+// Positions: the walk runs in word mode (B = 4: position q = stream word q,
+// Q = len / 4 words, tb = len % 4 trailing bytes) and, when the real chain
+// meets a fragment size that is not a multiple of 4, again in byte mode (B =
+// 1: position p = stream byte p, Q = len - 3 = the positions a whole mark can
+// start at, marks read unaligned; streams < 2 GiB).  A chain value >= Q ends
+// the walk in both.
+//
+// Next chain position after the mark m at position q < Q, or a terminal:
+// kFStop (fragment not fully received: size > remaining - 4,
+// RpcMessageParserTCP.java:77-79), kFUnal (word mode: size % 4 != 0).
+template <int B>
 __device__ __forceinline__ uint32_t fr_next(uint32_t m, uint32_t q, uint32_t Q, uint32_t tb) {
     const uint32_t size = m & kSizeMask;
+    if (B == 1) return size + 1 <= Q - q ? q + 4 + size : kFStop;   // Q + 3 - q bytes left
     const uint32_t R = Q - q;   // whole words left, >= 1
     const bool fits = R >= (1u << 30) || size + 4 <= 4 * R + tb;
     if (!fits) return kFStop;
     if (size & 3) return kFUnal;
     return q + 1 + (size >> 2);
+}
+
+// The raw (memory-order) mark word at position p < Q.  Byte mode: bytes p ..
+// p + 3 from the two words around them (the second one byte by byte where it
+// passes the stream's end, len = Q + 3).
+template <int B>
+__device__ __forceinline__ uint32_t fr_at(const uint32_t *w, uint32_t Q, uint32_t p) {
+    if (B == 4) return w[p];
+    const uint32_t i = p >> 2, s = p & 3;
+    const uint32_t a = w[i];
+    if (s == 0) return a;
+    const uint64_t len = (uint64_t)Q + 3;
+    uint32_t b = 0;
+    if (4 * (uint64_t)i + 8 <= len) {
+        b = w[i + 1];
+    } else {
+        const uint8_t *c = (const uint8_t *)w;
+        for (uint32_t j = 0; j < 4; ++j)
+            if (4 * (uint64_t)i + 4 + j < len) b |= (uint32_t)c[4 * (uint64_t)i + 4 + j] << (8 * j);
+    }
+    return __builtin_amdgcn_alignbyte(b, a, s);
 }
 
 // Word layout of a sub-chunk (kFChunk = 4096 words, 256 threads): thread t
@@ -66,16 +96,33 @@ __device__ __forceinline__ uint32_t fr_next(uint32_t m, uint32_t q, uint32_t Q, 
 // per thread measured slower: 16-byte accesses 64 bytes apart.)
 typedef uint32_t u32x4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t fr_cw(uint32_t tid, int i) { return 4 * tid + 1024 * (i >> 2) + (i & 3); }
+// Whether a sub-chunk's marks load without guards: word mode every word
+// inside; byte mode the 1025 words under it inside the stream.
+template <int B>
+__device__ __forceinline__ bool fr_full(uint32_t base, uint32_t Q) {
+    return B == 4 ? base + kFChunk <= Q : (uint64_t)base + kFChunk + 4 <= (uint64_t)Q + 3;
+}
+template <int B>
 __device__ __forceinline__ void fr_cload(const uint32_t *w, uint32_t Q, uint32_t base, uint32_t tid, uint32_t (&r)[16]) {
-    if (base + kFChunk <= Q) {
+    if (B == 4 && fr_full<B>(base, Q)) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const u32x4f v = __builtin_nontemporal_load((const u32x4f *)(w + base + 4 * tid + 1024 * k));
             r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
         }
+    } else if (B == 1 && fr_full<B>(base, Q)) {   // positions 4 tid + 1024 k + c: word wb + tid + 256 k, byte c
+        const uint32_t wb = base >> 2;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t a = w[wb + tid + 256 * k], b = w[wb + tid + 256 * k + 1];
+            r[4 * k] = a;
+            r[4 * k + 1] = __builtin_amdgcn_alignbyte(b, a, 1);
+            r[4 * k + 2] = __builtin_amdgcn_alignbyte(b, a, 2);
+            r[4 * k + 3] = __builtin_amdgcn_alignbyte(b, a, 3);
+        }
     } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) r[i] = base + fr_cw(tid, i) < Q ? w[base + fr_cw(tid, i)] : 0u;
+        for (int i = 0; i < 16; ++i) r[i] = base + fr_cw(tid, i) < Q ? fr_at<B>(w, Q, base + fr_cw(tid, i)) : 0u;
     }
 }
 
@@ -92,17 +139,6 @@ __device__ __forceinline__ bool fr_block_any(bool p, FrAny &a, uint32_t &par) {
     const u32x4f v = *(const u32x4f *)a.f[par];
     par ^= 1u;
     return (v.x | v.y | v.z | v.w) != 0;
-}
-
-// Next chain word on a full sub-chunk (every position < Q), R = whole words
-// left from q (>= 1): one compare of the size against R.  A size that is not
-// a multiple of 4 and reaches no further than the last whole word gives
-// kFUnal even when the fragment would end in the missing bytes of a partial
-// last word (fr_next says kFStop there): either way the real chain ending on
-// it leaves the word walk, and the exact walk settles it.
-__device__ __forceinline__ uint32_t fr_next_full(uint32_t m, uint32_t q, uint32_t R) {
-    const uint32_t sz4 = (m >> 2) & 0x1fffffffu;
-    return sz4 < R ? ((m & 3u) ? kFUnal : q + 1 + sz4) : kFStop;
 }
 
 // Inclusive prefix sum over the wave.
@@ -135,6 +171,7 @@ __device__ __forceinline__ uint32_t fr_wave_incl(uint32_t v) {
 // words (complete fragments all), acnt[sub] of them.
 constexpr uint32_t kFRes = 0x10000u;
 constexpr uint32_t kFPtr = 0xfffu;     // the local pointer of a J value (bit 12: the word's LAST flag)
+template <int B>
 __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
                                                       uint16_t *exitR, uint32_t *alist, uint32_t *acnt) {
     __shared__ __attribute__((aligned(16))) uint32_t J[kFChunk];
@@ -145,11 +182,11 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
     const uint32_t send = min(sbeg + kFSuper, Q);   // chain words past it leave the super-chunk
     const uint32_t nsub = (send - sbeg + kFChunk - 1) / kFChunk;
     uint32_t x[16], y[16];
-    fr_cload(w, Q, sbeg + (nsub - 1) * kFChunk, tid, x);
+    fr_cload<B>(w, Q, sbeg + (nsub - 1) * kFChunk, tid, x);
     for (int j = (int)nsub - 1; j >= 0; --j) {
         const uint32_t base = sbeg + (uint32_t)j * kFChunk;
         const uint32_t bend = base + kFChunk;
-        if (j > 0) fr_cload(w, Q, base - kFChunk, tid, y);   // next sub-chunk's words in flight
+        if (j > 0) fr_cload<B>(w, Q, base - kFChunk, tid, y);   // next sub-chunk's words in flight
         // J: a local pointer with the word's LAST flag (next mark inside), the
         // next mark's offset past bend when it lies in a later sub-chunk
         // [bend, send) (looked up below), else the word itself as the last one
@@ -157,12 +194,12 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
         const uint32_t lim = send > bend ? send - bend : 0u;
         const uint32_t own0 = kFRes | (base - sbeg + 4 * tid);
         uint32_t act = 0, look = 0;
-        if (bend <= Q) {
+        if (bend <= Q && fr_full<B>(base, Q)) {
             // a full sub-chunk: d = local position of the next mark.  A size
-            // that is not a multiple of 4 ends the chain (terminal), and a
-            // fragment that does not fit reaches past Q >= send, so neither
-            // needs its own test here.  One band of 4 words at a time (few
-            // live registers: occupancy bounds this kernel)
+            // that is not a multiple of 4 ends the chain (word mode terminal),
+            // and a fragment that does not fit reaches past Q >= send, so
+            // neither needs its own test here.  One band of 4 words at a time
+            // (few live registers: occupancy bounds this kernel)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 uint32_t t[4];
@@ -170,8 +207,9 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
                 for (int c = 0; c < 4; ++c) {
                     const int i = 4 * k + c;
                     const uint32_t m = fr_bswap(x[i]);
-                    const uint32_t d = ((m >> 2) & 0x1fffffffu) + 4 * tid + 1024 * k + c + 1;
-                    const bool al = (m & 3u) == 0;
+                    const uint32_t d = B == 4 ? ((m >> 2) & 0x1fffffffu) + 4 * tid + 1024 * k + c + 1
+                                              : (m & kSizeMask) + 4 * tid + 1024 * k + c + 4;
+                    const bool al = B == 1 || (m & 3u) == 0;
                     const bool in = al && d < kFChunk, lk = al && d - kFChunk < lim;
                     act |= (in ? 1u : 0u) << i;
                     look |= (lk ? 1u : 0u) << i;
@@ -187,7 +225,7 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
                 for (int c = 0; c < 4; ++c) {
                     const int i = 4 * k + c;
                     const uint32_t q = base + fr_cw(tid, i);
-                    const uint32_t v = q < Q ? fr_next(fr_bswap(x[i]), q, Q, tb) : kFStop;
+                    const uint32_t v = q < Q ? fr_next<B>(fr_bswap(x[i]), q, Q, tb) : kFStop;
                     act |= (v < bend ? 1u : 0u) << i;   // a word inside (terminals are >= kFUnal)
                     const bool lk = v - bend < lim;
                     look |= (lk ? 1u : 0u) << i;
@@ -259,10 +297,11 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
 
 // The super-chunk exit of word q < Q: the next mark after its chain's last
 // word inside the super-chunk (a word >= min(super end, Q), or a terminal).
+template <int B>
 __device__ __forceinline__ uint32_t fr_exit(const uint32_t *w, const uint16_t *exitR, uint32_t Q, uint32_t tb,
                                             uint32_t q) {
     const uint32_t r = (q & ~(kFSuper - 1)) + exitR[q];
-    return fr_next(fr_bswap(w[r]), r, Q, tb);
+    return fr_next<B>(fr_bswap(fr_at<B>(w, Q, r)), r, Q, tb);
 }
 
 // ---------------------------------------------------------------------------
@@ -280,15 +319,17 @@ __device__ __forceinline__ uint32_t fr_exit(const uint32_t *w, const uint16_t *e
 //                  entry of the group (sentry).
 constexpr uint32_t kFixWin = 256;   // entry words per super-chunk window
 constexpr uint32_t kFixGrp = 64;    // super-chunks per group
+template <int B>
 struct FrExits {   // what fr_exit reads
     const uint32_t *w;
     const uint16_t *exitR;
     uint32_t Q, tb;
-    __device__ __forceinline__ uint32_t operator()(uint32_t q) const { return fr_exit(w, exitR, Q, tb, q); }
+    __device__ __forceinline__ uint32_t operator()(uint32_t q) const { return fr_exit<B>(w, exitR, Q, tb, q); }
 };
 // k_fr_win: the window table, wtab[s][d] = exit of word d < kFixWin of
 // super-chunk s (kFStop past Q), every entry in parallel.
-__global__ __launch_bounds__(256) void k_fr_win(FrExits ex, uint32_t nsup, uint32_t *wtab) {
+template <int B>
+__global__ __launch_bounds__(256) void k_fr_win(FrExits<B> ex, uint32_t nsup, uint32_t *wtab) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (uint64_t)nsup * kFixWin) return;
     const uint64_t q = (i / kFixWin) * kFSuper + i % kFixWin;
@@ -304,7 +345,8 @@ __device__ __forceinline__ void fix_stage(const uint32_t *wtab, uint32_t nsup, u
     __syncthreads();
 }
 // One hop from chain word e inside group g: the exit of e's super-chunk.
-__device__ __forceinline__ uint32_t fix_hop(const FrExits &ex, const uint32_t *win, uint32_t g, uint32_t e) {
+template <int B>
+__device__ __forceinline__ uint32_t fix_hop(const FrExits<B> &ex, const uint32_t *win, uint32_t g, uint32_t e) {
     const uint32_t s = e >> (kFChunkLog2 + kFSuperLog2), d = e & (kFSuper - 1);
     return d < kFixWin ? win[(s - g * kFixGrp) * kFixWin + d] : ex(e);
 }
@@ -315,7 +357,8 @@ __device__ __forceinline__ uint32_t fix_hop(const FrExits &ex, const uint32_t *w
 // a walk must go on through fr_exit: gsx[g][k][d] (k_fr_fix_top uses it for
 // deep group entries).  Then the group exits of the first super-chunk's
 // window, gexit[g][d], resolved through the deep words.  128 KiB of LDS.
-__global__ __launch_bounds__(256) void k_fr_fix_grp(FrExits ex, const uint32_t *wtab, uint32_t nsup,
+template <int B>
+__global__ __launch_bounds__(256) void k_fr_fix_grp(FrExits<B> ex, const uint32_t *wtab, uint32_t nsup,
                                                     uint32_t *gsx, uint32_t *gexit) {
     __shared__ __attribute__((aligned(16))) uint32_t win[kFixGrp * kFixWin];
     __shared__ __attribute__((aligned(16))) uint32_t sg[kFixGrp * kFixWin];
@@ -355,7 +398,8 @@ __global__ __launch_bounds__(256) void k_fr_fix_grp(FrExits ex, const uint32_t *
 // The group exits go through LDS when they fit (a stream up to kFTopLds
 // groups, 2.5 GiB): the hop chain then costs LDS latency per group.
 constexpr uint32_t kFTopLds = 160;
-__global__ __launch_bounds__(1024) void k_fr_fix_top(FrExits ex, const uint32_t *gsx, const uint32_t *gexit,
+template <int B>
+__global__ __launch_bounds__(1024) void k_fr_fix_top(FrExits<B> ex, const uint32_t *gsx, const uint32_t *gexit,
                                                      uint32_t ngrp, uint32_t *gentry, uint64_t *res) {
     __shared__ __attribute__((aligned(16))) uint32_t gl[kFTopLds * kFixWin];
     const uint32_t Q = ex.Q;
@@ -388,7 +432,8 @@ __global__ __launch_bounds__(1024) void k_fr_fix_top(FrExits ex, const uint32_t 
     if (threadIdx.x == 0) res[0] = e;   // >= Q: ran to the end; kFStop / kFUnal: terminal met on the real chain
 }
 
-__global__ __launch_bounds__(256) void k_fr_fix_fill(FrExits ex, const uint32_t *wtab, const uint32_t *gentry,
+template <int B>
+__global__ __launch_bounds__(256) void k_fr_fix_fill(FrExits<B> ex, const uint32_t *wtab, const uint32_t *gentry,
                                                      uint32_t nsup, uint32_t *sentry) {
     __shared__ __attribute__((aligned(16))) uint32_t win[kFixGrp * kFixWin];
     const uint32_t g = blockIdx.x;
@@ -445,6 +490,7 @@ __device__ __forceinline__ uint32_t fr_wave_min(uint32_t v) {
     return v;
 }
 
+template <int B>
 __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
                                                      const uint32_t *sentry, const uint64_t *res,
                                                      const uint32_t *alist, const uint32_t *acnt, FrameSub *sub,
@@ -532,7 +578,7 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
         uint32_t guess = 0, gword = 0;
         if (tid == 0) {
             guess = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-            if (base + guess < Q) gword = w[base + guess];
+            if (base + guess < Q) gword = fr_at<B>(w, Q, base + guess);
         }
         // drop the nodes with no predecessor in S until nothing changes; every
         // node left reaches back to the entry (positions fall along
@@ -637,8 +683,8 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
             const uint32_t q = base + last;
             uint32_t v = kFStop;
             if (q < Q) {
-                const uint32_t m = fr_bswap(last == guess ? gword : w[q]);
-                v = fr_next(m, q, Q, tb);
+                const uint32_t m = fr_bswap(last == guess ? gword : fr_at<B>(w, Q, q));
+                v = fr_next<B>(m, q, Q, tb);
                 if (v < kFUnal) {
                     atomicOr(&fb[last >> 5], 1u << (last & 31));
                     if (m >> 31) atomicOr(&lb[last >> 5], 1u << (last & 31));
@@ -723,11 +769,26 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
     const uint64_t s0 = tid * R, s1 = min(s0 + R, nsup);
     uint64_t f = 0, l = 0;
     uint32_t t = 2u;
-    for (uint64_t s = s0; s < s1; ++s) {
-        const FrameSuper v = sup[s];
-        f += v.nfrag;
-        l += v.nlast;
-        if (v.nfrag) t = v.tail;
+    constexpr int kRun = 12;   // runs up to this long load at once (registers)
+    FrameSuper run[kRun];
+    if (R <= kRun) {
+#pragma unroll
+        for (int i = 0; i < kRun; ++i)
+            if (s0 + i < s1) run[i] = sup[s0 + i];
+#pragma unroll
+        for (int i = 0; i < kRun; ++i)
+            if (s0 + i < s1) {
+                f += run[i].nfrag;
+                l += run[i].nlast;
+                if (run[i].nfrag) t = run[i].tail;
+            }
+    } else {
+        for (uint64_t s = s0; s < s1; ++s) {
+            const FrameSuper v = sup[s];
+            f += v.nfrag;
+            l += v.nlast;
+            if (v.nfrag) t = v.tail;
+        }
     }
     sf[tid] = f;
     sl[tid] = l;
@@ -746,8 +807,7 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
     uint32_t ct = tid ? st[tid - 1] : 2u;
     if (ct == 2u) ct = 1u;   // fragment 0 starts a message
     uint64_t best = 0;
-    for (uint64_t s = s0; s < s1; ++s) {
-        const FrameSuper v = sup[s];
+    auto emit = [&](uint64_t s, const FrameSuper &v) {
         FrameBase o;
         o.frag = cf;
         o.last = cl;
@@ -758,6 +818,13 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
         cf += v.nfrag;
         cl += v.nlast;
         if (v.nfrag) ct = v.tail;
+    };
+    if (R <= kRun) {
+#pragma unroll
+        for (int i = 0; i < kRun; ++i)
+            if (s0 + i < s1) emit(s0 + i, run[i]);
+    } else {
+        for (uint64_t s = s0; s < s1; ++s) emit(s, sup[s]);
     }
     if (best) atomicMax((unsigned long long *)&fc, (unsigned long long)best);
     __syncthreads();
@@ -777,6 +844,7 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
 // offset, or the end of the last complete message) so k_fr_copy reads body
 // sizes as gaps.
 // ---------------------------------------------------------------------------
+template <int B>
 __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w, uint32_t Q, const FrameSub *sub,
                                                   const FrameBase *bases, const uint32_t *fbits,
                                                   const uint32_t *lbits, uint64_t cap, int stream_offsets,
@@ -822,19 +890,19 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
         if (f >= F) break;
         const uint32_t bt = __ffs(bits) - 1;
         const uint32_t lp = 32 * tid + bt;
-        const uint64_t p = 4 * (base + lp);
+        const uint64_t p = B * (base + lp);   // stream byte of the mark
         const bool last = (lw >> bt) & 1;
         const bool first = f == 0 || prev_last;
         if (first && m < mlim) {   // payload offsets: fragments tile the stream (p - 4 f)
             const uint32_t kk = (uint32_t)(m - lb0);
-            so[kk] = (uint16_t)(stream_offsets ? 4 * lp : 4 * (lp - (uint32_t)(f - fb0)));
+            so[kk] = (uint16_t)(stream_offsets ? B * lp : B * lp - 4 * (uint32_t)(f - fb0));
             klo = min(klo, kk);
             khi = max(khi, kk + 1);
         }
         if (first && m == cap) { res[3] = p; res[5] = f; }   // handleRead's split point (:57-60)
         if (frag_pos && m <= cap) frag_pos[f] = p;
         if (f + 1 == F) {   // the last LAST fragment closes the last complete message
-            const uint64_t size = fr_bswap(w[p >> 2]) & kSizeMask;
+            const uint64_t size = fr_bswap(fr_at<B>(w, Q, (uint32_t)(base + lp))) & kSizeMask;
             if (m + 1 <= cap) msg_offsets[m + 1] = stream_offsets ? p + 4 + size : p - 4 * f + size;
             if (M <= cap) {
                 res[3] = p + 4 + size;
@@ -851,7 +919,7 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
     __syncthreads();
     klo = min(wlo[0], wlo[1]);
     khi = max(whi[0], whi[1]);
-    const uint64_t vbase = stream_offsets ? 4 * base : 4 * (base - fb0);
+    const uint64_t vbase = stream_offsets ? B * base : B * base - 4 * fb0;
     for (uint32_t kk = klo + tid; kk < khi; kk += 128) msg_offsets[lb0 + kk] = vbase + so[kk];
 }
 
@@ -921,31 +989,37 @@ __global__ __launch_bounds__(256) void k_fr_copy(const uint8_t *in, const uint64
 }
 
 // ---- launchers -------------------------------------------------------------------
-int frame_parallel(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                   uint64_t *msg_offsets, bool frag_list, void *stream) {
-    hipStream_t st = (hipStream_t)stream;
+template <int B>
+static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+                        uint64_t *msg_offsets, bool frag_list, hipStream_t st) {
     const uint32_t *w = (const uint32_t *)in;
-    const uint32_t Q = (uint32_t)(len / 4), tb = (uint32_t)(len & 3);
+    const uint32_t Q = frame_positions(len, B), tb = B == 4 ? (uint32_t)(len & 3) : 0u;
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
-    hipLaunchKernelGGL(k_fr_exits, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitR, ws.alist, ws.acnt);
+    hipLaunchKernelGGL(k_fr_exits<B>, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitR, ws.alist, ws.acnt);
     const uint64_t ngrp = (nsup + kFixGrp - 1) / kFixGrp;
     if (hipMemsetAsync(ws.sentry, 0xff, nsup * 4, st) != hipSuccess) return (int)hipErrorUnknown;
     if (hipMemsetAsync(ws.gentry, 0xff, ngrp * 4, st) != hipSuccess) return (int)hipErrorUnknown;
-    const FrExits ex{w, ws.exitR, Q, tb};
-    hipLaunchKernelGGL(k_fr_win, dim3((uint32_t)((nsup * kFixWin + 255) / 256)), dim3(256), 0, st, ex, (uint32_t)nsup,
-                       ws.wtab);
-    hipLaunchKernelGGL(k_fr_fix_grp, dim3((uint32_t)ngrp), dim3(kFixWin), 0, st, ex, ws.wtab, (uint32_t)nsup, ws.gsx,
-                       ws.gexit);
-    hipLaunchKernelGGL(k_fr_fix_top, dim3(1), dim3(1024), 0, st, ex, ws.gsx, ws.gexit, (uint32_t)ngrp, ws.gentry,
+    const FrExits<B> ex{w, ws.exitR, Q, tb};
+    hipLaunchKernelGGL(k_fr_win<B>, dim3((uint32_t)((nsup * kFixWin + 255) / 256)), dim3(256), 0, st, ex,
+                       (uint32_t)nsup, ws.wtab);
+    hipLaunchKernelGGL(k_fr_fix_grp<B>, dim3((uint32_t)ngrp), dim3(kFixWin), 0, st, ex, ws.wtab, (uint32_t)nsup,
+                       ws.gsx, ws.gexit);
+    hipLaunchKernelGGL(k_fr_fix_top<B>, dim3(1), dim3(1024), 0, st, ex, ws.gsx, ws.gexit, (uint32_t)ngrp, ws.gentry,
                        ws.res);
-    hipLaunchKernelGGL(k_fr_fix_fill, dim3((uint32_t)ngrp), dim3(256), 0, st, ex, ws.wtab, ws.gentry, (uint32_t)nsup,
-                       ws.sentry);
-    hipLaunchKernelGGL(k_fr_mark, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.alist,
+    hipLaunchKernelGGL(k_fr_fix_fill<B>, dim3((uint32_t)ngrp), dim3(256), 0, st, ex, ws.wtab, ws.gentry,
+                       (uint32_t)nsup, ws.sentry);
+    hipLaunchKernelGGL(k_fr_mark<B>, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.alist,
                        ws.acnt, ws.sub, ws.fbits, ws.lbits, ws.sup);
     hipLaunchKernelGGL(k_fr_bases, dim3(1), dim3(1024), 0, st, ws.sup, nsup, ws.bases, ws.res);
-    hipLaunchKernelGGL(k_fr_emit, dim3((uint32_t)nsub), dim3(128), 0, st, w, Q, ws.sub, ws.bases, ws.fbits,
+    hipLaunchKernelGGL(k_fr_emit<B>, dim3((uint32_t)nsub), dim3(128), 0, st, w, Q, ws.sub, ws.bases, ws.fbits,
                        ws.lbits, cap, stream_offsets ? 1 : 0, msg_offsets, frag_list ? ws.frag_pos : nullptr, ws.res);
     return (int)hipGetLastError();
+}
+
+int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+                   uint64_t *msg_offsets, bool frag_list, void *stream) {
+    return B == 1 ? frame_launch<1>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, (hipStream_t)stream)
+                  : frame_launch<4>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, (hipStream_t)stream);
 }
 
 int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,

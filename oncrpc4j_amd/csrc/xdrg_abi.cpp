@@ -361,6 +361,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 27: if (!in(0, 2)) return -1; t.enc_out = (int32_t)v; return 0;
     case 28: if (!in(0, 1)) return -1; t.pay_nts = (int32_t)v; return 0;
     case 29: if (!in(0, 1)) return -1; t.stride_check = (int32_t)v; return 0;
+    case 30: if (!in(0, 1)) return -1; t.frame_bytes = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -1549,11 +1550,24 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
     if (rc) return rc;
     const bool stream_offsets = payload == nullptr;
     bool serial = !aligned(in, 4) || Q == 0;
-    if (!serial) {   // parallel walk; a real chain meeting a size % 4 != 0 goes serial
-        HIPCHK(c, (hipError_t)frame_parallel(in, len, ws, cap, stream_offsets, msg_offsets, !stream_offsets, c->stream));
+    if (!serial) {   // parallel walk over words; a real chain meeting a size % 4 != 0 walks again over bytes
+        HIPCHK(c, (hipError_t)frame_parallel(in, len, 4, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
+                                             c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 48, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (c->h_stat[2] == kFUnal) serial = true;
+        if (c->h_stat[2] == kFUnal) {
+            if (len < kFByteMaxLen && c->tune.frame_bytes) {
+                rc = frame_ws(c, frame_positions(len, 1), ws);
+                if (rc) return rc;
+                HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));
+                HIPCHK(c, (hipError_t)frame_parallel(in, len, 1, ws, cap, stream_offsets, msg_offsets,
+                                                     !stream_offsets, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 48, hipMemcpyDeviceToHost, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+            } else {
+                serial = true;
+            }
+        }
     }
     if (serial) {
         if (len < 4) {

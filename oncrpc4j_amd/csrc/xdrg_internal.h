@@ -182,6 +182,8 @@ struct Tuning {
     uint32_t sweep_tile = 21504;    // key 25: the sweep decode's LDS tile (k_dec_sweep, 4 blocks per CU)
     uint32_t big_rec = 1024;        // key 13: blocks averaging >= this many XDR bytes per record
                                     // take the group kernels (0 = never)
+    int32_t frame_bytes = 1;        // key 30: a frame walk whose chain meets a size % 4 != 0: 1 the
+                                    // parallel byte-mode walk, 0 the serial walk
     int32_t stride_check = 1;       // key 29: fixed-size decode at rec_offsets: 1 check for the fixed
                                     // stride and take the stride kernels (sync calls), 0 the record path
     int32_t pay_nts = 1;            // key 28: encode payload kernel: 1 nontemporal 16-byte stores, 0 plain
@@ -262,10 +264,17 @@ struct FrameWs {                              // device workspace of one walk
                                               // last LAST one) [3] consumed bytes [4] complete messages
                                               // [5] fragments of the first `cap` messages
 };
-// Parallel walk: every result in ws.res / msg_offsets (stream or payload
-// offsets); the fragment list too when frag_list.  res[0] == kFUnal: the
-// real chain met a size % 4 != 0 — run frame_serial instead.
-int frame_parallel(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+// Walk positions of a len-byte stream: B = 4 words (len / 4), B = 1 bytes a
+// whole mark can start at (len - 3).
+inline uint32_t frame_positions(uint64_t len, int B) {
+    return B == 4 ? (uint32_t)(len / 4) : (uint32_t)(len >= 4 ? len - 3 : 0);
+}
+constexpr uint64_t kFByteMaxLen = 1ull << 31;   // byte-mode walks (positions and chain values < 2^32)
+// Parallel walk over positions of B bytes (4: words, 1: bytes): every result
+// in ws.res / msg_offsets (stream or payload offsets); the fragment list too
+// when frag_list.  res[0] == kFUnal (word mode only): the real chain met a
+// size % 4 != 0 — walk again in byte mode.
+int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, uint64_t cap, bool stream_offsets,
                    uint64_t *msg_offsets, bool frag_list, void *stream);
 int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
                  uint64_t *msg_offsets, void *stream);

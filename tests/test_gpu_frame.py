@@ -5,7 +5,8 @@ assembleXdr, rpc/RpcMessageParserTCP.java:63-140) and the golden framing
 fixtures.  Streams span several 1 MiB super-chunks, carry fragments of many
 sizes (the re-fragmenter of ctest/rpc/RpcMessageParserTCPTest.java:161-181,
 oracle.fragment), bodies full of small integers that look like marks, cut
-tails, and fragment sizes that are not multiples of 4 (serial path)."""
+tails, and fragment sizes that are not multiples of 4 (the byte-position
+walk, tuning key 30 = 1, and the serial walk, key 30 = 0, must agree)."""
 import numpy as np
 import pytest
 
@@ -88,11 +89,52 @@ def test_parallel_walk_cut_tails(gpu_ctx):
         check(gpu_ctx, stream[:cut], bodies)
 
 
-def test_unaligned_fragment_sizes_use_the_serial_walk(gpu_ctx):
+@pytest.fixture(params=[1, 0], ids=["byte_walk", "serial_walk"])
+def odd_walk(request, gpu_ctx):
+    gpu_ctx.tune(30, request.param)
+    yield request.param
+    gpu_ctx.tune(0)
+
+
+def test_unaligned_fragment_sizes(gpu_ctx, odd_walk):
     rng = np.random.default_rng(8)
     stream, bodies = build(rng, 3000, aligned=False)
     k, _ = check(gpu_ctx, stream, bodies)
     assert k == len(bodies)
+
+
+@pytest.mark.parametrize("marks_in_body", [False, True], ids=["random-bodies", "mark-like-bodies"])
+def test_byte_walk_many_messages(gpu_ctx, odd_walk, marks_in_body):
+    """Several byte-mode super-chunks (64 KiB each), big fragments, bodies of
+    small integers (false chains at every byte offset)."""
+    rng = np.random.default_rng(21 + marks_in_body)
+    stream, bodies = build(rng, 8000, aligned=False, big=2, marks_in_body=marks_in_body)
+    k, _ = check(gpu_ctx, stream, bodies)
+    assert k == len(bodies)
+
+
+def test_byte_walk_cut_tails(gpu_ctx, odd_walk):
+    rng = np.random.default_rng(6)
+    stream, bodies = build(rng, 2000, aligned=False)
+    for cut in [5, 6, 7, len(stream) // 3, len(stream) // 2 + 1, len(stream) - 1, len(stream) - 2, len(stream) - 5]:
+        check(gpu_ctx, stream[:cut], bodies)
+
+
+def test_one_odd_fragment_then_aligned(gpu_ctx, odd_walk):
+    """The bench's serial-cliff shape: a 3-byte fragment, then aligned
+    messages (every later mark at byte offset 3 mod 4)."""
+    rng = np.random.default_rng(9)
+    stream, bodies = build(rng, 4000)
+    head = oracle.fragment(b"abc", 3)
+    k, _ = check(gpu_ctx, head + stream, [b"abc"] + bodies)
+    assert k == len(bodies) + 1
+
+
+def test_byte_walk_cap(gpu_ctx, odd_walk):
+    rng = np.random.default_rng(12)
+    stream, bodies = build(rng, 700, aligned=False)
+    for cap in (1, 7, 300):
+        check(gpu_ctx, stream, bodies, cap=cap)
 
 
 def test_cap_limits_messages(gpu_ctx):
