@@ -80,9 +80,36 @@ __device__ __forceinline__ int32_t disc_native(const VField &f, uint64_t r) {
     return f.type == XDRG_T_BOOL ? (int32_t)(*p != 0) : *(const int32_t *)p;
 }
 
+// ---- extent-derived decode counts (tuning key 31) ----------------------------
+// When a schema's last dynamic field is a vector of 4-byte elements followed
+// only by fixed fields (config 4: int, string<>, int<>), a record whose extent
+// holds no trailing bytes has count = (extent left after the count word -
+// fixed tail) / 4, so the sizes pass reads one length word per record fewer
+// (the string's, at a fixed offset from the record start) and the place
+// kernel, which stages every byte anyway, checks each decoded record's count
+// word against the derived count.  Any record the derivation cannot settle
+// (trailing bytes, a short tail, a mismatching count word, a capacity error, a
+// block of big records) clears *spec, and the exact walk reruns the decode
+// (spec_mode 2) from a reset error key: results and first-bad errors are then
+// exactly the walk's.  The derived pass reports only errors of checks that
+// come before the derived count word in Xdr's order (Xdr.java:171-531).
+// (spec_mode 3, one pass: every block runs, its look-back chain needs them all)
+__device__ __forceinline__ bool spec_skip(const RecArgs &a) {
+    if (a.spec_mode != 1 && a.spec_mode != 2) return false;
+    const uint32_t s = __hip_atomic_load(a.spec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return a.spec_mode == 1 ? s == 0 : s != 0;
+}
+__device__ __forceinline__ void spec_fail(const RecArgs &a) { atomicAnd(a.spec, 0u); }
+
+__global__ void k_spec_reset(const uint32_t *spec, unsigned long long *errkey) {
+    if (threadIdx.x == 0 && *spec == 0) *errkey = kNoError;
+}
+
 // ---- scan of per-block sums: one block (1024 threads) per row ---------------
+// gate (nullable): the exact rerun's scan runs only when *gate == 0 (spec failed)
 __global__ __launch_bounds__(1024) void k_scan_rows(uint64_t *sums, uint64_t nblocks,
-                                                    uint64_t *totals) {
+                                                    uint64_t *totals, const uint32_t *gate) {
+    if (gate && *gate != 0) return;
     __shared__ uint64_t wsum[16];
     __shared__ uint64_t carry_s;
     uint64_t *row = sums + (uint64_t)blockIdx.x * nblocks;
@@ -561,6 +588,22 @@ __host__ __device__ constexpr size_t enc_lds_bytes(uint32_t nd) {
     return (size_t)(kRecPerBlock + 2) * 8 + (size_t)nd * kRecPerBlock * 12;
 }
 
+// Average XDR bytes per record of this block >= a.big_rec (the split between
+// the group and the staged kernels, both launched over the whole grid).
+// Encode reads the scanned block sums, decode the record extents.
+__device__ __forceinline__ bool block_is_big_at(const RecArgs &a, uint64_t b, bool decode) {
+    const uint64_t rb = b * kRecPerBlock;
+    const uint64_t nrec = a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock;
+    uint64_t bytes;
+    if (!decode) bytes = (b + 1 < a.nblocks ? a.block_sums[b + 1] : a.totals[0]) - a.block_sums[b];
+    else if (a.rec_in) bytes = a.rec_in[rb + nrec] - a.rec_in[rb];
+    else bytes = a.rec_stride * nrec;
+    return bytes >= (uint64_t)a.big_rec * nrec;
+}
+__device__ __forceinline__ bool block_is_big(const RecArgs &a, bool decode) {
+    return block_is_big_at(a, blockIdx.x, decode);
+}
+
 // ---- decode ------------------------------------------------------------------------
 // Walk record r (known valid) and store each dynamic field's count at
 // cnt_row[d * kRecPerBlock]; returns the record's first payload byte.
@@ -624,9 +667,14 @@ __device__ __forceinline__ uint32_t walk_counts(const RecArgs &a, uint64_t r, ui
 // and their order are walk_counts' (Xdr.java:171-531, 1028-1037): err[j] =
 // 0 or the code of its first failing check, sub[j] that check's position;
 // counts are stored for the dynamic fields the walk passed.
+// SPEC (extent-derived counts, key 31): the last dynamic field's count word
+// is not read; the count is what the extent leaves after it and the fixed
+// tail (`tail` bytes), and *unc is set when that is not a whole count.
+template <bool SPEC = false>
 __device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t r0, uint32_t nj,
                                                      uint32_t *cnt_row, uint32_t (&err)[kRecPerThread],
-                                                     uint32_t (&sub)[kRecPerThread], uint32_t rs = 1) {
+                                                     uint32_t (&sub)[kRecPerThread], uint32_t rs = 1,
+                                                     uint32_t tail = 0, bool *unc = nullptr) {
     constexpr uint32_t kNone = 0xffu;                         // slot past the batch end
     const uint8_t *dummy = (const uint8_t *)a.block_sums;     // any 4 readable bytes
     uint64_t pos[kRecPerThread], end[kRecPerThread];
@@ -647,14 +695,21 @@ __device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t 
             const bool ok = !err[j] && end[j] - pos[j] >= 4;
             m[j] = *(const uint32_t *)(ok ? a.xdr + pos[j] : dummy);
         }
+        // branch-free: the per-record branches of this check, inlined into the
+        // one-pass sweep (and into a device-function form of the sizes
+        // kernel), lost the FRAME error of a record cut short by in_len on
+        // this compiler (ROCm 7.2; a printf in the branch made it correct);
+        // selects keep one straight-line form (tests/test_spec_counts.py)
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {
-            if (err[j]) continue;
-            if (end[j] - pos[j] < 4) { err[j] = XDRG_E_SHORT; continue; }
+            const uint64_t left = end[j] - pos[j];
             const uint32_t mk = bswap32r(m[j]);
-            const uint64_t want_len = a.rec_in ? end[j] - pos[j] - 4 : a.rec_stride - 4;
-            if (!(mk & kLastFrag) || (uint64_t)(mk & kSizeMask) != want_len) { err[j] = XDRG_E_FRAME; continue; }
-            pos[j] += 4;
+            const uint64_t want_len = a.rec_in ? left - 4 : a.rec_stride - 4;
+            const bool frame_ok = (mk & kLastFrag) && (uint64_t)(mk & kSizeMask) == want_len;
+            const uint32_t e = left < 4 ? (uint32_t)XDRG_E_SHORT : (frame_ok ? 0u : (uint32_t)XDRG_E_FRAME);
+            const bool live = err[j] == 0;
+            err[j] = live ? e : err[j];
+            pos[j] += (live && !e) ? 4 : 0;
         }
     }
     uint32_t d = 0;
@@ -670,18 +725,31 @@ __device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t 
             }
             continue;
         }
+        const bool derive = SPEC && d + 1 == a.ndyn;   // count from the extent, word not read
         uint32_t w[kRecPerThread];
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {   // all length words in flight
-            const bool ok = !err[j] && end[j] - pos[j] >= 4;
-            w[j] = *(const uint32_t *)(ok ? a.xdr + pos[j] : dummy);
+            const bool ok = !derive && !err[j] && end[j] - pos[j] >= 4;
+            w[j] = derive ? 0u : *(const uint32_t *)(ok ? a.xdr + pos[j] : dummy);
         }
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {
             if (err[j]) continue;
             sub[j] = 2 * k + 1;
             if (end[j] - pos[j] < 4) { err[j] = XDRG_E_SHORT; continue; }   // length word (Xdr.java:171-175)
-            const int32_t len = (int32_t)bswap32r(w[j]);
+            int32_t len;
+            if (derive) {
+                const uint64_t left = end[j] - pos[j] - 4;   // after the count word
+                const uint64_t body = left - tail;
+                if (left < tail || body % f.xsz || body / f.xsz > 0x7fffffffull) {
+                    *unc = true;        // the count word decides: exact rerun
+                    err[j] = kNone;     // (reported as no error; the rerun reports)
+                    continue;
+                }
+                len = (int32_t)(body / f.xsz);
+            } else {
+                len = (int32_t)bswap32r(w[j]);
+            }
             pos[j] += 4;
             uint64_t need;
             if (f.xsz == 1) {
@@ -705,62 +773,78 @@ __device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t 
 
 // LDS: scnt[ND][RPB] u32.  Also stores every record's counts in
 // a.rec_cnt[d * n + r] so the place kernel never walks the stream again.
+// SPEC: the extent-derived pass (tuning key 31, spec_mode 1).
+// Blocks loop over record blocks b = blockIdx.x + k * gridDim.x when LOOP
+// (the derived-count decode's exact rerun launches a small grid, so a rerun
+// that is not needed costs a few microseconds); otherwise one block each.
+template <bool SPEC, bool LOOP = false>
 __global__ __launch_bounds__(kRecThreads) void k_dec_sizes_g(const RecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint32_t *scnt = (uint32_t *)smem;
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
-    const uint32_t t0 = threadIdx.x * kRecPerThread;
-    bool dead = false;
-    if (!a.ncond) {
-        // thread t walks records rb + t + 256 j: each length-word load of a
-        // wave covers 64 consecutive records, so neighbouring records' words
-        // share cache lines inside one instruction (one line fetch each)
-        const uint32_t t = threadIdx.x;
+    if (!SPEC && spec_skip(a)) return;   // the exact rerun, and the derived counts held
+    for (uint64_t bid = blockIdx.x; bid < a.nblocks; bid += gridDim.x) {
+        extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+        uint32_t *scnt = (uint32_t *)smem;
+        const uint64_t rb = bid * kRecPerBlock;
+        const uint32_t t0 = threadIdx.x * kRecPerThread;
+        bool dead = false;
+        // a block of big records goes to the group kernel, which does not verify: exact rerun
+        if (SPEC && threadIdx.x == 0 && a.big_rec && block_is_big_at(a, bid, true)) spec_fail(a);
+        if (!a.ncond) {
+            // thread t walks records rb + t + 256 j: each length-word load of a
+            // wave covers 64 consecutive records, so neighbouring records' words
+            // share cache lines inside one instruction (one line fetch each)
+            const uint32_t t = threadIdx.x;
 #pragma unroll
-        for (int j = 0; j < kRecPerThread; ++j)
-            for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t + j * kRecThreads] = 0;
-        const uint64_t r0 = rb + t;
-        const uint32_t nj = r0 < a.n ? (uint32_t)((a.n - r0 + kRecThreads - 1) / kRecThreads < (uint64_t)kRecPerThread
-                                                  ? (a.n - r0 + kRecThreads - 1) / kRecThreads : (uint64_t)kRecPerThread)
-                                     : 0u;
-        uint32_t err[kRecPerThread], sub[kRecPerThread];
-        walk_counts_lockstep(a, r0, nj, scnt + t, err, sub, kRecThreads);
-#pragma unroll
-        for (int j = 0; j < kRecPerThread; ++j) {
-            if (!dead && err[j]) {
-                atomicMin(a.errkey, err_key(r0 + (uint64_t)j * kRecThreads, sub[j], err[j]));
-                dead = true;   // later records of this thread are past the error
-            }
-            if (dead)
+            for (int j = 0; j < kRecPerThread; ++j)
                 for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t + j * kRecThreads] = 0;
-        }
-    }
-    for (int j = 0; a.ncond && j < kRecPerThread; ++j) {   // conditional schemas: serial walk
-        const uint64_t r = rb + t0 + j;
-        for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
-        if (r >= a.n || dead) continue;
-        uint32_t sub;
-        uint64_t st, by;
-        const uint32_t err = walk_counts(a, r, scnt + t0 + j, &sub, &st, &by);
-        if (err) {
-            atomicMin(a.errkey, err_key(r, sub, err));
-            dead = true;  // later records of this thread are past the error
-            for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
-        }
-    }
-    __syncthreads();
-    // coalesced copy of the block's counts to the workspace
-    uint64_t nrec = a.n > rb ? a.n - rb : 0;
-    if (nrec > kRecPerBlock) nrec = kRecPerBlock;
-    for (uint32_t d = 0; d < a.ndyn; ++d)
-        for (uint32_t i = threadIdx.x; i < nrec; i += kRecThreads)
-            a.rec_cnt[(uint64_t)d * a.n + rb + i] = scnt[(size_t)d * kRecPerBlock + i];
-    for (uint32_t d = 0; d < a.ndyn; ++d) {
-        uint64_t s = 0;
+            const uint64_t r0 = rb + t;
+            const uint32_t nj = r0 < a.n ? (uint32_t)((a.n - r0 + kRecThreads - 1) / kRecThreads < (uint64_t)kRecPerThread
+                                                      ? (a.n - r0 + kRecThreads - 1) / kRecThreads : (uint64_t)kRecPerThread)
+                                         : 0u;
+            uint32_t err[kRecPerThread], sub[kRecPerThread];
+            uint32_t tail = 0;   // fixed XDR bytes after the last dynamic field
+            for (uint32_t k = a.dyn_idx[a.ndyn ? a.ndyn - 1 : 0] + 1; SPEC && k < a.nf; ++k) tail += a.f[k].xbytes;
+            bool unc = false;
+            walk_counts_lockstep<SPEC>(a, r0, nj, scnt + t, err, sub, kRecThreads, tail, &unc);
+            if (SPEC && unc) spec_fail(a);
 #pragma unroll
-        for (int j = 0; j < kRecPerThread; ++j) s += scnt[(size_t)d * kRecPerBlock + t0 + j];
-        const uint64_t tot = block_sum(s);
-        if (threadIdx.x == 0) a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x] = tot;
+            for (int j = 0; j < kRecPerThread; ++j) {
+                if (!dead && err[j]) {
+                    atomicMin(a.errkey, err_key(r0 + (uint64_t)j * kRecThreads, sub[j], err[j]));
+                    dead = true;   // later records of this thread are past the error
+                }
+                if (dead)
+                    for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t + j * kRecThreads] = 0;
+            }
+        }
+        for (int j = 0; a.ncond && j < kRecPerThread; ++j) {   // conditional schemas: serial walk
+            const uint64_t r = rb + t0 + j;
+            for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
+            if (r >= a.n || dead) continue;
+            uint32_t sub;
+            uint64_t st, by;
+            const uint32_t err = walk_counts(a, r, scnt + t0 + j, &sub, &st, &by);
+            if (err) {
+                atomicMin(a.errkey, err_key(r, sub, err));
+                dead = true;  // later records of this thread are past the error
+                for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + t0 + j] = 0;
+            }
+        }
+        __syncthreads();
+        // coalesced copy of the block's counts to the workspace
+        uint64_t nrec = a.n > rb ? a.n - rb : 0;
+        if (nrec > kRecPerBlock) nrec = kRecPerBlock;
+        for (uint32_t d = 0; d < a.ndyn; ++d)
+            for (uint32_t i = threadIdx.x; i < nrec; i += kRecThreads)
+                a.rec_cnt[(uint64_t)d * a.n + rb + i] = scnt[(size_t)d * kRecPerBlock + i];
+        for (uint32_t d = 0; d < a.ndyn; ++d) {
+            uint64_t s = 0;
+#pragma unroll
+            for (int j = 0; j < kRecPerThread; ++j) s += scnt[(size_t)d * kRecPerBlock + t0 + j];
+            const uint64_t tot = block_sum(s);
+            if (threadIdx.x == 0) a.block_sums[(uint64_t)d * a.nblocks + bid] = tot;
+        }
+        if (!LOOP) break;
+        __syncthreads();   // (LDS reuse by the next block)
     }
 }
 
@@ -1049,21 +1133,6 @@ __device__ __forceinline__ void dec_words4(uint8_t *const (&dst)[R], const uint8
     }
 }
 
-// Average XDR bytes per record of this block >= a.big_rec (the split between
-// the group and the staged kernels, both launched over the whole grid).
-// Encode reads the scanned block sums, decode the record extents.
-__device__ __forceinline__ bool block_is_big_at(const RecArgs &a, uint64_t b, bool decode) {
-    const uint64_t rb = b * kRecPerBlock;
-    const uint64_t nrec = a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock;
-    uint64_t bytes;
-    if (!decode) bytes = (b + 1 < a.nblocks ? a.block_sums[b + 1] : a.totals[0]) - a.block_sums[b];
-    else if (a.rec_in) bytes = a.rec_in[rb + nrec] - a.rec_in[rb];
-    else bytes = a.rec_stride * nrec;
-    return bytes >= (uint64_t)a.big_rec * nrec;
-}
-__device__ __forceinline__ bool block_is_big(const RecArgs &a, bool decode) {
-    return block_is_big_at(a, blockIdx.x, decode);
-}
 
 template <int U, int R>
 __global__ __launch_bounds__(kRecThreads) void k_enc_place_g(const RecArgs a) {
@@ -1211,14 +1280,14 @@ __host__ __device__ constexpr size_t dec_g_lds_bytes(uint32_t nd) {
 }
 
 template <int U, int R>
-__global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
+__device__ __forceinline__ void dec_place_g_block(const RecArgs &a, uint64_t bid) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *sstart = (uint64_t *)smem;
     uint64_t *snoff = sstart + kRecPerBlock;
     uint32_t *scnt = (uint32_t *)(snoff + (size_t)a.ndyn * kRecPerBlock);
     uint32_t *supto = scnt + (size_t)a.ndyn * kRecPerBlock;
-    if (a.big_rec && !block_is_big(a, true)) return;   // the staged kernel's block
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    if (a.big_rec && !block_is_big_at(a, bid, true)) return;   // the staged kernel's block
+    const uint64_t rb = bid * kRecPerBlock;
     const uint32_t t0 = threadIdx.x * kRecPerThread;
     const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
     const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
@@ -1238,7 +1307,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) s += scnt[(size_t)d * kRecPerBlock + t0 + j];
         uint64_t btot;
-        uint64_t off = a.block_sums[(uint64_t)d * a.nblocks + blockIdx.x] + block_excl_scan(s, &btot);
+        uint64_t off = a.block_sums[(uint64_t)d * a.nblocks + bid] + block_excl_scan(s, &btot);
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {
             const uint64_t r = rb + t0 + j;
@@ -1253,7 +1322,7 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
             }
             off += c;
         }
-        if (blockIdx.x == 0 && threadIdx.x == 0) f.offsets[a.n] = a.totals[d];
+        if (bid == 0 && threadIdx.x == 0) f.offsets[a.n] = a.totals[d];
     }
     __syncthreads();
     uint64_t nrec = a.n > rb ? a.n - rb : 0;
@@ -1343,6 +1412,15 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
         for (uint32_t j = tid; j < nrec; j += kRecThreads) sstart[j] += dyn_xdr_bytes(f, cn[j]);
         __syncthreads();
         ++d;
+    }
+}
+template <int U, int R, bool LOOP = false>
+__global__ __launch_bounds__(kRecThreads) void k_dec_place_g(const RecArgs a) {
+    if (spec_skip(a)) return;   // (a big block already cleared *spec in the derived pass)
+    if (!LOOP) { dec_place_g_block<U, R>(a, blockIdx.x); return; }
+    for (uint64_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) {   // as k_dec_sizes_g
+        dec_place_g_block<U, R>(a, b);
+        __syncthreads();
     }
 }
 
@@ -2279,6 +2357,9 @@ __device__ __forceinline__ void dec_record_block(const RecArgs &a, uint64_t r, u
         const bool bytes = f.xsz == 1;
         const uint32_t *rel = snrel + (size_t)d * rs;
         const uint64_t cnt1 = rel[j + 1] - rel[j];
+        // extent-derived count (key 31): the count word must say the same
+        if ((a.spec_mode & 1) && d + 1 == a.ndyn && tid == 0 && bswap32r(*(const uint32_t *)(in + pos)) != (uint32_t)cnt1)
+            spec_fail(a);
         uint8_t *dst[1] = {f.data + f.offsets[r] * (bytes ? 1 : f.nsz)};
         const uint8_t *src[1] = {in + pos + 4};
         const uint64_t cnt[1] = {cnt1};
@@ -2724,11 +2805,120 @@ __device__ __forceinline__ uint32_t dec_fit(const RecArgs &a, const uint32_t *ss
     return (uint32_t)__syncthreads_count(fits);
 }
 
+// ---- one-pass derived counts (tuning key 31 = 2, spec_mode 3) ---------------
+// The sweep block walks its own records (the derived pass's one length-word
+// gather per record), publishes its count totals and learns the native
+// offset of its first element per dynamic field from its predecessors: a
+// decoupled look-back over one status word per block and dynamic field, flag
+// in bits 62-63 (1 = the block's own total, 2 = the inclusive prefix over
+// blocks [0, b]) | value, stored and polled with agent-scope atomics (a tagged
+// word needs no fence).  Blocks take tickets in start order, so every block
+// waited on is running and publishes its total without waiting.  Errors stay
+// local: a block decodes its records before its own first walk error, and
+// the error key (atomicMin) orders them over the batch as the walk does.
+constexpr uint64_t kLbOwn = 1ull << 62, kLbIncl = 2ull << 62, kLbVal = kLbOwn - 1;
+
+__device__ __forceinline__ void lb_put(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_get(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+// Wave 0 of block b: publish agg, look back over the predecessors 64 at a
+// time down to the nearest inclusive prefix of each field, publish the
+// inclusive prefix; s_base[d] = the exclusive prefix of field d.
+__device__ __forceinline__ void lb_resolve(const RecArgs &a, uint64_t b, const uint64_t (&agg)[kMaxDynLds],
+                                           uint64_t *s_base) {
+    const uint32_t lane = threadIdx.x & 63, nd = a.ndyn;
+    const uint64_t nb = a.nblocks;
+    uint64_t *st = a.block_sums;
+    if (lane == 0)
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d)
+            if ((uint32_t)d < nd) lb_put(st + (uint64_t)d * nb + b, (b ? kLbOwn : kLbIncl) | agg[d]);
+    uint64_t pre[kMaxDynLds] = {0, 0, 0, 0};
+    uint32_t done = 0;
+    const uint32_t all = (1u << nd) - 1;
+    int64_t p = (int64_t)b - 1 - (int64_t)lane;
+    while (b && done != all) {
+        uint64_t v[kMaxDynLds];
+        for (;;) {
+            bool ready = true;
+#pragma unroll
+            for (int d = 0; d < kMaxDynLds; ++d) {
+                if ((uint32_t)d >= nd) { v[d] = kLbIncl; continue; }
+                const uint64_t x = p >= 0 ? lb_get(st + (uint64_t)d * nb + (uint64_t)p) : kLbIncl;
+                v[d] = x;
+                ready = ready && (x >> 62) != 0;
+            }
+            if (__all(ready)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d) {
+            if ((uint32_t)d >= nd || ((done >> d) & 1)) continue;
+            const uint64_t pm = __ballot((v[d] >> 62) == 2);
+            const uint32_t first = pm ? (uint32_t)__builtin_ctzll(pm) : 63u;   // nearest inclusive predecessor
+            pre[d] += wave_sum64(lane <= first ? (v[d] & kLbVal) : 0);
+            if (pm) done |= 1u << d;
+        }
+        p -= 64;
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d) {
+            if ((uint32_t)d >= nd) continue;
+            if (b) lb_put(st + (uint64_t)d * nb + b, kLbIncl | (pre[d] + agg[d]));
+            s_base[d] = pre[d];
+            if (b + 1 == nb) {
+                a.totals[d] = pre[d] + agg[d];
+                a.f[a.dyn_idx[d]].offsets[a.n] = pre[d] + agg[d];
+            }
+        }
+}
+
+// The one-pass sweep's walk of its block (k_dec_sizes_g<true>'s, over records
+// rb + tid + 256 j): counts into scnt, errors into the error key and the
+// block's first failing record into *s_bad.  (Its record-mark check is the
+// branch-free one of walk_counts_lockstep: the branchy form, inlined here as
+// in round 2's look-back decode, lost FRAME errors; tools/diag_trunc.py.)
+__device__ __forceinline__ void one_pass_walk(const RecArgs &a, uint64_t rb, uint32_t *scnt, uint32_t *s_bad) {
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j)
+        for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + tid + j * kRecThreads] = 0;
+    const uint64_t r0 = rb + tid;
+    const uint32_t nj = r0 < a.n ? (uint32_t)((a.n - r0 + kRecThreads - 1) / kRecThreads < (uint64_t)kRecPerThread
+                                              ? (a.n - r0 + kRecThreads - 1) / kRecThreads : (uint64_t)kRecPerThread)
+                                 : 0u;
+    uint32_t err[kRecPerThread], sub[kRecPerThread];
+    uint32_t tail = 0;   // fixed XDR bytes after the last dynamic field
+    for (uint32_t k = a.dyn_idx[a.ndyn - 1] + 1; k < a.nf; ++k) tail += a.f[k].xbytes;
+    bool unc = false, dead = false;
+    walk_counts_lockstep<true>(a, r0, nj, scnt + tid, err, sub, kRecThreads, tail, &unc);
+    if (unc) spec_fail(a);
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        if (!dead && err[j]) {
+            atomicMin(a.errkey, err_key(r0 + (uint64_t)j * kRecThreads, sub[j], err[j]));
+            atomicMin(s_bad, tid + j * kRecThreads);
+            dead = true;   // later records of this thread are past the error
+        }
+        if (dead)
+            for (uint32_t d = 0; d < a.ndyn; ++d) scnt[(size_t)d * kRecPerBlock + tid + j * kRecThreads] = 0;
+    }
+}
+
 #ifndef XDRG_DEC_STAGE_OCC
 #define XDRG_DEC_STAGE_OCC 5   // blocks per CU the register budget is sized for
 #endif
-template <bool SW>
-__device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
+template <bool SW, bool ONE = false>
+__device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;
     uint32_t *sstart = (uint32_t *)smem;
@@ -2739,17 +2929,49 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
     __shared__ uint64_t s_base[kMaxDynLds];   // native offset of the block's first element, per dynamic field
     const uint32_t tid = threadIdx.x, t0 = tid * kRecPerThread;
     const uint64_t nb = a.nblocks;
-    const uint64_t bid = blockIdx.x;
-    if (a.big_rec && block_is_big_at(a, bid, true)) return;   // the group kernel's block
+    uint32_t *scnt1 = (uint32_t *)tile;   // ONE: the block's walked counts [ndyn][RPB], read before staging
+    uint32_t nlive;
+    if (ONE) {
+        __shared__ unsigned long long s_tk;
+        __shared__ uint32_t s_bad1;
+        if (tid == 0) {
+            s_tk = atomicAdd(a.lb_ticket, 1ull) + 1ull;   // (the ticket word starts at ~0)
+            s_bad1 = kRecPerBlock;
+        }
+        __syncthreads();
+        bid = s_tk;
+        const uint64_t rb = bid * kRecPerBlock;
+        one_pass_walk(a, rb, scnt1, &s_bad1);
+        uint64_t agg[kMaxDynLds] = {0, 0, 0, 0};
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d) {
+            if ((uint32_t)d >= a.ndyn) continue;
+            uint64_t sv = 0;
+#pragma unroll
+            for (int j = 0; j < kRecPerThread; ++j) sv += scnt1[(size_t)d * kRecPerBlock + tid + j * kRecThreads];
+            agg[d] = block_sum(sv);   // (its barriers also publish s_bad1 and the counts)
+        }
+        if (tid < 64) lb_resolve(a, bid, agg, s_base);
+        __syncthreads();
+        // a block of big records would be the group kernel's, which is not
+        // launched here: the exact rerun decodes the batch
+        if (a.big_rec && block_is_big_at(a, bid, true)) { if (tid == 0) spec_fail(a); return; }
+        const uint32_t nr = (uint32_t)(a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0);
+        nlive = s_bad1 < nr ? s_bad1 : nr;
+    } else {
+        if (a.big_rec && block_is_big_at(a, bid, true)) return;   // the group kernel's block
+    }
     const uint64_t rb = bid * kRecPerBlock;
     const uint32_t nrec = (uint32_t)(a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0);
     uint32_t xs[kMaxDynLds];             // XDR element size per dynamic field (1: padded bytes)
 #pragma unroll
     for (int e = 0; e < kMaxDynLds; ++e) xs[e] = (uint32_t)e < a.ndyn ? a.f[a.dyn_idx[e]].xsz : 0u;
-    const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
-    const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
-    if (tid < a.ndyn) s_base[tid] = a.block_sums[(uint64_t)tid * nb + bid];
-    const uint32_t nlive = bad > rb ? (uint32_t)(bad - rb < (uint64_t)nrec ? bad - rb : (uint64_t)nrec) : 0;
+    if (!ONE) {
+        const unsigned long long walk_key = *a.errkey;  // final after k_dec_sizes_g
+        const uint64_t bad = walk_key == kNoError ? a.n : (uint64_t)(walk_key >> 16);
+        if (tid < a.ndyn) s_base[tid] = a.block_sums[(uint64_t)tid * nb + bid];
+        nlive = bad > rb ? (uint32_t)(bad - rb < (uint64_t)nrec ? bad - rb : (uint64_t)nrec) : 0;
+    }
     if (tid == 0) s_wide = 0;
     // ---- prologue: counts, native offsets (written to the columns), capacity, extents
     const uint64_t sb = nlive ? rec_extent(a, rb).a + (a.framed ? 4 : 0) : 0;   // stream offset of sstart 0
@@ -2775,11 +2997,11 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {
             const uint64_t r = rb + t0 + j;
-            c[j] = t0 + j < nlive ? a.rec_cnt[(uint64_t)d * a.n + r] : 0u;
+            c[j] = t0 + j < nlive ? (ONE ? scnt1[(size_t)d * kRecPerBlock + t0 + j] : a.rec_cnt[(uint64_t)d * a.n + r]) : 0u;
             s += c[j];
         }
         uint64_t btot;
-        const uint64_t base = a.block_sums[(uint64_t)d * nb + bid];
+        const uint64_t base = ONE ? s_base[d] : a.block_sums[(uint64_t)d * nb + bid];
         uint64_t off = base + block_excl_scan(s, &btot);
         wide |= btot * (f.xsz == 1 ? 1 : f.nsz) >= (1ull << 31);
 #pragma unroll
@@ -2791,12 +3013,13 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
                 if (t0 + j < nlive && off + c[j] > f.cap) {   // native column too small
                     atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
                     if (upto[j] > k) upto[j] = k;
+                    if (a.spec_mode & 1) spec_fail(a);   // on derived counts: the exact walk decides
                 }
             }
             off += c[j];
         }
         if (tid == kRecThreads - 1) snrel[d * RS + kRecPerBlock] = (uint32_t)(off - base);
-        if (tid == 0 && bid == 0) f.offsets[a.n] = a.totals[d];
+        if (!ONE && tid == 0 && bid == 0) f.offsets[a.n] = a.totals[d];   // (ONE: lb_resolve)
     }
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) supto[t0 + j] = (uint8_t)upto[j];
@@ -2865,8 +3088,17 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
         }
         __syncthreads();
         if (!SW) dec_stage_batch<RS>(a, tile, lds0, rb, js, je, sstart, snrel, supto, s_base, xs, lean, tid, kRecThreads);
-        else if (sweep) dec_stage_sweep<RS>(a, tile, lds0, rb, js, je, sstart, snrel, (uint32_t *)supto, smeta1, smap, sf);
-        else
+        else if (sweep) {
+            if ((a.spec_mode & 1) && tid < je - js) {   // derived counts (key 31): check the count words
+                const uint32_t j = js + tid, dl = a.ndyn - 1;
+                uint32_t fb = 0;   // fixed XDR bytes before the last dynamic field
+                for (uint32_t k = 0; k < a.dyn_idx[dl]; ++k) fb += a.f[k].kind != XDRG_K_DYNAMIC ? a.f[k].xbytes : 0u;
+                const uint32_t *rel = snrel + dl * RS;
+                const uint32_t cw = tile_word(tile, lds0 + (int64_t)(sstart[j] + fb + dyn_before_xs(xs, snrel, j, dl, RS)));
+                if (bswap32r(cw) != rel[j + 1] - rel[j]) spec_fail(a);
+            }
+            dec_stage_sweep<RS>(a, tile, lds0, rb, js, je, sstart, snrel, (uint32_t *)supto, smeta1, smap, sf);
+        } else
             for (uint32_t j = js; j < je; ++j)
                 dec_record_block(a, rb + j, sb + sstart[j], supto[j], snrel, j, tid, kRecThreads);
         js = je;
@@ -2878,11 +3110,27 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a) {
 #define XDRG_DEC_SWEEP_OCC 4   // blocks per CU the sweep kernel's register budget is sized for (5: 96 VGPRs
                                // with spills, 3.71 ms vs 3.18 ms on config 4 at its best tile)
 #endif
+// (LOOP: blocks loop over record blocks as k_dec_sizes_g)
+template <bool LOOP>
 __global__ __launch_bounds__(kRecThreads, XDRG_DEC_STAGE_OCC) void k_dec_stage(const RecArgs a) {
-    dec_stage_body<false>(a);
+    if (spec_skip(a)) return;
+    if (!LOOP) { dec_stage_body<false>(a, blockIdx.x); return; }
+    for (uint64_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) {
+        dec_stage_body<false>(a, b);
+        __syncthreads();
+    }
 }
+// MODE 0: a block per record block; 1 (LOOP): blocks loop over record blocks;
+// 2: one pass with derived counts (spec_mode 3: walk + look-back in the block)
+template <int MODE>
 __global__ __launch_bounds__(kRecThreads, XDRG_DEC_SWEEP_OCC) void k_dec_sweep(const RecArgs a) {
-    dec_stage_body<true>(a);
+    if (MODE == 2) { dec_stage_body<true, true>(a, 0); return; }
+    if (spec_skip(a)) return;   // derived counts already failed / held (key 31)
+    if (MODE == 0) { dec_stage_body<true>(a, blockIdx.x); return; }
+    for (uint64_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) {
+        dec_stage_body<true>(a, b);
+        __syncthreads();
+    }
 }
 
 // ===========================================================================
@@ -2899,11 +3147,35 @@ static void launch_ur(int u, int r, dim3 grid, size_t lds, hipStream_t st, const
 }
 template <int U, int R> struct EncG { static constexpr auto fn = k_enc_place_g<U, R>; };
 template <int U, int R> struct DecG { static constexpr auto fn = k_dec_place_g<U, R>; };
+template <int U, int R> struct DecGL { static constexpr auto fn = k_dec_place_g<U, R, true>; };
 
 int launch_scan_rows(uint64_t *sums, uint64_t nblocks, uint64_t *totals, uint32_t rows, void *stream) {
     if (!rows) return hipSuccess;
-    hipLaunchKernelGGL(k_scan_rows, dim3(rows), dim3(1024), 0, (hipStream_t)stream, sums, nblocks, totals);
+    hipLaunchKernelGGL(k_scan_rows, dim3(rows), dim3(1024), 0, (hipStream_t)stream, sums, nblocks, totals,
+                       (const uint32_t *)nullptr);
     return (int)hipGetLastError();
+}
+
+int launch_spec_reset(const uint32_t *spec, unsigned long long *errkey, void *stream) {
+    hipLaunchKernelGGL(k_spec_reset, dim3(1), dim3(64), 0, (hipStream_t)stream, spec, errkey);
+    return (int)hipGetLastError();
+}
+
+// The staged decode takes the output-stationary sweep (k_dec_sweep).
+static bool dec_sweep_ok(const RecArgs &a, const Tuning &t) {
+    bool sw = t.dec_lean == 2 && t.sweep_tile <= 32768 && a.ndyn <= 2;   // (16-bit tile offsets in meta)
+    for (uint32_t d = 0; d < a.ndyn && sw; ++d) {   // word columns take 16-byte stores of 4-byte elements
+        const VField &f = a.f[a.dyn_idx[d]];
+        sw = f.xsz == 1 || (f.nsz == 4 && ((uintptr_t)f.data & 3) == 0);
+    }
+    return sw;
+}
+
+bool rec_spec_ok(const RecArgs &a, const Tuning &t) {
+    if (!t.spec_sizes || t.rec != 4 || a.ncond || a.byref || !a.rec_in || !a.ndyn || a.ndyn > 2) return false;
+    for (uint32_t d = 0; d < a.ndyn; ++d)
+        if (!stage_type(a.f[a.dyn_idx[d]].type, a.f[a.dyn_idx[d]].xsz)) return false;
+    return a.f[a.dyn_idx[a.ndyn - 1]].xsz == 4 && dec_sweep_ok(a, t);   // a word vector last
 }
 
 static void launch_enc_payload(int hoist, int nts, dim3 grid, hipStream_t st, const RecArgs &a) {
@@ -2938,12 +3210,17 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     const bool pay = t.payload && a.pay_pos && a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1 &&
                      ((stage && t.big_rec) || (grp && !stage && t.rec == 0));
     a.payk = pay ? 1u : 0u;
+    // the derived-count decode's exact rerun (spec_mode 2) runs on a small grid
+    // whose blocks loop over the record blocks: when the rerun is not needed
+    // its kernels return at once for a few microseconds each
+    const dim3 dgrid((unsigned)(a.spec_mode == 2 && nb > 1024 ? 1024 : nb));
     const uint64_t pblk = (a.n + 3) / 4;   // a wave per record, 4 records per block
     const dim3 pgrid((unsigned)(pblk < (1u << 22) ? pblk : (1u << 22)));
     switch (phase) {
     case REC_ENC_SIZES: hipLaunchKernelGGL(k_enc_sizes, dim3(nb), dim3(kRecThreads), 0, st, a); break;
     case REC_ENC_SCAN:
-        hipLaunchKernelGGL(k_scan_rows, dim3(1), dim3(1024), 0, st, a.block_sums, nb, a.totals);
+        hipLaunchKernelGGL(k_scan_rows, dim3(1), dim3(1024), 0, st, a.block_sums, nb, a.totals,
+                           (const uint32_t *)nullptr);
         break;
     case REC_ENC_PLACE:
         if (stage) {   // small-record blocks staged, large-record blocks by the group kernel
@@ -2968,29 +3245,37 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
         }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
-    case REC_DEC_SIZES:   // (the ticket word precedes the status words)
-        if (grp || lane) hipLaunchKernelGGL(k_dec_sizes_g, dim3(nb), dim3(kRecThreads),
+    case REC_DEC_SIZES:
+        if (a.spec_mode == 3) break;   // one pass: the sweep walks its own block
+        if (a.spec_mode == 1) {   // extent-derived counts (key 31; rec_spec_ok held)
+            a.big_rec = t.big_rec;
+            hipLaunchKernelGGL(k_dec_sizes_g<true>, dim3(nb), dim3(kRecThreads), (size_t)a.ndyn * kRecPerBlock * 4, st, a);
+        } else if (a.spec_mode == 2) {
+            hipLaunchKernelGGL((k_dec_sizes_g<false, true>), dgrid, dim3(kRecThreads), (size_t)a.ndyn * kRecPerBlock * 4, st, a);
+        } else if (grp || lane) hipLaunchKernelGGL(k_dec_sizes_g<false>, dim3(nb), dim3(kRecThreads),
                                     (size_t)a.ndyn * kRecPerBlock * 4, st, a);
         else hipLaunchKernelGGL(k_dec_sizes_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
     case REC_DEC_SCAN:
-        if (a.ndyn)
-            hipLaunchKernelGGL(k_scan_rows, dim3(a.ndyn), dim3(1024), 0, st, a.block_sums, nb, a.totals);
+        if (a.ndyn && a.spec_mode != 3)
+            hipLaunchKernelGGL(k_scan_rows, dim3(a.ndyn), dim3(1024), 0, st, a.block_sums, nb, a.totals,
+                               (const uint32_t *)(a.spec_mode == 2 ? a.spec : nullptr));
         break;
     case REC_DEC_PLACE:
         if (stage) {
             a.big_rec = t.big_rec;
-            // the sweep writes word columns with 16-byte stores of 4-byte elements
-            bool sw = t.dec_lean == 2 && t.sweep_tile <= 32768 && a.ndyn <= 2;   // (16-bit tile offsets in meta)
-            for (uint32_t d = 0; d < a.ndyn && sw; ++d) {
-                const VField &f = a.f[a.dyn_idx[d]];
-                sw = f.xsz == 1 || (f.nsz == 4 && ((uintptr_t)f.data & 3) == 0);
-            }
+            const bool sw = dec_sweep_ok(a, t);
             if (sw) a.tile_bytes = t.sweep_tile;
             const size_t lds = dec_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack + (sw ? dec_sweep_extra(a.tile_bytes) : 0);
-            if (sw) hipLaunchKernelGGL(k_dec_sweep, dim3(nb), dim3(kRecThreads), lds, st, a);
-            else hipLaunchKernelGGL(k_dec_stage, dim3(nb), dim3(kRecThreads), lds, st, a);
-            if (a.big_rec) launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
+            const bool loop = a.spec_mode == 2;
+            if (sw && a.spec_mode == 3) hipLaunchKernelGGL(k_dec_sweep<2>, dim3(nb), dim3(kRecThreads), lds, st, a);
+            else if (sw && loop) hipLaunchKernelGGL(k_dec_sweep<1>, dgrid, dim3(kRecThreads), lds, st, a);
+            else if (sw) hipLaunchKernelGGL(k_dec_sweep<0>, dim3(nb), dim3(kRecThreads), lds, st, a);
+            else if (loop) hipLaunchKernelGGL(k_dec_stage<true>, dgrid, dim3(kRecThreads), lds, st, a);
+            else hipLaunchKernelGGL(k_dec_stage<false>, dim3(nb), dim3(kRecThreads), lds, st, a);
+            // (the derived-count pass hands any big-record block to the exact rerun)
+            if (a.big_rec && loop) launch_ur<DecGL>(t.dec_u, t.dec_r, dgrid, dec_g_lds_bytes(a.ndyn), st, a);
+            else if (a.big_rec && !(a.spec_mode & 1)) launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
             if (a.big_rec && pay) launch_dec_payload(t.pay_hoist, pgrid, st, a);
         } else if (lane || (grp && t.rec == 3)) {
             hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);

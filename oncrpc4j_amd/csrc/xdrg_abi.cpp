@@ -223,6 +223,7 @@ extern "C" uint64_t xdrg_schema_fixed_size(const xdrg_schema *s) { return s ? s-
 struct Timed {
     int kernel;
     hipEvent_t a, b;
+    bool count;   // adds a launch (false: time only, e.g. the derived-count decode's rerun)
 };
 
 // Staging ring of the XDRG_HOST_PTRS calls (host_stage.h): device slots, a
@@ -311,7 +312,7 @@ static void resolve_one(xdrg_ctx *c) {
     c->pending.pop_front();
     float ms = 0.f;
     if (hipEventSynchronize(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
-        c->launches[t.kernel] += 1;
+        c->launches[t.kernel] += t.count ? 1 : 0;
         c->ms[t.kernel] += ms;
     }
     c->pool.push_back(t.a);
@@ -322,8 +323,9 @@ static void resolve_one(xdrg_ctx *c) {
 struct TimedLaunch {
     xdrg_ctx *c;
     int kernel;
+    bool count;
     hipEvent_t a = nullptr, b = nullptr;
-    TimedLaunch(xdrg_ctx *c_, int k) : c(c_), kernel(k) {
+    TimedLaunch(xdrg_ctx *c_, int k, bool count_ = true) : c(c_), kernel(k), count(count_) {
         if (!(c->flags & XDRG_CTX_TIMING)) return;
         if (c->pending.size() > 4096) resolve_one(c);
         a = ev_get(c);
@@ -333,7 +335,7 @@ struct TimedLaunch {
     ~TimedLaunch() {
         if (!a || !b) return;
         (void)hipEventRecord(b, c->stream);
-        c->pending.push_back({kernel, a, b});
+        c->pending.push_back({kernel, a, b, count});
     }
 };
 
@@ -362,6 +364,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 28: if (!in(0, 1)) return -1; t.pay_nts = (int32_t)v; return 0;
     case 29: if (!in(0, 1)) return -1; t.stride_check = (int32_t)v; return 0;
     case 30: if (!in(0, 1)) return -1; t.frame_bytes = (int32_t)v; return 0;
+    case 31: if (!in(0, 2)) return -1; t.spec_sizes = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -1081,10 +1084,39 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
     a.rec_in = rec_offsets;
     a.byref = byref;
     a.ref_pos = ref_pos;
-    HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
+    // extent-derived counts (tuning key 31): the derived pass, then the exact
+    // walk's kernels, which return at once unless the derived counts failed
+    // (device flag, no host round trip: XDRG_ASYNC and graph capture keep working)
+    const bool spec = rec_spec_ok(a, c->tune) && (!c->tune.big_rec || in_len / n < c->tune.big_rec);
+    a.spec = spec ? (uint32_t *)(c->d_stat + 1) : nullptr;   // word 1: ~0 = derived counts hold
+    a.spec_mode = spec ? (c->tune.spec_sizes == 2 ? 3 : 1) : 0;
+    a.lb_ticket = c->d_stat + 2;                              // word 2: one-pass block tickets
+    HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, spec ? 24 : 8, c->stream));
+    if (a.spec_mode == 3)   // the look-back status words (in the block sums' place)
+        HIPCHK(c, hipMemsetAsync(a.block_sums, 0, (size_t)a.ndyn * a.nblocks * 8, c->stream));
     for (int ph = REC_DEC_SIZES; ph <= REC_DEC_PLACE; ++ph) {
         TimedLaunch t(c, rec_dec_kernel_id(ph));
         HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->tune, c->stream));
+    }
+    if (spec && !async) {   // one round trip reads the error key and the spec word together
+        HIPCHK(c, hipMemcpyAsync(c->h_stat, c->d_stat, 16, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if ((uint32_t)c->h_stat[1] != 0)   // the derived counts held: the key is final
+            return finish_decode(c, n, c->h_stat[0], false, false, first_bad, err);
+        HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));   // the exact walk, from scratch
+        a.spec = nullptr;
+        a.spec_mode = 0;
+        for (int ph = REC_DEC_SIZES; ph <= REC_DEC_PLACE; ++ph) {
+            TimedLaunch t(c, rec_dec_kernel_id(ph), false);
+            HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->tune, c->stream));
+        }
+    } else if (spec) {   // XDRG_ASYNC: no host round trip, the rerun's kernels check the word
+        HIPCHK(c, (hipError_t)launch_spec_reset(a.spec, c->d_stat, c->stream));
+        a.spec_mode = 2;
+        for (int ph = REC_DEC_SIZES; ph <= REC_DEC_PLACE; ++ph) {   // (their time, not extra launches)
+            TimedLaunch t(c, rec_dec_kernel_id(ph), false);
+            HIPCHK(c, (hipError_t)launch_rec_phase(a, ph, c->tune, c->stream));
+        }
     }
     return finish_decode(c, n, kNoError, true, async, first_bad, err);
 }

@@ -141,6 +141,12 @@ struct RecArgs {
     uint32_t pay_fb;           // payk: XDR bytes before that field in a record (mark + fixed fields)
     uint64_t *pay_pos;         // payk: per record, stream offset of that field's length word
                                // (decode: ~0 = not to be written)
+    uint32_t *spec;            // decode, extent-derived counts (spec_mode != 0): ~0 = the derived
+                               // counts hold so far, 0 = a kernel found they do not (exact rerun)
+    uint32_t spec_mode;        // 0 off; 1 the derived-count pass (sizes, place verifying the count
+                               // words); 2 the exact rerun (its kernels return unless *spec == 0);
+                               // 3 the derived counts in one pass (k_dec_sweep walks and looks back)
+    unsigned long long *lb_ticket;   // spec_mode 3: block tickets in start order (starts at ~0)
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
     int32_t cvals[XDRG_MAX_CASES];  // case values of the conditional fields
@@ -192,6 +198,12 @@ struct Tuning {
                                     // (k_enc_iostage); the image leaves as whole 16-byte lines
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
+    int32_t spec_sizes = 1;         // key 31: sweep decode whose last dynamic field is a word vector
+                                    // followed by fixed fields only: 1 derive its counts from the record
+                                    // extents (sizes reads one length word per record, the place kernel
+                                    // verifies every count word, exact rerun on a mismatch), 2 the same
+                                    // in one pass (the sweep walks its block and looks back for its
+                                    // native offsets: no sizes or scan kernel), 0 walk all
 };
 int set_tuning(Tuning &t, int key, long long value);   // 0, or -1 for an unknown key / bad value
 
@@ -353,6 +365,10 @@ enum GroupPhase { GRP_ENC_SIZES, GRP_ENC_PLACE, GRP_DEC_WALK, GRP_DEC_OFFSETS, G
 int launch_group_phase(const GroupArgs &a, int phase, void *stream);
 // exclusive scan of `rows` rows of nblocks block sums each (k_scan_rows)
 int launch_scan_rows(uint64_t *sums, uint64_t nblocks, uint64_t *totals, uint32_t rows, void *stream);
+// extent-derived decode counts failed (*spec == 0): reset the error key for the exact rerun
+int launch_spec_reset(const uint32_t *spec, unsigned long long *errkey, void *stream);
+// Can this decode derive its last dynamic field's counts from the record extents?
+bool rec_spec_ok(const RecArgs &a, const Tuning &t);
 
 constexpr int kRecThreads = 256;   // record path: threads per block
 constexpr int kRecPerThread = 4;   // records per thread in the size/scan pass

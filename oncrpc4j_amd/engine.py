@@ -181,6 +181,11 @@ class Context:
             _raise(rc)
         self._h = h
         self.device = device
+        # measurement runs (rocprofv3 over bench.py) may force kernel choices:
+        # XDRG_TUNE="key=value,key=value" (see tune())
+        for kv in filter(None, os.environ.get("XDRG_TUNE", "").split(",")):
+            k, v = kv.split("=")
+            self.tune(int(k), int(v))
 
     @property
     def handle(self):

@@ -1,0 +1,94 @@
+"""Throughput of conditional tapes (rpcgen unions / optional data; DESIGN.md
+§8f2, §8f4) on two builder-designed shapes:
+
+* RELEASE: lease_cache.x RELEASE(lease_key, lease_state) argument batches,
+  4 Mi records (unsigned hyper, string<1024> of 8..64 B, an int union whose
+  arms are opaque<64> / unsigned int / void);
+* READDIRPLUS: plus_types.x `plus_res` replies (the reply union, optional
+  directory attributes, a verifier and a `plus_entry *next` list whose every
+  element carries an optional attribute union and an optional handle union),
+  512 Ki records of 0..12 entries.
+
+Device-resident, HIP-event timed encode and decode (median of reps); bytes =
+native + XDR per direction, as bench.py counts them; round trip checked."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from oncrpc4j_amd import abi, engine, rpcgen  # noqa: E402
+from oncrpc4j_amd.columns import DeviceBatch, random_batch  # noqa: E402
+
+LEASE = 0x2000F33E
+
+
+def timed(fn, reps=7):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return sorted(ts)[len(ts) // 2]
+
+
+def discriminants(fields, conds, hb, rng):
+    """Realistic arm mixes: bool discriminants 0/1, int discriminants drawn
+    from their case values plus one that takes the default arm."""
+    for k in sorted({d for _, d, _, _ in conds}):
+        rows = hb.arrays[k].shape[0]
+        if fields[k][0] == abi.T_BOOL:
+            hb.arrays[k][:] = rng.integers(0, 2, rows, dtype=np.uint8)
+        else:
+            vals = sorted({v for _, d, _, vs in conds if d == k for v in vs})
+            pool = np.array(vals + [max(vals) + 1], dtype=np.int64)
+            hb.arrays[k][:] = pool[rng.integers(0, pool.size, rows)].astype(hb.arrays[k].dtype)
+
+
+def run(name, fields, conds, n, dyn_len, group_len=(0, 4)):
+    ctx = engine.Context(0)
+    ctx.set_stream(torch.cuda.current_stream())
+    hb = random_batch(fields, n, seed=3, dyn_len=dyn_len, group_len=group_len, special_floats=False)
+    discriminants(fields, conds, hb, np.random.default_rng(3))
+    sch = engine.Schema(fields, conds)
+    db = DeviceBatch.from_host(hb)
+    cap = hb.xdr_total() + 64            # every field present: an upper bound
+    out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    ro = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    cols = db.columns()
+    total = ctx.encode(sch, cols, n, out, cap, rec_offsets=ro)
+    t_enc = timed(lambda: ctx.encode(sch, cols, n, out, cap, rec_offsets=ro))
+    back = DeviceBatch.empty(fields, n, hb.dyn_caps())
+    bcols = back.columns()
+    t_dec = timed(lambda: ctx.decode(sch, out, total, n, bcols, rec_offsets=ro))
+    ok = ctx.decode(sch, out, total, n, bcols, rec_offsets=ro) == (0, n, 0)
+    nat = hb.native_bytes()
+    per_dir = nat + total
+    return {"shape": name, "records": n, "xdr_bytes": total, "native_bytes": nat,
+            "encode_ms": round(t_enc, 3), "decode_ms": round(t_dec, 3),
+            "encode_GBps": round(per_dir / t_enc / 1e6, 1), "decode_GBps": round(per_dir / t_dec / 1e6, 1),
+            "frac_of_8TBps": round(2 * per_dir / (t_enc + t_dec) / 1e6 / 8000, 4),
+            "Mrec_s": round(2 * n / (t_enc + t_dec) / 1e3, 1), "roundtrip_ok": ok}
+
+
+def main():
+    g = os.path.join(ROOT, "tests", "golden", "rpcgen")
+    lease = rpcgen.parse_file(os.path.join(g, "lease_cache.x"))
+    f, c = lease.args_tape(LEASE, 1, 2)
+    print(json.dumps(run("RELEASE(lease_key, lease_state) args", f, c, 4 << 20, (8, 64))), flush=True)
+    plus = rpcgen.parse_file(os.path.join(g, "plus_types.x"))
+    f, c = plus.tape("plus_res")
+    print(json.dumps(run("READDIRPLUS plus_res replies", f, c, 512 << 10, (0, 40), (0, 12))), flush=True)
+
+
+if __name__ == "__main__":
+    main()
