@@ -236,12 +236,26 @@ __device__ void g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t 
     }
 }
 
-// One wavefront writes record r at stream byte pos.
-__device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint64_t size) {
-    const uint32_t lane = threadIdx.x & 63;
+// G lanes (a wave or a part of one: G divides 64) write record r at stream
+// byte pos; ln = the lane's index in its group.  Fixed-size elements go a lane
+// per element at computed positions, others a lane per element after a
+// G-lane scan of their sizes.  G = 64 kept a wave per record (round 2); most
+// records hold a handful of elements, so a wave of 16-lane groups writes four
+// records at once (tuning key 32).
+template <uint32_t G>
+__device__ __forceinline__ uint64_t g_incl_scan(uint64_t v, uint32_t ln) {
+#pragma unroll
+    for (uint32_t d = 1; d < G; d <<= 1) {
+        const uint64_t t = __shfl_up(v, d, G);
+        if (ln >= d) v += t;
+    }
+    return v;
+}
+template <uint32_t G>
+__device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint64_t size, uint32_t ln) {
     uint8_t *out = a.xdr;
     if (a.framed) {   // GrizzlyRpcTransport.java:103-110
-        if (lane == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
+        if (ln == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
         pos += 4;
     }
     GDisc d{};
@@ -255,42 +269,44 @@ __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint6
             uint64_t e0, cnt;
             g_range(f, r, e0, cnt);
             if (f.kind == XDRG_K_DYNAMIC) {   // xdrEncodeInt($size) (jrpcgen.java:866-876)
-                if (lane == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)cnt);
+                if (ln == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)cnt);
                 pos += 4;
             }
             if (!f.ndm && !f.ncm) {   // elements of one size: a lane per element
-                for (uint64_t i = lane; i < cnt; i += 64) g_enc_elem(a, k, e0 + i, pos + i * f.efix, d);
+                for (uint64_t i = ln; i < cnt; i += G) g_enc_elem(a, k, e0 + i, pos + i * f.efix, d);
                 pos += cnt * f.efix;
             } else {        // a lane per element at its scanned position
-                for (uint64_t b = 0; b < cnt; b += 64) {
-                    const uint64_t i = b + lane;
+                // (the group's lanes stay together: the scan's shuffles need all G)
+                for (uint64_t b = 0; b < cnt; b += G) {
+                    const uint64_t i = b + ln;
                     const uint64_t z = i < cnt ? g_elem_bytes(a, k, e0 + i, d) : 0;
-                    const uint64_t incl = wave_incl_scan(z);
+                    const uint64_t incl = g_incl_scan<G>(z, ln);
                     if (i < cnt) g_enc_elem(a, k, e0 + i, pos + incl - z, d);
-                    pos += __shfl(incl, 63, 64);
+                    pos += __shfl(incl, G - 1, G);
                 }
             }
             if (f.kind == XDRG_K_LIST) {   // xdrEncodeBoolean(false): the list ends
-                if (lane == 0) *(uint32_t *)(out + pos) = 0;
+                if (ln == 0) *(uint32_t *)(out + pos) = 0;
                 pos += 4;
             }
             k += 1 + f.nmem;
             continue;
         }
         if (f.kind != XDRG_K_DYNAMIC) {
-            for (uint32_t w = lane; w < f.xbytes >> 2; w += 64) *(uint32_t *)(out + pos + 4 * w) = g_fixed_word(f, r, w);
+            for (uint32_t w = ln; w < f.xbytes >> 2; w += G) *(uint32_t *)(out + pos + 4 * w) = g_fixed_word(f, r, w);
             pos += f.xbytes;
         } else {
             const uint64_t e0 = f.offsets[r], cnt = f.offsets[r + 1] - e0;
-            if (lane == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)cnt);
+            if (ln == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)cnt);
             const uint64_t nw = g_dyn_words(f, cnt);
-            for (uint64_t w = lane; w < nw; w += 64) *(uint32_t *)(out + pos + 4 + 4 * w) = g_dyn_word(f, e0, cnt, w);
+            for (uint64_t w = ln; w < nw; w += G) *(uint32_t *)(out + pos + 4 + 4 * w) = g_dyn_word(f, e0, cnt, w);
             pos += 4 + 4 * nw;
         }
         ++k;
     }
 }
 
+template <uint32_t G>
 __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a) {
     __shared__ uint64_t soff[kRecPerBlock + 1];
     const uint64_t total = a.totals[0];
@@ -315,8 +331,13 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a
     if (a.rec_out && blockIdx.x == 0 && threadIdx.x == 0) a.rec_out[a.n] = total;
     __syncthreads();
     const uint64_t nrec = a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock;
-    for (uint32_t j = threadIdx.x >> 6; j < nrec; j += kRecThreads / 64)
-        g_enc_record(a, rb + j, soff[j], soff[j + 1] - soff[j]);
+    // groups of G lanes take records in turn; a group past the end idles
+    // through its last rounds (uniform loop bound: the scans' shuffles)
+    const uint32_t ng = kRecThreads / G, ln = threadIdx.x & (G - 1);
+    for (uint32_t j0 = 0; j0 < nrec; j0 += ng) {
+        const uint32_t j = j0 + threadIdx.x / G;
+        if (j < nrec) g_enc_record<G>(a, rb + j, soff[j], soff[j + 1] - soff[j], ln);
+    }
 }
 
 // ===========================================================================
@@ -598,7 +619,13 @@ int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
     const dim3 grid((uint32_t)a.nblocks), block(kRecThreads);
     switch (phase) {
     case GRP_ENC_SIZES: hipLaunchKernelGGL(k_grp_enc_sizes, grid, block, 0, st, a); break;
-    case GRP_ENC_PLACE: hipLaunchKernelGGL(k_grp_enc_place, grid, block, 0, st, a); break;
+    case GRP_ENC_PLACE:   // G lanes per record (tuning key 32)
+        if (a.enc_lanes == 4) hipLaunchKernelGGL(k_grp_enc_place<4>, grid, block, 0, st, a);
+        else if (a.enc_lanes == 8) hipLaunchKernelGGL(k_grp_enc_place<8>, grid, block, 0, st, a);
+        else if (a.enc_lanes == 16) hipLaunchKernelGGL(k_grp_enc_place<16>, grid, block, 0, st, a);
+        else if (a.enc_lanes == 32) hipLaunchKernelGGL(k_grp_enc_place<32>, grid, block, 0, st, a);
+        else hipLaunchKernelGGL(k_grp_enc_place<64>, grid, block, 0, st, a);
+        break;
     case GRP_DEC_WALK: hipLaunchKernelGGL(k_grp_dec_walk, grid, block, 0, st, a); break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
     case GRP_DEC_PLACE:   // a lane per record

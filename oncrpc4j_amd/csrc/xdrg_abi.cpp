@@ -365,6 +365,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 29: if (!in(0, 1)) return -1; t.stride_check = (int32_t)v; return 0;
     case 30: if (!in(0, 1)) return -1; t.frame_bytes = (int32_t)v; return 0;
     case 31: if (!in(0, 2)) return -1; t.spec_sizes = (int32_t)v; return 0;
+    case 32: if (v != 64 && v != 32 && v != 16 && v != 8 && v != 4) return -1; t.grp_enc_lanes = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -716,6 +717,7 @@ static int group_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *co
     GroupArgs a;
     int rc = fill_group(c, s, cols, n, framed, false, a);
     if (rc) return rc;
+    a.enc_lanes = (uint32_t)c->tune.grp_enc_lanes;
     a.xdr = out;
     a.xdr_cap = out_cap;
     a.rec_out = rec_offsets;

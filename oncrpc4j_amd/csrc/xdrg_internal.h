@@ -198,7 +198,8 @@ struct Tuning {
                                     // (k_enc_iostage); the image leaves as whole 16-byte lines
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
-    int32_t spec_sizes = 1;         // key 31: sweep decode whose last dynamic field is a word vector
+    int32_t grp_enc_lanes = 8;      // key 32: repeated-group encode, lanes per record (64 = a wave)
+    int32_t spec_sizes = 2;         // key 31: sweep decode whose last dynamic field is a word vector
                                     // followed by fixed fields only: 1 derive its counts from the record
                                     // extents (sizes reads one length word per record, the place kernel
                                     // verifies every count word, exact rerun on a mismatch), 2 the same
@@ -342,7 +343,7 @@ struct GroupArgs {
     uint32_t nf;
     uint32_t framed;
     uint32_t nslot;
-    uint32_t rsv;
+    uint32_t enc_lanes;          // encode place: lanes per record (64, 16, 8; tuning key 32)
     uint8_t *xdr;
     uint64_t xdr_cap;            // encode: out_cap; decode: in_len
     const uint64_t *rec_in;      // decode: record extents (n+1)

@@ -81,9 +81,17 @@ def _mutations(want, offs, n, rng):
     return out
 
 
+@pytest.fixture(params=[8, 64, 4], ids=lambda g: f"enc{g}")
+def enc_lanes(request, gpu_ctx):
+    """Group encode place: lanes per record (tuning key 32)."""
+    gpu_ctx.tune(32, request.param)
+    yield request.param
+    gpu_ctx.tune(0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("b", FIX["batches"], ids=_ids)
-def test_gpu_plus_res_fixture(gpu_ctx, b):
+def test_gpu_plus_res_fixture(gpu_ctx, enc_lanes, b):
     import torch
     from oncrpc4j_amd import engine
     from oncrpc4j_amd.columns import DeviceBatch
@@ -126,7 +134,7 @@ def test_gpu_plus_res_errors_vs_oracle(gpu_ctx, seed):
 
 
 @pytest.mark.gpu
-def test_gpu_plus_res_random_vs_oracle(gpu_ctx):
+def test_gpu_plus_res_random_vs_oracle(gpu_ctx, enc_lanes):
     """A larger random batch of the same tape (shapes the fixture does not
     hold: long lists, every arm mix) through the engine and the oracle."""
     import torch

@@ -175,7 +175,7 @@ def gpu_decode(ctx, fields, xdr, n, offs, caps, framed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("b", BATCHES, ids=_ids)
-def test_gpu_group_fixture(gpu_ctx, b):
+def test_gpu_group_fixture(gpu_ctx, enc_lanes, b):
     fields = _fields(b)
     hb = gold.batch_from_records(fields, b["records"])
     xdr, offs = gpu_encode(gpu_ctx, fields, hb, b["framed"])
@@ -208,10 +208,19 @@ def _sane(hb):
     return hb
 
 
+@pytest.fixture(params=[8, 64, 4], ids=lambda g: f"enc{g}")
+def enc_lanes(request, gpu_ctx):
+    """Group encode place: lanes per record (tuning key 32; 8 the default,
+    64 a wave per record, 4 the smallest group)."""
+    gpu_ctx.tune(32, request.param)
+    yield request.param
+    gpu_ctx.tune(0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("shape", list(SHAPES), ids=list(SHAPES))
-def test_gpu_group_vs_oracle(gpu_ctx, shape, framed):
+def test_gpu_group_vs_oracle(gpu_ctx, enc_lanes, shape, framed):
     fields = SHAPES[shape]
     for n, glen in ((1, (0, 3)), (3000, (0, 9)), (20000, (0, 3)), (900, (60, 140))):
         hb = _sane(random_batch(fields, n, seed=n + len(shape), dyn_len=(0, 21), group_len=glen))

@@ -64,7 +64,7 @@ def _both(ctx, fields, xdr, n, ro, caps, framed):
             ctx.tune(31, m)
             gs.append(gpu_decode(ctx, fields, xdr, n, ro, caps, framed))
     finally:
-        ctx.tune(31, 1)
+        ctx.tune(31, 2)   # the default
     return o, gs, None
 
 
