@@ -265,7 +265,7 @@ class Workload:
             del size
             self.rec_offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
             self.native_bytes = n * 4 * nh + sum(x[0].numel() * x[0].element_size() for x in self.dyn)
-            self.kernels = ("k_enc_place/k_dec_place (+payload)" if cfg == 3 else "k_enc_stage/k_dec_sweep",
+            self.kernels = ("k_enc_place/k_dec_place (+payload)" if cfg == 3 else "k_enc_stage_rm/k_dec_sweep",
                             abi.KERNEL_VAR_ENCODE, abi.KERNEL_VAR_DECODE)
             self.desc = ("configs[2]: 16 Mi NFS-WRITE-shaped records, 6 x int32 + opaque<4096>"
                          if cfg == 3 else

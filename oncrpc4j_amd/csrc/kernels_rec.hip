@@ -934,6 +934,7 @@ __device__ __forceinline__ void win_fix(Chunk5 &q, const Span &s, const uint8_t 
 __device__ __forceinline__ const uint8_t *blob_win(const uint8_t *src, uint64_t c) {
     return src - ((uintptr_t)src & 3) + 16 * c - 4;
 }
+template <bool NT = false>
 __device__ __forceinline__ void blob_store(uint8_t *dst, const Chunk5 &q, uint32_t sh, uint64_t c, uint64_t cnt) {
     const uint64_t nwb = 1 + ((cnt + 3) >> 2);
     uint32_t o0 = sh ? __builtin_amdgcn_alignbyte(q.q1, q.q0, sh) : q.q0;
@@ -949,7 +950,8 @@ __device__ __forceinline__ void blob_store(uint8_t *dst, const Chunk5 &q, uint32
     uint8_t *d = dst + 16 * c;
     if (4 * c + 4 <= nwb) {
         u32x4a o; o.x = o0; o.y = o1; o.z = o2; o.w = o3;
-        *(u32x4a *)d = o;
+        if (NT) __builtin_nontemporal_store(o, (u32x4a *)d);
+        else *(u32x4a *)d = o;
     } else {
         const uint64_t left = nwb - 4 * c;
         *(uint32_t *)d = o0;
@@ -996,6 +998,7 @@ __device__ __forceinline__ void enc_blob_bytes(uint8_t *const (&dst)[R], const u
 // int/uint/enum/float vector as one blob: [BE count][BE elements...]; blob
 // word b is element b - 1 of the 4-aligned native run src, so chunk c
 // reads the words at src + 16c - 4.
+template <bool NT = false>
 __device__ __forceinline__ void w4_store(uint8_t *dst, const Chunk5 &q, uint64_t c, uint64_t cnt, bool fl) {
     const uint64_t nwb = 1 + cnt;
     uint32_t o[4] = {q.q0, q.q1, q.q2, q.q3};
@@ -1005,7 +1008,8 @@ __device__ __forceinline__ void w4_store(uint8_t *dst, const Chunk5 &q, uint64_t
     uint32_t *d = (uint32_t *)(dst + 16 * c);
     if (4 * c + 4 <= nwb) {
         u32x4a ov; ov.x = o[0]; ov.y = o[1]; ov.z = o[2]; ov.w = o[3];
-        *(u32x4a *)d = ov;
+        if (NT) __builtin_nontemporal_store(ov, (u32x4a *)d);
+        else *(u32x4a *)d = ov;
     } else {
         for (uint64_t j = 0; 4 * c + j < nwb; ++j) d[j] = o[j];
     }
@@ -2119,10 +2123,13 @@ __device__ __forceinline__ void enc_flush(const uint8_t *img, uint8_t *A0, uint3
 
 // MODE 0: input-staged (k_enc_stage); 1: output-imaged, inputs straight from
 // HBM (k_enc_ostage); 2: both tiles — inputs staged, output composed in an
-// LDS image, whole lines out (k_enc_iostage).
+// LDS image, whole lines out (k_enc_iostage); 3: MODE 0 with nontemporal
+// 16-byte scatter stores (k_enc_stage_nt, tuning key 27 = 3).
 template <int MODE>
 __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
     constexpr bool OUT = MODE == 1;
+    constexpr bool NT = MODE == 3;
+    constexpr bool RM = MODE == 4;   // record-major scatter (k_enc_stage_rm, tuning key 27 = 4)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;   // row stride of soff / srel
     uint32_t *soff = (uint32_t *)smem;
@@ -2259,11 +2266,61 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
         }
         stage_copy(tile, a0, cb, a.ndyn);   // (stage_dma measured 3.70 vs 3.62 ms here: nothing to overlap)
         __syncthreads();
+        const uint32_t m = je - js;
+        if (RM) {   // MODE 4: record-major scatter, a group of lanes writes all of a record
+            const uint64_t rbytes = (uint64_t)(soff[je] - soff[js]) / m;
+            const uint32_t G = a.force_g ? a.force_g : pow2_lanes(rbytes, a.lane_bytes_enc);
+            const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
+            for (uint32_t j = js + tid / G; j < je; j += ng) {
+                uint8_t *rec = wout + soff[j];
+                uint32_t fpre = a.framed ? 4 : 0, d = 0;
+                uint64_t dynb = 0;   // XDR bytes of the record's dynamic fields so far
+                for (uint32_t k = 0; k < a.nf; ++k) {
+                    const VField &f = a.f[k];
+                    if (f.kind != XDRG_K_DYNAMIC) {
+                        const uint32_t nw = f.xbytes >> 2;
+                        uint8_t *dst = rec + fpre + dynb;
+                        for (uint32_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
+                        fpre += f.xbytes;
+                        continue;
+                    }
+                    const bool bytes = f.xsz == 1;
+                    const uint64_t esz = bytes ? 1 : f.nsz;
+                    const uint32_t *rel = srel + d * RS;
+                    const uint64_t cnt = rel[j + 1] - rel[j];
+                    const uint8_t *p = f.data + (base[d] + rel[j]) * esz;
+                    uint8_t *dst = rec + fpre + dynb;
+                    const int64_t L = 16 * (int64_t)cb[d] - (int64_t)(uintptr_t)a0[d] + (int64_t)(uintptr_t)p;
+                    if (bytes) {
+                        const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+                        const uint64_t nch = (1 + ((cnt + 3) >> 2) + 3) >> 2;
+                        for (uint64_t c = gl; c < nch; c += G) {
+                            const uint32_t *w = (const uint32_t *)(tile + (L - sh + 16 * (int64_t)c - 4));
+                            Chunk5 q;
+                            q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = w[4];
+                            blob_store(dst, q, sh, c, cnt);
+                        }
+                    } else {
+                        const uint64_t nch = (1 + cnt + 3) >> 2;
+                        for (uint64_t c = gl; c < nch; c += G) {
+                            const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c - 4));
+                            Chunk5 q;
+                            q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = 0;
+                            w4_store(dst, q, c, cnt, f.type == XDRG_T_FLOAT);
+                        }
+                    }
+                    dynb += dyn_xdr_bytes(f, cnt);
+                    ++d;
+                }
+            }
+            js = je;
+            k1 = js < nrec ? enc_fit(a, base, srel, js, nrec) : 0;   // its barrier ends the tiles' use
+            continue;
+        }
         // scatter, field-major; field k of record j sits at
         // soff[j] + (fixed bytes before k) + (dynamic bytes before k)
         uint32_t fpre = a.framed ? 4 : 0;
         uint32_t d = 0;
-        const uint32_t m = je - js;
         for (uint32_t k = 0; k < a.nf; ++k) {
             const VField &f = a.f[k];
             if (f.kind != XDRG_K_DYNAMIC) {
@@ -2300,7 +2357,7 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
                         const uint32_t *w = (const uint32_t *)(tile + (L - sh + 16 * (int64_t)c - 4));
                         Chunk5 q;
                         q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = w[4];
-                        blob_store(dst, q, sh, c, cnt);
+                        blob_store<NT>(dst, q, sh, c, cnt);
                     }
                 } else {
                     const uint64_t nch = (1 + cnt + 3) >> 2;
@@ -2308,7 +2365,7 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
                         const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c - 4));
                         Chunk5 q;
                         q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = 0;
-                        w4_store(dst, q, c, cnt, fl);
+                        w4_store<NT>(dst, q, c, cnt, fl);
                     }
                 }
             }
@@ -2325,6 +2382,8 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
 __global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) { k_enc_stage_t<0>(a); }
 __global__ __launch_bounds__(kRecThreads) void k_enc_ostage(const RecArgs a) { k_enc_stage_t<1>(a); }
 __global__ __launch_bounds__(kRecThreads) void k_enc_iostage(const RecArgs a) { k_enc_stage_t<2>(a); }
+__global__ __launch_bounds__(kRecThreads) void k_enc_stage_nt(const RecArgs a) { k_enc_stage_t<3>(a); }
+__global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) { k_enc_stage_t<4>(a); }
 
 // ---- decode -------------------------------------------------------------------
 // LDS: sstart[RPB + 1] u32 (record start - the block's first start) | snrel[ND][RPB + 1] u32 |
@@ -3225,7 +3284,13 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     case REC_ENC_PLACE:
         if (stage) {   // small-record blocks staged, large-record blocks by the group kernel
             a.big_rec = t.big_rec;
-            if (t.enc_out == 2)   // staged inputs, output image (tuning key 27)
+            if (t.enc_out == 4)   // input-staged, record-major scatter (tuning key 27)
+                hipLaunchKernelGGL(k_enc_stage_rm, dim3(nb), dim3(kRecThreads),
+                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            else if (t.enc_out == 3)   // input-staged, nontemporal scatter stores (tuning key 27)
+                hipLaunchKernelGGL(k_enc_stage_nt, dim3(nb), dim3(kRecThreads),
+                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            else if (t.enc_out == 2)   // staged inputs, output image (tuning key 27)
                 hipLaunchKernelGGL(k_enc_iostage, dim3(nb), dim3(kRecThreads),
                                    enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack + a.tile_bytes +
                                        (a.tile_bytes >> 3) + 32, st, a);

@@ -360,7 +360,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 24: if (!in(0, 1)) return -1; t.pay_hoist = (int32_t)v; return 0;
     case 25: if (!in(1024, 32768) || (v & 15)) return -1; t.sweep_tile = (uint32_t)v; return 0;
     case 26: if (!in(0, 1)) return -1; t.stage_copy = (int32_t)v; return 0;
-    case 27: if (!in(0, 2)) return -1; t.enc_out = (int32_t)v; return 0;
+    case 27: if (!in(0, 4)) return -1; t.enc_out = (int32_t)v; return 0;
     case 28: if (!in(0, 1)) return -1; t.pay_nts = (int32_t)v; return 0;
     case 29: if (!in(0, 1)) return -1; t.stride_check = (int32_t)v; return 0;
     case 30: if (!in(0, 1)) return -1; t.frame_bytes = (int32_t)v; return 0;

@@ -182,7 +182,8 @@ struct Tuning {
     int32_t enc_u = 2, dec_u = 2;   // keys 4/5: group kernels, 16-byte chunks per lane in flight
     int32_t enc_r = 1, dec_r = 1;   // keys 10/11: group kernels, records per lane in flight
     uint32_t force_g = 0;           // key 6: lanes per record (0 = sized from the field)
-    uint32_t lane_bytes_enc = 32;   // keys 7/8: group sizing, XDR bytes per lane
+    uint32_t lane_bytes_enc = 64;   // keys 7/8: group sizing, XDR bytes per lane (encode 64: the
+                                    // record-major staged encode's 4 lanes per config-4 record)
     uint32_t lane_bytes_dec = 32;
     uint32_t tile_bytes = 16384;    // key 12: staged kernels, LDS tile per sub-batch
     uint32_t sweep_tile = 21504;    // key 25: the sweep decode's LDS tile (k_dec_sweep, 4 blocks per CU)
@@ -193,9 +194,11 @@ struct Tuning {
     int32_t stride_check = 1;       // key 29: fixed-size decode at rec_offsets: 1 check for the fixed
                                     // stride and take the stride kernels (sync calls), 0 the record path
     int32_t pay_nts = 1;            // key 28: encode payload kernel: 1 nontemporal 16-byte stores, 0 plain
-    int32_t enc_out = 0;            // key 27: staged encode: 0 input-staged (k_enc_stage), 1 output image
+    int32_t enc_out = 4;            // key 27: staged encode: 4 input-staged, record-major scatter
+                                    // (k_enc_stage_rm: a record's bytes written together, lines whole
+                                    // in L2), 0 input-staged field-major (k_enc_stage), 1 output image
                                     // composed from HBM (k_enc_ostage), 2 input-staged + output image
-                                    // (k_enc_iostage); the image leaves as whole 16-byte lines
+                                    // (k_enc_iostage), 3 field-major with nontemporal stores
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
     int32_t grp_enc_lanes = 8;      // key 32: repeated-group encode, lanes per record (64 = a wave)

@@ -52,6 +52,8 @@ REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),),
                "staged_lean": ((9, 4), (20, 1)),
                "staged_out": ((9, 4), (27, 1)),    # output image from HBM inputs (k_enc_ostage)
                "staged_io": ((9, 4), (27, 2)),     # staged inputs + output image (k_enc_iostage)
+               "staged_nt": ((9, 4), (27, 3)),     # staged inputs, nontemporal scatter stores
+               "staged_fm": ((9, 4), (27, 0), (7, 32)),   # staged inputs, field-major scatter
                "staged_2pass": ((9, 4), (31, 1)),  # derived counts by the sizes pass (default: one pass)
                "staged_walk": ((9, 4), (31, 0))}   # every count word walked (no derived counts)
 

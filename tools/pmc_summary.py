@@ -40,24 +40,28 @@ CONFIGS = {
     "2f": (67108864, [("k_stream_framed_enc_lean", "150994944")], [("k_stream_framed_dec_lean", "134217728")]),
     "3": (16777216, [("k_enc_place_g", "4194304"), ("k_enc_payload", "1073741824")],
           [("k_dec_place_g", "4194304"), ("k_dec_payload", "1073741824")]),
-    "4": (33554432, [("k_enc_ostage|k_enc_stage", "8388608"), ("k_enc_place_g", "8388608")],
-          [("k_dec_sweep|k_dec_stage", "8388608"), ("k_dec_place_g", "8388608")]),
-    "4f": (33554432, [("k_enc_ostage|k_enc_stage", "8388608"), ("k_enc_place_g", "8388608")],
-           [("k_dec_sweep|k_dec_stage", "8388608"), ("k_dec_place_g", "8388608")]),
+    "4": (33554432, [("k_enc_stage_rm|k_enc_ostage|k_enc_stage", "8388608"), ("k_enc_place_g?", "8388608")],
+          [("k_dec_sweep|k_dec_stage", "8388608"), ("k_dec_place_g?", "8388608")]),
+    "4f": (33554432, [("k_enc_stage_rm|k_enc_ostage|k_enc_stage", "8388608"), ("k_enc_place_g?", "8388608")],
+           [("k_dec_sweep|k_dec_stage", "8388608"), ("k_dec_place_g?", "8388608")]),
 }
 # (a name "a|b" takes the first of the alternatives the profile holds: the
-# staged kernels' sweep variants replace them when the tuning selects them)
+# staged kernels' variants replace them when the tuning selects them; a name
+# ending in "?" is dropped when the profile does not hold it: the one-pass
+# derived-count decode launches no group kernel for big-record blocks)
 
 
 def resolve(ks, table):
     out = []
     for name, grid in ks:
-        for alt in name.split("|"):
+        opt = name.endswith("?")
+        for alt in name.rstrip("?").split("|"):
             if (alt, grid) in table:
                 out.append((alt, grid))
                 break
         else:
-            out.append((name, grid))
+            if not opt:
+                out.append((name, grid))
     return out
 
 
