@@ -26,6 +26,7 @@
 namespace xdrg {
 
 typedef uint32_t u32g __attribute__((aligned(1)));
+typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));   // 16-byte aligned
 
 __device__ __forceinline__ uint64_t g_dyn_bytes(const GField &f, uint64_t cnt) {
     return 4 + (f.xsz == 1 ? cnt + pad4(cnt) : cnt * f.xsz);
@@ -86,6 +87,32 @@ __device__ __forceinline__ void g_dyn_store(const GField &f, uint64_t e0, uint64
     }
     if (f.xsz == 8) dec_elem(f.type, f.data + (e0 + (w >> 1)) * 8, (uint32_t)(w & 1), v);
     else dec_elem(f.type, f.data + (e0 + w) * f.nsz, 0, v);
+}
+// len payload bytes from the 4-aligned src (stream or LDS tile) to dst at any
+// alignment: byte stores only for the head and tail of the destination,
+// aligned dwords composed from two source words in between (g_dyn_store
+// stored a byte-aligned dword per word, which the compiler splits into bytes).
+__device__ __forceinline__ void g_dec_bytes(uint8_t *dst, const uint8_t *src, uint64_t len) {
+    const uint32_t sh = (uint32_t)((uintptr_t)dst & 3);
+    const uint32_t head = (4 - sh) & 3;   // bytes before dst's first aligned dword
+    const uint32_t hb = head < len ? head : (uint32_t)len;
+    if (hb) {
+        const uint32_t w0 = *(const uint32_t *)src;
+        for (uint32_t b = 0; b < hb; ++b) dst[b] = (uint8_t)(w0 >> (8 * b));
+    }
+    if (len <= head) return;
+    const uint64_t body = (len - head) >> 2;   // whole aligned dwords
+    uint32_t *da = (uint32_t *)(dst + head);
+    const uint32_t *sw = (const uint32_t *)src;
+    for (uint64_t k = 0; k < body; ++k) {   // source bytes [head + 4k, head + 4k + 4)
+        const uint32_t lo = sw[k], hi = head ? sw[k + 1] : 0u;
+        da[k] = head ? __builtin_amdgcn_alignbyte(hi, lo, head) : lo;
+    }
+    const uint64_t t0 = head + 4 * body;
+    for (uint64_t b = t0; b < len; ++b) {   // tail bytes
+        const uint32_t w = sw[b >> 2];
+        dst[b] = (uint8_t)(w >> (8 * (b & 3)));
+    }
 }
 __device__ __forceinline__ uint64_t g_dyn_words(const GField &f, uint64_t cnt) {
     return f.xsz == 1 ? (cnt + 3) >> 2 : cnt * (f.xsz >> 2);
@@ -531,8 +558,9 @@ __device__ __forceinline__ void g_zero_fixed(const GField &f, uint64_t i) {
     for (uint64_t b = 0; b < nb; ++b) p[b] = 0;
 }
 
-__device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
-    const uint8_t *in = a.xdr;
+// in: where stream offset x is read, in + x (the stream, or an LDS tile
+// holding this record's bytes: k_grp_dec_place_lds).
+__device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in) {
     const uint64_t end = a.rec_in[r + 1];
     uint64_t pos = a.rec_in[r] + (a.framed ? 4 : 0);
     GDisc d{};
@@ -564,17 +592,31 @@ __device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
             const uint64_t e0 = f.kind == XDRG_K_FIXED ? r * f.count : a.rec_base[(uint64_t)(f.slot - 1) * a.n + r];
             const uint64_t cnt = f.kind == XDRG_K_FIXED ? f.count : a.rec_cnt[(uint64_t)(f.slot - 1) * a.n + r];
             if (f.kind == XDRG_K_DYNAMIC) pos += 4;
+            // each dynamic member's running native offset, in registers (slot-indexed
+            // selects): reading back the offsets just stored made every element wait
+            // for the previous one's store (READDIR decode 9.5 -> see DESIGN.md §5.7)
+            uint64_t run[kMaxSlots];
+#pragma unroll
+            for (int q = 0; q < kMaxSlots; ++q) run[q] = 0;
             for (uint32_t j = 1; j <= f.nmem; ++j) {   // each dynamic member's first value
                 const GField &m = a.f[k + j];
-                if (m.kind == XDRG_K_DYNAMIC) m.offsets[e0] = a.rec_base[(uint64_t)(m.slot - 1) * a.n + r];
+                if (m.kind != XDRG_K_DYNAMIC) continue;
+                const uint64_t b0 = a.rec_base[(uint64_t)(m.slot - 1) * a.n + r];
+                m.offsets[e0] = b0;
+#pragma unroll
+                for (int q = 0; q < kMaxSlots; ++q) run[q] = (uint32_t)q == m.slot - 1 ? b0 : run[q];
             }
             for (uint64_t e = e0; e < e0 + cnt; ++e) {
                 if (f.kind == XDRG_K_LIST) pos += 4;   // its TRUE
                 for (uint32_t j = 1; j <= f.nmem; ++j) {
                     const GField &m = a.f[k + j];
+                    uint64_t v0 = 0;
+                    if (m.kind == XDRG_K_DYNAMIC)
+#pragma unroll
+                        for (int q = 0; q < kMaxSlots; ++q) v0 = (uint32_t)q == m.slot - 1 ? run[q] : v0;
                     if (f.ncm && !g_dec_field_present(a, k + j, in, pos, end, d)) {   // an element's absent arm
                         if (m.kind != XDRG_K_DYNAMIC) g_zero_fixed(m, e);
-                        else m.offsets[e + 1] = m.offsets[e];
+                        else m.offsets[e + 1] = v0;
                         continue;
                     }
                     if (m.kind != XDRG_K_DYNAMIC) {
@@ -583,10 +625,12 @@ __device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
                         continue;
                     }
                     const uint64_t len = g_ld(in + pos);
-                    const uint64_t v0 = m.offsets[e];   // written for the element before (or above)
                     m.offsets[e + 1] = v0 + len;
+#pragma unroll
+                    for (int q = 0; q < kMaxSlots; ++q) run[q] = (uint32_t)q == m.slot - 1 ? v0 + len : run[q];
                     const uint64_t nw = g_dyn_words(m, len);
-                    for (uint64_t w = 0; w < nw; ++w) g_dyn_store(m, v0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
+                    if (m.xsz == 1) g_dec_bytes(m.data + v0, in + pos + 4, len);
+                    else for (uint64_t w = 0; w < nw; ++w) g_dyn_store(m, v0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
                     pos += 4 + 4 * nw;
                 }
             }
@@ -601,7 +645,8 @@ __device__ void g_dec_record(const GroupArgs &a, uint64_t r) {
             const uint64_t len = g_ld(in + pos);
             const uint64_t e0 = a.rec_base[(uint64_t)(f.slot - 1) * a.n + r];
             const uint64_t nw = g_dyn_words(f, len);
-            for (uint64_t w = 0; w < nw; ++w) g_dyn_store(f, e0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
+            if (f.xsz == 1) g_dec_bytes(f.data + e0, in + pos + 4, len);
+            else for (uint64_t w = 0; w < nw; ++w) g_dyn_store(f, e0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
             pos += 4 + 4 * nw;
         }
         ++k;
@@ -612,7 +657,51 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place(const GroupArgs a
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
     const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
     const uint64_t r = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x;
-    if (r < bad) g_dec_record(a, r);
+    if (r < bad) g_dec_record(a, r, a.xdr);
+}
+
+// Staged place (tuning key 33): the block's records go through an LDS tile in
+// sub-batches [js, je) whose stream bytes fit it (16-byte aligned, coalesced
+// 16-B loads), and each lane decodes its record from the tile: the walk's
+// dependent length words and list bools become LDS reads instead of HBM
+// round trips.  A record larger than the tile decodes from HBM.
+__global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
+    const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecThreads;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t lim = bad < a.n ? bad : a.n;
+    const uint32_t nlive = lim > rb ? (uint32_t)(lim - rb < (uint64_t)kRecThreads ? lim - rb : (uint64_t)kRecThreads) : 0u;
+    const uintptr_t xb = (uintptr_t)a.xdr;
+    uint32_t js = 0;
+    while (js < nlive) {
+        // records [js, js + 1 + tid) fit iff their aligned byte range does (monotone)
+        const uint32_t je1 = js + 1 + tid;
+        bool fits = false;
+        if (je1 <= nlive) {
+            const uintptr_t lo = (xb + a.rec_in[rb + js]) & ~(uintptr_t)15;
+            const uintptr_t hi = (xb + a.rec_in[rb + je1] + 15) & ~(uintptr_t)15;
+            fits = hi - lo <= a.dec_tile;
+        }
+        const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
+        if (k1 == 0) {   // one record larger than the tile: its lane decodes from HBM
+            if (tid == 0) g_dec_record(a, rb + js, a.xdr);
+            ++js;
+            continue;
+        }
+        const uint32_t je = js + k1;
+        const uintptr_t a0 = (xb + a.rec_in[rb + js]) & ~(uintptr_t)15;
+        const uint32_t nch = (uint32_t)((((xb + a.rec_in[rb + je] + 15) & ~(uintptr_t)15) - a0) >> 4);
+        for (uint32_t i = tid; i < nch; i += kRecThreads)
+            *(u32x4g *)(tile + 16 * (size_t)i) = __builtin_nontemporal_load((const u32x4g *)(a0 + 16 * (uintptr_t)i));
+        __syncthreads();
+        // stream offset x of these records is at tile + (xb + x - a0)
+        const uint8_t *in = tile + (uint32_t)(xb - a0);
+        if (js + tid < je) g_dec_record(a, rb + js + tid, in);
+        __syncthreads();   // the tile's next use
+        js = je;
+    }
 }
 
 int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
@@ -629,8 +718,12 @@ int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
         break;
     case GRP_DEC_WALK: hipLaunchKernelGGL(k_grp_dec_walk, grid, block, 0, st, a); break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
-    case GRP_DEC_PLACE:   // a lane per record
-        hipLaunchKernelGGL(k_grp_dec_place, dim3((uint32_t)((a.n + kRecThreads - 1) / kRecThreads)), block, 0, st, a);
+    case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
+        if (a.dec_tile)
+            hipLaunchKernelGGL(k_grp_dec_place_lds, dim3((uint32_t)((a.n + kRecThreads - 1) / kRecThreads)), block,
+                               a.dec_tile, st, a);
+        else
+            hipLaunchKernelGGL(k_grp_dec_place, dim3((uint32_t)((a.n + kRecThreads - 1) / kRecThreads)), block, 0, st, a);
         break;
     default: return (int)hipErrorInvalidValue;
     }

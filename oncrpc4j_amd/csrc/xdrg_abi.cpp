@@ -366,6 +366,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 30: if (!in(0, 1)) return -1; t.frame_bytes = (int32_t)v; return 0;
     case 31: if (!in(0, 2)) return -1; t.spec_sizes = (int32_t)v; return 0;
     case 32: if (v != 64 && v != 32 && v != 16 && v != 8 && v != 4) return -1; t.grp_enc_lanes = (int32_t)v; return 0;
+    case 33: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.grp_dec_tile = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -958,6 +959,7 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         GroupArgs a;
         rc = fill_group(c, s, cols, n, framed, true, a);
         if (rc) return rc;
+        a.dec_tile = (uint32_t)c->tune.grp_dec_tile;
         if (n == 0) {
             for (uint32_t q = 0; q < a.nslot; ++q)
                 if (!a.f[a.slot_field[q]].grp) HIPCHK(c, hipMemsetAsync(cols[a.slot_field[q]].offsets, 0, 8, c->stream));

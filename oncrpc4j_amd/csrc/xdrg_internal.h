@@ -201,6 +201,8 @@ struct Tuning {
                                     // (k_enc_iostage), 3 field-major with nontemporal stores
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
+    int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of
+                                    // records (0: each lane walks its record in HBM)
     int32_t grp_enc_lanes = 8;      // key 32: repeated-group encode, lanes per record (64 = a wave)
     int32_t spec_sizes = 2;         // key 31: sweep decode whose last dynamic field is a word vector
                                     // followed by fixed fields only: 1 derive its counts from the record
@@ -360,7 +362,7 @@ struct GroupArgs {
     unsigned long long *errkey;
     uint32_t slot_field[kMaxSlots];
     uint32_t ncond;              // conditional fields (0: every record / element has all of them)
-    uint32_t rsv2;
+    uint32_t dec_tile;           // decode place: LDS tile bytes (0: records read from HBM; key 33)
     int32_t cvals[XDRG_MAX_CASES];
     GField f[kMaxFields];
 };

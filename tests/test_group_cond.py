@@ -81,10 +81,14 @@ def _mutations(want, offs, n, rng):
     return out
 
 
-@pytest.fixture(params=[8, 64, 4], ids=lambda g: f"enc{g}")
+@pytest.fixture(params=[(8, 32768), (64, 0), (4, 1024)], ids=lambda p: f"enc{p[0]}-dtile{p[1]}")
 def enc_lanes(request, gpu_ctx):
-    """Group encode place: lanes per record (tuning key 32)."""
-    gpu_ctx.tune(32, request.param)
+    """Group kernels under each production choice: encode place lanes per
+    record (tuning key 32; 8 the default, 64 a wave per record) and decode
+    place LDS tile (key 33; 32 KiB the default, 0 records read from HBM,
+    1 KiB: most records larger than the tile take the HBM path)."""
+    gpu_ctx.tune(32, request.param[0])
+    gpu_ctx.tune(33, request.param[1])
     yield request.param
     gpu_ctx.tune(0)
 
@@ -110,7 +114,7 @@ def test_gpu_plus_res_fixture(gpu_ctx, enc_lanes, b):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_gpu_plus_res_errors_vs_oracle(gpu_ctx, seed):
+def test_gpu_plus_res_errors_vs_oracle(gpu_ctx, enc_lanes, seed):
     """Streams with errors inside list elements and changed discriminants:
     the engine's first bad record, code and the records before it equal the
     oracle's."""

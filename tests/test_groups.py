@@ -208,11 +208,14 @@ def _sane(hb):
     return hb
 
 
-@pytest.fixture(params=[8, 64, 4], ids=lambda g: f"enc{g}")
+@pytest.fixture(params=[(8, 32768), (64, 0), (4, 1024)], ids=lambda p: f"enc{p[0]}-dtile{p[1]}")
 def enc_lanes(request, gpu_ctx):
-    """Group encode place: lanes per record (tuning key 32; 8 the default,
-    64 a wave per record, 4 the smallest group)."""
-    gpu_ctx.tune(32, request.param)
+    """Group kernels under each production choice: encode place lanes per
+    record (tuning key 32; 8 the default, 64 a wave per record) and decode
+    place LDS tile (key 33; 32 KiB the default, 0 records read from HBM,
+    1 KiB: most records larger than the tile take the HBM path)."""
+    gpu_ctx.tune(32, request.param[0])
+    gpu_ctx.tune(33, request.param[1])
     yield request.param
     gpu_ctx.tune(0)
 
@@ -248,7 +251,7 @@ def _corrupt_cases():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", _corrupt_cases(), ids=lambda c: c[0])
-def test_gpu_group_errors_first_bad(gpu_ctx, case):
+def test_gpu_group_errors_first_bad(gpu_ctx, enc_lanes, case):
     """Every record is its own message; one broken record in the middle: the
     engine reports the oracle's (first_bad, code) and decodes every record
     before it."""
@@ -272,7 +275,7 @@ def test_gpu_group_errors_first_bad(gpu_ctx, case):
 
 
 @pytest.mark.gpu
-def test_gpu_group_capacity(gpu_ctx):
+def test_gpu_group_capacity(gpu_ctx, enc_lanes):
     fields = ITEMS
     hb = random_batch(fields, 500, seed=3, dyn_len=(0, 9), group_len=(0, 5))
     rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), hb.n, hb.xdr_total(False))
