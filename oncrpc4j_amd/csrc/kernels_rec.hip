@@ -2228,7 +2228,7 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
     const uint32_t mis = (uint32_t)((uintptr_t)out & 15);
     const uint32_t ocap = a.tile_bytes + (a.tile_bytes >> 3);   // the output image (MODE 2)
     uint8_t *const img = tile + a.tile_bytes + kStageSlack;
-    if (a.framed && !IMG)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
+    if (a.framed && !IMG && !RM)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
         for (uint32_t j = tid; j < nrec; j += kRecThreads)
             *(uint32_t *)(out + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
     // ---- sub-batches
@@ -2236,7 +2236,7 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
     uint32_t k1 = enc_fit(a, base, srel, js, nrec, IMG ? soff : nullptr, mis, ocap);
     while (js < nrec) {
         if (k1 == 0) {   // too large for the tile: the whole block writes record js
-            if (IMG && a.framed && tid == 0)
+            if ((IMG || RM) && a.framed && tid == 0)
                 *(uint32_t *)(out + soff[js]) = bswap32r((soff[js + 1] - soff[js] - 4) | kLastFrag);
             enc_record_block(a, rb + js, bbase + soff[js]);
             ++js;
@@ -2274,6 +2274,8 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
             for (uint32_t j = js + tid / G; j < je; j += ng) {
                 uint8_t *rec = wout + soff[j];
                 uint32_t fpre = a.framed ? 4 : 0, d = 0;
+                if (a.framed && gl == 0)   // the record's mark with its bytes (GrizzlyRpcTransport:103-110)
+                    *(uint32_t *)rec = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
                 uint64_t dynb = 0;   // XDR bytes of the record's dynamic fields so far
                 for (uint32_t k = 0; k < a.nf; ++k) {
                     const VField &f = a.f[k];
