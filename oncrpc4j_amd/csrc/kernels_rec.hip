@@ -3276,7 +3276,10 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     // its kernels return at once for a few microseconds each
     const dim3 dgrid((unsigned)(a.spec_mode == 2 && nb > 1024 ? 1024 : nb));
     const uint64_t pblk = (a.n + 3) / 4;   // a wave per record, 4 records per block
-    const dim3 pgrid((unsigned)(pblk < (1u << 22) ? pblk : (1u << 22)));
+    // (tuning key 34: a smaller grid whose blocks stride over the records,
+    // the resident blocks always on neighbouring records; 0 = a block per 4)
+    const uint64_t pcap = t.pay_grid ? (uint64_t)t.pay_grid : (1ull << 22);
+    const dim3 pgrid((unsigned)(pblk < pcap ? pblk : pcap));
     switch (phase) {
     case REC_ENC_SIZES: hipLaunchKernelGGL(k_enc_sizes, dim3(nb), dim3(kRecThreads), 0, st, a); break;
     case REC_ENC_SCAN:
