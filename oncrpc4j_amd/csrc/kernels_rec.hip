@@ -1784,6 +1784,55 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_lane(const RecArgs a) {
     }
 }
 
+// Lane j of the block decodes record r = rb + j from src (its first field's
+// bytes: in the stream, or in the LDS tile of k_dec_lane<TILE>), fields [0, upto).
+__device__ __forceinline__ void lane_dec_record(const RecArgs &a, uint64_t r, uint32_t j, uint32_t upto,
+                                                const uint8_t *src, const uint64_t *snoff, const uint32_t *scnt) {
+    uint32_t d = 0;
+    Disc dv;
+    dv.pres = 0;
+    for (uint32_t k = 0; k < upto; ++k) {
+        const VField &f = a.f[k];
+        if (a.ncond) {
+            if (!cond_present(a, f, dv)) {
+                // absent: fixed fields read as zero (a fresh rpcgen object), dynamic
+                // ones have an empty run (count 0 from the walk)
+                if (k + 1 == a.byref) a.ref_pos[r] = ~0ull;
+                if (f.kind == XDRG_K_DYNAMIC) { ++d; continue; }
+                uint8_t *base = f.data + (int64_t)r * f.stride;
+                const uint32_t nb = f.type == XDRG_T_OPAQUE ? f.count
+                                  : (f.kind == XDRG_K_FIXED ? f.count : 1u) * f.nsz;
+                for (uint32_t i = 0; i < nb; ++i) base[i] = 0;
+                continue;
+            }
+            cond_mark(f, k, f.slot ? (int32_t)ld_be32(src) : 0, dv);
+        }
+        if (f.kind != XDRG_K_DYNAMIC) {
+            const uint32_t nw = f.xbytes >> 2;
+            for (uint32_t i = 0; i < nw; ++i) fixed_store(f, r, 4 * i, *(const uint32_t *)(src + 4 * i));
+            src += f.xbytes;
+            continue;
+        }
+        const uint32_t cnt = scnt[(size_t)d * kRecPerBlock + j];
+        if (k + 1 == a.byref) {   // xdrDecodeByteBuffer (Xdr.java:423-439): a slice
+            a.ref_pos[r] = (uint64_t)(src + 4 - a.xdr);
+            src += 4 + cnt + pad4(cnt);
+            ++d;
+            continue;
+        }
+        const uint64_t no = snoff[(size_t)d * kRecPerBlock + j];
+        if (f.xsz == 1) lane_dec_bytes(f.data + no, src + 4, cnt);
+        else if (is_word4(f)) lane_dec_words((uint32_t *)(f.data + no * 4), src + 4, cnt);
+        else {
+            const uint64_t nw = (uint64_t)cnt * (f.xsz >> 2);
+            for (uint64_t i = 0; i < nw; ++i) dyn_store(f, no, cnt, 4 + 4 * i, *(const uint32_t *)(src + 4 + 4 * i));
+        }
+        src += dyn_xdr_bytes(f, cnt);
+        ++d;
+    }
+}
+
+template <bool TILE>
 __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *sstart = (uint64_t *)smem;
@@ -1829,53 +1878,45 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
     }
     __syncthreads();
     const uint64_t nrec = a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0;
-    for (uint32_t j = threadIdx.x; j < nrec; j += kRecThreads) {
-        const uint32_t upto = supto[j];
-        if (!upto) continue;
-        const uint64_t r = rb + j;
-        const uint8_t *src = a.xdr + sstart[j];
-        uint32_t d = 0;
-        Disc dv;
-        dv.pres = 0;
-        for (uint32_t k = 0; k < upto; ++k) {
-            const VField &f = a.f[k];
-            if (a.ncond) {
-                if (!cond_present(a, f, dv)) {
-                    // absent: fixed fields read as zero (a fresh rpcgen object), dynamic
-                    // ones have an empty run (count 0 from the walk)
-                    if (k + 1 == a.byref) a.ref_pos[r] = ~0ull;
-                    if (f.kind == XDRG_K_DYNAMIC) { ++d; continue; }
-                    uint8_t *base = f.data + (int64_t)r * f.stride;
-                    const uint32_t nb = f.type == XDRG_T_OPAQUE ? f.count
-                                      : (f.kind == XDRG_K_FIXED ? f.count : 1u) * f.nsz;
-                    for (uint32_t i = 0; i < nb; ++i) base[i] = 0;
-                    continue;
-                }
-                cond_mark(f, k, f.slot ? (int32_t)ld_be32(src) : 0, dv);
-            }
-            if (f.kind != XDRG_K_DYNAMIC) {
-                const uint32_t nw = f.xbytes >> 2;
-                for (uint32_t i = 0; i < nw; ++i) fixed_store(f, r, 4 * i, *(const uint32_t *)(src + 4 * i));
-                src += f.xbytes;
-                continue;
-            }
-            const uint32_t cnt = scnt[(size_t)d * kRecPerBlock + j];
-            if (k + 1 == a.byref) {   // xdrDecodeByteBuffer (Xdr.java:423-439): a slice
-                a.ref_pos[r] = (uint64_t)(src + 4 - a.xdr);
-                src += 4 + cnt + pad4(cnt);
-                ++d;
-                continue;
-            }
-            const uint64_t no = snoff[(size_t)d * kRecPerBlock + j];
-            if (f.xsz == 1) lane_dec_bytes(f.data + no, src + 4, cnt);
-            else if (is_word4(f)) lane_dec_words((uint32_t *)(f.data + no * 4), src + 4, cnt);
-            else {
-                const uint64_t nw = (uint64_t)cnt * (f.xsz >> 2);
-                for (uint64_t i = 0; i < nw; ++i) dyn_store(f, no, cnt, 4 + 4 * i, *(const uint32_t *)(src + 4 + 4 * i));
-            }
-            src += dyn_xdr_bytes(f, cnt);
-            ++d;
+    if (!TILE) {
+        for (uint32_t j = threadIdx.x; j < nrec; j += kRecThreads) {
+            const uint32_t upto = supto[j];
+            if (upto) lane_dec_record(a, rb + j, j, upto, a.xdr + sstart[j], snoff, scnt);
         }
+        return;
+    }
+    // TILE (tuning key 35): sub-batches of records whose stream bytes fit the
+    // tile are staged with coalesced 16-byte loads, each lane decodes its
+    // record from LDS (conditional schemas' per-record field walks read LDS
+    // instead of HBM); a record larger than the tile decodes from HBM
+    uint8_t *tile = (uint8_t *)(supto + kRecPerBlock);
+    const uintptr_t xb = (uintptr_t)a.xdr;
+    const uint32_t tid = threadIdx.x;
+    uint32_t js = 0;
+    while (js < nrec) {
+        const uint32_t je1 = js + 1 + tid;
+        bool fits = false;
+        if (je1 <= nrec) {
+            const uintptr_t lo = (xb + sstart[js]) & ~(uintptr_t)15;
+            const uintptr_t hi = (xb + rec_extent(a, rb + je1 - 1).b + 15) & ~(uintptr_t)15;
+            fits = hi >= lo && hi - lo <= a.tile_bytes;
+        }
+        const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
+        if (k1 == 0) {   // one record larger than the tile
+            if (tid == 0 && supto[js]) lane_dec_record(a, rb + js, js, supto[js], a.xdr + sstart[js], snoff, scnt);
+            ++js;
+            continue;
+        }
+        const uint32_t je = js + k1;
+        const uintptr_t a0 = (xb + sstart[js]) & ~(uintptr_t)15;
+        const uint32_t nch = (uint32_t)((((xb + rec_extent(a, rb + je - 1).b + 15) & ~(uintptr_t)15) - a0) >> 4);
+        for (uint32_t i = tid; i < nch; i += kRecThreads)
+            *(u32x4n *)(tile + 16 * (size_t)i) = __builtin_nontemporal_load((const u32x4n *)(a0 + 16 * (uintptr_t)i));
+        __syncthreads();
+        const uint32_t j = js + tid;
+        if (j < je && supto[j]) lane_dec_record(a, rb + j, j, supto[j], tile + (uint32_t)(xb + sstart[j] - a0), snoff, scnt);
+        __syncthreads();   // the tile's next use
+        js = je;
     }
 }
 
@@ -3348,7 +3389,13 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
             else if (a.big_rec && !(a.spec_mode & 1)) launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
             if (a.big_rec && pay) launch_dec_payload(t.pay_hoist, pgrid, st, a);
         } else if (lane || (grp && t.rec == 3)) {
-            hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+            if (t.lane_tile && !a.byref) {   // records staged through an LDS tile (tuning key 35)
+                a.tile_bytes = (uint32_t)t.lane_tile;
+                hipLaunchKernelGGL(k_dec_lane<true>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn) + t.lane_tile,
+                                   st, a);
+            } else {
+                hipLaunchKernelGGL(k_dec_lane<false>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+            }
         } else if (grp) {
             launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
             if (pay) launch_dec_payload(t.pay_hoist, pgrid, st, a);

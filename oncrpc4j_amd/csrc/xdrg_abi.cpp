@@ -368,6 +368,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 32: if (v != 64 && v != 32 && v != 16 && v != 8 && v != 4) return -1; t.grp_enc_lanes = (int32_t)v; return 0;
     case 33: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.grp_dec_tile = (int32_t)v; return 0;
     case 34: if (!in(0, 1 << 22)) return -1; t.pay_grid = (int32_t)v; return 0;
+    case 35: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.lane_tile = (int32_t)v; return 0;
     default: return -1;
     }
 }

@@ -201,6 +201,8 @@ struct Tuning {
                                     // (k_enc_iostage), 3 field-major with nontemporal stores
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
+    int32_t lane_tile = 0;          // key 35: lane-per-record decode (conditional schemas), LDS tile
+                                    // per sub-batch of records (0: records read from HBM)
     int32_t pay_grid = 0;           // key 34: payload kernels' grid (blocks striding over the records;
                                     // 0 = a block per 4 records)
     int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of

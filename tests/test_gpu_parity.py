@@ -47,7 +47,7 @@ SCHEMAS = {
 # default, 2),
 # key 9 = 0 group per record, 3 lane per record.  Tests taking `rec_kernel`
 # run under each.
-REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "staged": ((9, 4),),
+REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "lane_tile": ((9, 3), (35, 16384)), "staged": ((9, 4),),
                "staged_edges": ((9, 4), (20, 0)),
                "staged_lean": ((9, 4), (20, 1)),
                "staged_out": ((9, 4), (27, 1)),    # output image from HBM inputs (k_enc_ostage)
