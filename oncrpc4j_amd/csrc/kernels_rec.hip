@@ -1892,11 +1892,14 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
     uint8_t *tile = (uint8_t *)(supto + kRecPerBlock);
     const uintptr_t xb = (uintptr_t)a.xdr;
     const uint32_t tid = threadIdx.x;
+    // only records before the first failing one are decoded, and only theirs
+    // have a start in sstart: the sub-batches cover that prefix
+    const uint32_t nlive = bad > rb ? (uint32_t)(bad - rb < nrec ? bad - rb : nrec) : 0u;
     uint32_t js = 0;
-    while (js < nrec) {
+    while (js < nlive) {
         const uint32_t je1 = js + 1 + tid;
         bool fits = false;
-        if (je1 <= nrec) {
+        if (je1 <= nlive) {
             const uintptr_t lo = (xb + sstart[js]) & ~(uintptr_t)15;
             const uintptr_t hi = (xb + rec_extent(a, rb + je1 - 1).b + 15) & ~(uintptr_t)15;
             fits = hi >= lo && hi - lo <= a.tile_bytes;
