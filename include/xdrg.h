@@ -110,7 +110,10 @@ typedef struct xdrg_field {
  * element and a closing BE(0).  On the tape a group is one field
  * {XDRG_T_GROUP, kind FIXED / DYNAMIC / LIST, count, reserved = m} followed
  * by its m member fields (SCALAR, FIXED or DYNAMIC of the base types; no
- * nested groups, no conditions in a schema with groups).  Columns: the
+ * nested groups).  A condition (xdrg_cond below) stays on its level: a
+ * top-level field (the group field included) on a top-level discriminant,
+ * a member on an earlier member of its own group, evaluated per element.
+ * Columns: the
  * group's own column has offsets[n + 1] (DYNAMIC / LIST: record i owns
  * elements [offsets[i], offsets[i+1]); FIXED: element i*count + j, offsets
  * unused) and, on decode, cap = element capacity; data is unused.  A member's

@@ -35,8 +35,10 @@ reference's own portmap/pmaplist.java:50-69) — become repeated groups
 flattened fields as members).  Unions and optional data inside an element
 become conditions between members of the same group (evaluated per
 element), and a group may itself sit in a union arm or behind optional data
-(a condition on the group field).  Still not one tape: arrays of structs
-inside elements, and recursion anywhere but a struct's last declaration.
+(a condition on the group field).  A fixed-size array of structs inside an
+element (`T x[N]`, no count word) unrolls into N copies of T's members.
+Still not one tape: variable-length arrays of structs and lists inside
+elements, and recursion anywhere but a struct's last declaration.
 """
 import re
 
@@ -237,8 +239,14 @@ class _Tape:
 
     DISC_TYPES = (abi.T_INT, abi.T_UINT, abi.T_ENUM, abi.T_BOOL)
 
-    def __init__(self, spec):
+    # a fixed array of structs inside a group element unrolls into this many
+    # copies of the struct's members at most (the engine's field limit bounds
+    # the tape anyway)
+    MAX_UNROLL = 16
+
+    def __init__(self, spec, in_element=False):
         self.s = spec
+        self.in_element = in_element
         self.fields = _TapeFields()
         self.fields.reasons = []
         self.conds = []
@@ -325,9 +333,11 @@ class _Tape:
         group itself may sit under a guard (an array / list in a union arm or
         behind optional data); its members may carry conditions on earlier
         members of the same element (unions and optional data inside an
-        element, e.g. READDIRPLUS's post_op_attr).  Arrays of structs inside
-        an element are not one level of groups."""
-        sub = _Tape(self.s)
+        element, e.g. READDIRPLUS's post_op_attr).  A fixed array of structs
+        inside an element unrolls into its elements' members (decl()); a
+        variable-length one or a list inside an element is not one level of
+        groups."""
+        sub = _Tape(self.s, in_element=True)
         for d in decls:
             sub.decl(d, f"{where}.{d.name}", None, stack + (st.name,))
         fields, conds = sub.result()
@@ -355,6 +365,22 @@ class _Tape:
             # `T x<>` / `T x[N]` of a struct: the count (dynamic), then the elements
             if self._list_struct(st):
                 raise NotBatchable(f"{where}: an array of list heads {st.name}")
+            if self.in_element and decl.kind == FIXED:
+                # `T x[N]` inside a group element: no count word on the wire
+                # (jrpcgen.java:856-906, xdrEncodeFixedVector), so the N
+                # elements are N consecutive copies of T's declarations,
+                # members of the enclosing element like its other fields
+                n = self.s.value(decl.size)
+                if st.name in stack:
+                    raise NotBatchable(f"{where}: {st.name} contains itself (a recursive type has "
+                                       f"no bounded tape)")
+                if n > self.MAX_UNROLL:
+                    raise NotBatchable(f"{where}: {st.name}[{n}] inside a group element (at most "
+                                       f"{self.MAX_UNROLL} elements unroll)")
+                for j in range(n):
+                    for d in st.decls:
+                        self.decl(d, f"{where}[{j}].{d.name}", guard, stack + (st.name,))
+                return
             self.group(abi.K_FIXED if decl.kind == FIXED else abi.K_DYNAMIC,
                        self.s.value(decl.size) if decl.kind == FIXED else 0, st, st.decls, where, guard, stack)
             return

@@ -22,6 +22,8 @@ fixtures are plain JSON data and travel, this script's inputs do not need to.
 5. cond_vectors.json / group_vectors.json / group_cond_vectors.json — union
    and optional tapes, arrays of structs and lists, and unions inside list
    elements (rpcgen/plus_types.x), packed by xdrlib.
+   chunk_map_vectors.json — a fixed array of structs with optional data inside
+   list elements (rpcgen/chunk_map.x), packed by xdrlib.
 """
 import json
 import os
@@ -475,6 +477,66 @@ def group_cond_vectors(seed=0x9D1F):
     return out
 
 
+# ---- a fixed array of structs inside list elements ------------------------------
+# tests/golden/rpcgen/chunk_map.x `chunk_map`: every `chunk_ent *next` list
+# element holds `replica copies[2]` (no count word) and each replica an
+# optional checksum — packed by xdrlib from the declarations; records also in
+# tape layout (the element's unrolled members, absent crc as 0).
+def chunk_map_vectors(seed=0xC4A7):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oncrpc4j_amd import rpcgen
+    spec = rpcgen.parse_file(os.path.join(HERE, "rpcgen", "chunk_map.x"))
+    fields, conds = spec.tape("chunk_map")
+    rng = random.Random(seed)
+    out = {"source": "CPython 3.10 stdlib xdrlib (RFC 1014) packing chunk_map.x `chunk_map` from its "
+                     "declarations (a fixed array of structs with optional data inside "
+                     "`chunk_ent *next` list elements, jrpcgen.java:835-906)",
+           "seed": seed, "fields": [list(f) for f in fields], "conds": [list(c) for c in conds],
+           "batches": []}
+    for framed in (False, True):
+        n = 40
+        records, chunks = [], []
+        for i in range(n):
+            p = xdrlib.Packer()
+            volume = rng.getrandbits(32)
+            p.pack_uint(volume)
+            ents = []
+            for _ in range(rng.choice([0, 1, 2, 3, 5, 9])):
+                cid = rng.getrandbits(64)
+                p.pack_bool(True)
+                p.pack_uhyper(cid)
+                ent = [cid]
+                for _ in range(2):
+                    pool = rng.getrandbits(32)
+                    off = rng.getrandbits(64) - (1 << 63)
+                    tag = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 17)))
+                    has = rng.random() < 0.5
+                    crc = rng.getrandbits(32) if has else 0
+                    p.pack_uint(pool); p.pack_hyper(off); p.pack_opaque(tag)
+                    p.pack_bool(has)
+                    if has:
+                        p.pack_uint(crc)
+                    ent += [pool, off, tag.hex(), int(has), crc]
+                sealed = rng.randint(0, 1)
+                p.pack_bool(sealed)
+                ents.append(ent + [sealed])
+            p.pack_bool(False)
+            gen = rng.getrandbits(64) - (1 << 63)
+            p.pack_hyper(gen)
+            body = p.get_buffer()
+            if framed:
+                body = struct.pack(">I", len(body) | 0x80000000) + body
+            chunks.append(body)
+            records.append([volume, ents] + [None] * 12 + [gen])
+        offs = [0]
+        for ch in chunks:
+            offs.append(offs[-1] + len(ch))
+        out["batches"].append({"name": "chunk_map", "framed": framed, "n": n, "records": records,
+                               "xdr": b"".join(chunks).hex(), "rec_offsets": offs})
+    return out
+
+
 # ---- framing -----------------------------------------------------------------
 def call_message(xid, args_string):
     """RpcMessageParserTCPTest.XdrStreamBuilder.build (:127-142): CALL header,
@@ -617,7 +679,8 @@ def rpc_vectors(seed=0x5EED):
 GENERATORS = {"kat_reference.json": kat_reference, "kat_jdk_nan.json": kat_jdk_nan,
               "xdrlib_vectors.json": xdrlib_vectors, "framing.json": framing, "rpc_vectors.json": rpc_vectors,
               "cond_vectors.json": cond_vectors, "group_vectors.json": group_vectors,
-              "group_cond_vectors.json": group_cond_vectors}
+              "group_cond_vectors.json": group_cond_vectors,
+              "chunk_map_vectors.json": chunk_map_vectors}
 
 
 def main(names=None):
