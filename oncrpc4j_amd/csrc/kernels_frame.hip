@@ -173,7 +173,8 @@ constexpr uint32_t kFRes = 0x10000u;
 constexpr uint32_t kFPtr = 0xfffu;     // the local pointer of a J value (bit 12: the word's LAST flag)
 template <int B>
 __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
-                                                      uint16_t *exitR, uint32_t *alist, uint32_t *acnt) {
+                                                      uint16_t *exitR, uint32_t *alist, uint32_t *acnt,
+                                                      uint32_t *sentry, uint32_t *gentry, uint32_t ngrp) {
     __shared__ __attribute__((aligned(16))) uint32_t J[kFChunk];
     __shared__ __attribute__((aligned(16))) uint16_t L[kFChunk];   // active positions (sub-chunk local)
     __shared__ uint32_t wtot[4];
@@ -181,6 +182,11 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
     const uint32_t sbeg = blockIdx.x * kFSuper;
     const uint32_t send = min(sbeg + kFSuper, Q);   // chain words past it leave the super-chunk
     const uint32_t nsub = (send - sbeg + kFChunk - 1) / kFChunk;
+    // the entries k_fr_fix_* fill in start as "none" (one vector store a block)
+    if (tid == 0) {
+        sentry[blockIdx.x] = ~0u;
+        if (blockIdx.x < ngrp) gentry[blockIdx.x] = ~0u;
+    }
     uint32_t x[16], y[16];
     fr_cload<B>(w, Q, sbeg + (nsub - 1) * kFChunk, tid, x);
     for (int j = (int)nsub - 1; j >= 0; --j) {
@@ -845,24 +851,24 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
 // sizes as gaps.
 // ---------------------------------------------------------------------------
 template <int B>
-__global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w, uint32_t Q, const FrameSub *sub,
-                                                  const FrameBase *bases, const uint32_t *fbits,
-                                                  const uint32_t *lbits, uint64_t cap, int stream_offsets,
-                                                  uint64_t *msg_offsets, uint64_t *frag_pos, uint64_t *res) {
-    __shared__ uint32_t wsum[2][2], wtail[2], wlo[2], whi[2];
-    __shared__ uint16_t so[kFChunk + 1];           // staged message offsets
+__device__ __forceinline__ void fr_emit_sub(const uint32_t *__restrict__ w, uint32_t Q, const FrameSub *sub,
+                                            const FrameBase *bases, const uint32_t *fbits, const uint32_t *lbits,
+                                            uint64_t cap, int stream_offsets, uint64_t *msg_offsets,
+                                            uint64_t *frag_pos, uint64_t *res, uint64_t F, uint64_t M, uint64_t k,
+                                            uint16_t *so, uint32_t (&wsum)[2][2], uint32_t (&wtail)[2],
+                                            uint32_t (&wlo)[2], uint32_t (&whi)[2]) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint64_t k = blockIdx.x;                 // sub-chunk
     const uint64_t s = k / (kFSuper / kFChunk);
-    if (res[0] == kFUnal || k * kFChunk >= Q) return;
+    // every load issued before the first test: the workspace arrays cover the
+    // whole grid (frame_ws), so a sub-chunk skipped here read in-bounds words only
     const FrameSub info = sub[k];
-    if (!info.nfrag) return;
     const FrameBase b = bases[s];
-    const uint64_t F = res[1], M = res[4];
+    const uint32_t fw = fbits[k * 128 + tid], lw = lbits[k * 128 + tid];
+    if (k * kFChunk >= Q) return;
+    if (!info.nfrag) return;
     const uint64_t fb0 = b.frag + info.pre_frag, lb0 = b.last + info.pre_last;
     if (fb0 >= F) return;                          // past the last complete message
     const uint32_t in_tail = info.prev_tail != 2u ? info.prev_tail : b.prev_tail;
-    const uint32_t fw = fbits[k * 128 + tid], lw = lbits[k * 128 + tid];
     // exclusive prefixes over the block's words (wave scans + one barrier),
     // and the LAST flag of the fragment before each word ("last non-empty")
     uint32_t cf = __popc(fw), cl = __popc(lw);
@@ -921,6 +927,26 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
     khi = max(whi[0], whi[1]);
     const uint64_t vbase = stream_offsets ? B * base : B * base - 4 * fb0;
     for (uint32_t kk = klo + tid; kk < khi; kk += 128) msg_offsets[lb0 + kk] = vbase + so[kk];
+    __syncthreads();   // so / wsum / wlo free for the block's next sub-chunk
+}
+
+template <int B>
+__global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w, uint32_t Q, const FrameSub *sub,
+                                                  const FrameBase *bases, const uint32_t *fbits,
+                                                  const uint32_t *lbits, uint64_t cap, int stream_offsets,
+                                                  uint64_t *msg_offsets, uint64_t *frag_pos, uint64_t *res,
+                                                  uint64_t nsub, uint32_t per) {
+    __shared__ uint32_t wsum[2][2], wtail[2], wlo[2], whi[2];
+    __shared__ uint16_t so[kFChunk + 1];           // staged message offsets
+    const uint64_t r0 = res[0], F = res[1], M = res[4];
+    if (r0 == kFUnal) return;
+    // `per` consecutive sub-chunks per block (fewer, longer blocks: the
+    // per-sub-chunk work is a few hundred stores)
+    const uint64_t k0 = (uint64_t)blockIdx.x * per;
+    const uint64_t k1 = min(k0 + per, nsub);
+    for (uint64_t k = k0; k < k1; ++k)
+        fr_emit_sub<B>(w, Q, sub, bases, fbits, lbits, cap, stream_offsets, msg_offsets, frag_pos, res, F, M, k,
+                       so, wsum, wtail, wlo, whi);
 }
 
 // ---------------------------------------------------------------------------
@@ -991,14 +1017,13 @@ __global__ __launch_bounds__(256) void k_fr_copy(const uint8_t *in, const uint64
 // ---- launchers -------------------------------------------------------------------
 template <int B>
 static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                        uint64_t *msg_offsets, bool frag_list, hipStream_t st) {
+                        uint64_t *msg_offsets, bool frag_list, int emit_per, hipStream_t st) {
     const uint32_t *w = (const uint32_t *)in;
     const uint32_t Q = frame_positions(len, B), tb = B == 4 ? (uint32_t)(len & 3) : 0u;
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
-    hipLaunchKernelGGL(k_fr_exits<B>, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitR, ws.alist, ws.acnt);
-    const uint64_t ngrp = (nsup + kFixGrp - 1) / kFixGrp;
-    if (hipMemsetAsync(ws.sentry, 0xff, nsup * 4, st) != hipSuccess) return (int)hipErrorUnknown;
-    if (hipMemsetAsync(ws.gentry, 0xff, ngrp * 4, st) != hipSuccess) return (int)hipErrorUnknown;
+    const uint64_t ngrp = (nsup + kFixGrp - 1) / kFixGrp;   // <= nsup: k_fr_exits sets every gentry
+    hipLaunchKernelGGL(k_fr_exits<B>, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitR, ws.alist, ws.acnt,
+                       ws.sentry, ws.gentry, (uint32_t)ngrp);
     const FrExits<B> ex{w, ws.exitR, Q, tb};
     hipLaunchKernelGGL(k_fr_win<B>, dim3((uint32_t)((nsup * kFixWin + 255) / 256)), dim3(256), 0, st, ex,
                        (uint32_t)nsup, ws.wtab);
@@ -1011,15 +1036,22 @@ static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint
     hipLaunchKernelGGL(k_fr_mark<B>, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.alist,
                        ws.acnt, ws.sub, ws.fbits, ws.lbits, ws.sup);
     hipLaunchKernelGGL(k_fr_bases, dim3(1), dim3(1024), 0, st, ws.sup, nsup, ws.bases, ws.res);
-    hipLaunchKernelGGL(k_fr_emit<B>, dim3((uint32_t)nsub), dim3(128), 0, st, w, Q, ws.sub, ws.bases, ws.fbits,
-                       ws.lbits, cap, stream_offsets ? 1 : 0, msg_offsets, frag_list ? ws.frag_pos : nullptr, ws.res);
+    // several sub-chunks per block, while the grid keeps >= 64 blocks (short
+    // streams keep their parallelism)
+    uint32_t per = emit_per > 0 ? (uint32_t)emit_per : 1u;
+    while (per > 1 && nsub / per < 64) per >>= 1;
+    hipLaunchKernelGGL(k_fr_emit<B>, dim3((uint32_t)((nsub + per - 1) / per)), dim3(128), 0, st, w, Q, ws.sub,
+                       ws.bases, ws.fbits, ws.lbits, cap, stream_offsets ? 1 : 0, msg_offsets,
+                       frag_list ? ws.frag_pos : nullptr, ws.res, (uint64_t)nsub, per);
     return (int)hipGetLastError();
 }
 
 int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                   uint64_t *msg_offsets, bool frag_list, void *stream) {
-    return B == 1 ? frame_launch<1>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, (hipStream_t)stream)
-                  : frame_launch<4>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, (hipStream_t)stream);
+                   uint64_t *msg_offsets, bool frag_list, int emit_per, void *stream) {
+    return B == 1 ? frame_launch<1>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per,
+                                    (hipStream_t)stream)
+                  : frame_launch<4>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per,
+                                    (hipStream_t)stream);
 }
 
 int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,

@@ -369,6 +369,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 33: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.grp_dec_tile = (int32_t)v; return 0;
     case 34: if (!in(0, 1 << 22)) return -1; t.pay_grid = (int32_t)v; return 0;
     case 35: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.lane_tile = (int32_t)v; return 0;
+    case 36: if (!in(1, 64)) return -1; t.emit_per = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -1590,7 +1591,7 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
     bool serial = !aligned(in, 4) || Q == 0;
     if (!serial) {   // parallel walk over words; a real chain meeting a size % 4 != 0 walks again over bytes
         HIPCHK(c, (hipError_t)frame_parallel(in, len, 4, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
-                                             c->stream));
+                                             c->tune.emit_per, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 48, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (c->h_stat[2] == kFUnal) {
@@ -1599,7 +1600,7 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
                 if (rc) return rc;
                 HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));
                 HIPCHK(c, (hipError_t)frame_parallel(in, len, 1, ws, cap, stream_offsets, msg_offsets,
-                                                     !stream_offsets, c->stream));
+                                                     !stream_offsets, c->tune.emit_per, c->stream));
                 HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 48, hipMemcpyDeviceToHost, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
             } else {

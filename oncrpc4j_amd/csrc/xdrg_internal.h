@@ -201,6 +201,8 @@ struct Tuning {
                                     // (k_enc_iostage), 3 field-major with nontemporal stores
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
+    int32_t emit_per = 4;           // key 36: frame walk, sub-chunks per k_fr_emit block (at most;
+                                    // halved until the grid has >= 64 blocks)
     int32_t lane_tile = 0;          // key 35: lane-per-record decode (conditional schemas), LDS tile
                                     // per sub-batch of records (0: records read from HBM)
     int32_t pay_grid = 0;           // key 34: payload kernels' grid (blocks striding over the records;
@@ -297,7 +299,7 @@ constexpr uint64_t kFByteMaxLen = 1ull << 31;   // byte-mode walks (positions an
 // when frag_list.  res[0] == kFUnal (word mode only): the real chain met a
 // size % 4 != 0 — walk again in byte mode.
 int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                   uint64_t *msg_offsets, bool frag_list, void *stream);
+                   uint64_t *msg_offsets, bool frag_list, int emit_per, void *stream);
 int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
                  uint64_t *msg_offsets, void *stream);
 // Bodies of the first nf fragments into payload (marks stripped).

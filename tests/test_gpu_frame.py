@@ -17,6 +17,15 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
+@pytest.fixture(autouse=True, params=[1, 4, 7], ids=lambda v: f"emit{v}")
+def emit_per(request, gpu_ctx):
+    """Sub-chunks per k_fr_emit block (tuning key 36; 7 leaves a partial last
+    block)."""
+    gpu_ctx.tune(36, request.param)
+    yield request.param
+    gpu_ctx.tune(0)
+
+
 def _dev(b):
     if not b:
         return torch.zeros(4, dtype=torch.uint8, device="cuda")
