@@ -1,5 +1,5 @@
 """Throughput of conditional tapes (rpcgen unions / optional data; DESIGN.md
-§8f2, §8f4) on two builder-designed shapes:
+§8f2, §8f4) on three builder-designed shapes:
 
 * RELEASE: lease_cache.x RELEASE(lease_key, lease_state) argument batches,
   4 Mi records (unsigned hyper, string<1024> of 8..64 B, an int union whose
@@ -7,7 +7,10 @@
 * READDIRPLUS: plus_types.x `plus_res` replies (the reply union, optional
   directory attributes, a verifier and a `plus_entry *next` list whose every
   element carries an optional attribute union and an optional handle union),
-  512 Ki records of 0..12 entries.
+  512 Ki records of 0..12 entries;
+* chunk map: chunk_map.x `chunk_map` replies (a `chunk_ent *next` list whose
+  every element holds `replica copies[2]`, unrolled, each replica with an
+  optional checksum and a tag opaque<16>), 1 Mi records of 0..12 entries.
 
 Device-resident, HIP-event timed encode and decode (median of reps); bytes =
 native + XDR per direction, as bench.py counts them; round trip checked."""
@@ -88,6 +91,10 @@ def main():
     plus = rpcgen.parse_file(os.path.join(g, "plus_types.x"))
     f, c = plus.tape("plus_res")
     print(json.dumps(run("READDIRPLUS plus_res replies", f, c, 512 << 10, (0, 40), (0, 12))), flush=True)
+    cmap = rpcgen.parse_file(os.path.join(g, "chunk_map.x"))
+    f, c = cmap.tape("chunk_map")
+    print(json.dumps(run("chunk_map replies (replica copies[2] in list elements)", f, c, 1 << 20, (0, 16), (0, 12))),
+          flush=True)
 
 
 if __name__ == "__main__":
