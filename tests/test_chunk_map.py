@@ -170,3 +170,60 @@ def test_gpu_chunk_map_random_vs_oracle(gpu_ctx, enc_lanes):
     ref = HostBatch.empty(FIELDS, n, hb.dyn_caps())
     assert oracle.decode_batch(FIELDS, want, offs, n, ref.columns(), conds=CONDS) == (0, n, 0)
     assert back.to_host().equal(ref)
+
+
+NESTED = """
+const NB = 2;
+struct span { unsigned int off; unsigned int len; };
+union loc switch (int kind) {
+    case 1: span spans[NB];
+    case 2: opaque blob<8>;
+    default: void;
+};
+struct part { hyper id; loc where; };
+struct seg { part parts[2]; bool last; seg *next; };
+struct seg_list { unsigned int n; seg *segs; };
+"""
+
+
+def test_nested_unroll_tape():
+    """Fixed arrays of structs nested inside an unrolled copy, and inside a
+    union arm inside it: every copy carries its own conditions."""
+    f, c = rpcgen.parse(NESTED).tape("seg_list")
+    assert f[1][:2] == (abi.T_GROUP, abi.K_LIST)
+    m = f[1][3]
+    assert len(f) == 2 + m
+    # part = id, kind, 2 x (off, len), blob -> 7 fields; two parts + last
+    assert m == 2 * 7 + 1
+    # each part's span words hang off its own kind, the blob too
+    kinds = [k for k, x in enumerate(f) if k >= 2 and any(d == k for _, d, _, _ in c)]
+    assert len(kinds) == 2
+    for kd in kinds:
+        deps = sorted(k for k, d, _, _ in c if d == kd)
+        assert deps == [kd + 1, kd + 2, kd + 3, kd + 4, kd + 5]
+
+
+@pytest.mark.gpu
+def test_gpu_nested_unroll_random_vs_oracle(gpu_ctx):
+    import torch
+    from oncrpc4j_amd import engine
+    from oncrpc4j_amd.columns import DeviceBatch, random_batch
+    fields, conds = rpcgen.parse(NESTED).tape("seg_list")
+    n = 2000
+    hb = random_batch(fields, n, seed=5, dyn_len=(0, 8), group_len=(0, 6))
+    rng = np.random.default_rng(5)
+    for kd in sorted({d for _, d, _, _ in conds}):
+        hb.arrays[kd][:] = rng.choice(np.array([0, 1, 2], np.int32), hb.arrays[kd].shape[0])
+    rc, want, offs = oracle.encode_batch(fields, hb.columns(), n, hb.xdr_total() + 64, conds=conds)
+    assert rc == 0
+    sch = engine.Schema(fields, conds)
+    db = DeviceBatch.from_host(hb)
+    out = torch.zeros(len(want) + 64, dtype=torch.uint8, device="cuda")
+    ro = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    ln = gpu_ctx.encode(sch, db.columns(), n, out, len(want) + 64, rec_offsets=ro)
+    assert out[:ln].cpu().numpy().tobytes() == want
+    back = DeviceBatch.empty(fields, n, hb.dyn_caps())
+    assert gpu_ctx.decode(sch, out, ln, n, back.columns(), rec_offsets=ro) == (0, n, 0)
+    ref = HostBatch.empty(fields, n, hb.dyn_caps())
+    assert oracle.decode_batch(fields, want, offs, n, ref.columns(), conds=conds) == (0, n, 0)
+    assert back.to_host().equal(ref)
