@@ -704,6 +704,8 @@ def host_inclusive(device, sch, n, reps=3, slot_bytes=64 << 20, slots=4,
         (_, nat, p_nat), (_, xdr, p_xdr), (_, req, p_req), (_, back, p_back) = bufs
         nat.view(np.int32)[:] = rng.integers(-2**31, 2**31 - 1, m * 8, dtype=np.int32)
         ce, cd = engine.Context(device), engine.Context(device)
+        for c_ in (ce, cd):
+            c_.apply_tuning(os.environ.get("XDRG_TUNE"))   # measurement runs only
         for c in (ce, cd):
             c.host_staging(slot_bytes, slots)
             if mode == "staged_dma":   # the ring's copies on the DMA engines instead of copy kernels
@@ -773,6 +775,7 @@ def run_rank(args):
     else:
         from oncrpc4j_amd import engine
         ctx = engine.Context(R.local, timing=True)
+        ctx.apply_tuning(os.environ.get("XDRG_TUNE"))   # measurement runs only
         ctx.set_stream(torch.cuda.current_stream())
 
         def make(cfg, n, framed):

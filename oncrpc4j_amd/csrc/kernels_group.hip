@@ -561,8 +561,9 @@ __device__ __forceinline__ void g_zero_fixed(const GField &f, uint64_t i) {
 // in: where stream offset x is read, in + x (the stream, or an LDS tile
 // holding this record's bytes: k_grp_dec_place_lds).
 __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in) {
-    const uint64_t end = a.rec_in[r + 1];
-    uint64_t pos = a.rec_in[r] + (a.framed ? 4 : 0);
+    const GExtent ex = g_extent(a, r);   // the extent the walk checked (clamped to in_len)
+    const uint64_t end = ex.b;
+    uint64_t pos = ex.a + (a.framed ? 4 : 0);
     GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
         const GField &f = a.f[k];
@@ -674,15 +675,20 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
     const uint64_t lim = bad < a.n ? bad : a.n;
     const uint32_t nlive = lim > rb ? (uint32_t)(lim - rb < (uint64_t)kRecThreads ? lim - rb : (uint64_t)kRecThreads) : 0u;
     const uintptr_t xb = (uintptr_t)a.xdr;
+    // the walk reads no byte at or past in_len (g_dec_record clamps each record's
+    // end): the staged range is clamped the same way, so a record whose extent
+    // runs past the stream (a cut tail that still parses) never stages bytes
+    // beyond it — in XDRG_HOST_MAPPED mode those would be unmapped host memory
+    auto ext = [&](uint64_t r) -> uint64_t { const uint64_t x = a.rec_in[r]; return x < a.xdr_cap ? x : a.xdr_cap; };
     uint32_t js = 0;
     while (js < nlive) {
         // records [js, js + 1 + tid) fit iff their aligned byte range does (monotone)
         const uint32_t je1 = js + 1 + tid;
         bool fits = false;
         if (je1 <= nlive) {
-            const uintptr_t lo = (xb + a.rec_in[rb + js]) & ~(uintptr_t)15;
-            const uintptr_t hi = (xb + a.rec_in[rb + je1] + 15) & ~(uintptr_t)15;
-            fits = hi - lo <= a.dec_tile;
+            const uintptr_t lo = (xb + ext(rb + js)) & ~(uintptr_t)15;
+            const uintptr_t hi = (xb + ext(rb + je1) + 15) & ~(uintptr_t)15;
+            fits = hi >= lo && hi - lo <= a.dec_tile;
         }
         const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
         if (k1 == 0) {   // one record larger than the tile: its lane decodes from HBM
@@ -691,8 +697,9 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
             continue;
         }
         const uint32_t je = js + k1;
-        const uintptr_t a0 = (xb + a.rec_in[rb + js]) & ~(uintptr_t)15;
-        const uint32_t nch = (uint32_t)((((xb + a.rec_in[rb + je] + 15) & ~(uintptr_t)15) - a0) >> 4);
+        const uintptr_t a0 = (xb + ext(rb + js)) & ~(uintptr_t)15;
+        const uintptr_t a1 = (xb + ext(rb + je) + 15) & ~(uintptr_t)15;
+        const uint32_t nch = a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u;
         for (uint32_t i = tid; i < nch; i += kRecThreads)
             *(u32x4g *)(tile + 16 * (size_t)i) = __builtin_nontemporal_load((const u32x4g *)(a0 + 16 * (uintptr_t)i));
         __syncthreads();

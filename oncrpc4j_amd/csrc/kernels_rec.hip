@@ -1333,6 +1333,24 @@ __device__ __forceinline__ void dec_place_g_block(const RecArgs &a, uint64_t bid
     if (nrec > kRecPerBlock) nrec = kRecPerBlock;
     const uint8_t *in = a.xdr;
     const uint32_t tid = threadIdx.x;
+    if (a.payk) {   // k_dec_payload decodes these records whole: head words, payload, tail words
+        const uint32_t kp = a.dyn_idx[a.payk - 1];   // the one dynamic field
+        const uint64_t hb = a.pay_fb - (a.framed ? 4 : 0);   // its offset after the mark
+        for (uint32_t j = tid; j < nrec; j += kRecThreads) {
+            const uint32_t up = supto[j];
+            a.pay_pos[rb + j] = up == a.nf ? sstart[j] + hb : ~0ull;
+            if (up == 0 || up == a.nf) continue;
+            // a record whose payload did not fit the native column (CAPACITY):
+            // the fields before it are decoded here, a lane per record (rare)
+            uint64_t q = sstart[j];
+            for (uint32_t k = 0; k < kp; ++k) {
+                const VField &f = a.f[k];
+                for (uint32_t i = 0; i < f.xbytes >> 2; ++i) fixed_store(f, rb + j, 4 * i, *(const uint32_t *)(in + q + 4 * i));
+                q += f.xbytes;
+            }
+        }
+        return;
+    }
     uint64_t fixed_delta = 0;
     uint32_t d = 0;
     for (uint32_t k = 0; k < a.nf; ++k) {
@@ -1365,15 +1383,6 @@ __device__ __forceinline__ void dec_place_g_block(const RecArgs &a, uint64_t bid
         }
         const uint32_t *cn = scnt + (size_t)d * kRecPerBlock;
         const uint64_t *no = snoff + (size_t)d * kRecPerBlock;
-        if (a.payk == d + 1) {   // k_dec_payload moves this field (records the walk passed only)
-            for (uint32_t j = tid; j < nrec; j += kRecThreads)
-                a.pay_pos[rb + j] = k < supto[j] ? sstart[j] + fixed_delta : ~0ull;
-            __syncthreads();
-            for (uint32_t j = tid; j < nrec; j += kRecThreads) sstart[j] += dyn_xdr_bytes(f, cn[j]);
-            __syncthreads();
-            ++d;
-            continue;
-        }
         uint64_t ps = 0;
         for (uint32_t j = tid; j < nrec; j += kRecThreads) ps += cn[j];
         const uint64_t fbytes = block_sum(ps) * (f.xsz == 1 ? 1 : f.xsz) + 4 * nrec;
@@ -1475,26 +1484,22 @@ __device__ uint32_t payload_rec_word(const RecArgs &a, uint64_t r, uint64_t o, u
 // lines are shared with the neighbouring records, whose waves run alongside
 // and complete them in L2).  One pass over each line: the group kernel only
 // hands over the payload positions (pay_pos).
-template <uint32_t LPR, bool NT, bool NTS = NT, bool H = true>
+// Nontemporal 16-byte loads and stores; every metadata load is issued
+// together, before the checks that use them (24.8 vs 25.6 ms with the checks
+// first, profiles/r02_c3_hoist_ab.jsonl); plain stores and a smaller grid whose
+// blocks stride over the records measured slower.
+constexpr uint32_t kPayLanes = 64;   // lanes per record: a wave
 __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
     if (r >= a.n) return;
     const VField &f = a.f[a.dyn_idx[a.payk - 1]];
-    // H: every metadata load issued together, before the checks that use them
-    // (else the checks first; tuning key 24 A/Bs the two in one run)
-    uint64_t total, e0, e1, pp;
-    if (H) {
-        total = a.totals[0]; e0 = f.offsets[r]; e1 = f.offsets[r + 1]; pp = a.pay_pos[r];
-        const bool mine = payload_block(a, r, false);
-        if (total > a.xdr_cap || !mine) return;
-    } else {
-        total = a.totals[0];
-        if (total > a.xdr_cap || !payload_block(a, r, false)) return;
-        e0 = f.offsets[r]; e1 = f.offsets[r + 1]; pp = a.pay_pos[r];
-    }
+    const uint64_t total = a.totals[0], e0 = f.offsets[r], e1 = f.offsets[r + 1], pp = a.pay_pos[r];
+    const bool mine = payload_block(a, r, false);
+    if (total > a.xdr_cap || !mine) return;
     const uint64_t cnt = e1 - e0;
     const uint64_t R = pp - a.pay_fb;   // record start
     const uint64_t P = cnt + pad4(cnt), size = a.fixed_xdr + 4 + P;
     const uint8_t *src = f.data + e0;
+    constexpr uint32_t LPR = kPayLanes;
     const uint32_t lane = threadIdx.x % LPR;
     uint8_t *const A = a.xdr + (R & ~(uint64_t)15);
     const uint64_t sh = R & 15;                    // record start inside chunk 0
@@ -1506,16 +1511,14 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
         for (int u = 0; u < 4; ++u) {   // all loads in flight first
             const uint64_t c = c0 + LPR * u;
             if (c < cl) {
-                const u32x4a *p = (const u32x4a *)(src + 16 * c - p0);   // 4-aligned
-                v[u] = NT ? __builtin_nontemporal_load(p) : *p;
+                v[u] = __builtin_nontemporal_load((const u32x4a *)(src + 16 * c - p0));   // 4-aligned
             }
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint64_t c = c0 + LPR * u;
             if (c >= cl) continue;
-            if (NTS) __builtin_nontemporal_store(v[u], (u32x4n *)(A + 16 * c));
-            else *(u32x4n *)(A + 16 * c) = v[u];
+            __builtin_nontemporal_store(v[u], (u32x4n *)(A + 16 * c));
         }
     }
     // the record's words outside those chunks (mark, fixed fields, length,
@@ -1529,31 +1532,43 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
         *(uint32_t *)(a.xdr + R + 4 * wi) = payload_rec_word(a, r, 4 * wi, size, src, cnt);
     }
 }
-template <uint32_t LPR, bool NT, bool NTS = NT, bool H = true>   // lanes per record; grid-strided; NT: nontemporal loads, NTS: stores; H: hoisted metadata loads
+// a block per 4 records (a wave each): neighbouring blocks on neighbouring records
 __global__ __launch_bounds__(256) void k_enc_payload(const RecArgs a) {
-    const uint64_t step = (uint64_t)gridDim.x * (256 / LPR);
-    for (uint64_t r = (uint64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; r < a.n; r += step)
-        enc_payload_rec<LPR, NT, NTS, H>(a, r);
+    const uint64_t step = (uint64_t)gridDim.x * (256 / kPayLanes);   // (one pass below 2^32 records)
+    for (uint64_t r = (uint64_t)blockIdx.x * (256 / kPayLanes) + threadIdx.x / kPayLanes; r < a.n; r += step)
+        enc_payload_rec(a, r);
 }
-template <uint32_t LPR, bool NT, bool H = true>
 __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
     if (r >= a.n) return;
     const uint32_t d = a.payk - 1;
     const VField &f = a.f[a.dyn_idx[d]];
-    // H: metadata loads issued together, before the checks (one round trip ahead of the data)
-    uint64_t pos, cnt, o;
-    if (H) {
-        pos = a.pay_pos[r]; cnt = a.rec_cnt[(uint64_t)d * a.n + r]; o = f.offsets[r];
-        if (pos == ~0ull || !payload_block(a, r, true)) return;
-    } else {
-        if (!payload_block(a, r, true)) return;
-        pos = a.pay_pos[r];
-        if (pos == ~0ull) return;
-        cnt = a.rec_cnt[(uint64_t)d * a.n + r]; o = f.offsets[r];
-    }
+    // metadata loads issued together, before the checks (one round trip ahead of the data)
+    const uint64_t pos = a.pay_pos[r], cnt = a.rec_cnt[(uint64_t)d * a.n + r], o = f.offsets[r];
+    if (pos == ~0ull || !payload_block(a, r, true)) return;
     const uint8_t *src = a.xdr + pos + 4;
     uint8_t *dst = f.data + o;
+    constexpr uint32_t LPR = kPayLanes;
     const uint32_t lane = threadIdx.x % LPR;
+    // the record's fixed fields, a word per lane (the group kernel only placed
+    // the record): the head words before the length word, the tail words
+    // after the payload and its pad (Xdr.java:171-175 each; the walk has
+    // checked every length and bound in the reference's order)
+    {
+        const uint32_t hw = (uint32_t)(a.pay_fb - (a.framed ? 4 : 0)) >> 2;
+        const uint32_t tw = (a.fixed_xdr - a.pay_fb) >> 2;
+        const uint64_t h0 = pos - 4 * (uint64_t)hw, t0 = pos + 4 + cnt + pad4(cnt);
+        for (uint32_t i = lane; i < hw + tw; i += LPR) {
+            const uint32_t v = *(const uint32_t *)(a.xdr + (i < hw ? h0 + 4 * (uint64_t)i : t0 + 4 * (uint64_t)(i - hw)));
+            uint32_t w = i;   // fixed-field word index, declaration order
+            for (uint32_t k = 0; k < a.nf; ++k) {
+                const VField &g = a.f[k];
+                if (g.kind == XDRG_K_DYNAMIC) continue;
+                const uint32_t nw = g.xbytes >> 2;
+                if (w < nw) fixed_store(g, r, 4 * w, v);
+                w = w < nw ? ~0u >> 1 : w - nw;   // (stored: past every later field)
+            }
+        }
+    }
     const uint64_t nch = (cnt + 15) >> 4;
     for (uint64_t c0 = lane; c0 < nch; c0 += 4 * LPR) {
         u32x4a v[4];
@@ -1561,15 +1576,14 @@ __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
         for (int u = 0; u < 4; ++u) {
             const uint64_t c = c0 + LPR * u;
             if (16 * c + 16 <= cnt)
-                v[u] = NT ? __builtin_nontemporal_load((const u32x4a *)(src + 16 * c)) : *(const u32x4a *)(src + 16 * c);
+                v[u] = __builtin_nontemporal_load((const u32x4a *)(src + 16 * c));
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint64_t c = c0 + LPR * u;
             if (c >= nch) continue;
             if (16 * c + 16 <= cnt) {
-                if (NT) __builtin_nontemporal_store(v[u], (u32x4u *)(dst + 16 * c));
-                else *(u32x4u *)(dst + 16 * c) = v[u];
+                __builtin_nontemporal_store(v[u], (u32x4u *)(dst + 16 * c));
                 continue;
             }
             for (uint64_t b = 16 * c; b < cnt; b += 4) {   // last chunk (stream words are 4-aligned)
@@ -1581,11 +1595,10 @@ __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
         }
     }
 }
-template <uint32_t LPR, bool NT, bool H = true>   // lanes per record: 64 (a wave) or 256 (the block); grid-strided; NT: nontemporal
 __global__ __launch_bounds__(256) void k_dec_payload(const RecArgs a) {
-    const uint64_t step = (uint64_t)gridDim.x * (256 / LPR);
-    for (uint64_t r = (uint64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR; r < a.n; r += step)
-        dec_payload_rec<LPR, NT, H>(a, r);
+    const uint64_t step = (uint64_t)gridDim.x * (256 / kPayLanes);
+    for (uint64_t r = (uint64_t)blockIdx.x * (256 / kPayLanes) + threadIdx.x / kPayLanes; r < a.n; r += step)
+        dec_payload_rec(a, r);
 }
 
 // ===========================================================================
@@ -1785,7 +1798,8 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_lane(const RecArgs a) {
 }
 
 // Lane j of the block decodes record r = rb + j from src (its first field's
-// bytes: in the stream, or in the LDS tile of k_dec_lane<TILE>), fields [0, upto).
+// bytes in the stream), fields [0, upto).  (An LDS-tiled variant, records
+// staged in sub-batches, measured slower at every tile size: DESIGN.md §5.7.)
 __device__ __forceinline__ void lane_dec_record(const RecArgs &a, uint64_t r, uint32_t j, uint32_t upto,
                                                 const uint8_t *src, const uint64_t *snoff, const uint32_t *scnt) {
     uint32_t d = 0;
@@ -1832,7 +1846,6 @@ __device__ __forceinline__ void lane_dec_record(const RecArgs &a, uint64_t r, ui
     }
 }
 
-template <bool TILE>
 __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *sstart = (uint64_t *)smem;
@@ -1878,48 +1891,9 @@ __global__ __launch_bounds__(kRecThreads) void k_dec_lane(const RecArgs a) {
     }
     __syncthreads();
     const uint64_t nrec = a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0;
-    if (!TILE) {
-        for (uint32_t j = threadIdx.x; j < nrec; j += kRecThreads) {
-            const uint32_t upto = supto[j];
-            if (upto) lane_dec_record(a, rb + j, j, upto, a.xdr + sstart[j], snoff, scnt);
-        }
-        return;
-    }
-    // TILE (tuning key 35): sub-batches of records whose stream bytes fit the
-    // tile are staged with coalesced 16-byte loads, each lane decodes its
-    // record from LDS (conditional schemas' per-record field walks read LDS
-    // instead of HBM); a record larger than the tile decodes from HBM
-    uint8_t *tile = (uint8_t *)(supto + kRecPerBlock);
-    const uintptr_t xb = (uintptr_t)a.xdr;
-    const uint32_t tid = threadIdx.x;
-    // only records before the first failing one are decoded, and only theirs
-    // have a start in sstart: the sub-batches cover that prefix
-    const uint32_t nlive = bad > rb ? (uint32_t)(bad - rb < nrec ? bad - rb : nrec) : 0u;
-    uint32_t js = 0;
-    while (js < nlive) {
-        const uint32_t je1 = js + 1 + tid;
-        bool fits = false;
-        if (je1 <= nlive) {
-            const uintptr_t lo = (xb + sstart[js]) & ~(uintptr_t)15;
-            const uintptr_t hi = (xb + rec_extent(a, rb + je1 - 1).b + 15) & ~(uintptr_t)15;
-            fits = hi >= lo && hi - lo <= a.tile_bytes;
-        }
-        const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
-        if (k1 == 0) {   // one record larger than the tile
-            if (tid == 0 && supto[js]) lane_dec_record(a, rb + js, js, supto[js], a.xdr + sstart[js], snoff, scnt);
-            ++js;
-            continue;
-        }
-        const uint32_t je = js + k1;
-        const uintptr_t a0 = (xb + sstart[js]) & ~(uintptr_t)15;
-        const uint32_t nch = (uint32_t)((((xb + rec_extent(a, rb + je - 1).b + 15) & ~(uintptr_t)15) - a0) >> 4);
-        for (uint32_t i = tid; i < nch; i += kRecThreads)
-            *(u32x4n *)(tile + 16 * (size_t)i) = __builtin_nontemporal_load((const u32x4n *)(a0 + 16 * (uintptr_t)i));
-        __syncthreads();
-        const uint32_t j = js + tid;
-        if (j < je && supto[j]) lane_dec_record(a, rb + j, j, supto[j], tile + (uint32_t)(xb + sstart[j] - a0), snoff, scnt);
-        __syncthreads();   // the tile's next use
-        js = je;
+    for (uint32_t j = threadIdx.x; j < nrec; j += kRecThreads) {
+        const uint32_t upto = supto[j];
+        if (upto) lane_dec_record(a, rb + j, j, upto, a.xdr + sstart[j], snoff, scnt);
     }
 }
 
@@ -2062,13 +2036,10 @@ __device__ void enc_record_block(const RecArgs &a, uint64_t r, uint64_t pos) {
 // one barrier (which also ends every use of the tile before it).  0 = record
 // js alone exceeds the tile.
 __device__ __forceinline__ uint32_t enc_fit(const RecArgs &a, const uint64_t (&base)[kMaxDynLds],
-                                            const uint32_t *srel, uint32_t js, uint32_t nrec,
-                                            const uint32_t *soff = nullptr, uint32_t mis = 0, uint32_t ocap = 0) {
+                                            const uint32_t *srel, uint32_t js, uint32_t nrec) {
     const uint32_t je = js + 1 + threadIdx.x;
     bool fits = false;
-    // output-imaged sub-batches: the output bytes from record js's line fit the image too
-    // (one barrier for every thread: the count below)
-    if (je <= nrec && (!soff || soff[je] - soff[js] + ((mis + soff[js]) & 15u) <= ocap)) {
+    if (je <= nrec) {
         uint32_t need = 0;
 #pragma unroll
         for (int d = 0; d < kMaxDynLds; ++d) {
@@ -2084,96 +2055,13 @@ __device__ __forceinline__ uint32_t enc_fit(const RecArgs &a, const uint64_t (&b
     return (uint32_t)__syncthreads_count(fits);
 }
 
-// Output-staged sub-batches (k_enc_ostage): records [js, je) whose OUTPUT
-// bytes, from the 16-byte line the first one starts in, fit the tile.
-__device__ __forceinline__ uint32_t enc_out_fit(const uint32_t *soff, uint32_t js, uint32_t nrec, uint32_t mis,
-                                                uint32_t cap) {
-    const uint32_t je = js + 1 + threadIdx.x;
-    const bool fits = je <= nrec && soff[je] - soff[js] + ((mis + soff[js]) & 15u) <= cap;
-    return (uint32_t)__syncthreads_count(fits);
-}
-
-// Compose the XDR bytes of records [js, je) into the LDS image `img` (image
-// byte 0 = the 16-byte aligned stream line record js starts in, `head`
-// bytes before it): marks, fixed words and length-prefixed dynamic fields,
-// read straight from the native columns (16-byte windows realigned in
-// registers), written to LDS at any 4-byte alignment.
-__device__ void enc_compose(const RecArgs &a, uint8_t *img, uint32_t head, uint64_t rb, uint32_t js, uint32_t je,
-                            const uint32_t *soff, const uint32_t *srel, const uint64_t (&base)[kMaxDynLds]) {
-    constexpr uint32_t RS = kRecPerBlock + 1;
-    const uint32_t tid = threadIdx.x;
-    uint8_t *const at = img + head - soff[js];   // image byte of block-relative stream offset x: at + x
-    if (a.framed)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
-        for (uint32_t j = js + tid; j < je; j += kRecThreads)
-            *(uint32_t *)(at + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
-    uint32_t fpre = a.framed ? 4 : 0;
-    uint32_t d = 0;
-    const uint32_t m = je - js;
-    for (uint32_t k = 0; k < a.nf; ++k) {
-        const VField &f = a.f[k];
-        if (f.kind != XDRG_K_DYNAMIC) {
-            const uint32_t nw = f.xbytes >> 2;
-            if (nw) {
-                const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
-                const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-                for (uint32_t j = js + tid / G; j < je; j += ng) {
-                    uint8_t *dst = at + soff[j] + fpre + dyn_before(a, srel, j, d);
-                    for (uint32_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
-                }
-            }
-            fpre += f.xbytes;
-            continue;
-        }
-        const bool bytes = f.xsz == 1;
-        const uint64_t esz = bytes ? 1 : f.nsz;
-        const uint32_t *rel = srel + d * RS;
-        const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
-        const uint32_t G = a.force_g ? a.force_g : pow2_lanes(fbytes / m, a.lane_bytes_enc);
-        const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-        const Span sp = make_span(f.data + f.offsets[0] * esz, f.data + f.offsets[a.n] * esz,
-                                  (const uint8_t *)a.block_sums);
-        for (uint32_t j = js + tid / G; j < je; j += ng) {
-            const uint64_t cnt1 = rel[j + 1] - rel[j];
-            uint8_t *dst[1] = {at + soff[j] + fpre + dyn_before(a, srel, j, d)};
-            const uint8_t *src[1] = {f.data + (base[d] + rel[j]) * esz};
-            const uint64_t cnt[1] = {cnt1};
-            const uint64_t nwb = 1 + (bytes ? (cnt1 + 3) >> 2 : cnt1);
-            const uint64_t nch[1] = {(nwb + 3) >> 2};
-            if (bytes) enc_blob_bytes<2, 1>(dst, src, cnt, nch, sp, G, gl);
-            else enc_blob_words4<2, 1>(dst, src, cnt, nch, f.type == XDRG_T_FLOAT, sp, G, gl);
-        }
-        ++d;
-    }
-}
-
-// Write image bytes [head, nbytes) to the stream at A0 (16-byte aligned):
-// whole lines as aligned 16-byte stores, the first and last line's own
-// dwords only (the rest of those lines belong to the neighbouring records).
-__device__ __forceinline__ void enc_flush(const uint8_t *img, uint8_t *A0, uint32_t head, uint32_t nbytes) {
-    const uint32_t nch = (nbytes + 15) >> 4;
-    for (uint32_t i = threadIdx.x; i < nch; i += kRecThreads) {
-        const uint32_t lo = 16 * i;
-        const u32x4n v = *(const u32x4n *)(img + lo);
-        if (lo >= head && lo + 16 <= nbytes) {
-            __builtin_nontemporal_store(v, (u32x4n *)(A0 + lo));
-            continue;
-        }
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (lo + 4 * q >= head && lo + 4 * q + 4 <= nbytes) *(uint32_t *)(A0 + lo + 4 * q) = w[q];
-    }
-}
-
-// MODE 0: input-staged (k_enc_stage); 1: output-imaged, inputs straight from
-// HBM (k_enc_ostage); 2: both tiles — inputs staged, output composed in an
-// LDS image, whole lines out (k_enc_iostage); 3: MODE 0 with nontemporal
-// 16-byte scatter stores (k_enc_stage_nt, tuning key 27 = 3).
-template <int MODE>
-__device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
-    constexpr bool OUT = MODE == 1;
-    constexpr bool NT = MODE == 3;
-    constexpr bool RM = MODE == 4;   // record-major scatter (k_enc_stage_rm, tuning key 27 = 4)
+// Input-staged encode with a record-major scatter: a group of lanes writes
+// all of a record's fields, so its output lines are completed together and
+// leave L2 whole (WRITE 1.00x algorithmic on config 4).  Measured and removed
+// (git history): the field-major scatter (1.23x WRITE), the
+// same with nontemporal stores, an LDS output image composed from HBM inputs
+// or from the staged tile.
+__global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;   // row stride of soff / srel
     uint32_t *soff = (uint32_t *)smem;
@@ -2244,56 +2132,20 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
         }
         return;
     }
-    uint8_t *out = a.xdr + bbase;   // block-relative stream
-    if (OUT) {   // ---- output-staged sub-batches: compose in LDS, then whole lines out
-        const uint32_t mis = (uint32_t)((uintptr_t)out & 15);
-        uint32_t js = 0;
-        uint32_t k1 = enc_out_fit(soff, js, nrec, mis, a.tile_bytes);
-        while (js < nrec) {
-            if (k1 == 0) {   // too large for the tile: the whole block writes record js
-                if (a.framed && tid == 0)
-                    *(uint32_t *)(out + soff[js]) = bswap32r((soff[js + 1] - soff[js] - 4) | kLastFrag);
-                enc_record_block(a, rb + js, bbase + soff[js]);
-                ++js;
-                k1 = js < nrec ? enc_out_fit(soff, js, nrec, mis, a.tile_bytes) : 0;
-                continue;
-            }
-            const uint32_t je = js + k1;
-            const uint32_t head = (mis + soff[js]) & 15u;
-            enc_compose(a, tile, head, rb, js, je, soff, srel, base);
-            __syncthreads();
-            enc_flush(tile, out + soff[js] - head, head, head + soff[je] - soff[js]);
-            js = je;
-            k1 = js < nrec ? enc_out_fit(soff, js, nrec, mis, a.tile_bytes) : 0;   // its barrier ends the tile's use
-        }
-        return;
-    }
-    constexpr bool IMG = MODE == 2;
-    const uint32_t mis = (uint32_t)((uintptr_t)out & 15);
-    const uint32_t ocap = a.tile_bytes + (a.tile_bytes >> 3);   // the output image (MODE 2)
-    uint8_t *const img = tile + a.tile_bytes + kStageSlack;
-    if (a.framed && !IMG && !RM)   // one single-fragment message per record (GrizzlyRpcTransport:103-110)
-        for (uint32_t j = tid; j < nrec; j += kRecThreads)
-            *(uint32_t *)(out + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
+    uint8_t *const out = a.xdr + bbase;   // block-relative stream
     // ---- sub-batches
     uint32_t js = 0;
-    uint32_t k1 = enc_fit(a, base, srel, js, nrec, IMG ? soff : nullptr, mis, ocap);
+    uint32_t k1 = enc_fit(a, base, srel, js, nrec);
     while (js < nrec) {
         if (k1 == 0) {   // too large for the tile: the whole block writes record js
-            if ((IMG || RM) && a.framed && tid == 0)
+            if (a.framed && tid == 0)
                 *(uint32_t *)(out + soff[js]) = bswap32r((soff[js + 1] - soff[js] - 4) | kLastFrag);
             enc_record_block(a, rb + js, bbase + soff[js]);
             ++js;
-            k1 = js < nrec ? enc_fit(a, base, srel, js, nrec, IMG ? soff : nullptr, mis, ocap) : 0;
+            k1 = js < nrec ? enc_fit(a, base, srel, js, nrec) : 0;
             continue;
         }
         const uint32_t je = js + k1;
-        const uint32_t head = (mis + soff[js]) & 15u;
-        // where field bytes go: the stream, or the image (byte 0 = record js's 16-byte line)
-        uint8_t *const wout = IMG ? img + head - soff[js] : out;
-        if (IMG && a.framed)
-            for (uint32_t j = js + tid; j < je; j += kRecThreads)
-                *(uint32_t *)(wout + soff[j]) = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
         // stage every dynamic column's range of the sub-batch
         const uint8_t *a0[kMaxDynLds];
         uint32_t cb[kMaxDynLds + 1];
@@ -2311,12 +2163,12 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
         stage_copy(tile, a0, cb, a.ndyn);   // (stage_dma measured 3.70 vs 3.62 ms here: nothing to overlap)
         __syncthreads();
         const uint32_t m = je - js;
-        if (RM) {   // MODE 4: record-major scatter, a group of lanes writes all of a record
+        {   // record-major scatter: a group of lanes writes all of a record
             const uint64_t rbytes = (uint64_t)(soff[je] - soff[js]) / m;
             const uint32_t G = a.force_g ? a.force_g : pow2_lanes(rbytes, a.lane_bytes_enc);
             const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
             for (uint32_t j = js + tid / G; j < je; j += ng) {
-                uint8_t *rec = wout + soff[j];
+                uint8_t *rec = out + soff[j];
                 uint32_t fpre = a.framed ? 4 : 0, d = 0;
                 if (a.framed && gl == 0)   // the record's mark with its bytes (GrizzlyRpcTransport:103-110)
                     *(uint32_t *)rec = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
@@ -2359,77 +2211,11 @@ __device__ __forceinline__ void k_enc_stage_t(const RecArgs &a) {
                     ++d;
                 }
             }
-            js = je;
-            k1 = js < nrec ? enc_fit(a, base, srel, js, nrec) : 0;   // its barrier ends the tiles' use
-            continue;
-        }
-        // scatter, field-major; field k of record j sits at
-        // soff[j] + (fixed bytes before k) + (dynamic bytes before k)
-        uint32_t fpre = a.framed ? 4 : 0;
-        uint32_t d = 0;
-        for (uint32_t k = 0; k < a.nf; ++k) {
-            const VField &f = a.f[k];
-            if (f.kind != XDRG_K_DYNAMIC) {
-                const uint32_t nw = f.xbytes >> 2;
-                if (nw) {
-                    const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
-                    const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-                    for (uint32_t j = js + tid / G; j < je; j += ng) {
-                        uint8_t *dst = wout + soff[j] + fpre + dyn_before(a, srel, j, d);
-                        for (uint32_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
-                    }
-                }
-                fpre += f.xbytes;
-                continue;
-            }
-            const bool bytes = f.xsz == 1;
-            const uint64_t esz = bytes ? 1 : f.nsz;
-            const uint32_t *rel = srel + d * RS;
-            const uint64_t fbytes = (uint64_t)(rel[je] - rel[js]) * esz + 4ull * m;
-            const uint32_t G = a.force_g ? a.force_g : pow2_lanes(fbytes / m, a.lane_bytes_enc);
-            const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
-            const bool fl = f.type == XDRG_T_FLOAT;
-            // tile offset of the column byte at address x: lds0 + x
-            const int64_t lds0 = 16 * (int64_t)cb[d] - (int64_t)(uintptr_t)a0[d];
-            for (uint32_t j = js + tid / G; j < je; j += ng) {
-                const uint64_t cnt = rel[j + 1] - rel[j];
-                const uint8_t *p = f.data + (base[d] + rel[j]) * esz;
-                uint8_t *dst = wout + soff[j] + fpre + dyn_before(a, srel, j, d);
-                const int64_t L = lds0 + (int64_t)(uintptr_t)p;   // tile offset of p
-                if (bytes) {
-                    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
-                    const uint64_t nch = (1 + ((cnt + 3) >> 2) + 3) >> 2;
-                    for (uint64_t c = gl; c < nch; c += G) {
-                        const uint32_t *w = (const uint32_t *)(tile + (L - sh + 16 * (int64_t)c - 4));
-                        Chunk5 q;
-                        q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = w[4];
-                        blob_store<NT>(dst, q, sh, c, cnt);
-                    }
-                } else {
-                    const uint64_t nch = (1 + cnt + 3) >> 2;
-                    for (uint64_t c = gl; c < nch; c += G) {
-                        const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c - 4));
-                        Chunk5 q;
-                        q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = 0;
-                        w4_store<NT>(dst, q, c, cnt, fl);
-                    }
-                }
-            }
-            ++d;
-        }
-        if (IMG) {   // the image out as whole 16-byte lines
-            __syncthreads();
-            enc_flush(img, out + soff[js] - head, head, head + soff[je] - soff[js]);
         }
         js = je;
-        k1 = js < nrec ? enc_fit(a, base, srel, js, nrec, IMG ? soff : nullptr, mis, ocap) : 0;   // its barrier ends the tiles' use
+        k1 = js < nrec ? enc_fit(a, base, srel, js, nrec) : 0;   // its barrier ends the tile's use
     }
 }
-__global__ __launch_bounds__(kRecThreads) void k_enc_stage(const RecArgs a) { k_enc_stage_t<0>(a); }
-__global__ __launch_bounds__(kRecThreads) void k_enc_ostage(const RecArgs a) { k_enc_stage_t<1>(a); }
-__global__ __launch_bounds__(kRecThreads) void k_enc_iostage(const RecArgs a) { k_enc_stage_t<2>(a); }
-__global__ __launch_bounds__(kRecThreads) void k_enc_stage_nt(const RecArgs a) { k_enc_stage_t<3>(a); }
-__global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) { k_enc_stage_t<4>(a); }
 
 // ---- decode -------------------------------------------------------------------
 // LDS: sstart[RPB + 1] u32 (record start - the block's first start) | snrel[ND][RPB + 1] u32 |
@@ -3131,7 +2917,7 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
     bool full = true;   // every live record decodes every field: byte fields take dec_bytes_lean
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) full &= t0 + j >= nlive || upto[j] == a.nf;
-    const bool lean = __syncthreads_and(full) && a.dec_lean;
+    const bool lean = __syncthreads_and(full);
     // SW: the output-stationary sweep (key 20 = 2; the launcher checked the
     // word columns' alignment and ndyn <= 2) for error-free blocks, record by
     // record otherwise.  meta0 reuses supto (an error-free block's records all
@@ -3241,18 +3027,9 @@ __global__ __launch_bounds__(kRecThreads, XDRG_DEC_SWEEP_OCC) void k_dec_sweep(c
 // ===========================================================================
 // Launchers
 // ===========================================================================
-template <template <int, int> class K>
-static void launch_ur(int u, int r, dim3 grid, size_t lds, hipStream_t st, const RecArgs &a) {
-#define XDRG_UR(U_, R_) \
-    if (u == U_ && r == R_) { hipLaunchKernelGGL((K<U_, R_>::fn), grid, dim3(kRecThreads), lds, st, a); return; }
-    XDRG_UR(1, 1) XDRG_UR(1, 2) XDRG_UR(1, 4)
-    XDRG_UR(2, 1) XDRG_UR(2, 2) XDRG_UR(2, 4)
-    XDRG_UR(4, 1) XDRG_UR(4, 2) XDRG_UR(4, 4)
-#undef XDRG_UR
-}
-template <int U, int R> struct EncG { static constexpr auto fn = k_enc_place_g<U, R>; };
-template <int U, int R> struct DecG { static constexpr auto fn = k_dec_place_g<U, R>; };
-template <int U, int R> struct DecGL { static constexpr auto fn = k_dec_place_g<U, R, true>; };
+// Group kernels: U 16-byte chunks per lane and R records per lane in flight
+// (a U x R sweep on configs 3 and 4 stayed within 5 %: tools/sweep_rec.py).
+constexpr int kGroupU = 2, kGroupR = 1;
 
 int launch_scan_rows(uint64_t *sums, uint64_t nblocks, uint64_t *totals, uint32_t rows, void *stream) {
     if (!rows) return hipSuccess;
@@ -3283,23 +3060,12 @@ bool rec_spec_ok(const RecArgs &a, const Tuning &t) {
     return a.f[a.dyn_idx[a.ndyn - 1]].xsz == 4 && dec_sweep_ok(a, t);   // a word vector last
 }
 
-static void launch_enc_payload(int hoist, int nts, dim3 grid, hipStream_t st, const RecArgs &a) {
-    if (!nts) hipLaunchKernelGGL((k_enc_payload<64, true, false, true>), grid, dim3(256), 0, st, a);   // key 28 = 0
-    else if (hoist) hipLaunchKernelGGL((k_enc_payload<64, true, true, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_enc_payload<64, true, true, false>), grid, dim3(256), 0, st, a);
-}
-static void launch_dec_payload(int hoist, dim3 grid, hipStream_t st, const RecArgs &a) {
-    if (hoist) hipLaunchKernelGGL((k_dec_payload<64, true, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_dec_payload<64, true, false>), grid, dim3(256), 0, st, a);
-}
-
 int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stream) {
     RecArgs a = args;
     a.force_g = t.force_g;
     a.lane_bytes_enc = t.lane_bytes_enc;
     a.lane_bytes_dec = t.lane_bytes_dec;
     a.tile_bytes = t.tile_bytes;
-    a.dec_lean = (uint32_t)t.dec_lean;
     a.big_rec = 0;
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
@@ -3312,18 +3078,14 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     for (uint32_t d = 0; d < a.ndyn && stage; ++d)
         stage = stage_type(a.f[a.dyn_idx[d]].type, a.f[a.dyn_idx[d]].xsz);
     // one dynamic byte field, blocks on the group kernels: the payload kernels move it
-    const bool pay = t.payload && a.pay_pos && a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1 &&
-                     ((stage && t.big_rec) || (grp && !stage && t.rec == 0));
+    const bool pay = a.pay_pos && a.ndyn == 1 && a.f[a.dyn_idx[0]].xsz == 1 && ((stage && t.big_rec) || (grp && !stage));
     a.payk = pay ? 1u : 0u;
     // the derived-count decode's exact rerun (spec_mode 2) runs on a small grid
     // whose blocks loop over the record blocks: when the rerun is not needed
     // its kernels return at once for a few microseconds each
     const dim3 dgrid((unsigned)(a.spec_mode == 2 && nb > 1024 ? 1024 : nb));
-    const uint64_t pblk = (a.n + 3) / 4;   // a wave per record, 4 records per block
-    // (tuning key 34: a smaller grid whose blocks stride over the records,
-    // the resident blocks always on neighbouring records; 0 = a block per 4)
-    const uint64_t pcap = t.pay_grid ? (uint64_t)t.pay_grid : (1ull << 22);
-    const dim3 pgrid((unsigned)(pblk < pcap ? pblk : pcap));
+    const uint64_t pblk = (a.n + 3) / 4;   // payload kernels: a wave per record, 4 records per block
+    const dim3 pgrid((unsigned)(pblk < (1ull << 30) ? pblk : (1ull << 30)));
     switch (phase) {
     case REC_ENC_SIZES: hipLaunchKernelGGL(k_enc_sizes, dim3(nb), dim3(kRecThreads), 0, st, a); break;
     case REC_ENC_SCAN:
@@ -3333,29 +3095,15 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     case REC_ENC_PLACE:
         if (stage) {   // small-record blocks staged, large-record blocks by the group kernel
             a.big_rec = t.big_rec;
-            if (t.enc_out == 4)   // input-staged, record-major scatter (tuning key 27)
-                hipLaunchKernelGGL(k_enc_stage_rm, dim3(nb), dim3(kRecThreads),
-                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
-            else if (t.enc_out == 3)   // input-staged, nontemporal scatter stores (tuning key 27)
-                hipLaunchKernelGGL(k_enc_stage_nt, dim3(nb), dim3(kRecThreads),
-                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
-            else if (t.enc_out == 2)   // staged inputs, output image (tuning key 27)
-                hipLaunchKernelGGL(k_enc_iostage, dim3(nb), dim3(kRecThreads),
-                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack + a.tile_bytes +
-                                       (a.tile_bytes >> 3) + 32, st, a);
-            else if (t.enc_out)   // output-imaged sub-batches, inputs from HBM (tuning key 27)
-                hipLaunchKernelGGL(k_enc_ostage, dim3(nb), dim3(kRecThreads),
-                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
-            else
-                hipLaunchKernelGGL(k_enc_stage, dim3(nb), dim3(kRecThreads),
-                                   enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
-            if (a.big_rec) launch_ur<EncG>(t.enc_u, t.enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
-            if (a.big_rec && pay) launch_enc_payload(t.pay_hoist, t.pay_nts, pgrid, st, a);
-        } else if (lane || (grp && t.rec == 3)) {
+            hipLaunchKernelGGL(k_enc_stage_rm, dim3(nb), dim3(kRecThreads),
+                               enc_stage_meta(a.ndyn) + a.tile_bytes + kStageSlack, st, a);
+            if (a.big_rec) hipLaunchKernelGGL((k_enc_place_g<kGroupU, kGroupR>), dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
+            if (a.big_rec && pay) hipLaunchKernelGGL(k_enc_payload, pgrid, dim3(256), 0, st, a);
+        } else if (lane) {
             hipLaunchKernelGGL(k_enc_lane, dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
-            launch_ur<EncG>(t.enc_u, t.enc_r, dim3(nb), enc_lds_bytes(a.ndyn), st, a);
-            if (pay) launch_enc_payload(t.pay_hoist, t.pay_nts, pgrid, st, a);
+            hipLaunchKernelGGL((k_enc_place_g<kGroupU, kGroupR>), dim3(nb), dim3(kRecThreads), enc_lds_bytes(a.ndyn), st, a);
+            if (pay) hipLaunchKernelGGL(k_enc_payload, pgrid, dim3(256), 0, st, a);
         }
         else hipLaunchKernelGGL(k_enc_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;
@@ -3388,20 +3136,14 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
             else if (loop) hipLaunchKernelGGL(k_dec_stage<true>, dgrid, dim3(kRecThreads), lds, st, a);
             else hipLaunchKernelGGL(k_dec_stage<false>, dim3(nb), dim3(kRecThreads), lds, st, a);
             // (the derived-count pass hands any big-record block to the exact rerun)
-            if (a.big_rec && loop) launch_ur<DecGL>(t.dec_u, t.dec_r, dgrid, dec_g_lds_bytes(a.ndyn), st, a);
-            else if (a.big_rec && !(a.spec_mode & 1)) launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
-            if (a.big_rec && pay) launch_dec_payload(t.pay_hoist, pgrid, st, a);
-        } else if (lane || (grp && t.rec == 3)) {
-            if (t.lane_tile && !a.byref) {   // records staged through an LDS tile (tuning key 35)
-                a.tile_bytes = (uint32_t)t.lane_tile;
-                hipLaunchKernelGGL(k_dec_lane<true>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn) + t.lane_tile,
-                                   st, a);
-            } else {
-                hipLaunchKernelGGL(k_dec_lane<false>, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
-            }
+            if (a.big_rec && loop) hipLaunchKernelGGL((k_dec_place_g<kGroupU, kGroupR, true>), dgrid, dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+            else if (a.big_rec && !(a.spec_mode & 1)) hipLaunchKernelGGL((k_dec_place_g<kGroupU, kGroupR>), dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+            if (a.big_rec && pay) hipLaunchKernelGGL(k_dec_payload, pgrid, dim3(256), 0, st, a);
+        } else if (lane) {
+            hipLaunchKernelGGL(k_dec_lane, dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
         } else if (grp) {
-            launch_ur<DecG>(t.dec_u, t.dec_r, dim3(nb), dec_g_lds_bytes(a.ndyn), st, a);
-            if (pay) launch_dec_payload(t.pay_hoist, pgrid, st, a);
+            hipLaunchKernelGGL((k_dec_place_g<kGroupU, kGroupR>), dim3(nb), dim3(kRecThreads), dec_g_lds_bytes(a.ndyn), st, a);
+            if (pay) hipLaunchKernelGGL(k_dec_payload, pgrid, dim3(256), 0, st, a);
         }
         else hipLaunchKernelGGL(k_dec_place_wave, dim3(nb), dim3(kRecThreads), 0, st, a);
         break;

@@ -344,31 +344,20 @@ extern "C" int xdrg_abi_version(void) { return XDRG_ABI_VERSION; }
 int xdrg::set_tuning(Tuning &t, int key, long long v) {
     auto in = [&](long long lo, long long hi) { return v >= lo && v <= hi; };
     switch (key) {
-    case 4: case 5: case 10: case 11:
-        if (v != 1 && v != 2 && v != 4) return -1;
-        (key == 4 ? t.enc_u : key == 5 ? t.dec_u : key == 10 ? t.enc_r : t.dec_r) = (int32_t)v;
-        return 0;
     case 6: if (!in(0, 64) || (v & (v - 1))) return -1; t.force_g = (uint32_t)v; return 0;
     case 7: case 8: if (!in(4, 65536)) return -1; (key == 7 ? t.lane_bytes_enc : t.lane_bytes_dec) = (uint32_t)v; return 0;
-    case 9: if (v != 0 && v != 3 && v != 4) return -1; t.rec = (int32_t)v; return 0;
+    case 9: if (v != 0 && v != 4) return -1; t.rec = (int32_t)v; return 0;
     case 12: if (!in(1024, 98304) || (v & 15)) return -1; t.tile_bytes = (uint32_t)v; return 0;
     case 13: if (!in(0, 1ll << 31)) return -1; t.big_rec = (uint32_t)v; return 0;
     case 14: if (!in(1, 2)) return -1; t.framed = (int32_t)v; return 0;
     case 16: if (!in(0, 2)) return -1; t.words = (int32_t)v; return 0;
-    case 18: if (!in(0, 1)) return -1; t.payload = (int32_t)v; return 0;
-    case 20: if (!in(0, 2)) return -1; t.dec_lean = (int32_t)v; return 0;
-    case 24: if (!in(0, 1)) return -1; t.pay_hoist = (int32_t)v; return 0;
+    case 20: if (!in(1, 2)) return -1; t.dec_lean = (int32_t)v; return 0;
     case 25: if (!in(1024, 32768) || (v & 15)) return -1; t.sweep_tile = (uint32_t)v; return 0;
     case 26: if (!in(0, 1)) return -1; t.stage_copy = (int32_t)v; return 0;
-    case 27: if (!in(0, 4)) return -1; t.enc_out = (int32_t)v; return 0;
-    case 28: if (!in(0, 1)) return -1; t.pay_nts = (int32_t)v; return 0;
     case 29: if (!in(0, 1)) return -1; t.stride_check = (int32_t)v; return 0;
-    case 30: if (!in(0, 1)) return -1; t.frame_bytes = (int32_t)v; return 0;
     case 31: if (!in(0, 2)) return -1; t.spec_sizes = (int32_t)v; return 0;
     case 32: if (v != 64 && v != 32 && v != 16 && v != 8 && v != 4) return -1; t.grp_enc_lanes = (int32_t)v; return 0;
     case 33: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.grp_dec_tile = (int32_t)v; return 0;
-    case 34: if (!in(0, 1 << 22)) return -1; t.pay_grid = (int32_t)v; return 0;
-    case 35: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.lane_tile = (int32_t)v; return 0;
     case 36: if (!in(1, 64)) return -1; t.emit_per = (int32_t)v; return 0;
     default: return -1;
     }
@@ -1430,22 +1419,51 @@ static void stage_schema(const xdrg_schema *s, hs::Schema &v) {
     v.var_size = s->var_size;
 }
 
-// Device views of host columns (XDRG_HOST_MAPPED).
-static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n,
+// Device views of host columns (XDRG_HOST_MAPPED).  Every span a kernel may
+// touch must lie inside one registration (or one pinned allocation): a fixed
+// column's rows, a dynamic column's n + 1 offsets and its values (encode:
+// offsets[n] elements; decode: cap), a group member's rows over the batch's
+// elements (encode: the group's offsets[n]; decode: the group's element
+// capacity).  A buffer registered shorter than its use is refused.
+static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool decode,
                        std::vector<xdrg_column> &out) {
     out.assign(cols, cols + s->f.size());
+    auto rows_of = [&](size_t k) -> uint64_t {   // native rows of field k's column
+        if (!s->grp[k]) return n;
+        const size_t g = s->grp[k] - 1;
+        const xdrg_field &gf = s->f[g];
+        if (gf.kind == XDRG_K_FIXED) return n * gf.count;
+        if (decode) return cols[g].cap;
+        return n ? cols[g].offsets[n] : 0;   // host memory: the caller's group offsets
+    };
     for (size_t k = 0; k < s->f.size(); ++k) {
         xdrg_column &d = out[k];
-        if (d.offsets) {
-            d.offsets = (uint64_t *)span_device(cols[k].offsets, 8);
-            if (!d.offsets) return inval(c, "XDRG_HOST_MAPPED: column offsets not registered");
+        const xdrg_field &f = s->f[k];
+        const uint64_t rows = rows_of(k);
+        if (f.type == XDRG_T_GROUP) {
+            if (d.offsets && f.kind != XDRG_K_FIXED) {
+                d.offsets = (uint64_t *)span_device(cols[k].offsets, (n + 1) * 8);
+                if (!d.offsets) return inval(c, "XDRG_HOST_MAPPED: group offsets not registered for n + 1 entries");
+            }
+            continue;
         }
-        if (d.data) {
-            d.data = span_device(cols[k].data, 1);
-            if (!d.data) return inval(c, "XDRG_HOST_MAPPED: column data not registered");
+        if (f.kind == XDRG_K_DYNAMIC) {
+            d.offsets = (uint64_t *)span_device(cols[k].offsets, (rows + 1) * 8);
+            if (!d.offsets) return inval(c, "XDRG_HOST_MAPPED: column offsets not registered for every row + 1");
+            const uint64_t vals = decode ? cols[k].cap : (rows ? cols[k].offsets[rows] : 0);
+            if (d.data || vals) {
+                d.data = span_device(cols[k].data, vals * s->nsz[k]);
+                if (!d.data) return inval(c, "XDRG_HOST_MAPPED: column values not registered for their extent");
+            }
+            continue;
         }
+        if (!d.data) continue;
+        const uint64_t elem = (uint64_t)s->nsz[k] * (f.kind == XDRG_K_FIXED ? f.count : 1);
+        const int64_t st = eff_stride(s, k, cols[k]);
+        const uint64_t span = rows == 0 || st == 0 ? elem : (uint64_t)st * (rows - 1) + elem;
+        d.data = span_device(cols[k].data, span);
+        if (!d.data) return inval(c, "XDRG_HOST_MAPPED: column data not registered for every row");
     }
-    (void)n;
     return XDRG_OK;
 }
 
@@ -1468,10 +1486,10 @@ static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
     const uint32_t dflags = flags & XDRG_FRAME_RM;
     if (flags & XDRG_HOST_MAPPED) {
         std::vector<xdrg_column> dc;
-        rc = mapped_cols(c, s, cols, n, dc);
+        rc = mapped_cols(c, s, cols, n, false, dc);
         if (rc) return rc;
-        uint8_t *dout = n ? (uint8_t *)span_device(out, 1) : out;
-        uint64_t *drec = rec_offsets ? (uint64_t *)span_device(rec_offsets, 8) : nullptr;
+        uint8_t *dout = n ? (uint8_t *)span_device(out, out_cap) : out;
+        uint64_t *drec = rec_offsets ? (uint64_t *)span_device(rec_offsets, (n + 1) * 8) : nullptr;
         if ((n && !dout) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
         return encode_impl(c, s, dc.data(), n, dout, out_cap, drec, dflags, out_len, 0, nullptr);
     }
@@ -1504,7 +1522,7 @@ static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
     const uint32_t dflags = flags & XDRG_FRAME_RM;
     if (flags & XDRG_HOST_MAPPED) {
         std::vector<xdrg_column> dc;
-        rc = mapped_cols(c, s, cols, n, dc);
+        rc = mapped_cols(c, s, cols, n, true, dc);
         if (rc) return rc;
         const uint8_t *din = in_len ? (const uint8_t *)span_device(in, in_len) : in;
         const uint64_t *drec = rec_offsets ? (const uint64_t *)span_device(rec_offsets, (n + 1) * 8) : nullptr;
@@ -1595,7 +1613,7 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
         HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 48, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (c->h_stat[2] == kFUnal) {
-            if (len < kFByteMaxLen && c->tune.frame_bytes) {
+            if (len < kFByteMaxLen) {
                 rc = frame_ws(c, frame_positions(len, 1), ws);
                 if (rc) return rc;
                 HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));

@@ -134,7 +134,7 @@ struct RecArgs {
                                // kernels, the others the staged ones (0: one kernel for all)
     uint32_t ncond;            // conditional fields in the schema (0: every record has all fields)
     uint32_t byref;            // 0, or 1 + the field encoded by reference / decoded as a view
-    uint32_t dec_lean;         // staged decode: byte fields of error-free blocks by dec_bytes_lean
+    uint32_t rsv0;
     uint64_t *ref_pos;         // byref: encode splice[n] / decode payload_pos[n]
     uint32_t payk;             // 0, or 1 + the dynamic byte field the payload kernels move for the
                                // group kernels' blocks (k_enc/dec_payload)
@@ -172,15 +172,11 @@ constexpr unsigned long long kNoError = ~0ull;
 struct Tuning {
     int32_t words = 2;              // key 16: fixed 4-byte-word schemas: 2 LDS-staged, 1 lane per record, 0 word-map
     int32_t framed = 2;             // key 14: record-marked AoS decode: 2 lean, 1 wave-LDS transpose
-    int32_t rec = 4;                // key 9: record path: 4 staged sub-batches, 0 group per record, 3 lane per record
-    int32_t pay_hoist = 1;          // key 24: payload kernels: 1 metadata loads issued before the block
-                                    // checks, 0 checks first (A/B)
-    int32_t payload = 1;            // key 18: one dynamic byte field on group-kernel blocks: 1 payload kernels, 0 in place
-    int32_t dec_lean = 2;           // key 20: staged decode, byte fields of error-free blocks: 1 whole
-                                    // boundary dwords (dec_bytes_lean), 0 byte-stored record edges,
-                                    // 2 every dynamic field by the output-stationary sweep
-    int32_t enc_u = 2, dec_u = 2;   // keys 4/5: group kernels, 16-byte chunks per lane in flight
-    int32_t enc_r = 1, dec_r = 1;   // keys 10/11: group kernels, records per lane in flight
+    int32_t rec = 4;                // key 9: record path: 4 staged sub-batches (large-record blocks on the
+                                    // group kernels), 0 group kernels for every block
+    int32_t dec_lean = 2;           // key 20: staged decode of <= 2 dynamic fields: 2 the output-stationary
+                                    // sweep (k_dec_sweep), 1 record groups writing whole boundary dwords
+                                    // (k_dec_stage, the kernel of 3-4 dynamic fields)
     uint32_t force_g = 0;           // key 6: lanes per record (0 = sized from the field)
     uint32_t lane_bytes_enc = 64;   // keys 7/8: group sizing, XDR bytes per lane (encode 64: the
                                     // record-major staged encode's 4 lanes per config-4 record)
@@ -189,24 +185,12 @@ struct Tuning {
     uint32_t sweep_tile = 21504;    // key 25: the sweep decode's LDS tile (k_dec_sweep, 4 blocks per CU)
     uint32_t big_rec = 1024;        // key 13: blocks averaging >= this many XDR bytes per record
                                     // take the group kernels (0 = never)
-    int32_t frame_bytes = 1;        // key 30: a frame walk whose chain meets a size % 4 != 0: 1 the
-                                    // parallel byte-mode walk, 0 the serial walk
     int32_t stride_check = 1;       // key 29: fixed-size decode at rec_offsets: 1 check for the fixed
                                     // stride and take the stride kernels (sync calls), 0 the record path
-    int32_t pay_nts = 1;            // key 28: encode payload kernel: 1 nontemporal 16-byte stores, 0 plain
-    int32_t enc_out = 4;            // key 27: staged encode: 4 input-staged, record-major scatter
-                                    // (k_enc_stage_rm: a record's bytes written together, lines whole
-                                    // in L2), 0 input-staged field-major (k_enc_stage), 1 output image
-                                    // composed from HBM (k_enc_ostage), 2 input-staged + output image
-                                    // (k_enc_iostage), 3 field-major with nontemporal stores
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
     int32_t emit_per = 4;           // key 36: frame walk, sub-chunks per k_fr_emit block (at most;
                                     // halved until the grid has >= 64 blocks)
-    int32_t lane_tile = 0;          // key 35: lane-per-record decode (conditional schemas), LDS tile
-                                    // per sub-batch of records (0: records read from HBM)
-    int32_t pay_grid = 0;           // key 34: payload kernels' grid (blocks striding over the records;
-                                    // 0 = a block per 4 records)
     int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of
                                     // records (0: each lane walks its record in HBM)
     int32_t grp_enc_lanes = 8;      // key 32: repeated-group encode, lanes per record (64 = a wave)
@@ -217,6 +201,13 @@ struct Tuning {
                                     // in one pass (the sweep walks its block and looks back for its
                                     // native offsets: no sizes or scan kernel), 0 walk all
 };
+// Kernel variants measured slower in every A/B and removed (DESIGN.md §5,
+// git history): keys 4/5/10/11 (group kernels' loads in flight), 18 (payload
+// in the group kernels), 20 = 0 (byte-stored record edges), 24 (payload
+// checks before loads), 27 = 0-3 (field-major / output-image / nontemporal
+// staged encode), 28 (plain payload stores), 30 (serial frame walk for odd
+// fragment sizes), 34 (payload grid stride), 35 (LDS-tiled lane decode),
+// key 9 = 3 (lane-per-record kernels for unconditional schemas).
 int set_tuning(Tuning &t, int key, long long value);   // 0, or -1 for an unknown key / bad value
 
 // ---- launchers (kernels_*.hip) -----------------------------------------

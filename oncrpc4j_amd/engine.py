@@ -181,11 +181,6 @@ class Context:
             _raise(rc)
         self._h = h
         self.device = device
-        # measurement runs (rocprofv3 over bench.py) may force kernel choices:
-        # XDRG_TUNE="key=value,key=value" (see tune())
-        for kv in filter(None, os.environ.get("XDRG_TUNE", "").split(",")):
-            k, v = kv.split("=")
-            self.tune(int(k), int(v))
 
     @property
     def handle(self):
@@ -289,6 +284,20 @@ class Context:
         if rc not in (abi.OK, abi.E_INCOMPLETE):
             _raise(rc, self._h)
         return nm.value, used.value
+
+    def apply_tuning(self, spec):
+        """Measurement tools only (bench.py, tools/): force kernel choices from
+        a "key=value,key=value" string such as the XDRG_TUNE variable those
+        tools read.  A context never reads the environment by itself."""
+        for kv in filter(None, (x.strip() for x in (spec or "").split(","))):
+            k, sep, v = kv.partition("=")
+            try:
+                if not sep:
+                    raise ValueError
+                key, value = int(k), int(v)
+            except ValueError:
+                raise ValueError(f"tuning entry {kv!r}: expected key=value with integers") from None
+            self.tune(key, value)
 
     def tune(self, key, value=0):
         """Force one of this context's kernel choices (xdrg_internal.h Tuning:

@@ -164,20 +164,10 @@ def _random_cond_batch(fields, conds, n, seed):
     return hb
 
 
-@pytest.fixture(params=[0, 16384, 1024], ids=lambda t: f"tile{t}")
-def lane_tile(request, gpu_ctx):
-    """Lane-per-record decode of conditional tapes: records staged through an
-    LDS tile (tuning key 35; 0 the default: read from HBM, 16 KiB, 1 KiB: most
-    sub-batches of one record, larger records from HBM)."""
-    gpu_ctx.tune(35, request.param)
-    yield request.param
-    gpu_ctx.tune(0)
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted({b["name"] for b in BATCHES}))
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
-def test_gpu_cond_random_vs_oracle(gpu_ctx, lane_tile, name, framed):
+def test_gpu_cond_random_vs_oracle(gpu_ctx, name, framed):
     b = next(x for x in BATCHES if x["name"] == name)
     fields = [tuple(f) for f in b["fields"]]
     conds = _conds(b)
@@ -199,7 +189,7 @@ def test_gpu_cond_random_vs_oracle(gpu_ctx, lane_tile, name, framed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["result_union", "nested", "bool_union"])
-def test_gpu_cond_errors_vs_oracle(gpu_ctx, lane_tile, name):
+def test_gpu_cond_errors_vs_oracle(gpu_ctx, name):
     """Truncations and negative lengths inside arms: the engine reports the
     first failing record and the code a sequential decode throws."""
     b = next(x for x in BATCHES if x["name"] == name)

@@ -6,7 +6,7 @@ fixtures.  Streams span several 1 MiB super-chunks, carry fragments of many
 sizes (the re-fragmenter of ctest/rpc/RpcMessageParserTCPTest.java:161-181,
 oracle.fragment), bodies full of small integers that look like marks, cut
 tails, and fragment sizes that are not multiples of 4 (the byte-position
-walk, tuning key 30 = 1, and the serial walk, key 30 = 0, must agree)."""
+walk; the serial walk that a stream not 4-byte aligned takes must agree)."""
 import numpy as np
 import pytest
 
@@ -32,6 +32,15 @@ def _dev(b):
     return torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy()).cuda()
 
 
+def _dev_at(b, shift):
+    """(address, owner): the stream `shift` bytes past a 16-byte boundary
+    (a stream that is not 4-byte aligned takes the serial walk)."""
+    t = torch.zeros(len(b) + 16, dtype=torch.uint8, device="cuda")
+    if b:
+        t[shift:shift + len(b)] = torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy()).cuda()
+    return t.data_ptr() + shift, t
+
+
 def build(rng, nmsg, aligned=True, big=0, marks_in_body=False):
     """-> (stream, bodies): nmsg messages, each re-fragmented."""
     bodies, parts = [], []
@@ -53,10 +62,10 @@ def build(rng, nmsg, aligned=True, big=0, marks_in_body=False):
     return b"".join(parts), bodies
 
 
-def check(ctx, stream, bodies_all=None, cap=1 << 22):
+def check(ctx, stream, bodies_all=None, cap=1 << 22, shift=0):
     rc, want = oracle.frame_scan(stream, cap)
     k_want = len(want) - 1
-    dev = _dev(stream)
+    dev, _owner = _dev_at(stream, shift) if shift else (_dev(stream), None)
     offs = torch.zeros(cap + 1, dtype=torch.int64, device="cuda")
     k = ctx.frame_scan(dev, len(stream), offs, cap)
     assert k == k_want
@@ -98,17 +107,13 @@ def test_parallel_walk_cut_tails(gpu_ctx):
         check(gpu_ctx, stream[:cut], bodies)
 
 
-@pytest.fixture(params=[1, 0], ids=["byte_walk", "serial_walk"])
-def odd_walk(request, gpu_ctx):
-    gpu_ctx.tune(30, request.param)
-    yield request.param
-    gpu_ctx.tune(0)
-
-
-def test_unaligned_fragment_sizes(gpu_ctx, odd_walk):
+@pytest.mark.parametrize("shift", [0, 1, 3], ids=["byte_walk", "serial_walk1", "serial_walk3"])
+def test_unaligned_fragment_sizes(gpu_ctx, shift):
+    """Fragment sizes % 4 != 0: the parallel byte-position walk (an aligned
+    stream) and the serial walk (a stream 1 or 3 bytes off alignment)."""
     rng = np.random.default_rng(8)
     stream, bodies = build(rng, 3000, aligned=False)
-    k, _ = check(gpu_ctx, stream, bodies)
+    k, _ = check(gpu_ctx, stream, bodies, shift=shift)
     assert k == len(bodies)
 
 

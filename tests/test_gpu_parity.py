@@ -35,27 +35,22 @@ SCHEMAS = {
     "words_mixed": [(I, SC, 0), (F, SC, 0), (H, SC, 0), (D, SC, 0), (O, FX, 8), (I, FX, 2)],
     "odd_words": [(I, SC, 0)] * 3,
     "big_fixed": [(I, FX, 200), (O, FX, 37)],   # beyond the word-map limit -> record path
+    # one dynamic byte field between fixed fields of every width: the payload
+    # kernels decode head and tail words around it
+    "head_payload_tail": [(I, SC, 0), (H, SC, 0), (O, FX, 3), (O, DY, 0), (D, SC, 0), (S, SC, 0), (I, FX, 2)],
 }
 
 
 # Record-path implementations (kernels_rec.hip launch_rec_phase), as tuning
-# (key, value) pairs: key 9 = 4 staged (sub-batches through an LDS tile, the
-# default), key 20 = 0 its byte fields' record edges byte-stored instead of
-# written as whole dwords,
-# key 20 = 1 the byte fields of error-free blocks written record by record
-# with whole boundary dwords instead of by the output-stationary sweep (the
-# default, 2),
-# key 9 = 0 group per record, 3 lane per record.  Tests taking `rec_kernel`
-# run under each.
-REC_KERNELS = {"group": ((9, 0),), "lane": ((9, 3),), "lane_tile": ((9, 3), (35, 16384)), "staged": ((9, 4),),
-               "staged_edges": ((9, 4), (20, 0)),
-               "staged_lean": ((9, 4), (20, 1)),
-               "staged_out": ((9, 4), (27, 1)),    # output image from HBM inputs (k_enc_ostage)
-               "staged_io": ((9, 4), (27, 2)),     # staged inputs + output image (k_enc_iostage)
-               "staged_nt": ((9, 4), (27, 3)),     # staged inputs, nontemporal scatter stores
-               "staged_fm": ((9, 4), (27, 0), (7, 32)),   # staged inputs, field-major scatter
-               "staged_2pass": ((9, 4), (31, 1)),  # derived counts by the sizes pass (default: one pass)
-               "staged_walk": ((9, 4), (31, 0))}   # every count word walked (no derived counts)
+# (key, value) pairs: "staged" = the defaults (key 9 = 4: sub-batches through
+# an LDS tile, the output-stationary sweep decode with one-pass derived counts
+# where it applies, large-record blocks on the group kernels), "staged_walk"
+# the exact walk instead of derived counts (key 31 = 0, the fallback the
+# derived counts rerun), "staged_lean" the record-group staged decode that
+# schemas of 3-4 dynamic fields take (key 20 = 1), "group" the group kernels
+# for every block (key 9 = 0).  Tests taking `rec_kernel` run under each.
+REC_KERNELS = {"staged": ((9, 4),), "staged_walk": ((9, 4), (31, 0)), "staged_lean": ((9, 4), (20, 1)),
+               "group": ((9, 0),)}
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)
@@ -276,13 +271,12 @@ def test_error_parity(gpu_ctx, rec_kernel, name, framed):
             assert g2[:3] == o2[:3], desc
 
 
-@pytest.mark.parametrize("enc_out", [0, 1, 2], ids=["enc_in", "enc_out", "enc_io"])
-@pytest.mark.parametrize("lean", [1, 0, 2], ids=["lean", "edges", "sweep"])
+@pytest.mark.parametrize("lean", [1, 2], ids=["lean", "sweep"])
 @pytest.mark.parametrize("tile", [1024, 4096])
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("name", ["cfg1_int_int_string", "cfg3_6xint_opaque", "cfg4_int_string_intvec",
                                   "dyn_vectors"])
-def test_staged_tile_sizes(gpu_ctx, name, framed, tile, lean, enc_out):
+def test_staged_tile_sizes(gpu_ctx, name, framed, tile, lean):
     """Staged place kernels with small LDS tiles: records whose staged bytes
     exceed the tile take the whole-block direct path, the others form
     sub-batches of every size (dyn_vectors has non-stageable vector types and
@@ -297,7 +291,6 @@ def test_staged_tile_sizes(gpu_ctx, name, framed, tile, lean, enc_out):
     gpu_ctx.tune(25, tile)   # the sweep decode's own tile
     gpu_ctx.tune(13, 0)   # every block staged (no split of large-record blocks to the group kernel)
     gpu_ctx.tune(20, lean)
-    gpu_ctx.tune(27, enc_out)
     try:
         xdr, offs = gpu_encode(gpu_ctx, fields, hb, framed)
         assert xdr == want
@@ -417,26 +410,14 @@ def test_cfg2_full_size_roundtrip(gpu_ctx):
 
 
 # ---- big records (blocks averaging >= 1 KiB: the group kernels) and mixed blocks
-@pytest.fixture(params=[(1, 1), (1, 0), (0, 1)], ids=["pay_wave_nt", "pay_checks_first", "pay_off"])
-def payload(request, gpu_ctx):
-    """Payload kernels for a single dynamic byte field on the group kernels'
-    blocks (kernels_rec.hip k_enc/dec_payload, tuning key 18; key 24 = 0 their
-    block checks before the metadata loads), or the group kernels moving it
-    in place."""
-    gpu_ctx.tune(18, request.param[0])
-    gpu_ctx.tune(24, request.param[1])
-    yield request.param
-    gpu_ctx.tune(18, 1)
-    gpu_ctx.tune(24, 1)
-
-
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
-@pytest.mark.parametrize("name", ["cfg3_6xint_opaque", "cfg4_int_string_intvec", "cfg1_int_int_string"])
-def test_big_records(gpu_ctx, rec_kernel, payload, name, framed):
+@pytest.mark.parametrize("name", ["cfg3_6xint_opaque", "cfg4_int_string_intvec", "cfg1_int_int_string",
+                                  "head_payload_tail"])
+def test_big_records(gpu_ctx, rec_kernel, name, framed):
     """Records of 1-6 KiB (every block big) and a mix of small and big blocks:
     bytes, offsets and values against the oracle; then error parity (cut
     stream, negative / huge length) and a too-small native column.  Under
-    every record-path kernel and payload-kernel variant."""
+    every record-path kernel."""
     fields = SCHEMAS[name]
     for n, dyn in ((3000, (1000, 6000)), (5000, (0, 2600))):
         hb = random_batch(fields, n, seed=zlib.crc32(f"big/{name}/{framed}/{n}".encode()), dyn_len=dyn)

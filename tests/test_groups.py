@@ -301,3 +301,23 @@ def test_gpu_group_encode_capacity(gpu_ctx):
     with pytest.raises(engine.CapacityError):
         gpu_ctx.encode(sch, db.columns(), hb.n, out, need - 4)
     assert not out.any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+def test_gpu_group_extent_past_stream(gpu_ctx, enc_lanes, framed):
+    """rec_offsets[n] beyond in_len while the last record still parses (its
+    extent claims bytes the stream does not hold): decode reads nothing past
+    in_len, and the staged decode's tile is clamped the same way
+    (kernels_group.hip k_grp_dec_place_lds)."""
+    fields = SHAPES["dirlist"]
+    hb = _sane(random_batch(fields, 3000, seed=17, dyn_len=(0, 21), group_len=(0, 6)))
+    rc, xdr, offs = oracle.encode_batch(fields, hb.columns(), hb.n, hb.xdr_total(framed), framed=framed)
+    assert rc == 0
+    ro = offs.astype(np.uint64).copy()
+    ro[-1] += 4096   # the last extent runs 4 KiB past the stream
+    want = HostBatch.empty(fields, hb.n, hb.dyn_caps())
+    wrc, wfb, werr = oracle.decode_batch(fields, xdr, ro, hb.n, want.columns(), framed=framed)
+    rc, fb, err, out = gpu_decode(gpu_ctx, fields, xdr, hb.n, ro, hb.dyn_caps(), framed)
+    assert (rc, fb, err) == (wrc, wfb, werr)
+    assert out.equal(want, upto=wfb)

@@ -37,6 +37,7 @@ def main():
     values = [int(v) for v in a.values.split(",")]
     basek = [tuple(int(x) for x in kv.split("=")) for kv in a.base.split(",") if kv]
     ctx = engine.Context(0, timing=True)
+    ctx.apply_tuning(os.environ.get("XDRG_TUNE"))   # measurement runs only
     ctx.set_stream(torch.cuda.current_stream())
     n = a.records or bench.SIZES[a.config]
     wl = bench.Workload(ctx, a.config, n, a.framed)

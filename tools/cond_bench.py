@@ -59,6 +59,7 @@ def discriminants(fields, conds, hb, rng):
 
 def run(name, fields, conds, n, dyn_len, group_len=(0, 4)):
     ctx = engine.Context(0)
+    ctx.apply_tuning(os.environ.get("XDRG_TUNE"))   # measurement runs only
     ctx.set_stream(torch.cuda.current_stream())
     hb = random_batch(fields, n, seed=3, dyn_len=dyn_len, group_len=group_len, special_floats=False)
     discriminants(fields, conds, hb, np.random.default_rng(3))

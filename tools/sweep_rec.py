@@ -33,6 +33,7 @@ VARIANTS = {
 def run(cfg, variants, rounds):
     n = {3: 16 << 20, 4: 32 << 20}[cfg]
     ctx = engine.Context(0, timing=True)
+    ctx.apply_tuning(os.environ.get("XDRG_TUNE"))   # measurement runs only
     ctx.set_stream(torch.cuda.current_stream())
     wl = bench.Workload(ctx, cfg, n, False)
     res = {}
