@@ -10,6 +10,8 @@
  *   xdr/Xdr.java:39-1039               concrete codec semantics (bit-exact contract)
  *   grizzly/GrizzlyRpcTransport.java:97-110   record-mark prepend on send -> XDRG_FRAME_RM
  *   rpc/RpcMessageParserTCP.java:63-140       record-mark walk on receive -> xdrg_frame_scan
+ *   rpc/RpcMessageParserTCP.java:44-61 + XdrAble.xdrDecode of each message
+ *                                             (host socket buffer)   -> xdrg_receive_batch
  *
  * The reference is per-field and per-record (an XdrAble encodes its fields in
  * declaration order into one Xdr; xdr/XdrAble.java:40,49).  The engine works on
@@ -356,6 +358,56 @@ int  xdrg_frame_scan(xdrg_ctx *ctx, const uint8_t *in, uint64_t len,
 int  xdrg_deframe(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *payload,
                   uint64_t payload_cap, uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs,
                   uint64_t *consumed);
+
+/* ---- receive on host socket buffers --------------------
+ * The reference walks the marks of the host Grizzly Buffer its selector thread
+ * filled (rpc/RpcMessageParserTCP.java:44-61: isAllFragmentsArrived :63-99,
+ * assembleXdr :109-140, the remainder split :57-60) and hands each complete
+ * message to the next filter, whose XdrAble.xdrDecode reads it
+ * (rpc/RpcCall.java:351-354 leaves trailing bytes unread).  These calls take
+ * that buffer where it lives:
+ *   flags 0                                  device pointers (HBM);
+ *   XDRG_HOST_PTRS                           host memory moved through the context's
+ *                                            staging ring in windows: each window is
+ *                                            walked and decoded on the device, and the
+ *                                            next starts at the first byte not consumed
+ *                                            (its tail copied device to device), so each
+ *                                            stream byte crosses PCIe once;
+ *   XDRG_HOST_PTRS | XDRG_HOST_MAPPED        registered host memory (xdrg_host_register)
+ *                                            read and written in place over PCIe.
+ * Every pointer of the call follows the flags (n_msgs, consumed, first_bad and
+ * err are always host pointers).  The calls are synchronous.
+ *
+ * xdrg_frame_scan_ex / xdrg_deframe_ex: xdrg_frame_scan / xdrg_deframe with
+ * those flags and *consumed (the remainder starts there).  On host memory a
+ * deframe delivers the messages whose bodies fit payload_cap and returns
+ * XDRG_E_CAPACITY when a complete message was left for lack of room (the
+ * device form returns XDRG_E_CAPACITY with *consumed = the bytes needed and
+ * delivers nothing).
+ *
+ * xdrg_receive_batch: the walk, then every complete message (at most cap)
+ * decoded as one record of `schema` into cols (xdrg_decode_batch's column
+ * contract; rows = messages, fixed columns hold cap rows): a single-fragment
+ * message decodes in place with its mark checked (XDRG_FRAME_RM), a
+ * multi-fragment one from its assembled body.  *n_msgs = messages delivered,
+ * *consumed = stream bytes they occupy, msg_offsets (nullable, cap + 1
+ * entries) = each delivered message's first mark and *consumed.  Returns
+ * XDRG_OK, XDRG_E_INCOMPLETE (no complete message: STOP), or the first
+ * message's decode error: *first_bad = its index, *err = its code, columns
+ * hold the messages before it, and the call has delivered through it
+ * (*n_msgs = first_bad + 1, *consumed = its end: RpcDispatcher answers such a
+ * call GARBAGE_ARGS, RpcDispatcher.java:126-131, and the caller resumes at
+ * *consumed) — except XDRG_E_CAPACITY, which delivers up to it (*n_msgs =
+ * first_bad) so the caller can retry it with larger columns.  Host staging
+ * takes schemas without repeated groups (groups: device or mapped memory). */
+int  xdrg_frame_scan_ex(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint64_t *msg_offsets,
+                        uint64_t cap, uint64_t *n_msgs, uint64_t *consumed, uint32_t flags);
+int  xdrg_deframe_ex(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *payload,
+                     uint64_t payload_cap, uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs,
+                     uint64_t *consumed, uint32_t flags);
+int  xdrg_receive_batch(xdrg_ctx *ctx, const xdrg_schema *schema, const uint8_t *in, uint64_t len,
+                        uint64_t cap, xdrg_column *cols, uint32_t flags, uint64_t *msg_offsets,
+                        uint64_t *n_msgs, uint64_t *consumed, uint64_t *first_bad, int *err);
 
 /* ---- multi-GPU, one process ---------------------------
  * For a caller that drives several devices from one process (a JVM with one

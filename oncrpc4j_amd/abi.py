@@ -120,6 +120,10 @@ FUNCTIONS = {
                                               ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]),
     "xdrg_frame_scan": (ctypes.c_int, [_P, _P, _U64, _P, _U64, _PU64]),
     "xdrg_deframe": (ctypes.c_int, [_P, _P, _U64, _P, _U64, _P, _U64, _PU64, _PU64]),
+    "xdrg_frame_scan_ex": (ctypes.c_int, [_P, _P, _U64, _P, _U64, _PU64, _PU64, ctypes.c_uint32]),
+    "xdrg_deframe_ex": (ctypes.c_int, [_P, _P, _U64, _P, _U64, _P, _U64, _PU64, _PU64, ctypes.c_uint32]),
+    "xdrg_receive_batch": (ctypes.c_int, [_P, _P, _P, _U64, _U64, ctypes.POINTER(Column), ctypes.c_uint32, _P,
+                                          _PU64, _PU64, _PU64, ctypes.POINTER(ctypes.c_int)]),
     "xdrg_encode_batch_multi": (ctypes.c_int, [_P, ctypes.c_uint32, _P, _P, _P, _P, _U64, _P,
                                                ctypes.c_uint32, _PU64]),
     "xdrg_decode_batch_multi": (ctypes.c_int, [_P, ctypes.c_uint32, _P, _P, _U64, _P, _P, _P,

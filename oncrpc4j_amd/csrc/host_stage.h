@@ -38,6 +38,19 @@
 //                  uint64_t width, uint64_t rows);
 //   int d2h_done(uint32_t s);                    // event: slot s's outputs have left
 //   int grow(uint64_t slot_bytes);               // reallocate the ring (idle) for a larger chunk
+// and, for the receive pipeline (stage_receive):
+//   int scan(uint32_t s, const uint8_t *win, uint64_t wlen, uint64_t cap, uint64_t *offs, int bodies,
+//            uint8_t *body_dst, uint64_t *boffs, uint64_t *res);
+//       host-blocking, on the compute stream (after kernel_begin(s)): the record-mark walk of
+//       win[0, wlen) (RpcMessageParserTCP.java:63-140).  res[0] = complete messages (<= cap),
+//       res[1] = the stream bytes they occupy, res[2] = 1 if every one is a single fragment,
+//       offs[0..res[0]] = their offsets in win.  With bodies == 2 (or 1 and res[2] == 0) their
+//       bodies are also assembled, marks stripped (assembleXdr :109-140), into body_dst (NULL:
+//       the executor's own body buffer, body()), boffs[0..res[0]] = body offsets, res[3] = bytes.
+//   const uint8_t *body();                       // the executor's body buffer (device)
+//   int d2d(uint8_t *dst, const uint8_t *src, uint64_t bytes);   // copy stream, in order with dma_h2d
+//   int offs_copy(uint64_t *dst, const uint64_t *src, uint64_t n, uint64_t delta);   // compute stream:
+//                                                // dst[i] = src[i] + delta
 // Every call returns XDRG_OK or an XDRG_E_* status.
 #pragma once
 
@@ -69,6 +82,7 @@ struct Schema {
     std::vector<Field> f;
     uint64_t fixed_part = 0;   // XDR bytes of the fixed fields
     bool var_size = false;     // dynamic or conditional fields
+    uint64_t min_xdr = 0;      // fewest XDR bytes a well-formed record has (receive: rows per window)
 };
 
 inline uint64_t up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
@@ -684,6 +698,370 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
     if (first_bad) *first_bad = fb;
     if (err) *err = code;
     return code;
+}
+
+// ---------------------------------------------------------------------------
+// receive: a host socket buffer's record-mark walk, then (DECODE) every
+// complete message decoded as one record, or (DEFRAME) the bodies assembled
+// ---------------------------------------------------------------------------
+// RpcMessageParserTCP.handleRead (rpc/RpcMessageParserTCP.java:44-61) walks
+// the marks of the bytes a selector thread read, hands every complete message
+// on (assembleXdr :109-140) and keeps the remainder (:57-60).  Here the host
+// stream moves through the ring in windows; window k is scanned on the device
+// (its complete messages, at most the rows its slot holds), its messages
+// decoded from the same slot, and window k+1 starts at the first byte window k
+// did not consume: its fresh bytes were copied to the next slot already
+// (behind `H` bytes of room), and window k's unconsumed tail is copied device
+// to device in front of them, so every stream byte crosses PCIe once.  A tail
+// longer than the room restages the window from the host; a message longer
+// than a window grows the ring.  A window starts at a message boundary, so it
+// is as aligned on the device as the message is in the stream (XDR: 4 bytes;
+// the parallel walk needs that, an odd-sized fragment before it means the
+// serial walk).
+enum RecvMode { RECV_SCAN = 0, RECV_DEFRAME = 1, RECV_DECODE = 2 };
+
+struct RecvResult {
+    uint64_t n_msgs = 0, consumed = 0, first_bad = 0, payload = 0;
+    int err = XDRG_OK;
+};
+
+// mode RECV_SCAN: message offsets only; RECV_DEFRAME: bodies into the host
+// payload (payload_cap; messages whose bodies do not fit stay undelivered,
+// XDRG_E_CAPACITY); RECV_DECODE: each message one record of *sp into the
+// host columns (xdrg_decode_batch's column contract, rows = messages).
+// msg_offsets (host, nullable): stream offsets of the delivered messages and
+// the end of the last (DEFRAME: body offsets in payload).
+template <class X>
+int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t len, uint64_t cap,
+                  xdrg_column *cols, uint8_t *payload, uint64_t payload_cap, uint64_t *msg_offsets,
+                  RecvResult &out) {
+    out = RecvResult();
+    std::vector<Region> regs;
+    std::vector<uint32_t> dyn;
+    uint64_t minmsg = 4;   // a mark
+    if (mode == RECV_DECODE) {
+        HS_TRY(build_regions(*sp, cols, regs));
+        for (const Region &g : regs)
+            if (!g.stride) return XDRG_E_INVAL;   // constant columns are encode-only
+        for (uint32_t k = 0; k < sp->f.size(); ++k)
+            if (sp->f[k].kind == XDRG_K_DYNAMIC) dyn.push_back(k);
+        if (dyn.size() > 32) return XDRG_E_INVAL;
+        minmsg += sp->min_xdr;
+    }
+    if (msg_offsets) msg_offsets[0] = 0;
+    if (cap == 0 || len < 4) return XDRG_E_INCOMPLETE;
+    Stager<X> st(x);
+    // window geometry for the ring's slot size: room H and fresh bytes F
+    // (multiples of 16), the rows a window may deliver, and where the message
+    // offsets, body offsets, bodies (DEFRAME) and columns (DECODE) sit
+    struct Geo { uint64_t H, F, W, rows, offs, boffs, body, cols, need; };
+    auto geo_for = [&](uint64_t F) {
+        Geo g;
+        g.F = F;
+        g.H = std::max<uint64_t>(up(F / 8, 16), 64);
+        g.W = g.H + g.F;
+        g.rows = std::max<uint64_t>(g.W / minmsg, 1);
+        Bump b;
+        b.take(g.W);
+        g.offs = b.take((g.rows + 1) * 8);
+        g.boffs = b.take((g.rows + 1) * 8);
+        g.body = mode == RECV_DEFRAME ? b.take(g.W) : 0;
+        g.cols = b.used;
+        if (mode == RECV_DECODE) {
+            for (const Region &r : regs) b.take((uint64_t)r.stride * g.rows);
+            for (uint32_t k : dyn) {
+                b.take((g.rows + 1) * 8);
+                b.take((g.W / sp->f[k].xsz + 1) * sp->f[k].nsz);
+            }
+        }
+        g.need = b.used;
+        return g;
+    };
+    auto fit_geo = [&]() {
+        uint64_t F = std::max<uint64_t>(up(x.slot_bytes() / 2, 16), 16);
+        Geo g = geo_for(F);
+        while (g.need > x.slot_bytes() && F > 16) {
+            uint64_t nf = up((uint64_t)((double)F * (double)x.slot_bytes() / (double)g.need * 0.97), 16);
+            F = std::max<uint64_t>(std::min<uint64_t>(nf, F - 16), 16);
+            g = geo_for(F);
+        }
+        return g;
+    };
+    Geo G = fit_geo();
+    if (G.need > x.slot_bytes()) {
+        HS_TRY(x.grow(up(G.need + G.need / 2, 1 << 12)));
+        G = fit_geo();
+        if (G.need > x.slot_bytes()) return XDRG_E_NOMEM;
+    }
+
+    struct Win {               // one window: its slot, where it sits, what it holds
+        uint32_t slot = 0;
+        uint64_t off = 0;      // slot offset of window byte 0
+        uint64_t hpos = 0;     // host stream offset of window byte 0
+        uint64_t wl = 0;       // bytes in the window
+        uint64_t fresh_at = 0; // prefetched fresh bytes: host [fresh_at, fresh_end) at slot offset H
+        uint64_t fresh_end = 0;
+        bool prefetched = false;
+    };
+    struct Chunk {             // a decoded window awaiting its status
+        uint32_t slot;
+        uint64_t lo, m;        // first message index, messages
+        Layout L;              // its columns in the slot
+        std::vector<uint64_t> base, capg;
+        uint64_t hpos;         // host stream offset of its window
+        const uint64_t *doffs; // its messages' window offsets (device, in its slot)
+        uint64_t *hoffs;       // host message offsets [lo, lo + m] (msg_offsets), or NULL
+    };
+    std::deque<Chunk> pend;
+    bool stop = false;
+    std::vector<uint64_t> next_base(mode == RECV_DECODE ? sp->f.size() : 0, 0);
+    auto stage_fresh = [&](Win &w, uint64_t from) -> int {   // the F bytes after `from`, at slot offset H
+        w.fresh_at = from;
+        w.fresh_end = std::min(len, from + G.F);
+        w.prefetched = true;
+        return st.h2d(w.slot, x.slot(w.slot) + G.H, in + from, w.fresh_end - from);
+    };
+    // the oldest decoded window (its kernels are done): status, then its columns out
+    auto settle = [&]() -> int {
+        Chunk &c = pend.front();
+        uint64_t w[2 + 32];
+        HS_TRY(x.wait_kernel(c.slot, w));
+        uint64_t tot[32];
+        for (size_t i = 0; i < dyn.size(); ++i) {
+            // a failing window's totals may not cover its valid prefix (a decode
+            // stops at the error): it hands back every value it was granted
+            tot[i] = w[1] ? c.capg[dyn[i]] : std::min(w[2 + i], c.capg[dyn[i]]);
+            next_base[dyn[i]] = c.base[dyn[i]] + tot[i];
+        }
+        uint8_t *slot = x.slot(c.slot);
+        HS_TRY(x.d2h_begin(c.slot));
+        for (size_t r = 0; r < regs.size(); ++r) {
+            const Region &g = regs[r];
+            uint8_t *h = (uint8_t *)g.base + (uint64_t)g.stride * c.lo;
+            if (g.full) {
+                HS_TRY(st.d2h(c.slot, h, slot + c.L.reg[r], (uint64_t)g.stride * c.m));
+            } else {
+                for (auto &sg : g.segs)
+                    HS_TRY(st.d2h_2d(c.slot, h + sg.first, (uint64_t)g.stride, slot + c.L.reg[r] + sg.first,
+                                     sg.second - sg.first, c.m));
+            }
+        }
+        for (size_t i = 0; i < dyn.size(); ++i) {
+            const uint32_t k = dyn[i];
+            HS_TRY(x.add_u64(1, (uint64_t *)(slot + c.L.off[k]), c.m + 1, c.base[k]));
+            HS_TRY(st.d2h(c.slot, cols[k].offsets + c.lo, slot + c.L.off[k], (c.m + 1) * 8));
+            HS_TRY(st.d2h(c.slot, (uint8_t *)cols[k].data + c.base[k] * sp->f[k].nsz, slot + c.L.val[k],
+                          tot[i] * sp->f[k].nsz));
+        }
+        st.busy[c.slot] = true;
+        HS_TRY(x.d2h_done(c.slot));
+        if (w[1] && !stop) {   // the batch's first failing message (windows are in message order)
+            stop = true;
+            const uint64_t fb = c.lo + w[0];
+            const int e = (int)w[1];
+            // a bad message is delivered (and rejected: GARBAGE_ARGS, RpcDispatcher.java:126-131);
+            // one that did not fit the columns is not
+            const uint64_t upto = e == XDRG_E_CAPACITY ? fb : fb + 1;
+            uint64_t end = 0;
+            if (c.hoffs) {
+                HS_TRY(st.acquire(c.slot));   // its message offsets have landed on the host
+                end = c.hoffs[upto - c.lo];
+            } else {   // the one offset it needs, from the slot
+                HS_TRY(x.d2h_begin(c.slot));
+                HS_TRY(st.d2h(c.slot, &end, (const uint8_t *)(c.doffs + (upto - c.lo)), 8));
+                HS_TRY(x.d2h_done(c.slot));
+                HS_TRY(st.acquire(c.slot));
+                end += c.hpos;
+            }
+            out.first_bad = fb;
+            out.err = e;
+            out.n_msgs = upto;
+            out.consumed = end;
+        }
+        pend.pop_front();
+        return XDRG_OK;
+    };
+
+    const uint32_t S = x.nslots();
+    Win cur;
+    HS_TRY(st.acquire(0));
+    HS_TRY(stage_fresh(cur, 0));
+    cur.off = G.H;
+    cur.wl = cur.fresh_end;
+    HS_TRY(x.h2d_done(0));
+    uint64_t pos = 0, k = 0, pbytes = 0, chunk_no = 0;
+    int rc_final = XDRG_OK;
+    for (;;) {
+        Win nxt;
+        nxt.slot = (uint32_t)((chunk_no + 1) % S);
+        const uint64_t wend = cur.hpos + cur.wl;   // == cur's fresh end
+        // the next window's fresh bytes go out before this walk when its slot is free already
+        if (S >= 3 && wend < len) {
+            HS_TRY(st.acquire(nxt.slot));
+            HS_TRY(stage_fresh(nxt, wend));
+        }
+        uint8_t *slot = x.slot(cur.slot);
+        uint64_t *doffs = (uint64_t *)(slot + G.offs), *dboffs = (uint64_t *)(slot + G.boffs);
+        uint8_t *dbody = mode == RECV_DEFRAME ? slot + G.body : nullptr;
+        const int bodies = mode == RECV_DEFRAME ? 2 : (mode == RECV_DECODE ? 1 : 0);
+        const uint64_t want0 = std::min<uint64_t>(cap - k, G.rows);
+        uint64_t want = want0;
+        uint64_t res[4] = {0, 0, 1, 0};
+        HS_TRY(x.kernel_begin(cur.slot));
+        HS_TRY(x.scan(cur.slot, slot + cur.off, cur.wl, want, doffs, bodies, dbody, dboffs, res));
+        bool room_limited = false;
+        if (mode == RECV_DEFRAME)
+            while (res[0] > 1 && pbytes + res[3] > payload_cap) {   // the bodies that fit
+                room_limited = true;
+                want = std::min<uint64_t>(res[0] - 1, std::max<uint64_t>(1, (uint64_t)((double)res[0] *
+                       (double)(payload_cap - pbytes) / (double)res[3])));
+                HS_TRY(x.scan(cur.slot, slot + cur.off, cur.wl, want, doffs, bodies, dbody, dboffs, res));
+            }
+        // the previous window's kernels ran before this walk (one compute stream): settle it
+        while (!pend.empty()) HS_TRY(settle());
+        if (stop) break;
+        const uint64_t m = res[0], used = res[1];
+        if (mode == RECV_DEFRAME && m && pbytes + res[3] > payload_cap) {
+            rc_final = XDRG_E_CAPACITY;   // not one more body fits the payload buffer
+            break;
+        }
+        if (m == 0) {
+            if (wend == len) break;   // the remainder is not a complete message: STOP (:51-53)
+            // the message at pos is longer than a window: drain, grow the ring, restage
+            HS_TRY(st.drain());
+            HS_TRY(x.grow(up(x.slot_bytes() * 2, 1 << 12)));
+            G = fit_geo();
+            chunk_no = 0;
+            cur = Win();
+            cur.hpos = pos;
+            cur.wl = std::min(len - pos, G.W);
+            cur.fresh_end = pos + cur.wl;
+            HS_TRY(st.h2d(0, x.slot(0), in + pos, cur.wl));
+            HS_TRY(x.h2d_done(0));
+            continue;
+        }
+        // deliver: message offsets, then the bodies or the decoded records
+        const uint64_t lo = k;
+        Chunk c;
+        c.slot = cur.slot;
+        c.lo = lo;
+        c.m = m;
+        c.hpos = cur.hpos;
+        c.doffs = doffs;
+        c.hoffs = msg_offsets ? msg_offsets + lo : nullptr;
+        if (mode == RECV_DECODE) {
+            Bump b;
+            b.used = G.cols;
+            c.L.reg.assign(regs.size(), 0);
+            c.L.off.assign(sp->f.size(), 0);
+            c.L.val.assign(sp->f.size(), 0);
+            c.base.assign(sp->f.size(), 0);
+            c.capg.assign(sp->f.size(), 0);
+            std::vector<xdrg_column> dc(sp->f.size());
+            for (size_t r = 0; r < regs.size(); ++r) {
+                c.L.reg[r] = b.take((uint64_t)regs[r].stride * m, (uintptr_t)(regs[r].base + (uint64_t)regs[r].stride * lo));
+                for (uint32_t k2 : regs[r].fields) {
+                    dc[k2].data = slot + c.L.reg[r] + ((const uint8_t *)cols[k2].data - regs[r].base);
+                    dc[k2].stride = cols[k2].stride;
+                }
+            }
+            for (uint32_t k2 = 0; k2 < sp->f.size(); ++k2) {
+                const Field &fd = sp->f[k2];
+                if (fd.kind == XDRG_K_DYNAMIC) {
+                    c.L.off[k2] = b.take((m + 1) * 8);
+                    const uint64_t vc = cur.wl / fd.xsz + 1;   // a window holds at most this many elements
+                    c.L.val[k2] = b.take(vc * fd.nsz);
+                    c.base[k2] = next_base[k2];
+                    const uint64_t left = cols[k2].cap > c.base[k2] ? cols[k2].cap - c.base[k2] : 0;
+                    c.capg[k2] = std::min(left, vc);
+                    dc[k2].data = slot + c.L.val[k2];
+                    dc[k2].offsets = (uint64_t *)(slot + c.L.off[k2]);
+                    dc[k2].cap = c.capg[k2];
+                } else if (!fixed_elem_bytes(fd)) {
+                    dc[k2].data = slot;
+                    dc[k2].stride = 0;
+                }
+            }
+            if (b.used > x.slot_bytes()) return XDRG_E_NOMEM;   // (the geometry reserved G.rows rows)
+            // single fragments decode in place, record-marked (one mark per message,
+            // GrizzlyRpcTransport.java:103-110); assembled bodies without marks
+            const bool single = res[2] != 0;
+            if (single) {
+                HS_TRY(x.offs_copy(dboffs, doffs, m + 1, cur.off));   // window -> slot offsets
+                HS_TRY(x.decode(cur.slot, slot, cur.off + cur.wl, dboffs, m, dc.data(), XDRG_FRAME_RM));
+            } else {
+                HS_TRY(x.decode(cur.slot, x.body(), res[3], dboffs, m, dc.data(), 0));
+            }
+            std::vector<const uint64_t *> extra;
+            for (uint32_t k2 : dyn) extra.push_back((const uint64_t *)(slot + c.L.off[k2]) + m);
+            HS_TRY(x.kernel_end(cur.slot, extra.data(), (uint32_t)extra.size()));
+            if (c.hoffs) {   // the caller's message offsets (without them the device copy stays
+                HS_TRY(x.d2h_begin(cur.slot));   // window-relative: an error reads one entry, settle)
+                HS_TRY(x.add_u64(1, doffs, m + 1, cur.hpos));
+                HS_TRY(st.d2h(cur.slot, c.hoffs, (const uint8_t *)doffs, (m + 1) * 8));
+                HS_TRY(x.d2h_done(cur.slot));
+            }
+            pend.push_back(std::move(c));
+        } else {
+            HS_TRY(x.kernel_end(cur.slot, nullptr, 0));
+            HS_TRY(x.d2h_begin(cur.slot));
+            if (mode == RECV_DEFRAME) {
+                HS_TRY(st.d2h(cur.slot, payload + pbytes, dbody, res[3]));
+                HS_TRY(x.add_u64(1, dboffs, m + 1, pbytes));
+                if (c.hoffs) HS_TRY(st.d2h(cur.slot, c.hoffs, (const uint8_t *)dboffs, (m + 1) * 8));
+                pbytes += res[3];
+            } else if (c.hoffs) {
+                HS_TRY(x.add_u64(1, doffs, m + 1, cur.hpos));
+                HS_TRY(st.d2h(cur.slot, c.hoffs, (const uint8_t *)doffs, (m + 1) * 8));
+            }
+            st.busy[cur.slot] = true;
+            HS_TRY(x.d2h_done(cur.slot));
+        }
+        k += m;
+        pos += used;
+        if (room_limited) { rc_final = XDRG_E_CAPACITY; break; }
+        if (k == cap || pos == len || (wend == len && m < want0)) break;
+        // the next window: this one's unconsumed tail, then the fresh bytes
+        if (S == 1) {   // one slot: this window leaves first, the next restages from the host
+            while (!pend.empty()) HS_TRY(settle());
+            HS_TRY(st.drain());
+            if (stop) break;
+        }
+        const uint64_t tail = wend - pos;
+        if (S >= 2 && wend < len && !nxt.prefetched) {
+            HS_TRY(st.acquire(nxt.slot));
+            HS_TRY(stage_fresh(nxt, wend));
+        }
+        if (S >= 2 && tail <= G.H && (nxt.prefetched || wend == len)) {
+            if (!nxt.prefetched) {   // the stream ends in this window: the tail alone
+                HS_TRY(st.acquire(nxt.slot));
+                nxt.fresh_at = nxt.fresh_end = wend;
+            }
+            HS_TRY(x.d2d(x.slot(nxt.slot) + G.H - tail, slot + cur.off + used, tail));
+            nxt.off = G.H - tail;
+            nxt.wl = tail + (nxt.fresh_end - nxt.fresh_at);
+        } else {   // a long tail (or one slot): the window again from the host
+            if (S >= 2) HS_TRY(st.acquire(nxt.slot));
+            nxt.off = 0;
+            nxt.wl = std::min(len - pos, G.W);
+            HS_TRY(st.h2d(nxt.slot, x.slot(nxt.slot), in + pos, nxt.wl));
+        }
+        nxt.hpos = pos;
+        HS_TRY(x.h2d_done(nxt.slot));
+        cur = nxt;
+        ++chunk_no;
+    }
+    while (!pend.empty()) HS_TRY(settle());
+    HS_TRY(st.drain());
+    if (!stop) {
+        out.n_msgs = k;
+        out.consumed = pos;
+        out.first_bad = k;
+    }
+    out.payload = pbytes;
+    if (out.err) return out.err;
+    if (rc_final) return rc_final;
+    return out.n_msgs ? XDRG_OK : XDRG_E_INCOMPLETE;
 }
 
 #undef HS_TRY

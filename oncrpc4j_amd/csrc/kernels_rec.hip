@@ -1533,9 +1533,13 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
     }
 }
 // a block per 4 records (a wave each): neighbouring blocks on neighbouring records
+// (a.xcd: blocks in XCD order, xcd_block; one pass below 2^32 records)
+__device__ __forceinline__ uint64_t pay_block(const RecArgs &a) {
+    return a.xcd ? xcd_block(blockIdx.x, gridDim.x) : (uint64_t)blockIdx.x;
+}
 __global__ __launch_bounds__(256) void k_enc_payload(const RecArgs a) {
-    const uint64_t step = (uint64_t)gridDim.x * (256 / kPayLanes);   // (one pass below 2^32 records)
-    for (uint64_t r = (uint64_t)blockIdx.x * (256 / kPayLanes) + threadIdx.x / kPayLanes; r < a.n; r += step)
+    const uint64_t step = (uint64_t)gridDim.x * (256 / kPayLanes);
+    for (uint64_t r = pay_block(a) * (256 / kPayLanes) + threadIdx.x / kPayLanes; r < a.n; r += step)
         enc_payload_rec(a, r);
 }
 __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
@@ -1549,26 +1553,28 @@ __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
     uint8_t *dst = f.data + o;
     constexpr uint32_t LPR = kPayLanes;
     const uint32_t lane = threadIdx.x % LPR;
-    // the record's fixed fields, a word per lane (the group kernel only placed
-    // the record): the head words before the length word, the tail words
+    // The record's fixed fields, a word per lane (the group kernel only placed
+    // the record): the head words before the length word and the tail words
     // after the payload and its pad (Xdr.java:171-175 each; the walk has
-    // checked every length and bound in the reference's order)
-    {
-        const uint32_t hw = (uint32_t)(a.pay_fb - (a.framed ? 4 : 0)) >> 2;
-        const uint32_t tw = (a.fixed_xdr - a.pay_fb) >> 2;
-        const uint64_t h0 = pos - 4 * (uint64_t)hw, t0 = pos + 4 + cnt + pad4(cnt);
-        for (uint32_t i = lane; i < hw + tw; i += LPR) {
-            const uint32_t v = *(const uint32_t *)(a.xdr + (i < hw ? h0 + 4 * (uint64_t)i : t0 + 4 * (uint64_t)(i - hw)));
-            uint32_t w = i;   // fixed-field word index, declaration order
-            for (uint32_t k = 0; k < a.nf; ++k) {
-                const VField &g = a.f[k];
-                if (g.kind == XDRG_K_DYNAMIC) continue;
-                const uint32_t nw = g.xbytes >> 2;
-                if (w < nw) fixed_store(g, r, 4 * w, v);
-                w = w < nw ? ~0u >> 1 : w - nw;   // (stored: past every later field)
-            }
+    // checked every length and bound in the reference's order).  Their loads
+    // go out with the first payload loads and are stored after them, so a
+    // wave's record costs one memory round trip, not two.
+    const uint32_t hw = (uint32_t)(a.pay_fb - (a.framed ? 4 : 0)) >> 2;
+    const uint32_t nfw = hw + ((a.fixed_xdr - a.pay_fb) >> 2);
+    const uint64_t h0 = pos - 4 * (uint64_t)hw, t0 = pos + 4 + cnt + pad4(cnt);
+    auto fixed_at = [&](uint32_t i) { return *(const uint32_t *)(a.xdr + (i < hw ? h0 + 4 * (uint64_t)i : t0 + 4 * (uint64_t)(i - hw))); };
+    auto fixed_put = [&](uint32_t i, uint32_t v) {
+        uint32_t w = i;   // fixed-field word index, declaration order
+        for (uint32_t k = 0; k < a.nf; ++k) {
+            const VField &g = a.f[k];
+            if (g.kind == XDRG_K_DYNAMIC) continue;
+            const uint32_t nw = g.xbytes >> 2;
+            if (w < nw) fixed_store(g, r, 4 * w, v);
+            w = w < nw ? ~0u >> 1 : w - nw;   // (stored: past every later field)
         }
-    }
+    };
+    const bool hl = lane < nfw;
+    const uint32_t hv = hl ? fixed_at(lane) : 0u;
     const uint64_t nch = (cnt + 15) >> 4;
     for (uint64_t c0 = lane; c0 < nch; c0 += 4 * LPR) {
         u32x4a v[4];
@@ -1594,10 +1600,12 @@ __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
             }
         }
     }
+    if (hl) fixed_put(lane, hv);
+    for (uint32_t i = lane + LPR; i < nfw; i += LPR) fixed_put(i, fixed_at(i));   // > 64 fixed words
 }
 __global__ __launch_bounds__(256) void k_dec_payload(const RecArgs a) {
     const uint64_t step = (uint64_t)gridDim.x * (256 / kPayLanes);
-    for (uint64_t r = (uint64_t)blockIdx.x * (256 / kPayLanes) + threadIdx.x / kPayLanes; r < a.n; r += step)
+    for (uint64_t r = pay_block(a) * (256 / kPayLanes) + threadIdx.x / kPayLanes; r < a.n; r += step)
         dec_payload_rec(a, r);
 }
 
@@ -3067,6 +3075,7 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     a.lane_bytes_dec = t.lane_bytes_dec;
     a.tile_bytes = t.tile_bytes;
     a.big_rec = 0;
+    a.xcd = (uint32_t)t.xcd_order;
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
     // conditional schemas (unions / optional data) and by-reference payloads take

@@ -262,6 +262,8 @@ struct xdrg_ctx {
     double ms[XDRG_KERNEL_COUNT] = {};
     Tuning tune;                // this context's kernel choices (xdrg_internal_tune)
     StageRing ring;             // XDRG_HOST_PTRS staging (allocated on first use)
+    uint8_t *d_rx = nullptr;    // receive scratch: assembled message bodies / message offsets
+    size_t rx_bytes = 0;
 };
 
 static int hip_fail(xdrg_ctx *c, hipError_t e, const char *what) {
@@ -359,6 +361,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 32: if (v != 64 && v != 32 && v != 16 && v != 8 && v != 4) return -1; t.grp_enc_lanes = (int32_t)v; return 0;
     case 33: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.grp_dec_tile = (int32_t)v; return 0;
     case 36: if (!in(1, 64)) return -1; t.emit_per = (int32_t)v; return 0;
+    case 37: if (!in(0, 1)) return -1; t.xcd_order = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -424,6 +427,7 @@ extern "C" int xdrg_ctx_destroy(xdrg_ctx *c) {
     for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
     if (c->d_ws) (void)hipFree(c->d_ws);
     if (c->d_fws) (void)hipFree(c->d_fws);
+    if (c->d_rx) (void)hipFree(c->d_rx);
     if (c->d_stat) (void)hipFree(c->d_stat);
     if (c->h_stat) (void)hipHostFree(c->h_stat);
     delete c;
@@ -465,6 +469,24 @@ static int ensure_ws(xdrg_ctx *c, size_t words) {
     }
     HIPCHK(c, hipMalloc(&c->d_ws, words * sizeof(uint64_t)));
     c->ws_words = words;
+    return XDRG_OK;
+}
+
+// Receive scratch (assembled bodies, message offsets): grown on demand, after
+// the work that may still read it (the context's stream and its ring's
+// compute stream) has finished.
+static int ensure_rx(xdrg_ctx *c, size_t bytes) {
+    if (bytes <= c->rx_bytes) return XDRG_OK;
+    if (c->d_rx) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->ring.comp) HIPCHK(c, hipStreamSynchronize(c->ring.comp));
+        HIPCHK(c, hipFree(c->d_rx));
+        c->d_rx = nullptr;
+        c->rx_bytes = 0;
+    }
+    const size_t want = bytes + bytes / 4 + 4096;
+    HIPCHK(c, hipMalloc(&c->d_rx, want));
+    c->rx_bytes = want;
     return XDRG_OK;
 }
 
@@ -1296,6 +1318,10 @@ static int ring_ready(xdrg_ctx *c, uint64_t slot) {
     return XDRG_OK;
 }
 
+static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *payload, uint64_t payload_cap,
+                      uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs, uint64_t *consumed,
+                      uint64_t *frags, uint64_t *body_bytes);
+
 // host_stage.h executor on one context: copies on the ring's H2D / D2H
 // streams, kernels on its compute stream, ordered by per-slot events.
 struct HipExec {
@@ -1402,6 +1428,45 @@ struct HipExec {
         return XDRG_OK;
     }
     int grow(uint64_t slot) { return ring_ready(c, slot > r.slot ? slot : r.slot); }
+    // receive (hs::stage_receive): the record-mark walk of a slot window on the
+    // compute stream (host-blocking), bodies assembled by a second walk when asked
+    int scan(uint32_t, const uint8_t *win, uint64_t wlen, uint64_t cap, uint64_t *offs, int bodies,
+             uint8_t *body_dst, uint64_t *boffs, uint64_t *res) {
+        hipStream_t keep = c->stream;
+        c->stream = r.comp;
+        uint64_t nm = 0, used = 0, nf = 0;
+        int rc = frame_walk(c, win, wlen, nullptr, 0, offs, cap, &nm, &used, &nf, nullptr);
+        res[0] = res[1] = res[3] = 0;
+        res[2] = 1;
+        if (rc == XDRG_E_INCOMPLETE) rc = XDRG_OK;
+        if (!rc && nm) {
+            res[0] = nm;
+            res[1] = used;
+            res[2] = nf == nm;
+            if (bodies == 2 || (bodies == 1 && nf != nm)) {
+                uint8_t *dst = body_dst;
+                if (!dst) {
+                    rc = ensure_rx(c, used + 64);
+                    dst = c->d_rx;
+                }
+                uint64_t nm2 = 0, used2 = 0, bytes = 0;
+                if (!rc) rc = frame_walk(c, win, wlen, dst, used, boffs, nm, &nm2, &used2, nullptr, &bytes);
+                res[3] = bytes;
+            }
+        }
+        c->stream = keep;
+        return rc;
+    }
+    const uint8_t *body() const { return c->d_rx; }
+    int d2d(uint8_t *dst, const uint8_t *src, uint64_t n) {
+        if (n) HIPCHK(c, hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, r.h2d));
+        return XDRG_OK;
+    }
+    int offs_copy(uint64_t *dst, const uint64_t *src, uint64_t n, uint64_t delta) {
+        HIPCHK(c, hipMemcpyAsync(dst, src, n * 8, hipMemcpyDeviceToDevice, r.comp));
+        HIPCHK(c, (hipError_t)launch_add_u64(dst, n, delta, r.comp));
+        return XDRG_OK;
+    }
     // every copy and kernel of the call has finished (the caller's buffers are free again)
     int finish() {
         HIPCHK(c, hipStreamSynchronize(r.h2d));
@@ -1413,10 +1478,16 @@ struct HipExec {
 
 static void stage_schema(const xdrg_schema *s, hs::Schema &v) {
     v.f.resize(s->f.size());
-    for (size_t k = 0; k < s->f.size(); ++k)
+    uint64_t ndyn = 0;
+    for (size_t k = 0; k < s->f.size(); ++k) {
         v.f[k] = hs::Field{s->f[k].type, s->f[k].kind, s->f[k].count, s->nsz[k], s->xsz[k], s->xbytes[k]};
+        ndyn += s->f[k].kind == XDRG_K_DYNAMIC;
+    }
     v.fixed_part = s->fixed_part;
     v.var_size = s->var_size;
+    // a well-formed record: every fixed field, a length word per dynamic field
+    // (absent arms of a conditional schema may take any of it away)
+    v.min_xdr = s->ncond ? 0 : s->fixed_part + 4 * ndyn;
 }
 
 // Device views of host columns (XDRG_HOST_MAPPED).  Every span a kernel may
@@ -1591,7 +1662,8 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
 // One host round trip for xdrg_frame_scan (two for xdrg_deframe: the payload
 // size is checked before the bodies move).
 static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *payload, uint64_t payload_cap,
-                      uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs, uint64_t *consumed) {
+                      uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs, uint64_t *consumed,
+                      uint64_t *frags = nullptr, uint64_t *body_bytes = nullptr) {
     if (!c || !msg_offsets || !n_msgs) return XDRG_E_INVAL;
     if (len && !in) return inval(c, "stream is NULL");
     if (len > kFMaxLen) return inval(c, "stream longer than 16 GiB");
@@ -1639,6 +1711,7 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
     // [5] fragments of the first cap messages
     const uint64_t M = c->h_stat[2 + 4];
     const uint64_t nout = M < cap ? M : cap;
+    if (frags) *frags = nout ? c->h_stat[2 + 5] : 0;
     if (nout == 0) return XDRG_E_INCOMPLETE;   // NextAction STOP (RpcMessageParserTCP.java:51-53)
     *n_msgs = nout;
     if (consumed) *consumed = c->h_stat[2 + 3];
@@ -1647,6 +1720,7 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
         HIPCHK(c, hipMemcpyAsync(c->h_stat + 1, msg_offsets + nout, 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         const uint64_t bytes = c->h_stat[1];
+        if (body_bytes) *body_bytes = bytes;
         if (bytes > payload_cap) {
             c->err = "payload buffer too small";
             if (consumed) *consumed = bytes;
@@ -1669,6 +1743,190 @@ extern "C" int xdrg_deframe(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_
     if (!payload && payload_cap) return XDRG_E_INVAL;
     uint8_t dummy = 0;
     return frame_walk(c, in, len, payload ? payload : &dummy, payload_cap, msg_offsets, cap, n_msgs, consumed);
+}
+
+// ---------------------------------------------------------------------------
+// receive: host socket buffers (RpcMessageParserTCP.handleRead) and the
+// decode of every complete message
+// ---------------------------------------------------------------------------
+static int recv_flags(xdrg_ctx *c, uint32_t flags) {
+    if (flags & ~(XDRG_HOST_PTRS | XDRG_HOST_MAPPED)) return inval(c, "receive calls take XDRG_HOST_PTRS / XDRG_HOST_MAPPED only");
+    if ((flags & XDRG_HOST_MAPPED) && !(flags & XDRG_HOST_PTRS)) return inval(c, "XDRG_HOST_MAPPED without XDRG_HOST_PTRS");
+    return XDRG_OK;
+}
+
+// Device-resident receive (device pointers, or mapped views of registered
+// host memory): one walk of the whole stream, then one decode of its
+// messages — in place and record-marked when every message is one fragment
+// (the common case: GrizzlyRpcTransport sends one, :103-110), else from the
+// assembled bodies.  offs: device, cap + 1 entries.
+static int recv_device(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t len, uint64_t cap,
+                       xdrg_column *cols, uint64_t *offs, uint64_t *n_msgs, uint64_t *consumed, uint64_t *first_bad,
+                       int *err) {
+    *n_msgs = *consumed = 0;
+    *first_bad = 0;
+    *err = XDRG_OK;
+    uint64_t nm = 0, used = 0, nf = 0;
+    int rc = frame_walk(c, in, len, nullptr, 0, offs, cap, &nm, &used, &nf, nullptr);
+    if (rc) return rc;   // XDRG_E_INCOMPLETE: STOP
+    uint64_t fb = nm;
+    int e = XDRG_OK;
+    if (nf == nm) {
+        rc = decode_impl(c, s, in, len, offs, nm, cols, XDRG_FRAME_RM, &fb, &e, 0, nullptr);
+    } else {   // multi-fragment messages: bodies assembled behind their offsets in the scratch
+        const size_t ob = ((nm + 1) * 8 + 255) & ~(size_t)255;
+        rc = ensure_rx(c, ob + used + 64);
+        if (rc) return rc;
+        uint64_t *boffs = (uint64_t *)c->d_rx;
+        uint8_t *body = c->d_rx + ob;
+        uint64_t nm2 = 0, used2 = 0, bytes = 0;
+        rc = frame_walk(c, in, len, body, used, boffs, nm, &nm2, &used2, nullptr, &bytes);
+        if (rc) return rc;
+        rc = decode_impl(c, s, body, bytes, boffs, nm, cols, 0, &fb, &e, 0, nullptr);
+    }
+    if (rc && !e) return rc;   // an argument / HIP failure, not a decode error
+    *n_msgs = nm;
+    *consumed = used;
+    *first_bad = fb;
+    *err = e;
+    if (e) {   // deliver through the bad message (CAPACITY: up to it)
+        const uint64_t upto = e == XDRG_E_CAPACITY ? fb : fb + 1;
+        DeviceGuard dg;
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, hipMemcpyAsync(c->h_stat + 1, offs + upto, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        *n_msgs = upto;
+        *consumed = c->h_stat[1];
+        c->err = xdrg_status_string(e);
+        return e;
+    }
+    return XDRG_OK;
+}
+
+// Host memory through the staging ring (hs::stage_receive).
+static int recv_staged(xdrg_ctx *c, int mode, const xdrg_schema *s, const uint8_t *in, uint64_t len, uint64_t cap,
+                       xdrg_column *cols, uint8_t *payload, uint64_t payload_cap, uint64_t *msg_offsets,
+                       hs::RecvResult &R) {
+    hs::Schema v;
+    if (s) stage_schema(s, v);
+    int rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));   // the caller's earlier work on this context
+    HipExec x(c, s);
+    rc = hs::stage_receive(x, mode, s ? &v : nullptr, in, len, cap, cols, payload, payload_cap, msg_offsets, R);
+    const int fr = x.finish();
+    if (rc && rc != XDRG_E_INCOMPLETE && rc != XDRG_E_HIP && c->err.empty()) c->err = xdrg_status_string(rc);
+    return rc ? rc : fr;
+}
+
+extern "C" int xdrg_frame_scan_ex(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint64_t *msg_offsets,
+                                  uint64_t cap, uint64_t *n_msgs, uint64_t *consumed, uint32_t flags) {
+    if (!c || !msg_offsets || !n_msgs) return XDRG_E_INVAL;
+    int rc = recv_flags(c, flags);
+    if (rc) return rc;
+    uint64_t used = 0;
+    *n_msgs = 0;
+    if (consumed) *consumed = 0;
+    if (len && !in) return inval(c, "stream is NULL");
+    if (!(flags & XDRG_HOST_PTRS)) {
+        rc = frame_walk(c, in, len, nullptr, 0, msg_offsets, cap, n_msgs, &used, nullptr, nullptr);
+        if (consumed) *consumed = used;
+        return rc;
+    }
+    DeviceGuard dg;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (flags & XDRG_HOST_MAPPED) {
+        const uint8_t *din = len ? (const uint8_t *)span_device(in, len) : in;
+        uint64_t *doffs = (uint64_t *)span_device(msg_offsets, (cap + 1) * 8);
+        if ((len && !din) || !doffs) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
+        rc = frame_walk(c, din, len, nullptr, 0, doffs, cap, n_msgs, &used, nullptr, nullptr);
+        if (consumed) *consumed = used;
+        return rc;
+    }
+    hs::RecvResult R;
+    rc = recv_staged(c, hs::RECV_SCAN, nullptr, in, len, cap, nullptr, nullptr, 0, msg_offsets, R);
+    *n_msgs = R.n_msgs;
+    if (consumed) *consumed = R.consumed;
+    return rc;
+}
+
+extern "C" int xdrg_deframe_ex(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *payload, uint64_t payload_cap,
+                               uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs, uint64_t *consumed,
+                               uint32_t flags) {
+    if (!c || !msg_offsets || !n_msgs || (!payload && payload_cap)) return XDRG_E_INVAL;
+    int rc = recv_flags(c, flags);
+    if (rc) return rc;
+    *n_msgs = 0;
+    if (consumed) *consumed = 0;
+    if (len && !in) return inval(c, "stream is NULL");
+    if (!(flags & XDRG_HOST_PTRS)) return xdrg_deframe(c, in, len, payload, payload_cap, msg_offsets, cap, n_msgs, consumed);
+    DeviceGuard dg;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (flags & XDRG_HOST_MAPPED) {
+        const uint8_t *din = len ? (const uint8_t *)span_device(in, len) : in;
+        uint8_t *dpay = payload_cap ? (uint8_t *)span_device(payload, payload_cap) : nullptr;
+        uint64_t *doffs = (uint64_t *)span_device(msg_offsets, (cap + 1) * 8);
+        if ((len && !din) || (payload_cap && !dpay) || !doffs)
+            return inval(c, "XDRG_HOST_MAPPED: stream / payload / offsets not registered");
+        uint8_t dummy = 0;
+        return frame_walk(c, din, len, dpay ? dpay : &dummy, payload_cap, doffs, cap, n_msgs, consumed, nullptr, nullptr);
+    }
+    hs::RecvResult R;
+    rc = recv_staged(c, hs::RECV_DEFRAME, nullptr, in, len, cap, nullptr, payload, payload_cap, msg_offsets, R);
+    *n_msgs = R.n_msgs;
+    if (consumed) *consumed = R.consumed;
+    return rc;
+}
+
+extern "C" int xdrg_receive_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t len, uint64_t cap,
+                                  xdrg_column *cols, uint32_t flags, uint64_t *msg_offsets, uint64_t *n_msgs,
+                                  uint64_t *consumed, uint64_t *first_bad, int *err) {
+    if (!c || !s || !n_msgs || !consumed) return XDRG_E_INVAL;
+    int rc = recv_flags(c, flags);
+    if (rc) return rc;
+    *n_msgs = *consumed = 0;
+    uint64_t fb_ = 0;
+    int e_ = XDRG_OK;
+    if (!first_bad) first_bad = &fb_;
+    if (!err) err = &e_;
+    *first_bad = 0;
+    *err = XDRG_OK;
+    if (len && !in) return inval(c, "stream is NULL");
+    DeviceGuard dg;
+    HIPCHK(c, hipSetDevice(c->device));
+    rc = check_columns(c, s, cols, cap, true);
+    if (rc) return rc;
+    if ((flags & XDRG_HOST_PTRS) && !(flags & XDRG_HOST_MAPPED)) {
+        if (s->ngroups) return inval(c, "repeated groups: the receive staging ring takes no group schema yet");
+        hs::RecvResult R;
+        rc = recv_staged(c, hs::RECV_DECODE, s, in, len, cap, cols, nullptr, 0, msg_offsets, R);
+        *n_msgs = R.n_msgs;
+        *consumed = R.consumed;
+        *first_bad = R.first_bad;
+        *err = R.err;
+        if (rc == XDRG_E_INVAL && c->err.empty()) c->err = "host columns: unsupported layout";
+        return rc;
+    }
+    const uint8_t *din = in;
+    xdrg_column *dcols = cols;
+    std::vector<xdrg_column> mc;
+    uint64_t *doffs = msg_offsets;
+    if (flags & XDRG_HOST_MAPPED) {
+        rc = mapped_cols(c, s, cols, cap, true, mc);
+        if (rc) return rc;
+        dcols = mc.data();
+        din = len ? (const uint8_t *)span_device(in, len) : in;
+        doffs = msg_offsets ? (uint64_t *)span_device(msg_offsets, (cap + 1) * 8) : nullptr;
+        if ((len && !din) || (msg_offsets && !doffs)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
+    }
+    uint64_t *tmp = nullptr;   // no caller array: the offsets in stream-ordered scratch
+    if (!doffs) {
+        HIPCHK(c, hipMallocAsync((void **)&tmp, (cap + 1) * 8, c->stream));
+        doffs = tmp;
+    }
+    rc = recv_device(c, s, din, len, cap, dcols, doffs, n_msgs, consumed, first_bad, err);
+    if (tmp) (void)hipFreeAsync(tmp, c->stream);
+    return rc;
 }
 
 // ---------------------------------------------------------------------------

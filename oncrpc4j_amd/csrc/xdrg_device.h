@@ -100,4 +100,18 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v) {
     return tot;
 }
 
+// ---- XCD-aware block order ----------------------------------------------------
+// Blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one; each
+// XCD has its own L2; MI355X_MICROARCH.md "Workgroup dispatch").  Block b of a
+// one-pass grid of nb blocks takes logical block xcd_block(b, nb): XCD slot
+// x = b % 8 owns the contiguous logical range [x*q + min(x, r), ...), q = nb/8,
+// r = nb % 8, so the blocks resident on one XCD work on neighbouring records
+// and a 128-byte line that straddles two of them is completed in one L2
+// (else each XCD writes back its own partial copy of the line).  A bijection
+// of [0, nb) for speed only: correctness never depends on the placement.
+__device__ __forceinline__ uint64_t xcd_block(uint64_t b, uint64_t nb) {
+    const uint64_t x = b & 7, q = nb >> 3, r = nb & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 }  // namespace xdrg

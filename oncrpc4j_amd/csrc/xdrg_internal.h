@@ -134,7 +134,7 @@ struct RecArgs {
                                // kernels, the others the staged ones (0: one kernel for all)
     uint32_t ncond;            // conditional fields in the schema (0: every record has all fields)
     uint32_t byref;            // 0, or 1 + the field encoded by reference / decoded as a view
-    uint32_t rsv0;
+    uint32_t xcd;              // payload kernels: blocks in XCD order (xcd_block)
     uint64_t *ref_pos;         // byref: encode splice[n] / decode payload_pos[n]
     uint32_t payk;             // 0, or 1 + the dynamic byte field the payload kernels move for the
                                // group kernels' blocks (k_enc/dec_payload)
@@ -189,6 +189,8 @@ struct Tuning {
                                     // stride and take the stride kernels (sync calls), 0 the record path
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
+    int32_t xcd_order = 1;          // key 37: payload kernels walk the records in XCD order (xcd_block),
+                                    // 0 in block order
     int32_t emit_per = 4;           // key 36: frame walk, sub-chunks per k_fr_emit block (at most;
                                     // halved until the grid has >= 64 blocks)
     int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of

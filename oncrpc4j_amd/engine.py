@@ -266,24 +266,58 @@ class Context:
             _raise(rc, self._h, fb.value)
         return rc, fb.value, er.value
 
-    def frame_scan(self, data, length, msg_offsets, cap):
-        """xdrg_frame_scan -> number of complete messages (0 = STOP)."""
-        nm = ctypes.c_uint64(0)
-        rc = lib().xdrg_frame_scan(self._h, _ptr(data), int(length), _ptr(msg_offsets), int(cap),
-                                   ctypes.byref(nm))
-        if rc not in (abi.OK, abi.E_INCOMPLETE):
-            _raise(rc, self._h)
-        return nm.value
-
-    def deframe(self, data, length, payload, payload_cap, msg_offsets, cap):
-        """xdrg_deframe -> (messages, consumed stream bytes); (0, 0) = STOP."""
+    def frame_scan(self, data, length, msg_offsets, cap, host=False, mapped=False, with_consumed=False):
+        """xdrg_frame_scan (device) / xdrg_frame_scan_ex (host=True: a host socket
+        buffer through the staging ring, mapped=True: registered host memory in
+        place) -> number of complete messages (0 = STOP), or (messages,
+        consumed) with with_consumed."""
         nm = ctypes.c_uint64(0)
         used = ctypes.c_uint64(0)
-        rc = lib().xdrg_deframe(self._h, _ptr(data), int(length), _ptr(payload), int(payload_cap),
-                                _ptr(msg_offsets), int(cap), ctypes.byref(nm), ctypes.byref(used))
+        if host or mapped or with_consumed:
+            rc = lib().xdrg_frame_scan_ex(self._h, _ptr(data), int(length), _ptr(msg_offsets), int(cap),
+                                          ctypes.byref(nm), ctypes.byref(used), self._flags(False, False, host, mapped))
+        else:
+            rc = lib().xdrg_frame_scan(self._h, _ptr(data), int(length), _ptr(msg_offsets), int(cap),
+                                       ctypes.byref(nm))
+        if rc not in (abi.OK, abi.E_INCOMPLETE):
+            _raise(rc, self._h)
+        return (nm.value, used.value) if with_consumed else nm.value
+
+    def deframe(self, data, length, payload, payload_cap, msg_offsets, cap, host=False, mapped=False,
+                raise_on_error=True):
+        """xdrg_deframe / xdrg_deframe_ex -> (messages, consumed stream bytes);
+        (0, 0) = STOP.  On host memory a payload that fills up delivers the
+        bodies that fit (XDRG_E_CAPACITY, raised unless raise_on_error=False:
+        then (messages, consumed, status))."""
+        nm = ctypes.c_uint64(0)
+        used = ctypes.c_uint64(0)
+        if host or mapped:
+            rc = lib().xdrg_deframe_ex(self._h, _ptr(data), int(length), _ptr(payload), int(payload_cap),
+                                       _ptr(msg_offsets), int(cap), ctypes.byref(nm), ctypes.byref(used),
+                                       self._flags(False, False, host, mapped))
+        else:
+            rc = lib().xdrg_deframe(self._h, _ptr(data), int(length), _ptr(payload), int(payload_cap),
+                                    _ptr(msg_offsets), int(cap), ctypes.byref(nm), ctypes.byref(used))
+        if not raise_on_error:
+            return nm.value, used.value, rc
         if rc not in (abi.OK, abi.E_INCOMPLETE):
             _raise(rc, self._h)
         return nm.value, used.value
+
+    def receive(self, schema, data, length, cap, cols, msg_offsets=None, host=False, mapped=False,
+                raise_on_error=True):
+        """xdrg_receive_batch: RpcMessageParserTCP.handleRead over a socket
+        buffer plus the decode of every complete message as one record ->
+        (status, messages delivered, consumed bytes, first_bad, err)."""
+        carr = cols if isinstance(cols, ctypes.Array) else columns_array(cols)
+        nm, used, fb = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        er = ctypes.c_int(0)
+        rc = lib().xdrg_receive_batch(self._h, schema.handle, _ptr(data), int(length), int(cap), carr,
+                                      self._flags(False, False, host, mapped), _ptr(msg_offsets),
+                                      ctypes.byref(nm), ctypes.byref(used), ctypes.byref(fb), ctypes.byref(er))
+        if rc and rc != abi.E_INCOMPLETE and raise_on_error:
+            _raise(rc, self._h, fb.value)
+        return rc, nm.value, used.value, fb.value, er.value
 
     def apply_tuning(self, spec):
         """Measurement tools only (bench.py, tools/): force kernel choices from

@@ -78,6 +78,8 @@ _SIGS = {
     "xo_assemble": (ctypes.c_int, [_P, _SZ, _P, _SZ, ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
     "xo_frame_scan": (ctypes.c_int, [_P, _SZ, _P, _U64, ctypes.POINTER(_U64)]),
     "xo_fragment": (_SZ, [_P, _SZ, _SZ, _P, _SZ]),
+    "xo_receive_batch": (ctypes.c_int, [_PF, _SZ, _P, _SZ, _P, _U64, _U64, _PC, _P, ctypes.POINTER(_U64),
+                                        ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_int)]),
     "xo_encode_batch": (ctypes.c_int, [_PF, _SZ, _PC, _U64, _P, _U64, _P, ctypes.c_uint32, _P]),
     "xo_decode_batch": (ctypes.c_int, [_PF, _SZ, _P, _U64, _P, _U64, _PC, ctypes.c_uint32, _P, _P]),
     "xo_encode_batch_cond": (ctypes.c_int, [_PF, _SZ, _P, _SZ, _PC, _U64, _P, _U64, _P,
@@ -180,6 +182,23 @@ def frame_scan(data, cap):
     nm = _U64(0)
     rc = L.xo_frame_scan(buf.ctypes.data, len(data), offs.ctypes.data, cap, ctypes.byref(nm))
     return rc, offs[:nm.value + 1].tolist()
+
+
+def receive_batch(fields, data, cap, cols, conds=None):
+    """handleRead + per-message decode (xdrg_receive_batch's contract) ->
+    (status, messages delivered, consumed bytes, message offsets, first_bad, err)."""
+    import numpy as np
+    L = lib()
+    fa = fields_array(fields)
+    ca, keep = conds_array(conds)
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    offs = np.zeros(len(data) // 4 + 2, dtype=np.uint64)
+    nm, used, fb, err = _U64(0), _U64(0), _U64(0), ctypes.c_int(0)
+    rc = L.xo_receive_batch(fa, len(fields), ca, len(conds or ()), buf.ctypes.data, len(data), cap,
+                            ctypes.addressof(cols), offs.ctypes.data, ctypes.byref(nm), ctypes.byref(used),
+                            ctypes.byref(fb), ctypes.byref(err))
+    del keep
+    return rc, nm.value, used.value, offs[:nm.value + 1].tolist(), fb.value, err.value
 
 
 def fragment(payload, frag):

@@ -352,6 +352,59 @@ int xo_frame_scan(const uint8_t *buf, size_t len, uint64_t *msg_offsets, uint64_
     *n_msgs = k;
     return k ? XDRG_OK : XDRG_E_INCOMPLETE;
 }
+/* handleRead over one socket buffer followed by the decode of every complete
+ * message (RpcMessageParserTCP.java:44-61; assembleXdr :109-140 hands each
+ * message body to the next filter as one Xdr, which XdrAble.xdrDecode reads:
+ * RpcCall.java:351-354 leaves trailing bytes unread).  Restates the contract
+ * of xdrg_receive_batch (include/xdrg.h): at most cap messages; a decode
+ * error at message i delivers messages 0..i (CAPACITY: 0..i-1), so the
+ * caller resumes after the bad one (RpcDispatcher.java:126-131 answers it
+ * GARBAGE_ARGS) or retries it with larger columns.  Bodies go through one
+ * concatenated buffer; the per-message extents index it.                   */
+int xo_receive_batch(const xdrg_field *fs, size_t nf, const xdrg_cond *conds, size_t nconds,
+                     const uint8_t *in, uint64_t len, uint64_t cap, xdrg_column *cols,
+                     uint64_t *msg_offsets, uint64_t *n_msgs, uint64_t *consumed,
+                     uint64_t *first_bad, int *err) {
+    uint64_t k = 0;
+    size_t pos = 0;
+    uint8_t *body = (uint8_t *)malloc(len + 1);
+    uint64_t *ext = (uint64_t *)malloc(sizeof(uint64_t) * (len / 4 + 2));
+    uint64_t *mo = (uint64_t *)malloc(sizeof(uint64_t) * (len / 4 + 2));
+    if (!body || !ext || !mo) { free(body); free(ext); free(mo); return XDRG_E_NOMEM; }
+    size_t blen = 0;
+    ext[0] = 0;
+    while (k < cap && xo_all_fragments_arrived(in + pos, len - pos)) {
+        size_t plen = 0, used = 0;
+        if (xo_assemble(in + pos, len - pos, body + blen, len - blen, &plen, &used) != XDRG_OK) break;
+        mo[k] = pos;
+        pos += used;
+        blen += plen;
+        ext[++k] = blen;
+    }
+    mo[k] = pos;
+    *n_msgs = k;
+    *consumed = pos;
+    if (first_bad) *first_bad = k;
+    if (err) *err = XDRG_OK;
+    int rc = k ? XDRG_OK : XDRG_E_INCOMPLETE;
+    if (k) {
+        uint64_t fb = k;
+        int e = XDRG_OK;
+        rc = xo_decode_batch_cond(fs, nf, conds, nconds, body, blen, ext, k, cols, 0, &fb, &e);
+        if (rc == XDRG_E_INVAL || rc == XDRG_E_NOMEM) { free(body); free(ext); free(mo); return rc; }
+        if (e) {
+            const uint64_t upto = e == XDRG_E_CAPACITY ? fb : fb + 1;   /* messages delivered */
+            *n_msgs = upto;
+            *consumed = mo[upto];
+        }
+        if (first_bad) *first_bad = fb;
+        if (err) *err = e;
+    }
+    if (msg_offsets)
+        for (uint64_t i = 0; i <= *n_msgs; i++) msg_offsets[i] = mo[i];
+    free(body); free(ext); free(mo);
+    return rc;
+}
 /* toFragmentedBuffer (ctest/rpc/RpcMessageParserTCPTest.java:161-181). */
 size_t xo_fragment(const uint8_t *payload, size_t len, size_t frag, uint8_t *out, size_t cap) {
     size_t nfrag = len / frag + 1, pos = 0, o = 0;
@@ -361,7 +414,8 @@ size_t xo_fragment(const uint8_t *payload, size_t len, size_t frag, uint8_t *out
         size_t fs = len - pos < frag ? len - pos : frag;
         uint32_t m = nfrag > 0 ? (uint32_t)fs : ((uint32_t)fs | RPC_LAST_FRAG);
         put_be32(out + o, m); o += 4;
-        memcpy(out + o, payload + pos, fs); o += fs; pos += fs;
+        if (fs) memcpy(out + o, payload + pos, fs);
+        o += fs; pos += fs;
     } while (nfrag > 0);
     return o;
 }

@@ -110,6 +110,12 @@ int  xo_assemble(const uint8_t *buf, size_t len, uint8_t *payload, size_t payloa
 /* Host restatement of xdrg_frame_scan (see include/xdrg.h).                 */
 int  xo_frame_scan(const uint8_t *buf, size_t len, uint64_t *msg_offsets, uint64_t cap,
                    uint64_t *n_msgs);
+/* handleRead + the decode of each complete message as one record (the
+ * contract of xdrg_receive_batch, include/xdrg.h; HOST pointers).           */
+int  xo_receive_batch(const xdrg_field *fields, size_t nfields, const xdrg_cond *conds, size_t nconds,
+                      const uint8_t *in, uint64_t len, uint64_t cap, xdrg_column *cols,
+                      uint64_t *msg_offsets, uint64_t *n_msgs, uint64_t *consumed,
+                      uint64_t *first_bad, int *err);
 /* Split a payload into record-marked fragments of at most frag bytes each
  * (fixture generator restating ctest/rpc/RpcMessageParserTCPTest.java:161-181).
  * Returns bytes written into out (cap must be >= len + 4*(len/frag+1)).      */

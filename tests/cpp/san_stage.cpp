@@ -102,7 +102,7 @@ struct CpuExec {
     }
     int decode(uint32_t s, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m, xdrg_column *dc,
                uint32_t flags) {
-        CHECK(len == 0 || in_arena(in, len));
+        CHECK(len == 0 || in_arena(in, len) || (in == bodyb.data() && len <= bodyb.size()));
         uint64_t fb = 0;
         int err = 0;
         (void)xo_decode_batch_cond(fields, nf, conds, nc, in, len, rec, m, dc, flags, &fb, &err);
@@ -135,6 +135,62 @@ struct CpuExec {
         return XDRG_OK;
     }
     int d2h_done(uint32_t) { return XDRG_OK; }
+    // receive: the oracle's walk (xo_frame_scan, RpcMessageParserTCP restated)
+    // and assembleXdr (xo_assemble) on the arena-resident window
+    std::vector<uint8_t> bodyb;
+    uint64_t scans = 0, assembled = 0;
+    int scan(uint32_t, const uint8_t *win, uint64_t wlen, uint64_t cap, uint64_t *offs, int bodies, uint8_t *dst,
+             uint64_t *boffs, uint64_t *res) {
+        CHECK(wlen == 0 || in_arena(win, wlen));
+        CHECK(in_arena((const uint8_t *)offs, (cap + 1) * 8));
+        uint64_t nm = 0;
+        (void)xo_frame_scan(win, wlen, offs, cap, &nm);
+        uint64_t nf = 0;
+        for (uint64_t i = 0; i < nm; ++i)
+            for (uint64_t p = offs[i]; p < offs[i + 1];) {
+                const uint32_t m = (uint32_t)win[p] << 24 | (uint32_t)win[p + 1] << 16 | (uint32_t)win[p + 2] << 8 | win[p + 3];
+                p += 4 + (m & 0x7fffffffu);
+                ++nf;
+            }
+        res[0] = nm;
+        res[1] = nm ? offs[nm] : 0;
+        res[2] = nf == nm;
+        res[3] = 0;
+        ++scans;
+        if (nm && (bodies == 2 || (bodies == 1 && nf != nm))) {
+            uint8_t *d = dst;
+            if (!d) {
+                bodyb.assign(res[1] + 64, 0xc5);
+                d = bodyb.data();
+            } else {
+                CHECK(in_arena(d, res[1]));
+            }
+            CHECK(in_arena((const uint8_t *)boffs, (nm + 1) * 8));
+            uint64_t bo = 0;
+            boffs[0] = 0;
+            for (uint64_t i = 0; i < nm; ++i) {
+                size_t plen = 0, used = 0;
+                CHECK(xo_assemble(win + offs[i], wlen - offs[i], d + bo, res[1] - bo, &plen, &used) == XDRG_OK);
+                CHECK(used == offs[i + 1] - offs[i]);
+                bo += plen;
+                boffs[i + 1] = bo;
+            }
+            res[3] = bo;
+            ++assembled;
+        }
+        return XDRG_OK;
+    }
+    const uint8_t *body() const { return bodyb.data(); }
+    int d2d(uint8_t *dst, const uint8_t *src, uint64_t n) {
+        CHECK(n == 0 || (in_arena(dst, n) && in_arena(src, n)));
+        std::memmove(dst, src, n);
+        return XDRG_OK;
+    }
+    int offs_copy(uint64_t *dst, const uint64_t *src, uint64_t n, uint64_t delta) {
+        CHECK(in_arena((const uint8_t *)dst, n * 8) && in_arena((const uint8_t *)src, n * 8));
+        for (uint64_t i = 0; i < n; ++i) dst[i] = src[i] + delta;
+        return XDRG_OK;
+    }
     int grow(uint64_t bytes) {
         if (bytes <= sb) return XDRG_OK;
         sb = bytes;
@@ -350,6 +406,144 @@ static CpuExec make_exec(std::mt19937_64 &g, const Batch &b) {
     return x;
 }
 
+// Receive (hs::stage_receive) against the oracle's handleRead restatement:
+// a random batch encoded by the oracle, every record one message whose body
+// is re-fragmented (ctest/rpc/RpcMessageParserTCPTest.java:161-181) or left
+// one fragment, an incomplete tail, sometimes a corrupted body, a message
+// cap and small slots (windows hold few messages; long messages grow the
+// ring, long tails restage).  DECODE vs xo_receive_batch (status, delivered,
+// consumed, first_bad, err, offsets, columns), SCAN vs xo_frame_scan,
+// DEFRAME vs the assembled bodies.
+static uint64_t receive_rounds(std::mt19937_64 &g, int rounds) {
+    uint64_t windows = 0, multi = 0, stops = 0, errs = 0, assembled = 0;
+    for (int r = 0; r < rounds; ++r) {
+        Batch src;
+        random_schema(g, src);
+        src.n = g() % 4 == 0 ? g() % 5 : g() % 700;
+        random_values(g, src, false);
+        for (auto &c : src.c) c.values = src.cvals.data();
+        std::vector<uint8_t> raw(1 << 21);
+        std::vector<uint64_t> ro(src.n + 1);
+        uint64_t rl = 0;
+        CHECK(xo_encode_batch_cond(src.f.data(), src.f.size(), src.c.empty() ? nullptr : src.c.data(), src.c.size(),
+                                   src.cols.data(), src.n, raw.data(), raw.size(), ro.data(), 0, &rl) == XDRG_OK);
+        std::vector<uint8_t> stream;
+        const int style = (int)(g() % 3);   // 0 single fragments, 1 mixed, 2 every message re-fragmented
+        for (uint64_t i = 0; i < src.n; ++i) {
+            std::vector<uint8_t> body(raw.begin() + (long)ro[i], raw.begin() + (long)ro[i + 1]);
+            if (g() % 40 == 0 && !body.empty()) body[g() % body.size()] = 0xff;   // a corrupted body
+            size_t frag = body.size() + 1;
+            if (style == 2 || (style == 1 && g() % 3 == 0)) frag = 4 * (1 + g() % 24);
+            std::vector<uint8_t> fr(body.size() + 4 * (body.size() / frag + 2));
+            const size_t w = xo_fragment(body.data(), body.size(), frag, fr.data(), fr.size());
+            stream.insert(stream.end(), fr.begin(), fr.begin() + (long)w);
+        }
+        if (g() % 2 && src.n) {   // an incomplete tail: part of one more message
+            const uint64_t i = g() % src.n;
+            std::vector<uint8_t> fr(ro[i + 1] - ro[i] + 64);
+            const size_t w = xo_fragment(raw.data() + ro[i], ro[i + 1] - ro[i], 64, fr.data(), fr.size());
+            if (w > 4) stream.insert(stream.end(), fr.begin(), fr.begin() + (long)(1 + g() % (w - 1)));
+        }
+        const uint64_t len = stream.size();
+        stream.resize(len + 16, 0);
+        const uint64_t cap = 1 + g() % (src.n + 5);
+        Batch a, o;
+        std::mt19937_64 g2 = g;
+        empty_like(g, src, a, 0);
+        empty_like(g2, src, o, 0);   // same capacities
+        const int mode = (int)(g() % 4);   // 0 scan, 1 deframe, 2-3 decode
+        CpuExec x = make_exec(g, src);
+        x.sb = 1024 + (g() % 12) * 1024;
+        x.arena.assign((uint64_t)x.ns * x.sb, 0xab);
+        std::vector<uint64_t> offs(cap + 2, 0x99), woffs(len / 4 + 2);
+        hs::RecvResult R;
+        if (mode >= 2) {
+            uint64_t wn = 0, wused = 0, wfb = 0;
+            int werr = 0;
+            const int wrc = xo_receive_batch(src.f.data(), src.f.size(), src.c.empty() ? nullptr : src.c.data(),
+                                             src.c.size(), stream.data(), len, cap, o.cols.data(), woffs.data(), &wn,
+                                             &wused, &wfb, &werr);
+            const int rc = hs::stage_receive(x, hs::RECV_DECODE, &src.hs, stream.data(), len, cap, a.cols.data(), nullptr,
+                                             0, g() % 2 ? offs.data() : nullptr, R);
+            if (rc != wrc || R.n_msgs != wn || R.consumed != wused || (wrc != XDRG_E_INCOMPLETE && (R.first_bad != wfb || R.err != werr)))
+                std::fprintf(stderr, "receive round %d: rc %d/%d n %llu/%llu used %llu/%llu fb %llu/%llu err %d/%d cap %llu len %llu style %d slots %u x %llu\n",
+                             r, rc, wrc, (unsigned long long)R.n_msgs, (unsigned long long)wn,
+                             (unsigned long long)R.consumed, (unsigned long long)wused, (unsigned long long)R.first_bad,
+                             (unsigned long long)wfb, R.err, werr, (unsigned long long)cap, (unsigned long long)len, style,
+                             x.ns, (unsigned long long)x.sb);
+            CHECK(rc == wrc && R.n_msgs == wn && R.consumed == wused);
+            if (wrc != XDRG_E_INCOMPLETE) CHECK(R.first_bad == wfb && R.err == werr);
+            if (offs[0] != 0x99 && wn)
+                for (uint64_t i = 0; i <= wn; ++i) CHECK(offs[i] == woffs[i]);
+            a.n = o.n = wn;
+            if (wrc != XDRG_E_INCOMPLETE) compare_prefix(a, o, werr ? wfb : wn);
+            errs += werr != 0;
+        } else if (mode == 1) {
+            std::vector<uint8_t> pay(len + 8, 0xee);
+            const uint64_t pcap = g() % 3 == 0 ? g() % (len + 1) : len;
+            const int rc = hs::stage_receive(x, hs::RECV_DEFRAME, nullptr, stream.data(), len, cap, nullptr, pay.data(),
+                                             pcap, offs.data(), R);
+            uint64_t wn = 0;
+            std::vector<uint64_t> so(cap + 1);
+            const int wrc = xo_frame_scan(stream.data(), len, so.data(), cap, &wn);
+            // the bodies that fit, message by message
+            uint64_t bo = 0, k = 0;
+            std::vector<uint8_t> want;
+            for (; k < wn; ++k) {
+                std::vector<uint8_t> b(so[k + 1] - so[k]);
+                size_t pl = 0, used = 0;
+                CHECK(xo_assemble(stream.data() + so[k], len - so[k], b.data(), b.size(), &pl, &used) == XDRG_OK);
+                if (bo + pl > pcap) break;
+                want.insert(want.end(), b.begin(), b.begin() + (long)pl);
+                bo += pl;
+            }
+            const bool full = k == wn;
+            if (!(R.n_msgs <= k && (full ? R.n_msgs == k : true)))
+                std::fprintf(stderr, "deframe round %d: n %llu want %llu (of %llu) rc %d\n", r, (unsigned long long)R.n_msgs,
+                             (unsigned long long)k, (unsigned long long)wn, rc);
+            // chunked delivery may stop at a window's first body that does not fit: never
+            // more than the bodies that fit, all of them when all fit
+            CHECK(R.n_msgs <= k);
+            if (full) CHECK(R.n_msgs == k && (rc == (k ? XDRG_OK : wrc)));
+            else {
+                if (rc != XDRG_E_CAPACITY)
+                    std::fprintf(stderr, "deframe round %d: rc %d n %llu fit %llu of %llu pcap %llu len %llu cap %llu\n", r, rc,
+                                 (unsigned long long)R.n_msgs, (unsigned long long)k, (unsigned long long)wn,
+                                 (unsigned long long)pcap, (unsigned long long)len, (unsigned long long)cap);
+                CHECK(rc == XDRG_E_CAPACITY);
+            }
+            CHECK(R.consumed == so[R.n_msgs]);
+            uint64_t pb = 0;
+            for (uint64_t i = 0; i < R.n_msgs; ++i) {   // body offsets and bytes of the delivered messages
+                CHECK(offs[i] == pb);
+                size_t pl = 0, used = 0;
+                std::vector<uint8_t> b(so[i + 1] - so[i]);
+                CHECK(xo_assemble(stream.data() + so[i], len - so[i], b.data(), b.size(), &pl, &used) == XDRG_OK);
+                CHECK(std::memcmp(pay.data() + pb, b.data(), pl) == 0);
+                pb += pl;
+            }
+            CHECK(R.payload == pb);
+        } else {
+            const int rc = hs::stage_receive(x, hs::RECV_SCAN, nullptr, stream.data(), len, cap, nullptr, nullptr, 0,
+                                             offs.data(), R);
+            uint64_t wn = 0;
+            std::vector<uint64_t> so(cap + 1);
+            const int wrc = xo_frame_scan(stream.data(), len, so.data(), cap, &wn);
+            CHECK(rc == wrc && R.n_msgs == wn && R.consumed == (wn ? so[wn] : 0));
+            for (uint64_t i = 0; i <= wn && wn; ++i) CHECK(offs[i] == so[i]);
+        }
+        windows += x.scans;
+        assembled += x.assembled;
+        multi += style != 0;
+        stops += R.n_msgs == 0;
+    }
+    CHECK(windows > 4 * (uint64_t)rounds && assembled > 0 && errs > 0 && stops > 0);
+    std::printf("san_stage: receive: %llu multi-fragment rounds, %llu decode errors, %llu STOP, %llu assembled windows\n",
+                (unsigned long long)multi, (unsigned long long)errs, (unsigned long long)stops,
+                (unsigned long long)assembled);
+    return windows;
+}
+
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 300;
     std::mt19937_64 g(0x0DCAC4E5);
@@ -452,6 +646,8 @@ int main(int argc, char **argv) {
         direct += x.direct;
     }
     CHECK(chunks_grown > 0 && errs > 0 && caps > 0 && bounced > 0 && direct > 0);
+    const uint64_t rx = receive_rounds(g, rounds);
+    std::printf("san_stage: %d receive rounds ok (%llu windows)\n", rounds, (unsigned long long)rx);
     std::printf("san_stage: %d rounds ok (ring grown %llu times, %llu decode errors, %llu capacity, "
                 "%llu bounced / %llu direct copies)\n",
                 rounds, (unsigned long long)chunks_grown, (unsigned long long)errs, (unsigned long long)caps,

@@ -117,38 +117,42 @@ def test_unaligned_fragment_sizes(gpu_ctx, shift):
     assert k == len(bodies)
 
 
+@pytest.mark.parametrize("shift", [0, 1], ids=["byte_walk", "serial_walk"])
 @pytest.mark.parametrize("marks_in_body", [False, True], ids=["random-bodies", "mark-like-bodies"])
-def test_byte_walk_many_messages(gpu_ctx, odd_walk, marks_in_body):
+def test_byte_walk_many_messages(gpu_ctx, shift, marks_in_body):
     """Several byte-mode super-chunks (64 KiB each), big fragments, bodies of
     small integers (false chains at every byte offset)."""
     rng = np.random.default_rng(21 + marks_in_body)
     stream, bodies = build(rng, 8000, aligned=False, big=2, marks_in_body=marks_in_body)
-    k, _ = check(gpu_ctx, stream, bodies)
+    k, _ = check(gpu_ctx, stream, bodies, shift=shift)
     assert k == len(bodies)
 
 
-def test_byte_walk_cut_tails(gpu_ctx, odd_walk):
+@pytest.mark.parametrize("shift", [0, 2], ids=["byte_walk", "serial_walk"])
+def test_byte_walk_cut_tails(gpu_ctx, shift):
     rng = np.random.default_rng(6)
     stream, bodies = build(rng, 2000, aligned=False)
     for cut in [5, 6, 7, len(stream) // 3, len(stream) // 2 + 1, len(stream) - 1, len(stream) - 2, len(stream) - 5]:
-        check(gpu_ctx, stream[:cut], bodies)
+        check(gpu_ctx, stream[:cut], bodies, shift=shift)
 
 
-def test_one_odd_fragment_then_aligned(gpu_ctx, odd_walk):
+@pytest.mark.parametrize("shift", [0, 3], ids=["byte_walk", "serial_walk"])
+def test_one_odd_fragment_then_aligned(gpu_ctx, shift):
     """The bench's serial-cliff shape: a 3-byte fragment, then aligned
     messages (every later mark at byte offset 3 mod 4)."""
     rng = np.random.default_rng(9)
     stream, bodies = build(rng, 4000)
     head = oracle.fragment(b"abc", 3)
-    k, _ = check(gpu_ctx, head + stream, [b"abc"] + bodies)
+    k, _ = check(gpu_ctx, head + stream, [b"abc"] + bodies, shift=shift)
     assert k == len(bodies) + 1
 
 
-def test_byte_walk_cap(gpu_ctx, odd_walk):
+@pytest.mark.parametrize("shift", [0, 1], ids=["byte_walk", "serial_walk"])
+def test_byte_walk_cap(gpu_ctx, shift):
     rng = np.random.default_rng(12)
     stream, bodies = build(rng, 700, aligned=False)
     for cap in (1, 7, 300):
-        check(gpu_ctx, stream, bodies, cap=cap)
+        check(gpu_ctx, stream, bodies, cap=cap, shift=shift)
 
 
 def test_cap_limits_messages(gpu_ctx):
