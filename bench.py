@@ -305,15 +305,14 @@ class Workload:
 
     def receive(self):
         """The receive pipeline of a record-marked stream (RpcMessageParserTCP
-        -> RpcProtocolFilter): xdrg_frame_scan walks the marks, then
-        xdrg_decode_batch(XDRG_FRAME_RM) decodes the messages at the offsets
-        the walk found (never the encoder's).  Fixed-size messages decode
-        synchronously: the engine checks the offsets for the fixed stride and
-        then takes the stride kernels (tuning key 29)."""
-        m = self.ctx.frame_scan(self.xdr, self.xlen, self.scan_offs, self.n)
-        assert m == self.n, f"frame scan found {m} of {self.n} messages"
-        self.ctx.decode(self.sch, self.xdr, self.xlen, self.n, self.cout, rec_offsets=self.scan_offs,
-                        framed=True, async_=self.cfg != 2)
+        -> RpcProtocolFilter) in one C-ABI call, xdrg_receive_batch on device
+        memory: the mark walk, then the decode of every message at the offsets
+        the walk found (never the encoder's), in place with its mark checked.
+        Fixed-size messages: the engine checks the offsets for the fixed
+        stride and takes the stride kernels (tuning key 29)."""
+        rc, m, used, _, _ = self.ctx.receive(self.sch, self.xdr, self.xlen, self.n, self.cout,
+                                             msg_offsets=self.scan_offs)
+        assert (rc, m, used) == (0, self.n, self.xlen), f"receive: {rc}, {m} of {self.n} messages, {used} bytes"
 
     def clear_outputs(self):
         """Zero the XDR stream and every decode target (tools/sweep_rec.py:
@@ -761,6 +760,166 @@ def host_inclusive(device, sch, n, reps=3, slot_bytes=64 << 20, slots=4,
                       "xdrg_host_register, staged_pageable on unregistered memory (bounce copies)"}
 
 
+def _host_cols4(n, nchars, nints, mk):
+    """configs[3] columns (n records, nchars string bytes, nints vector
+    elements) in host memory made by mk(nbytes) -> numpy uint8 array:
+    (ctypes columns, (hdr, string bytes, string offsets, ints, int offsets))."""
+    import numpy as np
+    from oncrpc4j_amd import abi
+    a_hdr = mk(4 * n).view(np.int32)
+    a_sv = mk(max(nchars, 1))
+    a_so = mk(8 * (n + 1)).view(np.uint64)
+    a_iv = mk(4 * max(nints, 1)).view(np.int32)
+    a_io = mk(8 * (n + 1)).view(np.uint64)
+    arr = (abi.Column * 3)()
+    arr[0].data, arr[0].stride = a_hdr.ctypes.data, 4
+    arr[1].data, arr[1].offsets, arr[1].cap = a_sv.ctypes.data, a_so.ctypes.data, nchars
+    arr[2].data, arr[2].offsets, arr[2].cap = a_iv.ctypes.data, a_io.ctypes.data, nints
+    return arr, (a_hdr, a_sv, a_so, a_iv, a_io)
+
+
+def host_inclusive_var(device, n, reps=2, slot_bytes=64 << 20, slots=4):
+    """configs[3] (int32 + string<8..256> + int32<0..16>) on host memory
+    through the C-ABI, the variable-size counterpart of host_inclusive: replies
+    encode host columns into a host stream while requests decode a host
+    stream into host columns (two contexts, two threads), and the receive
+    side of a record-marked stream: xdrg_receive_batch walks the marks of a
+    host socket buffer and decodes every message into host columns
+    (RpcMessageParserTCP.handleRead + the per-message decode).  Legs: staged
+    (the staging ring, registered buffers), staged_pageable (unregistered,
+    bounce copies) and mapped (XDRG_HOST_MAPPED).  GiB/s = native + XDR bytes
+    of the direction(s) / wall time; every leg checked against the original
+    columns."""
+    import threading
+    import numpy as np
+    import torch
+    from oncrpc4j_amd import abi, engine
+    dev = torch.device("cuda", device)
+    d = _gen_shard(4, n, 0, dev)
+    hdr = d["hdr"].reshape(-1).cpu().numpy()
+    (lens, sv), (kk, iv) = d["dyn"]
+    so = np.zeros(n + 1, np.uint64)
+    io = np.zeros(n + 1, np.uint64)
+    np.cumsum(lens.cpu().numpy(), out=so[1:])
+    np.cumsum(kk.cpu().numpy(), out=io[1:])
+    sv = sv.cpu().numpy()
+    iv = iv.cpu().numpy()
+    del d, lens, kk
+    torch.cuda.empty_cache()
+    fields = [(abi.T_INT, abi.K_SCALAR, 0), (abi.T_STRING, abi.K_DYNAMIC, 0), (abi.T_INT, abi.K_DYNAMIC, 0)]
+    sch = engine.Schema(fields)
+    # the XDR streams (raw and record-marked) by one device encode each
+    sizes = 12 + (lens_np := np.diff(so)) + ((4 - (lens_np & 3)) & 3) + 4 * np.diff(io)
+    xlen = int(sizes.sum())
+    xlen_rm = xlen + 4 * n
+    native = 4 * n + sv.size + 4 * iv.size
+    ctx0 = engine.Context(device)
+    ctx0.set_stream(torch.cuda.current_stream())
+    streams = {}
+    for framed, ln in ((False, xlen), (True, xlen_rm)):
+        t = [torch.from_numpy(x).to(dev) for x in (hdr, sv, so.view(np.int64), iv, io.view(np.int64))]
+        arr = (abi.Column * 3)()
+        arr[0].data, arr[0].stride = t[0].data_ptr(), 4
+        arr[1].data, arr[1].offsets, arr[1].cap = t[1].data_ptr(), t[2].data_ptr(), sv.size
+        arr[2].data, arr[2].offsets, arr[2].cap = t[3].data_ptr(), t[4].data_ptr(), iv.size
+        out = torch.empty(ln, dtype=torch.uint8, device=dev)
+        assert ctx0.encode(sch, arr, n, out, ln, framed=framed) == ln
+        streams[framed] = out.cpu().numpy()
+        del t, out
+        torch.cuda.empty_cache()
+    ctx0.close()
+    regs = []
+
+    def mk_reg(nbytes):
+        m_, a_, p_ = _host_buffer(max(nbytes, 1), True)
+        regs.append((m_, p_))
+        return a_[:nbytes] if nbytes else a_
+
+    def mk_page(nbytes):
+        return np.zeros(max(nbytes, 1), np.uint8)[:max(nbytes, 1)]
+
+    def ok_cols(arrs, upto=n):
+        a_hdr, a_sv, a_so, a_iv, a_io = arrs
+        return (np.array_equal(a_hdr[:upto], hdr[:upto]) and np.array_equal(a_so, so)
+                and np.array_equal(a_io, io) and np.array_equal(a_sv[:sv.size], sv)
+                and np.array_equal(a_iv[:iv.size], iv))
+
+    def leg(mode):
+        mk = mk_page if mode == "staged_pageable" else mk_reg
+        kw = {"mapped": True} if mode == "mapped" else {"host": True}
+        src_cols, src = _host_cols4(n, sv.size, iv.size, mk)
+        for a_, b_ in zip(src, (hdr, sv, so, iv, io)):
+            a_[:b_.size] = b_
+        out_cols, outs = _host_cols4(n, sv.size, iv.size, mk)
+        back_cols, backs = _host_cols4(n, sv.size, iv.size, mk)
+        req = mk(xlen)
+        req[:] = streams[False]
+        xdr = mk(xlen)
+        ro = mk(8 * (n + 1)).view(np.uint64)
+        ce, cd = engine.Context(device), engine.Context(device)
+        for c in (ce, cd):
+            c.apply_tuning(os.environ.get("XDRG_TUNE"))   # measurement runs only
+            c.host_staging(slot_bytes, slots)
+        res = {}
+        # encode + decode at once (a server's replies and requests)
+        ce.encode(sch, src_cols, n, xdr, xlen, rec_offsets=ro, **kw)   # warm
+        cd.decode(sch, req, xlen, n, back_cols, rec_offsets=ro, **kw)
+
+        def enc():
+            for _ in range(reps):
+                ce.encode(sch, src_cols, n, xdr, xlen, rec_offsets=ro, **kw)
+
+        def dec():
+            for _ in range(reps):
+                cd.decode(sch, req, xlen, n, back_cols, rec_offsets=ro, **kw)
+
+        xdr[:] = 0
+        ts = [threading.Thread(target=enc), threading.Thread(target=dec)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        dt = (time.perf_counter() - t0) / reps
+        ok = bool(np.array_equal(xdr, streams[False])) and ok_cols(backs)
+        res["encode_decode"] = {"GiB_s": round(2 * (native + xlen) / dt / GIB, 3), "ms": round(dt * 1e3, 3),
+                                "ok": ok}
+        # receive: the record-marked socket buffer -> host columns
+        sock = mk(xlen_rm)
+        sock[:] = streams[True]
+        rc, m, used, _, _ = cd.receive(sch, sock, xlen_rm, n, out_cols, **kw)   # warm
+        for a_ in outs:
+            a_[:] = 0
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            rc, m, used, _, _ = cd.receive(sch, sock, xlen_rm, n, out_cols, **kw)
+        dt = (time.perf_counter() - t0) / reps
+        ok = (rc, m, used) == (0, n, xlen_rm) and ok_cols(outs)
+        res["receive"] = {"GiB_s": round((native + xlen_rm) / dt / GIB, 3), "ms": round(dt * 1e3, 3), "ok": ok}
+        for c in (ce, cd):
+            c.close()
+        for _, p_ in regs:
+            engine.host_unregister(p_)
+        regs.clear()
+        return res
+
+    legs = {mode: leg(mode) for mode in ("staged", "mapped", "staged_pageable")}
+    best = {k: max(legs, key=lambda m: legs[m][k]["GiB_s"] if legs[m][k]["ok"] else -1) for k in
+            ("encode_decode", "receive")}
+    return {"config": 4, "records": n, "native_bytes": native, "xdr_bytes": xlen, "xdr_bytes_framed": xlen_rm,
+            "encode_decode": {"GiB_s": legs[best["encode_decode"]]["encode_decode"]["GiB_s"],
+                              "best": best["encode_decode"]},
+            "receive": {"GiB_s": legs[best["receive"]]["receive"]["GiB_s"], "best": best["receive"]},
+            "legs": legs, "slots": [slots, slot_bytes],
+            "ok": all(v["ok"] for l_ in legs.values() for v in l_.values()),
+            "method": "C-ABI on host memory: encode_decode = xdrg_encode_batch + xdrg_decode_batch at once on two "
+                      "contexts (replies / requests), GiB/s of both directions' native + XDR bytes; receive = "
+                      "xdrg_receive_batch on a record-marked host socket buffer (mark walk + decode of every "
+                      "message into host columns), GiB/s of stream + native bytes; staged = XDRG_HOST_PTRS "
+                      "(staging ring, registered buffers), mapped = XDRG_HOST_MAPPED, staged_pageable = "
+                      "unregistered memory (bounce copies)"}
+
+
 # ---------------------------------------------------------------------------
 def run_rank(args):
     import torch
@@ -788,6 +947,11 @@ def run_rank(args):
             and ctx is not None:
         hinc = host_inclusive(R.local, wl.sch, min(n, 64 << 20))
     del wl
+    hvar = None
+    if hinc is not None and args.extra:
+        if R.cuda:
+            torch.cuda.empty_cache()
+        hvar = host_inclusive_var(R.local, SIZES[4])
     if R.cuda:
         torch.cuda.empty_cache()
 
@@ -829,6 +993,7 @@ def run_rank(args):
             "gather": head["gather"],
             "cpu_baseline": cpu,
             "host_inclusive": hinc,
+            "host_inclusive_var": hvar,
             "extra_configs": extra,
         }
         print(json.dumps(line), flush=True)

@@ -167,7 +167,8 @@ typedef struct xdrg_column {
  * is synchronous (XDRG_ASYNC is refused).  Results are those of the device
  * call on the same records, except that a variable-size encode that
  * overruns out_cap may have written the records before the overrun.
- * Schemas with repeated groups take XDRG_HOST_MAPPED.                        */
+ * Repeated groups: a chunk of records moves its elements' member rows with
+ * it (rows between the group offsets of its first and last record).        */
 #define XDRG_HOST_PTRS     0x4u
 /* With XDRG_HOST_PTRS: no staging — the kernels read and write the host
  * buffers in place over PCIe.  Every buffer must be registered

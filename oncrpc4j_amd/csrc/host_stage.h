@@ -29,8 +29,10 @@
 //              uint64_t *rec, uint32_t flags);   // async; result word 0 = stream bytes
 //   int decode(uint32_t s, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m,
 //              xdrg_column *dcols, uint32_t flags);   // async; words 0 / 1 = first_bad / err
-//   int kernel_end(uint32_t s, const uint64_t *const *extra, uint32_t nextra);
-//                                                // result words 2.. = *extra[i]; event
+//   int kernel_end(uint32_t s, const uint64_t *const *extra, const uint64_t *const *index,
+//                  const uint64_t *limit, uint32_t nextra);
+//                                                // result words 2 + i = index[i] ? (*index[i] <= limit[i] ?
+//                                                // extra[i][*index[i]] : 0) : *extra[i] (device words); event
 //   int wait_kernel(uint32_t s, uint64_t *words); // host-blocking; words[0 .. 2 + nextra)
 //   int d2h_begin(uint32_t s);                   // copy stream waits slot s's kernels
 //   int dma_d2h(void *host, const uint8_t *dev, uint64_t bytes);
@@ -72,17 +74,31 @@ constexpr uint64_t kSpanAlign = 256;   // every span starts on its own 256-B bou
 constexpr uint64_t kSpanSlack = 64;    // ... followed by slack the 16-B window loads may touch
 
 // One schema field as the pipeline sees it (the compiled xdrg_schema's view).
+// Repeated groups (include/xdrg.h): a group field (XDRG_T_GROUP) has no data
+// of its own (DYNAMIC / LIST: per-record element offsets), its members are
+// columns indexed by ELEMENT, so a chunk of records [lo, lo + m) moves the
+// member rows of its elements.
 struct Field {
     uint32_t type, kind, count;
     uint32_t nsz;      // native element bytes
     uint32_t xsz;      // XDR element bytes (1: opaque / string bytes)
     uint32_t xbytes;   // fixed fields: XDR bytes of the field
+    uint32_t grp = 0;  // member: its group's field index + 1
+    uint32_t emin = 0; // group: fewest XDR bytes of one element (0: elements may be empty)
 };
 struct Schema {
     std::vector<Field> f;
     uint64_t fixed_part = 0;   // XDR bytes of the fixed fields
     bool var_size = false;     // dynamic or conditional fields
     uint64_t min_xdr = 0;      // fewest XDR bytes a well-formed record has (receive: rows per window)
+    bool groups = false;
+};
+inline bool is_group(const Field &f) { return f.type == XDRG_T_GROUP; }
+
+// Rows of each field's column in a chunk: records [lo, lo + m) for top-level
+// fields, the chunk's elements for a group's members.
+struct Rows {
+    std::vector<uint64_t> lo, n;   // per field
 };
 
 inline uint64_t up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
@@ -93,6 +109,7 @@ inline uint64_t up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 struct Region {
     const uint8_t *base = nullptr;   // lowest field address (row 0)
     int64_t stride = 0;              // bytes per row; 0 = constant (encode only)
+    uint32_t space = 0;              // 0: records; g + 1: the elements of group field g
     uint64_t row_end = 0;            // bytes of a row that fields cover, from base
     bool full = false;               // fields cover every byte of a row (decode: one contiguous D2H)
     std::vector<uint32_t> fields;
@@ -107,29 +124,32 @@ inline uint64_t fixed_elem_bytes(const Field &f) {
 // pipeline does not take (negative or overlapping strides).
 inline int build_regions(const Schema &s, const xdrg_column *cols, std::vector<Region> &out) {
     out.clear();
-    struct C { const uint8_t *p; int64_t st; uint64_t e; uint32_t k; };
+    struct C { const uint8_t *p; int64_t st; uint64_t e; uint32_t k, sp; };
     std::vector<C> v;
     for (uint32_t k = 0; k < s.f.size(); ++k) {
         const Field &f = s.f[k];
-        if (f.kind == XDRG_K_DYNAMIC) continue;
+        if (f.kind == XDRG_K_DYNAMIC || is_group(f)) continue;
         const uint64_t e = fixed_elem_bytes(f);
         if (!e) continue;   // T x[0]: no bytes on either side
         int64_t st = cols[k].stride;
         if (st == XDRG_STRIDE_CONST) st = 0;
         else if (st == 0) st = (int64_t)e;
         else if (st < 0 || (uint64_t)st < e) return XDRG_E_INVAL;
-        v.push_back({(const uint8_t *)cols[k].data, st, e, k});
+        v.push_back({(const uint8_t *)cols[k].data, st, e, k, f.grp});
     }
-    std::sort(v.begin(), v.end(), [](const C &a, const C &b) { return a.st != b.st ? a.st < b.st : a.p < b.p; });
-    for (const C &c : v) {
+    std::sort(v.begin(), v.end(), [](const C &a, const C &b) {
+        return a.sp != b.sp ? a.sp < b.sp : a.st != b.st ? a.st < b.st : a.p < b.p;
+    });
+    for (const C &c : v) {   // (a region's fields share one row space: records, or one group's elements)
         Region *r = out.empty() ? nullptr : &out.back();
-        const bool joins = r && c.st && r->stride == c.st && c.p >= r->base &&
+        const bool joins = r && c.st && r->stride == c.st && r->space == c.sp && c.p >= r->base &&
                            (uint64_t)(c.p - r->base) + c.e <= (uint64_t)c.st;
         if (!joins) {
             out.push_back(Region());
             r = &out.back();
             r->base = c.p;
             r->stride = c.st;
+            r->space = c.sp;
         }
         const uint64_t a = (uint64_t)(c.p - r->base);
         r->fields.push_back(c.k);
@@ -165,21 +185,60 @@ struct Bump {
 struct Layout {
     uint64_t lo = 0, m = 0, need = 0;
     std::vector<uint64_t> reg;               // per region: slot offset of row 0's base
-    std::vector<uint64_t> val, off, vcap;    // per field (dynamic): values / offsets offset, value capacity
+    std::vector<uint64_t> val, off, vcap;    // per field (dynamic, group offsets): values / offsets, value capacity
+    std::vector<uint64_t> rows;              // decode: per field, the rows laid out (members: element bound)
     uint64_t xdr = 0, xcap = 0, rec = 0;     // stream span, its capacity, record offsets (m + 1)
     uint64_t win = 0, wlen = 0;              // decode: host window [win, win + wlen) of the stream
 };
 
-inline uint64_t bound_xdr(const Schema &s, bool framed, uint64_t m, const xdrg_column *cols, uint64_t lo,
-                          uint64_t hi) {
-    uint64_t b = m * (s.fixed_part + (framed ? 4 : 0));
+// Rows of a chunk of records [lo, lo + m): records for top-level fields, the
+// chunk's elements for group members (encode: from the host group offsets).
+inline void chunk_rows(const Schema &s, const xdrg_column *cols, uint64_t lo, uint64_t m, Rows &R) {
+    R.lo.assign(s.f.size(), lo);
+    R.n.assign(s.f.size(), m);
+    for (uint32_t g = 0; g < s.f.size(); ++g) {
+        const Field &f = s.f[g];
+        if (!is_group(f)) continue;
+        uint64_t elo, em;
+        if (f.kind == XDRG_K_FIXED) {
+            elo = lo * f.count;
+            em = m * f.count;
+        } else {
+            elo = cols[g].offsets[lo];
+            em = cols[g].offsets[lo + m] - elo;
+        }
+        for (uint32_t k = g + 1; k < s.f.size() && s.f[k].grp == g + 1; ++k) {
+            R.lo[k] = elo;
+            R.n[k] = em;
+        }
+    }
+}
+// Elements of group g in a chunk (encode), from its first member's rows.
+inline uint64_t group_elems(const Rows &R, uint32_t g) { return R.n[g + 1]; }
+
+// Bound on a chunk's XDR bytes (conditional fields may take some away).
+inline uint64_t bound_xdr(const Schema &s, bool framed, uint64_t m, const xdrg_column *cols, const Rows &R) {
+    uint64_t b = m * (framed ? 4 : 0);
     for (uint32_t k = 0; k < s.f.size(); ++k) {
         const Field &f = s.f[k];
-        if (f.kind != XDRG_K_DYNAMIC) continue;
-        b += m * (4 + (f.xsz == 1 ? 3 : 0)) + (cols[k].offsets[hi] - cols[k].offsets[lo]) * f.xsz;
+        if (is_group(f)) {   // a count word, or a bool per element and the closing one
+            if (f.kind == XDRG_K_DYNAMIC) b += 4 * m;
+            if (f.kind == XDRG_K_LIST) b += 4 * m + 4 * group_elems(R, k);
+        } else if (f.kind != XDRG_K_DYNAMIC) {
+            b += (uint64_t)f.xbytes * R.n[k];
+        } else {
+            const uint64_t *o = cols[k].offsets;
+            b += R.n[k] * (4 + (f.xsz == 1 ? 3 : 0)) + (o[R.lo[k] + R.n[k]] - o[R.lo[k]]) * f.xsz;
+        }
     }
     return b;
 }
+
+// A region's host span over `rows` rows (0 rows: nothing).
+inline uint64_t region_span(const Region &g, uint64_t rows) {
+    return rows ? (uint64_t)g.stride * (rows - 1) + g.row_end : 0;
+}
+inline uint32_t region_field0(const Region &g) { return g.fields.front(); }
 
 // ---------------------------------------------------------------------------
 // encode
@@ -192,38 +251,52 @@ struct EncPlan {
     std::vector<Region> regs;
 };
 
-inline void enc_layout(const EncPlan &p, uint64_t lo, uint64_t m, Layout &L) {
+inline void enc_layout(const EncPlan &p, uint64_t lo, uint64_t m, Layout &L, Rows &R) {
     const Schema &s = p.s;
     Bump b;
     L.lo = lo;
     L.m = m;
+    chunk_rows(s, p.cols, lo, m, R);
     L.reg.assign(p.regs.size(), 0);
     for (size_t r = 0; r < p.regs.size(); ++r) {
         const Region &g = p.regs[r];
-        const uint8_t *h = g.base + (uint64_t)g.stride * lo;
-        L.reg[r] = b.take((uint64_t)g.stride * (m - 1) + g.row_end, (uintptr_t)h);
+        const uint32_t k0 = region_field0(g);
+        const uint8_t *h = g.base + (uint64_t)g.stride * R.lo[k0];
+        L.reg[r] = b.take(region_span(g, R.n[k0]), (uintptr_t)h);
     }
     L.val.assign(s.f.size(), 0);
     L.off.assign(s.f.size(), 0);
     L.vcap.assign(s.f.size(), 0);
     for (uint32_t k = 0; k < s.f.size(); ++k) {
-        if (s.f[k].kind != XDRG_K_DYNAMIC) continue;
-        const uint64_t a = p.cols[k].offsets[lo], e = p.cols[k].offsets[lo + m];
+        const Field &f = s.f[k];
+        if (is_group(f)) {   // the group's per-record element offsets
+            if (f.kind != XDRG_K_FIXED) L.off[k] = b.take((m + 1) * 8, (uintptr_t)(p.cols[k].offsets + lo));
+            continue;
+        }
+        if (f.kind != XDRG_K_DYNAMIC) continue;
+        const uint64_t a = p.cols[k].offsets[R.lo[k]], e = p.cols[k].offsets[R.lo[k] + R.n[k]];
         L.vcap[k] = e - a;
-        L.val[k] = b.take((e - a) * s.f[k].nsz, (uintptr_t)((const uint8_t *)p.cols[k].data + a * s.f[k].nsz));
-        L.off[k] = b.take((m + 1) * 8, (uintptr_t)(p.cols[k].offsets + lo));
+        L.val[k] = b.take((e - a) * f.nsz, (uintptr_t)((const uint8_t *)p.cols[k].data + a * f.nsz));
+        L.off[k] = b.take((R.n[k] + 1) * 8, (uintptr_t)(p.cols[k].offsets + R.lo[k]));
     }
-    L.xcap = bound_xdr(s, p.framed, m, p.cols, lo, lo + m);
+    L.xcap = bound_xdr(s, p.framed, m, p.cols, R);
     L.xdr = b.take(L.xcap);
     L.rec = (p.want_rec || s.var_size) ? b.take((m + 1) * 8) : 0;
     L.need = b.used;
 }
 
-// Dynamic offsets must not decrease over the batch (the device call has the
-// same precondition); the pipeline checks the ends it cuts at.
-inline bool dyn_offsets_sane(const Schema &s, const xdrg_column *cols, uint64_t lo, uint64_t hi) {
+// Dynamic offsets (and group element offsets) must not decrease over the
+// batch (the device call has the same precondition); the pipeline checks the
+// ends it cuts at.
+inline bool dyn_offsets_sane(const Schema &s, const xdrg_column *cols, uint64_t n) {
+    for (uint32_t g = 0; g < s.f.size(); ++g)
+        if (is_group(s.f[g]) && s.f[g].kind != XDRG_K_FIXED && cols[g].offsets[n] < cols[g].offsets[0]) return false;
+    Rows R;
+    chunk_rows(s, cols, 0, n, R);
     for (uint32_t k = 0; k < s.f.size(); ++k)
-        if (s.f[k].kind == XDRG_K_DYNAMIC && cols[k].offsets[hi] < cols[k].offsets[lo]) return false;
+        if (!is_group(s.f[k]) && s.f[k].kind == XDRG_K_DYNAMIC &&
+            cols[k].offsets[R.lo[k] + R.n[k]] < cols[k].offsets[R.lo[k]])
+            return false;
     return true;
 }
 
@@ -248,7 +321,8 @@ uint64_t fit_chunk(uint64_t lo, uint64_t n, uint64_t guess, uint64_t cap, Layout
 inline double enc_avg_bytes(const EncPlan &p) {
     if (!p.n) return 1.0;
     Layout L;
-    enc_layout(p, 0, p.n, L);
+    Rows R;
+    enc_layout(p, 0, p.n, L, R);
     return (double)L.need / (double)p.n;
 }
 
@@ -256,8 +330,10 @@ inline double enc_avg_bytes(const EncPlan &p) {
 struct Flight {
     uint32_t slot;
     Layout L;
-    std::vector<uint64_t> base;   // decode: per field, elements before this chunk (dynamic fields)
-    std::vector<uint64_t> cap;    // decode: per field, device value capacity granted to the chunk
+    Rows R;
+    std::vector<uint64_t> base;   // decode: per field, rows / values before this chunk (dynamic: values,
+                                  // group: elements)
+    std::vector<uint64_t> cap;    // decode: per field, device capacity granted to the chunk (values / elements)
 };
 
 template <class X>
@@ -322,6 +398,16 @@ struct Stager {
         outs[s].push_back({host, b, width, rows, pitch, pitch});
         return x.dma_d2h_2d(b, pitch, dev, pitch, width, rows);
     }
+    // decoded fixed columns of `rows` rows from row `first` (regions of one row space)
+    int d2h_region(uint32_t s, const Region &g, uint64_t first, const uint8_t *dev, uint64_t rows) {
+        uint8_t *h = (uint8_t *)g.base + (uint64_t)g.stride * first;
+        if (g.full) return d2h(s, h, dev, (uint64_t)g.stride * rows);
+        for (auto &sg : g.segs) {
+            const int rc = d2h_2d(s, h + sg.first, (uint64_t)g.stride, dev + sg.first, sg.second - sg.first, rows);
+            if (rc) return rc;
+        }
+        return XDRG_OK;
+    }
 };
 
 #define HS_TRY(x)                 \
@@ -335,14 +421,16 @@ struct Stager {
 // bytes land at the sum of the earlier chunks' sizes and its record offsets
 // are rebased by it.  A variable-size batch that overruns out_cap keeps
 // sizing the remaining chunks and returns XDRG_E_CAPACITY with the bytes it
-// needs (the chunks before the overrun have been written).
+// needs (the chunks before the overrun have been written).  Repeated groups:
+// a chunk moves its records' elements with them (the members' rows between
+// the group offsets of its first and last record, rebased to the chunk).
 template <class X>
 int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uint8_t *out, uint64_t out_cap,
                  uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len) {
     const bool framed = flags & XDRG_FRAME_RM;
     EncPlan p{s, cols, n, framed, rec_offsets != nullptr, {}};
     HS_TRY(build_regions(s, cols, p.regs));
-    if (!dyn_offsets_sane(s, cols, 0, n)) return XDRG_E_INVAL;
+    if (!dyn_offsets_sane(s, cols, n)) return XDRG_E_INVAL;
     const uint64_t stride = s.fixed_part + (framed ? 4 : 0);
     if (!s.var_size) {
         const uint64_t total = n * stride;
@@ -356,7 +444,8 @@ int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uin
         return XDRG_OK;
     }
     Stager<X> st(x);
-    auto lay = [&](uint64_t lo, uint64_t m, Layout &L) { enc_layout(p, lo, m, L); };
+    Rows Rl;   // rows of the layout being sized
+    auto lay = [&](uint64_t lo, uint64_t m, Layout &L) { enc_layout(p, lo, m, L, Rl); };
     uint64_t guess = (uint64_t)((double)x.slot_bytes() / enc_avg_bytes(p));
     std::deque<Flight> q;
     uint64_t base = 0;   // stream bytes of the retired chunks
@@ -401,16 +490,19 @@ int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uin
             m = fit_chunk(lo, n, 1, x.slot_bytes(), lay, f.L);
             if (!m) return XDRG_E_NOMEM;
         }
+        f.R = Rl;   // (fit_chunk's last layout is the chunk's)
         guess = std::max<uint64_t>(m, 1);
         const uint32_t s_ = f.slot;
         while (!q.empty() && q.front().slot == s_) HS_TRY(retire());   // a one-slot ring: the chunk before leaves first
         HS_TRY(st.acquire(s_));
         uint8_t *slot = x.slot(s_);
         const Layout &L = f.L;
+        const Rows &R = f.R;
         std::vector<xdrg_column> dc(s.f.size());
         for (size_t r = 0; r < p.regs.size(); ++r) {
             const Region &g = p.regs[r];
-            HS_TRY(st.h2d(s_, slot + L.reg[r], g.base + (uint64_t)g.stride * lo, (uint64_t)g.stride * (m - 1) + g.row_end));
+            const uint32_t k0 = region_field0(g);
+            HS_TRY(st.h2d(s_, slot + L.reg[r], g.base + (uint64_t)g.stride * R.lo[k0], region_span(g, R.n[k0])));
             for (uint32_t k2 : g.fields) {
                 dc[k2].data = slot + L.reg[r] + ((const uint8_t *)cols[k2].data - g.base);
                 dc[k2].stride = cols[k2].stride;
@@ -418,10 +510,16 @@ int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uin
         }
         for (uint32_t k2 = 0; k2 < s.f.size(); ++k2) {
             const Field &fd = s.f[k2];
-            if (fd.kind == XDRG_K_DYNAMIC) {
-                const uint64_t a = cols[k2].offsets[lo];
+            if (is_group(fd)) {
+                if (fd.kind != XDRG_K_FIXED) {
+                    HS_TRY(st.h2d(s_, slot + L.off[k2], cols[k2].offsets + lo, (m + 1) * 8));
+                    dc[k2].offsets = (uint64_t *)(slot + L.off[k2]);
+                }
+                dc[k2].cap = group_elems(R, k2);
+            } else if (fd.kind == XDRG_K_DYNAMIC) {
+                const uint64_t a = cols[k2].offsets[R.lo[k2]];
                 HS_TRY(st.h2d(s_, slot + L.val[k2], (const uint8_t *)cols[k2].data + a * fd.nsz, L.vcap[k2] * fd.nsz));
-                HS_TRY(st.h2d(s_, slot + L.off[k2], cols[k2].offsets + lo, (m + 1) * 8));
+                HS_TRY(st.h2d(s_, slot + L.off[k2], cols[k2].offsets + R.lo[k2], (R.n[k2] + 1) * 8));
                 dc[k2].data = slot + L.val[k2];
                 dc[k2].offsets = (uint64_t *)(slot + L.off[k2]);
                 dc[k2].cap = L.vcap[k2];
@@ -432,12 +530,16 @@ int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uin
         }
         HS_TRY(x.h2d_done(s_));
         HS_TRY(x.kernel_begin(s_));
-        for (uint32_t k2 = 0; k2 < s.f.size(); ++k2)   // offsets relative to the chunk's first value
-            if (s.f[k2].kind == XDRG_K_DYNAMIC && cols[k2].offsets[lo])
+        for (uint32_t k2 = 0; k2 < s.f.size(); ++k2) {   // offsets relative to the chunk's first value / element
+            const Field &fd = s.f[k2];
+            if (is_group(fd) && fd.kind != XDRG_K_FIXED && cols[k2].offsets[lo])
                 HS_TRY(x.add_u64(0, dc[k2].offsets, m + 1, (uint64_t)0 - cols[k2].offsets[lo]));
+            else if (!is_group(fd) && fd.kind == XDRG_K_DYNAMIC && cols[k2].offsets[R.lo[k2]])
+                HS_TRY(x.add_u64(0, dc[k2].offsets, R.n[k2] + 1, (uint64_t)0 - cols[k2].offsets[R.lo[k2]]));
+        }
         HS_TRY(x.encode(s_, dc.data(), m, slot + L.xdr, L.xcap, L.rec ? (uint64_t *)(slot + L.rec) : nullptr,
                         flags & XDRG_FRAME_RM));
-        HS_TRY(x.kernel_end(s_, nullptr, 0));
+        HS_TRY(x.kernel_end(s_, nullptr, nullptr, nullptr, 0));
         q.push_back(std::move(f));
         // fixed-size chunks leave at once; a variable-size chunk waits for its
         // kernels while the next chunk's H2D and kernels are already queued
@@ -488,6 +590,15 @@ inline void dec_window(const DecPlan &p, uint64_t lo, uint64_t m, uint64_t &win,
     wlen = e > a ? e - a : 0;
 }
 
+// Element rows a decode window may produce for group g: each element takes
+// at least emin XDR bytes (a LIST's TRUE, the unconditional members); a
+// group whose elements may be empty is bounded by its column's capacity.
+inline uint64_t elem_bound(const Schema &s, const xdrg_column *cols, uint32_t g, uint64_t m, uint64_t wlen) {
+    const Field &f = s.f[g];
+    if (f.kind == XDRG_K_FIXED) return m * f.count;
+    return f.emin ? wlen / f.emin + 1 : cols[g].cap;
+}
+
 inline void dec_layout(const DecPlan &p, uint64_t lo, uint64_t m, Layout &L) {
     const Schema &s = p.s;
     Bump b;
@@ -496,22 +607,33 @@ inline void dec_layout(const DecPlan &p, uint64_t lo, uint64_t m, Layout &L) {
     dec_window(p, lo, m, L.win, L.wlen);
     L.xdr = b.take(L.wlen, (uintptr_t)(p.in + L.win));
     L.rec = p.ro ? b.take((m + 1) * 8, (uintptr_t)(p.ro + lo)) : 0;
+    L.rows.assign(s.f.size(), m);
+    for (uint32_t g = 0; g < s.f.size(); ++g)
+        if (is_group(s.f[g])) {
+            const uint64_t eb = elem_bound(s, p.cols, g, m, L.wlen);
+            for (uint32_t k = g + 1; k < s.f.size() && s.f[k].grp == g + 1; ++k) L.rows[k] = eb;
+        }
     L.reg.assign(p.regs.size(), 0);
     for (size_t r = 0; r < p.regs.size(); ++r) {
         const Region &g = p.regs[r];
-        L.reg[r] = b.take((uint64_t)g.stride * (m - 1) + g.row_end, (uintptr_t)(g.base + (uint64_t)g.stride * lo));
+        const uint64_t rows = L.rows[region_field0(g)];
+        L.reg[r] = b.take(region_span(g, rows), g.space ? 0 : (uintptr_t)(g.base + (uint64_t)g.stride * lo));
     }
     L.val.assign(s.f.size(), 0);
     L.off.assign(s.f.size(), 0);
     L.vcap.assign(s.f.size(), 0);
     for (uint32_t k = 0; k < s.f.size(); ++k) {
         const Field &f = s.f[k];
+        if (is_group(f)) {
+            if (f.kind != XDRG_K_FIXED) L.off[k] = b.take((m + 1) * 8);
+            continue;
+        }
         if (f.kind != XDRG_K_DYNAMIC) continue;
         // a record's elements are bounded by the bytes its stream holds
         const uint64_t cap = L.wlen / f.xsz + 1;
         L.vcap[k] = cap;
         L.val[k] = b.take(cap * f.nsz);
-        L.off[k] = b.take((m + 1) * 8);
+        L.off[k] = b.take((L.rows[k] + 1) * 8);
     }
     L.need = b.used;
 }
@@ -522,21 +644,25 @@ inline void dec_layout(const DecPlan &p, uint64_t lo, uint64_t m, Layout &L) {
 // host column's remainder); that wait overlaps chunk k's H2D.  Fixed-size
 // chunks leave as soon as they are queued; their status is read when their
 // slot comes round again.  The first chunk (in record order) that reports an
-// error ends the walk: its first failing record is the batch's.
+// error ends the walk: its first failing record is the batch's.  Repeated
+// groups: a chunk's elements follow the previous chunks' (the group column's
+// total per chunk), and its members' values follow theirs.
 template <class X>
 int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, const uint64_t *rec_offsets,
                  uint64_t n, xdrg_column *cols, uint32_t flags, uint64_t *first_bad, int *err) {
     const bool framed = flags & XDRG_FRAME_RM;
     DecPlan p{s, in, in_len, rec_offsets, n, framed, cols, {}};
     HS_TRY(build_regions(s, cols, p.regs));
-    std::vector<uint32_t> dyn;
+    // the counted columns whose totals place the next chunk: dynamic fields
+    // (their values) and DYNAMIC / LIST groups (their elements)
+    std::vector<uint32_t> cnt;
     for (uint32_t k = 0; k < s.f.size(); ++k)
-        if (s.f[k].kind == XDRG_K_DYNAMIC) dyn.push_back(k);
-    if (dyn.size() > 32) return XDRG_E_INVAL;
+        if (s.f[k].kind == XDRG_K_DYNAMIC || (is_group(s.f[k]) && s.f[k].kind != XDRG_K_FIXED)) cnt.push_back(k);
+    if (cnt.size() > 32) return XDRG_E_INVAL;
     if (first_bad) *first_bad = n;
     if (err) *err = XDRG_OK;
     if (n == 0) {
-        for (uint32_t k : dyn) cols[k].offsets[0] = 0;
+        for (uint32_t k : cnt) cols[k].offsets[0] = 0;
         return XDRG_OK;
     }
     Stager<X> st(x);
@@ -546,11 +672,11 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
         const uint64_t stride = s.fixed_part + (framed ? 4 : 0);
         double per = (double)std::max<uint64_t>(stride, 4);
         if (rec_offsets && rec_offsets[n] > rec_offsets[0]) per = (double)(rec_offsets[n] - rec_offsets[0]) / (double)n;
-        per = per * (1.0 + (double)dyn.size()) + 24.0 * (double)dyn.size() + (rec_offsets ? 8.0 : 0.0);
+        per = per * (1.0 + (double)cnt.size()) + 24.0 * (double)cnt.size() + (rec_offsets ? 8.0 : 0.0);
         for (const Region &g : p.regs) per += (double)g.stride;
         guess = std::max<uint64_t>((uint64_t)((double)x.slot_bytes() / per), 1);
     }
-    std::vector<uint64_t> next_base(s.f.size(), 0);   // elements of the chunks before the next one
+    std::vector<uint64_t> next_base(s.f.size(), 0);   // values / elements of the chunks before the next one
     std::deque<Flight> q;                              // variable-size: the chunk whose kernels run
     std::deque<std::pair<uint32_t, uint64_t>> pend;   // fixed-size: (slot, first record) awaiting status
     uint64_t fb = n;
@@ -565,29 +691,34 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
         }
         return XDRG_OK;
     };
-    // D2H of a chunk; `tot` = its element totals (variable-size)
-    auto retire = [&](const Flight &f, const uint64_t *tot) -> int {
+    // D2H of a chunk; tot[k] = its totals (values of a dynamic field, elements of a group)
+    auto retire = [&](const Flight &f, const std::vector<uint64_t> &tot) -> int {
         const uint32_t s_ = f.slot;
         const Layout &L = f.L;
         uint8_t *slot = x.slot(s_);
+        // rows of a field's column in this chunk and the first of them
+        auto rows_of = [&](uint32_t k) -> uint64_t {
+            if (!s.f[k].grp) return L.m;
+            const uint32_t g = s.f[k].grp - 1;
+            return s.f[g].kind == XDRG_K_FIXED ? L.m * s.f[g].count : tot[g];
+        };
+        auto first_of = [&](uint32_t k) -> uint64_t {
+            if (!s.f[k].grp) return L.lo;
+            const uint32_t g = s.f[k].grp - 1;
+            return s.f[g].kind == XDRG_K_FIXED ? L.lo * s.f[g].count : f.base[g];
+        };
         HS_TRY(x.d2h_begin(s_));
         for (size_t r = 0; r < p.regs.size(); ++r) {
-            const Region &g = p.regs[r];
-            uint8_t *h = (uint8_t *)g.base + (uint64_t)g.stride * L.lo;
-            if (g.full) {
-                HS_TRY(st.d2h(s_, h, slot + L.reg[r], (uint64_t)g.stride * L.m));
-            } else {
-                for (auto &sg : g.segs)
-                    HS_TRY(st.d2h_2d(s_, h + sg.first, (uint64_t)g.stride, slot + L.reg[r] + sg.first,
-                                     sg.second - sg.first, L.m));
-            }
+            const uint32_t k0 = region_field0(p.regs[r]);
+            HS_TRY(st.d2h_region(s_, p.regs[r], first_of(k0), slot + L.reg[r], rows_of(k0)));
         }
-        for (size_t i = 0; i < dyn.size(); ++i) {
-            const uint32_t k = dyn[i];
-            HS_TRY(x.add_u64(1, (uint64_t *)(slot + L.off[k]), L.m + 1, f.base[k]));
-            HS_TRY(st.d2h(s_, cols[k].offsets + L.lo, slot + L.off[k], (L.m + 1) * 8));
-            HS_TRY(st.d2h(s_, (uint8_t *)cols[k].data + f.base[k] * s.f[k].nsz, slot + L.val[k],
-                          tot[i] * s.f[k].nsz));
+        for (uint32_t k : cnt) {
+            const uint64_t rows = is_group(s.f[k]) ? L.m : rows_of(k);
+            const uint64_t first = is_group(s.f[k]) ? L.lo : first_of(k);
+            HS_TRY(x.add_u64(1, (uint64_t *)(slot + L.off[k]), rows + 1, f.base[k]));
+            HS_TRY(st.d2h(s_, cols[k].offsets + first, slot + L.off[k], (rows + 1) * 8));
+            if (!is_group(s.f[k]))
+                HS_TRY(st.d2h(s_, (uint8_t *)cols[k].data + f.base[k] * s.f[k].nsz, slot + L.val[k], tot[k] * s.f[k].nsz));
         }
         st.busy[s_] = true;
         return x.d2h_done(s_);
@@ -598,12 +729,13 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
         const Flight &f = q.front();
         uint64_t w[2 + 32];
         HS_TRY(status(f.slot, f.L.lo, w));
-        uint64_t tot[32];
-        for (size_t i = 0; i < dyn.size(); ++i) {
+        std::vector<uint64_t> tot(s.f.size(), 0);
+        for (size_t i = 0; i < cnt.size(); ++i) {
             // a failing chunk's totals may not cover its valid prefix (a decode
-            // stops at the error): it hands back every value it was granted
-            tot[i] = w[1] ? f.cap[dyn[i]] : std::min(w[2 + i], f.cap[dyn[i]]);
-            next_base[dyn[i]] = f.base[dyn[i]] + tot[i];
+            // stops at the error): it hands back every value / element it was granted
+            const uint32_t k = cnt[i];
+            tot[k] = w[1] ? f.cap[k] : std::min(w[2 + i], f.cap[k]);
+            next_base[k] = f.base[k] + tot[k];
         }
         HS_TRY(retire(f, tot));
         q.pop_front();
@@ -661,7 +793,18 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
         f.cap.assign(s.f.size(), 0);
         for (uint32_t k2 = 0; k2 < s.f.size(); ++k2) {
             const Field &fd = s.f[k2];
-            if (fd.kind == XDRG_K_DYNAMIC) {
+            if (is_group(fd)) {   // elements: after the chunks before, within the window's bound
+                if (fd.kind == XDRG_K_FIXED) {
+                    f.cap[k2] = m * fd.count;
+                    dc[k2].cap = f.cap[k2];
+                    continue;
+                }
+                f.base[k2] = next_base[k2];
+                const uint64_t left = cols[k2].cap > f.base[k2] ? cols[k2].cap - f.base[k2] : 0;
+                f.cap[k2] = std::min(left, L.rows[k2 + 1]);
+                dc[k2].offsets = (uint64_t *)(slot + L.off[k2]);
+                dc[k2].cap = f.cap[k2];
+            } else if (fd.kind == XDRG_K_DYNAMIC) {
                 f.base[k2] = next_base[k2];
                 const uint64_t left = cols[k2].cap > f.base[k2] ? cols[k2].cap - f.base[k2] : 0;
                 f.cap[k2] = std::min(left, L.vcap[k2]);
@@ -677,11 +820,29 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
         if (rec_offsets && L.win) HS_TRY(x.add_u64(0, (uint64_t *)(slot + L.rec), m + 1, (uint64_t)0 - L.win));
         HS_TRY(x.decode(s_, slot + L.xdr, L.wlen, rec_offsets ? (uint64_t *)(slot + L.rec) : nullptr, m, dc.data(),
                         flags & XDRG_FRAME_RM));
-        std::vector<const uint64_t *> extra;
-        for (uint32_t k2 : dyn) extra.push_back((const uint64_t *)(slot + L.off[k2]) + m);   // element totals
-        HS_TRY(x.kernel_end(s_, extra.data(), (uint32_t)extra.size()));
-        if (dyn.empty()) {
-            HS_TRY(retire(f, nullptr));
+        // totals: a dynamic field's offsets at its last row (a member's: at the
+        // chunk's element total, read on the device), a group's at record m
+        // (the element total is read on the device only when within the member's
+        // laid-out rows: a failing decode may leave it anywhere, and then the
+        // totals are the grants anyway)
+        std::vector<const uint64_t *> extra, index;
+        std::vector<uint64_t> limit;
+        for (uint32_t k2 : cnt) {
+            const Field &fd = s.f[k2];
+            const uint64_t *o = (const uint64_t *)(slot + L.off[k2]);
+            limit.push_back(L.rows[k2]);
+            if (!fd.grp || is_group(fd)) {
+                extra.push_back(o + m);
+                index.push_back(nullptr);
+            } else {
+                const Field &gf = s.f[fd.grp - 1];
+                extra.push_back(gf.kind == XDRG_K_FIXED ? o + m * gf.count : o);
+                index.push_back(gf.kind == XDRG_K_FIXED ? nullptr : (const uint64_t *)(slot + L.off[fd.grp - 1]) + m);
+            }
+        }
+        HS_TRY(x.kernel_end(s_, extra.data(), index.data(), limit.data(), (uint32_t)extra.size()));
+        if (cnt.empty()) {
+            HS_TRY(retire(f, std::vector<uint64_t>(s.f.size(), 0)));
             pend.push_back({s_, lo});
         } else {
             q.push_back(std::move(f));
@@ -740,6 +901,7 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
     std::vector<uint32_t> dyn;
     uint64_t minmsg = 4;   // a mark
     if (mode == RECV_DECODE) {
+        if (sp->groups) return XDRG_E_INVAL;   // (group schemas: device or mapped receive)
         HS_TRY(build_regions(*sp, cols, regs));
         for (const Region &g : regs)
             if (!g.stride) return XDRG_E_INVAL;   // constant columns are encode-only
@@ -994,7 +1156,7 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             }
             std::vector<const uint64_t *> extra;
             for (uint32_t k2 : dyn) extra.push_back((const uint64_t *)(slot + c.L.off[k2]) + m);
-            HS_TRY(x.kernel_end(cur.slot, extra.data(), (uint32_t)extra.size()));
+            HS_TRY(x.kernel_end(cur.slot, extra.data(), nullptr, nullptr, (uint32_t)extra.size()));
             if (c.hoffs) {   // the caller's message offsets (without them the device copy stays
                 HS_TRY(x.d2h_begin(cur.slot));   // window-relative: an error reads one entry, settle)
                 HS_TRY(x.add_u64(1, doffs, m + 1, cur.hpos));
@@ -1003,7 +1165,7 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             }
             pend.push_back(std::move(c));
         } else {
-            HS_TRY(x.kernel_end(cur.slot, nullptr, 0));
+            HS_TRY(x.kernel_end(cur.slot, nullptr, nullptr, nullptr, 0));
             HS_TRY(x.d2h_begin(cur.slot));
             if (mode == RECV_DEFRAME) {
                 HS_TRY(st.d2h(cur.slot, payload + pbytes, dbody, res[3]));

@@ -101,6 +101,16 @@ int launch_copy_link(uint8_t *dst, const uint8_t *src, uint64_t bytes, void *str
     return (int)hipGetLastError();
 }
 
+__global__ void k_pick_u64(uint64_t *dst, const uint64_t *base, const uint64_t *index, uint64_t limit) {
+    if (threadIdx.x || blockIdx.x) return;
+    const uint64_t i = *index;
+    *dst = i <= limit ? base[i] : 0;
+}
+int launch_pick_u64(uint64_t *dst, const uint64_t *base, const uint64_t *index, uint64_t limit, void *stream) {
+    hipLaunchKernelGGL(k_pick_u64, dim3(1), dim3(64), 0, (hipStream_t)stream, dst, base, index, limit);
+    return (int)hipGetLastError();
+}
+
 __global__ void k_add_u64(uint64_t *p, uint64_t n, uint64_t delta) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         p[i] += delta;

@@ -1390,11 +1390,15 @@ struct HipExec {
         c->stream = keep;
         return rc;
     }
-    int kernel_end(uint32_t i, const uint64_t *const *extra, uint32_t nextra) {
+    int kernel_end(uint32_t i, const uint64_t *const *extra, const uint64_t *const *index, const uint64_t *limit,
+                   uint32_t nextra) {
         if (nextra + 2 > kResWords) return inval(c, "too many dynamic fields for the staging status");
         uint64_t *w = r.d_res + (uint64_t)i * kResWords;
-        for (uint32_t j = 0; j < nextra; ++j)
-            HIPCHK(c, hipMemcpyAsync(w + 2 + j, extra[j], 8, hipMemcpyDeviceToDevice, r.comp));
+        for (uint32_t j = 0; j < nextra; ++j) {
+            if (index && index[j])
+                HIPCHK(c, (hipError_t)launch_pick_u64(w + 2 + j, extra[j], index[j], limit[j], r.comp));
+            else HIPCHK(c, hipMemcpyAsync(w + 2 + j, extra[j], 8, hipMemcpyDeviceToDevice, r.comp));
+        }
         HIPCHK(c, hipMemcpyAsync(r.h_res + (uint64_t)i * kResWords, w, 8 * (2 + nextra), hipMemcpyDeviceToHost, r.comp));
         r.nres[i] = 2 + nextra;
         HIPCHK(c, hipEventRecord(r.e_kern[i], r.comp));
@@ -1480,14 +1484,22 @@ static void stage_schema(const xdrg_schema *s, hs::Schema &v) {
     v.f.resize(s->f.size());
     uint64_t ndyn = 0;
     for (size_t k = 0; k < s->f.size(); ++k) {
-        v.f[k] = hs::Field{s->f[k].type, s->f[k].kind, s->f[k].count, s->nsz[k], s->xsz[k], s->xbytes[k]};
-        ndyn += s->f[k].kind == XDRG_K_DYNAMIC;
+        const xdrg_field &f = s->f[k];
+        v.f[k] = hs::Field{f.type, f.kind, f.count, s->nsz[k], s->xsz[k], s->xbytes[k], s->grp[k], 0};
+        ndyn += f.kind == XDRG_K_DYNAMIC;
+        if (f.type != XDRG_T_GROUP) continue;
+        // fewest XDR bytes of an element: a list's TRUE, its unconditional members
+        uint32_t e = f.kind == XDRG_K_LIST ? 4 : 0;
+        for (uint32_t j = 1; j <= f.reserved; ++j)
+            if (!s->cond[k + j]) e += s->f[k + j].kind == XDRG_K_DYNAMIC ? 4 : s->xbytes[k + j];
+        v.f[k].emin = e;
+        v.groups = true;
     }
     v.fixed_part = s->fixed_part;
     v.var_size = s->var_size;
     // a well-formed record: every fixed field, a length word per dynamic field
     // (absent arms of a conditional schema may take any of it away)
-    v.min_xdr = s->ncond ? 0 : s->fixed_part + 4 * ndyn;
+    v.min_xdr = s->ncond || s->ngroups ? 0 : s->fixed_part + 4 * ndyn;
 }
 
 // Device views of host columns (XDRG_HOST_MAPPED).  Every span a kernel may
@@ -1564,7 +1576,6 @@ static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
         if ((n && !dout) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
         return encode_impl(c, s, dc.data(), n, dout, out_cap, drec, dflags, out_len, 0, nullptr);
     }
-    if (s->ngroups) return inval(c, "repeated groups: XDRG_HOST_PTRS takes XDRG_HOST_MAPPED");
     hs::Schema v;
     stage_schema(s, v);
     rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);
@@ -1600,7 +1611,6 @@ static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         if ((in_len && !din) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
         return decode_impl(c, s, din, in_len, drec, n, dc.data(), dflags, first_bad, err, 0, nullptr);
     }
-    if (s->ngroups) return inval(c, "repeated groups: XDRG_HOST_PTRS takes XDRG_HOST_MAPPED");
     hs::Schema v;
     stage_schema(s, v);
     rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);

@@ -110,11 +110,21 @@ struct CpuExec {
         res[s][1] = (uint64_t)(uint32_t)err;
         return XDRG_OK;
     }
-    int kernel_end(uint32_t s, const uint64_t *const *extra, uint32_t ne) {
+    int kernel_end(uint32_t s, const uint64_t *const *extra, const uint64_t *const *index, const uint64_t *limit,
+                   uint32_t ne) {
         CHECK(ne <= 64);
         for (uint32_t j = 0; j < ne; ++j) {
-            CHECK(in_arena((const uint8_t *)extra[j], 8));
-            res[s][2 + j] = *extra[j];
+            const uint64_t *p = extra[j];
+            if (index && index[j]) {
+                CHECK(in_arena((const uint8_t *)index[j], 8));
+                if (*index[j] > limit[j]) {
+                    res[s][2 + j] = 0;
+                    continue;
+                }
+                p += *index[j];
+            }
+            CHECK(in_arena((const uint8_t *)p, 8));
+            res[s][2 + j] = *p;
         }
         nres[s] = 2 + ne;
         return XDRG_OK;
@@ -217,7 +227,7 @@ struct Batch {
     hs::Schema hs;
 };
 
-static void random_schema(std::mt19937_64 &g, Batch &b) {
+static void random_schema(std::mt19937_64 &g, Batch &b, bool with_groups = false) {
     static const uint32_t types[] = {XDRG_T_INT, XDRG_T_UINT, XDRG_T_ENUM, XDRG_T_BOOL, XDRG_T_HYPER,
                                      XDRG_T_UHYPER, XDRG_T_FLOAT, XDRG_T_DOUBLE, XDRG_T_SHORT, XDRG_T_BYTE,
                                      XDRG_T_OPAQUE, XDRG_T_STRING};
@@ -235,9 +245,35 @@ static void random_schema(std::mt19937_64 &g, Batch &b) {
         else if (disc >= 0 && g() % 3 == 0) b.c.push_back({(uint32_t)k, (uint32_t)disc, 1, 1, nullptr});
     }
     for (auto &c : b.c) c.values = b.cvals.data();
+    // sometimes a repeated group last (an array of structs or a list,
+    // include/xdrg.h "Repeated groups"), 1-3 members of the base types
+    if (with_groups && g() % 3 == 0) {
+        const uint32_t m = 1 + (uint32_t)(g() % 3);
+        const uint32_t kind = 1 + (uint32_t)(g() % 3);   // FIXED, DYNAMIC, LIST
+        b.f.push_back({XDRG_T_GROUP, kind, kind == XDRG_K_FIXED ? (uint32_t)(g() % 4) : 0u, m});
+        for (uint32_t j = 0; j < m; ++j) {
+            xdrg_field x{types[g() % 12], 0, 0, 0};
+            if (x.type == XDRG_T_STRING) x.kind = XDRG_K_DYNAMIC;
+            else if (x.type == XDRG_T_BOOL) x.kind = XDRG_K_SCALAR;
+            else if (x.type == XDRG_T_OPAQUE) x.kind = 1 + g() % 2;
+            else x.kind = g() % 3;
+            if (x.kind == XDRG_K_FIXED) x.count = 1 + (uint32_t)(g() % 5);
+            b.f.push_back(x);
+        }
+    }
     uint64_t fixed = 0;
     bool var = !b.c.empty();
-    for (auto &x : b.f) {
+    uint32_t grp = 0, left = 0;
+    for (size_t k = 0; k < b.f.size(); ++k) {
+        const auto &x = b.f[k];
+        if (x.type == XDRG_T_GROUP) {
+            b.hs.f.push_back({x.type, x.kind, x.count, 0, 0, 0, 0, 0});
+            b.hs.groups = true;
+            grp = (uint32_t)k + 1;
+            left = x.reserved;
+            var = true;
+            continue;
+        }
         const uint32_t ns = nsz_of(x.type), xs = xsz_of(x.type);
         uint32_t xb = 0;
         if (x.kind != XDRG_K_DYNAMIC) {
@@ -247,10 +283,24 @@ static void random_schema(std::mt19937_64 &g, Batch &b) {
         } else {
             var = true;
         }
-        b.hs.f.push_back({x.type, x.kind, x.count, ns, xs, xb});
+        b.hs.f.push_back({x.type, x.kind, x.count, ns, xs, xb, left ? grp : 0u, 0});
+        if (left && grp) {
+            auto &gf = b.hs.f[grp - 1];
+            gf.emin += x.kind == XDRG_K_DYNAMIC ? 4 : xb;
+            if (--left == 0 && gf.kind == XDRG_K_LIST) gf.emin += 4;
+        }
     }
     b.hs.fixed_part = fixed;
     b.hs.var_size = var;
+}
+
+// Rows of field k's column: records, or its group's elements.
+static uint64_t rows_of(const Batch &b, size_t k, uint64_t upto) {
+    const uint32_t gp = b.hs.f[k].grp;
+    if (!gp) return upto;
+    const xdrg_field &gf = b.f[gp - 1];
+    if (gf.kind == XDRG_K_FIXED) return upto * gf.count;
+    return b.offs[gp - 1][upto];
 }
 
 static void random_values(std::mt19937_64 &g, Batch &b, bool for_encode) {
@@ -259,12 +309,26 @@ static void random_values(std::mt19937_64 &g, Batch &b, bool for_encode) {
     b.offs.assign(nf, {});
     b.aos_off.assign(nf, UINT64_MAX);
     b.cols.assign(nf, xdrg_column{nullptr, 0, nullptr, 0});
+    for (size_t k = 0; k < nf; ++k) {   // group element offsets first (they size the members)
+        const auto &x = b.f[k];
+        if (x.type != XDRG_T_GROUP) continue;
+        xdrg_column &col = b.cols[k];
+        if (x.kind == XDRG_K_FIXED) {
+            col.cap = b.n * x.count;
+            continue;
+        }
+        auto &o = b.offs[k];
+        o.assign(b.n + 1, 0);
+        for (uint64_t i = 0; i < b.n; ++i) o[i + 1] = o[i] + (g() % 10 == 0 ? g() % 40 : g() % 4);
+        col.offsets = o.data();
+        col.cap = o[b.n];
+    }
     // AoS record: the fixed fields that draw it, each aligned to its element size
     uint64_t so = 0;
     const bool aos = g() % 2;
     for (size_t k = 0; k < nf; ++k) {
         const auto &x = b.f[k];
-        if (x.kind == XDRG_K_DYNAMIC || !aos || g() % 4 == 0) continue;
+        if (x.kind == XDRG_K_DYNAMIC || x.type == XDRG_T_GROUP || b.hs.f[k].grp || !aos || g() % 4 == 0) continue;
         const uint64_t e = hs::fixed_elem_bytes(b.hs.f[k]);
         if (!e) continue;
         const uint64_t al = nsz_of(x.type);   // natural alignment (the oracle loads elements in place)
@@ -277,36 +341,38 @@ static void random_values(std::mt19937_64 &g, Batch &b, bool for_encode) {
     for (auto &v : b.aos) v = (uint8_t)g();
     for (size_t k = 0; k < nf; ++k) {
         const auto &x = b.f[k];
+        if (x.type == XDRG_T_GROUP) continue;
         xdrg_column &col = b.cols[k];
         const uint32_t ns = nsz_of(x.type);
+        const uint64_t rows = rows_of(b, k, b.n);
         if (x.kind == XDRG_K_DYNAMIC) {
             auto &o = b.offs[k];
-            o.assign(b.n + 1, 0);
-            for (uint64_t i = 0; i < b.n; ++i) o[i + 1] = o[i] + (g() % 8 == 0 ? g() % 300 : g() % 12);
-            b.data[k].assign(o[b.n] * ns + 8, 0);
+            o.assign(rows + 1, 0);
+            for (uint64_t i = 0; i < rows; ++i) o[i + 1] = o[i] + (g() % 8 == 0 ? g() % 300 : g() % 12);
+            b.data[k].assign(o[rows] * ns + 8, 0);
             for (auto &v : b.data[k]) v = (uint8_t)g();
             col.data = b.data[k].data();
             col.offsets = o.data();
-            col.cap = o[b.n];
+            col.cap = o[rows];
             continue;
         }
         const uint64_t e = hs::fixed_elem_bytes(b.hs.f[k]);
         if (b.aos_off[k] != UINT64_MAX) {
             col.data = b.aos.data() + b.aos_off[k];
             col.stride = (int64_t)b.aos_stride;
-        } else if (for_encode && e && g() % 6 == 0) {
+        } else if (for_encode && e && !b.hs.f[k].grp && g() % 6 == 0) {
             b.data[k].assign(e, 0);
             for (auto &v : b.data[k]) v = (uint8_t)g();
             col.data = b.data[k].data();
             col.stride = XDRG_STRIDE_CONST;
         } else {
-            b.data[k].assign(e * b.n + 8, 0);
+            b.data[k].assign(e * rows + 8, 0);
             for (auto &v : b.data[k]) v = (uint8_t)g();
             col.data = b.data[k].data();
             col.stride = 0;
         }
         if (x.type == XDRG_T_BOOL) {   // discriminants and bools: 0 / 1
-            for (uint64_t i = 0; i < (col.stride == XDRG_STRIDE_CONST ? 1 : b.n); ++i) {
+            for (uint64_t i = 0; i < (col.stride == XDRG_STRIDE_CONST ? 1 : rows); ++i) {
                 uint8_t *p = (uint8_t *)col.data + (col.stride == XDRG_STRIDE_CONST ? 0 : i * (col.stride ? col.stride : 1));
                 *p = (uint8_t)(g() % 2);
             }
@@ -327,14 +393,28 @@ static void empty_like(std::mt19937_64 &g, const Batch &b, Batch &o, uint64_t sl
     o.aos_stride = b.aos_stride;
     o.aos.assign(b.aos.size(), 0x5a);
     o.cols.assign(nf, xdrg_column{nullptr, 0, nullptr, 0});
+    std::vector<uint64_t> rows(nf, b.n);   // rows of each column (members: the group's element capacity)
     for (size_t k = 0; k < nf; ++k) {
         const auto &x = b.f[k];
+        if (x.type != XDRG_T_GROUP) continue;
+        uint64_t cap = x.kind == XDRG_K_FIXED ? b.n * x.count : b.offs[k][b.n] + slack;
+        if (x.kind != XDRG_K_FIXED) {
+            if (g() % 8 == 0 && cap) cap = g() % cap;   // too few elements: CAPACITY
+            o.offs[k].assign(b.n + 1, 0x77);
+            o.cols[k].offsets = o.offs[k].data();
+        }
+        o.cols[k].cap = cap;
+        for (size_t j = k + 1; j < nf && b.hs.f[j].grp == k + 1; ++j) rows[j] = cap;
+    }
+    for (size_t k = 0; k < nf; ++k) {
+        const auto &x = b.f[k];
+        if (x.type == XDRG_T_GROUP) continue;
         xdrg_column &col = o.cols[k];
         const uint32_t ns = nsz_of(x.type);
         if (x.kind == XDRG_K_DYNAMIC) {
-            uint64_t cap = b.offs[k][b.n] + slack;
+            uint64_t cap = b.offs[k][rows_of(b, k, b.n)] + slack;
             if (g() % 8 == 0 && cap) cap = g() % cap;   // too small: CAPACITY
-            o.offs[k].assign(b.n + 1, 0x77);
+            o.offs[k].assign(rows[k] + 1, 0x77);
             o.data[k].assign(cap * ns + 8, 0x33);
             col.data = o.data[k].data();
             col.offsets = o.offs[k].data();
@@ -346,7 +426,7 @@ static void empty_like(std::mt19937_64 &g, const Batch &b, Batch &o, uint64_t sl
             col.data = o.aos.data() + o.aos_off[k];
             col.stride = (int64_t)o.aos_stride;
         } else {
-            o.data[k].assign(e * b.n + 8, 0x44);
+            o.data[k].assign(e * rows[k] + 8, 0x44);
             col.data = o.data[k].data();
             col.stride = 0;
         }
@@ -354,31 +434,38 @@ static void empty_like(std::mt19937_64 &g, const Batch &b, Batch &o, uint64_t sl
 }
 
 static void compare_prefix(const Batch &a, const Batch &b, uint64_t upto) {
+    for (size_t k = 0; k < a.f.size(); ++k) {   // group element offsets (they index the members below)
+        const auto &x = a.f[k];
+        if (x.type != XDRG_T_GROUP || x.kind == XDRG_K_FIXED || !a.n) continue;
+        for (uint64_t i = 0; i <= upto; ++i) CHECK(a.offs[k][i] == b.offs[k][i]);
+    }
     for (size_t k = 0; k < a.f.size(); ++k) {
         const auto &x = a.f[k];
+        if (x.type == XDRG_T_GROUP) continue;
         const uint32_t ns = nsz_of(x.type);
+        const uint64_t rup = a.n ? rows_of(b, k, upto) : 0;   // this column's rows of the records before upto
         if (x.kind == XDRG_K_DYNAMIC) {
             // (for n = 0 the oracle leaves offsets[0] alone; the engine writes 0)
             CHECK(a.n || a.offs[k][0] == 0);
-            for (uint64_t i = 0; i <= upto && a.n; ++i) {
+            for (uint64_t i = 0; i <= rup && a.n; ++i) {
                 if (a.offs[k][i] != b.offs[k][i])
                     std::fprintf(stderr, "field %zu rec %llu: staged %llu whole %llu (upto %llu, n %llu)\n", k,
                                  (unsigned long long)i, (unsigned long long)a.offs[k][i],
                                  (unsigned long long)b.offs[k][i], (unsigned long long)upto, (unsigned long long)a.n);
                 CHECK(a.offs[k][i] == b.offs[k][i]);
             }
-            if (a.n && std::memcmp(a.data[k].data(), b.data[k].data(), a.offs[k][upto] * ns) != 0) {
+            if (a.n && std::memcmp(a.data[k].data(), b.data[k].data(), a.offs[k][rup] * ns) != 0) {
                 uint64_t j = 0;
                 while (a.data[k][j] == b.data[k][j]) ++j;
                 std::fprintf(stderr, "field %zu values differ at byte %llu of %llu (type %u)\n", k, (unsigned long long)j,
-                             (unsigned long long)(a.offs[k][upto] * ns), a.f[k].type);
+                             (unsigned long long)(a.offs[k][rup] * ns), a.f[k].type);
                 CHECK(false);
             }
             continue;
         }
         const uint64_t e = hs::fixed_elem_bytes(a.hs.f[k]);
         const int64_t st = a.cols[k].stride ? a.cols[k].stride : (int64_t)e;
-        for (uint64_t i = 0; i < upto; ++i)
+        for (uint64_t i = 0; i < rup; ++i)
             CHECK(std::memcmp((const uint8_t *)a.cols[k].data + i * st, (const uint8_t *)b.cols[k].data + i * st, e) == 0);
     }
     // AoS bytes no field covers are the caller's: never written by a decode
@@ -547,10 +634,11 @@ static uint64_t receive_rounds(std::mt19937_64 &g, int rounds) {
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 300;
     std::mt19937_64 g(0x0DCAC4E5);
-    uint64_t chunks_grown = 0, errs = 0, caps = 0, bounced = 0, direct = 0;
+    uint64_t chunks_grown = 0, errs = 0, caps = 0, bounced = 0, direct = 0, group_rounds = 0;
     for (int r = 0; r < rounds; ++r) {
         Batch b;
-        random_schema(g, b);
+        random_schema(g, b, true);
+        group_rounds += b.hs.groups;
         b.n = g() % 5 == 0 ? g() % 4 : g() % 1500;
         random_values(g, b, true);
         const uint32_t flags = g() % 2 ? XDRG_FRAME_RM : 0;
@@ -645,7 +733,8 @@ int main(int argc, char **argv) {
         bounced += x.bounced;
         direct += x.direct;
     }
-    CHECK(chunks_grown > 0 && errs > 0 && caps > 0 && bounced > 0 && direct > 0);
+    CHECK(chunks_grown > 0 && errs > 0 && caps > 0 && bounced > 0 && direct > 0 && group_rounds > 0);
+    std::printf("san_stage: %llu rounds with a repeated group\n", (unsigned long long)group_rounds);
     const uint64_t rx = receive_rounds(g, rounds);
     std::printf("san_stage: %d receive rounds ok (%llu windows)\n", rounds, (unsigned long long)rx);
     std::printf("san_stage: %d rounds ok (ring grown %llu times, %llu decode errors, %llu capacity, "

@@ -296,29 +296,48 @@ def test_host_conditional_schema(hctx):
     assert back.equal(ref)
 
 
-def test_host_groups_take_mapped(hctx):
-    """Repeated groups: the staged host path refuses them (INVAL); mapped host
-    buffers decode them in place, equal to the oracle."""
-    fields = [(I, SC, 0), (G, LS, 0, 2), (U, SC, 0), (STR, DY, 0), (I, SC, 0)]
-    n = 2000
-    hb0 = random_batch(fields, n, seed=13, dyn_len=(0, 12), group_len=(0, 5))
-    rc, want, offs = oracle.encode_batch(fields, hb0.columns(), n, hb0.xdr_total() + 64)
+GROUP_SHAPES = {
+    # portmap DUMP's pmaplist (a T *next list), an array of structs with strings
+    # and vectors inside, a fixed array of structs; a top-level string beside them
+    "list": [(I, SC, 0), (G, LS, 0, 2), (U, SC, 0), (STR, DY, 0), (I, SC, 0)],
+    "array": [(STR, DY, 0), (G, DY, 0, 4), (H, SC, 0), (O, DY, 0), (I, DY, 0), (O, FX, 3)],
+    "fixed": [(U, SC, 0), (G, FX, 3, 2), (S, SC, 0), (STR, DY, 0), (D, SC, 0)],
+}
+
+
+@pytest.mark.parametrize("kind", ["pageable", "registered", "mapped"])
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
+@pytest.mark.parametrize("shape", list(GROUP_SHAPES))
+def test_host_groups_vs_oracle(hctx, shape, framed, kind):
+    """Repeated groups on host memory: staged (a chunk of records moves its
+    elements' member rows with it; 64 KiB slots, so lists straddle many
+    chunks) and mapped in place, encode and decode equal to the oracle;
+    then a decode with too few element slots (CAPACITY at the oracle's
+    record)."""
+    fields = GROUP_SHAPES[shape]
+    n = 3000
+    hb0 = random_batch(fields, n, seed=13 + len(shape), dyn_len=(0, 12), group_len=(0, 9), special_floats=False)
+    rc, want, offs = oracle.encode_batch(fields, hb0.columns(), n, hb0.xdr_total(framed) + 64, framed=framed)
     assert rc == 0
     sch = engine.Schema(fields)
-    with pytest.raises(engine.XdrgError):
-        hctx.encode(sch, hb0.columns(), n, np.zeros(len(want), np.uint8), len(want), host=True)
-    mem = Registered()
+    mem = Registered() if kind != "pageable" else Pageable()
+    host, mapped = kind != "mapped", kind == "mapped"
     try:
         hb = moved(hb0, mem)
         out = mem.array(np.zeros(len(want), np.uint8))
         ro = mem.array(np.zeros(n + 1, np.uint64))
-        assert hctx.encode(sch, hb.columns(), n, out, len(want), rec_offsets=ro, mapped=True) == len(want)
+        assert hctx.encode(sch, hb.columns(), n, out, len(want), rec_offsets=ro, framed=framed, host=host,
+                           mapped=mapped) == len(want)
         assert out.tobytes() == want
-        back = moved(HostBatch.empty(fields, n, hb0.dyn_caps()), mem)
-        assert hctx.decode(sch, out, len(want), n, back.columns(), rec_offsets=ro, mapped=True) == (0, n, 0)
-        ref = HostBatch.empty(fields, n, hb0.dyn_caps())
-        assert oracle.decode_batch(fields, want, offs, n, ref.columns()) == (0, n, 0)
-        assert back.equal(ref)
+        assert np.array_equal(ro, offs)
+        for caps in (hb0.dyn_caps(), {k: v // 2 for k, v in hb0.dyn_caps().items()}):
+            back = moved(HostBatch.empty(fields, n, caps), mem)
+            st = hctx.decode(sch, out, len(want), n, back.columns(), rec_offsets=ro, framed=framed, host=host,
+                             mapped=mapped, raise_on_error=False)
+            ref = HostBatch.empty(fields, n, caps)
+            wst = oracle.decode_batch(fields, want, offs, n, ref.columns(), framed=framed)
+            assert st == wst
+            assert back.equal(ref, upto=wst[1])
     finally:
         mem.close()
 
