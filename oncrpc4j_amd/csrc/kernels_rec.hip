@@ -698,8 +698,12 @@ __device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t 
         // branch-free: the per-record branches of this check, inlined into the
         // one-pass sweep (and into a device-function form of the sizes
         // kernel), lost the FRAME error of a record cut short by in_len on
-        // this compiler (ROCm 7.2; a printf in the branch made it correct);
-        // selects keep one straight-line form (tests/test_spec_counts.py)
+        // this compiler (ROCm 7.2; a printf in the branch made it correct):
+        // the join after the size compare runs the matched edge's phi copy
+        // of err under the restored exec of every LAST-set lane, see
+        // profiles/r04_compiler/README.md; selects keep one straight-line
+        // form (tests/test_spec_counts.py)
+#ifndef XDRG_BRANCHY_MARK
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {
             const uint64_t left = end[j] - pos[j];
@@ -711,6 +715,25 @@ __device__ __forceinline__ void walk_counts_lockstep(const RecArgs &a, uint64_t 
             err[j] = live ? e : err[j];
             pos[j] += (live && !e) ? 4 : 0;
         }
+#else   // experiment build (tools/mkexp.sh branchy -DXDRG_BRANCHY_MARK): round 3's branchy form
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
+            if (err[j]) continue;
+            if (end[j] - pos[j] < 4) { err[j] = XDRG_E_SHORT; continue; }
+            const uint32_t mk = bswap32r(m[j]);
+            const uint64_t want_len = a.rec_in ? end[j] - pos[j] - 4 : a.rec_stride - 4;
+#ifdef XDRG_BRANCHY_PRINTF
+            if (!(mk & kLastFrag) || (uint64_t)(mk & kSizeMask) != want_len) {
+                if (r0 + (uint64_t)j * rs + 1 == a.n) printf("frame r=%llu\n", (unsigned long long)(r0 + j * rs));
+                err[j] = XDRG_E_FRAME;
+                continue;
+            }
+#else
+            if (!(mk & kLastFrag) || (uint64_t)(mk & kSizeMask) != want_len) { err[j] = XDRG_E_FRAME; continue; }
+#endif
+            pos[j] += 4;
+        }
+#endif
     }
     uint32_t d = 0;
     for (uint32_t k = 0; k < a.nf; ++k) {
