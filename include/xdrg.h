@@ -111,18 +111,24 @@ typedef struct xdrg_field {
  * (struct T { ...; T *next; }, used as `T *x`) as BE(1) + element for every
  * element and a closing BE(0).  On the tape a group is one field
  * {XDRG_T_GROUP, kind FIXED / DYNAMIC / LIST, count, reserved = m} followed
- * by its m member fields (SCALAR, FIXED or DYNAMIC of the base types; no
- * nested groups).  A condition (xdrg_cond below) stays on its level: a
- * top-level field (the group field included) on a top-level discriminant,
- * a member on an earlier member of its own group, evaluated per element.
- * Columns: the
- * group's own column has offsets[n + 1] (DYNAMIC / LIST: record i owns
- * elements [offsets[i], offsets[i+1]); FIXED: element i*count + j, offsets
- * unused) and, on decode, cap = element capacity; data is unused.  A member's
- * column is indexed by ELEMENT: fixed members at data + e*stride, dynamic
- * members own [offsets[e], offsets[e+1]) (offsets has elements + 1 entries).
- * Decode errors keep the reference's order: the count / list bools / member
- * checks as the element loop meets them; a negative count is XDRG_E_NEG_SIZE. */
+ * by its m member fields (SCALAR, FIXED or DYNAMIC of the base types) — or,
+ * one level down, an inner group (an array of structs / list inside the
+ * element, jrpcgen.java:856-906 calling the inner elements' xdrEncode) whose
+ * own members are base types; the outer m counts the inner group's whole
+ * span.  A condition (xdrg_cond below) stays on its level: a top-level
+ * field (the group field included) on a top-level discriminant, a member (an
+ * inner group included) on an earlier member of its own group, evaluated per
+ * element.  Columns: the group's own column has offsets[rows + 1] (DYNAMIC /
+ * LIST: row i owns elements [offsets[i], offsets[i+1]); FIXED: element
+ * i*count + j, offsets unused) where rows are the records (top level) or the
+ * outer group's elements (an inner group), and, on decode, cap = element
+ * capacity; data is unused.  A member's column is indexed by ELEMENT of its
+ * own group: fixed members at data + e*stride, dynamic members own
+ * [offsets[e], offsets[e+1]) (offsets has elements + 1 entries).  Decode
+ * errors keep the reference's order: the count / list bools / member checks
+ * as the element loops meet them; a negative count is XDRG_E_NEG_SIZE.
+ * XDRG_HOST_PTRS staging takes one level of groups (inner groups: device
+ * memory or XDRG_HOST_MAPPED).                                              */
 
 /* One native column.  Fixed-size fields (SCALAR / FIXED): record i's first
  * element is at  data + i*stride  (stride 0 = packed = elem_size*count), so

@@ -14,7 +14,9 @@ engine works on a batch of N records of one schema laid out as columns
   its members; the group's array is offsets[n+1] (element ranges; None for
   a FIXED group: record i owns elements i*count ...), and every member array
   is indexed by ELEMENT (fixed: (E,) / (E, count); dynamic: (values,
-  offsets[E+1])).
+  offsets[E+1])).  A member may itself be a group (one level down, its
+  members counted in the outer `members`): its array is indexed by the outer
+  group's elements (offsets[E+1]) and its own members by its elements.
 
 HostBatch holds numpy arrays (fixtures, the oracle's host pointers);
 DeviceBatch holds torch tensors in HBM (the engine's device pointers).
@@ -41,18 +43,23 @@ def pad4(n):
 
 
 def parents(fields):
-    """parent[k] = index of the group field k is a member of, or -1."""
+    """parent[k] = index of the group field k is an immediate member of, or -1
+    (an inner group claims its own members after its parent's span)."""
     par = [-1] * len(fields)
-    k = 0
-    while k < len(fields):
-        f = fields[k]
+    for k, f in enumerate(fields):
         if f[0] == abi.T_GROUP:
             for j in range(1, f[3] + 1):
                 par[k + j] = k
-            k += f[3] + 1
-        else:
-            k += 1
     return par
+
+
+def direct_members(fields, g):
+    """Indices of group g's immediate members (an inner group's members skipped)."""
+    out, j = [], g + 1
+    while j <= g + fields[g][3]:
+        out.append(j)
+        j += 1 + (fields[j][3] if fields[j][0] == abi.T_GROUP else 0)
+    return out
 
 
 def _is_group(f):
@@ -93,23 +100,28 @@ class HostBatch:
     def elems(self, g, upto=None):
         """Elements of group g in records [0, upto)."""
         f = self.fields[g]
-        n = self.n if upto is None else upto
+        rows = self.rows(g, upto)
         if f[1] == abi.K_FIXED:
-            return n * f[2]
-        return int(self.arrays[g][n])
+            return rows * f[2]
+        return int(self.arrays[g][rows])
 
-    def rows(self, k):
-        """Rows of field k's array: records, or its group's elements."""
+    def rows(self, k, upto=None):
+        """Rows of field k's array in records [0, upto): records, or its group's elements."""
         g = self.parent[k]
-        return self.n if g < 0 else self.elems(g)
+        n = self.n if upto is None else upto
+        return n if g < 0 else self.elems(g, n)
 
     def _elem_cap(self, g):
         """Element capacity of group g: the smallest over its members (fixed
         members are indexed by element with no capacity of their own)."""
         caps = []
-        for j in range(1, self.fields[g][3] + 1):
-            m = self.arrays[g + j]
-            caps.append((len(m[1]) - 1) if self.fields[g + j][1] == abi.K_DYNAMIC else m.shape[0])
+        for j in direct_members(self.fields, g):
+            m = self.arrays[j]
+            f = self.fields[j]
+            if _is_group(f):
+                caps.append(len(m) - 1 if m is not None else self._elem_cap(j) // max(f[2], 1))
+            else:
+                caps.append((len(m[1]) - 1) if f[1] == abi.K_DYNAMIC else m.shape[0])
         return min(caps)
 
     # ---- construction ----------------------------------------------------
@@ -118,15 +130,14 @@ class HostBatch:
         """Zeroed output columns for a decode; dyn_caps[k] = element capacity
         (of a dynamic field, of a group, or of a group's dynamic member)."""
         fields = [tuple(f) for f in fields]
-        par = parents(fields)
         caps = dyn_caps or {}
+        rows_of = _cap_rows(fields, n, caps)
         arrays = []
         for k, f in enumerate(fields):
             t, kind, c = f[0], f[1], f[2]
-            rows = n if par[k] < 0 else (n * fields[par[k]][2] if fields[par[k]][1] == abi.K_FIXED
-                                          else caps.get(par[k], 0))
+            rows = rows_of[k]
             if _is_group(f):
-                arrays.append(None if kind == abi.K_FIXED else np.zeros(n + 1, dtype=np.uint64))
+                arrays.append(None if kind == abi.K_FIXED else np.zeros(rows + 1, dtype=np.uint64))
                 continue
             dt = NP_DTYPE[t]
             if kind == abi.K_DYNAMIC:
@@ -182,6 +193,22 @@ class HostBatch:
             return 4 + cnt * abi.XDR_SIZE[f[0]]
         return np.full(rows, field_xdr_bytes(f[:3]), dtype=np.uint64)
 
+    def _group_sizes(self, k, rows):
+        """XDR bytes of group k at each of its `rows` rows (its count / closing
+        bool and every element, inner groups included)."""
+        f = self.fields[k]
+        E = self.elems(k)
+        es = np.full(E, 4 if f[1] == abi.K_LIST else 0, dtype=np.uint64)
+        for j in direct_members(self.fields, k):
+            es += self._group_sizes(j, E) if _is_group(self.fields[j]) else self._field_sizes(j, E)
+        ce = np.zeros(E + 1, dtype=np.uint64)
+        np.cumsum(es, out=ce[1:])
+        if f[1] == abi.K_FIXED:
+            bounds = np.arange(rows + 1, dtype=np.uint64) * f[2]
+        else:
+            bounds = self.arrays[k][:rows + 1].astype(np.uint64)
+        return ce[bounds[1:]] - ce[bounds[:-1]] + {abi.K_DYNAMIC: 4, abi.K_LIST: 4, abi.K_FIXED: 0}[f[1]]
+
     def xdr_sizes(self, framed=False):
         """Per-record XDR size (numpy uint64)."""
         s = np.full(self.n, 4 if framed else 0, dtype=np.uint64)
@@ -192,18 +219,7 @@ class HostBatch:
                 s += self._field_sizes(k, self.n)
                 k += 1
                 continue
-            E = self.elems(k)
-            es = np.full(E, 4 if f[1] == abi.K_LIST else 0, dtype=np.uint64)
-            for j in range(k + 1, k + 1 + f[3]):
-                es += self._field_sizes(j, E)
-            ce = np.zeros(E + 1, dtype=np.uint64)
-            np.cumsum(es, out=ce[1:])
-            if f[1] == abi.K_FIXED:
-                bounds = np.arange(self.n + 1, dtype=np.uint64) * f[2]
-            else:
-                bounds = self.arrays[k][:self.n + 1].astype(np.uint64)
-            s += ce[bounds[1:]] - ce[bounds[:-1]]
-            s += {abi.K_DYNAMIC: 4, abi.K_LIST: 4, abi.K_FIXED: 0}[f[1]]
+            s += self._group_sizes(k, self.n)
             k += 1 + f[3]
         return s
 
@@ -216,7 +232,7 @@ class HostBatch:
         for k, f in enumerate(self.fields):
             if _is_group(f):
                 if self.arrays[k] is not None:
-                    tot += 8 * self.n
+                    tot += 8 * self.rows(k)
             elif f[1] == abi.K_DYNAMIC:
                 vals, offs = self.arrays[k]
                 tot += int(offs[self.rows(k)]) * vals.dtype.itemsize
@@ -243,11 +259,11 @@ class HostBatch:
             if _is_group(f):
                 if f[1] == abi.K_FIXED:
                     arrays.append(None)
-                    rng[k] = (lo * f[2], hi * f[2])
+                    rng[k] = (a * f[2], b * f[2])
                 else:
                     offs = self.arrays[k]
-                    arrays.append((offs[lo:hi + 1] - offs[lo]).astype(np.uint64))
-                    rng[k] = (int(offs[lo]), int(offs[hi]))
+                    arrays.append((offs[a:b + 1] - offs[a]).astype(np.uint64))
+                    rng[k] = (int(offs[a]), int(offs[b]))
             elif f[1] == abi.K_DYNAMIC:
                 vals, offs = self.arrays[k]
                 x, y = int(offs[a]), int(offs[b])
@@ -263,8 +279,8 @@ class HostBatch:
             g = self.parent[k]
             rows = n if g < 0 else self.elems(g, n)
             if _is_group(f):
-                if f[1] != abi.K_FIXED and not np.array_equal(self.arrays[k][:n + 1],
-                                                                other.arrays[k][:n + 1]):
+                if f[1] != abi.K_FIXED and not np.array_equal(self.arrays[k][:rows + 1],
+                                                                other.arrays[k][:rows + 1]):
                     return False
             elif f[1] == abi.K_DYNAMIC:
                 va, oa = self.arrays[k]
@@ -282,11 +298,12 @@ class HostBatch:
 
 # ---- synthetic batches (seeded) -------------------------------------------
 def random_batch(fields, n, seed, dyn_len=(0, 16), string_alphabet=b"abcdefghijklmnopqrstuvwxyz",
-                 special_floats=True, group_len=(0, 4)):
+                 special_floats=True, group_len=(0, 4), inner_len=(0, 3)):
     """Seeded synthetic batch: ints uniform over their full range, floats as
     random bit patterns (NaNs with payloads included), bools 0/1/other
     non-zero bytes, dynamic lengths uniform in dyn_len, DYNAMIC / LIST group
-    element counts uniform in group_len (both inclusive)."""
+    element counts uniform in group_len (inner groups: inner_len; both
+    inclusive)."""
     rng = np.random.default_rng(seed)
     fields = [tuple(f) for f in fields]
     par = parents(fields)
@@ -298,11 +315,11 @@ def random_batch(fields, n, seed, dyn_len=(0, 16), string_alphabet=b"abcdefghijk
         if t == abi.T_GROUP:
             if kind == abi.K_FIXED:
                 arrays.append(None)
-                elems[k] = n * c
+                elems[k] = rows * c
             else:
-                lo, hi = group_len
-                cnt = rng.integers(lo, hi + 1, size=n, dtype=np.uint64)
-                offs = np.zeros(n + 1, dtype=np.uint64)
+                lo, hi = group_len if par[k] < 0 else inner_len
+                cnt = rng.integers(lo, hi + 1, size=rows, dtype=np.uint64)
+                offs = np.zeros(rows + 1, dtype=np.uint64)
                 np.cumsum(cnt, out=offs[1:])
                 arrays.append(offs)
                 elems[k] = int(offs[-1])
@@ -325,6 +342,22 @@ def random_batch(fields, n, seed, dyn_len=(0, 16), string_alphabet=b"abcdefghijk
             size = int(np.prod(shape))
             arrays.append(_random_values(rng, dt, size, t, special_floats).reshape(shape))
     return HostBatch(fields, n, arrays)
+
+
+def _cap_rows(fields, n, caps):
+    """Rows of every field's array in an empty (decode output) batch: records
+    at top level, a FIXED group's rows x count, else caps[group]."""
+    par = parents(fields)
+    rows = [0] * len(fields)
+    for k in range(len(fields)):
+        p = par[k]
+        if p < 0:
+            rows[k] = n
+        elif fields[p][1] == abi.K_FIXED:
+            rows[k] = rows[p] * fields[p][2]
+        else:
+            rows[k] = caps.get(p, 0)
+    return rows
 
 
 def _random_values(rng, dt, size, t, special_floats):
@@ -407,16 +440,15 @@ class DeviceBatch:
     def empty(cls, fields, n, dyn_caps=None, device="cuda"):
         import torch
         fields = [tuple(f) for f in fields]
-        par = parents(fields)
         caps = dyn_caps or {}
+        rows_of = _cap_rows(fields, n, caps)
         tensors, dts = [], []
         for k, f in enumerate(fields):
             t, kind, c = f[0], f[1], f[2]
-            rows = n if par[k] < 0 else (n * fields[par[k]][2] if fields[par[k]][1] == abi.K_FIXED
-                                          else caps.get(par[k], 0))
+            rows = rows_of[k]
             if _is_group(f):
                 tensors.append(None if kind == abi.K_FIXED else
-                               torch.zeros(n + 1, dtype=torch.int64, device=device))
+                               torch.zeros(rows + 1, dtype=torch.int64, device=device))
                 dts.append(None)
                 continue
             dt = np.dtype(NP_DTYPE[t])
@@ -435,9 +467,13 @@ class DeviceBatch:
     def _elem_cap(self, g):
         """Element capacity of group g: the smallest over its members."""
         caps = []
-        for j in range(1, self.fields[g][3] + 1):
-            m = self.tensors[g + j]
-            caps.append((m[1].numel() - 1) if self.fields[g + j][1] == abi.K_DYNAMIC else m.shape[0])
+        for j in direct_members(self.fields, g):
+            m = self.tensors[j]
+            f = self.fields[j]
+            if _is_group(f):
+                caps.append(m.numel() - 1 if m is not None else self._elem_cap(j) // max(f[2], 1))
+            else:
+                caps.append((m[1].numel() - 1) if f[1] == abi.K_DYNAMIC else m.shape[0])
         return min(caps)
 
     def columns(self):

@@ -180,29 +180,58 @@ __device__ __forceinline__ bool g_dec_field_present(const GroupArgs &a, uint32_t
     return p;
 }
 
-// XDR bytes of element e of group g (its list bool included).
+// XDR bytes of element e of group g (its list bool included).  L = the
+// group's depth: an element at depth 0 may hold an inner array of structs /
+// list (a member group), whose count word, elements and closing bool are the
+// element's bytes too, as the element's generated xdrEncode writes them
+// (jrpcgen.java:856-906, 835-851).
+template <int L>
+__device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g, uint64_t row, GDisc &d);
+template <int L>
 __device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g, uint64_t e, GDisc d) {
-    if (!a.f[g].ncm) {
-        uint64_t s = a.f[g].efix;
-        for (uint32_t j = 1; j <= a.f[g].nmem; ++j) {
+    const GField &G = a.f[g];
+    if (!G.ncm && !G.ngm) {
+        uint64_t s = G.efix;
+        for (uint32_t j = 1; j <= G.nmem; ++j) {
             const GField &m = a.f[g + j];
             if (m.kind == XDRG_K_DYNAMIC) s += g_dyn_bytes(m, m.offsets[e + 1] - m.offsets[e]);
         }
         return s;
     }
-    uint64_t s = a.f[g].kind == XDRG_K_LIST ? 4 : 0;
-    for (uint32_t j = 1; j <= a.f[g].nmem; ++j) {
+    uint64_t s = G.kind == XDRG_K_LIST ? 4 : 0;
+    for (uint32_t j = 1; j <= G.nmem; ++j) {
         const GField &m = a.f[g + j];
-        if (!g_enc_field_present(a, g + j, e, d)) continue;
+        const bool p = !G.ncm || g_enc_field_present(a, g + j, e, d);
+        if (m.type == XDRG_T_GROUP) {
+            if constexpr (L == 0) {
+                if (p) s += g_group_bytes<1>(a, g + j, e, d);
+            }
+            j += m.nmem;
+            continue;
+        }
+        if (!p) continue;
         s += m.kind == XDRG_K_DYNAMIC ? g_dyn_bytes(m, m.offsets[e + 1] - m.offsets[e]) : (uint64_t)m.xbytes;
     }
+    return s;
+}
+// XDR bytes of group g at row `row` of its column (a record, or an element
+// of the enclosing group): its count / closing bool and every element.
+template <int L>
+__device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g, uint64_t row, GDisc &d) {
+    const GField &G = a.f[g];
+    uint64_t e0, cnt;
+    g_range(G, row, e0, cnt);
+    uint64_t s = G.kind == XDRG_K_FIXED ? 0 : 4;   // the count, or a list's closing bool
+    if (G.ndm || G.ncm) for (uint64_t e = e0; e < e0 + cnt; ++e) s += g_elem_bytes<L>(a, g, e, d);
+    else s += cnt * G.efix;
     return s;
 }
 
 // ===========================================================================
 // Encode
 // ===========================================================================
-__device__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
+template <bool NEST>
+__device__ __forceinline__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
     uint64_t s = a.framed ? 4 : 0;
     GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
@@ -212,11 +241,7 @@ __device__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
             continue;
         }
         if (f.type == XDRG_T_GROUP) {
-            uint64_t e0, cnt;
-            g_range(f, r, e0, cnt);
-            s += f.kind == XDRG_K_FIXED ? 0 : 4;   // the count, or a list's closing bool
-            if (f.ndm || f.ncm) for (uint64_t e = e0; e < e0 + cnt; ++e) s += g_elem_bytes(a, k, e, d);
-            else s += cnt * f.efix;
+            s += g_group_bytes<NEST ? 0 : 1>(a, k, r, d);
             k += 1 + f.nmem;
             continue;
         }
@@ -226,13 +251,14 @@ __device__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
     return s;
 }
 
+template <bool NEST>
 __global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a) {
     const uint64_t r0 = (uint64_t)blockIdx.x * kRecPerBlock + (uint64_t)threadIdx.x * kRecPerThread;
     uint64_t s = 0;
     for (int j = 0; j < kRecPerThread; ++j) {
         const uint64_t r = r0 + j;
         if (r >= a.n) break;
-        const uint64_t z = g_rec_size(a, r);
+        const uint64_t z = g_rec_size<NEST>(a, r);
         a.rec_size[r] = z;
         s += z;
     }
@@ -240,16 +266,28 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a
     if (threadIdx.x == 0) a.block_sums[blockIdx.x] = tot;
 }
 
-// One lane writes element e of group g at stream byte p.
-__device__ void g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t p, GDisc d) {
+// One lane writes element e of group g at stream byte p; returns its end.
+template <int L>
+__device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, uint64_t row, uint64_t p, GDisc &d);
+template <int L>
+__device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t p, GDisc d) {
     uint8_t *out = a.xdr;
-    if (a.f[g].kind == XDRG_K_LIST) {   // xdrEncodeBoolean(true) (pmaplist.java:65-67)
+    const GField &G = a.f[g];
+    if (G.kind == XDRG_K_LIST) {   // xdrEncodeBoolean(true) (pmaplist.java:65-67)
         *(uint32_t *)(out + p) = bswap32r(1u);
         p += 4;
     }
-    for (uint32_t j = 1; j <= a.f[g].nmem; ++j) {
+    for (uint32_t j = 1; j <= G.nmem; ++j) {
         const GField &m = a.f[g + j];
-        if (a.f[g].ncm && !g_enc_field_present(a, g + j, e, d)) continue;   // an element's absent arm
+        const bool present = !G.ncm || g_enc_field_present(a, g + j, e, d);   // an element's absent arm
+        if (m.type == XDRG_T_GROUP) {   // an inner array / list: this lane writes it whole
+            if constexpr (L == 0) {
+                if (present) p = g_enc_group<1>(a, g + j, e, p, d);
+            }
+            j += m.nmem;
+            continue;
+        }
+        if (!present) continue;
         if (m.kind != XDRG_K_DYNAMIC) {
             for (uint32_t w = 0; w < m.xbytes >> 2; ++w) *(uint32_t *)(out + p + 4 * w) = g_fixed_word(m, e, w);
             p += m.xbytes;
@@ -261,6 +299,25 @@ __device__ void g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t 
         for (uint64_t w = 0; w < nw; ++w) *(uint32_t *)(out + p + 4 + 4 * w) = g_dyn_word(m, e0, cnt, w);
         p += 4 + 4 * nw;
     }
+    return p;
+}
+// Group g at row `row` of its column, by one lane from stream byte p.
+template <int L>
+__device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, uint64_t row, uint64_t p, GDisc &d) {
+    uint8_t *out = a.xdr;
+    const GField &G = a.f[g];
+    uint64_t e0, cnt;
+    g_range(G, row, e0, cnt);
+    if (G.kind == XDRG_K_DYNAMIC) {   // xdrEncodeInt($size) (jrpcgen.java:866-876)
+        *(uint32_t *)(out + p) = bswap32r((uint32_t)cnt);
+        p += 4;
+    }
+    for (uint64_t e = e0; e < e0 + cnt; ++e) p = g_enc_elem<L>(a, g, e, p, d);
+    if (G.kind == XDRG_K_LIST) {      // xdrEncodeBoolean(false)
+        *(uint32_t *)(out + p) = 0;
+        p += 4;
+    }
+    return p;
 }
 
 // G lanes (a wave or a part of one: G divides 64) write record r at stream
@@ -279,8 +336,9 @@ __device__ __forceinline__ uint64_t g_incl_scan(uint64_t v, uint32_t ln) {
     }
     return v;
 }
-template <uint32_t G>
+template <uint32_t G, bool NEST>
 __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint64_t size, uint32_t ln) {
+    constexpr int L0 = NEST ? 0 : 1;   // depth the record's groups start at (1: inner groups compiled out)
     uint8_t *out = a.xdr;
     if (a.framed) {   // GrizzlyRpcTransport.java:103-110
         if (ln == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
@@ -301,15 +359,15 @@ __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint6
                 pos += 4;
             }
             if (!f.ndm && !f.ncm) {   // elements of one size: a lane per element
-                for (uint64_t i = ln; i < cnt; i += G) g_enc_elem(a, k, e0 + i, pos + i * f.efix, d);
+                for (uint64_t i = ln; i < cnt; i += G) g_enc_elem<L0>(a, k, e0 + i, pos + i * f.efix, d);
                 pos += cnt * f.efix;
             } else {        // a lane per element at its scanned position
                 // (the group's lanes stay together: the scan's shuffles need all G)
                 for (uint64_t b = 0; b < cnt; b += G) {
                     const uint64_t i = b + ln;
-                    const uint64_t z = i < cnt ? g_elem_bytes(a, k, e0 + i, d) : 0;
+                    const uint64_t z = i < cnt ? g_elem_bytes<L0>(a, k, e0 + i, d) : 0;
                     const uint64_t incl = g_incl_scan<G>(z, ln);
-                    if (i < cnt) g_enc_elem(a, k, e0 + i, pos + incl - z, d);
+                    if (i < cnt) g_enc_elem<L0>(a, k, e0 + i, pos + incl - z, d);
                     pos += __shfl(incl, G - 1, G);
                 }
             }
@@ -334,7 +392,7 @@ __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint6
     }
 }
 
-template <uint32_t G>
+template <uint32_t G, bool NEST>
 __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a) {
     __shared__ uint64_t soff[kRecPerBlock + 1];
     const uint64_t total = a.totals[0];
@@ -364,7 +422,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a
     const uint32_t ng = kRecThreads / G, ln = threadIdx.x & (G - 1);
     for (uint32_t j0 = 0; j0 < nrec; j0 += ng) {
         const uint32_t j = j0 + threadIdx.x / G;
-        if (j < nrec) g_enc_record<G>(a, rb + j, soff[j], soff[j + 1] - soff[j], ln);
+        if (j < nrec) g_enc_record<G, NEST>(a, rb + j, soff[j], soff[j + 1] - soff[j], ln);
     }
 }
 
@@ -402,8 +460,74 @@ __device__ __forceinline__ uint32_t g_walk_dyn(const GField &f, const uint8_t *i
     return 0;
 }
 
+// Walk group g from pos (its count word or list bools and every element, each
+// member's checks in the reference's order: jrpcgen.java:886-906 reads the
+// count with no checkArraySize, so a negative one is NegativeArraySizeException;
+// a list reads xdrDecodeBoolean() before every element, any non-zero = another,
+// Xdr.java:404-407); cnt[s] += the counts of the counted columns it meets.
+// L = depth: an element at depth 0 may hold an inner group, walked the same way.
+template <int L>
+__device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t end, uint64_t &pos,
+                                 uint32_t (&cnt)[kMaxSlots], GDisc &d) {
+    const GField &f = a.f[g];
+    uint64_t n;
+    if (f.kind == XDRG_K_DYNAMIC) {   // int $size = xdr.xdrDecodeInt(); new T[$size]
+        if (end - pos < 4) return XDRG_E_SHORT;
+        const int32_t c = (int32_t)g_ld(in + pos);
+        pos += 4;
+        if (c < 0) return XDRG_E_NEG_SIZE;
+        n = (uint64_t)c;
+    } else {
+        n = f.kind == XDRG_K_FIXED ? f.count : ~0ull;
+    }
+    if (!f.ndm && !f.ncm && f.kind != XDRG_K_LIST) {   // elements of one size
+        if ((end - pos) / f.efix < n) return XDRG_E_SHORT;
+        pos += n * f.efix;
+    } else {
+        uint64_t i = 0;
+        for (;; ++i) {
+            if (f.kind == XDRG_K_LIST) {   // xdrDecodeBoolean(): any non-zero = another
+                if (end - pos < 4) return XDRG_E_SHORT;
+                const uint32_t more = g_ld(in + pos);
+                pos += 4;
+                if (!more) break;
+            } else if (i == n) {
+                break;
+            }
+            for (uint32_t j = 1; j <= f.nmem; ++j) {
+                const GField &m = a.f[g + j];
+                const bool present = !f.ncm || g_dec_field_present(a, g + j, in, pos, end, d);
+                if (m.type == XDRG_T_GROUP) {   // an inner array / list of this element
+                    if constexpr (L == 0) {
+                        if (present) {
+                            const uint32_t err = g_walk_group<1>(a, g + j, in, end, pos, cnt, d);
+                            if (err) return err;
+                        }
+                    }
+                    j += m.nmem;
+                    continue;
+                }
+                if (!present) continue;
+                if (m.kind != XDRG_K_DYNAMIC) {
+                    if (end - pos < m.xbytes) return XDRG_E_SHORT;
+                    pos += m.xbytes;
+                } else {
+                    uint32_t len = 0;
+                    const uint32_t err = g_walk_dyn(m, in, end, pos, len);
+                    if (err) return err;
+                    cnt[m.slot - 1] += len;
+                }
+            }
+        }
+        n = i;
+    }
+    if (f.slot) cnt[f.slot - 1] += (uint32_t)n;   // (an inner group: summed over the outer elements)
+    return 0;
+}
+
 // Walk record r; cnt[s] = the record's count of counted column s.
-__device__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxSlots], uint32_t *sub) {
+template <bool NEST>
+__device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxSlots], uint32_t *sub) {
     const GExtent e = g_extent(a, r);
     const uint8_t *in = a.xdr;
     uint64_t pos = e.a;
@@ -423,47 +547,8 @@ __device__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxS
             continue;
         }
         if (f.type == XDRG_T_GROUP) {
-            uint64_t n;
-            if (f.kind == XDRG_K_DYNAMIC) {   // int $size = xdr.xdrDecodeInt(); new T[$size]
-                if (e.b - pos < 4) return XDRG_E_SHORT;
-                const int32_t c = (int32_t)g_ld(in + pos);
-                pos += 4;
-                if (c < 0) return XDRG_E_NEG_SIZE;
-                n = (uint64_t)c;
-            } else {
-                n = f.kind == XDRG_K_FIXED ? f.count : ~0ull;
-            }
-            if (!f.ndm && !f.ncm && f.kind != XDRG_K_LIST) {   // elements of one size
-                if ((e.b - pos) / f.efix < n) return XDRG_E_SHORT;
-                pos += n * f.efix;
-            } else {
-                uint64_t i = 0;
-                for (;; ++i) {
-                    if (f.kind == XDRG_K_LIST) {   // xdrDecodeBoolean(): any non-zero = another
-                        if (e.b - pos < 4) return XDRG_E_SHORT;
-                        const uint32_t more = g_ld(in + pos);
-                        pos += 4;
-                        if (!more) break;
-                    } else if (i == n) {
-                        break;
-                    }
-                    for (uint32_t j = 1; j <= f.nmem; ++j) {
-                        const GField &m = a.f[k + j];
-                        if (f.ncm && !g_dec_field_present(a, k + j, in, pos, e.b, d)) continue;
-                        if (m.kind != XDRG_K_DYNAMIC) {
-                            if (e.b - pos < m.xbytes) return XDRG_E_SHORT;
-                            pos += m.xbytes;
-                        } else {
-                            uint32_t len = 0;
-                            const uint32_t err = g_walk_dyn(m, in, e.b, pos, len);
-                            if (err) return err;
-                            cnt[m.slot - 1] += len;
-                        }
-                    }
-                }
-                n = i;
-            }
-            if (f.slot) cnt[f.slot - 1] = (uint32_t)n;
+            const uint32_t err = g_walk_group<NEST ? 0 : 1>(a, k, in, e.b, pos, cnt, d);
+            if (err) return err;
             k += 1 + f.nmem;
             continue;
         }
@@ -481,6 +566,7 @@ __device__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxS
     return 0;
 }
 
+template <bool NEST>
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a) {
     const uint64_t r0 = (uint64_t)blockIdx.x * kRecPerBlock + (uint64_t)threadIdx.x * kRecPerThread;
     uint64_t sums[kMaxSlots];
@@ -491,7 +577,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a)
         uint32_t cnt[kMaxSlots];
         for (uint32_t s = 0; s < a.nslot; ++s) cnt[s] = 0;
         uint32_t sub;
-        const uint32_t err = g_walk(a, r, cnt, &sub);
+        const uint32_t err = g_walk<NEST>(a, r, cnt, &sub);
         if (err) {
             atomicMin(a.errkey, err_key(r, sub, err));
             for (uint32_t s = 0; s < a.nslot; ++s) cnt[s] = 0;   // a failed record owns nothing
@@ -504,6 +590,25 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a)
     for (uint32_t s = 0; s < a.nslot; ++s) {
         const uint64_t tot = block_sum(sums[s]);
         if (threadIdx.x == 0) a.block_sums[(uint64_t)s * a.nblocks + blockIdx.x] = tot;
+    }
+}
+
+// Elements of group g over the whole batch (the rows of its members'
+// columns): a FIXED group multiplies its parent's rows, others have their
+// column total; false when a level's total exceeds its capacity (the
+// capacity error stands and no offsets[rows] entry is in bounds).
+__device__ __forceinline__ bool g_batch_rows(const GroupArgs &a, uint32_t g, uint64_t &rows) {
+    uint64_t mult = 1;
+    for (;;) {
+        const GField &G = a.f[g];
+        if (G.kind != XDRG_K_FIXED) {
+            const uint64_t t = a.totals[G.slot - 1];
+            rows = t * mult;
+            return t <= G.cap;
+        }
+        mult *= G.count;
+        if (!G.grp) { rows = a.n * mult; return true; }
+        g = G.grp - 1;
     }
 }
 
@@ -536,13 +641,9 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_offsets(const GroupArgs
             off += c[j];
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) {   // offsets[rows] = the column's total
-            if (!f.grp) {
-                f.offsets[a.n] = a.totals[s];
-            } else {
-                const GField &g = a.f[f.grp - 1];
-                const uint64_t rows = g.kind == XDRG_K_FIXED ? a.n * g.count : a.totals[g.slot - 1];
-                if (a.totals[s] <= f.cap && (g.kind == XDRG_K_FIXED || rows <= g.cap)) f.offsets[rows] = a.totals[s];
-            }
+            uint64_t rows;
+            if (!f.grp) f.offsets[a.n] = a.totals[s];
+            else if (a.totals[s] <= f.cap && g_batch_rows(a, f.grp - 1, rows)) f.offsets[rows] = a.totals[s];
         }
     }
 }
@@ -558,9 +659,146 @@ __device__ __forceinline__ void g_zero_fixed(const GField &f, uint64_t i) {
     for (uint64_t b = 0; b < nb; ++b) p[b] = 0;
 }
 
+// Running native offsets of the counted columns of one record's group, in
+// registers (slot-indexed selects): reading back the offsets just stored made
+// every element wait for the previous one's store (READDIR decode 9.5 ->
+// DESIGN.md §5.7).
+struct GRun {
+    uint64_t v[kMaxSlots];
+    __device__ __forceinline__ uint64_t get(uint32_t slot) const {   // slot = GField::slot (1-based)
+        uint64_t x = 0;
+#pragma unroll
+        for (int q = 0; q < kMaxSlots; ++q) x = (uint32_t)q + 1 == slot ? v[q] : x;
+        return x;
+    }
+    __device__ __forceinline__ void set(uint32_t slot, uint64_t x) {
+#pragma unroll
+        for (int q = 0; q < kMaxSlots; ++q) v[q] = (uint32_t)q + 1 == slot ? x : v[q];
+    }
+};
+__device__ __forceinline__ uint64_t g_rec_base(const GroupArgs &a, uint32_t slot, uint64_t r) {
+    return a.rec_base[(uint64_t)(slot - 1) * a.n + r];
+}
+// Top-level group k at record r, first element e0: every counted column of
+// its span starts at the record's base (a direct member at row e0, an inner
+// group's member at its record's first inner element), and its first offsets
+// entry is written (an empty record leaves the next record's entry the same).
+__device__ __forceinline__ void g_run_init(const GroupArgs &a, uint32_t k, uint64_t r, uint64_t e0, GRun &run) {
+#pragma unroll
+    for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;
+    const GField &f = a.f[k];
+    for (uint32_t j = 1; j <= f.nmem; ++j) {
+        const GField &m = a.f[k + j];
+        if (!m.slot) continue;
+        const uint64_t b0 = g_rec_base(a, m.slot, r);
+        run.set(m.slot, b0);
+        uint64_t row = e0;
+        if (m.grp != k + 1) {   // a member of an inner group: rows are inner elements
+            const GField &ig = a.f[m.grp - 1];
+            row = ig.kind == XDRG_K_FIXED ? e0 * ig.count : g_rec_base(a, ig.slot, r);
+        }
+        m.offsets[row] = b0;
+    }
+}
+
+// Element e of group g with no bytes on the wire (an absent T x[N]'s N
+// elements): fixed members zero, dynamic members and inner arrays empty.
+template <int L>
+__device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, uint64_t e, GRun &run) {
+    const GField &G = a.f[g];
+    for (uint32_t j = 1; j <= G.nmem; ++j) {
+        const GField &m = a.f[g + j];
+        if (m.type == XDRG_T_GROUP) {
+            if constexpr (L == 0) {
+                if (m.kind != XDRG_K_FIXED) m.offsets[e + 1] = run.get(m.slot);
+                else for (uint64_t i = e * m.count; i < (e + 1) * m.count; ++i) g_absent_elem<1>(a, g + j, i, run);
+            }
+            j += m.nmem;
+            continue;
+        }
+        if (m.kind != XDRG_K_DYNAMIC) g_zero_fixed(m, e);
+        else m.offsets[e + 1] = run.get(m.slot);
+    }
+}
+
+template <int L>
+__device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in, uint64_t &pos,
+                           uint64_t end, GDisc &d, GRun &run);
+// Inner group g (a member of an element at depth 0) of outer element e: its
+// count word or list bools, read as the walk checked them, then its elements.
+__device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in,
+                                            uint64_t &pos, uint64_t end, GDisc &d, GRun &run) {
+    const GField &G = a.f[g];
+    const uint64_t i0 = G.kind == XDRG_K_FIXED ? e * G.count : run.get(G.slot);
+    uint64_t n = G.count;
+    if (G.kind == XDRG_K_DYNAMIC) {
+        n = g_ld(in + pos);
+        pos += 4;
+    }
+    uint64_t i = 0;
+    for (;; ++i) {
+        if (G.kind == XDRG_K_LIST) {
+            const uint32_t more = g_ld(in + pos);
+            pos += 4;
+            if (!more) break;
+        } else if (i == n) {
+            break;
+        }
+        g_dec_elem<1>(a, g, i0 + i, in, pos, end, d, run);
+    }
+    if (G.kind != XDRG_K_FIXED) {
+        G.offsets[e + 1] = i0 + i;
+        run.set(G.slot, i0 + i);
+    }
+}
+
+// The members of element e of group g (after a list element's TRUE).
+template <int L>
+__device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in, uint64_t &pos,
+                           uint64_t end, GDisc &d, GRun &run) {
+    const GField &f = a.f[g];
+    for (uint32_t j = 1; j <= f.nmem; ++j) {
+        const GField &m = a.f[g + j];
+        const bool present = !f.ncm || g_dec_field_present(a, g + j, in, pos, end, d);   // an element's absent arm
+        if (m.type == XDRG_T_GROUP) {
+            if constexpr (L == 0) {
+                if (present) {
+                    g_dec_inner(a, g + j, e, in, pos, end, d, run);
+                } else if (m.kind != XDRG_K_FIXED) {
+                    m.offsets[e + 1] = run.get(m.slot);
+                } else {
+                    for (uint64_t i = e * m.count; i < (e + 1) * m.count; ++i) g_absent_elem<1>(a, g + j, i, run);
+                }
+            }
+            j += m.nmem;
+            continue;
+        }
+        const uint64_t v0 = m.kind == XDRG_K_DYNAMIC ? run.get(m.slot) : 0;
+        if (!present) {
+            if (m.kind != XDRG_K_DYNAMIC) g_zero_fixed(m, e);
+            else m.offsets[e + 1] = v0;
+            continue;
+        }
+        if (m.kind != XDRG_K_DYNAMIC) {
+            for (uint32_t w = 0; w < m.xbytes >> 2; ++w) g_fixed_store(m, e, w, *(const uint32_t *)(in + pos + 4 * w));
+            pos += m.xbytes;
+            continue;
+        }
+        const uint64_t len = g_ld(in + pos);
+        m.offsets[e + 1] = v0 + len;
+        run.set(m.slot, v0 + len);
+        const uint64_t nw = g_dyn_words(m, len);
+        if (m.xsz == 1) g_dec_bytes(m.data + v0, in + pos + 4, len);
+        else for (uint64_t w = 0; w < nw; ++w) g_dyn_store(m, v0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
+        pos += 4 + 4 * nw;
+    }
+}
+
 // in: where stream offset x is read, in + x (the stream, or an LDS tile
 // holding this record's bytes: k_grp_dec_place_lds).
+template <bool NEST>
 __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in) {
+    constexpr int L0 = NEST ? 0 : 1;   // depth the record's groups start at (1: inner groups compiled out)
     const GExtent ex = g_extent(a, r);   // the extent the walk checked (clamped to in_len)
     const uint64_t end = ex.b;
     uint64_t pos = ex.a + (a.framed ? 4 : 0);
@@ -574,66 +812,22 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
                 continue;
             }
             if (f.kind == XDRG_K_FIXED) {   // an absent T x[N]: N zero / empty elements
-                for (uint32_t j = 1; j <= f.nmem; ++j) {
-                    const GField &m = a.f[k + j];
-                    for (uint64_t e = r * f.count; e < (r + 1) * f.count; ++e) {
-                        if (m.kind != XDRG_K_DYNAMIC) {
-                            g_zero_fixed(m, e);
-                        } else {
-                            if (e == r * f.count) m.offsets[e] = a.rec_base[(uint64_t)(m.slot - 1) * a.n + r];
-                            m.offsets[e + 1] = m.offsets[e];
-                        }
-                    }
-                }
+                GRun run;
+                g_run_init(a, k, r, r * f.count, run);
+                for (uint64_t e = r * f.count; e < (r + 1) * f.count; ++e) g_absent_elem<L0>(a, k, e, run);
             }
             k += 1 + f.nmem;
             continue;
         }
         if (f.type == XDRG_T_GROUP) {
-            const uint64_t e0 = f.kind == XDRG_K_FIXED ? r * f.count : a.rec_base[(uint64_t)(f.slot - 1) * a.n + r];
+            const uint64_t e0 = f.kind == XDRG_K_FIXED ? r * f.count : g_rec_base(a, f.slot, r);
             const uint64_t cnt = f.kind == XDRG_K_FIXED ? f.count : a.rec_cnt[(uint64_t)(f.slot - 1) * a.n + r];
             if (f.kind == XDRG_K_DYNAMIC) pos += 4;
-            // each dynamic member's running native offset, in registers (slot-indexed
-            // selects): reading back the offsets just stored made every element wait
-            // for the previous one's store (READDIR decode 9.5 -> see DESIGN.md §5.7)
-            uint64_t run[kMaxSlots];
-#pragma unroll
-            for (int q = 0; q < kMaxSlots; ++q) run[q] = 0;
-            for (uint32_t j = 1; j <= f.nmem; ++j) {   // each dynamic member's first value
-                const GField &m = a.f[k + j];
-                if (m.kind != XDRG_K_DYNAMIC) continue;
-                const uint64_t b0 = a.rec_base[(uint64_t)(m.slot - 1) * a.n + r];
-                m.offsets[e0] = b0;
-#pragma unroll
-                for (int q = 0; q < kMaxSlots; ++q) run[q] = (uint32_t)q == m.slot - 1 ? b0 : run[q];
-            }
+            GRun run;
+            g_run_init(a, k, r, e0, run);
             for (uint64_t e = e0; e < e0 + cnt; ++e) {
                 if (f.kind == XDRG_K_LIST) pos += 4;   // its TRUE
-                for (uint32_t j = 1; j <= f.nmem; ++j) {
-                    const GField &m = a.f[k + j];
-                    uint64_t v0 = 0;
-                    if (m.kind == XDRG_K_DYNAMIC)
-#pragma unroll
-                        for (int q = 0; q < kMaxSlots; ++q) v0 = (uint32_t)q == m.slot - 1 ? run[q] : v0;
-                    if (f.ncm && !g_dec_field_present(a, k + j, in, pos, end, d)) {   // an element's absent arm
-                        if (m.kind != XDRG_K_DYNAMIC) g_zero_fixed(m, e);
-                        else m.offsets[e + 1] = v0;
-                        continue;
-                    }
-                    if (m.kind != XDRG_K_DYNAMIC) {
-                        for (uint32_t w = 0; w < m.xbytes >> 2; ++w) g_fixed_store(m, e, w, *(const uint32_t *)(in + pos + 4 * w));
-                        pos += m.xbytes;
-                        continue;
-                    }
-                    const uint64_t len = g_ld(in + pos);
-                    m.offsets[e + 1] = v0 + len;
-#pragma unroll
-                    for (int q = 0; q < kMaxSlots; ++q) run[q] = (uint32_t)q == m.slot - 1 ? v0 + len : run[q];
-                    const uint64_t nw = g_dyn_words(m, len);
-                    if (m.xsz == 1) g_dec_bytes(m.data + v0, in + pos + 4, len);
-                    else for (uint64_t w = 0; w < nw; ++w) g_dyn_store(m, v0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
-                    pos += 4 + 4 * nw;
-                }
+                g_dec_elem<L0>(a, k, e, in, pos, end, d, run);
             }
             if (f.kind == XDRG_K_LIST) pos += 4;   // its FALSE
             k += 1 + f.nmem;
@@ -644,7 +838,7 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
             pos += f.xbytes;
         } else {
             const uint64_t len = g_ld(in + pos);
-            const uint64_t e0 = a.rec_base[(uint64_t)(f.slot - 1) * a.n + r];
+            const uint64_t e0 = g_rec_base(a, f.slot, r);
             const uint64_t nw = g_dyn_words(f, len);
             if (f.xsz == 1) g_dec_bytes(f.data + e0, in + pos + 4, len);
             else for (uint64_t w = 0; w < nw; ++w) g_dyn_store(f, e0, len, w, *(const uint32_t *)(in + pos + 4 + 4 * w));
@@ -654,11 +848,12 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
     }
 }
 
+template <bool NEST>
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place(const GroupArgs a) {
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
     const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
     const uint64_t r = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x;
-    if (r < bad) g_dec_record(a, r, a.xdr);
+    if (r < bad) g_dec_record<NEST>(a, r, a.xdr);
 }
 
 // Staged place (tuning key 33): the block's records go through an LDS tile in
@@ -666,6 +861,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place(const GroupArgs a
 // 16-B loads), and each lane decodes its record from the tile: the walk's
 // dependent length words and list bools become LDS reads instead of HBM
 // round trips.  A record larger than the tile decodes from HBM.
+template <bool NEST>
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
@@ -692,7 +888,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
         }
         const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
         if (k1 == 0) {   // one record larger than the tile: its lane decodes from HBM
-            if (tid == 0) g_dec_record(a, rb + js, a.xdr);
+            if (tid == 0) g_dec_record<NEST>(a, rb + js, a.xdr);
             ++js;
             continue;
         }
@@ -705,35 +901,42 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
         __syncthreads();
         // stream offset x of these records is at tile + (xb + x - a0)
         const uint8_t *in = tile + (uint32_t)(xb - a0);
-        if (js + tid < je) g_dec_record(a, rb + js + tid, in);
+        if (js + tid < je) g_dec_record<NEST>(a, rb + js + tid, in);
         __syncthreads();   // the tile's next use
         js = je;
     }
 }
 
-int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
-    hipStream_t st = (hipStream_t)stream;
+// Schemas with groups inside group elements take the NEST instantiations;
+// the others keep kernels with the inner-group code compiled out (their
+// running offsets stay in registers).
+template <bool NEST>
+static void launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) {
     const dim3 grid((uint32_t)a.nblocks), block(kRecThreads);
+    const dim3 rgrid((uint32_t)((a.n + kRecThreads - 1) / kRecThreads));
     switch (phase) {
-    case GRP_ENC_SIZES: hipLaunchKernelGGL(k_grp_enc_sizes, grid, block, 0, st, a); break;
+    case GRP_ENC_SIZES: hipLaunchKernelGGL(k_grp_enc_sizes<NEST>, grid, block, 0, st, a); break;
     case GRP_ENC_PLACE:   // G lanes per record (tuning key 32)
-        if (a.enc_lanes == 4) hipLaunchKernelGGL(k_grp_enc_place<4>, grid, block, 0, st, a);
-        else if (a.enc_lanes == 8) hipLaunchKernelGGL(k_grp_enc_place<8>, grid, block, 0, st, a);
-        else if (a.enc_lanes == 16) hipLaunchKernelGGL(k_grp_enc_place<16>, grid, block, 0, st, a);
-        else if (a.enc_lanes == 32) hipLaunchKernelGGL(k_grp_enc_place<32>, grid, block, 0, st, a);
-        else hipLaunchKernelGGL(k_grp_enc_place<64>, grid, block, 0, st, a);
+        if (a.enc_lanes == 4) hipLaunchKernelGGL((k_grp_enc_place<4, NEST>), grid, block, 0, st, a);
+        else if (a.enc_lanes == 8) hipLaunchKernelGGL((k_grp_enc_place<8, NEST>), grid, block, 0, st, a);
+        else if (a.enc_lanes == 16) hipLaunchKernelGGL((k_grp_enc_place<16, NEST>), grid, block, 0, st, a);
+        else if (a.enc_lanes == 32) hipLaunchKernelGGL((k_grp_enc_place<32, NEST>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((k_grp_enc_place<64, NEST>), grid, block, 0, st, a);
         break;
-    case GRP_DEC_WALK: hipLaunchKernelGGL(k_grp_dec_walk, grid, block, 0, st, a); break;
+    case GRP_DEC_WALK: hipLaunchKernelGGL(k_grp_dec_walk<NEST>, grid, block, 0, st, a); break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
     case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
-        if (a.dec_tile)
-            hipLaunchKernelGGL(k_grp_dec_place_lds, dim3((uint32_t)((a.n + kRecThreads - 1) / kRecThreads)), block,
-                               a.dec_tile, st, a);
-        else
-            hipLaunchKernelGGL(k_grp_dec_place, dim3((uint32_t)((a.n + kRecThreads - 1) / kRecThreads)), block, 0, st, a);
+        if (a.dec_tile) hipLaunchKernelGGL(k_grp_dec_place_lds<NEST>, rgrid, block, a.dec_tile, st, a);
+        else hipLaunchKernelGGL(k_grp_dec_place<NEST>, rgrid, block, 0, st, a);
         break;
-    default: return (int)hipErrorInvalidValue;
+    default: break;
     }
+}
+
+int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
+    if (phase < GRP_ENC_SIZES || phase > GRP_DEC_PLACE) return (int)hipErrorInvalidValue;
+    if (a.nest) launch_group_phase_t<true>(a, phase, (hipStream_t)stream);
+    else launch_group_phase_t<false>(a, phase, (hipStream_t)stream);
     return (int)hipGetLastError();
 }
 

@@ -41,10 +41,12 @@ struct xdrg_schema {
     uint32_t ncond = 0;
     bool stream_types = true;       // every field is word-for-word (int/float/hyper/double/opaque%4)
     uint32_t nwords = 0;
-    // repeated groups (include/xdrg.h): grp[k] = its group's index + 1 for a
-    // member, 0 otherwise; such schemas take the group kernels
+    // repeated groups (include/xdrg.h): grp[k] = its immediate group's index
+    // + 1 for a member, 0 otherwise; such schemas take the group kernels.
+    // nested: a group sits inside another group's element
     std::vector<uint32_t> grp;
     uint32_t ngroups = 0;
+    bool nested = false;
 };
 
 static uint32_t native_size(uint32_t t) {
@@ -72,6 +74,34 @@ static bool field_valid(const xdrg_field &f) {
     if (f.kind == XDRG_K_FIXED && f.count > 0x7fffffffu) return false;
     return true;
 }
+// The group at fs[k] spanning at most `lim` fields (depth 0 = top level):
+// grp[] of its members (its immediate members get k + 1, an inner group's
+// members that group), *sized = an element encodes to >= 1 XDR word.
+static bool group_valid(const xdrg_field *fs, size_t k, size_t lim, int depth, std::vector<uint32_t> &grp,
+                        bool *sized) {
+    const xdrg_field &g = fs[k];
+    const uint32_t m = g.reserved;
+    if (!(g.kind >= XDRG_K_FIXED && g.kind <= XDRG_K_LIST && m >= 1 && (size_t)m < lim) ||
+        (g.kind == XDRG_K_FIXED && g.count > 0x7fffffffu) || (g.kind == XDRG_K_LIST && g.count))
+        return false;
+    bool sz = g.kind == XDRG_K_LIST;
+    for (uint32_t j = 1; j <= m; ++j) {
+        const xdrg_field &f = fs[k + j];
+        grp[k + j] = (uint32_t)k + 1;
+        if (f.type == XDRG_T_GROUP) {   // an array of structs / list inside the element
+            bool s2 = false;
+            if (depth > 0 || !group_valid(fs, k + j, (size_t)m + 1 - j, depth + 1, grp, &s2) || !s2) return false;
+            sz |= f.kind != XDRG_K_FIXED || f.count > 0;
+            j += f.reserved;
+            continue;
+        }
+        if (!field_valid(f)) return false;
+        sz |= f.kind != XDRG_K_FIXED || f.count > 0;
+    }
+    *sized = sz;
+    return true;
+}
+
 static uint8_t scalar_op(uint32_t t, bool second_half) {
     switch (t) {
     case XDRG_T_FLOAT: return OP_FLOAT;
@@ -94,24 +124,17 @@ extern "C" int xdrg_schema_create_cond(const xdrg_field *fields, size_t nfields,
     if (!s) return XDRG_E_NOMEM;
     uint64_t words = 0;
     // repeated groups: {XDRG_T_GROUP, FIXED / DYNAMIC / LIST, count, m} and m
-    // member fields of the base types, an element of at least one XDR word
+    // member fields of the base types or (one level down) a group of them,
+    // an element of at least one XDR word
     s->grp.assign(nfields, 0);
     for (size_t k = 0; k < nfields; ++k) {
-        const xdrg_field &g = fields[k];
-        if (g.type != XDRG_T_GROUP) continue;
-        const uint32_t m = g.reserved;
-        bool ok = g.kind >= XDRG_K_FIXED && g.kind <= XDRG_K_LIST && m >= 1 && (size_t)m < nfields - k &&
-                  !(g.kind == XDRG_K_FIXED && g.count > 0x7fffffffu) && !(g.kind == XDRG_K_LIST && g.count);
-        bool sized = g.kind == XDRG_K_LIST;
-        for (uint32_t j = 1; ok && j <= m; ++j) {
-            const xdrg_field &f = fields[k + j];
-            ok = field_valid(f);
-            sized |= f.kind != XDRG_K_FIXED || f.count > 0;
-            s->grp[k + j] = (uint32_t)k + 1;
-        }
-        if (!ok || !sized) { delete s; return XDRG_E_INVAL; }
+        if (fields[k].type != XDRG_T_GROUP) continue;
+        bool sized = false;
+        if (!group_valid(fields, k, nfields - k, 0, s->grp, &sized) || !sized) { delete s; return XDRG_E_INVAL; }
+        for (size_t j = k + 1; j <= k + fields[k].reserved; ++j)
+            if (fields[j].type == XDRG_T_GROUP) s->nested = true;
         ++s->ngroups;
-        k += m;
+        k += fields[k].reserved;
     }
     for (size_t k = 0; k < nfields; ++k) {
         const xdrg_field &f = fields[k];
@@ -670,7 +693,8 @@ static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols
         v.count = f.count;
         v.xbytes = s->xbytes[k];
         v.grp = s->grp[k];
-        v.top = v.grp ? v.grp - 1 : (uint32_t)k;
+        v.top = (uint32_t)k;   // the top-level field that owns it (an inner group's member: two levels up)
+        while (s->grp[v.top]) v.top = s->grp[v.top] - 1;
         v.data = (uint8_t *)cols[k].data;
         v.stride = (f.kind == XDRG_K_DYNAMIC || f.type == XDRG_T_GROUP) ? 0 : eff_stride(s, k, cols[k]);
         v.offsets = cols[k].offsets;
@@ -685,8 +709,16 @@ static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols
         if (f.type == XDRG_T_GROUP) {
             v.nmem = f.reserved;
             v.efix = f.kind == XDRG_K_LIST ? 4 : 0;
-            for (uint32_t j = 1; j <= f.reserved; ++j) {
-                if (s->f[k + j].kind == XDRG_K_DYNAMIC) ++v.ndm;
+            for (uint32_t j = 1; j <= f.reserved; ++j) {   // its immediate members
+                const xdrg_field &m = s->f[k + j];
+                if (m.type == XDRG_T_GROUP) {   // an inner array / list: elements of varying size
+                    ++v.ndm;
+                    ++v.ngm;
+                    if (s->cond[k + j]) ++v.ncm;
+                    j += m.reserved;
+                    continue;
+                }
+                if (m.kind == XDRG_K_DYNAMIC) ++v.ndm;
                 else v.efix += s->xbytes[k + j];
                 if (s->cond[k + j]) ++v.ncm;
             }
@@ -698,6 +730,7 @@ static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols
         v.dslot = s->slot[k];
     }
     a.ncond = s->ncond;
+    a.nest = s->nested ? 1u : 0u;
     for (size_t i = 0; i < s->cvals.size(); ++i) a.cvals[i] = s->cvals[i];
     a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;
     if (!a.nblocks) a.nblocks = 1;
@@ -1511,22 +1544,25 @@ static void stage_schema(const xdrg_schema *s, hs::Schema &v) {
 static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool decode,
                        std::vector<xdrg_column> &out) {
     out.assign(cols, cols + s->f.size());
-    auto rows_of = [&](size_t k) -> uint64_t {   // native rows of field k's column
-        if (!s->grp[k]) return n;
+    // native rows of every field's column (a group precedes its members):
+    // records, a FIXED group's rows x count, else the group's elements
+    std::vector<uint64_t> rows_of(s->f.size(), n);
+    for (size_t k = 0; k < s->f.size(); ++k) {
+        if (!s->grp[k]) continue;
         const size_t g = s->grp[k] - 1;
         const xdrg_field &gf = s->f[g];
-        if (gf.kind == XDRG_K_FIXED) return n * gf.count;
-        if (decode) return cols[g].cap;
-        return n ? cols[g].offsets[n] : 0;   // host memory: the caller's group offsets
-    };
+        if (gf.kind == XDRG_K_FIXED) rows_of[k] = rows_of[g] * gf.count;
+        else if (decode) rows_of[k] = cols[g].cap;
+        else rows_of[k] = rows_of[g] ? cols[g].offsets[rows_of[g]] : 0;   // host memory: the caller's offsets
+    }
     for (size_t k = 0; k < s->f.size(); ++k) {
         xdrg_column &d = out[k];
         const xdrg_field &f = s->f[k];
-        const uint64_t rows = rows_of(k);
+        const uint64_t rows = rows_of[k];
         if (f.type == XDRG_T_GROUP) {
             if (d.offsets && f.kind != XDRG_K_FIXED) {
-                d.offsets = (uint64_t *)span_device(cols[k].offsets, (n + 1) * 8);
-                if (!d.offsets) return inval(c, "XDRG_HOST_MAPPED: group offsets not registered for n + 1 entries");
+                d.offsets = (uint64_t *)span_device(cols[k].offsets, (rows + 1) * 8);
+                if (!d.offsets) return inval(c, "XDRG_HOST_MAPPED: group offsets not registered for every row + 1");
             }
             continue;
         }
@@ -1576,6 +1612,7 @@ static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
         if ((n && !dout) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
         return encode_impl(c, s, dc.data(), n, dout, out_cap, drec, dflags, out_len, 0, nullptr);
     }
+    if (s->nested) return inval(c, "XDRG_HOST_PTRS: groups inside group elements take XDRG_HOST_MAPPED or device memory (the staging ring moves one level of element rows)");
     hs::Schema v;
     stage_schema(s, v);
     rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);
@@ -1611,6 +1648,7 @@ static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         if ((in_len && !din) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
         return decode_impl(c, s, din, in_len, drec, n, dc.data(), dflags, first_bad, err, 0, nullptr);
     }
+    if (s->nested) return inval(c, "XDRG_HOST_PTRS: groups inside group elements take XDRG_HOST_MAPPED or device memory (the staging ring moves one level of element rows)");
     hs::Schema v;
     stage_schema(s, v);
     rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);

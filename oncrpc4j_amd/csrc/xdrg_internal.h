@@ -326,13 +326,14 @@ struct GField {
     uint32_t type, kind, nsz, xsz;
     uint32_t count;   // FIXED count (of a field's elements or a group's)
     uint32_t xbytes;  // fixed field: XDR bytes (incl. pad)
-    uint32_t grp;     // member: its group's field index + 1; top level: 0
+    uint32_t grp;     // member: its immediate group's field index + 1; top level: 0
     uint32_t nmem;    // group: member fields that follow it
     uint32_t efix;    // group: XDR bytes of an element's fixed members (+ 4: a list's bool)
     uint32_t ndm;     // group: dynamic members
     uint32_t slot;    // counted column: slot + 1, else 0
     uint32_t top;     // top-level field index that owns it (the group for a member)
     uint32_t ncm;     // group: conditional members (elements then differ in size)
+    uint32_t ngm;     // group: inner groups among its immediate members (one level down)
     // conditional fields (xdrg_cond) on their own level: a top-level field on
     // an earlier top-level discriminant, a member on an earlier member of its
     // group (per element): present iff field cond-1 is present and its value
@@ -364,6 +365,7 @@ struct GroupArgs {
     uint32_t slot_field[kMaxSlots];
     uint32_t ncond;              // conditional fields (0: every record / element has all of them)
     uint32_t dec_tile;           // decode place: LDS tile bytes (0: records read from HBM; key 33)
+    uint32_t nest;               // some group holds an inner group (the NEST kernels)
     int32_t cvals[XDRG_MAX_CASES];
     GField f[kMaxFields];
 };

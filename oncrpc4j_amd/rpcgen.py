@@ -36,9 +36,12 @@ flattened fields as members).  Unions and optional data inside an element
 become conditions between members of the same group (evaluated per
 element), and a group may itself sit in a union arm or behind optional data
 (a condition on the group field).  A fixed-size array of structs inside an
-element (`T x[N]`, no count word) unrolls into N copies of T's members.
-Still not one tape: variable-length arrays of structs and lists inside
-elements, and recursion anywhere but a struct's last declaration.
+element (`T x[N]`, no count word) unrolls into N copies of T's members; a
+variable-length array of structs or a list inside an element becomes an
+inner group (one level down: its members are the inner element's flattened
+fields, its rows the outer elements).  Still not one tape: arrays of structs
+or lists two levels down, and recursion anywhere but a struct's last
+declaration.
 """
 import re
 
@@ -244,9 +247,10 @@ class _Tape:
     # the tape anyway)
     MAX_UNROLL = 16
 
-    def __init__(self, spec, in_element=False):
+    def __init__(self, spec, in_element=False, depth=0):
         self.s = spec
         self.in_element = in_element
+        self.depth = depth   # group levels above this tape (0: a record's tape)
         self.fields = _TapeFields()
         self.fields.reasons = []
         self.conds = []
@@ -335,15 +339,15 @@ class _Tape:
         members of the same element (unions and optional data inside an
         element, e.g. READDIRPLUS's post_op_attr).  A fixed array of structs
         inside an element unrolls into its elements' members (decl()); a
-        variable-length one or a list inside an element is not one level of
-        groups."""
-        sub = _Tape(self.s, in_element=True)
+        variable-length one or a list inside an element is an inner group
+        (its span counted in this group's members), one level down only."""
+        sub = _Tape(self.s, in_element=True, depth=self.depth + 1)
         for d in decls:
             sub.decl(d, f"{where}.{d.name}", None, stack + (st.name,))
         fields, conds = sub.result()
-        if any(f[0] == abi.T_GROUP for f in fields):
+        if self.depth >= 1 and any(f[0] == abi.T_GROUP for f in fields):
             raise NotBatchable(f"{where}: elements of {st.name} hold arrays of structs or lists "
-                               f"(no one-level group)")
+                               f"two group levels down (one inner level is batched)")
         if not fields:
             raise NotBatchable(f"{where}: elements of {st.name} have no fields")
         g = self.add((abi.T_GROUP, kind, count, len(fields)), guard)

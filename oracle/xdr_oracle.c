@@ -461,14 +461,14 @@ static inline const uint8_t *fixed_ptr(const xdrg_field *f, const xdrg_column *c
 typedef struct { const xdrg_cond *cond_of[64]; } xo_conds;
 
 static int has_group(const xdrg_field *fs, size_t nf);
-/* grp_of[k] = index + 1 of the group field k is a member of, 0 at top level */
+/* grp_of[k] = index + 1 of the group field k is an immediate member of, 0
+ * at top level (a group inside an element claims its own members after its
+ * parent has claimed the whole span) */
 static void group_of(const xdrg_field *fs, size_t nf, uint32_t *grp_of) {
     for (size_t k = 0; k < nf; k++) grp_of[k] = 0;
     for (size_t k = 0; k < nf; k++)
-        if (fs[k].type == XDRG_T_GROUP) {
+        if (fs[k].type == XDRG_T_GROUP)
             for (uint32_t j = 1; j <= fs[k].reserved && k + j < nf; j++) grp_of[k + j] = (uint32_t)k + 1;
-            k += fs[k].reserved;
-        }
 }
 /* With repeated groups a condition stays on its level: a top-level field
  * (a group included: the whole array / list present or not) on an earlier
@@ -588,8 +588,16 @@ static int encode_group(xo_stream *s, const xdrg_field *g, const xdrg_column *gc
         for (uint32_t j = 1; !rc && j <= m; j++) {
             /* an element's union arms / optional data (jrpcgen.java:1240-1340) */
             enc_presence(cc, gk + j, &g[j], &gc[j], e, pres, val);
-            if (!pres[gk + j]) continue;
-            rc = encode_field(s, &g[j], &gc[j], e);
+            const uint32_t span = g[j].type == XDRG_T_GROUP ? g[j].reserved : 0;
+            if (pres[gk + j]) {
+                /* an array of structs / list inside the element: its own count
+                 * and elements, as the element's generated xdrEncode calls the
+                 * inner elements' (jrpcgen.java:856-906, 835-851); its column
+                 * is indexed by this group's element e */
+                rc = span ? encode_group(s, &g[j], &gc[j], e, cc, gk + j, pres, val)
+                          : encode_field(s, &g[j], &gc[j], e);
+            }
+            j += span;
         }
     }
     if (!rc && g->kind == XDRG_K_LIST) rc = xo_encode_boolean(s, 0);
@@ -649,11 +657,36 @@ static int encode_record(xo_stream *s, const xdrg_field *fs, size_t nf, const xd
 }
 
 /* Repeated groups (include/xdrg.h): the group field, then `reserved` member
- * fields of the base types; no nested groups; an element that encodes to at
- * least one byte (list elements carry their bool). */
+ * fields of the base types or — one level down — a group whose members are
+ * base types (its own span counted in the outer `reserved`); an element that
+ * encodes to at least one byte (list elements carry their bool, a counted
+ * inner array its count). */
 static int has_group(const xdrg_field *fs, size_t nf) {
     for (size_t k = 0; k < nf; k++) if (fs[k].type == XDRG_T_GROUP) return 1;
     return 0;
+}
+/* The group at g (a span of `lim` fields from g on, depth 0 = top level):
+ * XDRG_OK and *sized = whether an element encodes to >= 1 byte. */
+static int check_group(const xdrg_field *g, size_t lim, int depth, int *sized_out) {
+    const uint32_t m = g->reserved;
+    if (g->kind < XDRG_K_FIXED || g->kind > XDRG_K_LIST || m == 0 || m > lim - 1) return XDRG_E_INVAL;
+    if ((g->kind == XDRG_K_FIXED && g->count > 0x7fffffffu) || (g->kind == XDRG_K_LIST && g->count))
+        return XDRG_E_INVAL;
+    int sized = g->kind == XDRG_K_LIST;
+    for (uint32_t j = 1; j <= m; j++) {
+        const xdrg_field *f = &g[j];
+        if (f->type == XDRG_T_GROUP) {
+            int s2 = 0;
+            if (depth > 0 || check_group(f, (size_t)m + 1 - j, depth + 1, &s2) || !s2) return XDRG_E_INVAL;
+            sized |= f->kind != XDRG_K_FIXED || f->count > 0;
+            j += f->reserved;
+            continue;
+        }
+        if (!field_valid(f)) return XDRG_E_INVAL;
+        sized |= f->kind == XDRG_K_DYNAMIC || f->kind == XDRG_K_SCALAR || f->count > 0;
+    }
+    *sized_out = sized;
+    return XDRG_OK;
 }
 static int check_schema(const xdrg_field *fs, size_t nf) {
     if (!fs || !nf || nf > 64) return XDRG_E_INVAL;
@@ -663,18 +696,9 @@ static int check_schema(const xdrg_field *fs, size_t nf) {
             if (!field_valid(g)) return XDRG_E_INVAL;
             continue;
         }
-        const uint32_t m = g->reserved;
-        if (g->kind < XDRG_K_FIXED || g->kind > XDRG_K_LIST || m == 0 || m > nf - 1 - k) return XDRG_E_INVAL;
-        if ((g->kind == XDRG_K_FIXED && g->count > 0x7fffffffu) || (g->kind == XDRG_K_LIST && g->count))
-            return XDRG_E_INVAL;
-        int sized = g->kind == XDRG_K_LIST;
-        for (uint32_t j = 1; j <= m; j++) {
-            const xdrg_field *f = &g[j];
-            if (!field_valid(f)) return XDRG_E_INVAL;
-            sized |= f->kind == XDRG_K_DYNAMIC || f->kind == XDRG_K_SCALAR || f->count > 0;
-        }
-        if (!sized) return XDRG_E_INVAL;
-        k += m;
+        int sized = 0;
+        if (check_group(g, nf - k, 0, &sized) || !sized) return XDRG_E_INVAL;
+        k += g->reserved;
     }
     return XDRG_OK;
 }
@@ -853,6 +877,17 @@ static int walk_group(xo_stream *s, const xdrg_field *g, uint64_t *cnt_out, uint
         for (uint32_t j = 1; j <= m; j++) {
             const xdrg_field *f = &g[j];
             dec_presence(cc, gk + j, f, s, pres, val);
+            if (f->type == XDRG_T_GROUP) {   /* an inner array / list: its elements and members */
+                if (pres[gk + j]) {
+                    uint64_t icnt = 0, imcnt[64];
+                    rc = walk_group(s, f, &icnt, imcnt, cc, gk + j, pres, val);
+                    if (rc) return rc;
+                    mcnt[j] += icnt;
+                    for (uint32_t jj = 1; jj <= f->reserved; jj++) mcnt[j + jj] += imcnt[jj];
+                }
+                j += f->reserved;
+                continue;
+            }
             if (!pres[gk + j]) continue;
             if (f->kind == XDRG_K_DYNAMIC) {
                 int32_t len;
@@ -895,6 +930,20 @@ static void absent_field(const xdrg_field *f, xdrg_column *c, uint64_t e) {
         memset((uint8_t *)fixed_ptr(f, c, e), 0, cnt * native_size(f->type));
     }
 }
+/* An absent array / list at row i of its column: no elements, or a T x[N]'s
+ * N zero / empty elements (inner arrays in them empty too). */
+static void absent_group(const xdrg_field *g, xdrg_column *gc, uint64_t i) {
+    if (g->kind != XDRG_K_FIXED) { gc->offsets[i + 1] = gc->offsets[i]; return; }
+    for (uint64_t e = i * g->count; e < (i + 1) * g->count; e++)
+        for (uint32_t j = 1; j <= g->reserved; j++) {
+            if (g[j].type == XDRG_T_GROUP) {
+                absent_group(&g[j], &gc[j], e);
+                j += g[j].reserved;
+            } else {
+                absent_field(&g[j], &gc[j], e);
+            }
+        }
+}
 
 static int decode_group(xo_stream *s, const xdrg_field *g, xdrg_column *gc, uint64_t i,
                         const xo_conds *cc, size_t gk, int *pres, int32_t *val) {
@@ -905,19 +954,36 @@ static int decode_group(xo_stream *s, const xdrg_field *g, xdrg_column *gc, uint
     if (rc) return rc;
     const uint64_t e0 = g->kind == XDRG_K_FIXED ? i * g->count : gc->offsets[i];
     if (g->kind != XDRG_K_FIXED && e0 + cnt > gc->cap) return XDRG_E_CAPACITY;
-    for (uint32_t j = 1; j <= m; j++)
+    for (uint32_t j = 1; j <= m; j++) {
+        if (g[j].type == XDRG_T_GROUP) {   /* an inner array: its elements start at row i0 */
+            const xdrg_field *ig = &g[j];
+            const xdrg_column *ic = &gc[j];
+            const uint64_t i0 = ig->kind == XDRG_K_FIXED ? e0 * ig->count : ic->offsets[e0];
+            if (ig->kind != XDRG_K_FIXED && i0 + mcnt[j] > ic->cap) return XDRG_E_CAPACITY;
+            for (uint32_t jj = 1; jj <= ig->reserved; jj++)
+                if (ig[jj].kind == XDRG_K_DYNAMIC && ic[jj].offsets[i0] + mcnt[j + jj] > ic[jj].cap)
+                    return XDRG_E_CAPACITY;
+            j += ig->reserved;
+            continue;
+        }
         if (g[j].kind == XDRG_K_DYNAMIC && gc[j].offsets[e0] + mcnt[j] > gc[j].cap) return XDRG_E_CAPACITY;
+    }
     if (g->kind == XDRG_K_DYNAMIC) s->pos += 4;
     for (uint64_t e = e0; e < e0 + cnt; e++) {
         if (g->kind == XDRG_K_LIST) s->pos += 4;
         for (uint32_t j = 1; j <= m; j++) {
             dec_presence(cc, gk + j, &g[j], s, pres, val);
+            const uint32_t span = g[j].type == XDRG_T_GROUP ? g[j].reserved : 0;
             if (!pres[gk + j]) {
-                absent_field(&g[j], &gc[j], e);
+                if (span) absent_group(&g[j], &gc[j], e);
+                else absent_field(&g[j], &gc[j], e);
+                j += span;
                 continue;
             }
-            rc = decode_field(s, &g[j], &gc[j], e);
+            rc = span ? decode_group(s, &g[j], &gc[j], e, cc, gk + j, pres, val)
+                      : decode_field(s, &g[j], &gc[j], e);
             if (rc) return rc;
+            j += span;
         }
     }
     if (g->kind == XDRG_K_LIST) s->pos += 4;
@@ -944,12 +1010,7 @@ static int decode_record(xo_stream *s, const xdrg_field *fs, size_t nf, xdrg_col
             if (!pres[k]) {   /* absent: the defaults of a new rpcgen object */
                 if ((int)k == view) view_pos[i] = UINT64_MAX;
                 if (f->type == XDRG_T_GROUP) {   /* no elements (a FIXED group's are zero / empty) */
-                    if (f->kind != XDRG_K_FIXED) {
-                        c->offsets[i + 1] = c->offsets[i];
-                    } else {
-                        for (uint64_t e = i * f->count; e < (i + 1) * f->count; e++)
-                            for (uint32_t j = 1; j <= f->reserved; j++) absent_field(&f[j], &c[j], e);
-                    }
+                    absent_group(f, c, i);
                     k += f->reserved;
                     continue;
                 }

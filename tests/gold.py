@@ -30,25 +30,30 @@ def batch_from_records(fields, records):
     fields = [tuple(f) for f in fields]
     n = len(records)
     par = parents(fields)
+    rowvals = {}   # field k -> its value at every row of its array
+
+    def rows_of(k):
+        if k not in rowvals:
+            g = par[k]
+            if g < 0:
+                rowvals[k] = [r[k] for r in records]
+            else:   # member of group g (an inner group's slot holds its elements): a row per element
+                rowvals[k] = [e[k - g - 1] for els in rows_of(g) for e in els]
+        return rowvals[k]
+
     arrays = []
     for k, f in enumerate(fields):
         t, kind, c = f[0], f[1], f[2]
+        col = rows_of(k)
         if t == abi.T_GROUP:
-            lens = [len(r[k]) for r in records]
             if kind == abi.K_FIXED:
                 arrays.append(None)
             else:
-                offs = np.zeros(n + 1, dtype=np.uint64)
-                np.cumsum(np.array(lens, dtype=np.uint64), out=offs[1:])
+                offs = np.zeros(len(col) + 1, dtype=np.uint64)
+                np.cumsum(np.array([len(v) for v in col], dtype=np.uint64), out=offs[1:])
                 arrays.append(offs)
             continue
-        if par[k] >= 0:   # member j of group g: one row per element
-            g = par[k]
-            col = [e[k - g - 1] for r in records for e in r[g]]
-        else:
-            col = [r[k] for r in records]
-        n_rows = len(col)
-        arrays.append(_column(t, kind, c, col, n_rows))
+        arrays.append(_column(t, kind, c, col, len(col)))
     return HostBatch(fields, n, arrays)
 
 

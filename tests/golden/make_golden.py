@@ -24,6 +24,8 @@ fixtures are plain JSON data and travel, this script's inputs do not need to.
    elements (rpcgen/plus_types.x), packed by xdrlib.
    chunk_map_vectors.json — a fixed array of structs with optional data inside
    list elements (rpcgen/chunk_map.x), packed by xdrlib.
+   volume_index_vectors.json — a list and a counted array of structs inside
+   list elements (rpcgen/volume_index.x), packed by xdrlib.
 """
 import json
 import os
@@ -537,6 +539,87 @@ def chunk_map_vectors(seed=0xC4A7):
     return out
 
 
+# ---- groups inside group elements ---------------------------------------------
+# tests/golden/rpcgen/volume_index.x `volume_index`: every `volume *next` list
+# element holds an `extent *next` list (each extent with an optional crc) and,
+# behind a bool union, `ace entries<8>` (each entry with a string) — packed by
+# xdrlib from the declarations; records in tape layout (an inner group's slot
+# holds its elements, its members' slots None, an absent crc as 0).
+def volume_index_vectors(seed=0x7015):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oncrpc4j_amd import rpcgen
+    spec = rpcgen.parse_file(os.path.join(HERE, "rpcgen", "volume_index.x"))
+    fields, conds = spec.tape("volume_index")
+    rng = random.Random(seed)
+    out = {"source": "CPython 3.10 stdlib xdrlib (RFC 1014) packing volume_index.x `volume_index` from its "
+                     "declarations (a list and a counted array of structs inside `volume *next` list "
+                     "elements, jrpcgen.java:835-906)",
+           "seed": seed, "fields": [list(f) for f in fields], "conds": [list(c) for c in conds],
+           "batches": []}
+    name = lambda k: bytes(rng.choice(b"abcdefghijklmnop/._") for _ in range(rng.randrange(0, k)))
+    for framed in (False, True):
+        n = 48
+        records, chunks, probes = [], [], []
+        base = 0
+        for i in range(n):
+            p = xdrlib.Packer()
+            at = lambda kind: probes.append([i, kind, base + (4 if framed else 0) + len(p.get_buffer())])
+            node = rng.getrandbits(32)
+            p.pack_uint(node)
+            vols = []
+            for _ in range(rng.choice([0, 1, 1, 2, 3, 6])):
+                vid, label = rng.getrandbits(64), name(33)
+                p.pack_bool(True)
+                p.pack_uhyper(vid)
+                p.pack_string(label)
+                exts = []
+                for _ in range(rng.choice([0, 0, 1, 2, 4, 7])):
+                    st, ln = rng.getrandbits(64), rng.getrandbits(32)
+                    has = rng.random() < 0.5
+                    crc = rng.getrandbits(32) if has else 0
+                    at("ext_bool")
+                    p.pack_bool(True)
+                    p.pack_uhyper(st); p.pack_uint(ln); p.pack_bool(has)
+                    if has:
+                        p.pack_uint(crc)
+                    exts.append([st, ln, int(has), crc])
+                p.pack_bool(False)
+                present = rng.random() < 0.7
+                p.pack_bool(present)
+                aces = []
+                if present:
+                    k = rng.choice([0, 1, 2, 3, 8])
+                    at("acl_count")
+                    p.pack_uint(k)
+                    for _ in range(k):
+                        pr, mk, who = rng.getrandbits(32) - (1 << 31), rng.getrandbits(32), name(20)
+                        p.pack_int(pr); p.pack_uint(mk)
+                        at("who_len")
+                        p.pack_string(who)
+                        aces.append([pr, mk, who.hex()])
+                online = rng.randint(0, 1)
+                p.pack_bool(online)
+                vols.append([vid, label.hex(), exts, None, None, None, None, int(present), aces,
+                             None, None, None, online])
+            p.pack_bool(False)
+            stamp = rng.getrandbits(64) - (1 << 63)
+            p.pack_hyper(stamp)
+            body = p.get_buffer()
+            if framed:
+                body = struct.pack(">I", len(body) | 0x80000000) + body
+            chunks.append(body)
+            base += len(body)
+            records.append([node, vols] + [None] * 13 + [stamp])
+        offs = [0]
+        for ch in chunks:
+            offs.append(offs[-1] + len(ch))
+        out["batches"].append({"name": "volume_index", "framed": framed, "n": n, "records": records,
+                               "xdr": b"".join(chunks).hex(), "rec_offsets": offs,
+                               "probes": probes})   # [record, what, stream offset of that word]
+    return out
+
+
 # ---- framing -----------------------------------------------------------------
 def call_message(xid, args_string):
     """RpcMessageParserTCPTest.XdrStreamBuilder.build (:127-142): CALL header,
@@ -680,7 +763,8 @@ GENERATORS = {"kat_reference.json": kat_reference, "kat_jdk_nan.json": kat_jdk_n
               "xdrlib_vectors.json": xdrlib_vectors, "framing.json": framing, "rpc_vectors.json": rpc_vectors,
               "cond_vectors.json": cond_vectors, "group_vectors.json": group_vectors,
               "group_cond_vectors.json": group_cond_vectors,
-              "chunk_map_vectors.json": chunk_map_vectors}
+              "chunk_map_vectors.json": chunk_map_vectors,
+              "volume_index_vectors.json": volume_index_vectors}
 
 
 def main(names=None):

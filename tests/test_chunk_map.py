@@ -55,8 +55,14 @@ def test_unroll_limits():
     var = """struct r { int a; };
              struct e { r xs<4>; e *next; };
              struct top { e *l; };"""
-    with pytest.raises(rpcgen.NotBatchable):
-        rpcgen.parse(var).tape("top")
+    f, c = rpcgen.parse(var).tape("top")   # an inner group: list element -> counted array
+    assert f == [(abi.T_GROUP, abi.K_LIST, 0, 2), (abi.T_GROUP, abi.K_DYNAMIC, 0, 1), (abi.T_INT, abi.K_SCALAR, 0)]
+    deep = """struct q { int a; };
+              struct r { q qs<>; };
+              struct e { r xs<4>; e *next; };
+              struct top { e *l; };"""
+    with pytest.raises(rpcgen.NotBatchable):   # two levels down
+        rpcgen.parse(deep).tape("top")
     ok = """struct r { int a; hyper b; };
             struct e { r xs[3]; };
             struct top { e l<>; };"""
