@@ -794,10 +794,46 @@ __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint6
     }
 }
 
+// Element e's members parsed without storing (the element-parallel place's
+// record walk): pos past the element, run past its dynamic members.
+__device__ __forceinline__ void g_elem_skip(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t &pos,
+                                            uint64_t end, GDisc &d, GRun &run) {
+    const GField &f = a.f[g];
+    for (uint32_t j = 1; j <= f.nmem; ++j) {
+        const GField &m = a.f[g + j];
+        if (f.ncm && !g_dec_field_present(a, g + j, in, pos, end, d)) continue;
+        if (m.kind != XDRG_K_DYNAMIC) {
+            pos += m.xbytes;
+            continue;
+        }
+        const uint64_t len = g_ld(in + pos);
+        run.set(m.slot, run.get(m.slot) + len);
+        pos += 4 + 4 * g_dyn_words(m, len);
+    }
+}
+
+// Element-parallel place (tuning key 38): the element descriptors a record
+// lane leaves for a sub-batch — element i (= e - E0) starts at tile offset
+// pos[i], and dynamic member q (of at most 2) at native offset sb[q] +
+// rel[q * cap + i].
+struct GElDesc {   // (scalar members: an indexed array here went to scratch)
+    uint32_t *pos, *rel;
+    uint32_t cap;                 // descriptors per sub-batch
+    uint64_t E0;                  // the sub-batch's first element
+    uint32_t nm;                  // dynamic members
+    uint32_t ms0, ms1;            // their slots
+    uint64_t sb0, sb1;            // their native offsets at E0
+    const uint8_t *tile;
+};
+
 // in: where stream offset x is read, in + x (the stream, or an LDS tile
 // holding this record's bytes: k_grp_dec_place_lds).
-template <bool NEST>
-__device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in) {
+// EL (element-parallel place): the record's one group leaves descriptors in
+// *el instead of decoding its elements (the block decodes them afterwards,
+// a lane per element).
+template <bool NEST, bool EL = false>
+__device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in,
+                                             const GElDesc &el = GElDesc{}) {
     constexpr int L0 = NEST ? 0 : 1;   // depth the record's groups start at (1: inner groups compiled out)
     const GExtent ex = g_extent(a, r);   // the extent the walk checked (clamped to in_len)
     const uint64_t end = ex.b;
@@ -827,7 +863,15 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
             g_run_init(a, k, r, e0, run);
             for (uint64_t e = e0; e < e0 + cnt; ++e) {
                 if (f.kind == XDRG_K_LIST) pos += 4;   // its TRUE
-                g_dec_elem<L0>(a, k, e, in, pos, end, d, run);
+                if constexpr (EL) {
+                    const uint32_t i = (uint32_t)(e - el.E0);
+                    el.pos[i] = (uint32_t)(in + pos - el.tile);
+                    if (el.nm > 0) el.rel[i] = (uint32_t)(run.get(el.ms0) - el.sb0);
+                    if (el.nm > 1) el.rel[el.cap + i] = (uint32_t)(run.get(el.ms1) - el.sb1);
+                    g_elem_skip(a, k, in, pos, end, d, run);
+                } else {
+                    g_dec_elem<L0>(a, k, e, in, pos, end, d, run);
+                }
             }
             if (f.kind == XDRG_K_LIST) pos += 4;   // its FALSE
             k += 1 + f.nmem;
@@ -854,6 +898,22 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place(const GroupArgs a
     const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
     const uint64_t r = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x;
     if (r < bad) g_dec_record<NEST>(a, r, a.xdr);
+}
+
+// nch 16-byte chunks from the 16-aligned global address a0 into the tile by
+// LDS-DMA (global_load_lds_dwordx4: every load of the block in flight at once,
+// no registers; a copy loop through registers waited one memory round trip
+// per 4 KiB of tile).  A wave's 64 chunks land contiguously (the LDS address
+// is wave-uniform base + 16 * lane).  Each wave waits for its own DMA before
+// the caller's barrier: LDS-DMA retires on vmcnt, not lgkmcnt.
+__device__ __forceinline__ void g_stage_tile(uint8_t *tile, uintptr_t a0, uint32_t nch) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i0 = (threadIdx.x >> 6) * 64; i0 < nch; i0 += kRecThreads) {
+        if (i0 + lane < nch)
+            __builtin_amdgcn_global_load_lds((const void *)(a0 + 16 * (uintptr_t)(i0 + lane)),
+                                             (__attribute__((address_space(3))) void *)(tile + 16 * (size_t)i0), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Staged place (tuning key 33): the block's records go through an LDS tile in
@@ -896,13 +956,99 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
         const uintptr_t a0 = (xb + ext(rb + js)) & ~(uintptr_t)15;
         const uintptr_t a1 = (xb + ext(rb + je) + 15) & ~(uintptr_t)15;
         const uint32_t nch = a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u;
-        for (uint32_t i = tid; i < nch; i += kRecThreads)
-            *(u32x4g *)(tile + 16 * (size_t)i) = __builtin_nontemporal_load((const u32x4g *)(a0 + 16 * (uintptr_t)i));
+        g_stage_tile(tile, a0, nch);
         __syncthreads();
         // stream offset x of these records is at tile + (xb + x - a0)
         const uint8_t *in = tile + (uint32_t)(xb - a0);
         if (js + tid < je) g_dec_record<NEST>(a, rb + js + tid, in);
         __syncthreads();   // the tile's next use
+        js = je;
+    }
+}
+
+// Element-parallel place (tuning key 38 > 0: at most that many elements per
+// sub-batch; schemas with one top-level group, no inner groups, at most two
+// dynamic members).  The lane-per-record place wrote each element's members
+// at the lane's own record: the 64 stores of one instruction hit 64 rows
+// far apart.  Here a sub-batch of records is staged in the LDS tile as in
+// k_grp_dec_place_lds, each record lane walks its record once (top-level
+// fields decoded, the group's elements parsed for their tile offsets and
+// member native offsets: descriptors in LDS), and then every lane of the
+// block decodes an element: consecutive lanes, consecutive elements, so the
+// member stores of an instruction fall on consecutive rows.
+__global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_el(const GroupArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *tile = smem;
+    uint32_t *dpos = (uint32_t *)(smem + a.dec_tile);
+    uint32_t *drel = dpos + a.dec_el;
+    const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
+    const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecThreads;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t lim = bad < a.n ? bad : a.n;
+    const uint32_t nlive = lim > rb ? (uint32_t)(lim - rb < (uint64_t)kRecThreads ? lim - rb : (uint64_t)kRecThreads) : 0u;
+    const uintptr_t xb = (uintptr_t)a.xdr;
+    const uint32_t g = a.el_g;
+    const GField &G = a.f[g];
+    auto ext = [&](uint64_t r) -> uint64_t { const uint64_t x = a.rec_in[r]; return x < a.xdr_cap ? x : a.xdr_cap; };
+    // first element of record r (r <= n)
+    auto E = [&](uint64_t r) -> uint64_t {
+        if (G.kind == XDRG_K_FIXED) return r * G.count;
+        return r < a.n ? g_rec_base(a, G.slot, r) : a.totals[G.slot - 1];
+    };
+    GElDesc el;
+    el.pos = dpos;
+    el.rel = drel;
+    el.cap = a.dec_el;
+    el.tile = tile;
+    el.nm = 0;
+    el.ms0 = el.ms1 = 0;
+    el.sb0 = el.sb1 = 0;
+    for (uint32_t j = 1; j <= G.nmem; ++j) {
+        if (a.f[g + j].kind != XDRG_K_DYNAMIC) continue;
+        if (el.nm == 0) el.ms0 = a.f[g + j].slot;
+        else el.ms1 = a.f[g + j].slot;
+        ++el.nm;
+    }
+    uint32_t js = 0;
+    while (js < nlive) {
+        const uint32_t je1 = js + 1 + tid;
+        bool fits = false;
+        if (je1 <= nlive) {
+            const uintptr_t lo = (xb + ext(rb + js)) & ~(uintptr_t)15;
+            const uintptr_t hi = (xb + ext(rb + je1) + 15) & ~(uintptr_t)15;
+            fits = hi >= lo && hi - lo <= a.dec_tile && E(rb + je1) - E(rb + js) <= a.dec_el;
+        }
+        const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
+        if (k1 == 0) {   // one record larger than the tile or the descriptors: its lane decodes from HBM
+            if (tid == 0) g_dec_record<false>(a, rb + js, a.xdr);
+            ++js;
+            continue;
+        }
+        const uint32_t je = js + k1;
+        const uintptr_t a0 = (xb + ext(rb + js)) & ~(uintptr_t)15;
+        const uintptr_t a1 = (xb + ext(rb + je) + 15) & ~(uintptr_t)15;
+        const uint32_t nch = a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u;
+        g_stage_tile(tile, a0, nch);
+        el.E0 = E(rb + js);
+        if (el.nm > 0) el.sb0 = g_rec_base(a, el.ms0, rb + js);
+        if (el.nm > 1) el.sb1 = g_rec_base(a, el.ms1, rb + js);
+        __syncthreads();
+        const uint8_t *in = tile + (uint32_t)(xb - a0);   // stream offset x at in + x
+        if (js + tid < je) g_dec_record<false, true>(a, rb + js + tid, in, el);
+        __syncthreads();   // descriptors
+        const uint64_t nel = E(rb + je) - el.E0;
+        for (uint32_t i = tid; i < nel; i += kRecThreads) {
+            GRun run;
+#pragma unroll
+            for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;
+            if (el.nm > 0) run.set(el.ms0, el.sb0 + drel[i]);
+            if (el.nm > 1) run.set(el.ms1, el.sb1 + drel[el.cap + i]);
+            GDisc d{};
+            uint64_t pos = dpos[i];
+            g_dec_elem<1>(a, g, el.E0 + i, tile, pos, ~0ull, d, run);
+        }
+        __syncthreads();   // the tile's and the descriptors' next use
         js = je;
     }
 }
@@ -926,7 +1072,9 @@ static void launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) 
     case GRP_DEC_WALK: hipLaunchKernelGGL(k_grp_dec_walk<NEST>, grid, block, 0, st, a); break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
     case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
-        if (a.dec_tile) hipLaunchKernelGGL(k_grp_dec_place_lds<NEST>, rgrid, block, a.dec_tile, st, a);
+        if (!NEST && a.dec_el && a.dec_tile)
+            hipLaunchKernelGGL(k_grp_dec_place_el, rgrid, block, a.dec_tile + 12 * (size_t)a.dec_el, st, a);
+        else if (a.dec_tile) hipLaunchKernelGGL(k_grp_dec_place_lds<NEST>, rgrid, block, a.dec_tile, st, a);
         else hipLaunchKernelGGL(k_grp_dec_place<NEST>, rgrid, block, 0, st, a);
         break;
     default: break;

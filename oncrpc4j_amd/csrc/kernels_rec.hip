@@ -1356,7 +1356,7 @@ __device__ __forceinline__ void dec_place_g_block(const RecArgs &a, uint64_t bid
     if (nrec > kRecPerBlock) nrec = kRecPerBlock;
     const uint8_t *in = a.xdr;
     const uint32_t tid = threadIdx.x;
-    if (a.payk) {   // k_dec_payload decodes these records whole: head words, payload, tail words
+    if (a.payk && a.pay_heads) {   // k_dec_payload decodes these records whole: head words, payload, tail words
         const uint32_t kp = a.dyn_idx[a.payk - 1];   // the one dynamic field
         const uint64_t hb = a.pay_fb - (a.framed ? 4 : 0);   // its offset after the mark
         for (uint32_t j = tid; j < nrec; j += kRecThreads) {
@@ -1406,6 +1406,15 @@ __device__ __forceinline__ void dec_place_g_block(const RecArgs &a, uint64_t bid
         }
         const uint32_t *cn = scnt + (size_t)d * kRecPerBlock;
         const uint64_t *no = snoff + (size_t)d * kRecPerBlock;
+        if (a.payk == d + 1) {   // k_dec_payload moves this field (records the walk passed only)
+            for (uint32_t j = tid; j < nrec; j += kRecThreads)
+                a.pay_pos[rb + j] = k < supto[j] ? sstart[j] + fixed_delta : ~0ull;
+            __syncthreads();
+            for (uint32_t j = tid; j < nrec; j += kRecThreads) sstart[j] += dyn_xdr_bytes(f, cn[j]);
+            __syncthreads();
+            ++d;
+            continue;
+        }
         uint64_t ps = 0;
         for (uint32_t j = tid; j < nrec; j += kRecThreads) ps += cn[j];
         const uint64_t fbytes = block_sum(ps) * (f.xsz == 1 ? 1 : f.xsz) + 4 * nrec;
@@ -1596,7 +1605,7 @@ __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
             w = w < nw ? ~0u >> 1 : w - nw;   // (stored: past every later field)
         }
     };
-    const bool hl = lane < nfw;
+    const bool hl = a.pay_heads && lane < nfw;   // (key 39 = 0: the group kernel stored them)
     const uint32_t hv = hl ? fixed_at(lane) : 0u;
     const uint64_t nch = (cnt + 15) >> 4;
     for (uint64_t c0 = lane; c0 < nch; c0 += 4 * LPR) {
@@ -1624,7 +1633,7 @@ __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
         }
     }
     if (hl) fixed_put(lane, hv);
-    for (uint32_t i = lane + LPR; i < nfw; i += LPR) fixed_put(i, fixed_at(i));   // > 64 fixed words
+    for (uint32_t i = lane + LPR; a.pay_heads && i < nfw; i += LPR) fixed_put(i, fixed_at(i));   // > 64 fixed words
 }
 __global__ __launch_bounds__(256) void k_dec_payload(const RecArgs a) {
     const uint64_t step = (uint64_t)gridDim.x * (256 / kPayLanes);
@@ -3099,6 +3108,7 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     a.tile_bytes = t.tile_bytes;
     a.big_rec = 0;
     a.xcd = (uint32_t)t.xcd_order;
+    a.pay_heads = (uint32_t)t.pay_heads;
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
     // conditional schemas (unions / optional data) and by-reference payloads take

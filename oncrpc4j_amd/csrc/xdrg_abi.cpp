@@ -385,6 +385,8 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 33: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.grp_dec_tile = (int32_t)v; return 0;
     case 36: if (!in(1, 64)) return -1; t.emit_per = (int32_t)v; return 0;
     case 37: if (!in(0, 1)) return -1; t.xcd_order = (int32_t)v; return 0;
+    case 38: if (v && !in(64, 4096)) return -1; t.grp_dec_el = (int32_t)v; return 0;
+    case 39: if (!in(0, 1)) return -1; t.pay_heads = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -1007,6 +1009,17 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         rc = fill_group(c, s, cols, n, framed, true, a);
         if (rc) return rc;
         a.dec_tile = (uint32_t)c->tune.grp_dec_tile;
+        // the element-parallel place: one top-level group without inner groups,
+        // at most two dynamic members, LDS for the tile and the descriptors
+        if (c->tune.grp_dec_el && a.dec_tile && !a.nest && s->ngroups == 1 &&
+            a.dec_tile + 12ull * (uint64_t)c->tune.grp_dec_el <= 65536) {
+            for (uint32_t k = 0; k < a.nf; ++k)
+                if (a.f[k].type == XDRG_T_GROUP && !a.f[k].grp && a.f[k].ndm <= 2 &&
+                    !(a.f[k].kind == XDRG_K_FIXED && a.f[k].cond)) {   // (an absent T x[N] has no descriptors)
+                    a.dec_el = (uint32_t)c->tune.grp_dec_el;
+                    a.el_g = k;
+                }
+        }
         if (n == 0) {
             for (uint32_t q = 0; q < a.nslot; ++q)
                 if (!a.f[a.slot_field[q]].grp) HIPCHK(c, hipMemsetAsync(cols[a.slot_field[q]].offsets, 0, 8, c->stream));
@@ -1673,7 +1686,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     const uint64_t F = Q + 2;
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_ex = take(2 * Q), o_al = take(4 * (size_t)kFChunk * nsub), o_ac = take(4 * nsub), o_se = take(4 * nsup), o_wt = take(4 * 256 * nsup), o_gs = take(4 * 256 * (nsup + 64)), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
+    const size_t o_ex = take(2 * Q), o_al = take(4 * (size_t)kFChunk * nsub), o_ac = take(4 * nsub), o_gm = take(8 * nsub), o_se = take(4 * nsup), o_wt = take(4 * 256 * nsup), o_gs = take(4 * 256 * (nsup + 64)), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
                  o_fb = take(512 * nsub), o_lb = take(512 * nsub), o_su = take(sizeof(FrameSuper) * nsup),
                  o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_re = take(64);
     if (off > c->fws_bytes) {
@@ -1690,6 +1703,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     ws.exitR = (uint16_t *)(b + o_ex);
     ws.alist = (uint32_t *)(b + o_al);
     ws.acnt = (uint32_t *)(b + o_ac);
+    ws.gmark = (uint64_t *)(b + o_gm);
     ws.sentry = (uint32_t *)(b + o_se);
     ws.wtab = (uint32_t *)(b + o_wt);
     ws.gsx = (uint32_t *)(b + o_gs);

@@ -139,6 +139,8 @@ struct RecArgs {
     uint32_t payk;             // 0, or 1 + the dynamic byte field the payload kernels move for the
                                // group kernels' blocks (k_enc/dec_payload)
     uint32_t pay_fb;           // payk: XDR bytes before that field in a record (mark + fixed fields)
+    uint32_t pay_heads;        // decode, payk: 1 k_dec_payload also stores the record's fixed fields,
+                               // 0 the group kernel stores them (tuning key 39)
     uint64_t *pay_pos;         // payk: per record, stream offset of that field's length word
                                // (decode: ~0 = not to be written)
     uint32_t *spec;            // decode, extent-derived counts (spec_mode != 0): ~0 = the derived
@@ -196,6 +198,13 @@ struct Tuning {
     int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of
                                     // records (0: each lane walks its record in HBM)
     int32_t grp_enc_lanes = 8;      // key 32: repeated-group encode, lanes per record (64 = a wave)
+    int32_t pay_heads = 0;          // key 39: config-3-shaped decode, the fixed fields of payload records:
+                                    // 0 stored by the group kernel (23.4 ms on config 3), 1 by the payload
+                                    // kernel's wave with the payload (29.1 ms: a wave per record writes
+                                    // its 6 head words as scattered dwords), DESIGN.md §5.0b
+    int32_t grp_dec_el = 0;         // key 38: repeated-group decode place element-parallel (one top-level
+                                    // group, no inner groups, <= 2 dynamic members), at most this many
+                                    // elements per sub-batch (0: a lane per record)
     int32_t spec_sizes = 2;         // key 31: sweep decode whose last dynamic field is a word vector
                                     // followed by fixed fields only: 1 derive its counts from the record
                                     // extents (sizes reads one length word per record, the place kernel
@@ -266,6 +275,8 @@ struct FrameWs {                              // device workspace of one walk
                                               // local): the exit is that word's next mark
     uint32_t *alist, *acnt;                   // [nsub][kFChunk], [nsub]: active words of each sub-chunk
                                               // (position | next << 12 | LAST << 24), their count
+    uint64_t *gmark;                          // [nsub] largest active target << 32 | its raw mark word
+                                              // (~0: none): the chain's likely last word, for k_fr_mark
     uint32_t *sentry;                         // [nsup] super-chunk entries on the real chain
     uint32_t *wtab;                           // [nsup][256] super-chunk exits of each one's first words
     uint32_t *gsx;                            // [nsup][256] walk from each window entry to the group end
@@ -366,6 +377,8 @@ struct GroupArgs {
     uint32_t ncond;              // conditional fields (0: every record / element has all of them)
     uint32_t dec_tile;           // decode place: LDS tile bytes (0: records read from HBM; key 33)
     uint32_t nest;               // some group holds an inner group (the NEST kernels)
+    uint32_t dec_el;             // decode place: element-parallel, descriptors per sub-batch (0: off; key 38)
+    uint32_t el_g;               // the element-parallel place's group (the schema's one top-level group)
     int32_t cvals[XDRG_MAX_CASES];
     GField f[kMaxFields];
 };

@@ -98,12 +98,14 @@ def _mutations(want, offs, n, rng):
     return out
 
 
-@pytest.fixture(params=[(8, 32768), (64, 0), (4, 1024)], ids=lambda p: f"enc{p[0]}-dtile{p[1]}")
+@pytest.fixture(params=[(8, 32768, 0), (64, 0, 0), (4, 1024, 0), (8, 16384, 256)],
+                ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}")
 def enc_lanes(request, gpu_ctx):
     """Group kernels under each production choice (tuning keys 32 / 33, as
     tests/test_group_cond.py)."""
     gpu_ctx.tune(32, request.param[0])
     gpu_ctx.tune(33, request.param[1])
+    gpu_ctx.tune(38, request.param[2])   # element-parallel place (one top-level group)
     yield request.param
     gpu_ctx.tune(0)
 
