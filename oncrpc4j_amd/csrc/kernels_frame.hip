@@ -152,22 +152,6 @@ __device__ __forceinline__ uint32_t fr_wave_incl(uint32_t v) {
     return v;
 }
 
-__device__ __forceinline__ uint32_t fr_wave_sum(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-__device__ __forceinline__ uint32_t fr_wave_max(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
-    return v;
-}
-__device__ __forceinline__ uint32_t fr_wave_min(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
-    return v;
-}
-
 // ---------------------------------------------------------------------------
 // k_fr_exits
 // ---------------------------------------------------------------------------
@@ -184,20 +168,16 @@ __device__ __forceinline__ uint32_t fr_wave_min(uint32_t v) {
 // sub-chunk's results kept in LDS instead measured slower: 32 KiB, fewer
 // blocks per CU.)  The compacted list goes out too, for k_fr_mark: per
 // sub-chunk alist[sub][k] = position | next << 12 | LAST << 24 of its active
-// words (complete fragments all), acnt[sub] of them, and gmark[sub] = the
-// largest active target << 32 | its raw stream word (~0: no active word): the
-// chain's last word in k_fr_mark is almost always that target, whose next mark
-// k_fr_mark then has without a dependent HBM load per sub-chunk.
+// words (complete fragments all), acnt[sub] of them.
 constexpr uint32_t kFRes = 0x10000u;
 constexpr uint32_t kFPtr = 0xfffu;     // the local pointer of a J value (bit 12: the word's LAST flag)
 template <int B>
 __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
                                                       uint16_t *exitR, uint32_t *alist, uint32_t *acnt,
-                                                      uint64_t *gmark, uint32_t *sentry, uint32_t *gentry,
-                                                      uint32_t ngrp) {
+                                                      uint32_t *sentry, uint32_t *gentry, uint32_t ngrp) {
     __shared__ __attribute__((aligned(16))) uint32_t J[kFChunk];
     __shared__ __attribute__((aligned(16))) uint16_t L[kFChunk];   // active positions (sub-chunk local)
-    __shared__ uint32_t wtot[4], wmx[4];
+    __shared__ uint32_t wtot[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t sbeg = blockIdx.x * kFSuper;
     const uint32_t send = min(sbeg + kFSuper, Q);   // chain words past it leave the super-chunk
@@ -278,15 +258,10 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
             __syncthreads();   // L
             // the list out (coalesced), before this thread's own entries jump
             uint32_t *al = alist + sub * kFChunk;
-            uint32_t tm = 0;   // the largest target among this thread's entries
             for (uint32_t k = tid; k < A; k += 256) {
                 const uint32_t li = L[k];
-                const uint32_t jv = J[li];
-                al[k] = li | (jv & 0x1fffu) << 12;
-                tm = max(tm, jv & kFPtr);
+                al[k] = li | (J[li] & 0x1fffu) << 12;
             }
-            tm = fr_wave_max(tm);
-            if (lane == 0) wmx[wv] = tm;
             // this thread's list entries: tid + 256 c, c < ceil((A - tid) / 256).
             // Asynchronous pointer jumping: a thread jumps its own entries until
             // they hold results, reading whatever the other threads have written
@@ -305,14 +280,7 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
                     if (u >= kFRes) pend &= ~(1u << c);
                 }
             }
-            __syncthreads();   // every entry holds its result; wmx
-            // the largest active target's raw word (an L2 hit: just staged)
-            if (tid == 0) {
-                const uint32_t M = max(max(wmx[0], wmx[1]), max(wmx[2], wmx[3]));
-                gmark[sub] = (uint64_t)M << 32 | (base + M < Q ? fr_at<B>(w, Q, base + M) : 0u);   // (a target may be Q)
-            }
-        } else if (tid == 0) {
-            gmark[sub] = ~0ull;
+            __syncthreads();   // every entry holds its result
         }
         typedef uint16_t u16x4f __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -329,7 +297,7 @@ __global__ __launch_bounds__(256, 6) void k_fr_exits(const uint32_t *__restrict_
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = y[i];
-        __syncthreads();   // this sub-chunk's exitR visible to the block; J, L, wtot, wmx free again
+        __syncthreads();   // this sub-chunk's exitR visible to the block; J, L, wtot free again
     }
 }
 
@@ -512,13 +480,27 @@ struct FrWaveStat {       // waves 0 and 1 (bitmap words 64 v .. 64 v + 63)
 };
 // bytes b0..b3 of w, each 0 or 1, as bits 0..3
 __device__ __forceinline__ uint32_t fr_bytes01(uint32_t w) { return (w * 0x01020408u) >> 24 & 0xfu; }
+__device__ __forceinline__ uint32_t fr_wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t fr_wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t fr_wave_min(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
+    return v;
+}
 
 template <int B>
 __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
                                                      const uint32_t *sentry, const uint64_t *res,
-                                                     const uint32_t *alist, const uint32_t *acnt,
-                                                     const uint64_t *gmark, FrameSub *sub, uint32_t *fbits,
-                                                     uint32_t *lbits, FrameSuper *sup) {
+                                                     const uint32_t *alist, const uint32_t *acnt, FrameSub *sub,
+                                                     uint32_t *fbits, uint32_t *lbits, FrameSuper *sup) {
     // J[1] (pointer doubling) and pred (pruning) are never live together: one
     // buffer; a doubling pass clears it afterwards, as pred's stamps expect
     __shared__ __attribute__((aligned(16))) uint16_t J[2][kFChunk];
@@ -548,20 +530,17 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
     *(u32x4m *)&J[1][8 * tid + 2048] = z4;
     if (tid < 128) fb[tid] = 0; else lb[tid - 128] = 0;
     __syncthreads();
-    // the next sub-chunk's list count, first two entries and likely last word, loaded one ahead
+    // the next sub-chunk's list count and first two entries, loaded one ahead
     uint32_t nA = acnt[sub0], n0 = alist[sub0 * kFChunk + tid], n1 = alist[sub0 * kFChunk + 256 + tid];
-    uint64_t ngm = tid == 0 ? gmark[sub0] : 0ull;
     for (uint32_t j = 0; j < nsub; ++j) {
         const uint32_t base = sbeg + j * kFChunk;
         const uint32_t bend = base + kFChunk;
         const uint64_t sj = sub0 + j;
         const uint32_t A = nA, p0 = n0, p1 = n1;
-        const uint64_t gm = ngm;
         if (j + 1 < nsub) {
             nA = acnt[sj + 1];
             n0 = alist[(sj + 1) * kFChunk + tid];
             n1 = alist[(sj + 1) * kFChunk + 256 + tid];
-            if (tid == 0) ngm = gmark[sj + 1];
         }
         FrameSub info;
         info.pre_frag = pre_f;
@@ -605,9 +584,7 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
         uint32_t guess = 0, gword = 0;
         if (tid == 0) {
             guess = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-            // the largest list target: k_fr_exits left its word (gmark); else a load
-            if (guess == (uint32_t)(gm >> 32)) gword = (uint32_t)gm;
-            else if (base + guess < Q) gword = fr_at<B>(w, Q, base + guess);
+            if (base + guess < Q) gword = fr_at<B>(w, Q, base + guess);
         }
         // drop the nodes with no predecessor in S until nothing changes; every
         // node left reaches back to the entry (positions fall along
@@ -1046,7 +1023,7 @@ static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
     const uint64_t ngrp = (nsup + kFixGrp - 1) / kFixGrp;   // <= nsup: k_fr_exits sets every gentry
     hipLaunchKernelGGL(k_fr_exits<B>, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.exitR, ws.alist, ws.acnt,
-                       ws.gmark, ws.sentry, ws.gentry, (uint32_t)ngrp);
+                       ws.sentry, ws.gentry, (uint32_t)ngrp);
     const FrExits<B> ex{w, ws.exitR, Q, tb};
     hipLaunchKernelGGL(k_fr_win<B>, dim3((uint32_t)((nsup * kFixWin + 255) / 256)), dim3(256), 0, st, ex,
                        (uint32_t)nsup, ws.wtab);
@@ -1057,7 +1034,7 @@ static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint
     hipLaunchKernelGGL(k_fr_fix_fill<B>, dim3((uint32_t)ngrp), dim3(256), 0, st, ex, ws.wtab, ws.gentry,
                        (uint32_t)nsup, ws.sentry);
     hipLaunchKernelGGL(k_fr_mark<B>, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.alist,
-                       ws.acnt, ws.gmark, ws.sub, ws.fbits, ws.lbits, ws.sup);
+                       ws.acnt, ws.sub, ws.fbits, ws.lbits, ws.sup);
     hipLaunchKernelGGL(k_fr_bases, dim3(1), dim3(1024), 0, st, ws.sup, nsup, ws.bases, ws.res);
     // several sub-chunks per block, while the grid keeps >= 64 blocks (short
     // streams keep their parallelism)

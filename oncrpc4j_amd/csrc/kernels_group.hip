@@ -799,6 +799,10 @@ __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint6
 __device__ __forceinline__ void g_elem_skip(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t &pos,
                                             uint64_t end, GDisc &d, GRun &run) {
     const GField &f = a.f[g];
+    if (!f.ndm && !f.ncm) {   // elements of one size (a list's TRUE is already past)
+        pos += f.efix - (f.kind == XDRG_K_LIST ? 4 : 0);
+        return;
+    }
     for (uint32_t j = 1; j <= f.nmem; ++j) {
         const GField &m = a.f[g + j];
         if (f.ncm && !g_dec_field_present(a, g + j, in, pos, end, d)) continue;

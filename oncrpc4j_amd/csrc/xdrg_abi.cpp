@@ -1686,7 +1686,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     const uint64_t F = Q + 2;
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_ex = take(2 * Q), o_al = take(4 * (size_t)kFChunk * nsub), o_ac = take(4 * nsub), o_gm = take(8 * nsub), o_se = take(4 * nsup), o_wt = take(4 * 256 * nsup), o_gs = take(4 * 256 * (nsup + 64)), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
+    const size_t o_ex = take(2 * Q), o_al = take(4 * (size_t)kFChunk * nsub), o_ac = take(4 * nsub), o_se = take(4 * nsup), o_wt = take(4 * 256 * nsup), o_gs = take(4 * 256 * (nsup + 64)), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
                  o_fb = take(512 * nsub), o_lb = take(512 * nsub), o_su = take(sizeof(FrameSuper) * nsup),
                  o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_re = take(64);
     if (off > c->fws_bytes) {
@@ -1703,7 +1703,6 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     ws.exitR = (uint16_t *)(b + o_ex);
     ws.alist = (uint32_t *)(b + o_al);
     ws.acnt = (uint32_t *)(b + o_ac);
-    ws.gmark = (uint64_t *)(b + o_gm);
     ws.sentry = (uint32_t *)(b + o_se);
     ws.wtab = (uint32_t *)(b + o_wt);
     ws.gsx = (uint32_t *)(b + o_gs);

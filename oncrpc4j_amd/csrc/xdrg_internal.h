@@ -275,8 +275,6 @@ struct FrameWs {                              // device workspace of one walk
                                               // local): the exit is that word's next mark
     uint32_t *alist, *acnt;                   // [nsub][kFChunk], [nsub]: active words of each sub-chunk
                                               // (position | next << 12 | LAST << 24), their count
-    uint64_t *gmark;                          // [nsub] largest active target << 32 | its raw mark word
-                                              // (~0: none): the chain's likely last word, for k_fr_mark
     uint32_t *sentry;                         // [nsup] super-chunk entries on the real chain
     uint32_t *wtab;                           // [nsup][256] super-chunk exits of each one's first words
     uint32_t *gsx;                            // [nsup][256] walk from each window entry to the group end

@@ -96,6 +96,10 @@ def main():
     f, c = cmap.tape("chunk_map")
     print(json.dumps(run("chunk_map replies (replica copies[2] in list elements)", f, c, 1 << 20, (0, 16), (0, 12))),
           flush=True)
+    vix = rpcgen.parse_file(os.path.join(g, "volume_index.x"))
+    f, c = vix.tape("volume_index")
+    print(json.dumps(run("volume_index replies (a list and an array inside list elements)", f, c, 512 << 10,
+                         (0, 24), (0, 6))), flush=True)
 
 
 if __name__ == "__main__":
