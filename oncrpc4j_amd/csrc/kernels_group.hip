@@ -826,8 +826,12 @@ struct GElDesc {   // (scalar members: an indexed array here went to scratch)
     uint64_t E0;                  // the sub-batch's first element
     uint32_t nm;                  // dynamic members
     uint32_t ms0, ms1;            // their slots
+    uint32_t mk0, mk1;            // their field indices
     uint64_t sb0, sb1;            // their native offsets at E0
     const uint8_t *tile;
+    uint64_t rb;                  // the block's first record; per block record j (LDS, prefetched):
+    const uint64_t *mE;           //   the group's first element of record rb + j (j <= 256)
+    const uint64_t *mb0, *mb1;    //   the dynamic members' native offsets at it
 };
 
 // in: where stream offset x is read, in + x (the stream, or an LDS tile
@@ -860,11 +864,22 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
             continue;
         }
         if (f.type == XDRG_T_GROUP) {
-            const uint64_t e0 = f.kind == XDRG_K_FIXED ? r * f.count : g_rec_base(a, f.slot, r);
-            const uint64_t cnt = f.kind == XDRG_K_FIXED ? f.count : a.rec_cnt[(uint64_t)(f.slot - 1) * a.n + r];
-            if (f.kind == XDRG_K_DYNAMIC) pos += 4;
+            uint64_t e0, cnt;
             GRun run;
-            g_run_init(a, k, r, e0, run);
+            if constexpr (EL) {   // the block's metadata, prefetched into LDS
+                const uint32_t j = (uint32_t)(r - el.rb);
+                e0 = el.mE[j];
+                cnt = el.mE[j + 1] - e0;
+#pragma unroll
+                for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;
+                if (el.nm > 0) { run.set(el.ms0, el.mb0[j]); a.f[el.mk0].offsets[e0] = el.mb0[j]; }
+                if (el.nm > 1) { run.set(el.ms1, el.mb1[j]); a.f[el.mk1].offsets[e0] = el.mb1[j]; }
+            } else {
+                e0 = f.kind == XDRG_K_FIXED ? r * f.count : g_rec_base(a, f.slot, r);
+                cnt = f.kind == XDRG_K_FIXED ? f.count : a.rec_cnt[(uint64_t)(f.slot - 1) * a.n + r];
+                g_run_init(a, k, r, e0, run);
+            }
+            if (f.kind == XDRG_K_DYNAMIC) pos += 4;
             for (uint64_t e = e0; e < e0 + cnt; ++e) {
                 if (f.kind == XDRG_K_LIST) pos += 4;   // its TRUE
                 if constexpr (EL) {
@@ -980,10 +995,17 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
 // member native offsets: descriptors in LDS), and then every lane of the
 // block decodes an element: consecutive lanes, consecutive elements, so the
 // member stores of an instruction fall on consecutive rows.
+// LDS of k_grp_dec_place_el: per-block metadata (extents, the group's first
+// elements, the dynamic members' bases: 4 x 257 u64) | tile | descriptors
+constexpr size_t kElMeta = 4 * (kRecThreads + 1) * 8;
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_el(const GroupArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t *tile = smem;
-    uint32_t *dpos = (uint32_t *)(smem + a.dec_tile);
+    uint64_t *mx = (uint64_t *)smem;             // [257] record extents (clamped to in_len)
+    uint64_t *mE = mx + (kRecThreads + 1);       // [257] the group's first element of each record
+    uint64_t *mb0 = mE + (kRecThreads + 1);      // [257] dynamic member 0's base
+    uint64_t *mb1 = mb0 + (kRecThreads + 1);     // [257] dynamic member 1's base
+    uint8_t *tile = smem + kElMeta;
+    uint32_t *dpos = (uint32_t *)(tile + a.dec_tile);
     uint32_t *drel = dpos + a.dec_el;
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
     const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
@@ -994,34 +1016,42 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_el(const GroupArg
     const uintptr_t xb = (uintptr_t)a.xdr;
     const uint32_t g = a.el_g;
     const GField &G = a.f[g];
-    auto ext = [&](uint64_t r) -> uint64_t { const uint64_t x = a.rec_in[r]; return x < a.xdr_cap ? x : a.xdr_cap; };
-    // first element of record r (r <= n)
-    auto E = [&](uint64_t r) -> uint64_t {
-        if (G.kind == XDRG_K_FIXED) return r * G.count;
-        return r < a.n ? g_rec_base(a, G.slot, r) : a.totals[G.slot - 1];
-    };
     GElDesc el;
     el.pos = dpos;
     el.rel = drel;
     el.cap = a.dec_el;
     el.tile = tile;
     el.nm = 0;
-    el.ms0 = el.ms1 = 0;
+    el.ms0 = el.ms1 = el.mk0 = el.mk1 = 0;
     el.sb0 = el.sb1 = 0;
     for (uint32_t j = 1; j <= G.nmem; ++j) {
         if (a.f[g + j].kind != XDRG_K_DYNAMIC) continue;
-        if (el.nm == 0) el.ms0 = a.f[g + j].slot;
-        else el.ms1 = a.f[g + j].slot;
+        if (el.nm == 0) { el.ms0 = a.f[g + j].slot; el.mk0 = g + j; }
+        else { el.ms1 = a.f[g + j].slot; el.mk1 = g + j; }
         ++el.nm;
     }
+    el.rb = rb;
+    el.mE = mE;
+    el.mb0 = mb0;
+    el.mb1 = mb1;
+    // the block's metadata in one round trip (records rb .. rb + nlive, one past the last)
+    for (uint32_t j = tid; j <= nlive; j += kRecThreads) {
+        const uint64_t r = rb + j;
+        const uint64_t x = a.rec_in[r];
+        mx[j] = x < a.xdr_cap ? x : a.xdr_cap;
+        mE[j] = G.kind == XDRG_K_FIXED ? r * G.count : (r < a.n ? g_rec_base(a, G.slot, r) : a.totals[G.slot - 1]);
+        if (el.nm > 0) mb0[j] = r < a.n ? g_rec_base(a, el.ms0, r) : a.totals[el.ms0 - 1];
+        if (el.nm > 1) mb1[j] = r < a.n ? g_rec_base(a, el.ms1, r) : a.totals[el.ms1 - 1];
+    }
+    __syncthreads();
     uint32_t js = 0;
     while (js < nlive) {
         const uint32_t je1 = js + 1 + tid;
         bool fits = false;
         if (je1 <= nlive) {
-            const uintptr_t lo = (xb + ext(rb + js)) & ~(uintptr_t)15;
-            const uintptr_t hi = (xb + ext(rb + je1) + 15) & ~(uintptr_t)15;
-            fits = hi >= lo && hi - lo <= a.dec_tile && E(rb + je1) - E(rb + js) <= a.dec_el;
+            const uintptr_t lo = (xb + mx[js]) & ~(uintptr_t)15;
+            const uintptr_t hi = (xb + mx[je1] + 15) & ~(uintptr_t)15;
+            fits = hi >= lo && hi - lo <= a.dec_tile && mE[je1] - mE[js] <= a.dec_el;
         }
         const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
         if (k1 == 0) {   // one record larger than the tile or the descriptors: its lane decodes from HBM
@@ -1030,18 +1060,18 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_el(const GroupArg
             continue;
         }
         const uint32_t je = js + k1;
-        const uintptr_t a0 = (xb + ext(rb + js)) & ~(uintptr_t)15;
-        const uintptr_t a1 = (xb + ext(rb + je) + 15) & ~(uintptr_t)15;
+        const uintptr_t a0 = (xb + mx[js]) & ~(uintptr_t)15;
+        const uintptr_t a1 = (xb + mx[je] + 15) & ~(uintptr_t)15;
         const uint32_t nch = a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u;
         g_stage_tile(tile, a0, nch);
-        el.E0 = E(rb + js);
-        if (el.nm > 0) el.sb0 = g_rec_base(a, el.ms0, rb + js);
-        if (el.nm > 1) el.sb1 = g_rec_base(a, el.ms1, rb + js);
+        el.E0 = mE[js];
+        el.sb0 = mb0[js];
+        el.sb1 = mb1[js];
         __syncthreads();
         const uint8_t *in = tile + (uint32_t)(xb - a0);   // stream offset x at in + x
         if (js + tid < je) g_dec_record<false, true>(a, rb + js + tid, in, el);
         __syncthreads();   // descriptors
-        const uint64_t nel = E(rb + je) - el.E0;
+        const uint64_t nel = mE[je] - el.E0;
         for (uint32_t i = tid; i < nel; i += kRecThreads) {
             GRun run;
 #pragma unroll
@@ -1077,7 +1107,7 @@ static void launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) 
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
     case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
         if (!NEST && a.dec_el && a.dec_tile)
-            hipLaunchKernelGGL(k_grp_dec_place_el, rgrid, block, a.dec_tile + 12 * (size_t)a.dec_el, st, a);
+            hipLaunchKernelGGL(k_grp_dec_place_el, rgrid, block, kElMeta + a.dec_tile + 12 * (size_t)a.dec_el, st, a);
         else if (a.dec_tile) hipLaunchKernelGGL(k_grp_dec_place_lds<NEST>, rgrid, block, a.dec_tile, st, a);
         else hipLaunchKernelGGL(k_grp_dec_place<NEST>, rgrid, block, 0, st, a);
         break;

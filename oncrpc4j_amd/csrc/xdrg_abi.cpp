@@ -1012,7 +1012,7 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         // the element-parallel place: one top-level group without inner groups,
         // at most two dynamic members, LDS for the tile and the descriptors
         if (c->tune.grp_dec_el && a.dec_tile && !a.nest && s->ngroups == 1 &&
-            a.dec_tile + 12ull * (uint64_t)c->tune.grp_dec_el <= 65536) {
+            8224ull + a.dec_tile + 12ull * (uint64_t)c->tune.grp_dec_el <= 65536) {   // (+ kElMeta)
             for (uint32_t k = 0; k < a.nf; ++k)
                 if (a.f[k].type == XDRG_T_GROUP && !a.f[k].grp && a.f[k].ndm <= 2 &&
                     !(a.f[k].kind == XDRG_K_FIXED && a.f[k].cond)) {   // (an absent T x[N] has no descriptors)

@@ -202,9 +202,10 @@ struct Tuning {
                                     // 0 stored by the group kernel (23.4 ms on config 3), 1 by the payload
                                     // kernel's wave with the payload (29.1 ms: a wave per record writes
                                     // its 6 head words as scattered dwords), DESIGN.md §5.0b
-    int32_t grp_dec_el = 0;         // key 38: repeated-group decode place element-parallel (one top-level
+    int32_t grp_dec_el = 1024;      // key 38: repeated-group decode place element-parallel (one top-level
                                     // group, no inner groups, <= 2 dynamic members), at most this many
-                                    // elements per sub-batch (0: a lane per record)
+                                    // elements per sub-batch (0: a lane per record; READDIR decode 9.3 ->
+                                    // 5.5 ms, DUMP 3.0 -> 1.9)
     int32_t spec_sizes = 2;         // key 31: sweep decode whose last dynamic field is a word vector
                                     // followed by fixed fields only: 1 derive its counts from the record
                                     // extents (sizes reads one length word per record, the place kernel

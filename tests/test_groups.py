@@ -210,7 +210,7 @@ def _sane(hb):
     return hb
 
 
-@pytest.fixture(params=[(8, 32768, 0), (64, 0, 0), (4, 1024, 0), (8, 16384, 256)],
+@pytest.fixture(params=[(8, 32768, 1024), (8, 32768, 0), (64, 0, 0), (4, 1024, 0), (8, 16384, 256)],
                 ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}")
 def enc_lanes(request, gpu_ctx):
     """Group kernels under each production choice: encode place lanes per

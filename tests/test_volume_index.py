@@ -179,7 +179,7 @@ def test_oracle_random_roundtrip():
     assert out.equal(hb)
 
 
-@pytest.fixture(params=[(8, 32768, 0), (64, 0, 0), (4, 1024, 0), (8, 16384, 256)],
+@pytest.fixture(params=[(8, 32768, 1024), (8, 32768, 0), (64, 0, 0), (4, 1024, 0), (8, 16384, 256)],
                 ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}")
 def grp_tune(request, gpu_ctx):
     """Group kernels under each production choice (tuning keys 32 / 33)."""
