@@ -834,18 +834,22 @@ struct GElDesc {   // (scalar members: an indexed array here went to scratch)
     const uint64_t *mb0, *mb1;    //   the dynamic members' native offsets at it
 };
 
-// in: where stream offset x is read, in + x (the stream, or an LDS tile
-// holding this record's bytes: k_grp_dec_place_lds).
+// in: where stream offset x is read, in + (x - base) (the stream with base 0,
+// or an LDS tile holding this record's bytes whose first byte is stream offset
+// base: k_grp_dec_place_lds).  Positions are tile-relative so that no pointer
+// into the tile ever lies below it: a generic (flat) access through a tile
+// pointer moved below the tile's 32-bit LDS address wraps out of the LDS
+// aperture (the place kernels' former tile + (uint32_t)(xb - a0) faulted so).
 // EL (element-parallel place): the record's one group leaves descriptors in
 // *el instead of decoding its elements (the block decodes them afterwards,
 // a lane per element).
 template <bool NEST, bool EL = false>
-__device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in,
+__device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in, uint64_t base = 0,
                                              const GElDesc &el = GElDesc{}) {
     constexpr int L0 = NEST ? 0 : 1;   // depth the record's groups start at (1: inner groups compiled out)
     const GExtent ex = g_extent(a, r);   // the extent the walk checked (clamped to in_len)
-    const uint64_t end = ex.b;
-    uint64_t pos = ex.a + (a.framed ? 4 : 0);
+    const uint64_t end = ex.b - base;
+    uint64_t pos = ex.a + (a.framed ? 4 : 0) - base;
     GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
         const GField &f = a.f[k];
@@ -974,12 +978,10 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
         const uint32_t je = js + k1;
         const uintptr_t a0 = (xb + ext(rb + js)) & ~(uintptr_t)15;
         const uintptr_t a1 = (xb + ext(rb + je) + 15) & ~(uintptr_t)15;
-        const uint32_t nch = a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u;
-        g_stage_tile(tile, a0, nch);
+        g_stage_tile(tile, a0, a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u);
         __syncthreads();
-        // stream offset x of these records is at tile + (xb + x - a0)
-        const uint8_t *in = tile + (uint32_t)(xb - a0);
-        if (js + tid < je) g_dec_record<NEST>(a, rb + js + tid, in);
+        // stream offset x of these records is at tile + (x - (a0 - xb))
+        if (js + tid < je) g_dec_record<NEST>(a, rb + js + tid, tile, a0 - xb);
         __syncthreads();   // the tile's next use
         js = je;
     }
@@ -995,6 +997,9 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
 // member native offsets: descriptors in LDS), and then every lane of the
 // block decodes an element: consecutive lanes, consecutive elements, so the
 // member stores of an instruction fall on consecutive rows.
+#ifndef XDRG_EL_PROBE
+#define XDRG_EL_PROBE 0   // experiment builds only (wrong output): 1 no element decode, 2 no record walk, 4 no staging
+#endif
 // LDS of k_grp_dec_place_el: per-block metadata (extents, the group's first
 // elements, the dynamic members' bases: 4 x 257 u64) | tile | descriptors
 constexpr size_t kElMeta = 4 * (kRecThreads + 1) * 8;
@@ -1063,16 +1068,16 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_el(const GroupArg
         const uintptr_t a0 = (xb + mx[js]) & ~(uintptr_t)15;
         const uintptr_t a1 = (xb + mx[je] + 15) & ~(uintptr_t)15;
         const uint32_t nch = a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u;
-        g_stage_tile(tile, a0, nch);
+        if (!(XDRG_EL_PROBE & 4)) g_stage_tile(tile, a0, nch);
         el.E0 = mE[js];
         el.sb0 = mb0[js];
         el.sb1 = mb1[js];
         __syncthreads();
-        const uint8_t *in = tile + (uint32_t)(xb - a0);   // stream offset x at in + x
-        if (js + tid < je) g_dec_record<false, true>(a, rb + js + tid, in, el);
+        // stream offset x at tile + (x - (a0 - xb))
+        if (!(XDRG_EL_PROBE & 2) && js + tid < je) g_dec_record<false, true>(a, rb + js + tid, tile, a0 - xb, el);
         __syncthreads();   // descriptors
         const uint64_t nel = mE[je] - el.E0;
-        for (uint32_t i = tid; i < nel; i += kRecThreads) {
+        for (uint32_t i = tid; !(XDRG_EL_PROBE & 1) && i < nel; i += kRecThreads) {
             GRun run;
 #pragma unroll
             for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;

@@ -384,7 +384,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 32: if (v != 64 && v != 32 && v != 16 && v != 8 && v != 4) return -1; t.grp_enc_lanes = (int32_t)v; return 0;
     case 33: if (v && (!in(1024, 65536) || (v & 15))) return -1; t.grp_dec_tile = (int32_t)v; return 0;
     case 36: if (!in(1, 64)) return -1; t.emit_per = (int32_t)v; return 0;
-    case 37: if (!in(0, 1)) return -1; t.xcd_order = (int32_t)v; return 0;
+    case 37: if (!in(0, 3)) return -1; t.xcd_order = (int32_t)v; return 0;
     case 38: if (v && !in(64, 4096)) return -1; t.grp_dec_el = (int32_t)v; return 0;
     case 39: if (!in(0, 1)) return -1; t.pay_heads = (int32_t)v; return 0;
     default: return -1;

@@ -191,8 +191,8 @@ struct Tuning {
                                     // stride and take the stride kernels (sync calls), 0 the record path
     int32_t stage_copy = 1;         // key 26: XDRG_HOST_PTRS copies of device-mapped host spans:
                                     // 1 copy kernels (k_copy_link), 0 the DMA engines (hipMemcpyAsync)
-    int32_t xcd_order = 1;          // key 37: payload kernels walk the records in XCD order (xcd_block),
-                                    // 0 in block order
+    int32_t xcd_order = 1;          // key 37: payload kernels walk the records in XCD order (xcd_block):
+                                    // bit 0 encode, bit 1 decode (0 in block order)
     int32_t emit_per = 4;           // key 36: frame walk, sub-chunks per k_fr_emit block (at most;
                                     // halved until the grid has >= 64 blocks)
     int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of
