@@ -440,24 +440,28 @@ __device__ __forceinline__ GExtent g_extent(const GroupArgs &a, uint64_t r) {
 // A dynamic field's length word at pos, then its payload: the reference's
 // check order (Xdr.java:171-175 length, :374-383 / :392-401 len == 0 first,
 // checkArraySize :1034-1037, ensureBytes :1028-1032).  Returns 0 or an error.
-__device__ __forceinline__ uint32_t g_walk_dyn(const GField &f, const uint8_t *in, uint64_t end, uint64_t &pos,
-                                               uint32_t &len_out) {
+__device__ __forceinline__ uint32_t g_walk_dyn_z(uint32_t xsz, const uint8_t *in, uint64_t end, uint64_t &pos,
+                                                 uint32_t &len_out) {
     if (end - pos < 4) return XDRG_E_SHORT;
     const int32_t len = (int32_t)g_ld(in + pos);
     pos += 4;
     uint64_t need;
-    if (f.xsz == 1) {
+    if (xsz == 1) {
         if (len == 0) { len_out = 0; return 0; }
         if (len < 0) return XDRG_E_CORRUPT;
         need = (uint64_t)len + pad4((uint64_t)len);
     } else {
         if (len < 0) return XDRG_E_CORRUPT;
-        need = (uint64_t)len * f.xsz;
+        need = (uint64_t)len * xsz;
     }
     if (end - pos < need) return XDRG_E_SHORT;
     pos += need;
     len_out = (uint32_t)len;
     return 0;
+}
+__device__ __forceinline__ uint32_t g_walk_dyn(const GField &f, const uint8_t *in, uint64_t end, uint64_t &pos,
+                                               uint32_t &len_out) {
+    return g_walk_dyn_z(f.xsz, in, end, pos, len_out);
 }
 
 // Walk group g from pos (its count word or list bools and every element, each
@@ -483,6 +487,40 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
     if (!f.ndm && !f.ncm && f.kind != XDRG_K_LIST) {   // elements of one size
         if ((end - pos) / f.efix < n) return XDRG_E_SHORT;
         pos += n * f.efix;
+    } else if (g + 1 == a.lay_g) {   // one layout: the same checks, member descriptors not read
+        // (a run of fixed members is SHORT iff one of them is, with the same sub)
+        const uint32_t pre = a.lay_pre, mid = a.lay_mid, post = a.lay_post, nd = f.ndm;
+        uint64_t c0 = 0, c1 = 0, i = 0;
+        for (;; ++i) {
+            if (f.kind == XDRG_K_LIST) {   // xdrDecodeBoolean(): any non-zero = another
+                if (end - pos < 4) return XDRG_E_SHORT;
+                const uint32_t more = g_ld(in + pos);
+                pos += 4;
+                if (!more) break;
+            } else if (i == n) {
+                break;
+            }
+            if (end - pos < pre) return XDRG_E_SHORT;
+            pos += pre;
+            if (nd > 0) {
+                uint32_t len = 0;
+                uint32_t err = g_walk_dyn_z(a.lay_z0, in, end, pos, len);
+                if (err) return err;
+                c0 += len;
+                if (end - pos < mid) return XDRG_E_SHORT;
+                pos += mid;
+                if (nd > 1) {
+                    err = g_walk_dyn_z(a.lay_z1, in, end, pos, len);
+                    if (err) return err;
+                    c1 += len;
+                    if (end - pos < post) return XDRG_E_SHORT;
+                    pos += post;
+                }
+            }
+        }
+        if (nd > 0) cnt[a.lay_s0 - 1] += (uint32_t)c0;
+        if (nd > 1) cnt[a.lay_s1 - 1] += (uint32_t)c1;
+        n = i;
     } else {
         uint64_t i = 0;
         for (;; ++i) {
@@ -832,7 +870,16 @@ struct GElDesc {   // (scalar members: an indexed array here went to scratch)
     uint64_t rb;                  // the block's first record; per block record j (LDS, prefetched):
     const uint64_t *mE;           //   the group's first element of record rb + j (j <= 256)
     const uint64_t *mb0, *mb1;    //   the dynamic members' native offsets at it
+    // an element without conditional members as a layout (lay = 1): fixed
+    // bytes pre, dynamic member 0 (XDR element size z0), fixed bytes mid,
+    // member 1 (z1), fixed bytes post; the record walk then reads one length
+    // word per dynamic member and no member descriptor
+    uint32_t lay, pre, mid, post, z0, z1;
 };
+// XDR words of cnt elements of XDR size z (g_dyn_words by size alone)
+__device__ __forceinline__ uint64_t g_dyn_words_z(uint32_t z, uint64_t cnt) {
+    return z == 1 ? (cnt + 3) >> 2 : cnt * (z >> 2);
+}
 
 // in: where stream offset x is read, in + (x - base) (the stream with base 0,
 // or an LDS tile holding this record's bytes whose first byte is stream offset
@@ -884,6 +931,33 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
                 g_run_init(a, k, r, e0, run);
             }
             if (f.kind == XDRG_K_DYNAMIC) pos += 4;
+            if constexpr (EL) {
+                if (el.lay) {   // elements of a fixed layout: one length word per dynamic member
+                    const uint32_t lb = f.kind == XDRG_K_LIST ? 4u : 0u;
+                    uint64_t r0 = el.nm > 0 ? run.get(el.ms0) : 0, r1 = el.nm > 1 ? run.get(el.ms1) : 0;
+                    for (uint64_t e = e0; e < e0 + cnt; ++e) {
+                        pos += lb;   // a list's TRUE
+                        const uint32_t i = (uint32_t)(e - el.E0);
+                        el.pos[i] = (uint32_t)pos;   // (in is the tile)
+                        pos += el.pre;
+                        if (el.nm > 0) {
+                            el.rel[i] = (uint32_t)(r0 - el.sb0);
+                            const uint64_t len = g_ld(in + pos);
+                            r0 += len;
+                            pos += 4 + 4 * g_dyn_words_z(el.z0, len) + el.mid;
+                            if (el.nm > 1) {
+                                el.rel[el.cap + i] = (uint32_t)(r1 - el.sb1);
+                                const uint64_t len1 = g_ld(in + pos);
+                                r1 += len1;
+                                pos += 4 + 4 * g_dyn_words_z(el.z1, len1) + el.post;
+                            }
+                        }
+                    }
+                    if (f.kind == XDRG_K_LIST) pos += 4;   // its FALSE
+                    k += 1 + f.nmem;
+                    continue;
+                }
+            }
             for (uint64_t e = e0; e < e0 + cnt; ++e) {
                 if (f.kind == XDRG_K_LIST) pos += 4;   // its TRUE
                 if constexpr (EL) {
@@ -970,6 +1044,21 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
             fits = hi >= lo && hi - lo <= a.dec_tile;
         }
         const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
+        if constexpr (NEST) {
+            // one call site of the record decode (two inlined copies of the NEST
+            // form kept the kernel arguments in 4 KB of scratch): a record larger
+            // than the tile (k1 = 0) decodes from the stream through the same
+            // generic pointer, tile-relative positions keep both in range
+            const uint32_t je = js + (k1 ? k1 : 1);
+            const uintptr_t a0 = (xb + ext(rb + js)) & ~(uintptr_t)15;
+            const uintptr_t a1 = (xb + ext(rb + je) + 15) & ~(uintptr_t)15;
+            g_stage_tile(tile, a0, k1 && a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u);
+            __syncthreads();
+            if (js + tid < je) g_dec_record<NEST>(a, rb + js + tid, k1 ? tile : a.xdr, k1 ? a0 - xb : 0);
+            __syncthreads();   // the tile's next use
+            js = je;
+            continue;
+        }
         if (k1 == 0) {   // one record larger than the tile: its lane decodes from HBM
             if (tid == 0) g_dec_record<NEST>(a, rb + js, a.xdr);
             ++js;
@@ -1003,7 +1092,11 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
 // LDS of k_grp_dec_place_el: per-block metadata (extents, the group's first
 // elements, the dynamic members' bases: 4 x 257 u64) | tile | descriptors
 constexpr size_t kElMeta = 4 * (kRecThreads + 1) * 8;
-__global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_el(const GroupArgs a) {
+#ifndef XDRG_EL_OCC
+#define XDRG_EL_OCC 1   // blocks per CU the register budget is sized for (experiment builds: 2, 3)
+#endif
+template <bool LAY>   // LAY: the group is GroupArgs::lay_g (the record walk reads the layout)
+__global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(const GroupArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *mx = (uint64_t *)smem;             // [257] record extents (clamped to in_len)
     uint64_t *mE = mx + (kRecThreads + 1);       // [257] the group's first element of each record
@@ -1035,6 +1128,13 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_el(const GroupArg
         else { el.ms1 = a.f[g + j].slot; el.mk1 = g + j; }
         ++el.nm;
     }
+    // the element layout (GroupArgs::lay_g: every element has the same fields)
+    el.lay = LAY;
+    el.pre = a.lay_pre;
+    el.mid = a.lay_mid;
+    el.post = a.lay_post;
+    el.z0 = a.lay_z0;
+    el.z1 = a.lay_z1;
     el.rb = rb;
     el.mE = mE;
     el.mb0 = mb0;
@@ -1111,8 +1211,11 @@ static void launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) 
     case GRP_DEC_WALK: hipLaunchKernelGGL(k_grp_dec_walk<NEST>, grid, block, 0, st, a); break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
     case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
-        if (!NEST && a.dec_el && a.dec_tile)
-            hipLaunchKernelGGL(k_grp_dec_place_el, rgrid, block, kElMeta + a.dec_tile + 12 * (size_t)a.dec_el, st, a);
+        if (!NEST && a.dec_el && a.dec_tile) {
+            const size_t lds = kElMeta + a.dec_tile + 12 * (size_t)a.dec_el;
+            if (a.lay_g == a.el_g + 1) hipLaunchKernelGGL(k_grp_dec_place_el<true>, rgrid, block, lds, st, a);
+            else hipLaunchKernelGGL(k_grp_dec_place_el<false>, rgrid, block, lds, st, a);
+        }
         else if (a.dec_tile) hipLaunchKernelGGL(k_grp_dec_place_lds<NEST>, rgrid, block, a.dec_tile, st, a);
         else hipLaunchKernelGGL(k_grp_dec_place<NEST>, rgrid, block, 0, st, a);
         break;

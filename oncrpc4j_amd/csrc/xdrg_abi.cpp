@@ -733,6 +733,22 @@ static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols
     }
     a.ncond = s->ncond;
     a.nest = s->nested ? 1u : 0u;
+    // the element layout of a schema's one top-level group (GroupArgs::lay_g)
+    a.lay_g = 0;
+    for (uint32_t k = 0; k < a.nf && s->ngroups == 1 && !a.nest; ++k) {
+        const GField &G = a.f[k];
+        if (G.type != XDRG_T_GROUP || G.grp || G.ncm || G.ngm || G.ndm > 2) continue;
+        uint32_t q = 0, fb[3] = {0, 0, 0}, z[2] = {4, 4}, sl[2] = {0, 0};
+        for (uint32_t j = 1; j <= G.nmem; ++j) {
+            const GField &m = a.f[k + j];
+            if (m.kind == XDRG_K_DYNAMIC) { z[q] = m.xsz; sl[q] = m.slot; ++q; }
+            else fb[q] += m.xbytes;
+        }
+        a.lay_g = k + 1;
+        a.lay_pre = fb[0]; a.lay_mid = fb[1]; a.lay_post = fb[2];
+        a.lay_z0 = z[0]; a.lay_z1 = z[1];
+        a.lay_s0 = sl[0]; a.lay_s1 = sl[1];
+    }
     for (size_t i = 0; i < s->cvals.size(); ++i) a.cvals[i] = s->cvals[i];
     a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;
     if (!a.nblocks) a.nblocks = 1;

@@ -378,6 +378,14 @@ struct GroupArgs {
     uint32_t nest;               // some group holds an inner group (the NEST kernels)
     uint32_t dec_el;             // decode place: element-parallel, descriptors per sub-batch (0: off; key 38)
     uint32_t el_g;               // the element-parallel place's group (the schema's one top-level group)
+    // 1 + the top-level group whose elements have one layout (no conditional
+    // members, no inner groups, at most two dynamic members), 0: none.  The walk
+    // and the element-parallel place then read one length word per dynamic
+    // member of an element and no member descriptor.
+    uint32_t lay_g;
+    uint32_t lay_pre, lay_mid, lay_post;   // fixed member bytes before / between / after the dynamic members
+    uint32_t lay_z0, lay_z1;               // the dynamic members' XDR element sizes
+    uint32_t lay_s0, lay_s1;               // their counted-column slots
     int32_t cvals[XDRG_MAX_CASES];
     GField f[kMaxFields];
 };

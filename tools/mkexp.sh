@@ -1,8 +1,13 @@
 #!/bin/bash
-# experiment builds of kernels_rec.hip with -D flags: mkexp.sh name "flags"
+# experiment builds of one kernel source with -D flags, linked with the regular
+# objects of the others: mkexp.sh name kernels_rec|kernels_group|kernels_frame "flags"
 set -e
 cd "$(dirname "$0")/../oncrpc4j_amd/csrc"
 mkdir -p ../../exp
 B=build
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics $2 -c kernels_rec.hip -o /tmp/exp_$1.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../exp/lib_$1.so $B/kernels_fixed.o /tmp/exp_$1.o $B/kernels_multi.o $B/kernels_frame.o $B/kernels_group.o $B/xdrg_abi.o
+objs=""
+for k in kernels_fixed kernels_rec kernels_multi kernels_frame kernels_group xdrg_abi; do
+    if [ "$k" = "$2" ]; then objs="$objs /tmp/exp_$1.o"; else objs="$objs $B/$k.o"; fi
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics $3 -c $2.hip -o /tmp/exp_$1.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../exp/lib_$1.so $objs
