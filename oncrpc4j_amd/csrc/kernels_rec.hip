@@ -2139,6 +2139,10 @@ __device__ __forceinline__ uint32_t enc_fit(const RecArgs &a, const uint64_t (&b
 // (git history): the field-major scatter (1.23x WRITE), the
 // same with nontemporal stores, an LDS output image composed from HBM inputs
 // or from the staged tile.
+#ifndef XDRG_ENC_PROBE
+#define XDRG_ENC_PROBE 0   // experiment builds only (wrong output): 1 no byte chunks, 2 no word chunks,
+                           // 4 no fixed fields, 8 no staging copy
+#endif
 __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;   // row stride of soff / srel
@@ -2238,7 +2242,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
             cb[d + 1] += stage_chunks(f.data + (base[d] + srel[d * RS + js]) * esz,
                                       f.data + (base[d] + srel[d * RS + je]) * esz, &a0[d]);
         }
-        stage_copy(tile, a0, cb, a.ndyn);   // (stage_dma measured 3.70 vs 3.62 ms here: nothing to overlap)
+        if (!(XDRG_ENC_PROBE & 8)) stage_copy(tile, a0, cb, a.ndyn);   // (stage_dma measured 3.70 vs 3.62 ms here: nothing to overlap)
         __syncthreads();
         const uint32_t m = je - js;
         {   // record-major scatter: a group of lanes writes all of a record
@@ -2256,7 +2260,8 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
                     if (f.kind != XDRG_K_DYNAMIC) {
                         const uint32_t nw = f.xbytes >> 2;
                         uint8_t *dst = rec + fpre + dynb;
-                        for (uint32_t i = gl; i < nw; i += G) *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
+                        for (uint32_t i = gl; !(XDRG_ENC_PROBE & 4) && i < nw; i += G)
+                            *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
                         fpre += f.xbytes;
                         continue;
                     }
@@ -2270,7 +2275,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
                     if (bytes) {
                         const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
                         const uint64_t nch = (1 + ((cnt + 3) >> 2) + 3) >> 2;
-                        for (uint64_t c = gl; c < nch; c += G) {
+                        for (uint64_t c = gl; !(XDRG_ENC_PROBE & 1) && c < nch; c += G) {
                             const uint32_t *w = (const uint32_t *)(tile + (L - sh + 16 * (int64_t)c - 4));
                             Chunk5 q;
                             q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = w[4];
@@ -2278,7 +2283,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
                         }
                     } else {
                         const uint64_t nch = (1 + cnt + 3) >> 2;
-                        for (uint64_t c = gl; c < nch; c += G) {
+                        for (uint64_t c = gl; !(XDRG_ENC_PROBE & 2) && c < nch; c += G) {
                             const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c - 4));
                             Chunk5 q;
                             q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = 0;

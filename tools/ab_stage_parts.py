@@ -6,7 +6,8 @@ No round-trip check: a variant that skips work writes wrong bytes on purpose.
   XDRG_LIBRARY=exp/lib_NOBYTES.so python tools/ab_stage_parts.py [records]
 
 XDRG_TUNE="20=0,21=1" applies per-context kernel choices (xdrg_internal.h
-Tuning keys) first.
+Tuning keys) first; XDRG_PARTS=encode times only the encode (a build that
+drops encode work leaves a stream the decode need not walk).
 """
 import json
 import os
@@ -32,7 +33,10 @@ def main():
     cfg = int(os.environ.get("XDRG_CONFIG", "4"))
     wl = bench.Workload(ctx, cfg, n, False)
     out = {"lib": os.path.basename(os.environ.get("XDRG_LIBRARY", "libxdrgpu.so")), "tune": tune, "records": n}
+    parts = os.environ.get("XDRG_PARTS", "encode,decode").split(",")   # encode probes: encode only
     for name, fn in (("encode", wl.encode), ("decode", wl.decode)):
+        if name not in parts:
+            continue
         fn()
         torch.cuda.synchronize()
         ctx.reset_stats()
