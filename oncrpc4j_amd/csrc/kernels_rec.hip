@@ -2517,7 +2517,8 @@ __device__ __forceinline__ void dec_stage_batch(const RecArgs &a, const uint8_t 
 // §5.3) is gone.  Byte fields: Xdr.java:760-763 / :797-800 (bytes, pad
 // skipped); int vectors: Xdr.java:607-613 (one bswap per element).
 #ifndef XDRG_SW_PROBE
-#define XDRG_SW_PROBE 0   // experiment builds only: parts of the sweep switched off (wrong output)
+#define XDRG_SW_PROBE 0   // experiment builds only: parts of the sweep switched off (wrong output;
+                          // 32: no sub-batch at all)
 #endif
 constexpr uint32_t kSweepMetaPad = 4;   // meta sentinels after the sub-batch's last record
 
@@ -3030,6 +3031,7 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
             dec_record_block(a, rb + j, rec_extent(a, rb + j).a + (a.framed ? 4 : 0), supto[j], snrel, j, tid, kRecThreads);
         return;
     }
+    if (XDRG_SW_PROBE & 32) return;   // (experiment builds: walk, look-back and prologue only)
     // ---- sub-batches
     uint32_t js = 0;
     uint32_t k1 = nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
