@@ -426,6 +426,204 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a
     }
 }
 
+// Element-parallel encode place (tuning key 41 = bytes of an LDS image of the
+// output, 0: off) for schemas without conditional fields whose one top-level
+// group has a layout (GroupArgs::lay_g).  The lane-group place above writes a
+// record's elements from its own lanes as scattered dwords.  Here a sub-batch
+// of records whose XDR fits the image is composed in LDS: every lane sizes
+// elements (the layout and the dynamic members' offsets), a block scan places
+// them, record lanes write the top-level fields, counts and list ends, every
+// lane writes elements (consecutive lanes, consecutive elements), and the
+// block copies the image out with 16-byte stores.  Same words as
+// g_enc_record (jrpcgen.java:835-906 counts / list bools, Xdr.java:765-800).
+constexpr uint32_t kEncElCap = 1024;   // elements per sub-batch
+__host__ __device__ constexpr size_t enc_el_lds_bytes(uint32_t img) {
+    return (size_t)(kRecPerBlock + 1) * 8 + (size_t)(kEncElCap + 1) * 4 + (size_t)kRecPerBlock * 4 +
+           (size_t)kEncElCap * 2 + (size_t)(kRecPerBlock + 1) * 2 + 16 + img;
+}
+__device__ __forceinline__ void g_st_img(uint8_t *img, uint32_t p, uint32_t v) { *(uint32_t *)(img + p) = v; }
+// XDR bytes of element e of the layout group g
+__device__ __forceinline__ uint32_t g_lay_elem_bytes(const GroupArgs &a, const GField &G, uint64_t e) {
+    uint64_t z = (G.kind == XDRG_K_LIST ? 4 : 0) + a.lay_pre;
+    if (G.ndm > 0) {
+        const GField &m0 = a.f[a.slot_field[a.lay_s0 - 1]];
+        const uint64_t c0 = m0.offsets[e + 1] - m0.offsets[e];
+        z += 4 + (a.lay_z0 == 1 ? c0 + pad4(c0) : c0 * a.lay_z0) + a.lay_mid;
+        if (G.ndm > 1) {
+            const GField &m1 = a.f[a.slot_field[a.lay_s1 - 1]];
+            const uint64_t c1 = m1.offsets[e + 1] - m1.offsets[e];
+            z += 4 + (a.lay_z1 == 1 ? c1 + pad4(c1) : c1 * a.lay_z1) + a.lay_post;
+        }
+    }
+    return (uint32_t)z;
+}
+// Element e of group g into the image at p (its list bool, then every member)
+__device__ __forceinline__ void g_enc_elem_img(const GroupArgs &a, uint32_t g, uint64_t e, uint8_t *img, uint32_t p) {
+    const GField &G = a.f[g];
+    if (G.kind == XDRG_K_LIST) {   // xdrEncodeBoolean(true) (pmaplist.java:65-67)
+        g_st_img(img, p, bswap32r(1u));
+        p += 4;
+    }
+    for (uint32_t j = 1; j <= G.nmem; ++j) {
+        const GField &m = a.f[g + j];
+        if (m.kind != XDRG_K_DYNAMIC) {
+            for (uint32_t w = 0; w < m.xbytes >> 2; ++w) g_st_img(img, p + 4 * w, g_fixed_word(m, e, w));
+            p += m.xbytes;
+            continue;
+        }
+        const uint64_t e0 = m.offsets[e], cnt = m.offsets[e + 1] - e0;
+        g_st_img(img, p, bswap32r((uint32_t)cnt));
+        const uint32_t nw = (uint32_t)g_dyn_words(m, cnt);
+        for (uint32_t w = 0; w < nw; ++w) g_st_img(img, p + 4 + 4 * w, g_dyn_word(m, e0, cnt, w));
+        p += 4 + 4 * nw;
+    }
+}
+// Record r's own words into the image at p (its mark, top-level fields, the
+// group's count and list end); returns the image offset of its first element
+// (its elements take gbytes there).
+__device__ __forceinline__ uint32_t g_enc_top_img(const GroupArgs &a, uint64_t r, uint8_t *img, uint32_t p,
+                                                  uint64_t size, uint32_t gbytes) {
+    uint32_t first = p;
+    if (a.framed) {   // GrizzlyRpcTransport.java:103-110
+        g_st_img(img, p, bswap32r((uint32_t)(size - 4) | kLastFrag));
+        p += 4;
+    }
+    for (uint32_t k = 0; k < a.nf;) {
+        const GField &f = a.f[k];
+        if (f.type == XDRG_T_GROUP) {
+            uint64_t e0, cnt;
+            g_range(f, r, e0, cnt);
+            if (f.kind == XDRG_K_DYNAMIC) {   // xdrEncodeInt($size) (jrpcgen.java:866-876)
+                g_st_img(img, p, bswap32r((uint32_t)cnt));
+                p += 4;
+            }
+            first = p;
+            p += gbytes;
+            if (f.kind == XDRG_K_LIST) {   // xdrEncodeBoolean(false): the list ends
+                g_st_img(img, p, 0u);
+                p += 4;
+            }
+            k += 1 + f.nmem;
+            continue;
+        }
+        if (f.kind != XDRG_K_DYNAMIC) {
+            for (uint32_t w = 0; w < f.xbytes >> 2; ++w) g_st_img(img, p + 4 * w, g_fixed_word(f, r, w));
+            p += f.xbytes;
+        } else {
+            const uint64_t e0 = f.offsets[r], cnt = f.offsets[r + 1] - e0;
+            g_st_img(img, p, bswap32r((uint32_t)cnt));
+            const uint32_t nw = (uint32_t)g_dyn_words(f, cnt);
+            for (uint32_t w = 0; w < nw; ++w) g_st_img(img, p + 4 + 4 * w, g_dyn_word(f, e0, cnt, w));
+            p += 4 + 4 * nw;
+        }
+        ++k;
+    }
+    return first;
+}
+__global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint64_t *soff = (uint64_t *)smem;                       // [RPB + 1] record offsets in the stream
+    uint32_t *xs = (uint32_t *)(soff + kRecPerBlock + 1);    // [cap + 1] element offsets in the sub-batch's elements
+    uint32_t *rst = xs + kEncElCap + 1;                      // [RPB] image offset of a record's first element
+    uint16_t *own = (uint16_t *)(rst + kRecPerBlock);        // [cap] an element's record (sub-batch index)
+    uint16_t *fj = own + kEncElCap;                          // [RPB + 1] a record's first element (sub-batch index)
+    uint8_t *img = smem + ((enc_el_lds_bytes(0) - 16 + 15) & ~(size_t)15);
+    const uint64_t total = a.totals[0];
+    if (total > a.xdr_cap) return;   // XDRG_E_CAPACITY: write nothing
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t tid = threadIdx.x, t0 = tid * kRecPerThread;
+    uint64_t sz[kRecPerThread], s = 0;
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        sz[j] = rb + t0 + j < a.n ? a.rec_size[rb + t0 + j] : 0;
+        s += sz[j];
+    }
+    uint64_t btot;
+    uint64_t off = a.block_sums[blockIdx.x] + block_excl_scan(s, &btot);
+#pragma unroll
+    for (int j = 0; j < kRecPerThread; ++j) {
+        soff[t0 + j] = off;
+        if (a.rec_out && rb + t0 + j < a.n) a.rec_out[rb + t0 + j] = off;
+        off += sz[j];
+    }
+    if (tid == kRecThreads - 1) soff[kRecPerBlock] = off;
+    if (a.rec_out && blockIdx.x == 0 && tid == 0) a.rec_out[a.n] = total;
+    __syncthreads();
+    const uint32_t nrec = (uint32_t)(a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock);
+    const uint32_t g = a.lay_g - 1;
+    const GField &G = a.f[g];
+    auto gfirst = [&](uint32_t j) -> uint64_t {   // the group's first element of block record j (j <= nrec)
+        const uint64_t r = rb + j;
+        return G.kind == XDRG_K_FIXED ? r * G.count : G.offsets[r];
+    };
+    uint32_t js = 0;
+    while (js < nrec) {
+        // records [js, js + 1 + tid) fit iff their bytes and elements do (monotone)
+        const uint32_t je1 = js + 1 + tid;
+        bool fits = false;
+        if (je1 <= nrec)
+            fits = soff[je1] - soff[js] <= a.enc_img && gfirst(je1) - gfirst(js) <= kEncElCap;
+        const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
+        if (k1 == 0) {   // one record larger than the image: wave 0 writes it to the stream
+            if (tid < 64) g_enc_record<64, false>(a, rb + js, soff[js], soff[js + 1] - soff[js], tid);
+            ++js;
+            continue;
+        }
+        const uint32_t je = js + k1, m = k1;
+        const uint64_t E0 = gfirst(js);
+        const uint32_t nel = (uint32_t)(gfirst(je) - E0);
+        for (uint32_t t = tid; t <= m; t += kRecThreads) fj[t] = (uint16_t)(gfirst(js + t) - E0);
+        // element sizes, four consecutive elements per lane, placed by a block scan
+        uint32_t z[4], zs = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = 4 * tid + u;
+            z[u] = i < nel ? g_lay_elem_bytes(a, G, E0 + i) : 0u;
+            zs += z[u];
+        }
+        uint64_t ztot;
+        uint32_t x = (uint32_t)block_excl_scan(zs, &ztot);   // (its barriers publish fj)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = 4 * tid + u;
+            if (i < nel) xs[i] = x;
+            x += z[u];
+        }
+        if (tid == 0) xs[nel] = (uint32_t)ztot;
+        for (uint32_t t = tid; t < m; t += kRecThreads)
+            for (uint32_t i = fj[t]; i < fj[t + 1]; ++i) own[i] = (uint16_t)t;
+        __syncthreads();
+        // record lanes: their own words; the image starts at record js
+        const uint64_t ib = soff[js];
+        for (uint32_t t = tid; t < m; t += kRecThreads) {
+            const uint32_t j = js + t;
+            rst[t] = g_enc_top_img(a, rb + j, img, (uint32_t)(soff[j] - ib), soff[j + 1] - soff[j],
+                                   xs[fj[t + 1]] - xs[fj[t]]);
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < nel; i += kRecThreads) {
+            const uint32_t t = own[i];
+            g_enc_elem_img(a, g, E0 + i, img, rst[t] + xs[i] - xs[fj[t]]);
+        }
+        __syncthreads();
+        // the image out: dwords up to a 16-byte boundary, 16-byte stores, dwords
+        const uint32_t nb = (uint32_t)(soff[je] - ib);
+        uint8_t *dst = a.xdr + ib;   // (4-aligned: XDR words)
+        const uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15) < nb ? (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15) : nb;
+        const uint32_t nchunk = (nb - head) >> 4;
+        for (uint32_t i = tid; i < nchunk; i += kRecThreads) {
+            const uint32_t *w = (const uint32_t *)(img + head + 16 * i);
+            u32x4g o;
+            o.x = w[0]; o.y = w[1]; o.z = w[2]; o.w = w[3];
+            *(u32x4g *)(dst + head + 16 * i) = o;
+        }
+        const uint32_t tail0 = head + 16 * nchunk;
+        if (tid < (head >> 2)) *(uint32_t *)(dst + 4 * tid) = *(const uint32_t *)(img + 4 * tid);
+        if (tid < ((nb - tail0) >> 2)) *(uint32_t *)(dst + tail0 + 4 * tid) = *(const uint32_t *)(img + tail0 + 4 * tid);
+        js = je;   // (the next fit's barrier ends the image's use)
+    }
+}
+
 // ===========================================================================
 // Decode
 // ===========================================================================
@@ -1201,8 +1399,9 @@ static void launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) 
     const dim3 rgrid((uint32_t)((a.n + kRecThreads - 1) / kRecThreads));
     switch (phase) {
     case GRP_ENC_SIZES: hipLaunchKernelGGL(k_grp_enc_sizes<NEST>, grid, block, 0, st, a); break;
-    case GRP_ENC_PLACE:   // G lanes per record (tuning key 32)
-        if (a.enc_lanes == 4) hipLaunchKernelGGL((k_grp_enc_place<4, NEST>), grid, block, 0, st, a);
+    case GRP_ENC_PLACE:   // element-parallel (key 41) or G lanes per record (key 32)
+        if (!NEST && a.enc_img) hipLaunchKernelGGL(k_grp_enc_place_el, grid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (a.enc_lanes == 4) hipLaunchKernelGGL((k_grp_enc_place<4, NEST>), grid, block, 0, st, a);
         else if (a.enc_lanes == 8) hipLaunchKernelGGL((k_grp_enc_place<8, NEST>), grid, block, 0, st, a);
         else if (a.enc_lanes == 16) hipLaunchKernelGGL((k_grp_enc_place<16, NEST>), grid, block, 0, st, a);
         else if (a.enc_lanes == 32) hipLaunchKernelGGL((k_grp_enc_place<32, NEST>), grid, block, 0, st, a);

@@ -387,6 +387,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 37: if (!in(0, 3)) return -1; t.xcd_order = (int32_t)v; return 0;
     case 38: if (v && !in(64, 4096)) return -1; t.grp_dec_el = (int32_t)v; return 0;
     case 39: if (!in(0, 1)) return -1; t.pay_heads = (int32_t)v; return 0;
+    case 41: if (v && (!in(4096, 49152) || (v & 15))) return -1; t.grp_enc_img = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -784,6 +785,8 @@ static int group_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *co
     int rc = fill_group(c, s, cols, n, framed, false, a);
     if (rc) return rc;
     a.enc_lanes = (uint32_t)c->tune.grp_enc_lanes;
+    // the element-parallel place: a group with a layout, no conditional field
+    if (c->tune.grp_enc_img && a.lay_g && !s->ncond) a.enc_img = (uint32_t)c->tune.grp_enc_img;
     a.xdr = out;
     a.xdr_cap = out_cap;
     a.rec_out = rec_offsets;

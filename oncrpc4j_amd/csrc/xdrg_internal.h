@@ -202,6 +202,10 @@ struct Tuning {
                                     // 0 stored by the group kernel (23.4 ms on config 3), 1 by the payload
                                     // kernel's wave with the payload (29.1 ms: a wave per record writes
                                     // its 6 head words as scattered dwords), DESIGN.md §5.0b
+    int32_t grp_enc_img = 16384;    // key 41: repeated-group encode place element-parallel through an LDS
+                                    // image of this many bytes (schemas without conditional fields whose
+                                    // group has a layout; 0: lanes per record, key 32).  DUMP encode 2.19 ->
+                                    // 0.83 ms, READDIR 5.07 -> 3.03 (32 KiB: 0.92 / 2.99), DESIGN.md §5.7
     int32_t grp_dec_el = 1024;      // key 38: repeated-group decode place element-parallel (one top-level
                                     // group, no inner groups, <= 2 dynamic members), at most this many
                                     // elements per sub-batch (0: a lane per record; READDIR decode 9.3 ->
@@ -386,6 +390,7 @@ struct GroupArgs {
     uint32_t lay_pre, lay_mid, lay_post;   // fixed member bytes before / between / after the dynamic members
     uint32_t lay_z0, lay_z1;               // the dynamic members' XDR element sizes
     uint32_t lay_s0, lay_s1;               // their counted-column slots
+    uint32_t enc_img;            // encode place: element-parallel, LDS image bytes (0: off; key 41)
     int32_t cvals[XDRG_MAX_CASES];
     GField f[kMaxFields];
 };

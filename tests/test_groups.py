@@ -210,16 +210,20 @@ def _sane(hb):
     return hb
 
 
-@pytest.fixture(params=[(8, 32768, 1024), (8, 32768, 0), (64, 0, 0), (4, 1024, 0), (8, 16384, 256)],
-                ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}")
+@pytest.fixture(params=[(8, 32768, 1024, 32768), (8, 32768, 0, 0), (64, 0, 0, 0), (4, 1024, 0, 4096),
+                        (8, 16384, 256, 16384)],
+                ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}-img{p[3]}")
 def enc_lanes(request, gpu_ctx):
     """Group kernels under each production choice: encode place lanes per
     record (tuning key 32; 8 the default, 64 a wave per record) and decode
     place LDS tile (key 33; 32 KiB the default, 0 records read from HBM,
-    1 KiB: most records larger than the tile take the HBM path)."""
+    1 KiB: most records larger than the tile take the HBM path); the
+    element-parallel places (key 38 decode, key 41 encode image: 4 KiB sends
+    the large-element records through the lane path)."""
     gpu_ctx.tune(32, request.param[0])
     gpu_ctx.tune(33, request.param[1])
     gpu_ctx.tune(38, request.param[2])   # element-parallel place (one top-level group)
+    gpu_ctx.tune(41, request.param[3])   # element-parallel encode (layout groups, no conditional fields)
     yield request.param
     gpu_ctx.tune(0)
 
