@@ -406,7 +406,8 @@ int  xdrg_deframe(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *paylo
  * call GARBAGE_ARGS, RpcDispatcher.java:126-131, and the caller resumes at
  * *consumed) — except XDRG_E_CAPACITY, which delivers up to it (*n_msgs =
  * first_bad) so the caller can retry it with larger columns.  Host staging
- * takes schemas without repeated groups (groups: device or mapped memory). */
+ * of a schema with repeated groups walks, deframes and then decodes the
+ * complete messages' bodies (three staged passes; the same results).      */
 int  xdrg_frame_scan_ex(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint64_t *msg_offsets,
                         uint64_t cap, uint64_t *n_msgs, uint64_t *consumed, uint32_t flags);
 int  xdrg_deframe_ex(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *payload,

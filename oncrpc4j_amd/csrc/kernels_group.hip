@@ -222,8 +222,31 @@ __device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g
     uint64_t e0, cnt;
     g_range(G, row, e0, cnt);
     uint64_t s = G.kind == XDRG_K_FIXED ? 0 : 4;   // the count, or a list's closing bool
-    if (G.ndm || G.ncm) for (uint64_t e = e0; e < e0 + cnt; ++e) s += g_elem_bytes<L>(a, g, e, d);
-    else s += cnt * G.efix;
+    if (G.ndm && g + 1 == a.lay_g) {   // one layout: the fixed bytes, and each dynamic member's from its offsets
+        s += cnt * (uint64_t)(G.efix + 4 * G.ndm);
+        const uint64_t *o0 = a.f[a.slot_field[a.lay_s0 - 1]].offsets;
+        const uint32_t z0 = a.lay_z0;
+        uint64_t p0 = o0[e0];
+        for (uint64_t e = e0; e < e0 + cnt; ++e) {
+            const uint64_t q0 = o0[e + 1], c = q0 - p0;
+            s += z0 == 1 ? c + pad4(c) : c * z0;
+            p0 = q0;
+        }
+        if (G.ndm > 1) {
+            const uint64_t *o1 = a.f[a.slot_field[a.lay_s1 - 1]].offsets;
+            const uint32_t z1 = a.lay_z1;
+            uint64_t p1 = o1[e0];
+            for (uint64_t e = e0; e < e0 + cnt; ++e) {
+                const uint64_t q1 = o1[e + 1], c = q1 - p1;
+                s += z1 == 1 ? c + pad4(c) : c * z1;
+                p1 = q1;
+            }
+        }
+    } else if (G.ndm || G.ncm) {
+        for (uint64_t e = e0; e < e0 + cnt; ++e) s += g_elem_bytes<L>(a, g, e, d);
+    } else {
+        s += cnt * G.efix;
+    }
     return s;
 }
 

@@ -1899,6 +1899,43 @@ static int recv_staged(xdrg_ctx *c, int mode, const xdrg_schema *s, const uint8_
     return rc ? rc : fr;
 }
 
+// Group schemas on host memory: the staged walk (stream offsets of the
+// complete messages), the staged deframe of those messages (their bodies into
+// host scratch), then the staged decode of the bodies (xdrg_decode_batch with
+// XDRG_HOST_PTRS, whose ring moves a chunk's element rows).  The same results
+// as the device receive, which also decodes assembled bodies; each stream byte
+// crosses PCIe three times here instead of once.
+static int recv_staged_groups(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t len, uint64_t cap,
+                              xdrg_column *cols, uint64_t *msg_offsets, uint64_t *n_msgs, uint64_t *consumed,
+                              uint64_t *first_bad, int *err) {
+    std::vector<uint64_t> so(cap + 1, 0);
+    hs::RecvResult R;
+    int rc = recv_staged(c, hs::RECV_SCAN, nullptr, in, len, cap, nullptr, nullptr, 0, so.data(), R);
+    if (rc) return rc;   // XDRG_E_INCOMPLETE: STOP
+    const uint64_t nm = R.n_msgs, used = R.consumed;
+    std::vector<uint8_t> body(used + 16);
+    std::vector<uint64_t> bo(nm + 1, 0);
+    hs::RecvResult D;
+    rc = recv_staged(c, hs::RECV_DEFRAME, nullptr, in, used, nm, nullptr, body.data(), used, bo.data(), D);
+    if (rc) return rc;
+    if (D.n_msgs != nm || D.consumed != used) {
+        c->err = "receive: the deframe of the scanned messages disagrees with the scan";
+        return XDRG_E_HIP;
+    }
+    uint64_t fb = nm;
+    int e = XDRG_OK;
+    rc = xdrg_decode_batch(c, s, body.data(), bo[nm], bo.data(), nm, cols, XDRG_HOST_PTRS, &fb, &e);
+    if (rc && !e) return rc;   // an argument / HIP failure, not a decode error
+    const uint64_t upto = !e ? nm : (e == XDRG_E_CAPACITY ? fb : fb + 1);   // (recv_device's delivery)
+    if (msg_offsets) memcpy(msg_offsets, so.data(), (nm + 1) * 8);
+    *n_msgs = upto;
+    *consumed = so[upto];
+    *first_bad = e ? fb : nm;
+    *err = e;
+    if (e) c->err = xdrg_status_string(e);
+    return e;
+}
+
 extern "C" int xdrg_frame_scan_ex(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint64_t *msg_offsets,
                                   uint64_t cap, uint64_t *n_msgs, uint64_t *consumed, uint32_t flags) {
     if (!c || !msg_offsets || !n_msgs) return XDRG_E_INVAL;
@@ -1977,7 +2014,7 @@ extern "C" int xdrg_receive_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8
     rc = check_columns(c, s, cols, cap, true);
     if (rc) return rc;
     if ((flags & XDRG_HOST_PTRS) && !(flags & XDRG_HOST_MAPPED)) {
-        if (s->ngroups) return inval(c, "repeated groups: the receive staging ring takes no group schema yet");
+        if (s->ngroups) return recv_staged_groups(c, s, in, len, cap, cols, msg_offsets, n_msgs, consumed, first_bad, err);
         hs::RecvResult R;
         rc = recv_staged(c, hs::RECV_DECODE, s, in, len, cap, cols, nullptr, 0, msg_offsets, R);
         *n_msgs = R.n_msgs;

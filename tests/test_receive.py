@@ -47,6 +47,12 @@ SCHEMAS = {
     # optional data and unions as a conditional tape (include/xdrg.h xdrg_cond)
     "cond_union": ([(U, SC, 0), (B, SC, 0), (STR, DY, 0), (I, SC, 0), (H, SC, 0), (O, DY, 0)],
                    [(2, 1, 0, [1]), (4, 3, 0, [1, 2]), (5, 3, 0, [7])]),
+    # repeated groups (READDIR-like list of {fileid, name<>, cookie, bool}; a
+    # counted array of {int, string<>} between scalars): on host memory the
+    # walk, the deframe and the decode of the bodies are three staged passes
+    "dirlist_group": ([(abi.T_GROUP, abi.K_LIST, 0, 4), (H, SC, 0), (STR, DY, 0), (H, SC, 0), (B, SC, 0),
+                       (I, SC, 0)], None),
+    "items_group": ([(I, SC, 0), (abi.T_GROUP, DY, 0, 2), (I, SC, 0), (STR, DY, 0), (I, SC, 0)], None),
 }
 SLOT = 64 << 10
 MEMS = ["device", "pageable", "registered", "mapped"]
@@ -66,8 +72,8 @@ def _sane(hb, conds):
     """Discriminants that pick every arm; bools 0 / 1."""
     rng = np.random.default_rng(hb.n)
     for k, f in enumerate(hb.fields):
-        if f[0] == B:
-            hb.arrays[k][:] = rng.integers(0, 2, hb.n, dtype=np.uint8)
+        if f[0] == B:   # (a group member's array holds one value per element)
+            hb.arrays[k][:] = rng.integers(0, 2, len(hb.arrays[k]), dtype=np.uint8)
     for _, d, _, vals in conds or ():
         if hb.fields[d][0] != B:
             pool = np.array(list(vals) + [0, 5], dtype=np.int64)
@@ -182,7 +188,7 @@ def test_receive_cap_and_remainder(rctx, cap, mem):
 
 
 @pytest.mark.parametrize("mem", MEMS)
-@pytest.mark.parametrize("name", ["cfg4_shape", "many_dynamic", "cond_union"])
+@pytest.mark.parametrize("name", ["cfg4_shape", "many_dynamic", "cond_union", "dirlist_group"])
 def test_receive_errors_vs_oracle(rctx, name, mem):
     """Corrupted bodies: the first bad message and its code; the call delivers
     through it (consumed = its end) and the columns hold the messages before."""
