@@ -127,8 +127,9 @@ typedef struct xdrg_field {
  * [offsets[e], offsets[e+1]) (offsets has elements + 1 entries).  Decode
  * errors keep the reference's order: the count / list bools / member checks
  * as the element loops meet them; a negative count is XDRG_E_NEG_SIZE.
- * XDRG_HOST_PTRS staging takes one level of groups (inner groups: device
- * memory or XDRG_HOST_MAPPED).                                              */
+ * XDRG_HOST_PTRS staging windows one level of groups; a schema with inner
+ * groups on host memory goes through device scratch whole (the spans the call
+ * touches copied in and back, overlapping column spans merged).            */
 
 /* One native column.  Fixed-size fields (SCALAR / FIXED): record i's first
  * element is at  data + i*stride  (stride 0 = packed = elem_size*count), so

@@ -7,6 +7,7 @@
 // interface it replaces in include/xdrg.h.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1573,8 +1574,13 @@ static void stage_schema(const xdrg_schema *s, hs::Schema &v) {
 // offsets[n] elements; decode: cap), a group member's rows over the batch's
 // elements (encode: the group's offsets[n]; decode: the group's element
 // capacity).  A buffer registered shorter than its use is refused.
-static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool decode,
-                       std::vector<xdrg_column> &out) {
+// Every column's host span (bytes the call touches: rows x stride, values,
+// offsets + 1) mapped by fn(ptr, bytes) -> the device address (nullptr: not
+// covered).  XDRG_HOST_MAPPED maps through the registrations; the bounce path
+// through device scratch.
+template <typename F>
+static int map_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool decode,
+                    std::vector<xdrg_column> &out, F fn) {
     out.assign(cols, cols + s->f.size());
     // native rows of every field's column (a group precedes its members):
     // records, a FIXED group's rows x count, else the group's elements
@@ -1593,17 +1599,17 @@ static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
         const uint64_t rows = rows_of[k];
         if (f.type == XDRG_T_GROUP) {
             if (d.offsets && f.kind != XDRG_K_FIXED) {
-                d.offsets = (uint64_t *)span_device(cols[k].offsets, (rows + 1) * 8);
+                d.offsets = (uint64_t *)fn(cols[k].offsets, (rows + 1) * 8);
                 if (!d.offsets) return inval(c, "XDRG_HOST_MAPPED: group offsets not registered for every row + 1");
             }
             continue;
         }
         if (f.kind == XDRG_K_DYNAMIC) {
-            d.offsets = (uint64_t *)span_device(cols[k].offsets, (rows + 1) * 8);
+            d.offsets = (uint64_t *)fn(cols[k].offsets, (rows + 1) * 8);
             if (!d.offsets) return inval(c, "XDRG_HOST_MAPPED: column offsets not registered for every row + 1");
             const uint64_t vals = decode ? cols[k].cap : (rows ? cols[k].offsets[rows] : 0);
             if (d.data || vals) {
-                d.data = span_device(cols[k].data, vals * s->nsz[k]);
+                d.data = fn(cols[k].data, vals * s->nsz[k]);
                 if (!d.data) return inval(c, "XDRG_HOST_MAPPED: column values not registered for their extent");
             }
             continue;
@@ -1612,10 +1618,100 @@ static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
         const uint64_t elem = (uint64_t)s->nsz[k] * (f.kind == XDRG_K_FIXED ? f.count : 1);
         const int64_t st = eff_stride(s, k, cols[k]);
         const uint64_t span = rows == 0 || st == 0 ? elem : (uint64_t)st * (rows - 1) + elem;
-        d.data = span_device(cols[k].data, span);
+        d.data = fn(cols[k].data, span);
         if (!d.data) return inval(c, "XDRG_HOST_MAPPED: column data not registered for every row");
     }
     return XDRG_OK;
+}
+static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool decode,
+                       std::vector<xdrg_column> &out) {
+    return map_cols(c, s, cols, n, decode, out, [](const void *p, uint64_t b) { return span_device(p, b); });
+}
+
+// Host memory of a schema the staging ring does not window (groups inside
+// group elements: it moves one level of element rows) goes whole through
+// device scratch: the host spans the call touches — columns, stream, offsets;
+// overlapping ones merged (array-of-structs columns share bytes) — are copied
+// in, the device call runs, and the spans it writes are copied back.
+struct Bounce {
+    struct Span { const uint8_t *h; uint64_t len; bool out; };
+    struct Reg { uint8_t *h; uint64_t len; uint8_t *d; bool out; };
+    std::vector<Span> spans;
+    std::vector<Reg> regs;
+    void add(const void *p, uint64_t len, bool out) { if (p && len) spans.push_back({(const uint8_t *)p, len, out}); }
+    // merge the spans, allocate and fill the device regions
+    int place(xdrg_ctx *c) {
+        std::sort(spans.begin(), spans.end(), [](const Span &a, const Span &b) { return a.h < b.h; });
+        for (const Span &sp : spans) {
+            if (!regs.empty() && sp.h <= regs.back().h + regs.back().len) {
+                Reg &r = regs.back();
+                const uint8_t *e = std::max<const uint8_t *>(r.h + r.len, sp.h + sp.len);
+                r.len = (uint64_t)(e - r.h);
+                r.out |= sp.out;
+            } else {
+                regs.push_back({(uint8_t *)sp.h, sp.len, nullptr, sp.out});
+            }
+        }
+        for (Reg &r : regs) {
+            HIPCHK(c, hipMallocAsync((void **)&r.d, r.len, c->stream));
+            HIPCHK(c, hipMemcpyAsync(r.d, r.h, r.len, hipMemcpyHostToDevice, c->stream));
+        }
+        return XDRG_OK;
+    }
+    void *dev(const void *p) const {
+        const uint8_t *q = (const uint8_t *)p;
+        for (const Reg &r : regs)
+            if (q >= r.h && q < r.h + r.len) return r.d + (q - r.h);
+        return nullptr;
+    }
+    int finish(xdrg_ctx *c, bool copy_back) {
+        int rc = XDRG_OK;
+        for (Reg &r : regs) {
+            if (copy_back && r.out && hipMemcpyAsync(r.h, r.d, r.len, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+                rc = XDRG_E_HIP;
+            (void)hipFreeAsync(r.d, c->stream);
+        }
+        if (hipStreamSynchronize(c->stream) != hipSuccess) rc = XDRG_E_HIP;
+        return rc;
+    }
+};
+static int bounce_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, uint8_t *out,
+                         uint64_t out_cap, uint64_t *rec_offsets, uint32_t dflags, uint64_t *out_len) {
+    Bounce B;
+    std::vector<xdrg_column> dc;
+    int rc = map_cols(c, s, cols, n, false, dc, [&](const void *p, uint64_t b) { B.add(p, b, false); return (void *)p; });
+    if (rc) return rc;
+    B.add(out, out_cap, true);
+    B.add(rec_offsets, (n + 1) * 8, true);
+    HIPCHK(c, hipStreamSynchronize(c->stream));   // the caller's earlier work on this context
+    rc = B.place(c);
+    if (rc) { (void)B.finish(c, false); return rc; }
+    rc = map_cols(c, s, cols, n, false, dc, [&](const void *p, uint64_t) { return B.dev(p); });
+    uint64_t len = 0;
+    if (!rc) rc = encode_impl(c, s, dc.data(), n, (uint8_t *)B.dev(out), out_cap,
+                              (uint64_t *)B.dev(rec_offsets), dflags, &len, 0, nullptr);
+    const int fr = B.finish(c, rc == XDRG_OK);
+    if (!rc && out_len) *out_len = len;
+    return rc ? rc : fr;
+}
+static int bounce_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t in_len,
+                         const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t dflags,
+                         uint64_t *first_bad, int *err) {
+    Bounce B;
+    std::vector<xdrg_column> dc;
+    int rc = map_cols(c, s, cols, n, true, dc, [&](const void *p, uint64_t b) { B.add(p, b, true); return (void *)p; });
+    if (rc) return rc;
+    B.add(in, in_len, false);
+    B.add(rec_offsets, (n + 1) * 8, false);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    rc = B.place(c);
+    if (rc) { (void)B.finish(c, false); return rc; }
+    rc = map_cols(c, s, cols, n, true, dc, [&](const void *p, uint64_t) { return B.dev(p); });
+    if (!rc) rc = decode_impl(c, s, (const uint8_t *)B.dev(in), in_len, (const uint64_t *)B.dev(rec_offsets), n,
+                              dc.data(), dflags, first_bad, err, 0, nullptr);
+    const bool dec_err = rc && *err;   // a decode error: the records before it are delivered
+    const int fr = B.finish(c, rc == XDRG_OK || dec_err);
+    return rc ? rc : fr;
 }
 
 static int host_common(xdrg_ctx *c, const xdrg_schema *s, uint32_t flags) {
@@ -1644,7 +1740,7 @@ static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
         if ((n && !dout) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
         return encode_impl(c, s, dc.data(), n, dout, out_cap, drec, dflags, out_len, 0, nullptr);
     }
-    if (s->nested) return inval(c, "XDRG_HOST_PTRS: groups inside group elements take XDRG_HOST_MAPPED or device memory (the staging ring moves one level of element rows)");
+    if (s->nested) return bounce_encode(c, s, cols, n, out, out_cap, rec_offsets, dflags, out_len);
     hs::Schema v;
     stage_schema(s, v);
     rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);
@@ -1680,7 +1776,7 @@ static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         if ((in_len && !din) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
         return decode_impl(c, s, din, in_len, drec, n, dc.data(), dflags, first_bad, err, 0, nullptr);
     }
-    if (s->nested) return inval(c, "XDRG_HOST_PTRS: groups inside group elements take XDRG_HOST_MAPPED or device memory (the staging ring moves one level of element rows)");
+    if (s->nested) return bounce_decode(c, s, in, in_len, rec_offsets, n, cols, dflags, first_bad, err);
     hs::Schema v;
     stage_schema(s, v);
     rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);

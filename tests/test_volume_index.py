@@ -271,7 +271,7 @@ def test_gpu_volume_index_random_vs_oracle(gpu_ctx, grp_tune, framed):
 @pytest.mark.gpu
 def test_gpu_volume_index_mapped_host():
     """XDRG_HOST_MAPPED: the kernels read and write registered host columns
-    of the nested schema in place; the staging ring refuses the schema."""
+    of the nested schema in place."""
     import torch
     from oncrpc4j_amd import engine
     from hostmem import Registered, moved
@@ -290,8 +290,46 @@ def test_gpu_volume_index_mapped_host():
         back = moved(HostBatch.empty(FIELDS, n, hb0.dyn_caps()), mem)
         assert c.decode(sch, out, ln, n, back.columns(), rec_offsets=ro, mapped=True) == (0, n, 0)
         assert back.equal(hb0)
-        with pytest.raises(engine.XdrgError):   # the staging ring moves one level of element rows
-            c.encode(sch, hb.columns(), n, out, len(want) + 64, rec_offsets=ro, host=True)
+    finally:
+        mem.close()
+        c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["pageable", "registered"])
+def test_gpu_volume_index_host_ptrs(kind):
+    """XDRG_HOST_PTRS on the nested schema: the staging ring moves one level
+    of element rows, so the call bounces the spans it touches through device
+    scratch (merged where columns share bytes).  Encode == the xdrlib fixture,
+    decode == the batch, and a broken stream's status and the records before
+    its first bad one == the oracle's."""
+    import torch
+    from oncrpc4j_amd import engine
+    from hostmem import Pageable, Registered, moved
+    assert torch.cuda.is_available()
+    b = FIX["batches"][0]
+    hb0, want, offs = _batch(b)
+    n = hb0.n
+    c = engine.Context(0)
+    mem = Registered() if kind == "registered" else Pageable()
+    try:
+        hb = moved(hb0, mem)
+        sch = engine.Schema(FIELDS, CONDS)
+        out = mem.array(np.zeros(len(want) + 64, np.uint8))
+        ro = mem.array(np.zeros(n + 1, np.uint64))
+        ln = c.encode(sch, hb.columns(), n, out, len(want) + 64, rec_offsets=ro, host=True)
+        assert out[:ln].tobytes() == want and np.array_equal(ro, offs)
+        back = moved(HostBatch.empty(FIELDS, n, hb0.dyn_caps()), mem)
+        assert c.decode(sch, out, ln, n, back.columns(), rec_offsets=ro, host=True) == (0, n, 0)
+        assert back.equal(hb0)
+        for name, x, in_len, _ in _mutations(b, want, offs, np.random.default_rng(5)):
+            xin = mem.array(np.frombuffer(x, np.uint8).copy())
+            got = moved(HostBatch.empty(FIELDS, n, hb0.dyn_caps()), mem)
+            st = c.decode(sch, xin, in_len, n, got.columns(), rec_offsets=ro, host=True, raise_on_error=False)
+            ref = HostBatch.empty(FIELDS, n, hb0.dyn_caps())
+            rst = oracle.decode_batch(FIELDS, x[:in_len], offs, n, ref.columns(), conds=CONDS)
+            assert st == rst, (name, st, rst)
+            assert got.equal(ref, upto=st[1]), name
     finally:
         mem.close()
         c.close()
