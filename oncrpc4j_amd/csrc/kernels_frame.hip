@@ -839,6 +839,7 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
         res[4] = sl[1023];      // complete messages
         res[5] = fc;
         res[3] = 0;
+        res[6] = 0;             // k_fr_emit: a message offset off the expected stride
     }
 }
 
@@ -855,8 +856,8 @@ __device__ __forceinline__ void fr_emit_sub(const uint32_t *__restrict__ w, uint
                                             const FrameBase *bases, const uint32_t *fbits, const uint32_t *lbits,
                                             uint64_t cap, int stream_offsets, uint64_t *msg_offsets,
                                             uint64_t *frag_pos, uint64_t *res, uint64_t F, uint64_t M, uint64_t k,
-                                            uint16_t *so, uint32_t (&wsum)[2][2], uint32_t (&wtail)[2],
-                                            uint32_t (&wlo)[2], uint32_t (&whi)[2]) {
+                                            uint64_t stride, uint16_t *so, uint32_t (&wsum)[2][2],
+                                            uint32_t (&wtail)[2], uint32_t (&wlo)[2], uint32_t (&whi)[2]) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t s = k / (kFSuper / kFChunk);
     // every load issued before the first test: the workspace arrays cover the
@@ -926,7 +927,13 @@ __device__ __forceinline__ void fr_emit_sub(const uint32_t *__restrict__ w, uint
     klo = min(wlo[0], wlo[1]);
     khi = max(whi[0], whi[1]);
     const uint64_t vbase = stream_offsets ? B * base : B * base - 4 * fb0;
-    for (uint32_t kk = klo + tid; kk < khi; kk += 128) msg_offsets[lb0 + kk] = vbase + so[kk];
+    bool off_stride = false;   // stride > 0: message m should start at m * stride (the receive's fixed-size decode)
+    for (uint32_t kk = klo + tid; kk < khi; kk += 128) {
+        const uint64_t o = vbase + so[kk];
+        msg_offsets[lb0 + kk] = o;
+        off_stride |= stride && o != (lb0 + kk) * stride;
+    }
+    if (__ballot(off_stride) && lane == 0) atomicOr((unsigned long long *)(res + 6), 1ull);
     __syncthreads();   // so / wsum / wlo free for the block's next sub-chunk
 }
 
@@ -935,7 +942,7 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
                                                   const FrameBase *bases, const uint32_t *fbits,
                                                   const uint32_t *lbits, uint64_t cap, int stream_offsets,
                                                   uint64_t *msg_offsets, uint64_t *frag_pos, uint64_t *res,
-                                                  uint64_t nsub, uint32_t per) {
+                                                  uint64_t nsub, uint32_t per, uint64_t stride) {
     __shared__ uint32_t wsum[2][2], wtail[2], wlo[2], whi[2];
     __shared__ uint16_t so[kFChunk + 1];           // staged message offsets
     const uint64_t r0 = res[0], F = res[1], M = res[4];
@@ -946,7 +953,7 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
     const uint64_t k1 = min(k0 + per, nsub);
     for (uint64_t k = k0; k < k1; ++k)
         fr_emit_sub<B>(w, Q, sub, bases, fbits, lbits, cap, stream_offsets, msg_offsets, frag_pos, res, F, M, k,
-                       so, wsum, wtail, wlo, whi);
+                       stride, so, wsum, wtail, wlo, whi);
 }
 
 // ---------------------------------------------------------------------------
@@ -1017,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_fr_copy(const uint8_t *in, const uint64
 // ---- launchers -------------------------------------------------------------------
 template <int B>
 static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                        uint64_t *msg_offsets, bool frag_list, int emit_per, hipStream_t st) {
+                        uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, hipStream_t st) {
     const uint32_t *w = (const uint32_t *)in;
     const uint32_t Q = frame_positions(len, B), tb = B == 4 ? (uint32_t)(len & 3) : 0u;
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
@@ -1042,15 +1049,15 @@ static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint
     while (per > 1 && nsub / per < 64) per >>= 1;
     hipLaunchKernelGGL(k_fr_emit<B>, dim3((uint32_t)((nsub + per - 1) / per)), dim3(128), 0, st, w, Q, ws.sub,
                        ws.bases, ws.fbits, ws.lbits, cap, stream_offsets ? 1 : 0, msg_offsets,
-                       frag_list ? ws.frag_pos : nullptr, ws.res, (uint64_t)nsub, per);
+                       frag_list ? ws.frag_pos : nullptr, ws.res, (uint64_t)nsub, per, stream_offsets ? stride : 0ull);
     return (int)hipGetLastError();
 }
 
 int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                   uint64_t *msg_offsets, bool frag_list, int emit_per, void *stream) {
-    return B == 1 ? frame_launch<1>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per,
+                   uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream) {
+    return B == 1 ? frame_launch<1>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per, stride,
                                     (hipStream_t)stream)
-                  : frame_launch<4>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per,
+                  : frame_launch<4>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per, stride,
                                     (hipStream_t)stream);
 }
 

@@ -433,7 +433,7 @@ extern "C" int xdrg_ctx_create(int device, uint32_t flags, xdrg_ctx **out) {
     c->device = device;
     c->flags = flags;
     if (hipMalloc(&c->d_stat, 64) != hipSuccess ||
-        hipHostMalloc(&c->h_stat, 64, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&c->h_stat, 128, hipHostMallocDefault) != hipSuccess) {
         if (c->d_stat) (void)hipFree(c->d_stat);
         delete c;
         return XDRG_E_HIP;
@@ -1386,7 +1386,8 @@ static int ring_ready(xdrg_ctx *c, uint64_t slot) {
 
 static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *payload, uint64_t payload_cap,
                       uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs, uint64_t *consumed,
-                      uint64_t *frags, uint64_t *body_bytes);
+                      uint64_t *frags = nullptr, uint64_t *body_bytes = nullptr, uint64_t stride = 0,
+                      bool *uniform = nullptr);
 
 // host_stage.h executor on one context: copies on the ring's H2D / D2H
 // streams, kernels on its compute stream, ordered by per-slot events.
@@ -1837,9 +1838,13 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
 // (at most cap) as stream offsets (payload == NULL) or assembled bodies.
 // One host round trip for xdrg_frame_scan (two for xdrg_deframe: the payload
 // size is checked before the bodies move).
+// stride > 0 (stream offsets): *uniform = every delivered message starts at
+// its index x stride (checked by k_fr_emit as it writes the offsets; the
+// parallel walk only).
 static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *payload, uint64_t payload_cap,
                       uint64_t *msg_offsets, uint64_t cap, uint64_t *n_msgs, uint64_t *consumed,
-                      uint64_t *frags = nullptr, uint64_t *body_bytes = nullptr) {
+                      uint64_t *frags, uint64_t *body_bytes, uint64_t stride, bool *uniform) {
+    if (uniform) *uniform = false;
     if (!c || !msg_offsets || !n_msgs) return XDRG_E_INVAL;
     if (len && !in) return inval(c, "stream is NULL");
     if (len > kFMaxLen) return inval(c, "stream longer than 16 GiB");
@@ -1857,8 +1862,8 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
     bool serial = !aligned(in, 4) || Q == 0;
     if (!serial) {   // parallel walk over words; a real chain meeting a size % 4 != 0 walks again over bytes
         HIPCHK(c, (hipError_t)frame_parallel(in, len, 4, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
-                                             c->tune.emit_per, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 48, hipMemcpyDeviceToHost, c->stream));
+                                             c->tune.emit_per, stride, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 56, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (c->h_stat[2] == kFUnal) {
             if (len < kFByteMaxLen) {
@@ -1866,8 +1871,8 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
                 if (rc) return rc;
                 HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));
                 HIPCHK(c, (hipError_t)frame_parallel(in, len, 1, ws, cap, stream_offsets, msg_offsets,
-                                                     !stream_offsets, c->tune.emit_per, c->stream));
-                HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 48, hipMemcpyDeviceToHost, c->stream));
+                                                     !stream_offsets, c->tune.emit_per, stride, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 56, hipMemcpyDeviceToHost, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
             } else {
                 serial = true;
@@ -1891,6 +1896,7 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
     if (nout == 0) return XDRG_E_INCOMPLETE;   // NextAction STOP (RpcMessageParserTCP.java:51-53)
     *n_msgs = nout;
     if (consumed) *consumed = c->h_stat[2 + 3];
+    if (uniform) *uniform = stride && !serial && c->h_stat[2 + 6] == 0 && c->h_stat[2 + 3] == nout * stride;
     if (payload) {
         const uint64_t nfc = c->h_stat[2 + 5];
         HIPCHK(c, hipMemcpyAsync(c->h_stat + 1, msg_offsets + nout, 8, hipMemcpyDeviceToHost, c->stream));
@@ -1943,11 +1949,18 @@ static int recv_device(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
     *first_bad = 0;
     *err = XDRG_OK;
     uint64_t nm = 0, used = 0, nf = 0;
-    int rc = frame_walk(c, in, len, nullptr, 0, offs, cap, &nm, &used, &nf, nullptr);
+    // fixed-size records: the walk's emit also checks the offsets against the
+    // stride (single-fragment messages back to back decode by the stride
+    // kernels with no separate pass over the offsets, tuning key 29)
+    const uint64_t stride = !s->var_size && c->tune.stride_check ? s->fixed_size + 4 : 0;
+    bool uniform = false;
+    int rc = frame_walk(c, in, len, nullptr, 0, offs, cap, &nm, &used, &nf, nullptr, stride, &uniform);
     if (rc) return rc;   // XDRG_E_INCOMPLETE: STOP
     uint64_t fb = nm;
     int e = XDRG_OK;
-    if (nf == nm) {
+    if (nf == nm && uniform && aligned(in, 4)) {
+        rc = decode_impl(c, s, in, nm * stride, nullptr, nm, cols, XDRG_FRAME_RM, &fb, &e, 0, nullptr);
+    } else if (nf == nm) {
         rc = decode_impl(c, s, in, len, offs, nm, cols, XDRG_FRAME_RM, &fb, &e, 0, nullptr);
     } else {   // multi-fragment messages: bodies assembled behind their offsets in the scratch
         const size_t ob = ((nm + 1) * 8 + 255) & ~(size_t)255;

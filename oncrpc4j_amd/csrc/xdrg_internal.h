@@ -305,8 +305,11 @@ constexpr uint64_t kFByteMaxLen = 1ull << 31;   // byte-mode walks (positions an
 // in ws.res / msg_offsets (stream or payload offsets); the fragment list too
 // when frag_list.  res[0] == kFUnal (word mode only): the real chain met a
 // size % 4 != 0 — walk again in byte mode.
+// stride > 0 (stream offsets): res[6] = 1 when some message does not start at
+// message index x stride (xdrg_receive_batch's fixed-size decode skips its own
+// check of the offsets when none is off)
 int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                   uint64_t *msg_offsets, bool frag_list, int emit_per, void *stream);
+                   uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream);
 int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
                  uint64_t *msg_offsets, void *stream);
 // Bodies of the first nf fragments into payload (marks stripped).
