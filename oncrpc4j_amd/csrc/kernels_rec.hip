@@ -2141,7 +2141,7 @@ __device__ __forceinline__ uint32_t enc_fit(const RecArgs &a, const uint64_t (&b
 // or from the staged tile.
 #ifndef XDRG_ENC_PROBE
 #define XDRG_ENC_PROBE 0   // experiment builds only (wrong output): 1 no byte chunks, 2 no word chunks,
-                           // 4 no fixed fields, 8 no staging copy
+                           // 4 no fixed fields, 8 no staging copy, 16 the prologue only
 #endif
 __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2214,6 +2214,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
         }
         return;
     }
+    if (XDRG_ENC_PROBE & 16) return;   // (experiment builds: the prologue only)
     uint8_t *const out = a.xdr + bbase;   // block-relative stream
     // ---- sub-batches
     uint32_t js = 0;
