@@ -460,6 +460,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a
 // block copies the image out with 16-byte stores.  Same words as
 // g_enc_record (jrpcgen.java:835-906 counts / list bools, Xdr.java:765-800).
 constexpr uint32_t kEncElCap = 1024;   // elements per sub-batch
+constexpr uint16_t kNoOwner = 0xffff;   // an element of a record whose group is absent
 __host__ __device__ constexpr size_t enc_el_lds_bytes(uint32_t img) {
     return (size_t)(kRecPerBlock + 1) * 8 + (size_t)(kEncElCap + 1) * 4 + (size_t)kRecPerBlock * 4 +
            (size_t)kEncElCap * 2 + (size_t)(kRecPerBlock + 1) * 2 + 16 + img;
@@ -481,14 +482,17 @@ __device__ __forceinline__ uint32_t g_lay_elem_bytes(const GroupArgs &a, const G
     return (uint32_t)z;
 }
 // Element e of group g into the image at p (its list bool, then every member)
+template <bool COND>
 __device__ __forceinline__ void g_enc_elem_img(const GroupArgs &a, uint32_t g, uint64_t e, uint8_t *img, uint32_t p) {
     const GField &G = a.f[g];
     if (G.kind == XDRG_K_LIST) {   // xdrEncodeBoolean(true) (pmaplist.java:65-67)
         g_st_img(img, p, bswap32r(1u));
         p += 4;
     }
+    GDisc d{};   // (a member's condition names an earlier member of its element)
     for (uint32_t j = 1; j <= G.nmem; ++j) {
         const GField &m = a.f[g + j];
+        if (COND && G.ncm && !g_enc_field_present(a, g + j, e, d)) continue;   // an element's absent arm
         if (m.kind != XDRG_K_DYNAMIC) {
             for (uint32_t w = 0; w < m.xbytes >> 2; ++w) g_st_img(img, p + 4 * w, g_fixed_word(m, e, w));
             p += m.xbytes;
@@ -504,6 +508,7 @@ __device__ __forceinline__ void g_enc_elem_img(const GroupArgs &a, uint32_t g, u
 // Record r's own words into the image at p (its mark, top-level fields, the
 // group's count and list end); returns the image offset of its first element
 // (its elements take gbytes there).
+template <bool COND>
 __device__ __forceinline__ uint32_t g_enc_top_img(const GroupArgs &a, uint64_t r, uint8_t *img, uint32_t p,
                                                   uint64_t size, uint32_t gbytes) {
     uint32_t first = p;
@@ -511,8 +516,13 @@ __device__ __forceinline__ uint32_t g_enc_top_img(const GroupArgs &a, uint64_t r
         g_st_img(img, p, bswap32r((uint32_t)(size - 4) | kLastFrag));
         p += 4;
     }
+    GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
         const GField &f = a.f[k];
+        if (COND && !g_enc_field_present(a, k, r, d)) {   // the record's absent arm / optional value
+            k += f.type == XDRG_T_GROUP ? 1 + f.nmem : 1;
+            continue;
+        }
         if (f.type == XDRG_T_GROUP) {
             uint64_t e0, cnt;
             g_range(f, r, e0, cnt);
@@ -543,6 +553,7 @@ __device__ __forceinline__ uint32_t g_enc_top_img(const GroupArgs &a, uint64_t r
     }
     return first;
 }
+template <bool COND>   // COND: the schema has conditional fields
 __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *soff = (uint64_t *)smem;                       // [RPB + 1] record offsets in the stream
@@ -573,8 +584,9 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArg
     if (a.rec_out && blockIdx.x == 0 && tid == 0) a.rec_out[a.n] = total;
     __syncthreads();
     const uint32_t nrec = (uint32_t)(a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock);
-    const uint32_t g = a.lay_g - 1;
+    const uint32_t g = a.el_g;
     const GField &G = a.f[g];
+    const bool lay = a.lay_g == g + 1;   // (no conditional member: every element has the layout)
     auto gfirst = [&](uint32_t j) -> uint64_t {   // the group's first element of block record j (j <= nrec)
         const uint64_t r = rb + j;
         return G.kind == XDRG_K_FIXED ? r * G.count : G.offsets[r];
@@ -595,17 +607,38 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArg
         const uint32_t je = js + k1, m = k1;
         const uint64_t E0 = gfirst(js);
         const uint32_t nel = (uint32_t)(gfirst(je) - E0);
-        for (uint32_t t = tid; t <= m; t += kRecThreads) fj[t] = (uint16_t)(gfirst(js + t) - E0);
+        // record lanes: the first element and the element owner map; an element
+        // of a record whose group is absent (its arm / optional value not
+        // taken) is owned by no record (kNoOwner) and writes nothing
+        for (uint32_t t = tid; t < m; t += kRecThreads) {
+            const uint32_t f0 = (uint32_t)(gfirst(js + t) - E0), f1 = (uint32_t)(gfirst(js + t + 1) - E0);
+            bool gp = true;
+            if (COND) {   // the top-level fields up to the group, for its condition
+                GDisc d{};
+                for (uint32_t k = 0; k <= g;) {
+                    const GField &f = a.f[k];
+                    const bool p = g_enc_field_present(a, k, rb + js + t, d);
+                    if (k == g) { gp = p; break; }
+                    k += f.type == XDRG_T_GROUP ? 1 + f.nmem : 1;
+                }
+            }
+            fj[t] = (uint16_t)f0;
+            for (uint32_t i = f0; i < f1; ++i) own[i] = gp ? (uint16_t)t : kNoOwner;
+        }
+        if (tid == 0) fj[m] = (uint16_t)nel;
+        __syncthreads();
         // element sizes, four consecutive elements per lane, placed by a block scan
         uint32_t z[4], zs = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t i = 4 * tid + u;
-            z[u] = i < nel ? g_lay_elem_bytes(a, G, E0 + i) : 0u;
+            z[u] = 0;
+            if (i < nel && own[i] != kNoOwner)
+                z[u] = lay ? g_lay_elem_bytes(a, G, E0 + i) : (uint32_t)g_elem_bytes<1>(a, g, E0 + i, GDisc{});
             zs += z[u];
         }
         uint64_t ztot;
-        uint32_t x = (uint32_t)block_excl_scan(zs, &ztot);   // (its barriers publish fj)
+        uint32_t x = (uint32_t)block_excl_scan(zs, &ztot);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const uint32_t i = 4 * tid + u;
@@ -613,20 +646,18 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArg
             x += z[u];
         }
         if (tid == 0) xs[nel] = (uint32_t)ztot;
-        for (uint32_t t = tid; t < m; t += kRecThreads)
-            for (uint32_t i = fj[t]; i < fj[t + 1]; ++i) own[i] = (uint16_t)t;
         __syncthreads();
         // record lanes: their own words; the image starts at record js
         const uint64_t ib = soff[js];
         for (uint32_t t = tid; t < m; t += kRecThreads) {
             const uint32_t j = js + t;
-            rst[t] = g_enc_top_img(a, rb + j, img, (uint32_t)(soff[j] - ib), soff[j + 1] - soff[j],
+            rst[t] = g_enc_top_img<COND>(a, rb + j, img, (uint32_t)(soff[j] - ib), soff[j + 1] - soff[j],
                                    xs[fj[t + 1]] - xs[fj[t]]);
         }
         __syncthreads();
         for (uint32_t i = tid; i < nel; i += kRecThreads) {
             const uint32_t t = own[i];
-            g_enc_elem_img(a, g, E0 + i, img, rst[t] + xs[i] - xs[fj[t]]);
+            if (t != kNoOwner) g_enc_elem_img<COND>(a, g, E0 + i, img, rst[t] + xs[i] - xs[fj[t]]);
         }
         __syncthreads();
         // the image out: dwords up to a 16-byte boundary, 16-byte stores, dwords
@@ -1423,7 +1454,8 @@ static void launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) 
     switch (phase) {
     case GRP_ENC_SIZES: hipLaunchKernelGGL(k_grp_enc_sizes<NEST>, grid, block, 0, st, a); break;
     case GRP_ENC_PLACE:   // element-parallel (key 41) or G lanes per record (key 32)
-        if (!NEST && a.enc_img) hipLaunchKernelGGL(k_grp_enc_place_el, grid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        if (!NEST && a.enc_img && a.ncond) hipLaunchKernelGGL(k_grp_enc_place_el<true>, grid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (!NEST && a.enc_img) hipLaunchKernelGGL(k_grp_enc_place_el<false>, grid, block, enc_el_lds_bytes(a.enc_img), st, a);
         else if (a.enc_lanes == 4) hipLaunchKernelGGL((k_grp_enc_place<4, NEST>), grid, block, 0, st, a);
         else if (a.enc_lanes == 8) hipLaunchKernelGGL((k_grp_enc_place<8, NEST>), grid, block, 0, st, a);
         else if (a.enc_lanes == 16) hipLaunchKernelGGL((k_grp_enc_place<16, NEST>), grid, block, 0, st, a);

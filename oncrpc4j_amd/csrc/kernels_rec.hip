@@ -1357,24 +1357,6 @@ __device__ __forceinline__ void dec_place_g_block(const RecArgs &a, uint64_t bid
     if (nrec > kRecPerBlock) nrec = kRecPerBlock;
     const uint8_t *in = a.xdr;
     const uint32_t tid = threadIdx.x;
-    if (a.payk && a.pay_heads) {   // k_dec_payload decodes these records whole: head words, payload, tail words
-        const uint32_t kp = a.dyn_idx[a.payk - 1];   // the one dynamic field
-        const uint64_t hb = a.pay_fb - (a.framed ? 4 : 0);   // its offset after the mark
-        for (uint32_t j = tid; j < nrec; j += kRecThreads) {
-            const uint32_t up = supto[j];
-            a.pay_pos[rb + j] = up == a.nf ? sstart[j] + hb : ~0ull;
-            if (up == 0 || up == a.nf) continue;
-            // a record whose payload did not fit the native column (CAPACITY):
-            // the fields before it are decoded here, a lane per record (rare)
-            uint64_t q = sstart[j];
-            for (uint32_t k = 0; k < kp; ++k) {
-                const VField &f = a.f[k];
-                for (uint32_t i = 0; i < f.xbytes >> 2; ++i) fixed_store(f, rb + j, 4 * i, *(const uint32_t *)(in + q + 4 * i));
-                q += f.xbytes;
-            }
-        }
-        return;
-    }
     uint64_t fixed_delta = 0;
     uint32_t d = 0, k = 0;
     {   // The fixed fields before the first dynamic one (config 3's head words):
@@ -1623,28 +1605,9 @@ __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
     uint8_t *dst = f.data + o;
     constexpr uint32_t LPR = kPayLanes;
     const uint32_t lane = threadIdx.x % LPR;
-    // The record's fixed fields, a word per lane (the group kernel only placed
-    // the record): the head words before the length word and the tail words
-    // after the payload and its pad (Xdr.java:171-175 each; the walk has
-    // checked every length and bound in the reference's order).  Their loads
-    // go out with the first payload loads and are stored after them, so a
-    // wave's record costs one memory round trip, not two.
-    const uint32_t hw = (uint32_t)(a.pay_fb - (a.framed ? 4 : 0)) >> 2;
-    const uint32_t nfw = hw + ((a.fixed_xdr - a.pay_fb) >> 2);
-    const uint64_t h0 = pos - 4 * (uint64_t)hw, t0 = pos + 4 + cnt + pad4(cnt);
-    auto fixed_at = [&](uint32_t i) { return *(const uint32_t *)(a.xdr + (i < hw ? h0 + 4 * (uint64_t)i : t0 + 4 * (uint64_t)(i - hw))); };
-    auto fixed_put = [&](uint32_t i, uint32_t v) {
-        uint32_t w = i;   // fixed-field word index, declaration order
-        for (uint32_t k = 0; k < a.nf; ++k) {
-            const VField &g = a.f[k];
-            if (g.kind == XDRG_K_DYNAMIC) continue;
-            const uint32_t nw = g.xbytes >> 2;
-            if (w < nw) fixed_store(g, r, 4 * w, v);
-            w = w < nw ? ~0u >> 1 : w - nw;   // (stored: past every later field)
-        }
-    };
-    const bool hl = a.pay_heads && lane < nfw;   // (key 39 = 0: the group kernel stored them)
-    const uint32_t hv = hl ? fixed_at(lane) : 0u;
+    // (the record's fixed fields are the group kernel's, k_dec_place_g: a wave
+    // per record writing its six head words measured slower, 29.1 vs 25.2 ms
+    // on config 3)
     const uint64_t nch = (cnt + 15) >> 4;
     for (uint64_t c0 = lane; c0 < nch; c0 += 4 * LPR) {
         u32x4a v[4];
@@ -1670,8 +1633,6 @@ __device__ __forceinline__ void dec_payload_rec(const RecArgs &a, uint64_t r) {
             }
         }
     }
-    if (hl) fixed_put(lane, hv);
-    for (uint32_t i = lane + LPR; a.pay_heads && i < nfw; i += LPR) fixed_put(i, fixed_at(i));   // > 64 fixed words
 }
 __global__ __launch_bounds__(256) void k_dec_payload(const RecArgs a) {
     const uint64_t step = (uint64_t)gridDim.x * (256 / kPayLanes);
@@ -3154,7 +3115,6 @@ int launch_rec_phase(const RecArgs &args, int phase, const Tuning &t, void *stre
     a.tile_bytes = t.tile_bytes;
     a.big_rec = 0;
     a.xcd = (uint32_t)t.xcd_order;
-    a.pay_heads = (uint32_t)t.pay_heads;
     hipStream_t st = (hipStream_t)stream;
     const uint64_t nb = a.nblocks;
     // conditional schemas (unions / optional data) and by-reference payloads take

@@ -387,7 +387,6 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 36: if (!in(1, 64)) return -1; t.emit_per = (int32_t)v; return 0;
     case 37: if (!in(0, 3)) return -1; t.xcd_order = (int32_t)v; return 0;
     case 38: if (v && !in(64, 4096)) return -1; t.grp_dec_el = (int32_t)v; return 0;
-    case 39: if (!in(0, 1)) return -1; t.pay_heads = (int32_t)v; return 0;
     case 41: if (v && (!in(4096, 49152) || (v & 15))) return -1; t.grp_enc_img = (int32_t)v; return 0;
     default: return -1;
     }
@@ -786,8 +785,13 @@ static int group_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *co
     int rc = fill_group(c, s, cols, n, framed, false, a);
     if (rc) return rc;
     a.enc_lanes = (uint32_t)c->tune.grp_enc_lanes;
-    // the element-parallel place: a group with a layout, no conditional field
-    if (c->tune.grp_enc_img && a.lay_g && !s->ncond) a.enc_img = (uint32_t)c->tune.grp_enc_img;
+    // the element-parallel place: one top-level group without inner groups
+    if (c->tune.grp_enc_img && s->ngroups == 1 && !a.nest)
+        for (uint32_t k = 0; k < a.nf; ++k)
+            if (a.f[k].type == XDRG_T_GROUP && !a.f[k].grp && !a.f[k].ngm) {
+                a.enc_img = (uint32_t)c->tune.grp_enc_img;
+                a.el_g = k;
+            }
     a.xdr = out;
     a.xdr_cap = out_cap;
     a.rec_out = rec_offsets;

@@ -139,8 +139,6 @@ struct RecArgs {
     uint32_t payk;             // 0, or 1 + the dynamic byte field the payload kernels move for the
                                // group kernels' blocks (k_enc/dec_payload)
     uint32_t pay_fb;           // payk: XDR bytes before that field in a record (mark + fixed fields)
-    uint32_t pay_heads;        // decode, payk: 1 k_dec_payload also stores the record's fixed fields,
-                               // 0 the group kernel stores them (tuning key 39)
     uint64_t *pay_pos;         // payk: per record, stream offset of that field's length word
                                // (decode: ~0 = not to be written)
     uint32_t *spec;            // decode, extent-derived counts (spec_mode != 0): ~0 = the derived
@@ -198,10 +196,6 @@ struct Tuning {
     int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of
                                     // records (0: each lane walks its record in HBM)
     int32_t grp_enc_lanes = 8;      // key 32: repeated-group encode, lanes per record (64 = a wave)
-    int32_t pay_heads = 0;          // key 39: config-3-shaped decode, the fixed fields of payload records:
-                                    // 0 stored by the group kernel (23.4 ms on config 3), 1 by the payload
-                                    // kernel's wave with the payload (29.1 ms: a wave per record writes
-                                    // its 6 head words as scattered dwords), DESIGN.md §5.0b
     int32_t grp_enc_img = 16384;    // key 41: repeated-group encode place element-parallel through an LDS
                                     // image of this many bytes (schemas without conditional fields whose
                                     // group has a layout; 0: lanes per record, key 32).  DUMP encode 2.19 ->

@@ -112,18 +112,9 @@ def _decode(ctx, sh, out, total, ro, framed):
     return (rc, fb, err), hb, dyn
 
 
-@pytest.fixture(params=[0, 1], ids=["heads_grp", "heads_pay"])
-def pay_heads(request, gpu_ctx):
-    """Config-3 decode: the fixed fields of payload records stored by the
-    group kernel (key 39 = 0, the default) or by the payload kernel."""
-    gpu_ctx.tune(39, request.param)
-    yield request.param
-    gpu_ctx.tune(0)
-
-
 @pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("cfg,n", [(3, 32 << 10), (4, 128 << 10)], ids=["cfg3", "cfg4"])
-def test_exact_shape_vs_oracle(gpu_ctx, pay_heads, cfg, n, framed):
+def test_exact_shape_vs_oracle(gpu_ctx, cfg, n, framed):
     sh = Shape(cfg, n, seed=0x0DCAC4E5 + cfg)
     out, ro, total = _encode(gpu_ctx, sh, framed)
     hbatch = sh.host_records(np.arange(n))

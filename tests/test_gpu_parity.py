@@ -48,11 +48,9 @@ SCHEMAS = {
 # the exact walk instead of derived counts (key 31 = 0, the fallback the
 # derived counts rerun), "staged_lean" the record-group staged decode that
 # schemas of 3-4 dynamic fields take (key 20 = 1), "group" the group kernels
-# for every block (key 9 = 0), "group_payheads" the same with the payload
-# kernel storing a payload record's fixed fields (key 39 = 1).  Tests taking
-# `rec_kernel` run under each.
+# for every block (key 9 = 0).  Tests taking `rec_kernel` run under each.
 REC_KERNELS = {"staged": ((9, 4),), "staged_walk": ((9, 4), (31, 0)), "staged_lean": ((9, 4), (20, 1)),
-               "group": ((9, 0),), "group_payheads": ((9, 0), (39, 1))}
+               "group": ((9, 0),)}
 
 
 @pytest.fixture(params=sorted(REC_KERNELS), ids=str)

@@ -223,7 +223,7 @@ def enc_lanes(request, gpu_ctx):
     gpu_ctx.tune(32, request.param[0])
     gpu_ctx.tune(33, request.param[1])
     gpu_ctx.tune(38, request.param[2])   # element-parallel place (one top-level group)
-    gpu_ctx.tune(41, request.param[3])   # element-parallel encode (layout groups, no conditional fields)
+    gpu_ctx.tune(41, request.param[3])   # element-parallel encode (one top-level group without inner groups)
     yield request.param
     gpu_ctx.tune(0)
 
