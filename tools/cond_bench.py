@@ -58,6 +58,10 @@ def discriminants(fields, conds, hb, rng):
 
 
 def run(name, fields, conds, n, dyn_len, group_len=(0, 4)):
+    # XDRG_SHAPES=plus,chunk: only the shapes whose name holds one of these (profiling runs)
+    want = [w.lower() for w in os.environ.get("XDRG_SHAPES", "").split(",") if w]
+    if want and not any(w in name.lower() for w in want):
+        return {"shape": name, "skipped": True}
     ctx = engine.Context(0)
     ctx.apply_tuning(os.environ.get("XDRG_TUNE"))   # measurement runs only
     ctx.set_stream(torch.cuda.current_stream())
