@@ -25,6 +25,12 @@
 
 namespace xdrg {
 
+// A field-table index every live lane of the wave holds (the walks step
+// through the schema in lockstep; only the number of elements differs):
+// said so to the compiler, the table is read with scalar loads instead of a
+// vector load in every member's dependent chain.
+__device__ __forceinline__ uint32_t g_uni(uint32_t k) { return __builtin_amdgcn_readfirstlane(k); }
+
 typedef uint32_t u32g __attribute__((aligned(1)));
 typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));   // 16-byte aligned
 
@@ -189,10 +195,12 @@ template <int L>
 __device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g, uint64_t row, GDisc &d);
 template <int L>
 __device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g, uint64_t e, GDisc d) {
+    g = g_uni(g);
     const GField &G = a.f[g];
     if (!G.ncm && !G.ngm) {
         uint64_t s = G.efix;
         for (uint32_t j = 1; j <= G.nmem; ++j) {
+            j = g_uni(j);
             const GField &m = a.f[g + j];
             if (m.kind == XDRG_K_DYNAMIC) s += g_dyn_bytes(m, m.offsets[e + 1] - m.offsets[e]);
         }
@@ -200,6 +208,7 @@ __device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g,
     }
     uint64_t s = G.kind == XDRG_K_LIST ? 4 : 0;
     for (uint32_t j = 1; j <= G.nmem; ++j) {
+        j = g_uni(j);
         const GField &m = a.f[g + j];
         const bool p = !G.ncm || g_enc_field_present(a, g + j, e, d);
         if (m.type == XDRG_T_GROUP) {
@@ -218,6 +227,7 @@ __device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g,
 // of the enclosing group): its count / closing bool and every element.
 template <int L>
 __device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g, uint64_t row, GDisc &d) {
+    g = g_uni(g);
     const GField &G = a.f[g];
     uint64_t e0, cnt;
     g_range(G, row, e0, cnt);
@@ -258,6 +268,7 @@ __device__ __forceinline__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
     uint64_t s = a.framed ? 4 : 0;
     GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
+        k = g_uni(k);
         const GField &f = a.f[k];
         if (!g_enc_field_present(a, k, r, d)) {   // an absent field / array / list writes nothing
             k += f.type == XDRG_T_GROUP ? 1 + f.nmem : 1;
@@ -295,12 +306,14 @@ __device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, 
 template <int L>
 __device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t p, GDisc d) {
     uint8_t *out = a.xdr;
+    g = g_uni(g);
     const GField &G = a.f[g];
     if (G.kind == XDRG_K_LIST) {   // xdrEncodeBoolean(true) (pmaplist.java:65-67)
         *(uint32_t *)(out + p) = bswap32r(1u);
         p += 4;
     }
     for (uint32_t j = 1; j <= G.nmem; ++j) {
+        j = g_uni(j);
         const GField &m = a.f[g + j];
         const bool present = !G.ncm || g_enc_field_present(a, g + j, e, d);   // an element's absent arm
         if (m.type == XDRG_T_GROUP) {   // an inner array / list: this lane writes it whole
@@ -328,6 +341,7 @@ __device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint32_t g, u
 template <int L>
 __device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, uint64_t row, uint64_t p, GDisc &d) {
     uint8_t *out = a.xdr;
+    g = g_uni(g);
     const GField &G = a.f[g];
     uint64_t e0, cnt;
     g_range(G, row, e0, cnt);
@@ -369,6 +383,7 @@ __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint6
     }
     GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
+        k = g_uni(k);
         const GField &f = a.f[k];
         if (!g_enc_field_present(a, k, r, d)) {   // the record's absent arm / optional value
             k += f.type == XDRG_T_GROUP ? 1 + f.nmem : 1;
@@ -484,6 +499,7 @@ __device__ __forceinline__ uint32_t g_lay_elem_bytes(const GroupArgs &a, const G
 // Element e of group g into the image at p (its list bool, then every member)
 template <bool COND>
 __device__ __forceinline__ void g_enc_elem_img(const GroupArgs &a, uint32_t g, uint64_t e, uint8_t *img, uint32_t p) {
+    g = g_uni(g);
     const GField &G = a.f[g];
     if (G.kind == XDRG_K_LIST) {   // xdrEncodeBoolean(true) (pmaplist.java:65-67)
         g_st_img(img, p, bswap32r(1u));
@@ -491,6 +507,7 @@ __device__ __forceinline__ void g_enc_elem_img(const GroupArgs &a, uint32_t g, u
     }
     GDisc d{};   // (a member's condition names an earlier member of its element)
     for (uint32_t j = 1; j <= G.nmem; ++j) {
+        j = g_uni(j);
         const GField &m = a.f[g + j];
         if (COND && G.ncm && !g_enc_field_present(a, g + j, e, d)) continue;   // an element's absent arm
         if (m.kind != XDRG_K_DYNAMIC) {
@@ -518,6 +535,7 @@ __device__ __forceinline__ uint32_t g_enc_top_img(const GroupArgs &a, uint64_t r
     }
     GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
+        k = g_uni(k);
         const GField &f = a.f[k];
         if (COND && !g_enc_field_present(a, k, r, d)) {   // the record's absent arm / optional value
             k += f.type == XDRG_T_GROUP ? 1 + f.nmem : 1;
@@ -725,6 +743,7 @@ __device__ __forceinline__ uint32_t g_walk_dyn(const GField &f, const uint8_t *i
 template <int L>
 __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t end, uint64_t &pos,
                                  uint32_t (&cnt)[kMaxSlots], GDisc &d) {
+    g = g_uni(g);
     const GField &f = a.f[g];
     uint64_t n;
     if (f.kind == XDRG_K_DYNAMIC) {   // int $size = xdr.xdrDecodeInt(); new T[$size]
@@ -785,6 +804,7 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
                 break;
             }
             for (uint32_t j = 1; j <= f.nmem; ++j) {
+                j = g_uni(j);
                 const GField &m = a.f[g + j];
                 const bool present = !f.ncm || g_dec_field_present(a, g + j, in, pos, end, d);
                 if (m.type == XDRG_T_GROUP) {   // an inner array / list of this element
@@ -830,6 +850,7 @@ __device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint3
     }
     GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
+        k = g_uni(k);   // (every live lane is at the same field: scalar field-table loads)
         const GField &f = a.f[k];
         *sub = 2 * k + 1;
         if (!g_dec_field_present(a, k, in, pos, e.b, d)) {   // absent: nothing on the wire
@@ -978,6 +999,7 @@ __device__ __forceinline__ void g_run_init(const GroupArgs &a, uint32_t k, uint6
     for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;
     const GField &f = a.f[k];
     for (uint32_t j = 1; j <= f.nmem; ++j) {
+        j = g_uni(j);
         const GField &m = a.f[k + j];
         if (!m.slot) continue;
         const uint64_t b0 = g_rec_base(a, m.slot, r);
@@ -995,8 +1017,10 @@ __device__ __forceinline__ void g_run_init(const GroupArgs &a, uint32_t k, uint6
 // elements): fixed members zero, dynamic members and inner arrays empty.
 template <int L>
 __device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, uint64_t e, GRun &run) {
+    g = g_uni(g);
     const GField &G = a.f[g];
     for (uint32_t j = 1; j <= G.nmem; ++j) {
+        j = g_uni(j);
         const GField &m = a.f[g + j];
         if (m.type == XDRG_T_GROUP) {
             if constexpr (L == 0) {
@@ -1018,6 +1042,7 @@ __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint6
 // count word or list bools, read as the walk checked them, then its elements.
 __device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in,
                                             uint64_t &pos, uint64_t end, GDisc &d, GRun &run) {
+    g = g_uni(g);
     const GField &G = a.f[g];
     const uint64_t i0 = G.kind == XDRG_K_FIXED ? e * G.count : run.get(G.slot);
     uint64_t n = G.count;
@@ -1046,8 +1071,10 @@ __device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint
 template <int L>
 __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in, uint64_t &pos,
                            uint64_t end, GDisc &d, GRun &run) {
+    g = g_uni(g);
     const GField &f = a.f[g];
     for (uint32_t j = 1; j <= f.nmem; ++j) {
+        j = g_uni(j);
         const GField &m = a.f[g + j];
         const bool present = !f.ncm || g_dec_field_present(a, g + j, in, pos, end, d);   // an element's absent arm
         if (m.type == XDRG_T_GROUP) {
@@ -1088,12 +1115,14 @@ __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint6
 // record walk): pos past the element, run past its dynamic members.
 __device__ __forceinline__ void g_elem_skip(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t &pos,
                                             uint64_t end, GDisc &d, GRun &run) {
+    g = g_uni(g);
     const GField &f = a.f[g];
     if (!f.ndm && !f.ncm) {   // elements of one size (a list's TRUE is already past)
         pos += f.efix - (f.kind == XDRG_K_LIST ? 4 : 0);
         return;
     }
     for (uint32_t j = 1; j <= f.nmem; ++j) {
+        j = g_uni(j);
         const GField &m = a.f[g + j];
         if (f.ncm && !g_dec_field_present(a, g + j, in, pos, end, d)) continue;
         if (m.kind != XDRG_K_DYNAMIC) {
@@ -1151,6 +1180,7 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
     uint64_t pos = ex.a + (a.framed ? 4 : 0) - base;
     GDisc d{};
     for (uint32_t k = 0; k < a.nf;) {
+        k = g_uni(k);
         const GField &f = a.f[k];
         if (!g_dec_field_present(a, k, in, pos, end, d)) {
             if (f.type != XDRG_T_GROUP) {
@@ -1375,6 +1405,7 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
     el.ms0 = el.ms1 = el.mk0 = el.mk1 = 0;
     el.sb0 = el.sb1 = 0;
     for (uint32_t j = 1; j <= G.nmem; ++j) {
+        j = g_uni(j);
         if (a.f[g + j].kind != XDRG_K_DYNAMIC) continue;
         if (el.nm == 0) { el.ms0 = a.f[g + j].slot; el.mk0 = g + j; }
         else { el.ms1 = a.f[g + j].slot; el.mk1 = g + j; }
