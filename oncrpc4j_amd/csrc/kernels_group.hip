@@ -285,11 +285,27 @@ __device__ __forceinline__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
     return s;
 }
 
+// The walk (and the encode sizes pass) is a dependent chain of loads per
+// record: kWalkSplit blocks share
+// one scan block's kRecPerBlock records (fewer records per lane, more waves
+// in flight), and add their totals into its block_sums entry (zeroed first).
+// One record per lane (4) against four (1), decode / encode ms
+// (`profiles/r04_groups/walk_split_ab.jsonl`): READDIRPLUS 1.40 -> 1.23 /
+// 1.81 -> 1.67, chunk_map 3.04 -> 2.75 / 1.89 -> 1.77, volume_index 2.80 ->
+// 2.67 / 1.77 -> 1.65, DUMP 1.13 -> 1.06, READDIR 2.33 -> 2.25 / 2.61 -> 2.49.
+#ifndef XDRG_WALK_SPLIT
+#define XDRG_WALK_SPLIT 4
+#endif
+constexpr int kWalkSplit = XDRG_WALK_SPLIT;
+static_assert(kRecPerThread % kWalkSplit == 0, "records per lane");
 template <bool NEST>
 __global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a) {
-    const uint64_t r0 = (uint64_t)blockIdx.x * kRecPerBlock + (uint64_t)threadIdx.x * kRecPerThread;
+    constexpr int per = kRecPerThread / kWalkSplit;
+    const uint64_t blk = blockIdx.x / kWalkSplit;
+    const uint64_t r0 = blk * kRecPerBlock + (uint64_t)(blockIdx.x % kWalkSplit) * (kRecPerBlock / kWalkSplit) +
+                        (uint64_t)threadIdx.x * per;
     uint64_t s = 0;
-    for (int j = 0; j < kRecPerThread; ++j) {
+    for (int j = 0; j < per; ++j) {
         const uint64_t r = r0 + j;
         if (r >= a.n) break;
         const uint64_t z = g_rec_size<NEST>(a, r);
@@ -297,7 +313,10 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a
         s += z;
     }
     const uint64_t tot = block_sum(s);
-    if (threadIdx.x == 0) a.block_sums[blockIdx.x] = tot;
+    if (threadIdx.x == 0) {
+        if (kWalkSplit == 1) a.block_sums[blk] = tot;
+        else atomicAdd((unsigned long long *)&a.block_sums[blk], (unsigned long long)tot);
+    }
 }
 
 // One lane writes element e of group g at stream byte p; returns its end.
@@ -879,10 +898,13 @@ __device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint3
 
 template <bool NEST>
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a) {
-    const uint64_t r0 = (uint64_t)blockIdx.x * kRecPerBlock + (uint64_t)threadIdx.x * kRecPerThread;
+    constexpr int per = kRecPerThread / kWalkSplit;
+    const uint64_t blk = blockIdx.x / kWalkSplit;
+    const uint64_t r0 = blk * kRecPerBlock + (uint64_t)(blockIdx.x % kWalkSplit) * (kRecPerBlock / kWalkSplit) +
+                        (uint64_t)threadIdx.x * per;
     uint64_t sums[kMaxSlots];
     for (uint32_t s = 0; s < a.nslot; ++s) sums[s] = 0;
-    for (int j = 0; j < kRecPerThread; ++j) {
+    for (int j = 0; j < per; ++j) {
         const uint64_t r = r0 + j;
         if (r >= a.n) break;
         uint32_t cnt[kMaxSlots];
@@ -900,7 +922,10 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a)
     }
     for (uint32_t s = 0; s < a.nslot; ++s) {
         const uint64_t tot = block_sum(sums[s]);
-        if (threadIdx.x == 0) a.block_sums[(uint64_t)s * a.nblocks + blockIdx.x] = tot;
+        if (threadIdx.x == 0) {
+            if (kWalkSplit == 1) a.block_sums[(uint64_t)s * a.nblocks + blk] = tot;
+            else atomicAdd((unsigned long long *)&a.block_sums[(uint64_t)s * a.nblocks + blk], (unsigned long long)tot);
+        }
     }
 }
 
@@ -1479,11 +1504,17 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
 // the others keep kernels with the inner-group code compiled out (their
 // running offsets stay in registers).
 template <bool NEST>
-static void launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) {
+static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) {
     const dim3 grid((uint32_t)a.nblocks), block(kRecThreads);
     const dim3 rgrid((uint32_t)((a.n + kRecThreads - 1) / kRecThreads));
     switch (phase) {
-    case GRP_ENC_SIZES: hipLaunchKernelGGL(k_grp_enc_sizes<NEST>, grid, block, 0, st, a); break;
+    case GRP_ENC_SIZES:
+        if (kWalkSplit > 1) {
+            const hipError_t e = hipMemsetAsync(a.block_sums, 0, (size_t)a.nblocks * 8, st);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_grp_enc_sizes<NEST>, dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
+        break;
     case GRP_ENC_PLACE:   // element-parallel (key 41) or G lanes per record (key 32)
         if (!NEST && a.enc_img && a.ncond) hipLaunchKernelGGL(k_grp_enc_place_el<true>, grid, block, enc_el_lds_bytes(a.enc_img), st, a);
         else if (!NEST && a.enc_img) hipLaunchKernelGGL(k_grp_enc_place_el<false>, grid, block, enc_el_lds_bytes(a.enc_img), st, a);
@@ -1493,7 +1524,13 @@ static void launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) 
         else if (a.enc_lanes == 32) hipLaunchKernelGGL((k_grp_enc_place<32, NEST>), grid, block, 0, st, a);
         else hipLaunchKernelGGL((k_grp_enc_place<64, NEST>), grid, block, 0, st, a);
         break;
-    case GRP_DEC_WALK: hipLaunchKernelGGL(k_grp_dec_walk<NEST>, grid, block, 0, st, a); break;
+    case GRP_DEC_WALK:
+        if (kWalkSplit > 1 && a.nslot) {
+            const hipError_t e = hipMemsetAsync(a.block_sums, 0, (size_t)a.nslot * a.nblocks * 8, st);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_grp_dec_walk<NEST>, dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
+        break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
     case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
         if (!NEST && a.dec_el && a.dec_tile) {
@@ -1506,13 +1543,14 @@ static void launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) 
         break;
     default: break;
     }
+    return hipSuccess;
 }
 
 int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
     if (phase < GRP_ENC_SIZES || phase > GRP_DEC_PLACE) return (int)hipErrorInvalidValue;
-    if (a.nest) launch_group_phase_t<true>(a, phase, (hipStream_t)stream);
-    else launch_group_phase_t<false>(a, phase, (hipStream_t)stream);
-    return (int)hipGetLastError();
+    const hipError_t e = a.nest ? launch_group_phase_t<true>(a, phase, (hipStream_t)stream)
+                                : launch_group_phase_t<false>(a, phase, (hipStream_t)stream);
+    return (int)(e != hipSuccess ? e : hipGetLastError());
 }
 
 }  // namespace xdrg
