@@ -590,7 +590,14 @@ __device__ __forceinline__ uint32_t g_enc_top_img(const GroupArgs &a, uint64_t r
     }
     return first;
 }
-template <bool COND>   // COND: the schema has conditional fields
+// Small batches: gridDim.x / nblocks (1, 2 or 4, enc_el_split) blocks share a
+// scan block's records; each scans all of its sizes (the offsets need them)
+// and composes its own share.  512 Ki READDIRPLUS replies are 512 scan
+// blocks, two per CU: two blocks per scan block take their encode place from
+// 1.68 to 1.11 ms; batches of 1,024 scan blocks and more lose 1-3 % when split
+// (`profiles/r04_groups/enc_el_split_ab.jsonl`), so they are not.
+__host__ __device__ inline uint32_t enc_el_split(uint64_t nblocks) { return nblocks >= 1024 ? 1u : nblocks >= 512 ? 2u : 4u; }
+template <bool COND, bool SHARE>   // COND: the schema has conditional fields; SHARE: split > 1
 __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *soff = (uint64_t *)smem;                       // [RPB + 1] record offsets in the stream
@@ -601,26 +608,32 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArg
     uint8_t *img = smem + ((enc_el_lds_bytes(0) - 16 + 15) & ~(size_t)15);
     const uint64_t total = a.totals[0];
     if (total > a.xdr_cap) return;   // XDRG_E_CAPACITY: write nothing
-    const uint64_t rb = (uint64_t)blockIdx.x * kRecPerBlock;
+    const uint32_t split = SHARE ? gridDim.x / (uint32_t)a.nblocks : 1u, kShare = kRecPerBlock / split;
+    const uint64_t blk = blockIdx.x / split, q = blockIdx.x % split;
+    const uint64_t rb0 = blk * kRecPerBlock;
     const uint32_t tid = threadIdx.x, t0 = tid * kRecPerThread;
     uint64_t sz[kRecPerThread], s = 0;
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) {
-        sz[j] = rb + t0 + j < a.n ? a.rec_size[rb + t0 + j] : 0;
+        sz[j] = rb0 + t0 + j < a.n ? a.rec_size[rb0 + t0 + j] : 0;
         s += sz[j];
     }
     uint64_t btot;
-    uint64_t off = a.block_sums[blockIdx.x] + block_excl_scan(s, &btot);
+    uint64_t off = a.block_sums[blk] + block_excl_scan(s, &btot);
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) {
         soff[t0 + j] = off;
-        if (a.rec_out && rb + t0 + j < a.n) a.rec_out[rb + t0 + j] = off;
+        if (a.rec_out && rb0 + t0 + j < a.n && (t0 + j) / kShare == q) a.rec_out[rb0 + t0 + j] = off;
         off += sz[j];
     }
     if (tid == kRecThreads - 1) soff[kRecPerBlock] = off;
     if (a.rec_out && blockIdx.x == 0 && tid == 0) a.rec_out[a.n] = total;
     __syncthreads();
-    const uint32_t nrec = (uint32_t)(a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock);
+    // this block's share: records rb .. rb + nrec, offsets from soff[0]
+    const uint64_t rb = rb0 + q * kShare;
+    if (rb >= a.n) return;
+    if (SHARE) soff += q * kShare;
+    const uint32_t nrec = (uint32_t)(a.n - rb < (uint64_t)kShare ? a.n - rb : (uint64_t)kShare);
     const uint32_t g = a.el_g;
     const GField &G = a.f[g];
     const bool lay = a.lay_g == g + 1;   // (no conditional member: every element has the layout)
@@ -1507,6 +1520,8 @@ template <bool NEST>
 static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) {
     const dim3 grid((uint32_t)a.nblocks), block(kRecThreads);
     const dim3 rgrid((uint32_t)((a.n + kRecThreads - 1) / kRecThreads));
+    const dim3 egrid((uint32_t)a.nblocks * enc_el_split(a.nblocks));
+    const bool esh = enc_el_split(a.nblocks) > 1;
     switch (phase) {
     case GRP_ENC_SIZES:
         if (kWalkSplit > 1) {
@@ -1516,8 +1531,10 @@ static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_
         hipLaunchKernelGGL(k_grp_enc_sizes<NEST>, dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
         break;
     case GRP_ENC_PLACE:   // element-parallel (key 41) or G lanes per record (key 32)
-        if (!NEST && a.enc_img && a.ncond) hipLaunchKernelGGL(k_grp_enc_place_el<true>, grid, block, enc_el_lds_bytes(a.enc_img), st, a);
-        else if (!NEST && a.enc_img) hipLaunchKernelGGL(k_grp_enc_place_el<false>, grid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        if (!NEST && a.enc_img && a.ncond && esh) hipLaunchKernelGGL((k_grp_enc_place_el<true, true>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (!NEST && a.enc_img && a.ncond) hipLaunchKernelGGL((k_grp_enc_place_el<true, false>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (!NEST && a.enc_img && esh) hipLaunchKernelGGL((k_grp_enc_place_el<false, true>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (!NEST && a.enc_img) hipLaunchKernelGGL((k_grp_enc_place_el<false, false>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
         else if (a.enc_lanes == 4) hipLaunchKernelGGL((k_grp_enc_place<4, NEST>), grid, block, 0, st, a);
         else if (a.enc_lanes == 8) hipLaunchKernelGGL((k_grp_enc_place<8, NEST>), grid, block, 0, st, a);
         else if (a.enc_lanes == 16) hipLaunchKernelGGL((k_grp_enc_place<16, NEST>), grid, block, 0, st, a);
