@@ -227,6 +227,22 @@ int  xdrg_ctx_host_staging(xdrg_ctx *ctx, uint64_t slot_bytes, uint32_t slots);
 int  xdrg_host_register(xdrg_ctx *ctx, void *ptr, uint64_t bytes);
 int  xdrg_host_unregister(xdrg_ctx *ctx, void *ptr);
 
+/* Device buffers for a caller with no device allocator of its own (a JVM):
+ * the HBM counterpart of GrizzlyMemoryManager.allocate / wrap
+ * (grizzly/GrizzlyMemoryManager.java:42-57).  The pointers these return are
+ * what the device forms of every call take (no flags; the multi-GPU calls;
+ * XDRG_ASYNC result words).  xdrg_device_alloc: `bytes` on the context's
+ * device (256-byte aligned; 0 bytes gives a valid 256-byte buffer).
+ * xdrg_copy: `bytes` from src to dst on the context's stream, then a
+ * synchronise; kind says which side is which.  A host side may be any host
+ * memory (pinned or registered spans move at DMA speed).                    */
+#define XDRG_COPY_H2D 1
+#define XDRG_COPY_D2H 2
+#define XDRG_COPY_D2D 3
+int  xdrg_device_alloc(xdrg_ctx *ctx, uint64_t bytes, void **out);
+int  xdrg_device_free(xdrg_ctx *ctx, void *ptr);
+int  xdrg_copy(xdrg_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
+
 /* ---- schema ----------------------------------------------------------------- */
 /* Compile a field tape (rpcgen struct body, jrpcgen.java:758-913) into an
  * engine schema.  Host-side object; may be shared by contexts.                 */
@@ -314,9 +330,15 @@ int  xdrg_decode_batch(xdrg_ctx *ctx, const xdrg_schema *schema,
  * (4 - (len & 3)) & 3.  splice[i] = UINT64_MAX when the field is absent
  * (conditional schemas): the message is out[rec_offsets[i], rec_offsets[i+1]).
  * The field column's `data` is never dereferenced (it may be a host
- * buffer, a file mapping or NULL); its `offsets` must be device memory.
+ * buffer, a file mapping or NULL).
  * With XDRG_FRAME_RM each mark counts every part (sendRawTCP :135-139,
- * getMessagesSize :224-231).  splice: device array of n entries.            */
+ * getMessagesSize :224-231).  splice: an array of n entries.
+ * Memory: device pointers (flags 0, XDRG_ASYNC); or, as for
+ * xdrg_encode_batch, XDRG_HOST_PTRS — every other column, out, rec_offsets,
+ * splice and out_len host memory moved through the staging ring, the payload
+ * column's values never read nor staged (only the heads cross PCIe: the
+ * Grizzly buffer a sender writes around the payload, Xdr.java:582-597) — or
+ * XDRG_HOST_PTRS | XDRG_HOST_MAPPED (registered host memory in place).     */
 int  xdrg_encode_batch_shallow(xdrg_ctx *ctx, const xdrg_schema *schema,
                                const xdrg_column *cols, uint64_t n,
                                uint8_t *out, uint64_t out_cap,
@@ -328,7 +350,12 @@ int  xdrg_encode_batch_shallow(xdrg_ctx *ctx, const xdrg_schema *schema,
  * stream instead of a copy.  payload_pos[i] (device, n entries) = offset in
  * `in` of record i's payload (UINT64_MAX if absent); the column's offsets
  * are written as for a copy (len_i = offsets[i+1] - offsets[i]); its data
- * and cap are ignored.  Checks and error parity as xdrg_decode_batch.       */
+ * and cap are ignored.  Checks and error parity as xdrg_decode_batch.
+ * Memory as xdrg_decode_batch: device pointers, XDRG_HOST_PTRS (the stream
+ * staged, payload_pos and the columns returned to host memory: the slices
+ * then point into the caller's own host buffer, as Xdr's do), or
+ * XDRG_HOST_PTRS | XDRG_HOST_MAPPED.  Any other flag bit, on this and every
+ * codec call, is XDRG_E_INVAL.                                              */
 int  xdrg_decode_batch_view(xdrg_ctx *ctx, const xdrg_schema *schema,
                             const uint8_t *in, uint64_t in_len,
                             const uint64_t *rec_offsets, uint64_t n,

@@ -42,6 +42,7 @@ HOST_PTRS = 0x4     # every pointer of the call is host memory (staging ring, in
 HOST_MAPPED = 0x8   # with HOST_PTRS: kernels access the registered host buffers in place
 STRIDE_CONST = -(1 << 63)   # XDRG_STRIDE_CONST: every record reads element run 0 (encode only)
 CTX_TIMING = 0x1
+COPY_H2D, COPY_D2H, COPY_D2D = 1, 2, 3   # xdrg_copy kinds
 
 # kernel ids for xdrg_ctx_kernel_stats
 KERNEL_FIXED_ENCODE = 0
@@ -103,6 +104,9 @@ FUNCTIONS = {
     "xdrg_ctx_host_staging": (ctypes.c_int, [_P, _U64, ctypes.c_uint32]),
     "xdrg_host_register": (ctypes.c_int, [_P, _P, _U64]),
     "xdrg_host_unregister": (ctypes.c_int, [_P, _P]),
+    "xdrg_device_alloc": (ctypes.c_int, [_P, _U64, ctypes.POINTER(_P)]),
+    "xdrg_device_free": (ctypes.c_int, [_P, _P]),
+    "xdrg_copy": (ctypes.c_int, [_P, _P, _P, _U64, ctypes.c_int]),
     "xdrg_schema_create": (ctypes.c_int, [ctypes.POINTER(Field), ctypes.c_size_t,
                                           ctypes.POINTER(_P)]),
     "xdrg_schema_create_cond": (ctypes.c_int, [ctypes.POINTER(Field), ctypes.c_size_t,

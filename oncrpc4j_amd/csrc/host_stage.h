@@ -25,10 +25,17 @@
 //   int h2d_done(uint32_t s);                    // event: slot s's inputs are on the device
 //   int kernel_begin(uint32_t s);                // compute stream waits h2d_done(s)
 //   int add_u64(int on_d2h, uint64_t *dev, uint64_t n, uint64_t delta);  // dev[0..n) += delta
+//   int add_pos(uint64_t *dev, uint64_t n, uint64_t delta);   // copy stream: the same, UINT64_MAX kept
 //   int encode(uint32_t s, const xdrg_column *dcols, uint64_t m, uint8_t *out, uint64_t cap,
-//              uint64_t *rec, uint32_t flags);   // async; result word 0 = stream bytes
+//              uint64_t *rec, uint32_t flags, uint32_t byref, uint64_t *ref);
+//                                                // async; result word 0 = stream bytes; byref = 0 or
+//                                                // 1 + the field encoded by reference, ref its splice
+//                                                // positions (xdrg_encode_batch_shallow)
 //   int decode(uint32_t s, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m,
-//              xdrg_column *dcols, uint32_t flags);   // async; words 0 / 1 = first_bad / err
+//              xdrg_column *dcols, uint32_t flags, uint32_t byref, uint64_t *ref);
+//                                                // async; words 0 / 1 = first_bad / err; byref: the
+//                                                // field decoded as a view, ref its payload positions
+//                                                // (xdrg_decode_batch_view)
 //   int kernel_end(uint32_t s, const uint64_t *const *extra, const uint64_t *const *index,
 //                  const uint64_t *limit, uint32_t nextra);
 //                                                // result words 2 + i = index[i] ? (*index[i] <= limit[i] ?
@@ -188,6 +195,7 @@ struct Layout {
     std::vector<uint64_t> val, off, vcap;    // per field (dynamic, group offsets): values / offsets, value capacity
     std::vector<uint64_t> rows;              // decode: per field, the rows laid out (members: element bound)
     uint64_t xdr = 0, xcap = 0, rec = 0;     // stream span, its capacity, record offsets (m + 1)
+    uint64_t ref = 0;                        // by-reference field: splice / payload positions (m)
     uint64_t win = 0, wlen = 0;              // decode: host window [win, win + wlen) of the stream
 };
 
@@ -217,11 +225,14 @@ inline void chunk_rows(const Schema &s, const xdrg_column *cols, uint64_t lo, ui
 inline uint64_t group_elems(const Rows &R, uint32_t g) { return R.n[g + 1]; }
 
 // Bound on a chunk's XDR bytes (conditional fields may take some away).
-inline uint64_t bound_xdr(const Schema &s, bool framed, uint64_t m, const xdrg_column *cols, const Rows &R) {
+inline uint64_t bound_xdr(const Schema &s, bool framed, uint64_t m, const xdrg_column *cols, const Rows &R,
+                          uint32_t byref = 0) {
     uint64_t b = m * (framed ? 4 : 0);
     for (uint32_t k = 0; k < s.f.size(); ++k) {
         const Field &f = s.f[k];
-        if (is_group(f)) {   // a count word, or a bool per element and the closing one
+        if (k + 1 == byref) {   // by reference: the length word stays, the payload goes out on its own
+            b += 4 * R.n[k];
+        } else if (is_group(f)) {   // a count word, or a bool per element and the closing one
             if (f.kind == XDRG_K_DYNAMIC) b += 4 * m;
             if (f.kind == XDRG_K_LIST) b += 4 * m + 4 * group_elems(R, k);
         } else if (f.kind != XDRG_K_DYNAMIC) {
@@ -249,6 +260,7 @@ struct EncPlan {
     uint64_t n;
     bool framed, want_rec;
     std::vector<Region> regs;
+    uint32_t byref = 0;   // 1 + the field encoded by reference (its values never move), or 0
 };
 
 inline void enc_layout(const EncPlan &p, uint64_t lo, uint64_t m, Layout &L, Rows &R) {
@@ -275,13 +287,16 @@ inline void enc_layout(const EncPlan &p, uint64_t lo, uint64_t m, Layout &L, Row
         }
         if (f.kind != XDRG_K_DYNAMIC) continue;
         const uint64_t a = p.cols[k].offsets[R.lo[k]], e = p.cols[k].offsets[R.lo[k] + R.n[k]];
-        L.vcap[k] = e - a;
-        L.val[k] = b.take((e - a) * f.nsz, (uintptr_t)((const uint8_t *)p.cols[k].data + a * f.nsz));
+        if (k + 1 != p.byref) {
+            L.vcap[k] = e - a;
+            L.val[k] = b.take((e - a) * f.nsz, (uintptr_t)((const uint8_t *)p.cols[k].data + a * f.nsz));
+        }
         L.off[k] = b.take((R.n[k] + 1) * 8, (uintptr_t)(p.cols[k].offsets + R.lo[k]));
     }
-    L.xcap = bound_xdr(s, p.framed, m, p.cols, R);
+    L.xcap = bound_xdr(s, p.framed, m, p.cols, R, p.byref);
     L.xdr = b.take(L.xcap);
     L.rec = (p.want_rec || s.var_size) ? b.take((m + 1) * 8) : 0;
+    L.ref = p.byref ? b.take(m * 8) : 0;
     L.need = b.used;
 }
 
@@ -424,11 +439,15 @@ struct Stager {
 // needs (the chunks before the overrun have been written).  Repeated groups:
 // a chunk moves its records' elements with them (the members' rows between
 // the group offsets of its first and last record, rebased to the chunk).
+// By reference (byref = 1 + field, xdrg_encode_batch_shallow): that field's
+// values stay on the host — only its offsets cross — and splice (host, n)
+// receives each record's splice position, rebased like its record offset.
 template <class X>
 int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uint8_t *out, uint64_t out_cap,
-                 uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len) {
+                 uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len, uint32_t byref = 0,
+                 uint64_t *splice = nullptr) {
     const bool framed = flags & XDRG_FRAME_RM;
-    EncPlan p{s, cols, n, framed, rec_offsets != nullptr, {}};
+    EncPlan p{s, cols, n, framed, rec_offsets != nullptr, {}, byref};
     HS_TRY(build_regions(s, cols, p.regs));
     if (!dyn_offsets_sane(s, cols, n)) return XDRG_E_INVAL;
     const uint64_t stride = s.fixed_part + (framed ? 4 : 0);
@@ -469,6 +488,10 @@ int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uin
             if (rec_offsets) {
                 HS_TRY(x.add_u64(1, (uint64_t *)(slot + L.rec), L.m + 1, base));
                 HS_TRY(st.d2h(s_, rec_offsets + L.lo, slot + L.rec, (L.m + 1) * 8));
+            }
+            if (byref) {
+                HS_TRY(x.add_pos((uint64_t *)(slot + L.ref), L.m, base));
+                HS_TRY(st.d2h(s_, splice + L.lo, slot + L.ref, L.m * 8));
             }
         } else {
             st.busy[s_] = true;
@@ -518,9 +541,10 @@ int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uin
                 dc[k2].cap = group_elems(R, k2);
             } else if (fd.kind == XDRG_K_DYNAMIC) {
                 const uint64_t a = cols[k2].offsets[R.lo[k2]];
-                HS_TRY(st.h2d(s_, slot + L.val[k2], (const uint8_t *)cols[k2].data + a * fd.nsz, L.vcap[k2] * fd.nsz));
+                if (k2 + 1 != byref)
+                    HS_TRY(st.h2d(s_, slot + L.val[k2], (const uint8_t *)cols[k2].data + a * fd.nsz, L.vcap[k2] * fd.nsz));
                 HS_TRY(st.h2d(s_, slot + L.off[k2], cols[k2].offsets + R.lo[k2], (R.n[k2] + 1) * 8));
-                dc[k2].data = slot + L.val[k2];
+                dc[k2].data = k2 + 1 == byref ? nullptr : slot + L.val[k2];
                 dc[k2].offsets = (uint64_t *)(slot + L.off[k2]);
                 dc[k2].cap = L.vcap[k2];
             } else if (!fixed_elem_bytes(fd)) {
@@ -538,7 +562,7 @@ int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uin
                 HS_TRY(x.add_u64(0, dc[k2].offsets, R.n[k2] + 1, (uint64_t)0 - cols[k2].offsets[R.lo[k2]]));
         }
         HS_TRY(x.encode(s_, dc.data(), m, slot + L.xdr, L.xcap, L.rec ? (uint64_t *)(slot + L.rec) : nullptr,
-                        flags & XDRG_FRAME_RM));
+                        flags & XDRG_FRAME_RM, byref, byref ? (uint64_t *)(slot + L.ref) : nullptr));
         HS_TRY(x.kernel_end(s_, nullptr, nullptr, nullptr, 0));
         q.push_back(std::move(f));
         // fixed-size chunks leave at once; a variable-size chunk waits for its
@@ -564,6 +588,7 @@ struct DecPlan {
     bool framed;
     xdrg_column *cols;
     std::vector<Region> regs;
+    uint32_t byref = 0;   // 1 + the field decoded as a view (its values are never written), or 0
 };
 
 // The chunk's stream window: [min, max] of its record extents (rebased by
@@ -630,11 +655,14 @@ inline void dec_layout(const DecPlan &p, uint64_t lo, uint64_t m, Layout &L) {
         }
         if (f.kind != XDRG_K_DYNAMIC) continue;
         // a record's elements are bounded by the bytes its stream holds
-        const uint64_t cap = L.wlen / f.xsz + 1;
-        L.vcap[k] = cap;
-        L.val[k] = b.take(cap * f.nsz);
+        if (k + 1 != p.byref) {
+            const uint64_t cap = L.wlen / f.xsz + 1;
+            L.vcap[k] = cap;
+            L.val[k] = b.take(cap * f.nsz);
+        }
         L.off[k] = b.take((L.rows[k] + 1) * 8);
     }
+    L.ref = p.byref ? b.take(m * 8) : 0;
     L.need = b.used;
 }
 
@@ -646,12 +674,16 @@ inline void dec_layout(const DecPlan &p, uint64_t lo, uint64_t m, Layout &L) {
 // slot comes round again.  The first chunk (in record order) that reports an
 // error ends the walk: its first failing record is the batch's.  Repeated
 // groups: a chunk's elements follow the previous chunks' (the group column's
-// total per chunk), and its members' values follow theirs.
+// total per chunk), and its members' values follow theirs.  As a view
+// (byref = 1 + field, xdrg_decode_batch_view): that field's offsets are
+// written as for a copy, its values are not, and payload_pos (host, n)
+// receives each payload's offset in `in` (the chunk's window start added).
 template <class X>
 int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, const uint64_t *rec_offsets,
-                 uint64_t n, xdrg_column *cols, uint32_t flags, uint64_t *first_bad, int *err) {
+                 uint64_t n, xdrg_column *cols, uint32_t flags, uint64_t *first_bad, int *err,
+                 uint32_t byref = 0, uint64_t *payload_pos = nullptr) {
     const bool framed = flags & XDRG_FRAME_RM;
-    DecPlan p{s, in, in_len, rec_offsets, n, framed, cols, {}};
+    DecPlan p{s, in, in_len, rec_offsets, n, framed, cols, {}, byref};
     HS_TRY(build_regions(s, cols, p.regs));
     // the counted columns whose totals place the next chunk: dynamic fields
     // (their values) and DYNAMIC / LIST groups (their elements)
@@ -717,8 +749,12 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
             const uint64_t first = is_group(s.f[k]) ? L.lo : first_of(k);
             HS_TRY(x.add_u64(1, (uint64_t *)(slot + L.off[k]), rows + 1, f.base[k]));
             HS_TRY(st.d2h(s_, cols[k].offsets + first, slot + L.off[k], (rows + 1) * 8));
-            if (!is_group(s.f[k]))
+            if (!is_group(s.f[k]) && k + 1 != byref)
                 HS_TRY(st.d2h(s_, (uint8_t *)cols[k].data + f.base[k] * s.f[k].nsz, slot + L.val[k], tot[k] * s.f[k].nsz));
+        }
+        if (byref) {   // payload positions: window-relative on the device, stream offsets on the host
+            HS_TRY(x.add_pos((uint64_t *)(slot + L.ref), L.m, L.win));
+            HS_TRY(st.d2h(s_, payload_pos + L.lo, slot + L.ref, L.m * 8));
         }
         st.busy[s_] = true;
         return x.d2h_done(s_);
@@ -734,7 +770,8 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
             // a failing chunk's totals may not cover its valid prefix (a decode
             // stops at the error): it hands back every value / element it was granted
             const uint32_t k = cnt[i];
-            tot[k] = w[1] ? f.cap[k] : std::min(w[2 + i], f.cap[k]);
+            tot[k] = k + 1 == byref ? (w[1] ? 0 : w[2 + i])   // (a view's values are never placed)
+                                    : w[1] ? f.cap[k] : std::min(w[2 + i], f.cap[k]);
             next_base[k] = f.base[k] + tot[k];
         }
         HS_TRY(retire(f, tot));
@@ -804,6 +841,11 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
                 f.cap[k2] = std::min(left, L.rows[k2 + 1]);
                 dc[k2].offsets = (uint64_t *)(slot + L.off[k2]);
                 dc[k2].cap = f.cap[k2];
+            } else if (k2 + 1 == byref) {   // a view: offsets only, no capacity
+                f.base[k2] = next_base[k2];
+                dc[k2].data = nullptr;
+                dc[k2].offsets = (uint64_t *)(slot + L.off[k2]);
+                dc[k2].cap = 0;
             } else if (fd.kind == XDRG_K_DYNAMIC) {
                 f.base[k2] = next_base[k2];
                 const uint64_t left = cols[k2].cap > f.base[k2] ? cols[k2].cap - f.base[k2] : 0;
@@ -819,7 +861,7 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
         HS_TRY(x.kernel_begin(s_));
         if (rec_offsets && L.win) HS_TRY(x.add_u64(0, (uint64_t *)(slot + L.rec), m + 1, (uint64_t)0 - L.win));
         HS_TRY(x.decode(s_, slot + L.xdr, L.wlen, rec_offsets ? (uint64_t *)(slot + L.rec) : nullptr, m, dc.data(),
-                        flags & XDRG_FRAME_RM));
+                        flags & XDRG_FRAME_RM, byref, byref ? (uint64_t *)(slot + L.ref) : nullptr));
         // totals: a dynamic field's offsets at its last row (a member's: at the
         // chunk's element total, read on the device), a group's at record m
         // (the element total is read on the device only when within the member's
@@ -913,7 +955,8 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
     if (msg_offsets) msg_offsets[0] = 0;
     if (cap == 0 || len < 4) return XDRG_E_INCOMPLETE;
     Stager<X> st(x);
-    // window geometry for the ring's slot size: room H and fresh bytes F
+    // window geometry for the ring's slot size (reserving every region's worst
+    // alignment, so a window that fills G.rows rows fits): room H and fresh bytes F
     // (multiples of 16), the rows a window may deliver, and where the message
     // offsets, body offsets, bodies (DEFRAME) and columns (DECODE) sit
     struct Geo { uint64_t H, F, W, rows, offs, boffs, body, cols, need; };
@@ -930,7 +973,8 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
         g.body = mode == RECV_DEFRAME ? b.take(g.W) : 0;
         g.cols = b.used;
         if (mode == RECV_DECODE) {
-            for (const Region &r : regs) b.take((uint64_t)r.stride * g.rows);
+            // (a window's regions keep their host address modulo 16: the worst case)
+            for (const Region &r : regs) b.take((uint64_t)r.stride * g.rows, 15);
             for (uint32_t k : dyn) {
                 b.take((g.rows + 1) * 8);
                 b.take((g.W / sp->f[k].xsz + 1) * sp->f[k].nsz);
@@ -1150,9 +1194,9 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             const bool single = res[2] != 0;
             if (single) {
                 HS_TRY(x.offs_copy(dboffs, doffs, m + 1, cur.off));   // window -> slot offsets
-                HS_TRY(x.decode(cur.slot, slot, cur.off + cur.wl, dboffs, m, dc.data(), XDRG_FRAME_RM));
+                HS_TRY(x.decode(cur.slot, slot, cur.off + cur.wl, dboffs, m, dc.data(), XDRG_FRAME_RM, 0, nullptr));
             } else {
-                HS_TRY(x.decode(cur.slot, x.body(), res[3], dboffs, m, dc.data(), 0));
+                HS_TRY(x.decode(cur.slot, x.body(), res[3], dboffs, m, dc.data(), 0, 0, nullptr));
             }
             std::vector<const uint64_t *> extra;
             for (uint32_t k2 : dyn) extra.push_back((const uint64_t *)(slot + c.L.off[k2]) + m);

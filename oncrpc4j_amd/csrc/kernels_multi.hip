@@ -124,4 +124,19 @@ int launch_add_u64(uint64_t *p, uint64_t n, uint64_t delta, void *stream) {
     return (int)hipGetLastError();
 }
 
+__global__ void k_add_pos(uint64_t *p, uint64_t n, uint64_t delta) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = p[i];
+        if (v != ~0ull) p[i] = v + delta;
+    }
+}
+
+int launch_add_pos(uint64_t *p, uint64_t n, uint64_t delta, void *stream) {
+    if (!n || !delta) return 0;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_add_pos, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, p, n, delta);
+    return (int)hipGetLastError();
+}
+
 }  // namespace xdrg

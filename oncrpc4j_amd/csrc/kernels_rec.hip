@@ -1555,6 +1555,17 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
     const uint64_t sh = R & 15;                    // record start inside chunk 0
     const uint64_t p0 = sh + a.pay_fb + 4;         // payload start, chunk coordinates
     const uint64_t cf = (p0 + 15) >> 4, cl = (p0 + cnt) >> 4;   // payload-only chunks: [cf, cl)
+    // the record's words outside those chunks (mark, fixed fields, length,
+    // the payload's first and last bytes, pad, trailing fixed fields): a word
+    // per lane, loaded before the payload so both round trips overlap
+    const uint64_t hw = cl > cf ? (16 * cf - sh) >> 2 : (size >> 2);   // head words
+    const uint64_t tw0 = cl > cf ? (16 * cl - sh) >> 2 : (size >> 2);  // first tail word
+    const uint64_t nslow = hw + (size >> 2) - tw0;
+#if !XDRG_PAY_OLD
+    uint32_t w0 = 0;
+    const uint64_t wi0 = lane < hw ? lane : tw0 + (lane - hw);
+    if (lane < nslow) w0 = payload_rec_word(a, r, 4 * wi0, size, src, cnt);
+#endif
     for (uint64_t c0 = cf + lane; c0 < cl; c0 += 4 * LPR) {   // payload-only chunks
         u32x4a v[4];
 #pragma unroll
@@ -1571,13 +1582,12 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
             __builtin_nontemporal_store(v[u], (u32x4n *)(A + 16 * c));
         }
     }
-    // the record's words outside those chunks (mark, fixed fields, length,
-    // the payload's first and last bytes, pad, trailing fixed fields): a word
-    // per lane, their loads in parallel
-    const uint64_t hw = cl > cf ? (16 * cf - sh) >> 2 : (size >> 2);   // head words
-    const uint64_t tw0 = cl > cf ? (16 * cl - sh) >> 2 : (size >> 2);  // first tail word
-    const uint64_t nslow = hw + (size >> 2) - tw0;
+#if !XDRG_PAY_OLD
+    if (lane < nslow) *(uint32_t *)(a.xdr + R + 4 * wi0) = w0;
+    for (uint64_t i = lane + LPR; i < nslow; i += LPR) {   // (records of > 64 such words: short payloads)
+#else
     for (uint64_t i = lane; i < nslow; i += LPR) {
+#endif
         const uint64_t wi = i < hw ? i : tw0 + (i - hw);
         *(uint32_t *)(a.xdr + R + 4 * wi) = payload_rec_word(a, r, 4 * wi, size, src, cnt);
     }

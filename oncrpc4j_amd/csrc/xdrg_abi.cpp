@@ -945,16 +945,28 @@ static int encode_impl(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
 }
 
 static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, uint8_t *out,
-                       uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len);
+                       uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len,
+                       uint32_t byref, uint64_t *splice);
 static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t in_len,
                        const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
-                       uint64_t *first_bad, int *err);
+                       uint64_t *first_bad, int *err, uint32_t byref, uint64_t *payload_pos);
+
+// The flags of the codec calls (encode / decode, their by-reference forms);
+// any other bit is refused before a pointer is looked at, so a caller's host
+// buffer never reaches a kernel under a flag the call does not know.
+static int codec_flags(xdrg_ctx *c, uint32_t flags) {
+    if (flags & ~(XDRG_FRAME_RM | XDRG_ASYNC | XDRG_HOST_PTRS | XDRG_HOST_MAPPED))
+        return inval(c, "unknown flag bits");
+    if ((flags & XDRG_HOST_MAPPED) && !(flags & XDRG_HOST_PTRS)) return inval(c, "XDRG_HOST_MAPPED without XDRG_HOST_PTRS");
+    return XDRG_OK;
+}
 
 extern "C" int xdrg_encode_batch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols,
                                  uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *rec_offsets,
                                  uint32_t flags, uint64_t *out_len) {
-    if (flags & XDRG_HOST_PTRS) return host_encode(c, s, cols, n, out, out_cap, rec_offsets, flags, out_len);
-    if (flags & XDRG_HOST_MAPPED) return inval(c, "XDRG_HOST_MAPPED without XDRG_HOST_PTRS");
+    const int rc = codec_flags(c, flags);
+    if (rc) return rc;
+    if (flags & XDRG_HOST_PTRS) return host_encode(c, s, cols, n, out, out_cap, rec_offsets, flags, out_len, 0, nullptr);
     return encode_impl(c, s, cols, n, out, out_cap, rec_offsets, flags, out_len, 0, nullptr);
 }
 
@@ -973,8 +985,11 @@ extern "C" int xdrg_encode_batch_shallow(xdrg_ctx *c, const xdrg_schema *s, cons
                                          uint64_t n, uint8_t *out, uint64_t out_cap,
                                          uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len,
                                          uint32_t field, uint64_t *splice) {
-    const int rc = check_byref(c, s, field, n ? splice : (void *)1);
+    int rc = codec_flags(c, flags);
+    if (!rc) rc = check_byref(c, s, field, n ? splice : (void *)1);
     if (rc) return rc;
+    if (flags & XDRG_HOST_PTRS)
+        return host_encode(c, s, cols, n, out, out_cap, rec_offsets, flags, out_len, field + 1, splice);
     return encode_impl(c, s, cols, n, out, out_cap, rec_offsets, flags, out_len, field + 1, splice);
 }
 
@@ -1212,8 +1227,10 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
 extern "C" int xdrg_decode_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in,
                                  uint64_t in_len, const uint64_t *rec_offsets, uint64_t n,
                                  xdrg_column *cols, uint32_t flags, uint64_t *first_bad, int *err) {
-    if (flags & XDRG_HOST_PTRS) return host_decode(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err);
-    if (flags & XDRG_HOST_MAPPED) return inval(c, "XDRG_HOST_MAPPED without XDRG_HOST_PTRS");
+    const int rc = codec_flags(c, flags);
+    if (rc) return rc;
+    if (flags & XDRG_HOST_PTRS)
+        return host_decode(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err, 0, nullptr);
     return decode_impl(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err, 0, nullptr);
 }
 
@@ -1221,8 +1238,11 @@ extern "C" int xdrg_decode_batch_view(xdrg_ctx *c, const xdrg_schema *s, const u
                                       uint64_t in_len, const uint64_t *rec_offsets, uint64_t n,
                                       xdrg_column *cols, uint32_t flags, uint64_t *first_bad,
                                       int *err, uint32_t field, uint64_t *payload_pos) {
-    const int rc = check_byref(c, s, field, n ? payload_pos : (void *)1);
+    int rc = codec_flags(c, flags);
+    if (!rc) rc = check_byref(c, s, field, n ? payload_pos : (void *)1);
     if (rc) return rc;
+    if (flags & XDRG_HOST_PTRS)
+        return host_decode(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err, field + 1, payload_pos);
     return decode_impl(c, s, in, in_len, rec_offsets, n, cols, flags, first_bad, err, field + 1,
                        payload_pos);
 }
@@ -1315,6 +1335,48 @@ extern "C" int xdrg_host_unregister(xdrg_ctx *c, void *ptr) {
     DeviceGuard dg;
     if (c) HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipHostUnregister(ptr));
+    return XDRG_OK;
+}
+
+// Device buffers for a caller without a device allocator (GrizzlyMemoryManager
+// allocate / wrap, grizzly/GrizzlyMemoryManager.java:42-57, in HBM).
+extern "C" int xdrg_device_alloc(xdrg_ctx *c, uint64_t bytes, void **out) {
+    if (!c || !out) return XDRG_E_INVAL;
+    *out = nullptr;
+    DeviceGuard dg;
+    HIPCHK(c, hipSetDevice(c->device));
+    void *p = nullptr;
+    const hipError_t e = hipMalloc(&p, bytes ? bytes : 256);
+    if (e != hipSuccess) {
+        (void)hip_fail(c, e, "hipMalloc");
+        return XDRG_E_NOMEM;
+    }
+    *out = p;
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_device_free(xdrg_ctx *c, void *p) {
+    if (!c) return XDRG_E_INVAL;
+    if (!p) return XDRG_OK;
+    DeviceGuard dg;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));   // (work queued on it may still read the buffer)
+    HIPCHK(c, hipFree(p));
+    return XDRG_OK;
+}
+
+extern "C" int xdrg_copy(xdrg_ctx *c, void *dst, const void *src, uint64_t bytes, int kind) {
+    if (!c) return XDRG_E_INVAL;
+    const hipMemcpyKind k = kind == XDRG_COPY_H2D ? hipMemcpyHostToDevice
+                          : kind == XDRG_COPY_D2H ? hipMemcpyDeviceToHost
+                          : kind == XDRG_COPY_D2D ? hipMemcpyDeviceToDevice : hipMemcpyDefault;
+    if (k == hipMemcpyDefault) return inval(c, "xdrg_copy: kind must be XDRG_COPY_H2D / D2H / D2D");
+    if (!bytes) return XDRG_OK;
+    if (!dst || !src) return inval(c, "xdrg_copy: NULL buffer");
+    DeviceGuard dg;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, k, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return XDRG_OK;
 }
 
@@ -1443,21 +1505,25 @@ struct HipExec {
         HIPCHK(c, (hipError_t)launch_add_u64(p, n, delta, on_d2h ? r.d2h : r.comp));
         return XDRG_OK;
     }
+    int add_pos(uint64_t *p, uint64_t n, uint64_t delta) {
+        HIPCHK(c, (hipError_t)launch_add_pos(p, n, delta, r.d2h));
+        return XDRG_OK;
+    }
     int encode(uint32_t i, const xdrg_column *dc, uint64_t m, uint8_t *out, uint64_t cap, uint64_t *rec,
-               uint32_t flags) {
+               uint32_t flags, uint32_t byref, uint64_t *ref) {
         hipStream_t keep = c->stream;
         c->stream = r.comp;
         const int rc = encode_impl(c, s, dc, m, out, cap, rec, flags | XDRG_ASYNC, r.d_res + (uint64_t)i * kResWords,
-                                   0, nullptr);
+                                   byref, ref);
         c->stream = keep;
         return rc;
     }
     int decode(uint32_t i, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m, xdrg_column *dc,
-               uint32_t flags) {
+               uint32_t flags, uint32_t byref, uint64_t *ref) {
         hipStream_t keep = c->stream;
         c->stream = r.comp;
         uint64_t *w = r.d_res + (uint64_t)i * kResWords;
-        const int rc = decode_impl(c, s, in, len, rec, m, dc, flags | XDRG_ASYNC, w, (int *)(w + 1), 0, nullptr);
+        const int rc = decode_impl(c, s, in, len, rec, m, dc, flags | XDRG_ASYNC, w, (int *)(w + 1), byref, ref);
         c->stream = keep;
         return rc;
     }
@@ -1583,9 +1649,11 @@ static void stage_schema(const xdrg_schema *s, hs::Schema &v) {
 // offsets + 1) mapped by fn(ptr, bytes) -> the device address (nullptr: not
 // covered).  XDRG_HOST_MAPPED maps through the registrations; the bounce path
 // through device scratch.
+// byref = 1 + a field whose values the call never touches (a by-reference
+// payload, a view): its offsets map, its data is NULL.
 template <typename F>
 static int map_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool decode,
-                    std::vector<xdrg_column> &out, F fn) {
+                    std::vector<xdrg_column> &out, F fn, uint32_t byref = 0) {
     out.assign(cols, cols + s->f.size());
     // native rows of every field's column (a group precedes its members):
     // records, a FIXED group's rows x count, else the group's elements
@@ -1612,6 +1680,11 @@ static int map_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, 
         if (f.kind == XDRG_K_DYNAMIC) {
             d.offsets = (uint64_t *)fn(cols[k].offsets, (rows + 1) * 8);
             if (!d.offsets) return inval(c, "XDRG_HOST_MAPPED: column offsets not registered for every row + 1");
+            if (k + 1 == byref) {
+                d.data = nullptr;
+                d.cap = 0;
+                continue;
+            }
             const uint64_t vals = decode ? cols[k].cap : (rows ? cols[k].offsets[rows] : 0);
             if (d.data || vals) {
                 d.data = fn(cols[k].data, vals * s->nsz[k]);
@@ -1622,15 +1695,21 @@ static int map_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, 
         if (!d.data) continue;
         const uint64_t elem = (uint64_t)s->nsz[k] * (f.kind == XDRG_K_FIXED ? f.count : 1);
         const int64_t st = eff_stride(s, k, cols[k]);
-        const uint64_t span = rows == 0 || st == 0 ? elem : (uint64_t)st * (rows - 1) + elem;
+        // no rows: no bytes (a member column of a group without elements may be
+        // a zero-length allocation); a constant column (stride 0): one row
+        const uint64_t span = rows == 0 ? 0 : st == 0 ? elem : (uint64_t)st * (rows - 1) + elem;
         d.data = fn(cols[k].data, span);
         if (!d.data) return inval(c, "XDRG_HOST_MAPPED: column data not registered for every row");
     }
     return XDRG_OK;
 }
 static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool decode,
-                       std::vector<xdrg_column> &out) {
-    return map_cols(c, s, cols, n, decode, out, [](const void *p, uint64_t b) { return span_device(p, b); });
+                       std::vector<xdrg_column> &out, uint32_t byref = 0) {
+    // a span of no bytes is never dereferenced: any valid device address stands in
+    return map_cols(c, s, cols, n, decode, out, [c](const void *p, uint64_t b) -> void * {
+        void *d = span_device(p, b);
+        return d || b ? d : (void *)c->d_stat;
+    }, byref);
 }
 
 // Host memory of a schema the staging ring does not window (groups inside
@@ -1643,6 +1722,7 @@ struct Bounce {
     struct Reg { uint8_t *h; uint64_t len; uint8_t *d; bool out; };
     std::vector<Span> spans;
     std::vector<Reg> regs;
+    uint8_t *empty = nullptr;   // stands in for every span of no bytes (never dereferenced)
     void add(const void *p, uint64_t len, bool out) { if (p && len) spans.push_back({(const uint8_t *)p, len, out}); }
     // merge the spans, allocate and fill the device regions
     int place(xdrg_ctx *c) {
@@ -1661,13 +1741,16 @@ struct Bounce {
             HIPCHK(c, hipMallocAsync((void **)&r.d, r.len, c->stream));
             HIPCHK(c, hipMemcpyAsync(r.d, r.h, r.len, hipMemcpyHostToDevice, c->stream));
         }
+        HIPCHK(c, hipMallocAsync((void **)&empty, 256, c->stream));
         return XDRG_OK;
     }
-    void *dev(const void *p) const {
+    // the device address of host p, a span of `len` bytes (0: the stand-in)
+    void *dev(const void *p, uint64_t len) const {
+        if (!p) return nullptr;
         const uint8_t *q = (const uint8_t *)p;
         for (const Reg &r : regs)
             if (q >= r.h && q < r.h + r.len) return r.d + (q - r.h);
-        return nullptr;
+        return len ? nullptr : empty;
     }
     int finish(xdrg_ctx *c, bool copy_back) {
         int rc = XDRG_OK;
@@ -1676,6 +1759,7 @@ struct Bounce {
                 rc = XDRG_E_HIP;
             (void)hipFreeAsync(r.d, c->stream);
         }
+        if (empty) (void)hipFreeAsync(empty, c->stream);
         if (hipStreamSynchronize(c->stream) != hipSuccess) rc = XDRG_E_HIP;
         return rc;
     }
@@ -1691,10 +1775,10 @@ static int bounce_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *c
     HIPCHK(c, hipStreamSynchronize(c->stream));   // the caller's earlier work on this context
     rc = B.place(c);
     if (rc) { (void)B.finish(c, false); return rc; }
-    rc = map_cols(c, s, cols, n, false, dc, [&](const void *p, uint64_t) { return B.dev(p); });
+    rc = map_cols(c, s, cols, n, false, dc, [&](const void *p, uint64_t b) { return B.dev(p, b); });
     uint64_t len = 0;
-    if (!rc) rc = encode_impl(c, s, dc.data(), n, (uint8_t *)B.dev(out), out_cap,
-                              (uint64_t *)B.dev(rec_offsets), dflags, &len, 0, nullptr);
+    if (!rc) rc = encode_impl(c, s, dc.data(), n, (uint8_t *)B.dev(out, out_cap), out_cap,
+                              (uint64_t *)B.dev(rec_offsets, (n + 1) * 8), dflags, &len, 0, nullptr);
     const int fr = B.finish(c, rc == XDRG_OK);
     if (!rc && out_len) *out_len = len;
     return rc ? rc : fr;
@@ -1711,8 +1795,9 @@ static int bounce_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, u
     HIPCHK(c, hipStreamSynchronize(c->stream));
     rc = B.place(c);
     if (rc) { (void)B.finish(c, false); return rc; }
-    rc = map_cols(c, s, cols, n, true, dc, [&](const void *p, uint64_t) { return B.dev(p); });
-    if (!rc) rc = decode_impl(c, s, (const uint8_t *)B.dev(in), in_len, (const uint64_t *)B.dev(rec_offsets), n,
+    rc = map_cols(c, s, cols, n, true, dc, [&](const void *p, uint64_t b) { return B.dev(p, b); });
+    if (!rc) rc = decode_impl(c, s, (const uint8_t *)B.dev(in, in_len), in_len,
+                              (const uint64_t *)B.dev(rec_offsets, (n + 1) * 8), n,
                               dc.data(), dflags, first_bad, err, 0, nullptr);
     const bool dec_err = rc && *err;   // a decode error: the records before it are delivered
     const int fr = B.finish(c, rc == XDRG_OK || dec_err);
@@ -1725,8 +1810,12 @@ static int host_common(xdrg_ctx *c, const xdrg_schema *s, uint32_t flags) {
     return XDRG_OK;
 }
 
+// byref / splice: xdrg_encode_batch_shallow on host memory — the payload
+// field's values are never read (nor staged: only the heads cross PCIe), its
+// offsets are; splice is a host array of n entries.
 static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, uint8_t *out,
-                       uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len) {
+                       uint64_t out_cap, uint64_t *rec_offsets, uint32_t flags, uint64_t *out_len,
+                       uint32_t byref, uint64_t *splice) {
     int rc = host_common(c, s, flags);
     if (rc) return rc;
     DeviceGuard dg;
@@ -1736,14 +1825,17 @@ static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
     rc = check_columns(c, s, cols, n, false);
     if (rc) return rc;
     const uint32_t dflags = flags & XDRG_FRAME_RM;
+    if (byref && s->ngroups) return inval(c, "by-reference payloads in a schema with repeated groups");
     if (flags & XDRG_HOST_MAPPED) {
         std::vector<xdrg_column> dc;
-        rc = mapped_cols(c, s, cols, n, false, dc);
+        rc = mapped_cols(c, s, cols, n, false, dc, byref);
         if (rc) return rc;
         uint8_t *dout = n ? (uint8_t *)span_device(out, out_cap) : out;
         uint64_t *drec = rec_offsets ? (uint64_t *)span_device(rec_offsets, (n + 1) * 8) : nullptr;
         if ((n && !dout) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
-        return encode_impl(c, s, dc.data(), n, dout, out_cap, drec, dflags, out_len, 0, nullptr);
+        uint64_t *dspl = byref && n ? (uint64_t *)span_device(splice, n * 8) : splice;
+        if (byref && n && !dspl) return inval(c, "XDRG_HOST_MAPPED: splice positions not registered");
+        return encode_impl(c, s, dc.data(), n, dout, out_cap, drec, dflags, out_len, byref, dspl);
     }
     if (s->nested) return bounce_encode(c, s, cols, n, out, out_cap, rec_offsets, dflags, out_len);
     hs::Schema v;
@@ -1752,16 +1844,19 @@ static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));   // the caller's earlier work on this context
     HipExec x(c, s);
-    rc = hs::stage_encode(x, v, cols, n, out, out_cap, rec_offsets, dflags, out_len);
+    rc = hs::stage_encode(x, v, cols, n, out, out_cap, rec_offsets, dflags, out_len, byref, splice);
     const int fr = x.finish();
     if (rc == XDRG_E_CAPACITY) c->err = "output buffer too small";
     else if (rc == XDRG_E_INVAL && c->err.empty()) c->err = "host columns: unsupported layout";
     return rc ? rc : fr;
 }
 
+// byref / payload_pos: xdrg_decode_batch_view on host memory — the stream
+// is staged, the payload field's offsets come back as for a copy, its values
+// are never written, payload_pos (host, n) = offsets in `in`.
 static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t in_len,
                        const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
-                       uint64_t *first_bad, int *err) {
+                       uint64_t *first_bad, int *err, uint32_t byref, uint64_t *payload_pos) {
     int rc = host_common(c, s, flags);
     if (rc) return rc;
     DeviceGuard dg;
@@ -1772,14 +1867,17 @@ static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
     rc = check_columns(c, s, cols, n, true);
     if (rc) return rc;
     const uint32_t dflags = flags & XDRG_FRAME_RM;
+    if (byref && s->ngroups) return inval(c, "payload views in a schema with repeated groups");
     if (flags & XDRG_HOST_MAPPED) {
         std::vector<xdrg_column> dc;
-        rc = mapped_cols(c, s, cols, n, true, dc);
+        rc = mapped_cols(c, s, cols, n, true, dc, byref);
         if (rc) return rc;
         const uint8_t *din = in_len ? (const uint8_t *)span_device(in, in_len) : in;
         const uint64_t *drec = rec_offsets ? (const uint64_t *)span_device(rec_offsets, (n + 1) * 8) : nullptr;
         if ((in_len && !din) || (rec_offsets && !drec)) return inval(c, "XDRG_HOST_MAPPED: stream / offsets not registered");
-        return decode_impl(c, s, din, in_len, drec, n, dc.data(), dflags, first_bad, err, 0, nullptr);
+        uint64_t *dpos = byref && n ? (uint64_t *)span_device(payload_pos, n * 8) : payload_pos;
+        if (byref && n && !dpos) return inval(c, "XDRG_HOST_MAPPED: payload positions not registered");
+        return decode_impl(c, s, din, in_len, drec, n, dc.data(), dflags, first_bad, err, byref, dpos);
     }
     if (s->nested) return bounce_decode(c, s, in, in_len, rec_offsets, n, cols, dflags, first_bad, err);
     hs::Schema v;
@@ -1788,7 +1886,7 @@ static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HipExec x(c, s);
-    rc = hs::stage_decode(x, v, in, in_len, rec_offsets, n, cols, dflags, first_bad, err);
+    rc = hs::stage_decode(x, v, in, in_len, rec_offsets, n, cols, dflags, first_bad, err, byref, payload_pos);
     const int fr = x.finish();
     if (rc && rc != XDRG_E_INVAL && rc != XDRG_E_HIP && rc != XDRG_E_NOMEM) c->err = xdrg_status_string(rc);
     else if (rc == XDRG_E_INVAL && c->err.empty()) c->err = "host columns: unsupported layout";
@@ -2183,7 +2281,8 @@ static int multi_args(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *s
     if (!ctxs || !s || !counts || nctx == 0 || nctx > (uint32_t)kMaxGatherSeg / 2) return XDRG_E_INVAL;
     for (uint32_t i = 0; i < nctx; ++i)
         if (!ctxs[i]) return XDRG_E_INVAL;
-    if (flags & ~XDRG_FRAME_RM) return inval(ctxs[0], "multi-GPU calls are synchronous (no XDRG_ASYNC)");
+    if (flags & ~XDRG_FRAME_RM)   // synchronous, device memory (xdrg_device_alloc / xdrg_copy for a JVM)
+        return inval(ctxs[0], "multi-GPU calls take XDRG_FRAME_RM only (device memory, synchronous)");
     if (s->ngroups) return inval(ctxs[0], "multi-GPU calls take schemas without repeated groups");
     return XDRG_OK;
 }

@@ -321,6 +321,8 @@ struct GatherArgs {             // copy bytes[s] from src[s] (a peer's HBM) to d
 };
 int launch_gather(const GatherArgs &a, void *stream);
 int launch_add_u64(uint64_t *p, uint64_t n, uint64_t delta, void *stream);   // p[0..n) += delta
+// p[i] += delta for every p[i] != UINT64_MAX (splice / payload positions: UINT64_MAX = absent)
+int launch_add_pos(uint64_t *p, uint64_t n, uint64_t delta, void *stream);
 // *dst = *index <= limit ? base[*index] : 0
 int launch_pick_u64(uint64_t *dst, const uint64_t *base, const uint64_t *index, uint64_t limit, void *stream);
 // dst[0..bytes) = src[0..bytes) by the CUs, one side host memory the device maps

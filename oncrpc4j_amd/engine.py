@@ -236,11 +236,12 @@ class Context:
         return rc, (None if async_ else fb.value), (None if async_ else er.value)
 
     def encode_shallow(self, schema, cols, n, out, out_cap, field, splice, rec_offsets=None,
-                       framed=False):
+                       framed=False, host=False, mapped=False):
         """xdrg_encode_batch_shallow: field `field` travels by reference
         (xdrEncodeFileChunk, Xdr.java:978-988); splice[i] = where record i's
-        payload + zero pad go in its message.  -> bytes written to out."""
-        flags = abi.FRAME_RM if framed else 0
+        payload + zero pad go in its message.  -> bytes written to out.
+        host / mapped as for encode (the payload's values never cross)."""
+        flags = self._flags(framed, False, host, mapped)
         carr = cols if isinstance(cols, ctypes.Array) else columns_array(cols)
         ol = ctypes.c_uint64(0)
         rc = lib().xdrg_encode_batch_shallow(self._h, schema.handle, carr, int(n), _ptr(out),
@@ -251,10 +252,11 @@ class Context:
         return ol.value
 
     def decode_view(self, schema, xdr, xdr_len, n, cols, field, payload_pos, rec_offsets=None,
-                    framed=False, raise_on_error=True):
+                    framed=False, raise_on_error=True, host=False, mapped=False):
         """xdrg_decode_batch_view: field `field` decodes as a stream slice
-        (xdrDecodeByteBuffer, Xdr.java:423-439) -> (status, first_bad, err)."""
-        flags = abi.FRAME_RM if framed else 0
+        (xdrDecodeByteBuffer, Xdr.java:423-439) -> (status, first_bad, err).
+        host / mapped as for decode."""
+        flags = self._flags(framed, False, host, mapped)
         carr = cols if isinstance(cols, ctypes.Array) else columns_array(cols)
         fb = ctypes.c_uint64(0)
         er = ctypes.c_int(0)
@@ -265,6 +267,25 @@ class Context:
         if rc and raise_on_error:
             _raise(rc, self._h, fb.value)
         return rc, fb.value, er.value
+
+    def device_alloc(self, nbytes):
+        """xdrg_device_alloc -> device address (int); free with device_free."""
+        p = ctypes.c_void_p()
+        rc = lib().xdrg_device_alloc(self._h, int(nbytes), ctypes.byref(p))
+        if rc:
+            _raise(rc, self._h)
+        return p.value
+
+    def device_free(self, ptr):
+        rc = lib().xdrg_device_free(self._h, _ptr(ptr))
+        if rc:
+            _raise(rc, self._h)
+
+    def copy(self, dst, src, nbytes, kind):
+        """xdrg_copy (kind: abi.COPY_H2D / COPY_D2H / COPY_D2D), synchronous."""
+        rc = lib().xdrg_copy(self._h, _ptr(dst), _ptr(src), int(nbytes), int(kind))
+        if rc:
+            _raise(rc, self._h)
 
     def frame_scan(self, data, length, msg_offsets, cap, host=False, mapped=False, with_consumed=False):
         """xdrg_frame_scan (device) / xdrg_frame_scan_ex (host=True: a host socket

@@ -91,21 +91,35 @@ struct CpuExec {
         for (uint64_t i = 0; i < n; ++i) p[i] += d;
         return XDRG_OK;
     }
+    int add_pos(uint64_t *p, uint64_t n, uint64_t d) {
+        CHECK(in_arena((uint8_t *)p, n * 8));
+        for (uint64_t i = 0; i < n; ++i)
+            if (p[i] != UINT64_MAX) p[i] += d;
+        return XDRG_OK;
+    }
     int encode(uint32_t s, const xdrg_column *dc, uint64_t m, uint8_t *out, uint64_t cap, uint64_t *rec,
-               uint32_t flags) {
+               uint32_t flags, uint32_t byref, uint64_t *ref) {
         CHECK(in_arena(out, cap));
         uint64_t len = 0;
-        const int rc = xo_encode_batch_cond(fields, nf, conds, nc, dc, m, out, cap, rec, flags, &len);
+        if (byref) CHECK(dc[byref - 1].data == nullptr && in_arena((const uint8_t *)ref, m * 8));
+        const int rc = byref ? xo_encode_batch_shallow(fields, nf, conds, nc, dc, m, out, cap, rec, flags, &len,
+                                                       byref - 1, ref)
+                             : xo_encode_batch_cond(fields, nf, conds, nc, dc, m, out, cap, rec, flags, &len);
         CHECK(rc == XDRG_OK);   // the slot span is sized to the chunk's bound
         res[s][0] = len;
         return XDRG_OK;
     }
     int decode(uint32_t s, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m, xdrg_column *dc,
-               uint32_t flags) {
+               uint32_t flags, uint32_t byref, uint64_t *ref) {
         CHECK(len == 0 || in_arena(in, len) || (in == bodyb.data() && len <= bodyb.size()));
         uint64_t fb = 0;
         int err = 0;
-        (void)xo_decode_batch_cond(fields, nf, conds, nc, in, len, rec, m, dc, flags, &fb, &err);
+        if (byref) {
+            CHECK(dc[byref - 1].data == nullptr && in_arena((const uint8_t *)ref, m * 8));
+            (void)xo_decode_batch_view(fields, nf, conds, nc, in, len, rec, m, dc, flags, &fb, &err, byref - 1, ref);
+        } else {
+            (void)xo_decode_batch_cond(fields, nf, conds, nc, in, len, rec, m, dc, flags, &fb, &err);
+        }
         res[s][0] = fb;
         res[s][1] = (uint64_t)(uint32_t)err;
         return XDRG_OK;
@@ -631,6 +645,105 @@ static uint64_t receive_rounds(std::mt19937_64 &g, int rounds) {
     return windows;
 }
 
+// By reference (hs::stage_encode / stage_decode with byref: the host forms
+// of xdrg_encode_batch_shallow / xdrg_decode_batch_view) against the oracle's
+// whole-batch xo_encode_batch_shallow / xo_decode_batch_view: heads, record
+// offsets, splice / payload positions, errors; the payload column is NULL
+// throughout (never read, never staged, never written).
+static void byref_rounds(std::mt19937_64 &g, int rounds) {
+    uint64_t errs = 0, absent = 0;
+    for (int r = 0; r < rounds; ++r) {
+        Batch b;
+        random_schema(g, b);
+        // the by-reference field: a dynamic opaque / string (one appended if none)
+        std::vector<uint32_t> cand;
+        for (uint32_t k = 0; k < b.f.size(); ++k)
+            if (b.f[k].kind == XDRG_K_DYNAMIC && (b.f[k].type == XDRG_T_OPAQUE || b.f[k].type == XDRG_T_STRING))
+                cand.push_back(k);
+        if (cand.empty()) {
+            b.f.push_back({XDRG_T_OPAQUE, XDRG_K_DYNAMIC, 0, 0});
+            b.hs.f.push_back({XDRG_T_OPAQUE, XDRG_K_DYNAMIC, 0, 1, 1, 0, 0, 0});
+            b.hs.var_size = true;
+            for (auto &c : b.c) c.values = b.cvals.data();
+            cand.push_back((uint32_t)b.f.size() - 1);
+        }
+        const uint32_t fld = cand[g() % cand.size()];
+        b.n = g() % 5 == 0 ? g() % 4 : g() % 1200;
+        random_values(g, b, false);
+        for (auto &c : b.c) c.values = b.cvals.data();
+        const uint32_t flags = g() % 2 ? XDRG_FRAME_RM : 0;
+        const uint32_t nc = (uint32_t)b.c.size();
+        const xdrg_cond *cp = nc ? b.c.data() : nullptr;
+        // whole-batch oracle: heads + splice, then the full stream for the view
+        std::vector<uint8_t> want(1 << 22), deep(1 << 22);
+        std::vector<uint64_t> wro(b.n + 1), wspl(b.n + 1), dro(b.n + 1);
+        uint64_t wlen = 0, dlen = 0;
+        CHECK(xo_encode_batch_shallow(b.f.data(), b.f.size(), cp, nc, b.cols.data(), b.n, want.data(), want.size(),
+                                      wro.data(), flags, &wlen, fld, wspl.data()) == XDRG_OK);
+        CHECK(xo_encode_batch_cond(b.f.data(), b.f.size(), cp, nc, b.cols.data(), b.n, deep.data(), deep.size(),
+                                   dro.data(), flags, &dlen) == XDRG_OK);
+        {
+            std::vector<xdrg_column> cols = b.cols;
+            cols[fld].data = nullptr;
+            CpuExec x = make_exec(g, b);
+            const uint64_t cap = wlen + g() % 64;
+            std::vector<uint8_t> out(cap + 16, 0xee);
+            std::vector<uint64_t> ro(b.n + 1, 0x99), spl(b.n + 1, 0x99);
+            uint64_t len = 0;
+            const int rc = hs::stage_encode(x, b.hs, cols.data(), b.n, out.data(), cap, g() % 3 ? ro.data() : nullptr,
+                                            flags, &len, fld + 1, spl.data());
+            CHECK(rc == XDRG_OK && len == wlen);
+            CHECK(std::memcmp(out.data(), want.data(), wlen) == 0);
+            for (uint64_t i = wlen; i < out.size(); ++i) CHECK(out[i] == 0xee);
+            if (ro[0] != 0x99)
+                for (uint64_t i = 0; i <= b.n; ++i) CHECK(ro[i] == wro[i]);
+            for (uint64_t i = 0; i < b.n; ++i) {
+                CHECK(spl[i] == wspl[i]);
+                absent += spl[i] == UINT64_MAX;
+            }
+            CHECK(spl[b.n] == 0x99);
+        }
+        // the view decode of the full stream, sometimes cut short or corrupted
+        std::vector<uint8_t> stream(deep.begin(), deep.begin() + (long)dlen);
+        uint64_t in_len = dlen;
+        const int mut = (int)(g() % 4);
+        if (mut == 1 && in_len) in_len = (g() % in_len) & ~3ull;
+        if (mut == 2 && b.n) {
+            const uint64_t i = g() % b.n, o = dro[i] + ((g() % 4) * 4);
+            if (o + 4 <= dlen) { stream[o] = 0x80; stream[o + 1] = (uint8_t)g(); }
+        }
+        stream.resize(dlen + 16, 0);
+        Batch a, o;
+        std::mt19937_64 g2 = g;
+        empty_like(g, b, a, 0);
+        empty_like(g2, b, o, 0);
+        for (Batch *t : {&a, &o}) {   // the view's column: no values, no capacity
+            t->data[fld].assign(b.offs[fld][b.n] + 8, 0x33);
+            t->cols[fld].data = nullptr;
+            t->cols[fld].cap = 0;
+        }
+        std::vector<uint64_t> wpos(b.n + 1, 0x99), pos(b.n + 1, 0x99);
+        uint64_t fb_w = 0, fb = 0;
+        int err_w = 0, err = 0;
+        const int rc_w = xo_decode_batch_view(b.f.data(), b.f.size(), cp, nc, stream.data(), in_len, dro.data(), b.n,
+                                              o.cols.data(), flags, &fb_w, &err_w, fld, wpos.data());
+        CpuExec x = make_exec(g, b);
+        const int rc = hs::stage_decode(x, b.hs, stream.data(), in_len, dro.data(), b.n, a.cols.data(), flags, &fb, &err,
+                                        fld + 1, pos.data());
+        if (!(rc == rc_w && fb == fb_w && err == err_w))
+            std::fprintf(stderr, "byref round %d: rc %d/%d fb %llu/%llu err %d/%d n %llu mut %d\n", r, rc, rc_w,
+                         (unsigned long long)fb, (unsigned long long)fb_w, err, err_w, (unsigned long long)b.n, mut);
+        CHECK(rc == rc_w && fb == fb_w && err == err_w);
+        for (uint64_t i = 0; i < fb; ++i) CHECK(pos[i] == wpos[i]);
+        CHECK(pos[b.n] == 0x99);
+        compare_prefix(a, o, fb);
+        errs += rc != 0;
+    }
+    CHECK(errs > 0 && absent > 0);
+    std::printf("san_stage: %d by-reference rounds ok (%llu decode errors, %llu absent payloads)\n", rounds,
+                (unsigned long long)errs, (unsigned long long)absent);
+}
+
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 300;
     std::mt19937_64 g(0x0DCAC4E5);
@@ -735,6 +848,7 @@ int main(int argc, char **argv) {
     }
     CHECK(chunks_grown > 0 && errs > 0 && caps > 0 && bounced > 0 && direct > 0 && group_rounds > 0);
     std::printf("san_stage: %llu rounds with a repeated group\n", (unsigned long long)group_rounds);
+    byref_rounds(g, rounds);
     const uint64_t rx = receive_rounds(g, rounds);
     std::printf("san_stage: %d receive rounds ok (%llu windows)\n", rounds, (unsigned long long)rx);
     std::printf("san_stage: %d rounds ok (ring grown %llu times, %llu decode errors, %llu capacity, "

@@ -26,6 +26,14 @@ fixtures are plain JSON data and travel, this script's inputs do not need to.
    list elements (rpcgen/chunk_map.x), packed by xdrlib.
    volume_index_vectors.json — a list and a counted array of structs inside
    list elements (rpcgen/volume_index.x), packed by xdrlib.
+6. reference_rpcgen_vectors.json — the arguments and results of the
+   reference's own rpcgen test programs, oncrpc4j-rpcgen/src/test/xdr/
+   BlobStore.x (put(Key, Value) / get(Key) -> Value, Value a bool union over
+   opaque<1024>) and Calculator.x (add(hyper, hyper) -> CalculationResult,
+   addSimple(hyper, hyper) -> hyper), packed by xdrlib from those
+   declarations (jrpcgen.java:758-913 codingMethod, :1240-1340 unions).  The
+   fixture holds data only: the tapes the engine must derive and the packed
+   bytes; the .x files stay in the reference.
 """
 import json
 import os
@@ -759,12 +767,93 @@ def rpc_vectors(seed=0x5EED):
                       "records": calls, "stream": stream.hex(), "rec_offsets": offs}}
 
 
+# ---- the reference's own rpcgen inputs (BlobStore.x, Calculator.x) -------------
+RPCGEN_REF = "oncrpc4j-rpcgen/src/test/xdr/"
+
+
+def reference_rpcgen_vectors(seed=0xB10B):
+    """Each message shape is packed from its declarations, argument by
+    argument in declaration order (jrpcgen's generated xdrEncode): Key =
+    struct { opaque data<16>; }, Value = union switch (bool notNull) { case
+    TRUE: opaque data<1024>; case FALSE: void; }, CalculationResult = struct
+    { hyper result; unsigned hyper startMillis; unsigned hyper finishMillis; }."""
+    rng = random.Random(seed)
+
+    def key():
+        return [bytes(rng.randrange(256) for _ in range(rng.choice([0, 1, 5, 8, 16, rng.randrange(17)])))]
+
+    def value():
+        nn = rng.randrange(4) != 0   # mostly TRUE, some FALSE (void arm)
+        data = bytes(rng.randrange(256) for _ in range(rng.choice([0, 3, 4, 64, 1024, rng.randrange(1025)]))) \
+            if nn else b""
+        return [int(nn), data]
+
+    def pack_key(p, r):
+        p.pack_opaque(r[0])
+
+    def pack_value(p, r):
+        p.pack_int(r[0])   # bool discriminant (xdrEncodeBoolean: 1 / 0)
+        if r[0]:
+            p.pack_opaque(r[1])
+
+    def hyper():
+        return rng.choice([0, -1, 1, -2**63, 2**63 - 1, rng.randrange(-2**63, 2**63)])
+
+    def uhyper():
+        return rng.choice([0, 2**64 - 1, 2**63, rng.randrange(2**64)])
+
+    KEY, VAL = [[T_OPAQUE, K_DYNAMIC, 0]], [[T_BOOL, K_SCALAR, 0], [T_OPAQUE, K_DYNAMIC, 0]]
+    H, UH = [T_HYPER, K_SCALAR, 0], [T_UHYPER, K_SCALAR, 0]
+    shapes = [
+        # name, program, version, procedure, which, fields, conds, make record, pack record
+        ("BlobStore.put args", 118, 1, 1, "args", KEY + VAL, [[2, 1, 0, [1]]],
+         lambda: key() + value(), lambda p, r: (pack_key(p, r[:1]), pack_value(p, r[1:]))),
+        ("BlobStore.get args", 118, 1, 2, "args", KEY, [], key, pack_key),
+        ("BlobStore.get result", 118, 1, 2, "result", VAL, [[1, 0, 0, [1]]], value, pack_value),
+        ("Calculator.add args", 117, 1, 1, "args", [H, H], [], lambda: [hyper(), hyper()],
+         lambda p, r: (p.pack_hyper(r[0]), p.pack_hyper(r[1]))),
+        ("Calculator.add result", 117, 1, 1, "result", [H, UH, UH], [], lambda: [hyper(), uhyper(), uhyper()],
+         lambda p, r: (p.pack_hyper(r[0]), p.pack_uhyper(r[1]), p.pack_uhyper(r[2]))),
+        ("Calculator.addSimple args", 117, 1, 2, "args", [H, H], [], lambda: [hyper(), hyper()],
+         lambda p, r: (p.pack_hyper(r[0]), p.pack_hyper(r[1]))),
+        ("Calculator.addSimple result", 117, 1, 2, "result", [H], [], lambda: [hyper()],
+         lambda p, r: p.pack_hyper(r[0])),
+    ]
+    out = {"source": "CPython 3.10 stdlib xdrlib (RFC 1014) packing the arguments / results of the reference's "
+                     "rpcgen test programs from their declarations", "seed": seed,
+           "cite": {"BlobStore.x": RPCGEN_REF + "BlobStore.x", "Calculator.x": RPCGEN_REF + "Calculator.x",
+                    "encode order": "oncrpc4j-rpcgen/src/main/java/org/acplt/oncrpc/apps/jrpcgen/jrpcgen.java:"
+                                    "758-913, 1240-1340"},
+           "messages": []}
+    for name, prog, vers, proc, which, fields, conds, make, pack in shapes:
+        for framed in (False, True):
+            n = 40
+            records, chunks = [], []
+            for _ in range(n):
+                r = make()
+                p = xdrlib.Packer()
+                pack(p, r)
+                body = p.get_buffer()
+                if framed:
+                    body = struct.pack(">I", len(body) | 0x80000000) + body
+                chunks.append(body)
+                records.append([x.hex() if isinstance(x, bytes) else x for x in r])
+            offs = [0]
+            for ch in chunks:
+                offs.append(offs[-1] + len(ch))
+            out["messages"].append({"name": name, "program": prog, "version": vers, "procedure": proc,
+                                    "which": which, "framed": framed, "fields": fields, "conds": conds, "n": n,
+                                    "records": records, "xdr": b"".join(chunks).hex(), "rec_offsets": offs})
+    return out
+
+
 GENERATORS = {"kat_reference.json": kat_reference, "kat_jdk_nan.json": kat_jdk_nan,
               "xdrlib_vectors.json": xdrlib_vectors, "framing.json": framing, "rpc_vectors.json": rpc_vectors,
               "cond_vectors.json": cond_vectors, "group_vectors.json": group_vectors,
               "group_cond_vectors.json": group_cond_vectors,
               "chunk_map_vectors.json": chunk_map_vectors,
-              "volume_index_vectors.json": volume_index_vectors}
+              "volume_index_vectors.json": volume_index_vectors,
+              "reference_rpcgen_vectors.json": reference_rpcgen_vectors}
 
 
 def main(names=None):

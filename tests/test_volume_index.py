@@ -333,3 +333,65 @@ def test_gpu_volume_index_host_ptrs(kind):
     finally:
         mem.close()
         c.close()
+
+
+def _empty_members_batches():
+    """Batches whose inner columns hold nothing: every inner string / label
+    empty, volumes without extents or entries, and no records at all."""
+    rng = np.random.default_rng(31)
+    out = []
+    hb = _random(300, 41)   # every string empty (offsets all 0)
+    for k in (WHO, LABEL):
+        vals, offs = hb.arrays[k]
+        hb.arrays[k] = (np.zeros(0, np.uint8), np.zeros_like(offs))
+    out.append(("empty_strings", hb))
+    hb = random_batch(FIELDS, 200, seed=43, dyn_len=(0, 24), group_len=(1, 4), inner_len=(0, 0))
+    hb.arrays[9][:] = rng.integers(0, 2, hb.arrays[9].shape[0], dtype=np.uint8)
+    hb.arrays[14][:] = rng.integers(0, 2, hb.arrays[14].shape[0], dtype=np.uint8)
+    for k in range(len(FIELDS)):   # the inner groups' member columns: zero rows, zero-length arrays
+        if hb.rows(k) == 0 and FIELDS[k][0] != abi.T_GROUP:
+            a = hb.arrays[k]
+            hb.arrays[k] = ((a[0][:0], a[1][:1]) if FIELDS[k][1] == abi.K_DYNAMIC else a[:0])
+    out.append(("no_inner_elements", hb))
+    out.append(("no_records", random_batch(FIELDS, 0, seed=44)))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["pageable", "registered", "mapped"])
+def test_gpu_volume_index_host_empty_members(kind):
+    """Nested schema on host memory with columns that hold no bytes (ADVICE
+    r4: the bounce path mapped zero-byte spans to nothing and copied a fixed
+    member's row out of a zero-row column): encode == oracle, decode == the
+    batch, into zero-length member arrays."""
+    import torch
+    from oncrpc4j_amd import engine
+    from hostmem import Pageable, Registered, moved
+    assert torch.cuda.is_available()
+    c = engine.Context(0)
+    mem = Pageable() if kind == "pageable" else Registered()
+    host, mapped = kind != "mapped", kind == "mapped"
+    try:
+        for name, hb0 in _empty_members_batches():
+            n = hb0.n
+            rc, want, offs = oracle.encode_batch(FIELDS, hb0.columns(), n, hb0.xdr_total() + 64, conds=CONDS)
+            assert rc == 0, name
+            ref = HostBatch.empty(FIELDS, n, hb0.dyn_caps())
+            assert oracle.decode_batch(FIELDS, want, offs, n, ref.columns(), conds=CONDS) == (0, n, 0), name
+            hb = moved(hb0, mem)
+            sch = engine.Schema(FIELDS, CONDS)
+            out = mem.array(np.zeros(len(want) + 64, np.uint8))
+            ro = mem.array(np.zeros(n + 1, np.uint64))
+            ln = c.encode(sch, hb.columns(), n, out, len(want) + 64, rec_offsets=ro, host=host, mapped=mapped)
+            assert out[:ln].tobytes() == want and np.array_equal(ro, offs), name
+            back0 = HostBatch.empty(FIELDS, n, hb0.dyn_caps())
+            for k in range(len(FIELDS)):   # zero-row member columns as zero-length arrays
+                if FIELDS[k][0] != abi.T_GROUP and back0.rows(k) == 0 and n:
+                    a = back0.arrays[k]
+                    back0.arrays[k] = (a[0][:0], a[1][:1]) if FIELDS[k][1] == abi.K_DYNAMIC else a[:0]
+            back = moved(back0, mem)
+            assert c.decode(sch, out, ln, n, back.columns(), rec_offsets=ro, host=host, mapped=mapped) == (0, n, 0), name
+            assert back.equal(ref), name
+    finally:
+        mem.close()
+        c.close()
