@@ -923,6 +923,19 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
 // serial walk).
 enum RecvMode { RECV_SCAN = 0, RECV_DEFRAME = 1, RECV_DECODE = 2 };
 
+// Schemas whose decode a receive window carries: repeated groups one level
+// deep (an inner group inside an element is moved whole by the caller) whose
+// elements take at least one XDR byte each, so a window's bytes bound its
+// element rows.
+inline bool recv_groups_ok(const Schema &s) {
+    for (const Field &f : s.f) {
+        if (!is_group(f)) continue;
+        if (f.grp) return false;
+        if (f.kind != XDRG_K_FIXED && f.emin == 0) return false;
+    }
+    return true;
+}
+
 struct RecvResult {
     uint64_t n_msgs = 0, consumed = 0, first_bad = 0, payload = 0;
     int err = XDRG_OK;
@@ -940,18 +953,29 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
                   RecvResult &out) {
     out = RecvResult();
     std::vector<Region> regs;
+    // the counted columns (stage_decode's): dynamic fields (values) and
+    // DYNAMIC / LIST groups (elements, whose member rows ride with the window)
     std::vector<uint32_t> dyn;
     uint64_t minmsg = 4;   // a mark
     if (mode == RECV_DECODE) {
-        if (sp->groups) return XDRG_E_INVAL;   // (group schemas: device or mapped receive)
+        if (!recv_groups_ok(*sp)) return XDRG_E_INVAL;
         HS_TRY(build_regions(*sp, cols, regs));
         for (const Region &g : regs)
             if (!g.stride) return XDRG_E_INVAL;   // constant columns are encode-only
         for (uint32_t k = 0; k < sp->f.size(); ++k)
-            if (sp->f[k].kind == XDRG_K_DYNAMIC) dyn.push_back(k);
+            if (sp->f[k].kind == XDRG_K_DYNAMIC || (is_group(sp->f[k]) && sp->f[k].kind != XDRG_K_FIXED))
+                dyn.push_back(k);
         if (dyn.size() > 32) return XDRG_E_INVAL;
         minmsg += sp->min_xdr;
     }
+    // rows of field k's column for `msgs` messages in a window of W bytes:
+    // messages, or the elements of its group (FIXED: msgs x count; else at most
+    // one per emin bytes of the window, as stage_decode's elem_bound)
+    auto rows_in = [&](uint32_t k, uint64_t msgs, uint64_t W) -> uint64_t {
+        if (!sp->f[k].grp) return msgs;
+        const Field &gf = sp->f[sp->f[k].grp - 1];
+        return gf.kind == XDRG_K_FIXED ? msgs * gf.count : W / gf.emin + 1;
+    };
     if (msg_offsets) msg_offsets[0] = 0;
     if (cap == 0 || len < 4) return XDRG_E_INCOMPLETE;
     Stager<X> st(x);
@@ -974,9 +998,13 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
         g.cols = b.used;
         if (mode == RECV_DECODE) {
             // (a window's regions keep their host address modulo 16: the worst case)
-            for (const Region &r : regs) b.take((uint64_t)r.stride * g.rows, 15);
+            for (const Region &r : regs) b.take((uint64_t)r.stride * rows_in(region_field0(r), g.rows, g.W), 15);
             for (uint32_t k : dyn) {
-                b.take((g.rows + 1) * 8);
+                if (is_group(sp->f[k])) {
+                    b.take((g.rows + 1) * 8);
+                    continue;
+                }
+                b.take((rows_in(k, g.rows, g.W) + 1) * 8);
                 b.take((g.W / sp->f[k].xsz + 1) * sp->f[k].nsz);
             }
         }
@@ -1032,32 +1060,39 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
         Chunk &c = pend.front();
         uint64_t w[2 + 32];
         HS_TRY(x.wait_kernel(c.slot, w));
-        uint64_t tot[32];
+        std::vector<uint64_t> tot(sp->f.size(), 0);   // per counted field: values / elements
         for (size_t i = 0; i < dyn.size(); ++i) {
             // a failing window's totals may not cover its valid prefix (a decode
             // stops at the error): it hands back every value it was granted
-            tot[i] = w[1] ? c.capg[dyn[i]] : std::min(w[2 + i], c.capg[dyn[i]]);
-            next_base[dyn[i]] = c.base[dyn[i]] + tot[i];
+            const uint32_t k = dyn[i];
+            tot[k] = w[1] ? c.capg[k] : std::min(w[2 + i], c.capg[k]);
+            next_base[k] = c.base[k] + tot[k];
         }
+        // rows of a field's column in this window and the first of them
+        auto rows_of = [&](uint32_t k) -> uint64_t {
+            if (!sp->f[k].grp) return c.m;
+            const uint32_t g = sp->f[k].grp - 1;
+            return sp->f[g].kind == XDRG_K_FIXED ? c.m * sp->f[g].count : tot[g];
+        };
+        auto first_of = [&](uint32_t k) -> uint64_t {
+            if (!sp->f[k].grp) return c.lo;
+            const uint32_t g = sp->f[k].grp - 1;
+            return sp->f[g].kind == XDRG_K_FIXED ? c.lo * sp->f[g].count : c.base[g];
+        };
         uint8_t *slot = x.slot(c.slot);
         HS_TRY(x.d2h_begin(c.slot));
         for (size_t r = 0; r < regs.size(); ++r) {
-            const Region &g = regs[r];
-            uint8_t *h = (uint8_t *)g.base + (uint64_t)g.stride * c.lo;
-            if (g.full) {
-                HS_TRY(st.d2h(c.slot, h, slot + c.L.reg[r], (uint64_t)g.stride * c.m));
-            } else {
-                for (auto &sg : g.segs)
-                    HS_TRY(st.d2h_2d(c.slot, h + sg.first, (uint64_t)g.stride, slot + c.L.reg[r] + sg.first,
-                                     sg.second - sg.first, c.m));
-            }
+            const uint32_t k0 = region_field0(regs[r]);
+            HS_TRY(st.d2h_region(c.slot, regs[r], first_of(k0), slot + c.L.reg[r], rows_of(k0)));
         }
-        for (size_t i = 0; i < dyn.size(); ++i) {
-            const uint32_t k = dyn[i];
-            HS_TRY(x.add_u64(1, (uint64_t *)(slot + c.L.off[k]), c.m + 1, c.base[k]));
-            HS_TRY(st.d2h(c.slot, cols[k].offsets + c.lo, slot + c.L.off[k], (c.m + 1) * 8));
-            HS_TRY(st.d2h(c.slot, (uint8_t *)cols[k].data + c.base[k] * sp->f[k].nsz, slot + c.L.val[k],
-                          tot[i] * sp->f[k].nsz));
+        for (uint32_t k : dyn) {
+            const bool grp = is_group(sp->f[k]);
+            const uint64_t rows = grp ? c.m : rows_of(k), first = grp ? c.lo : first_of(k);
+            HS_TRY(x.add_u64(1, (uint64_t *)(slot + c.L.off[k]), rows + 1, c.base[k]));
+            HS_TRY(st.d2h(c.slot, cols[k].offsets + first, slot + c.L.off[k], (rows + 1) * 8));
+            if (!grp)
+                HS_TRY(st.d2h(c.slot, (uint8_t *)cols[k].data + c.base[k] * sp->f[k].nsz, slot + c.L.val[k],
+                              tot[k] * sp->f[k].nsz));
         }
         st.busy[c.slot] = true;
         HS_TRY(x.d2h_done(c.slot));
@@ -1161,11 +1196,17 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             c.L.reg.assign(regs.size(), 0);
             c.L.off.assign(sp->f.size(), 0);
             c.L.val.assign(sp->f.size(), 0);
+            c.L.rows.assign(sp->f.size(), 0);
             c.base.assign(sp->f.size(), 0);
             c.capg.assign(sp->f.size(), 0);
+            for (uint32_t k2 = 0; k2 < sp->f.size(); ++k2) c.L.rows[k2] = rows_in(k2, m, cur.wl);
             std::vector<xdrg_column> dc(sp->f.size());
             for (size_t r = 0; r < regs.size(); ++r) {
-                c.L.reg[r] = b.take((uint64_t)regs[r].stride * m, (uintptr_t)(regs[r].base + (uint64_t)regs[r].stride * lo));
+                // (group members: the elements of the window's messages; a
+                // member region's host address is not known yet, so no modulus)
+                const uint32_t k0 = region_field0(regs[r]);
+                c.L.reg[r] = b.take((uint64_t)regs[r].stride * c.L.rows[k0],
+                                    regs[r].space ? 0 : (uintptr_t)(regs[r].base + (uint64_t)regs[r].stride * lo));
                 for (uint32_t k2 : regs[r].fields) {
                     dc[k2].data = slot + c.L.reg[r] + ((const uint8_t *)cols[k2].data - regs[r].base);
                     dc[k2].stride = cols[k2].stride;
@@ -1173,8 +1214,20 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             }
             for (uint32_t k2 = 0; k2 < sp->f.size(); ++k2) {
                 const Field &fd = sp->f[k2];
-                if (fd.kind == XDRG_K_DYNAMIC) {
+                if (is_group(fd)) {   // elements: after the windows before, within the window's bound
+                    if (fd.kind == XDRG_K_FIXED) {
+                        c.capg[k2] = m * fd.count;
+                        dc[k2].cap = c.capg[k2];
+                        continue;
+                    }
                     c.L.off[k2] = b.take((m + 1) * 8);
+                    c.base[k2] = next_base[k2];
+                    const uint64_t left = cols[k2].cap > c.base[k2] ? cols[k2].cap - c.base[k2] : 0;
+                    c.capg[k2] = std::min(left, c.L.rows[k2 + 1]);
+                    dc[k2].offsets = (uint64_t *)(slot + c.L.off[k2]);
+                    dc[k2].cap = c.capg[k2];
+                } else if (fd.kind == XDRG_K_DYNAMIC) {
+                    c.L.off[k2] = b.take((c.L.rows[k2] + 1) * 8);
                     const uint64_t vc = cur.wl / fd.xsz + 1;   // a window holds at most this many elements
                     c.L.val[k2] = b.take(vc * fd.nsz);
                     c.base[k2] = next_base[k2];
@@ -1198,9 +1251,26 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             } else {
                 HS_TRY(x.decode(cur.slot, x.body(), res[3], dboffs, m, dc.data(), 0, 0, nullptr));
             }
-            std::vector<const uint64_t *> extra;
-            for (uint32_t k2 : dyn) extra.push_back((const uint64_t *)(slot + c.L.off[k2]) + m);
-            HS_TRY(x.kernel_end(cur.slot, extra.data(), nullptr, nullptr, (uint32_t)extra.size()));
+            // totals (stage_decode's): a field's offsets at its last row; a
+            // member of a DYNAMIC / LIST group at the window's element total,
+            // read on the device when within the member's laid-out rows
+            std::vector<const uint64_t *> extra, index;
+            std::vector<uint64_t> limit;
+            for (uint32_t k2 : dyn) {
+                const Field &fd = sp->f[k2];
+                const uint64_t *o = (const uint64_t *)(slot + c.L.off[k2]);
+                limit.push_back(c.L.rows[k2]);
+                if (!fd.grp || is_group(fd)) {
+                    extra.push_back(o + m);
+                    index.push_back(nullptr);
+                } else {
+                    const Field &gf = sp->f[fd.grp - 1];
+                    extra.push_back(gf.kind == XDRG_K_FIXED ? o + m * gf.count : o);
+                    index.push_back(gf.kind == XDRG_K_FIXED ? nullptr
+                                                            : (const uint64_t *)(slot + c.L.off[fd.grp - 1]) + m);
+                }
+            }
+            HS_TRY(x.kernel_end(cur.slot, extra.data(), index.data(), limit.data(), (uint32_t)extra.size()));
             if (c.hoffs) {   // the caller's message offsets (without them the device copy stays
                 HS_TRY(x.d2h_begin(cur.slot));   // window-relative: an error reads one entry, settle)
                 HS_TRY(x.add_u64(1, doffs, m + 1, cur.hpos));

@@ -1498,10 +1498,16 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
         if (!(XDRG_EL_PROBE & 2) && js + tid < je) g_dec_record<false, true>(a, rb + js + tid, tile, a0 - xb, el);
         __syncthreads();   // descriptors
         const uint64_t nel = mE[je] - el.E0;
+        XDRG_DCHECK(nel <= a.dec_el);   // (the fit count bounded the sub-batch's elements)
         for (uint32_t i = tid; !(XDRG_EL_PROBE & 1) && i < nel; i += kRecThreads) {
             GRun run;
 #pragma unroll
             for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;
+            // the record walk left every element a tile position inside the staged
+            // bytes and member offsets inside the members' capacities
+            XDRG_DCHECK(dpos[i] < 16u * nch);
+            XDRG_DCHECK(el.nm < 1 || el.sb0 + drel[i] <= a.f[el.mk0].cap);
+            XDRG_DCHECK(el.nm < 2 || el.sb1 + drel[el.cap + i] <= a.f[el.mk1].cap);
             if (el.nm > 0) run.set(el.ms0, el.sb0 + drel[i]);
             if (el.nm > 1) run.set(el.ms1, el.sb1 + drel[el.cap + i]);
             GDisc d{};
@@ -1520,8 +1526,9 @@ template <bool NEST>
 static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) {
     const dim3 grid((uint32_t)a.nblocks), block(kRecThreads);
     const dim3 rgrid((uint32_t)((a.n + kRecThreads - 1) / kRecThreads));
-    const dim3 egrid((uint32_t)a.nblocks * enc_el_split(a.nblocks));
-    const bool esh = enc_el_split(a.nblocks) > 1;
+    const uint32_t split = a.enc_split ? a.enc_split : enc_el_split(a.nblocks);
+    const dim3 egrid((uint32_t)a.nblocks * split);
+    const bool esh = split > 1;
     switch (phase) {
     case GRP_ENC_SIZES:
         if (kWalkSplit > 1) {

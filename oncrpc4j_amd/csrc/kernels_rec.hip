@@ -892,6 +892,11 @@ __device__ __forceinline__ uint32_t mask_bytes(uint32_t v, int64_t valid) {
     return v & ((1u << (8 * valid)) - 1u);
 }
 
+// The low `n` bytes of a dword (n clamped to 0..4), in 32-bit arithmetic.
+__device__ __forceinline__ uint32_t lo_mask(int32_t n) {
+    return n <= 0 ? 0u : n >= 4 ? ~0u : (1u << (8 * n)) - 1u;
+}
+
 struct Chunk5 { uint32_t q0, q1, q2, q3, q4; };
 
 __device__ __forceinline__ uint32_t pow2_lanes(uint64_t bytes_per_rec, uint32_t bytes_per_lane) {
@@ -1555,17 +1560,6 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
     const uint64_t sh = R & 15;                    // record start inside chunk 0
     const uint64_t p0 = sh + a.pay_fb + 4;         // payload start, chunk coordinates
     const uint64_t cf = (p0 + 15) >> 4, cl = (p0 + cnt) >> 4;   // payload-only chunks: [cf, cl)
-    // the record's words outside those chunks (mark, fixed fields, length,
-    // the payload's first and last bytes, pad, trailing fixed fields): a word
-    // per lane, loaded before the payload so both round trips overlap
-    const uint64_t hw = cl > cf ? (16 * cf - sh) >> 2 : (size >> 2);   // head words
-    const uint64_t tw0 = cl > cf ? (16 * cl - sh) >> 2 : (size >> 2);  // first tail word
-    const uint64_t nslow = hw + (size >> 2) - tw0;
-#if !XDRG_PAY_OLD
-    uint32_t w0 = 0;
-    const uint64_t wi0 = lane < hw ? lane : tw0 + (lane - hw);
-    if (lane < nslow) w0 = payload_rec_word(a, r, 4 * wi0, size, src, cnt);
-#endif
     for (uint64_t c0 = cf + lane; c0 < cl; c0 += 4 * LPR) {   // payload-only chunks
         u32x4a v[4];
 #pragma unroll
@@ -1582,12 +1576,15 @@ __device__ __forceinline__ void enc_payload_rec(const RecArgs &a, uint64_t r) {
             __builtin_nontemporal_store(v[u], (u32x4n *)(A + 16 * c));
         }
     }
-#if !XDRG_PAY_OLD
-    if (lane < nslow) *(uint32_t *)(a.xdr + R + 4 * wi0) = w0;
-    for (uint64_t i = lane + LPR; i < nslow; i += LPR) {   // (records of > 64 such words: short payloads)
-#else
+    // the record's words outside those chunks (mark, fixed fields, length,
+    // the payload's first and last bytes, pad, trailing fixed fields): a word
+    // per lane, their loads in parallel.  (Loading them before the payload
+    // loop, to overlap the two round trips, measured slower: 6.41 vs 6.32 ms
+    // on 4 Mi config-3 records, profiles/r05_c3/pay_head_hoist_ab.jsonl.)
+    const uint64_t hw = cl > cf ? (16 * cf - sh) >> 2 : (size >> 2);   // head words
+    const uint64_t tw0 = cl > cf ? (16 * cl - sh) >> 2 : (size >> 2);  // first tail word
+    const uint64_t nslow = hw + (size >> 2) - tw0;
     for (uint64_t i = lane; i < nslow; i += LPR) {
-#endif
         const uint64_t wi = i < hw ? i : tw0 + (i - hw);
         *(uint32_t *)(a.xdr + R + 4 * wi) = payload_rec_word(a, r, 4 * wi, size, src, cnt);
     }
@@ -2045,10 +2042,13 @@ __device__ __forceinline__ uint64_t dyn_before(const RecArgs &a, const uint32_t 
 }
 
 // ---- encode -------------------------------------------------------------------
-// LDS: soff[RPB + 1] u32 (record offset - block offset) | srel[ND][RPB + 1] u32 | tile
-__host__ __device__ constexpr size_t enc_stage_meta(uint32_t nd) {
+// LDS: soff[RPB + 1] u32 (record offset - block offset) | srel[ND][RPB + 1] u32 |
+// pad masks [17][4] u32 | tile
+constexpr uint32_t kPadMasks = 17 * 16;   // row i: the dwords of 16 bytes whose first i are kept
+__host__ __device__ constexpr size_t enc_stage_rows(uint32_t nd) {
     return ((size_t)(nd + 1) * (kRecPerBlock + 1) * 4 + 15) & ~(size_t)15;
 }
+__host__ __device__ constexpr size_t enc_stage_meta(uint32_t nd) { return enc_stage_rows(nd) + kPadMasks; }
 
 // The whole block writes record r at stream offset pos from the native
 // columns (records too large for the tile).
@@ -2119,7 +2119,10 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
     constexpr uint32_t RS = kRecPerBlock + 1;   // row stride of soff / srel
     uint32_t *soff = (uint32_t *)smem;
     uint32_t *srel = soff + RS;
+    uint32_t *padm = (uint32_t *)(smem + enc_stage_rows(a.ndyn));
     uint8_t *tile = smem + enc_stage_meta(a.ndyn);
+    if (threadIdx.x < kPadMasks / 4)   // (read after the prologue's barrier)
+        padm[threadIdx.x] = lo_mask((int32_t)(threadIdx.x >> 2) - 4 * (int32_t)(threadIdx.x & 3));
     const uint64_t total = a.totals[0];
     if (total > a.xdr_cap) return;  // XDRG_E_CAPACITY: write nothing
     if (a.big_rec && block_is_big(a, false)) return;   // the group kernel's block
@@ -2217,52 +2220,98 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
         if (!(XDRG_ENC_PROBE & 8)) stage_copy(tile, a0, cb, a.ndyn);   // (stage_dma measured 3.70 vs 3.62 ms here: nothing to overlap)
         __syncthreads();
         const uint32_t m = je - js;
+        // tile offset of element 0 of the block's dynamic column d, minus its
+        // 16-aligned staged start (wave-uniform): element e of the column sits
+        // at tile byte tadj[d] + e * esz.  Everything below is 32-bit
+        // (block-relative offsets < 2^32, the `wide` check), stores address
+        // the block's output as a uniform base + 32-bit lane offset.
+        int32_t tadj[kMaxDynLds];
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d) {
+            tadj[d] = 0;
+            if ((uint32_t)d >= a.ndyn) continue;
+            const VField &f = a.f[a.dyn_idx[d]];
+            const uint64_t esz = f.xsz == 1 ? 1 : f.nsz;
+            tadj[d] = (int32_t)(16 * cb[d]) + (int32_t)((uintptr_t)(f.data + base[d] * esz) - (uintptr_t)a0[d]);
+        }
         {   // record-major scatter: a group of lanes writes all of a record
-            const uint64_t rbytes = (uint64_t)(soff[je] - soff[js]) / m;
+            const uint32_t rbytes = (soff[je] - soff[js]) / m;
             const uint32_t G = a.force_g ? a.force_g : pow2_lanes(rbytes, a.lane_bytes_enc);
             const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
             for (uint32_t j = js + tid / G; j < je; j += ng) {
-                uint8_t *rec = out + soff[j];
-                uint32_t fpre = a.framed ? 4 : 0, d = 0;
+                const uint32_t r0 = soff[j];
+                uint32_t o = r0 + (a.framed ? 4u : 0u), d = 0;   // output offset of the next field
                 if (a.framed && gl == 0)   // the record's mark with its bytes (GrizzlyRpcTransport:103-110)
-                    *(uint32_t *)rec = bswap32r((soff[j + 1] - soff[j] - 4) | kLastFrag);
-                uint64_t dynb = 0;   // XDR bytes of the record's dynamic fields so far
+                    *(uint32_t *)(out + r0) = bswap32r((soff[j + 1] - r0 - 4) | kLastFrag);
                 for (uint32_t k = 0; k < a.nf; ++k) {
                     const VField &f = a.f[k];
                     if (f.kind != XDRG_K_DYNAMIC) {
                         const uint32_t nw = f.xbytes >> 2;
-                        uint8_t *dst = rec + fpre + dynb;
                         for (uint32_t i = gl; !(XDRG_ENC_PROBE & 4) && i < nw; i += G)
-                            *(uint32_t *)(dst + 4 * i) = fixed_word(f, rb + j, 4 * i);
-                        fpre += f.xbytes;
+                            *(uint32_t *)(out + (o + 4 * i)) = fixed_word(f, rb + j, 4 * i);
+                        o += f.xbytes;
                         continue;
                     }
-                    const bool bytes = f.xsz == 1;
-                    const uint64_t esz = bytes ? 1 : f.nsz;
                     const uint32_t *rel = srel + d * RS;
-                    const uint64_t cnt = rel[j + 1] - rel[j];
-                    const uint8_t *p = f.data + (base[d] + rel[j]) * esz;
-                    uint8_t *dst = rec + fpre + dynb;
-                    const int64_t L = 16 * (int64_t)cb[d] - (int64_t)(uintptr_t)a0[d] + (int64_t)(uintptr_t)p;
-                    if (bytes) {
-                        const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
-                        const uint64_t nch = (1 + ((cnt + 3) >> 2) + 3) >> 2;
-                        for (uint64_t c = gl; !(XDRG_ENC_PROBE & 1) && c < nch; c += G) {
-                            const uint32_t *w = (const uint32_t *)(tile + (L - sh + 16 * (int64_t)c - 4));
-                            Chunk5 q;
-                            q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = w[4];
-                            blob_store(dst, q, sh, c, cnt);
+                    const uint32_t e0 = rel[j], cnt = rel[j + 1] - e0;
+                    if (f.xsz == 1) {
+                        // blob [BE length][bytes][zero pad] (Xdr.java:776-800): chunk c =
+                        // blob bytes [16c, 16c + 16) from the five tile words at w + 16c
+                        const int32_t t = tadj[d] + (int32_t)e0;   // tile byte of the payload
+                        const uint32_t sh = (uint32_t)t & 3u;     // (a0 is 16-aligned)
+                        const int32_t w = t - (int32_t)sh - 4;
+                        const uint32_t nwb = 1 + ((cnt + 3) >> 2), nch = (nwb + 3) >> 2;
+                        for (uint32_t c = gl; !(XDRG_ENC_PROBE & 1) && c < nch; c += G) {
+                            const uint32_t *q = (const uint32_t *)(tile + (w + 16 * (int32_t)c));
+                            const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
+                            // (alignbyte by 0 is the low word: no select for aligned payloads)
+                            uint32_t o0 = __builtin_amdgcn_alignbyte(q1, q0, sh);
+                            uint32_t o1 = __builtin_amdgcn_alignbyte(q2, q1, sh);
+                            uint32_t o2 = __builtin_amdgcn_alignbyte(q3, q2, sh);
+                            uint32_t o3 = __builtin_amdgcn_alignbyte(q4, q3, sh);
+                            // blob bytes from the chunk start: the last chunk's zero pad
+                            // (Xdr.java:765) by a mask row (every other chunk: row 16)
+                            const int32_t rem = 4 + (int32_t)cnt - 16 * (int32_t)c;
+                            const u32x4a pm = *(const u32x4a *)(padm + 4 * (rem < 16 ? rem : 16));
+                            o0 &= pm.x;
+                            o1 &= pm.y;
+                            o2 &= pm.z;
+                            o3 &= pm.w;
+                            if (c == 0) o0 = bswap32r(cnt);
+                            uint8_t *dd = out + (o + 16 * c);
+                            if (4 * c + 4 <= nwb) {
+                                u32x4a v; v.x = o0; v.y = o1; v.z = o2; v.w = o3;
+                                *(u32x4a *)dd = v;
+                            } else {
+                                const uint32_t left = nwb - 4 * c;
+                                *(uint32_t *)dd = o0;
+                                if (left > 1) *(uint32_t *)(dd + 4) = o1;
+                                if (left > 2) *(uint32_t *)(dd + 8) = o2;
+                            }
                         }
+                        o += 4 + ((cnt + 3) & ~3u);
                     } else {
-                        const uint64_t nch = (1 + cnt + 3) >> 2;
-                        for (uint64_t c = gl; !(XDRG_ENC_PROBE & 2) && c < nch; c += G) {
-                            const uint32_t *w = (const uint32_t *)(tile + (L + 16 * (int64_t)c - 4));
-                            Chunk5 q;
-                            q.q0 = w[0]; q.q1 = w[1]; q.q2 = w[2]; q.q3 = w[3]; q.q4 = 0;
-                            w4_store(dst, q, c, cnt, f.type == XDRG_T_FLOAT);
+                        // [BE count][BE elements] (Xdr.java:607-613): blob word b is element
+                        // b - 1, chunk c reads the four tile words at t - 4 + 16c
+                        const int32_t t = tadj[d] + 4 * (int32_t)e0 - 4;
+                        const bool fl = f.type == XDRG_T_FLOAT;
+                        const uint32_t nwb = 1 + cnt, nch = (nwb + 3) >> 2;
+                        for (uint32_t c = gl; !(XDRG_ENC_PROBE & 2) && c < nch; c += G) {
+                            const uint32_t *q = (const uint32_t *)(tile + (t + 16 * (int32_t)c));
+                            uint32_t v[4] = {q[0], q[1], q[2], q[3]};
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) v[i] = bswap32r(fl ? canon_f32r(v[i]) : v[i]);
+                            if (c == 0) v[0] = bswap32r(cnt);
+                            uint32_t *dd = (uint32_t *)(out + (o + 16 * c));
+                            if (4 * c + 4 <= nwb) {
+                                u32x4a x; x.x = v[0]; x.y = v[1]; x.z = v[2]; x.w = v[3];
+                                *(u32x4a *)dd = x;
+                            } else {
+                                for (uint32_t i = 0; 4 * c + i < nwb; ++i) dd[i] = v[i];
+                            }
                         }
+                        o += 4 * nwb;
                     }
-                    dynb += dyn_xdr_bytes(f, cnt);
                     ++d;
                 }
             }
@@ -2494,11 +2543,14 @@ __device__ __forceinline__ void dec_stage_batch(const RecArgs &a, const uint8_t 
 #endif
 constexpr uint32_t kSweepMetaPad = 4;   // meta sentinels after the sub-batch's last record
 
-// LDS the sweep adds after the tile: the second field's meta and the chunk
-// map of both fields (their chunks together cover at most the tile's bytes).
+// LDS the sweep adds after the tile: the second field's meta, the chunk
+// map of both fields (their chunks together cover at most the tile's bytes)
+// and the byte-mask rows (kPadMasks: row i keeps the first i bytes of 16).
+__host__ __device__ constexpr size_t dec_sweep_map(uint32_t tile_bytes) {
+    return ((size_t)(tile_bytes >> 4) + 32 + 15) & ~(size_t)15;
+}
 __host__ __device__ constexpr size_t dec_sweep_extra(uint32_t tile_bytes) {
-    return (((size_t)kRecThreads + kSweepMetaPad) * 4 + 15 & ~(size_t)15) +
-           (((size_t)(tile_bytes >> 4) + 32 + 15) & ~(size_t)15);
+    return (((size_t)kRecThreads + kSweepMetaPad) * 4 + 15 & ~(size_t)15) + dec_sweep_map(tile_bytes) + kPadMasks;
 }
 
 // Record lanes of the sub-batch [js, js + m): meta[t] = (start - x0) | tile
@@ -2560,8 +2612,8 @@ __device__ __forceinline__ void tile16(const uint8_t *tile, int32_t w, uint32_t 
 // Byte field: col = the column at block-relative element 0, chunk q = bytes
 // [x0 + 16 q, + 16) with col + x0 16-aligned, [xb, xe) = the sub-batch's bytes.
 __device__ __forceinline__ void sweep_bytes(uint8_t *col, const uint8_t *tile, const uint32_t *meta,
-                                            const uint8_t *map, int32_t x0, uint32_t nq, uint32_t m, int32_t xb,
-                                            int32_t xe) {
+                                            const uint8_t *map, const uint32_t *padm, int32_t x0, uint32_t nq,
+                                            uint32_t m, int32_t xb, int32_t xe) {
     for (uint32_t q = threadIdx.x; q < nq; q += kRecThreads) {
         const int32_t xr = 16 * (int32_t)q;   // chunk start relative to x0
         uint32_t j = q ? map[q] : 0u;
@@ -2581,13 +2633,12 @@ __device__ __forceinline__ void sweep_bytes(uint8_t *col, const uint8_t *tile, c
         // clamp the window so the read stays inside the block's LDS
         const int32_t wb = (int32_t)(m1 >> 16) + (xr - hiA);
         tile16(tile, wb < 0 ? 0 : wb, b);
-        const int32_t sp = hiA - xr;   // chunk bytes [0, sp) from A, [sp, ..) from B
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int32_t o = sp - 4 * k;
-            const uint32_t mk = o >= 4 ? 0xffffffffu : (o <= 0 ? 0u : (1u << (8 * o)) - 1u);
-            v[k] = (a[k] & mk) | (b[k] & ~mk);
-        }
+        const int32_t sp = hiA - xr;   // chunk bytes [0, sp) from A, [sp, ..) from B (sp >= 1)
+        const u32x4a mk = *(const u32x4a *)(padm + 4 * (sp < 16 ? sp : 16));   // (a mask row: one LDS read)
+        v[0] = (a[0] & mk.x) | (b[0] & ~mk.x);
+        v[1] = (a[1] & mk.y) | (b[1] & ~mk.y);
+        v[2] = (a[2] & mk.z) | (b[2] & ~mk.z);
+        v[3] = (a[3] & mk.w) | (b[3] & ~mk.w);
         if (hiB < xr + 16) {   // a third record (or more) inside the chunk: B was short or empty
             int32_t lo = hiB;
             for (uint32_t jj = j + 2; lo < xr + 16 && jj < m; ++jj) {
@@ -2710,7 +2761,7 @@ template <uint32_t RS>
 __device__ __forceinline__ void dec_stage_sweep(const RecArgs &a, const uint8_t *tile, int64_t lds0, uint64_t rb,
                                                 uint32_t js, uint32_t je, const uint32_t *sstart,
                                                 const uint32_t *snrel, const uint32_t *meta0, const uint32_t *meta1,
-                                                const uint8_t *map, const SweepField *sf) {
+                                                const uint8_t *map, const uint32_t *padm, const SweepField *sf) {
     const uint32_t tid = threadIdx.x, m = je - js;
     uint32_t fpre = 0, d = 0;
     for (uint32_t k = 0; k < a.nf; ++k) {
@@ -2731,7 +2782,8 @@ __device__ __forceinline__ void dec_stage_sweep(const RecArgs &a, const uint8_t 
         }
         const SweepField &s = sf[d];
         if (f.xsz == 1) {
-            if (!(XDRG_SW_PROBE & 1)) sweep_bytes(s.col, tile, d ? meta1 : meta0, map + s.moff, s.x0, s.nq, m, s.xb, s.xe);
+            if (!(XDRG_SW_PROBE & 1))
+                sweep_bytes(s.col, tile, d ? meta1 : meta0, map + s.moff, padm, s.x0, s.nq, m, s.xb, s.xe);
         } else if (!(XDRG_SW_PROBE & 2)) {
             sweep_words((uint32_t *)s.col, tile, d ? meta1 : meta0, map + s.moff, s.x0, s.nq, m, s.xb, s.xe);
         }
@@ -2981,6 +3033,9 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
     const bool sweep = SW && lean;
     uint32_t *smeta1 = (uint32_t *)(tile + a.tile_bytes + kStageSlack);
     uint8_t *smap = (uint8_t *)smeta1 + ((((size_t)kRecThreads + kSweepMetaPad) * 4 + 15) & ~(size_t)15);
+    uint32_t *spadm = (uint32_t *)(smap + dec_sweep_map(a.tile_bytes));
+    if (SW && threadIdx.x < kPadMasks / 4)   // (read after the sub-batches' stage barriers)
+        spadm[threadIdx.x] = lo_mask((int32_t)(threadIdx.x >> 2) - 4 * (int32_t)(threadIdx.x & 3));
     __shared__ SweepField sf[2];
     // staging needs every record's fields to end where the next begins or
     // before (records in stream order); otherwise the block goes direct
@@ -3045,7 +3100,7 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
                 const uint32_t cw = tile_word(tile, lds0 + (int64_t)(sstart[j] + fb + dyn_before_xs(xs, snrel, j, dl, RS)));
                 if (bswap32r(cw) != rel[j + 1] - rel[j]) spec_fail(a);
             }
-            dec_stage_sweep<RS>(a, tile, lds0, rb, js, je, sstart, snrel, (uint32_t *)supto, smeta1, smap, sf);
+            dec_stage_sweep<RS>(a, tile, lds0, rb, js, je, sstart, snrel, (uint32_t *)supto, smeta1, smap, spadm, sf);
         } else
             for (uint32_t j = js; j < je; ++j)
                 dec_record_block(a, rb + j, sb + sstart[j], supto[j], snrel, j, tid, kRecThreads);

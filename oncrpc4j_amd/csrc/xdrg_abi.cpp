@@ -388,6 +388,8 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 37: if (!in(0, 3)) return -1; t.xcd_order = (int32_t)v; return 0;
     case 38: if (v && !in(64, 4096)) return -1; t.grp_dec_el = (int32_t)v; return 0;
     case 41: if (v && (!in(4096, 49152) || (v & 15))) return -1; t.grp_enc_img = (int32_t)v; return 0;
+    case 42: if (!in(0, 1)) return -1; t.recv_win = (int32_t)v; return 0;
+    case 43: if (v != 0 && v != 1 && v != 2 && v != 4) return -1; t.grp_enc_split = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -785,6 +787,7 @@ static int group_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *co
     int rc = fill_group(c, s, cols, n, framed, false, a);
     if (rc) return rc;
     a.enc_lanes = (uint32_t)c->tune.grp_enc_lanes;
+    a.enc_split = (uint32_t)c->tune.grp_enc_split;
     // the element-parallel place: one top-level group without inner groups
     if (c->tune.grp_enc_img && s->ngroups == 1 && !a.nest)
         for (uint32_t k = 0; k < a.nf; ++k)
@@ -2110,12 +2113,14 @@ static int recv_staged(xdrg_ctx *c, int mode, const xdrg_schema *s, const uint8_
     return rc ? rc : fr;
 }
 
-// Group schemas on host memory: the staged walk (stream offsets of the
-// complete messages), the staged deframe of those messages (their bodies into
-// host scratch), then the staged decode of the bodies (xdrg_decode_batch with
-// XDRG_HOST_PTRS, whose ring moves a chunk's element rows).  The same results
-// as the device receive, which also decodes assembled bodies; each stream byte
-// crosses PCIe three times here instead of once.
+// Schemas the receive windows do not carry (groups inside group elements,
+// group elements of no XDR bytes) on host memory: the staged walk (stream
+// offsets of the complete messages), the staged deframe of those messages
+// (their bodies into host scratch), then the staged decode of the bodies
+// (xdrg_decode_batch with XDRG_HOST_PTRS).  The same results as the device
+// receive; each stream byte crosses PCIe three times here.  Every other
+// schema, repeated groups included, goes through hs::stage_receive's windows
+// (one crossing).
 static int recv_staged_groups(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t len, uint64_t cap,
                               xdrg_column *cols, uint64_t *msg_offsets, uint64_t *n_msgs, uint64_t *consumed,
                               uint64_t *first_bad, int *err) {
@@ -2225,7 +2230,11 @@ extern "C" int xdrg_receive_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8
     rc = check_columns(c, s, cols, cap, true);
     if (rc) return rc;
     if ((flags & XDRG_HOST_PTRS) && !(flags & XDRG_HOST_MAPPED)) {
-        if (s->ngroups) return recv_staged_groups(c, s, in, len, cap, cols, msg_offsets, n_msgs, consumed, first_bad, err);
+        hs::Schema v;
+        stage_schema(s, v);
+        if (!hs::recv_groups_ok(v) || (s->ngroups && !c->tune.recv_win))   // inner groups / elements of no
+                                                                            // bytes: walk, deframe, decode
+            return recv_staged_groups(c, s, in, len, cap, cols, msg_offsets, n_msgs, consumed, first_bad, err);
         hs::RecvResult R;
         rc = recv_staged(c, hs::RECV_DECODE, s, in, len, cap, cols, nullptr, 0, msg_offsets, R);
         *n_msgs = R.n_msgs;

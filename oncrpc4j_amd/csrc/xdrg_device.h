@@ -11,6 +11,23 @@
 
 namespace xdrg {
 
+// Debug builds (make debug: -DXDRG_DEBUG) check the invariants the kernels
+// trust (element descriptors, tile windows): a broken one stops the kernel
+// with its condition printed instead of becoming a wild access.  Product
+// builds compile the checks out.
+#ifdef XDRG_DEBUG
+#define XDRG_DCHECK(c)                                                                         \
+    do {                                                                                       \
+        if (!(c)) {                                                                            \
+            printf("XDRG_DCHECK failed %s:%d: %s (block %u thread %u)\n", __FILE__, __LINE__, #c, \
+                   blockIdx.x, threadIdx.x);                                                   \
+            __builtin_trap();                                                                  \
+        }                                                                                      \
+    } while (0)
+#else
+#define XDRG_DCHECK(c) do {} while (0)
+#endif
+
 __device__ __forceinline__ uint32_t bswap32r(uint32_t x) { return __builtin_bswap32(x); }
 __device__ __forceinline__ uint32_t pad4(uint64_t n) { return (uint32_t)((4 - (n & 3)) & 3); }
 

@@ -204,6 +204,11 @@ struct Tuning {
                                     // group, no inner groups, <= 2 dynamic members), at most this many
                                     // elements per sub-batch (0: a lane per record; READDIR decode 9.3 ->
                                     // 5.5 ms, DUMP 3.0 -> 1.9)
+    int32_t recv_win = 1;           // key 42: XDRG_HOST_PTRS receive of repeated-group schemas: 1 the
+                                    // staging windows carry the element rows (one PCIe crossing), 0 the
+                                    // staged walk, deframe and body decode (three; A/B only)
+    int32_t grp_enc_split = 0;      // key 43: element-parallel group encode, blocks per scan block (1, 2,
+                                    // 4; 0 = by batch size, enc_el_split)
     int32_t spec_sizes = 2;         // key 31: sweep decode whose last dynamic field is a word vector
                                     // followed by fixed fields only: 1 derive its counts from the record
                                     // extents (sizes reads one length word per record, the place kernel
@@ -390,6 +395,7 @@ struct GroupArgs {
     uint32_t lay_z0, lay_z1;               // the dynamic members' XDR element sizes
     uint32_t lay_s0, lay_s1;               // their counted-column slots
     uint32_t enc_img;            // encode place: element-parallel, LDS image bytes (0: off; key 41)
+    uint32_t enc_split;          // its blocks per scan block (0: enc_el_split; key 43)
     int32_t cvals[XDRG_MAX_CASES];
     GField f[kMaxFields];
 };

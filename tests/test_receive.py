@@ -304,3 +304,33 @@ def test_deframe_ex_host_vs_oracle(rctx, mem):
                 assert got == bodies[:k]
             finally:
                 host.close()
+
+
+@pytest.mark.parametrize("win", [1, 0], ids=["windows", "three_pass"])
+@pytest.mark.parametrize("mem", ["pageable", "registered"])
+@pytest.mark.parametrize("name", ["dirlist_group", "items_group"])
+def test_receive_groups_staged_vs_oracle(rctx, name, mem, win):
+    """Repeated groups on host memory: the staging windows carry each
+    message's element rows (tuning key 42 = 1, one PCIe crossing) or the
+    staged walk, deframe and body decode run (key 42 = 0); both equal the
+    oracle's handleRead + decode, with element capacities that run out
+    mid-stream (CAPACITY, delivered up to it) and messages over many 64 KiB
+    windows."""
+    fields, conds = SCHEMAS[name]
+    rctx.tune(42, win)
+    try:
+        n = 4000
+        hb = _sane(random_batch(fields, n, seed=zlib.crc32(f"grx/{name}".encode()) & 0xffff, dyn_len=(0, 40),
+                                special_floats=False), conds)
+        for style in ("single", "mixed"):
+            stream = build_stream(fields, conds, hb, style, seed=n + len(style), tail=True)
+            want = check_receive(rctx, name, stream, n + 3, hb.dyn_caps(), mem)
+            assert want[0] == 0 and want[1] == n
+        g = next(k for k, f in enumerate(fields) if f[0] == abi.T_GROUP)
+        caps = hb.dyn_caps()
+        caps[g] = caps[g] * 2 // 3   # the group's elements run out two thirds in
+        stream = build_stream(fields, conds, hb, "single", seed=7)
+        want = check_receive(rctx, name, stream, n, caps, mem)
+        assert want[0] == abi.E_CAPACITY and want[1] == want[3] < n
+    finally:
+        rctx.tune(0)

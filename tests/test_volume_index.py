@@ -385,8 +385,8 @@ def test_gpu_volume_index_host_empty_members(kind):
             ln = c.encode(sch, hb.columns(), n, out, len(want) + 64, rec_offsets=ro, host=host, mapped=mapped)
             assert out[:ln].tobytes() == want and np.array_equal(ro, offs), name
             back0 = HostBatch.empty(FIELDS, n, hb0.dyn_caps())
-            for k in range(len(FIELDS)):   # zero-row member columns as zero-length arrays
-                if FIELDS[k][0] != abi.T_GROUP and back0.rows(k) == 0 and n:
+            for k in range(len(FIELDS)):   # zero-row member columns (rows of the batch) as zero-length arrays
+                if FIELDS[k][0] != abi.T_GROUP and hb0.rows(k) == 0 and n:
                     a = back0.arrays[k]
                     back0.arrays[k] = (a[0][:0], a[1][:1]) if FIELDS[k][1] == abi.K_DYNAMIC else a[:0]
             back = moved(back0, mem)

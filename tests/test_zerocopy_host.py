@@ -180,7 +180,7 @@ def test_host_shallow_heads_only_cross(hctx):
     small = HostBatch(fields, n, [a if k != field else (np.zeros(1, np.uint8), np.zeros(n + 1, np.uint64))
                                   for k, a in enumerate(hb0.arrays)])
     # the oracle on zero-length payloads gives the heads; splice and marks follow from the lengths
-    heads = 28 * n
+    heads = 32 * n   # mark + six ints + length word per message
     out = np.zeros(heads + 64, np.uint8)
     spl = np.zeros(n, np.uint64)
     ro = np.zeros(n + 1, np.uint64)
