@@ -920,6 +920,97 @@ def host_inclusive_var(device, n, reps=2, slot_bytes=64 << 20, slots=4):
                       "unregistered memory (bounce copies)"}
 
 
+def host_inclusive_byref(device, n=512 << 10, reps=3, slot_bytes=64 << 20, slots=4):
+    """configs[2]-shaped replies (6 x int32 + a 4 KiB opaque, NFS WRITE / READ
+    data) sent by reference from host memory: xdrg_encode_batch_shallow with
+    XDRG_HOST_PTRS, the payload column NULL (the FileChunk / shallow
+    ByteBuffer of Xdr.java:839-866, 978-988 stays where it is; only the
+    heads are produced and cross PCIe), record-marked as sendRawTCP marks
+    all parts (GrizzlyRpcTransport.java:130-168).  Legs: byref_staged (the
+    staging ring, registered buffers), byref_mapped (XDRG_HOST_MAPPED), and
+    copy_staged, the same replies encoded whole from a host payload column
+    (every payload byte across PCIe twice).  wire_GiB_s = the messages' bytes
+    on the wire (head + payload) / wall time; pcie_bytes = what the call
+    moves.  Heads checked against their closed form (marks, big-endian
+    ints, length words, splice positions)."""
+    import numpy as np
+    from oncrpc4j_amd import abi, engine
+    P = 4096
+    fields = [(abi.T_INT, abi.K_SCALAR, 0)] * 6 + [(abi.T_OPAQUE, abi.K_DYNAMIC, 0)]
+    sch = engine.Schema(fields)
+    rng = np.random.default_rng(0x0DCAC4E5 + 3)
+    regs = []
+
+    def mk(nbytes):
+        m_, a_, p_ = _host_buffer(max(nbytes, 1), True)
+        regs.append(p_)
+        return a_[:nbytes]
+
+    hdr = mk(24 * n).view(np.int32).reshape(n, 6)
+    hdr[:] = rng.integers(-2**31, 2**31 - 1, (n, 6), dtype=np.int32)
+    poffs = mk(8 * (n + 1)).view(np.uint64)
+    poffs[:] = np.arange(n + 1, dtype=np.uint64) * P
+    head = 4 + 24 + 4   # mark, six ints, length word
+    out = mk(head * n)
+    ro = mk(8 * (n + 1)).view(np.uint64)
+    spl = mk(8 * n).view(np.uint64)
+    want = np.empty((n, head // 4), ">u4")
+    want[:, 0] = 0x80000000 | (head - 4 + P)
+    want[:, 1:7] = hdr.view(np.uint32)
+    want[:, 7] = P
+    want = want.view(np.uint8).reshape(-1)
+
+    def cols(payload):
+        arr = (abi.Column * 7)()
+        for k in range(6):
+            arr[k].data, arr[k].stride = hdr.ctypes.data + 4 * k, 24
+        arr[6].data = payload.ctypes.data if payload is not None else None
+        arr[6].offsets, arr[6].cap = poffs.ctypes.data, n * P if payload is not None else 0
+        return arr
+
+    res = {}
+    ctx = engine.Context(device)
+    ctx.apply_tuning(os.environ.get("XDRG_TUNE"))   # measurement runs only
+    ctx.host_staging(slot_bytes, slots)
+    for mode in ("byref_staged", "byref_mapped"):
+        kw = {"mapped": True} if mode == "byref_mapped" else {"host": True}
+        c = cols(None)
+        ctx.encode_shallow(sch, c, n, out, head * n, 6, spl, rec_offsets=ro, framed=True, **kw)   # warm
+        out[:] = 0
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            ln = ctx.encode_shallow(sch, c, n, out, head * n, 6, spl, rec_offsets=ro, framed=True, **kw)
+        dt = (time.perf_counter() - t0) / reps
+        ok = ln == head * n and bool(np.array_equal(out, want)) and \
+            bool(np.array_equal(spl, np.arange(n, dtype=np.uint64) * head + head)) and \
+            bool(np.array_equal(ro, np.arange(n + 1, dtype=np.uint64) * head))
+        res[mode] = {"ms": round(dt * 1e3, 3), "wire_GiB_s": round(n * (head + P) / dt / GIB, 2),
+                     "Mmsg_s": round(n / dt / 1e6, 2), "pcie_bytes": n * (24 + 8 + head + 8 + 8), "ok": ok}
+    # the copy form: the same replies with the payload column in host memory
+    payload = mk(n * P)
+    payload[:] = 7
+    full = mk((head + P) * n)
+    c = cols(payload)
+    ctx.encode(sch, c, n, full, (head + P) * n, rec_offsets=ro, framed=True, host=True)   # warm
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ln = ctx.encode(sch, c, n, full, (head + P) * n, rec_offsets=ro, framed=True, host=True)
+    dt = (time.perf_counter() - t0) / reps
+    f2 = full.reshape(n, head + P)
+    ok = ln == (head + P) * n and bool(np.array_equal(f2[:, :head].reshape(-1), want)) and bool((f2[:, head:] == 7).all())
+    res["copy_staged"] = {"ms": round(dt * 1e3, 3), "wire_GiB_s": round(n * (head + P) / dt / GIB, 2),
+                          "Mmsg_s": round(n / dt / 1e6, 2), "pcie_bytes": n * (24 + 8 + 2 * P + head + 8), "ok": ok}
+    ctx.close()
+    for p_ in regs:
+        engine.host_unregister(p_)
+    del hdr, poffs, out, ro, spl, payload, full, f2
+    return {"config": 3, "records": n, "payload_bytes": P, "legs": res,
+            "ok": all(v["ok"] for v in res.values()),
+            "method": "C-ABI xdrg_encode_batch_shallow (XDRG_HOST_PTRS / XDRG_HOST_MAPPED, payload column NULL) "
+                      "vs xdrg_encode_batch of the same record-marked replies from a host payload column; host "
+                      "buffers pinned with xdrg_host_register; wire_GiB_s counts head + payload bytes per message"}
+
+
 # ---------------------------------------------------------------------------
 def run_rank(args):
     import torch
@@ -947,11 +1038,12 @@ def run_rank(args):
             and ctx is not None:
         hinc = host_inclusive(R.local, wl.sch, min(n, 64 << 20))
     del wl
-    hvar = None
+    hvar = hbyref = None
     if hinc is not None and args.extra:
         if R.cuda:
             torch.cuda.empty_cache()
         hvar = host_inclusive_var(R.local, SIZES[4])
+        hbyref = host_inclusive_byref(R.local)
     if R.cuda:
         torch.cuda.empty_cache()
 
@@ -994,6 +1086,7 @@ def run_rank(args):
             "cpu_baseline": cpu,
             "host_inclusive": hinc,
             "host_inclusive_var": hvar,
+            "host_inclusive_byref": hbyref,
             "extra_configs": extra,
         }
         print(json.dumps(line), flush=True)
