@@ -1,0 +1,7 @@
+cd $GRAFT_REPO_ROOT
+for lib in oncrpc4j_amd/libxdrgpu.so exp/lib_swp1.so exp/lib_swp2.so exp/lib_swp16.so exp/lib_swp32.so; do
+  XDRG_LIBRARY=$PWD/$lib XDRG_PARTS=decode timeout -k 10 120 python tools/ab_stage_parts.py || exit 3
+done
+for lib in oncrpc4j_amd/libxdrgpu.so exp/lib_enp1.so exp/lib_enp2.so exp/lib_enp4.so exp/lib_enp8.so exp/lib_enp16.so; do
+  XDRG_LIBRARY=$PWD/$lib XDRG_PARTS=encode timeout -k 10 120 python tools/ab_stage_parts.py || exit 3
+done
