@@ -1406,9 +1406,6 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
 // member native offsets: descriptors in LDS), and then every lane of the
 // block decodes an element: consecutive lanes, consecutive elements, so the
 // member stores of an instruction fall on consecutive rows.
-#ifndef XDRG_EL_PROBE
-#define XDRG_EL_PROBE 0   // experiment builds only (wrong output): 1 no element decode, 2 no record walk, 4 no staging
-#endif
 // LDS of k_grp_dec_place_el: per-block metadata (extents, the group's first
 // elements, the dynamic members' bases: 4 x 257 u64) | tile | descriptors
 constexpr size_t kElMeta = 4 * (kRecThreads + 1) * 8;
@@ -1489,17 +1486,17 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
         const uintptr_t a0 = (xb + mx[js]) & ~(uintptr_t)15;
         const uintptr_t a1 = (xb + mx[je] + 15) & ~(uintptr_t)15;
         const uint32_t nch = a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u;
-        if (!(XDRG_EL_PROBE & 4)) g_stage_tile(tile, a0, nch);
+        g_stage_tile(tile, a0, nch);
         el.E0 = mE[js];
         el.sb0 = mb0[js];
         el.sb1 = mb1[js];
         __syncthreads();
         // stream offset x at tile + (x - (a0 - xb))
-        if (!(XDRG_EL_PROBE & 2) && js + tid < je) g_dec_record<false, true>(a, rb + js + tid, tile, a0 - xb, el);
+        if (js + tid < je) g_dec_record<false, true>(a, rb + js + tid, tile, a0 - xb, el);
         __syncthreads();   // descriptors
         const uint64_t nel = mE[je] - el.E0;
         XDRG_DCHECK(nel <= a.dec_el);   // (the fit count bounded the sub-batch's elements)
-        for (uint32_t i = tid; !(XDRG_EL_PROBE & 1) && i < nel; i += kRecThreads) {
+        for (uint32_t i = tid; i < nel; i += kRecThreads) {
             GRun run;
 #pragma unroll
             for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;

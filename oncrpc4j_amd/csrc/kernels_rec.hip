@@ -2110,10 +2110,6 @@ __device__ __forceinline__ uint32_t enc_fit(const RecArgs &a, const uint64_t (&b
 // (git history): the field-major scatter (1.23x WRITE), the
 // same with nontemporal stores, an LDS output image composed from HBM inputs
 // or from the staged tile.
-#ifndef XDRG_ENC_PROBE
-#define XDRG_ENC_PROBE 0   // experiment builds only (wrong output): 1 no byte chunks, 2 no word chunks,
-                           // 4 no fixed fields, 8 no staging copy, 16 the prologue only
-#endif
 __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr uint32_t RS = kRecPerBlock + 1;   // row stride of soff / srel
@@ -2188,7 +2184,6 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
         }
         return;
     }
-    if (XDRG_ENC_PROBE & 16) return;   // (experiment builds: the prologue only)
     uint8_t *const out = a.xdr + bbase;   // block-relative stream
     // ---- sub-batches
     uint32_t js = 0;
@@ -2217,7 +2212,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
             cb[d + 1] += stage_chunks(f.data + (base[d] + srel[d * RS + js]) * esz,
                                       f.data + (base[d] + srel[d * RS + je]) * esz, &a0[d]);
         }
-        if (!(XDRG_ENC_PROBE & 8)) stage_copy(tile, a0, cb, a.ndyn);   // (stage_dma measured 3.70 vs 3.62 ms here: nothing to overlap)
+        stage_copy(tile, a0, cb, a.ndyn);   // (stage_dma measured 3.70 vs 3.62 ms here: nothing to overlap)
         __syncthreads();
         const uint32_t m = je - js;
         // tile offset of element 0 of the block's dynamic column d, minus its
@@ -2247,7 +2242,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
                     const VField &f = a.f[k];
                     if (f.kind != XDRG_K_DYNAMIC) {
                         const uint32_t nw = f.xbytes >> 2;
-                        for (uint32_t i = gl; !(XDRG_ENC_PROBE & 4) && i < nw; i += G)
+                        for (uint32_t i = gl; i < nw; i += G)
                             *(uint32_t *)(out + (o + 4 * i)) = fixed_word(f, rb + j, 4 * i);
                         o += f.xbytes;
                         continue;
@@ -2261,7 +2256,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
                         const uint32_t sh = (uint32_t)t & 3u;     // (a0 is 16-aligned)
                         const int32_t w = t - (int32_t)sh - 4;
                         const uint32_t nwb = 1 + ((cnt + 3) >> 2), nch = (nwb + 3) >> 2;
-                        for (uint32_t c = gl; !(XDRG_ENC_PROBE & 1) && c < nch; c += G) {
+                        for (uint32_t c = gl; c < nch; c += G) {
                             const uint32_t *q = (const uint32_t *)(tile + (w + 16 * (int32_t)c));
                             const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4];
                             // (alignbyte by 0 is the low word: no select for aligned payloads)
@@ -2296,7 +2291,7 @@ __global__ __launch_bounds__(kRecThreads) void k_enc_stage_rm(const RecArgs a) {
                         const int32_t t = tadj[d] + 4 * (int32_t)e0 - 4;
                         const bool fl = f.type == XDRG_T_FLOAT;
                         const uint32_t nwb = 1 + cnt, nch = (nwb + 3) >> 2;
-                        for (uint32_t c = gl; !(XDRG_ENC_PROBE & 2) && c < nch; c += G) {
+                        for (uint32_t c = gl; c < nch; c += G) {
                             const uint32_t *q = (const uint32_t *)(tile + (t + 16 * (int32_t)c));
                             uint32_t v[4] = {q[0], q[1], q[2], q[3]};
 #pragma unroll
@@ -2537,10 +2532,6 @@ __device__ __forceinline__ void dec_stage_batch(const RecArgs &a, const uint8_t 
 // control flow of groups of lanes (what bounds dec_stage_batch, DESIGN.md
 // §5.3) is gone.  Byte fields: Xdr.java:760-763 / :797-800 (bytes, pad
 // skipped); int vectors: Xdr.java:607-613 (one bswap per element).
-#ifndef XDRG_SW_PROBE
-#define XDRG_SW_PROBE 0   // experiment builds only: parts of the sweep switched off (wrong output;
-                          // 32: no sub-batch at all)
-#endif
 constexpr uint32_t kSweepMetaPad = 4;   // meta sentinels after the sub-batch's last record
 
 // LDS the sweep adds after the tile: the second field's meta, the chunk
@@ -2768,7 +2759,7 @@ __device__ __forceinline__ void dec_stage_sweep(const RecArgs &a, const uint8_t 
         const VField &f = a.f[k];
         if (f.kind != XDRG_K_DYNAMIC) {
             const uint32_t nw = f.xbytes >> 2;
-            if (nw && !(XDRG_SW_PROBE & 16)) {
+            if (nw) {
                 const uint32_t G = a.force_g ? a.force_g : pow2_lanes((uint64_t)nw * 4, 16);
                 const uint32_t gl = tid & (G - 1), ng = kRecThreads / G;
                 for (uint32_t j = js + tid / G; j < je; j += ng) {
@@ -2782,9 +2773,8 @@ __device__ __forceinline__ void dec_stage_sweep(const RecArgs &a, const uint8_t 
         }
         const SweepField &s = sf[d];
         if (f.xsz == 1) {
-            if (!(XDRG_SW_PROBE & 1))
-                sweep_bytes(s.col, tile, d ? meta1 : meta0, map + s.moff, padm, s.x0, s.nq, m, s.xb, s.xe);
-        } else if (!(XDRG_SW_PROBE & 2)) {
+            sweep_bytes(s.col, tile, d ? meta1 : meta0, map + s.moff, padm, s.x0, s.nq, m, s.xb, s.xe);
+        } else {
             sweep_words((uint32_t *)s.col, tile, d ? meta1 : meta0, map + s.moff, s.x0, s.nq, m, s.xb, s.xe);
         }
         ++d;
@@ -3058,7 +3048,6 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
             dec_record_block(a, rb + j, rec_extent(a, rb + j).a + (a.framed ? 4 : 0), supto[j], snrel, j, tid, kRecThreads);
         return;
     }
-    if (XDRG_SW_PROBE & 32) return;   // (experiment builds: walk, look-back and prologue only)
     // ---- sub-batches
     uint32_t js = 0;
     uint32_t k1 = nlive ? dec_fit(a, sstart, sb, snrel, js, nlive) : 0;
