@@ -2818,18 +2818,22 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
-// Wave 0 of block b: publish agg, look back over the predecessors 64 at a
-// time down to the nearest inclusive prefix of each field, publish the
-// inclusive prefix; s_base[d] = the exclusive prefix of field d.
-__device__ __forceinline__ void lb_resolve(const RecArgs &a, uint64_t b, const uint64_t (&agg)[kMaxDynLds],
-                                           uint64_t *s_base) {
+// Wave 0 of block b: publish agg (lb_publish, as soon as the walk has the
+// block's totals); later (lb_wait, after the block's offset-free prologue, so
+// the predecessors' totals arrive meanwhile) look back over the predecessors
+// 64 at a time down to the nearest inclusive prefix of each field, publish
+// the inclusive prefix; s_base[d] = the exclusive prefix of field d.
+__device__ __forceinline__ void lb_publish(const RecArgs &a, uint64_t b, const uint64_t (&agg)[kMaxDynLds]) {
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d)
+            if ((uint32_t)d < a.ndyn) lb_put(a.block_sums + (uint64_t)d * a.nblocks + b, (b ? kLbOwn : kLbIncl) | agg[d]);
+}
+__device__ __forceinline__ void lb_wait(const RecArgs &a, uint64_t b, const uint64_t (&agg)[kMaxDynLds],
+                                        uint64_t *s_base) {
     const uint32_t lane = threadIdx.x & 63, nd = a.ndyn;
     const uint64_t nb = a.nblocks;
     uint64_t *st = a.block_sums;
-    if (lane == 0)
-#pragma unroll
-        for (int d = 0; d < kMaxDynLds; ++d)
-            if ((uint32_t)d < nd) lb_put(st + (uint64_t)d * nb + b, (b ? kLbOwn : kLbIncl) | agg[d]);
     uint64_t pre[kMaxDynLds] = {0, 0, 0, 0};
     uint32_t done = 0;
     const uint32_t all = (1u << nd) - 1;
@@ -2920,6 +2924,7 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
     const uint64_t nb = a.nblocks;
     uint32_t *scnt1 = (uint32_t *)tile;   // ONE: the block's walked counts [ndyn][RPB], read before staging
     uint32_t nlive;
+    uint64_t agg1[kMaxDynLds] = {0, 0, 0, 0};   // ONE: the block's totals (published, waited on below)
     if (ONE) {
         __shared__ unsigned long long s_tk;
         __shared__ uint32_t s_bad1;
@@ -2940,11 +2945,17 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
             for (int j = 0; j < kRecPerThread; ++j) sv += scnt1[(size_t)d * kRecPerBlock + tid + j * kRecThreads];
             agg[d] = block_sum(sv);   // (its barriers also publish s_bad1 and the counts)
         }
-        if (tid < 64) lb_resolve(a, bid, agg, s_base);
-        __syncthreads();
+        if (tid < 64) lb_publish(a, bid, agg);
         // a block of big records would be the group kernel's, which is not
-        // launched here: the exact rerun decodes the batch
-        if (a.big_rec && block_is_big_at(a, bid, true)) { if (tid == 0) spec_fail(a); return; }
+        // launched here: the exact rerun decodes the batch (the block still
+        // settles its prefix: its successors wait for it)
+        if (a.big_rec && block_is_big_at(a, bid, true)) {
+            if (tid < 64) lb_wait(a, bid, agg, s_base);
+            if (tid == 0) spec_fail(a);
+            return;
+        }
+#pragma unroll
+        for (int d = 0; d < kMaxDynLds; ++d) agg1[d] = agg[d];
         const uint32_t nr = (uint32_t)(a.n > rb ? (a.n - rb < (uint64_t)kRecPerBlock ? a.n - rb : (uint64_t)kRecPerBlock) : 0);
         nlive = s_bad1 < nr ? s_bad1 : nr;
     } else {
@@ -2962,7 +2973,8 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
         nlive = bad > rb ? (uint32_t)(bad - rb < (uint64_t)nrec ? bad - rb : (uint64_t)nrec) : 0;
     }
     if (tid == 0) s_wide = 0;
-    // ---- prologue: counts, native offsets (written to the columns), capacity, extents
+    // ---- prologue: counts, native offsets (written to the columns), capacity,
+    // extents; block-relative first (ONE: while the look-back's predecessors settle)
     const uint64_t sb = nlive ? rec_extent(a, rb).a + (a.framed ? 4 : 0) : 0;   // stream offset of sstart 0
     uint32_t upto[kRecPerThread];
     bool wide = false;
@@ -2990,25 +3002,42 @@ __device__ __forceinline__ void dec_stage_body(const RecArgs &a, uint64_t bid) {
             s += c[j];
         }
         uint64_t btot;
-        const uint64_t base = ONE ? s_base[d] : a.block_sums[(uint64_t)d * nb + bid];
-        uint64_t off = base + block_excl_scan(s, &btot);
+        uint64_t off = block_excl_scan(s, &btot);   // block-relative
         wide |= btot * (f.xsz == 1 ? 1 : f.nsz) >= (1ull << 31);
 #pragma unroll
         for (int j = 0; j < kRecPerThread; ++j) {
+            snrel[d * RS + t0 + j] = (uint32_t)off;
+            off += c[j];
+        }
+        if (tid == kRecThreads - 1) snrel[d * RS + kRecPerBlock] = (uint32_t)off;
+    }
+    if (ONE) {
+        if (tid < 64) lb_wait(a, bid, agg1, s_base);
+        __syncthreads();   // s_base; snrel
+    } else {
+        __syncthreads();   // snrel
+    }
+#pragma unroll
+    for (int d = 0; d < kMaxDynLds; ++d) {   // native offsets and capacity, now absolute
+        if ((uint32_t)d >= a.ndyn) continue;
+        const uint32_t k = a.dyn_idx[d];
+        const VField &f = a.f[k];
+        const uint64_t base = ONE ? s_base[d] : a.block_sums[(uint64_t)d * nb + bid];
+        const uint32_t *rel = snrel + d * RS;
+#pragma unroll
+        for (int j = 0; j < kRecPerThread; ++j) {
             const uint64_t r = rb + t0 + j;
-            snrel[d * RS + t0 + j] = (uint32_t)(off - base);
+            const uint64_t off = base + rel[t0 + j];
             if (t0 + j < nrec) {
                 f.offsets[r] = off;
-                if (t0 + j < nlive && off + c[j] > f.cap) {   // native column too small
+                if (t0 + j < nlive && off + (rel[t0 + j + 1] - rel[t0 + j]) > f.cap) {   // native column too small
                     atomicMin(a.errkey, err_key(r, 2 * k + 2, XDRG_E_CAPACITY));
                     if (upto[j] > k) upto[j] = k;
                     if (a.spec_mode & 1) spec_fail(a);   // on derived counts: the exact walk decides
                 }
             }
-            off += c[j];
         }
-        if (tid == kRecThreads - 1) snrel[d * RS + kRecPerBlock] = (uint32_t)(off - base);
-        if (!ONE && tid == 0 && bid == 0) f.offsets[a.n] = a.totals[d];   // (ONE: lb_resolve)
+        if (!ONE && tid == 0 && bid == 0) f.offsets[a.n] = a.totals[d];   // (ONE: lb_wait)
     }
 #pragma unroll
     for (int j = 0; j < kRecPerThread; ++j) supto[t0 + j] = (uint8_t)upto[j];
