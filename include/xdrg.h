@@ -111,11 +111,11 @@ typedef struct xdrg_field {
  * (struct T { ...; T *next; }, used as `T *x`) as BE(1) + element for every
  * element and a closing BE(0).  On the tape a group is one field
  * {XDRG_T_GROUP, kind FIXED / DYNAMIC / LIST, count, reserved = m} followed
- * by its m member fields (SCALAR, FIXED or DYNAMIC of the base types) — or,
- * one level down, an inner group (an array of structs / list inside the
- * element, jrpcgen.java:856-906 calling the inner elements' xdrEncode) whose
- * own members are base types; the outer m counts the inner group's whole
- * span.  A condition (xdrg_cond below) stays on its level: a top-level
+ * by its m member fields (SCALAR, FIXED or DYNAMIC of the base types) or
+ * inner groups (an array of structs / list inside the element,
+ * jrpcgen.java:856-906 calling the inner elements' xdrEncode), recursively
+ * up to four group levels in all; an outer m counts every inner group's
+ * whole span.  A condition (xdrg_cond below) stays on its level: a top-level
  * field (the group field included) on a top-level discriminant, a member (an
  * inner group included) on an earlier member of its own group, evaluated per
  * element.  Columns: the group's own column has offsets[rows + 1] (DYNAMIC /
@@ -127,7 +127,9 @@ typedef struct xdrg_field {
  * [offsets[e], offsets[e+1]) (offsets has elements + 1 entries).  Decode
  * errors keep the reference's order: the count / list bools / member checks
  * as the element loops meet them; a negative count is XDRG_E_NEG_SIZE.
- * XDRG_HOST_PTRS staging windows one level of groups; a schema with inner
+ * A deeper inner group's column is indexed by the elements of the group
+ * that holds it, the same way.  XDRG_HOST_PTRS staging windows one level of
+ * groups; a schema with inner
  * groups on host memory goes through device scratch whole (the spans the call
  * touches copied in and back, overlapping column spans merged).            */
 

@@ -14,9 +14,10 @@ engine works on a batch of N records of one schema laid out as columns
   its members; the group's array is offsets[n+1] (element ranges; None for
   a FIXED group: record i owns elements i*count ...), and every member array
   is indexed by ELEMENT (fixed: (E,) / (E, count); dynamic: (values,
-  offsets[E+1])).  A member may itself be a group (one level down, its
-  members counted in the outer `members`): its array is indexed by the outer
-  group's elements (offsets[E+1]) and its own members by its elements.
+  offsets[E+1])).  A member may itself be a group (up to four group levels
+  in all, its members counted in the outer `members`): its array is indexed
+  by the enclosing group's elements (offsets[E+1]) and its own members by
+  its elements.
 
 HostBatch holds numpy arrays (fixtures, the oracle's host pointers);
 DeviceBatch holds torch tensors in HBM (the engine's device pointers).

@@ -191,9 +191,9 @@ __device__ __forceinline__ bool g_dec_field_present(const GroupArgs &a, uint32_t
 // list (a member group), whose count word, elements and closing bool are the
 // element's bytes too, as the element's generated xdrEncode writes them
 // (jrpcgen.java:856-906, 835-851).
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g, uint64_t row, GDisc &d);
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g, uint64_t e, GDisc d) {
     g = g_uni(g);
     const GField &G = a.f[g];
@@ -212,8 +212,8 @@ __device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g,
         const GField &m = a.f[g + j];
         const bool p = !G.ncm || g_enc_field_present(a, g + j, e, d);
         if (m.type == XDRG_T_GROUP) {
-            if constexpr (L == 0) {
-                if (p) s += g_group_bytes<1>(a, g + j, e, d);
+            if constexpr (L + 1 < D) {
+                if (p) s += g_group_bytes<L + 1, D>(a, g + j, e, d);
             }
             j += m.nmem;
             continue;
@@ -225,7 +225,7 @@ __device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g,
 }
 // XDR bytes of group g at row `row` of its column (a record, or an element
 // of the enclosing group): its count / closing bool and every element.
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g, uint64_t row, GDisc &d) {
     g = g_uni(g);
     const GField &G = a.f[g];
@@ -253,7 +253,7 @@ __device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g
             }
         }
     } else if (G.ndm || G.ncm) {
-        for (uint64_t e = e0; e < e0 + cnt; ++e) s += g_elem_bytes<L>(a, g, e, d);
+        for (uint64_t e = e0; e < e0 + cnt; ++e) s += g_elem_bytes<L, D>(a, g, e, d);
     } else {
         s += cnt * G.efix;
     }
@@ -263,7 +263,7 @@ __device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g
 // ===========================================================================
 // Encode
 // ===========================================================================
-template <bool NEST>
+template <int D>
 __device__ __forceinline__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
     uint64_t s = a.framed ? 4 : 0;
     GDisc d{};
@@ -275,7 +275,7 @@ __device__ __forceinline__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
             continue;
         }
         if (f.type == XDRG_T_GROUP) {
-            s += g_group_bytes<NEST ? 0 : 1>(a, k, r, d);
+            s += g_group_bytes<0, D>(a, k, r, d);
             k += 1 + f.nmem;
             continue;
         }
@@ -298,7 +298,7 @@ __device__ __forceinline__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
 #endif
 constexpr int kWalkSplit = XDRG_WALK_SPLIT;
 static_assert(kRecPerThread % kWalkSplit == 0, "records per lane");
-template <bool NEST>
+template <int D>
 __global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a) {
     constexpr int per = kRecPerThread / kWalkSplit;
     const uint64_t blk = blockIdx.x / kWalkSplit;
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a
     for (int j = 0; j < per; ++j) {
         const uint64_t r = r0 + j;
         if (r >= a.n) break;
-        const uint64_t z = g_rec_size<NEST>(a, r);
+        const uint64_t z = g_rec_size<D>(a, r);
         a.rec_size[r] = z;
         s += z;
     }
@@ -320,9 +320,9 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a
 }
 
 // One lane writes element e of group g at stream byte p; returns its end.
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, uint64_t row, uint64_t p, GDisc &d);
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t p, GDisc d) {
     uint8_t *out = a.xdr;
     g = g_uni(g);
@@ -336,8 +336,8 @@ __device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint32_t g, u
         const GField &m = a.f[g + j];
         const bool present = !G.ncm || g_enc_field_present(a, g + j, e, d);   // an element's absent arm
         if (m.type == XDRG_T_GROUP) {   // an inner array / list: this lane writes it whole
-            if constexpr (L == 0) {
-                if (present) p = g_enc_group<1>(a, g + j, e, p, d);
+            if constexpr (L + 1 < D) {
+                if (present) p = g_enc_group<L + 1, D>(a, g + j, e, p, d);
             }
             j += m.nmem;
             continue;
@@ -357,7 +357,7 @@ __device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint32_t g, u
     return p;
 }
 // Group g at row `row` of its column, by one lane from stream byte p.
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, uint64_t row, uint64_t p, GDisc &d) {
     uint8_t *out = a.xdr;
     g = g_uni(g);
@@ -368,7 +368,7 @@ __device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, 
         *(uint32_t *)(out + p) = bswap32r((uint32_t)cnt);
         p += 4;
     }
-    for (uint64_t e = e0; e < e0 + cnt; ++e) p = g_enc_elem<L>(a, g, e, p, d);
+    for (uint64_t e = e0; e < e0 + cnt; ++e) p = g_enc_elem<L, D>(a, g, e, p, d);
     if (G.kind == XDRG_K_LIST) {      // xdrEncodeBoolean(false)
         *(uint32_t *)(out + p) = 0;
         p += 4;
@@ -392,9 +392,8 @@ __device__ __forceinline__ uint64_t g_incl_scan(uint64_t v, uint32_t ln) {
     }
     return v;
 }
-template <uint32_t G, bool NEST>
+template <uint32_t G, int D>
 __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint64_t size, uint32_t ln) {
-    constexpr int L0 = NEST ? 0 : 1;   // depth the record's groups start at (1: inner groups compiled out)
     uint8_t *out = a.xdr;
     if (a.framed) {   // GrizzlyRpcTransport.java:103-110
         if (ln == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
@@ -416,15 +415,15 @@ __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint6
                 pos += 4;
             }
             if (!f.ndm && !f.ncm) {   // elements of one size: a lane per element
-                for (uint64_t i = ln; i < cnt; i += G) g_enc_elem<L0>(a, k, e0 + i, pos + i * f.efix, d);
+                for (uint64_t i = ln; i < cnt; i += G) g_enc_elem<0, D>(a, k, e0 + i, pos + i * f.efix, d);
                 pos += cnt * f.efix;
             } else {        // a lane per element at its scanned position
                 // (the group's lanes stay together: the scan's shuffles need all G)
                 for (uint64_t b = 0; b < cnt; b += G) {
                     const uint64_t i = b + ln;
-                    const uint64_t z = i < cnt ? g_elem_bytes<L0>(a, k, e0 + i, d) : 0;
+                    const uint64_t z = i < cnt ? g_elem_bytes<0, D>(a, k, e0 + i, d) : 0;
                     const uint64_t incl = g_incl_scan<G>(z, ln);
-                    if (i < cnt) g_enc_elem<L0>(a, k, e0 + i, pos + incl - z, d);
+                    if (i < cnt) g_enc_elem<0, D>(a, k, e0 + i, pos + incl - z, d);
                     pos += __shfl(incl, G - 1, G);
                 }
             }
@@ -449,7 +448,7 @@ __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint6
     }
 }
 
-template <uint32_t G, bool NEST>
+template <uint32_t G, int D>
 __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a) {
     __shared__ uint64_t soff[kRecPerBlock + 1];
     const uint64_t total = a.totals[0];
@@ -479,7 +478,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a
     const uint32_t ng = kRecThreads / G, ln = threadIdx.x & (G - 1);
     for (uint32_t j0 = 0; j0 < nrec; j0 += ng) {
         const uint32_t j = j0 + threadIdx.x / G;
-        if (j < nrec) g_enc_record<G, NEST>(a, rb + j, soff[j], soff[j + 1] - soff[j], ln);
+        if (j < nrec) g_enc_record<G, D>(a, rb + j, soff[j], soff[j + 1] - soff[j], ln);
     }
 }
 
@@ -684,7 +683,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArg
             const uint32_t i = 4 * tid + u;
             z[u] = 0;
             if (i < nel && own[i] != kNoOwner)
-                z[u] = lay ? g_lay_elem_bytes(a, G, E0 + i) : (uint32_t)g_elem_bytes<1>(a, g, E0 + i, GDisc{});
+                z[u] = lay ? g_lay_elem_bytes(a, G, E0 + i) : (uint32_t)g_elem_bytes<0, 1>(a, g, E0 + i, GDisc{});
             zs += z[u];
         }
         uint64_t ztot;
@@ -772,7 +771,7 @@ __device__ __forceinline__ uint32_t g_walk_dyn(const GField &f, const uint8_t *i
 // a list reads xdrDecodeBoolean() before every element, any non-zero = another,
 // Xdr.java:404-407); cnt[s] += the counts of the counted columns it meets.
 // L = depth: an element at depth 0 may hold an inner group, walked the same way.
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t end, uint64_t &pos,
                                  uint32_t (&cnt)[kMaxSlots], GDisc &d) {
     g = g_uni(g);
@@ -840,9 +839,9 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
                 const GField &m = a.f[g + j];
                 const bool present = !f.ncm || g_dec_field_present(a, g + j, in, pos, end, d);
                 if (m.type == XDRG_T_GROUP) {   // an inner array / list of this element
-                    if constexpr (L == 0) {
+                    if constexpr (L + 1 < D) {
                         if (present) {
-                            const uint32_t err = g_walk_group<1>(a, g + j, in, end, pos, cnt, d);
+                            const uint32_t err = g_walk_group<L + 1, D>(a, g + j, in, end, pos, cnt, d);
                             if (err) return err;
                         }
                     }
@@ -868,7 +867,7 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
 }
 
 // Walk record r; cnt[s] = the record's count of counted column s.
-template <bool NEST>
+template <int D>
 __device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxSlots], uint32_t *sub) {
     const GExtent e = g_extent(a, r);
     const uint8_t *in = a.xdr;
@@ -890,7 +889,7 @@ __device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint3
             continue;
         }
         if (f.type == XDRG_T_GROUP) {
-            const uint32_t err = g_walk_group<NEST ? 0 : 1>(a, k, in, e.b, pos, cnt, d);
+            const uint32_t err = g_walk_group<0, D>(a, k, in, e.b, pos, cnt, d);
             if (err) return err;
             k += 1 + f.nmem;
             continue;
@@ -909,7 +908,7 @@ __device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint3
     return 0;
 }
 
-template <bool NEST>
+template <int D>
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a) {
     constexpr int per = kRecPerThread / kWalkSplit;
     const uint64_t blk = blockIdx.x / kWalkSplit;
@@ -923,7 +922,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a)
         uint32_t cnt[kMaxSlots];
         for (uint32_t s = 0; s < a.nslot; ++s) cnt[s] = 0;
         uint32_t sub;
-        const uint32_t err = g_walk<NEST>(a, r, cnt, &sub);
+        const uint32_t err = g_walk<D>(a, r, cnt, &sub);
         if (err) {
             atomicMin(a.errkey, err_key(r, sub, err));
             for (uint32_t s = 0; s < a.nslot; ++s) cnt[s] = 0;   // a failed record owns nothing
@@ -1028,6 +1027,18 @@ struct GRun {
 __device__ __forceinline__ uint64_t g_rec_base(const GroupArgs &a, uint32_t slot, uint64_t r) {
     return a.rec_base[(uint64_t)(slot - 1) * a.n + r];
 }
+// The first element (row of its members' columns) of group g for record r,
+// inside top-level group k whose first element is e0.
+__device__ __forceinline__ uint64_t g_first_row(const GroupArgs &a, uint32_t k, uint64_t e0, uint32_t g, uint64_t r) {
+    uint64_t mult = 1;
+    for (;;) {
+        if (g == k) return e0 * mult;
+        const GField &G = a.f[g];
+        if (G.kind != XDRG_K_FIXED) return g_rec_base(a, G.slot, r) * mult;
+        mult *= G.count;
+        g = G.grp - 1;
+    }
+}
 // Top-level group k at record r, first element e0: every counted column of
 // its span starts at the record's base (a direct member at row e0, an inner
 // group's member at its record's first inner element), and its first offsets
@@ -1042,18 +1053,17 @@ __device__ __forceinline__ void g_run_init(const GroupArgs &a, uint32_t k, uint6
         if (!m.slot) continue;
         const uint64_t b0 = g_rec_base(a, m.slot, r);
         run.set(m.slot, b0);
-        uint64_t row = e0;
-        if (m.grp != k + 1) {   // a member of an inner group: rows are inner elements
-            const GField &ig = a.f[m.grp - 1];
-            row = ig.kind == XDRG_K_FIXED ? e0 * ig.count : g_rec_base(a, ig.slot, r);
-        }
+        // a member of an inner group: rows are that group's elements, whose
+        // first for record r its parents give (counted ones from their
+        // record base, a T x[N] as N times its parent's first row)
+        const uint64_t row = m.grp == k + 1 ? e0 : g_first_row(a, k, e0, m.grp - 1, r);
         m.offsets[row] = b0;
     }
 }
 
 // Element e of group g with no bytes on the wire (an absent T x[N]'s N
 // elements): fixed members zero, dynamic members and inner arrays empty.
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, uint64_t e, GRun &run) {
     g = g_uni(g);
     const GField &G = a.f[g];
@@ -1061,9 +1071,9 @@ __device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, ui
         j = g_uni(j);
         const GField &m = a.f[g + j];
         if (m.type == XDRG_T_GROUP) {
-            if constexpr (L == 0) {
+            if constexpr (L + 1 < D) {
                 if (m.kind != XDRG_K_FIXED) m.offsets[e + 1] = run.get(m.slot);
-                else for (uint64_t i = e * m.count; i < (e + 1) * m.count; ++i) g_absent_elem<1>(a, g + j, i, run);
+                else for (uint64_t i = e * m.count; i < (e + 1) * m.count; ++i) g_absent_elem<L + 1, D>(a, g + j, i, run);
             }
             j += m.nmem;
             continue;
@@ -1073,11 +1083,13 @@ __device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, ui
     }
 }
 
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in, uint64_t &pos,
                            uint64_t end, GDisc &d, GRun &run);
-// Inner group g (a member of an element at depth 0) of outer element e: its
-// count word or list bools, read as the walk checked them, then its elements.
+// Inner group g (at depth L, a member of an element at depth L - 1) of outer
+// element e: its count word or list bools, read as the walk checked them,
+// then its elements.
+template <int L, int D>
 __device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in,
                                             uint64_t &pos, uint64_t end, GDisc &d, GRun &run) {
     g = g_uni(g);
@@ -1097,7 +1109,7 @@ __device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint
         } else if (i == n) {
             break;
         }
-        g_dec_elem<1>(a, g, i0 + i, in, pos, end, d, run);
+        g_dec_elem<L, D>(a, g, i0 + i, in, pos, end, d, run);
     }
     if (G.kind != XDRG_K_FIXED) {
         G.offsets[e + 1] = i0 + i;
@@ -1106,7 +1118,7 @@ __device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint
 }
 
 // The members of element e of group g (after a list element's TRUE).
-template <int L>
+template <int L, int D>
 __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in, uint64_t &pos,
                            uint64_t end, GDisc &d, GRun &run) {
     g = g_uni(g);
@@ -1116,13 +1128,13 @@ __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint6
         const GField &m = a.f[g + j];
         const bool present = !f.ncm || g_dec_field_present(a, g + j, in, pos, end, d);   // an element's absent arm
         if (m.type == XDRG_T_GROUP) {
-            if constexpr (L == 0) {
+            if constexpr (L + 1 < D) {
                 if (present) {
-                    g_dec_inner(a, g + j, e, in, pos, end, d, run);
+                    g_dec_inner<L + 1, D>(a, g + j, e, in, pos, end, d, run);
                 } else if (m.kind != XDRG_K_FIXED) {
                     m.offsets[e + 1] = run.get(m.slot);
                 } else {
-                    for (uint64_t i = e * m.count; i < (e + 1) * m.count; ++i) g_absent_elem<1>(a, g + j, i, run);
+                    for (uint64_t i = e * m.count; i < (e + 1) * m.count; ++i) g_absent_elem<L + 1, D>(a, g + j, i, run);
                 }
             }
             j += m.nmem;
@@ -1209,10 +1221,9 @@ __device__ __forceinline__ uint64_t g_dyn_words_z(uint32_t z, uint64_t cnt) {
 // EL (element-parallel place): the record's one group leaves descriptors in
 // *el instead of decoding its elements (the block decodes them afterwards,
 // a lane per element).
-template <bool NEST, bool EL = false>
+template <int D, bool EL = false>
 __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in, uint64_t base = 0,
                                              const GElDesc &el = GElDesc{}) {
-    constexpr int L0 = NEST ? 0 : 1;   // depth the record's groups start at (1: inner groups compiled out)
     const GExtent ex = g_extent(a, r);   // the extent the walk checked (clamped to in_len)
     const uint64_t end = ex.b - base;
     uint64_t pos = ex.a + (a.framed ? 4 : 0) - base;
@@ -1229,7 +1240,7 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
             if (f.kind == XDRG_K_FIXED) {   // an absent T x[N]: N zero / empty elements
                 GRun run;
                 g_run_init(a, k, r, r * f.count, run);
-                for (uint64_t e = r * f.count; e < (r + 1) * f.count; ++e) g_absent_elem<L0>(a, k, e, run);
+                for (uint64_t e = r * f.count; e < (r + 1) * f.count; ++e) g_absent_elem<0, D>(a, k, e, run);
             }
             k += 1 + f.nmem;
             continue;
@@ -1287,7 +1298,7 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
                     if (el.nm > 1) el.rel[el.cap + i] = (uint32_t)(run.get(el.ms1) - el.sb1);
                     g_elem_skip(a, k, in, pos, end, d, run);
                 } else {
-                    g_dec_elem<L0>(a, k, e, in, pos, end, d, run);
+                    g_dec_elem<0, D>(a, k, e, in, pos, end, d, run);
                 }
             }
             if (f.kind == XDRG_K_LIST) pos += 4;   // its FALSE
@@ -1309,12 +1320,12 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
     }
 }
 
-template <bool NEST>
+template <int D>
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place(const GroupArgs a) {
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
     const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
     const uint64_t r = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x;
-    if (r < bad) g_dec_record<NEST>(a, r, a.xdr);
+    if (r < bad) g_dec_record<D>(a, r, a.xdr);
 }
 
 // nch 16-byte chunks from the 16-aligned global address a0 into the tile by
@@ -1338,7 +1349,7 @@ __device__ __forceinline__ void g_stage_tile(uint8_t *tile, uintptr_t a0, uint32
 // 16-B loads), and each lane decodes its record from the tile: the walk's
 // dependent length words and list bools become LDS reads instead of HBM
 // round trips.  A record larger than the tile decodes from HBM.
-template <bool NEST>
+template <int D>
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
@@ -1364,8 +1375,8 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
             fits = hi >= lo && hi - lo <= a.dec_tile;
         }
         const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
-        if constexpr (NEST) {
-            // one call site of the record decode (two inlined copies of the NEST
+        if constexpr (D > 1) {
+            // one call site of the record decode (two inlined copies of the nested
             // form kept the kernel arguments in 4 KB of scratch): a record larger
             // than the tile (k1 = 0) decodes from the stream through the same
             // generic pointer, tile-relative positions keep both in range
@@ -1374,13 +1385,13 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
             const uintptr_t a1 = (xb + ext(rb + je) + 15) & ~(uintptr_t)15;
             g_stage_tile(tile, a0, k1 && a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u);
             __syncthreads();
-            if (js + tid < je) g_dec_record<NEST>(a, rb + js + tid, k1 ? tile : a.xdr, k1 ? a0 - xb : 0);
+            if (js + tid < je) g_dec_record<D>(a, rb + js + tid, k1 ? tile : a.xdr, k1 ? a0 - xb : 0);
             __syncthreads();   // the tile's next use
             js = je;
             continue;
         }
         if (k1 == 0) {   // one record larger than the tile: its lane decodes from HBM
-            if (tid == 0) g_dec_record<NEST>(a, rb + js, a.xdr);
+            if (tid == 0) g_dec_record<D>(a, rb + js, a.xdr);
             ++js;
             continue;
         }
@@ -1390,7 +1401,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
         g_stage_tile(tile, a0, a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u);
         __syncthreads();
         // stream offset x of these records is at tile + (x - (a0 - xb))
-        if (js + tid < je) g_dec_record<NEST>(a, rb + js + tid, tile, a0 - xb);
+        if (js + tid < je) g_dec_record<D>(a, rb + js + tid, tile, a0 - xb);
         __syncthreads();   // the tile's next use
         js = je;
     }
@@ -1478,7 +1489,7 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
         }
         const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
         if (k1 == 0) {   // one record larger than the tile or the descriptors: its lane decodes from HBM
-            if (tid == 0) g_dec_record<false>(a, rb + js, a.xdr);
+            if (tid == 0) g_dec_record<1>(a, rb + js, a.xdr);
             ++js;
             continue;
         }
@@ -1492,7 +1503,7 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
         el.sb1 = mb1[js];
         __syncthreads();
         // stream offset x at tile + (x - (a0 - xb))
-        if (js + tid < je) g_dec_record<false, true>(a, rb + js + tid, tile, a0 - xb, el);
+        if (js + tid < je) g_dec_record<1, true>(a, rb + js + tid, tile, a0 - xb, el);
         __syncthreads();   // descriptors
         const uint64_t nel = mE[je] - el.E0;
         XDRG_DCHECK(nel <= a.dec_el);   // (the fit count bounded the sub-batch's elements)
@@ -1509,17 +1520,18 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
             if (el.nm > 1) run.set(el.ms1, el.sb1 + drel[el.cap + i]);
             GDisc d{};
             uint64_t pos = dpos[i];
-            g_dec_elem<1>(a, g, el.E0 + i, tile, pos, ~0ull, d, run);
+            g_dec_elem<0, 1>(a, g, el.E0 + i, tile, pos, ~0ull, d, run);
         }
         __syncthreads();   // the tile's and the descriptors' next use
         js = je;
     }
 }
 
-// Schemas with groups inside group elements take the NEST instantiations;
-// the others keep kernels with the inner-group code compiled out (their
-// running offsets stay in registers).
-template <bool NEST>
+// Kernels are instantiated per group levels D: 1 (no group inside an element:
+// the inner-group code compiled out, running offsets in registers), 2 (one
+// level of groups inside elements, the common nested shapes) and kGrpLevels
+// (deeper schemas; their inlined levels take more registers).
+template <int D>
 static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_t st) {
     const dim3 grid((uint32_t)a.nblocks), block(kRecThreads);
     const dim3 rgrid((uint32_t)((a.n + kRecThreads - 1) / kRecThreads));
@@ -1532,35 +1544,35 @@ static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_
             const hipError_t e = hipMemsetAsync(a.block_sums, 0, (size_t)a.nblocks * 8, st);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_grp_enc_sizes<NEST>, dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
+        hipLaunchKernelGGL(k_grp_enc_sizes<D>, dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
         break;
     case GRP_ENC_PLACE:   // element-parallel (key 41) or G lanes per record (key 32)
-        if (!NEST && a.enc_img && a.ncond && esh) hipLaunchKernelGGL((k_grp_enc_place_el<true, true>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
-        else if (!NEST && a.enc_img && a.ncond) hipLaunchKernelGGL((k_grp_enc_place_el<true, false>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
-        else if (!NEST && a.enc_img && esh) hipLaunchKernelGGL((k_grp_enc_place_el<false, true>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
-        else if (!NEST && a.enc_img) hipLaunchKernelGGL((k_grp_enc_place_el<false, false>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
-        else if (a.enc_lanes == 4) hipLaunchKernelGGL((k_grp_enc_place<4, NEST>), grid, block, 0, st, a);
-        else if (a.enc_lanes == 8) hipLaunchKernelGGL((k_grp_enc_place<8, NEST>), grid, block, 0, st, a);
-        else if (a.enc_lanes == 16) hipLaunchKernelGGL((k_grp_enc_place<16, NEST>), grid, block, 0, st, a);
-        else if (a.enc_lanes == 32) hipLaunchKernelGGL((k_grp_enc_place<32, NEST>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((k_grp_enc_place<64, NEST>), grid, block, 0, st, a);
+        if (D == 1 && a.enc_img && a.ncond && esh) hipLaunchKernelGGL((k_grp_enc_place_el<true, true>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (D == 1 && a.enc_img && a.ncond) hipLaunchKernelGGL((k_grp_enc_place_el<true, false>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (D == 1 && a.enc_img && esh) hipLaunchKernelGGL((k_grp_enc_place_el<false, true>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (D == 1 && a.enc_img) hipLaunchKernelGGL((k_grp_enc_place_el<false, false>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (a.enc_lanes == 4) hipLaunchKernelGGL((k_grp_enc_place<4, D>), grid, block, 0, st, a);
+        else if (a.enc_lanes == 8) hipLaunchKernelGGL((k_grp_enc_place<8, D>), grid, block, 0, st, a);
+        else if (a.enc_lanes == 16) hipLaunchKernelGGL((k_grp_enc_place<16, D>), grid, block, 0, st, a);
+        else if (a.enc_lanes == 32) hipLaunchKernelGGL((k_grp_enc_place<32, D>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((k_grp_enc_place<64, D>), grid, block, 0, st, a);
         break;
     case GRP_DEC_WALK:
         if (kWalkSplit > 1 && a.nslot) {
             const hipError_t e = hipMemsetAsync(a.block_sums, 0, (size_t)a.nslot * a.nblocks * 8, st);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_grp_dec_walk<NEST>, dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
+        hipLaunchKernelGGL(k_grp_dec_walk<D>, dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
         break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
     case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
-        if (!NEST && a.dec_el && a.dec_tile) {
+        if (D == 1 && a.dec_el && a.dec_tile) {
             const size_t lds = kElMeta + a.dec_tile + 12 * (size_t)a.dec_el;
             if (a.lay_g == a.el_g + 1) hipLaunchKernelGGL(k_grp_dec_place_el<true>, rgrid, block, lds, st, a);
             else hipLaunchKernelGGL(k_grp_dec_place_el<false>, rgrid, block, lds, st, a);
         }
-        else if (a.dec_tile) hipLaunchKernelGGL(k_grp_dec_place_lds<NEST>, rgrid, block, a.dec_tile, st, a);
-        else hipLaunchKernelGGL(k_grp_dec_place<NEST>, rgrid, block, 0, st, a);
+        else if (a.dec_tile) hipLaunchKernelGGL(k_grp_dec_place_lds<D>, rgrid, block, a.dec_tile, st, a);
+        else hipLaunchKernelGGL(k_grp_dec_place<D>, rgrid, block, 0, st, a);
         break;
     default: break;
     }
@@ -1569,8 +1581,9 @@ static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_
 
 int launch_group_phase(const GroupArgs &a, int phase, void *stream) {
     if (phase < GRP_ENC_SIZES || phase > GRP_DEC_PLACE) return (int)hipErrorInvalidValue;
-    const hipError_t e = a.nest ? launch_group_phase_t<true>(a, phase, (hipStream_t)stream)
-                                : launch_group_phase_t<false>(a, phase, (hipStream_t)stream);
+    const hipError_t e = a.levels > 2 ? launch_group_phase_t<kGrpLevels>(a, phase, (hipStream_t)stream)
+                       : a.levels == 2 ? launch_group_phase_t<2>(a, phase, (hipStream_t)stream)
+                                       : launch_group_phase_t<1>(a, phase, (hipStream_t)stream);
     return (int)(e != hipSuccess ? e : hipGetLastError());
 }
 

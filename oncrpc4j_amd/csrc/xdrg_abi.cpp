@@ -75,9 +75,10 @@ static bool field_valid(const xdrg_field &f) {
     if (f.kind == XDRG_K_FIXED && f.count > 0x7fffffffu) return false;
     return true;
 }
-// The group at fs[k] spanning at most `lim` fields (depth 0 = top level):
-// grp[] of its members (its immediate members get k + 1, an inner group's
-// members that group), *sized = an element encodes to >= 1 XDR word.
+// The group at fs[k] spanning at most `lim` fields (depth 0 = top level,
+// groups nest down to depth kGrpLevels - 1): grp[] of its members (its
+// immediate members get k + 1, an inner group's members that group),
+// *sized = an element encodes to >= 1 XDR word.
 static bool group_valid(const xdrg_field *fs, size_t k, size_t lim, int depth, std::vector<uint32_t> &grp,
                         bool *sized) {
     const xdrg_field &g = fs[k];
@@ -91,7 +92,8 @@ static bool group_valid(const xdrg_field *fs, size_t k, size_t lim, int depth, s
         grp[k + j] = (uint32_t)k + 1;
         if (f.type == XDRG_T_GROUP) {   // an array of structs / list inside the element
             bool s2 = false;
-            if (depth > 0 || !group_valid(fs, k + j, (size_t)m + 1 - j, depth + 1, grp, &s2) || !s2) return false;
+            if (depth + 1 >= kGrpLevels || !group_valid(fs, k + j, (size_t)m + 1 - j, depth + 1, grp, &s2) || !s2)
+                return false;
             sz |= f.kind != XDRG_K_FIXED || f.count > 0;
             j += f.reserved;
             continue;
@@ -125,8 +127,8 @@ extern "C" int xdrg_schema_create_cond(const xdrg_field *fields, size_t nfields,
     if (!s) return XDRG_E_NOMEM;
     uint64_t words = 0;
     // repeated groups: {XDRG_T_GROUP, FIXED / DYNAMIC / LIST, count, m} and m
-    // member fields of the base types or (one level down) a group of them,
-    // an element of at least one XDR word
+    // member fields of the base types or groups of them (down to kGrpLevels
+    // levels), an element of at least one XDR word
     s->grp.assign(nfields, 0);
     for (size_t k = 0; k < nfields; ++k) {
         if (fields[k].type != XDRG_T_GROUP) continue;
@@ -736,6 +738,13 @@ static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols
     }
     a.ncond = s->ncond;
     a.nest = s->nested ? 1u : 0u;
+    a.levels = 1;
+    for (size_t k = 0; k < s->f.size(); ++k) {   // a group's level = its group ancestors
+        if (s->f[k].type != XDRG_T_GROUP) continue;
+        uint32_t lv = 1;
+        for (uint32_t g = s->grp[k]; g; g = s->grp[g - 1]) ++lv;
+        if (lv > a.levels) a.levels = lv;
+    }
     // the element layout of a schema's one top-level group (GroupArgs::lay_g)
     a.lay_g = 0;
     for (uint32_t k = 0; k < a.nf && s->ngroups == 1 && !a.nest; ++k) {

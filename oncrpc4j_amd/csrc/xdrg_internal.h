@@ -340,6 +340,12 @@ int launch_copy_link(uint8_t *dst, const uint8_t *src, uint64_t bytes, void *str
 // field, a DYNAMIC / LIST group (its elements) or a group's dynamic member
 // (its values over the record's elements).
 constexpr int kMaxSlots = 16;
+// Group nesting levels: a top-level group (level 0) and groups inside its
+// elements down to level kGrpLevels - 1 (jrpcgen nests arrays of structs and
+// lists without a limit, jrpcgen.java:856-906; the kernels are instantiated
+// per level, kGrpLast = the innermost, whose elements hold no group).
+constexpr int kGrpLevels = 4;
+constexpr int kGrpLast = kGrpLevels - 1;
 struct GField {
     uint32_t type, kind, nsz, xsz;
     uint32_t count;   // FIXED count (of a field's elements or a group's)
@@ -383,7 +389,8 @@ struct GroupArgs {
     uint32_t slot_field[kMaxSlots];
     uint32_t ncond;              // conditional fields (0: every record / element has all of them)
     uint32_t dec_tile;           // decode place: LDS tile bytes (0: records read from HBM; key 33)
-    uint32_t nest;               // some group holds an inner group (the NEST kernels)
+    uint32_t nest;               // some group holds an inner group
+    uint32_t levels;             // group levels of the schema (1 + the deepest nesting; the kernels' D)
     uint32_t dec_el;             // decode place: element-parallel, descriptors per sub-batch (0: off; key 38)
     uint32_t el_g;               // the element-parallel place's group (the schema's one top-level group)
     // 1 + the top-level group whose elements have one layout (no conditional

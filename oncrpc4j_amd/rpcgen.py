@@ -38,16 +38,17 @@ element), and a group may itself sit in a union arm or behind optional data
 (a condition on the group field).  A fixed-size array of structs inside an
 element (`T x[N]`, no count word) unrolls into N copies of T's members; a
 variable-length array of structs or a list inside an element becomes an
-inner group (one level down: its members are the inner element's flattened
-fields, its rows the outer elements).  Still not one tape: arrays of structs
-or lists two levels down, and recursion anywhere but a struct's last
-declaration.
+inner group (its members are the inner element's flattened fields, its rows
+the outer elements), and so on down to GROUP_LEVELS levels.  Still not one
+tape: deeper nesting, arrays of list heads, and recursion anywhere but a
+struct's last declaration.
 """
 import re
 
 from . import abi
 
 INT = (abi.T_INT, abi.K_SCALAR, 0)
+GROUP_LEVELS = 4   # group nesting levels the engine batches (xdrg_internal.h kGrpLevels)
 
 
 class XdrSyntaxError(ValueError):
@@ -340,14 +341,15 @@ class _Tape:
         element, e.g. READDIRPLUS's post_op_attr).  A fixed array of structs
         inside an element unrolls into its elements' members (decl()); a
         variable-length one or a list inside an element is an inner group
-        (its span counted in this group's members), one level down only."""
+        (its span counted in this group's members), down to GROUP_LEVELS
+        levels (the engine's kernels are instantiated per level)."""
         sub = _Tape(self.s, in_element=True, depth=self.depth + 1)
         for d in decls:
             sub.decl(d, f"{where}.{d.name}", None, stack + (st.name,))
         fields, conds = sub.result()
-        if self.depth >= 1 and any(f[0] == abi.T_GROUP for f in fields):
+        if self.depth + 1 >= GROUP_LEVELS and any(f[0] == abi.T_GROUP for f in fields):
             raise NotBatchable(f"{where}: elements of {st.name} hold arrays of structs or lists "
-                               f"two group levels down (one inner level is batched)")
+                               f"{GROUP_LEVELS} group levels down ({GROUP_LEVELS} levels are batched)")
         if not fields:
             raise NotBatchable(f"{where}: elements of {st.name} have no fields")
         g = self.add((abi.T_GROUP, kind, count, len(fields)), guard)

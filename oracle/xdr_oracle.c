@@ -657,10 +657,11 @@ static int encode_record(xo_stream *s, const xdrg_field *fs, size_t nf, const xd
 }
 
 /* Repeated groups (include/xdrg.h): the group field, then `reserved` member
- * fields of the base types or — one level down — a group whose members are
- * base types (its own span counted in the outer `reserved`); an element that
- * encodes to at least one byte (list elements carry their bool, a counted
- * inner array its count). */
+ * fields of the base types or groups of them, down to XO_GROUP_LEVELS levels
+ * (an inner group's own span counted in the outer `reserved`); an element
+ * that encodes to at least one byte (list elements carry their bool, a
+ * counted inner array its count). */
+#define XO_GROUP_LEVELS 4
 static int has_group(const xdrg_field *fs, size_t nf) {
     for (size_t k = 0; k < nf; k++) if (fs[k].type == XDRG_T_GROUP) return 1;
     return 0;
@@ -677,7 +678,8 @@ static int check_group(const xdrg_field *g, size_t lim, int depth, int *sized_ou
         const xdrg_field *f = &g[j];
         if (f->type == XDRG_T_GROUP) {
             int s2 = 0;
-            if (depth > 0 || check_group(f, (size_t)m + 1 - j, depth + 1, &s2) || !s2) return XDRG_E_INVAL;
+            if (depth + 1 >= XO_GROUP_LEVELS || check_group(f, (size_t)m + 1 - j, depth + 1, &s2) || !s2)
+                return XDRG_E_INVAL;
             sized |= f->kind != XDRG_K_FIXED || f->count > 0;
             j += f->reserved;
             continue;
@@ -945,6 +947,27 @@ static void absent_group(const xdrg_field *g, xdrg_column *gc, uint64_t i) {
         }
 }
 
+/* Capacity of every column in group g's span for the rows one record adds:
+ * its members' from row e0 on (the group's first element for the record),
+ * an inner group's elements from its first row i0 and, recursively, its own
+ * members; mcnt[j] = what the record's walk counted for member j. */
+static int members_fit(const xdrg_field *g, const xdrg_column *gc, uint64_t e0, const uint64_t *mcnt) {
+    for (uint32_t j = 1; j <= g->reserved; j++) {
+        if (g[j].type == XDRG_T_GROUP) {   /* an inner array: its elements start at row i0 */
+            const xdrg_field *ig = &g[j];
+            const xdrg_column *ic = &gc[j];
+            const uint64_t i0 = ig->kind == XDRG_K_FIXED ? e0 * ig->count : ic->offsets[e0];
+            if (ig->kind != XDRG_K_FIXED && i0 + mcnt[j] > ic->cap) return XDRG_E_CAPACITY;
+            int rc = members_fit(ig, ic, i0, mcnt + j);
+            if (rc) return rc;
+            j += ig->reserved;
+            continue;
+        }
+        if (g[j].kind == XDRG_K_DYNAMIC && gc[j].offsets[e0] + mcnt[j] > gc[j].cap) return XDRG_E_CAPACITY;
+    }
+    return XDRG_OK;
+}
+
 static int decode_group(xo_stream *s, const xdrg_field *g, xdrg_column *gc, uint64_t i,
                         const xo_conds *cc, size_t gk, int *pres, int32_t *val) {
     const uint32_t m = g->reserved;
@@ -954,20 +977,8 @@ static int decode_group(xo_stream *s, const xdrg_field *g, xdrg_column *gc, uint
     if (rc) return rc;
     const uint64_t e0 = g->kind == XDRG_K_FIXED ? i * g->count : gc->offsets[i];
     if (g->kind != XDRG_K_FIXED && e0 + cnt > gc->cap) return XDRG_E_CAPACITY;
-    for (uint32_t j = 1; j <= m; j++) {
-        if (g[j].type == XDRG_T_GROUP) {   /* an inner array: its elements start at row i0 */
-            const xdrg_field *ig = &g[j];
-            const xdrg_column *ic = &gc[j];
-            const uint64_t i0 = ig->kind == XDRG_K_FIXED ? e0 * ig->count : ic->offsets[e0];
-            if (ig->kind != XDRG_K_FIXED && i0 + mcnt[j] > ic->cap) return XDRG_E_CAPACITY;
-            for (uint32_t jj = 1; jj <= ig->reserved; jj++)
-                if (ig[jj].kind == XDRG_K_DYNAMIC && ic[jj].offsets[i0] + mcnt[j + jj] > ic[jj].cap)
-                    return XDRG_E_CAPACITY;
-            j += ig->reserved;
-            continue;
-        }
-        if (g[j].kind == XDRG_K_DYNAMIC && gc[j].offsets[e0] + mcnt[j] > gc[j].cap) return XDRG_E_CAPACITY;
-    }
+    rc = members_fit(g, gc, e0, mcnt);
+    if (rc) return rc;
     if (g->kind == XDRG_K_DYNAMIC) s->pos += 4;
     for (uint64_t e = e0; e < e0 + cnt; e++) {
         if (g->kind == XDRG_K_LIST) s->pos += 4;

@@ -26,6 +26,9 @@ fixtures are plain JSON data and travel, this script's inputs do not need to.
    list elements (rpcgen/chunk_map.x), packed by xdrlib.
    volume_index_vectors.json — a list and a counted array of structs inside
    list elements (rpcgen/volume_index.x), packed by xdrlib.
+   acl_tree_vectors.json — four group levels: a list, a list inside its
+   elements, a counted array inside those and another inside those, with
+   optional data at the third level (rpcgen/acl_tree.x), packed by xdrlib.
 6. reference_rpcgen_vectors.json — the arguments and results of the
    reference's own rpcgen test programs, oncrpc4j-rpcgen/src/test/xdr/
    BlobStore.x (put(Key, Value) / get(Key) -> Value, Value a bool union over
@@ -628,6 +631,93 @@ def volume_index_vectors(seed=0x7015):
     return out
 
 
+# ---- four group levels -------------------------------------------------------
+# tests/golden/rpcgen/acl_tree.x `tree_res`: the `tree_entry *next` list, a
+# `tree_ace *next` list inside each entry, `tree_principal who<8>` inside each
+# access entry (each with optional data) and `tree_tag tags<>` inside each
+# principal — packed by xdrlib from the declarations; records in tape layout
+# (a group's slot holds its elements, the slots of everything inside it None,
+# an absent gid as 0).
+def acl_tree_vectors(seed=0xAC17):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oncrpc4j_amd import rpcgen
+    spec = rpcgen.parse_file(os.path.join(HERE, "rpcgen", "acl_tree.x"))
+    fields, conds = spec.tape("tree_res")
+    rng = random.Random(seed)
+    out = {"source": "CPython 3.10 stdlib xdrlib (RFC 1014) packing acl_tree.x `tree_res` from its "
+                     "declarations (four levels of lists and counted arrays of structs, "
+                     "jrpcgen.java:835-906)",
+           "seed": seed, "fields": [list(f) for f in fields], "conds": [list(c) for c in conds],
+           "batches": []}
+    word = lambda k: bytes(rng.choice(b"abcdefghijklmnop-._") for _ in range(rng.randrange(0, k)))
+    for framed in (False, True):
+        n = 40
+        records, chunks, probes = [], [], []
+        base = 0
+        for i in range(n):
+            p = xdrlib.Packer()
+            at = lambda kind: probes.append([i, kind, base + (4 if framed else 0) + len(p.get_buffer())])
+            status = rng.choice([0, 0, 0, 2, -5])
+            p.pack_int(status)
+            ents = []
+            for _ in range(rng.choice([0, 1, 2, 3, 5])):
+                cookie, name = rng.getrandbits(64), word(40)
+                p.pack_bool(True)
+                p.pack_uhyper(cookie)
+                p.pack_string(name)
+                aces = []
+                for _ in range(rng.choice([0, 1, 1, 2, 4])):
+                    mask = rng.getrandbits(32)
+                    at("ace_bool")
+                    p.pack_bool(True)
+                    p.pack_uint(mask)
+                    whos = []
+                    k = rng.choice([0, 1, 2, 3])
+                    at("who_count")
+                    p.pack_uint(k)
+                    for _ in range(k):
+                        pid, realm = rng.getrandbits(32), word(20)
+                        has = rng.random() < 0.5
+                        gid = rng.getrandbits(32) if has else 0
+                        p.pack_uint(pid)
+                        at("realm_len")
+                        p.pack_string(realm)
+                        p.pack_bool(has)
+                        if has:
+                            p.pack_uint(gid)
+                        tags = []
+                        t = rng.choice([0, 0, 1, 2, 4])
+                        at("tags_count")
+                        p.pack_uint(t)
+                        for _ in range(t):
+                            key, val = rng.getrandbits(32) - (1 << 31), word(17)
+                            p.pack_int(key)
+                            at("value_len")
+                            p.pack_opaque(val)
+                            tags.append([key, val.hex()])
+                        whos.append([pid, realm.hex(), int(has), gid, tags, None, None])
+                    aces.append([mask, whos] + [None] * 7)
+                p.pack_bool(False)   # the acl list ends
+                ents.append([cookie, name.hex(), aces] + [None] * 9)
+            p.pack_bool(False)       # the entry list ends
+            eof = rng.randint(0, 1)
+            p.pack_bool(eof)
+            body = p.get_buffer()
+            if framed:
+                body = struct.pack(">I", len(body) | 0x80000000) + body
+            chunks.append(body)
+            base += len(body)
+            records.append([status, ents] + [None] * 12 + [eof])
+        offs = [0]
+        for ch in chunks:
+            offs.append(offs[-1] + len(ch))
+        out["batches"].append({"name": "acl_tree", "framed": framed, "n": n, "records": records,
+                               "xdr": b"".join(chunks).hex(), "rec_offsets": offs,
+                               "probes": probes})   # [record, what, stream offset of that word]
+    return out
+
+
 # ---- framing -----------------------------------------------------------------
 def call_message(xid, args_string):
     """RpcMessageParserTCPTest.XdrStreamBuilder.build (:127-142): CALL header,
@@ -853,6 +943,7 @@ GENERATORS = {"kat_reference.json": kat_reference, "kat_jdk_nan.json": kat_jdk_n
               "group_cond_vectors.json": group_cond_vectors,
               "chunk_map_vectors.json": chunk_map_vectors,
               "volume_index_vectors.json": volume_index_vectors,
+              "acl_tree_vectors.json": acl_tree_vectors,
               "reference_rpcgen_vectors.json": reference_rpcgen_vectors}
 
 

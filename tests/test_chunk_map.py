@@ -61,8 +61,17 @@ def test_unroll_limits():
               struct r { q qs<>; };
               struct e { r xs<4>; e *next; };
               struct top { e *l; };"""
-    with pytest.raises(rpcgen.NotBatchable):   # two levels down
-        rpcgen.parse(deep).tape("top")
+    f, c = rpcgen.parse(deep).tape("top")   # three levels: list -> counted array -> counted array
+    assert f == [(abi.T_GROUP, abi.K_LIST, 0, 3), (abi.T_GROUP, abi.K_DYNAMIC, 0, 2),
+                 (abi.T_GROUP, abi.K_DYNAMIC, 0, 1), (abi.T_INT, abi.K_SCALAR, 0)] and not c
+    deeper = """struct z { int a; };
+                struct y { z zs<>; };
+                struct x { y ys<>; };
+                struct q { x xs<>; };
+                struct r { q qs<>; };
+                struct top { r rs<>; };"""
+    with pytest.raises(rpcgen.NotBatchable):   # five levels (rpcgen.GROUP_LEVELS = 4)
+        rpcgen.parse(deeper).tape("top")
     ok = """struct r { int a; hyper b; };
             struct e { r xs[3]; };
             struct top { e l<>; };"""

@@ -107,7 +107,7 @@ def test_oracle_group_capacity_after_walk():
     [(G, DY, 0, 0), (I, SC, 0)],               # no members
     [(G, DY, 0, 3), (I, SC, 0)],               # members past the tape
     [(G, LS, 2, 1), (I, SC, 0)],               # a list has no count
-    [(G, DY, 0, 3), (G, DY, 0, 2), (G, DY, 0, 1), (I, SC, 0)],   # groups two levels down
+    [(G, DY, 0, 5), (G, DY, 0, 4), (G, DY, 0, 3), (G, DY, 0, 2), (G, DY, 0, 1), (I, SC, 0)],   # five levels
     [(G, DY, 0, 2), (I, SC, 0), (G, DY, 0, 1), (I, SC, 0)],      # an inner group past its parent's span
     [(G, DY, 0, 2), (G, FX, 2, 1), (I, FX, 0)],                  # inner elements of no bytes
     [(G, FX, 4, 1), (I, FX, 0)],               # elements of no bytes

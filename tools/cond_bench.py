@@ -10,7 +10,9 @@
   512 Ki records of 0..12 entries;
 * chunk map: chunk_map.x `chunk_map` replies (a `chunk_ent *next` list whose
   every element holds `replica copies[2]`, unrolled, each replica with an
-  optional checksum and a tag opaque<16>), 1 Mi records of 0..12 entries.
+  optional checksum and a tag opaque<16>), 1 Mi records of 0..12 entries;
+* volume_index.x and acl_tree.x: groups inside group elements, two and four
+  group levels.
 
 Device-resident, HIP-event timed encode and decode (median of reps); bytes =
 native + XDR per direction, as bench.py counts them; round trip checked."""
@@ -104,6 +106,10 @@ def main():
     f, c = vix.tape("volume_index")
     print(json.dumps(run("volume_index replies (a list and an array inside list elements)", f, c, 512 << 10,
                          (0, 24), (0, 6))), flush=True)
+    acl = rpcgen.parse_file(os.path.join(g, "acl_tree.x"))
+    f, c = acl.tape("tree_res")
+    print(json.dumps(run("acl_tree replies (four group levels: entry list > ace list > who<8> > tags<>)", f, c,
+                         256 << 10, (0, 24), (0, 4))), flush=True)
 
 
 if __name__ == "__main__":
