@@ -39,9 +39,11 @@ element), and a group may itself sit in a union arm or behind optional data
 element (`T x[N]`, no count word) unrolls into N copies of T's members; a
 variable-length array of structs or a list inside an element becomes an
 inner group (its members are the inner element's flattened fields, its rows
-the outer elements), and so on down to GROUP_LEVELS levels.  Still not one
-tape: deeper nesting, arrays of list heads, and recursion anywhere but a
-struct's last declaration.
+the outer elements), and so on down to GROUP_LEVELS levels.  An array of list
+nodes (each element the head of a chain, jrpcgen.java:1103-1121) is a group
+whose element is the head's fields followed by the chain's remaining nodes as
+an inner list.  Still not one tape: deeper nesting, and recursion anywhere but
+a struct's last declaration.
 """
 import re
 
@@ -368,9 +370,12 @@ class _Tape:
             self.group(abi.K_LIST, 0, st, st.decls[:-1], where, guard, stack)
             return
         if decl.kind in (FIXED, DYNAMIC) and st is not None:
-            # `T x<>` / `T x[N]` of a struct: the count (dynamic), then the elements
-            if self._list_struct(st):
-                raise NotBatchable(f"{where}: an array of list heads {st.name}")
+            # `T x<>` / `T x[N]` of a struct: the count (dynamic), then the elements.
+            # An element of a list node type T is a list head: T's xdrEncode is a
+            # do/while over the chain (jrpcgen.java:1103-1121), the head's fields
+            # and then xdrEncodeBoolean(next != null) + the next node's fields ...
+            # — the head's fields followed by the `T *next` list, which st.decls
+            # already ends with (decl() makes it an inner list group).
             if self.in_element and decl.kind == FIXED:
                 # `T x[N]` inside a group element: no count word on the wire
                 # (jrpcgen.java:856-906, xdrEncodeFixedVector), so the N

@@ -29,6 +29,8 @@ fixtures are plain JSON data and travel, this script's inputs do not need to.
    acl_tree_vectors.json — four group levels: a list, a list inside its
    elements, a counted array inside those and another inside those, with
    optional data at the third level (rpcgen/acl_tree.x), packed by xdrlib.
+   seg_lists_vectors.json — arrays of list heads and a list head held by
+   value (rpcgen/seg_lists.x), packed by xdrlib.
 6. reference_rpcgen_vectors.json — the arguments and results of the
    reference's own rpcgen test programs, oncrpc4j-rpcgen/src/test/xdr/
    BlobStore.x (put(Key, Value) / get(Key) -> Value, Value a bool union over
@@ -718,6 +720,77 @@ def acl_tree_vectors(seed=0xAC17):
     return out
 
 
+# ---- arrays of list heads ----------------------------------------------------
+# tests/golden/rpcgen/seg_lists.x `seg_map`: `seg_node chains<>` and
+# `seg_node spare[2]` (arrays whose elements are list heads: each element is
+# a node and the rest of its chain, jrpcgen.java:1103-1121) and a `seg_node`
+# held by value — packed by xdrlib from the declarations; records in tape
+# layout (a head's own fields, then its chain as an inner list).
+def seg_lists_vectors(seed=0x5E61):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oncrpc4j_amd import rpcgen
+    spec = rpcgen.parse_file(os.path.join(HERE, "rpcgen", "seg_lists.x"))
+    fields, conds = spec.tape("seg_map")
+    rng = random.Random(seed)
+    out = {"source": "CPython 3.10 stdlib xdrlib (RFC 1014) packing seg_lists.x `seg_map` from its "
+                     "declarations (arrays of list heads, jrpcgen.java:856-906, 1103-1121)",
+           "seed": seed, "fields": [list(f) for f in fields], "conds": [list(c) for c in conds],
+           "batches": []}
+
+    def chain(p, at):
+        """One list head and its chain: [head fields..., rest elements]."""
+        nodes = [[rng.getrandbits(64), rng.getrandbits(32),
+                  bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 9)))]
+                 for _ in range(1 + rng.choice([0, 0, 1, 2, 5]))]
+        for j, (off, ln, tag) in enumerate(nodes):
+            p.pack_uhyper(off); p.pack_uint(ln)
+            at("tag_len")
+            p.pack_opaque(tag)
+            at("next_bool")
+            p.pack_bool(j + 1 < len(nodes))   # xdrEncodeBoolean($this != null)
+        fmt = lambda nd: [nd[0], nd[1], nd[2].hex()]
+        return fmt(nodes[0]), [fmt(nd) for nd in nodes[1:]]
+
+    for framed in (False, True):
+        n = 48
+        records, chunks, probes = [], [], []
+        base = 0
+        for i in range(n):
+            p = xdrlib.Packer()
+            at = lambda kind: probes.append([i, kind, base + (4 if framed else 0) + len(p.get_buffer())])
+            rid = rng.getrandbits(32)
+            p.pack_uint(rid)
+            k = rng.choice([0, 1, 2, 3, 7])
+            at("chains_count")
+            p.pack_uint(k)
+            chains = []
+            for _ in range(k):
+                head, rest = chain(p, at)
+                chains.append(head + [rest, None, None, None])
+            spare = []
+            for _ in range(2):
+                head, rest = chain(p, at)
+                spare.append(head + [rest, None, None, None])
+            head, rest = chain(p, at)
+            done = rng.randint(0, 1)
+            p.pack_bool(done)
+            body = p.get_buffer()
+            if framed:
+                body = struct.pack(">I", len(body) | 0x80000000) + body
+            chunks.append(body)
+            base += len(body)
+            records.append([rid, chains] + [None] * 7 + [spare] + [None] * 7 + head + [rest, None, None, None,
+                                                                                     done])
+        offs = [0]
+        for ch in chunks:
+            offs.append(offs[-1] + len(ch))
+        out["batches"].append({"name": "seg_lists", "framed": framed, "n": n, "records": records,
+                               "xdr": b"".join(chunks).hex(), "rec_offsets": offs,
+                               "probes": probes})   # [record, what, stream offset of that word]
+    return out
+
+
 # ---- framing -----------------------------------------------------------------
 def call_message(xid, args_string):
     """RpcMessageParserTCPTest.XdrStreamBuilder.build (:127-142): CALL header,
@@ -943,7 +1016,7 @@ GENERATORS = {"kat_reference.json": kat_reference, "kat_jdk_nan.json": kat_jdk_n
               "group_cond_vectors.json": group_cond_vectors,
               "chunk_map_vectors.json": chunk_map_vectors,
               "volume_index_vectors.json": volume_index_vectors,
-              "acl_tree_vectors.json": acl_tree_vectors,
+              "acl_tree_vectors.json": acl_tree_vectors, "seg_lists_vectors.json": seg_lists_vectors,
               "reference_rpcgen_vectors.json": reference_rpcgen_vectors}
 
 
