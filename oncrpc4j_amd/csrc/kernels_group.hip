@@ -20,6 +20,8 @@
 // it again and stores every value).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "xdrg_device.h"
 #include "xdrg_internal.h"
 
@@ -260,6 +262,18 @@ __device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g
     return s;
 }
 
+// The kernels' GroupArgs (one by-value kernel argument, 4 KB).  The deepest
+// instances (D = kGrpLevels) read it in place in the kernarg segment: their
+// inlined four levels of element functions make the compiler give the
+// argument a private copy otherwise (4 KB of scratch per lane, a 4 KB copy
+// per lane at entry).  The others keep the plain argument (no change in their
+// code).
+template <int D>
+__device__ __forceinline__ const GroupArgs &g_kargs(const GroupArgs &a) {
+    if constexpr (D > 2) return *(const GroupArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    else return a;
+}
+
 // ===========================================================================
 // Encode
 // ===========================================================================
@@ -299,7 +313,8 @@ __device__ __forceinline__ uint64_t g_rec_size(const GroupArgs &a, uint64_t r) {
 constexpr int kWalkSplit = XDRG_WALK_SPLIT;
 static_assert(kRecPerThread % kWalkSplit == 0, "records per lane");
 template <int D>
-__global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a) {
+__global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a_) {
+    const GroupArgs &a = g_kargs<D>(a_);
     constexpr int per = kRecPerThread / kWalkSplit;
     const uint64_t blk = blockIdx.x / kWalkSplit;
     const uint64_t r0 = blk * kRecPerBlock + (uint64_t)(blockIdx.x % kWalkSplit) * (kRecPerBlock / kWalkSplit) +
@@ -393,7 +408,7 @@ __device__ __forceinline__ uint64_t g_incl_scan(uint64_t v, uint32_t ln) {
     return v;
 }
 template <uint32_t G, int D>
-__device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint64_t size, uint32_t ln) {
+__device__ __forceinline__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint64_t size, uint32_t ln) {
     uint8_t *out = a.xdr;
     if (a.framed) {   // GrizzlyRpcTransport.java:103-110
         if (ln == 0) *(uint32_t *)(out + pos) = bswap32r((uint32_t)(size - 4) | kLastFrag);
@@ -449,7 +464,8 @@ __device__ void g_enc_record(const GroupArgs &a, uint64_t r, uint64_t pos, uint6
 }
 
 template <uint32_t G, int D>
-__global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a) {
+__global__ __launch_bounds__(kRecThreads) void k_grp_enc_place(const GroupArgs a_) {
+    const GroupArgs &a = g_kargs<D>(a_);
     __shared__ uint64_t soff[kRecPerBlock + 1];
     const uint64_t total = a.totals[0];
     if (total > a.xdr_cap) return;   // XDRG_E_CAPACITY: write nothing
@@ -909,7 +925,8 @@ __device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint3
 }
 
 template <int D>
-__global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a) {
+__global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a_) {
+    const GroupArgs &a = g_kargs<D>(a_);
     constexpr int per = kRecPerThread / kWalkSplit;
     const uint64_t blk = blockIdx.x / kWalkSplit;
     const uint64_t r0 = blk * kRecPerBlock + (uint64_t)(blockIdx.x % kWalkSplit) * (kRecPerBlock / kWalkSplit) +
@@ -1023,7 +1040,34 @@ struct GRun {
 #pragma unroll
         for (int q = 0; q < kMaxSlots; ++q) v[q] = (uint32_t)q + 1 == slot ? x : v[q];
     }
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int q = 0; q < kMaxSlots; ++q) v[q] = 0;
+    }
 };
+// The same in LDS, a column per lane (slot q of lane t at v[q * kRecThreads],
+// v = base + t), for the deepest instances (D > 2): their inlined levels left
+// no registers for 16 running offsets and their selects (dec place 245-256
+// VGPRs, one wave per SIMD).
+struct GRunL {
+    uint64_t *v;
+    __device__ __forceinline__ uint64_t get(uint32_t slot) const { return slot ? v[(slot - 1) * kRecThreads] : 0; }
+    __device__ __forceinline__ void set(uint32_t slot, uint64_t x) {
+        if (slot) v[(slot - 1) * kRecThreads] = x;
+    }
+    __device__ __forceinline__ void zero() {
+        for (int q = 0; q < kMaxSlots; ++q) v[q * kRecThreads] = 0;
+    }
+};
+#ifndef XDRG_RUN_LDS_D
+#define XDRG_RUN_LDS_D 1   // instances deeper than this keep their running offsets in LDS
+#endif
+constexpr bool g_run_lds(int D) { return D > XDRG_RUN_LDS_D; }
+template <int D>
+using GRunOf = typename std::conditional<g_run_lds(D), GRunL, GRun>::type;
+__device__ __forceinline__ void g_run_bind(GRun &, uint64_t *) {}
+__device__ __forceinline__ void g_run_bind(GRunL &run, uint64_t *rl) { run.v = rl; }
+constexpr uint32_t kRunLds = kMaxSlots * kRecThreads;   // GRunL words of a block
 __device__ __forceinline__ uint64_t g_rec_base(const GroupArgs &a, uint32_t slot, uint64_t r) {
     return a.rec_base[(uint64_t)(slot - 1) * a.n + r];
 }
@@ -1043,9 +1087,9 @@ __device__ __forceinline__ uint64_t g_first_row(const GroupArgs &a, uint32_t k, 
 // its span starts at the record's base (a direct member at row e0, an inner
 // group's member at its record's first inner element), and its first offsets
 // entry is written (an empty record leaves the next record's entry the same).
-__device__ __forceinline__ void g_run_init(const GroupArgs &a, uint32_t k, uint64_t r, uint64_t e0, GRun &run) {
-#pragma unroll
-    for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;
+template <class R>
+__device__ __forceinline__ void g_run_init(const GroupArgs &a, uint32_t k, uint64_t r, uint64_t e0, R &run) {
+    run.zero();
     const GField &f = a.f[k];
     for (uint32_t j = 1; j <= f.nmem; ++j) {
         j = g_uni(j);
@@ -1064,7 +1108,7 @@ __device__ __forceinline__ void g_run_init(const GroupArgs &a, uint32_t k, uint6
 // Element e of group g with no bytes on the wire (an absent T x[N]'s N
 // elements): fixed members zero, dynamic members and inner arrays empty.
 template <int L, int D>
-__device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, uint64_t e, GRun &run) {
+__device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, uint64_t e, GRunOf<D> &run) {
     g = g_uni(g);
     const GField &G = a.f[g];
     for (uint32_t j = 1; j <= G.nmem; ++j) {
@@ -1085,13 +1129,13 @@ __device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, ui
 
 template <int L, int D>
 __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in, uint64_t &pos,
-                           uint64_t end, GDisc &d, GRun &run);
+                           uint64_t end, GDisc &d, GRunOf<D> &run);
 // Inner group g (at depth L, a member of an element at depth L - 1) of outer
 // element e: its count word or list bools, read as the walk checked them,
 // then its elements.
 template <int L, int D>
 __device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in,
-                                            uint64_t &pos, uint64_t end, GDisc &d, GRun &run) {
+                                            uint64_t &pos, uint64_t end, GDisc &d, GRunOf<D> &run) {
     g = g_uni(g);
     const GField &G = a.f[g];
     const uint64_t i0 = G.kind == XDRG_K_FIXED ? e * G.count : run.get(G.slot);
@@ -1120,7 +1164,7 @@ __device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint
 // The members of element e of group g (after a list element's TRUE).
 template <int L, int D>
 __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in, uint64_t &pos,
-                           uint64_t end, GDisc &d, GRun &run) {
+                           uint64_t end, GDisc &d, GRunOf<D> &run) {
     g = g_uni(g);
     const GField &f = a.f[g];
     for (uint32_t j = 1; j <= f.nmem; ++j) {
@@ -1163,8 +1207,9 @@ __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint6
 
 // Element e's members parsed without storing (the element-parallel place's
 // record walk): pos past the element, run past its dynamic members.
+template <class R>
 __device__ __forceinline__ void g_elem_skip(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t &pos,
-                                            uint64_t end, GDisc &d, GRun &run) {
+                                            uint64_t end, GDisc &d, R &run) {
     g = g_uni(g);
     const GField &f = a.f[g];
     if (!f.ndm && !f.ncm) {   // elements of one size (a list's TRUE is already past)
@@ -1221,9 +1266,10 @@ __device__ __forceinline__ uint64_t g_dyn_words_z(uint32_t z, uint64_t cnt) {
 // EL (element-parallel place): the record's one group leaves descriptors in
 // *el instead of decoding its elements (the block decodes them afterwards,
 // a lane per element).
+// rl: the lane's GRunL column (D > 2).
 template <int D, bool EL = false>
 __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in, uint64_t base = 0,
-                                             const GElDesc &el = GElDesc{}) {
+                                             const GElDesc &el = GElDesc{}, uint64_t *rl = nullptr) {
     const GExtent ex = g_extent(a, r);   // the extent the walk checked (clamped to in_len)
     const uint64_t end = ex.b - base;
     uint64_t pos = ex.a + (a.framed ? 4 : 0) - base;
@@ -1238,7 +1284,8 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
                 continue;
             }
             if (f.kind == XDRG_K_FIXED) {   // an absent T x[N]: N zero / empty elements
-                GRun run;
+                GRunOf<D> run;
+                g_run_bind(run, rl);
                 g_run_init(a, k, r, r * f.count, run);
                 for (uint64_t e = r * f.count; e < (r + 1) * f.count; ++e) g_absent_elem<0, D>(a, k, e, run);
             }
@@ -1247,13 +1294,13 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
         }
         if (f.type == XDRG_T_GROUP) {
             uint64_t e0, cnt;
-            GRun run;
+            GRunOf<D> run;
+            g_run_bind(run, rl);
             if constexpr (EL) {   // the block's metadata, prefetched into LDS
                 const uint32_t j = (uint32_t)(r - el.rb);
                 e0 = el.mE[j];
                 cnt = el.mE[j + 1] - e0;
-#pragma unroll
-                for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;
+                run.zero();
                 if (el.nm > 0) { run.set(el.ms0, el.mb0[j]); a.f[el.mk0].offsets[e0] = el.mb0[j]; }
                 if (el.nm > 1) { run.set(el.ms1, el.mb1[j]); a.f[el.mk1].offsets[e0] = el.mb1[j]; }
             } else {
@@ -1321,11 +1368,13 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
 }
 
 template <int D>
-__global__ __launch_bounds__(kRecThreads) void k_grp_dec_place(const GroupArgs a) {
+__global__ __launch_bounds__(kRecThreads) void k_grp_dec_place(const GroupArgs a_) {
+    const GroupArgs &a = g_kargs<D>(a_);
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
     const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
     const uint64_t r = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x;
-    if (r < bad) g_dec_record<D>(a, r, a.xdr);
+    __shared__ uint64_t runs[g_run_lds(D) ? kRunLds : 1];
+    if (r < bad) g_dec_record<D>(a, r, a.xdr, 0, GElDesc{}, runs + threadIdx.x);
 }
 
 // nch 16-byte chunks from the 16-aligned global address a0 into the tile by
@@ -1350,8 +1399,10 @@ __device__ __forceinline__ void g_stage_tile(uint8_t *tile, uintptr_t a0, uint32
 // dependent length words and list bools become LDS reads instead of HBM
 // round trips.  A record larger than the tile decodes from HBM.
 template <int D>
-__global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupArgs a) {
+__global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupArgs a_) {
+    const GroupArgs &a = g_kargs<D>(a_);
     extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+    __shared__ uint64_t runs[g_run_lds(D) ? kRunLds : 1];
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
     const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
     const uint64_t rb = (uint64_t)blockIdx.x * kRecThreads;
@@ -1385,13 +1436,14 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
             const uintptr_t a1 = (xb + ext(rb + je) + 15) & ~(uintptr_t)15;
             g_stage_tile(tile, a0, k1 && a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u);
             __syncthreads();
-            if (js + tid < je) g_dec_record<D>(a, rb + js + tid, k1 ? tile : a.xdr, k1 ? a0 - xb : 0);
+            if (js + tid < je)
+                g_dec_record<D>(a, rb + js + tid, k1 ? tile : a.xdr, k1 ? a0 - xb : 0, GElDesc{}, runs + tid);
             __syncthreads();   // the tile's next use
             js = je;
             continue;
         }
         if (k1 == 0) {   // one record larger than the tile: its lane decodes from HBM
-            if (tid == 0) g_dec_record<D>(a, rb + js, a.xdr);
+            if (tid == 0) g_dec_record<D>(a, rb + js, a.xdr, 0, GElDesc{}, runs + tid);
             ++js;
             continue;
         }
@@ -1401,7 +1453,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_lds(const GroupAr
         g_stage_tile(tile, a0, a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u);
         __syncthreads();
         // stream offset x of these records is at tile + (x - (a0 - xb))
-        if (js + tid < je) g_dec_record<D>(a, rb + js + tid, tile, a0 - xb);
+        if (js + tid < je) g_dec_record<D>(a, rb + js + tid, tile, a0 - xb, GElDesc{}, runs + tid);
         __syncthreads();   // the tile's next use
         js = je;
     }
@@ -1431,6 +1483,7 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
     uint64_t *mb0 = mE + (kRecThreads + 1);      // [257] dynamic member 0's base
     uint64_t *mb1 = mb0 + (kRecThreads + 1);     // [257] dynamic member 1's base
     uint8_t *tile = smem + kElMeta;
+    __shared__ uint64_t runs[g_run_lds(1) ? kRunLds : 1];
     uint32_t *dpos = (uint32_t *)(tile + a.dec_tile);
     uint32_t *drel = dpos + a.dec_el;
     const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
@@ -1489,7 +1542,7 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
         }
         const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
         if (k1 == 0) {   // one record larger than the tile or the descriptors: its lane decodes from HBM
-            if (tid == 0) g_dec_record<1>(a, rb + js, a.xdr);
+            if (tid == 0) g_dec_record<1>(a, rb + js, a.xdr, 0, GElDesc{}, runs + tid);
             ++js;
             continue;
         }
@@ -1503,14 +1556,14 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
         el.sb1 = mb1[js];
         __syncthreads();
         // stream offset x at tile + (x - (a0 - xb))
-        if (js + tid < je) g_dec_record<1, true>(a, rb + js + tid, tile, a0 - xb, el);
+        if (js + tid < je) g_dec_record<1, true>(a, rb + js + tid, tile, a0 - xb, el, runs + tid);
         __syncthreads();   // descriptors
         const uint64_t nel = mE[je] - el.E0;
         XDRG_DCHECK(nel <= a.dec_el);   // (the fit count bounded the sub-batch's elements)
         for (uint32_t i = tid; i < nel; i += kRecThreads) {
-            GRun run;
-#pragma unroll
-            for (int q = 0; q < kMaxSlots; ++q) run.v[q] = 0;
+            GRunOf<1> run;
+            g_run_bind(run, runs + tid);
+            run.zero();
             // the record walk left every element a tile position inside the staged
             // bytes and member offsets inside the members' capacities
             XDRG_DCHECK(dpos[i] < 16u * nch);
