@@ -263,11 +263,11 @@ __device__ __forceinline__ uint64_t g_group_bytes(const GroupArgs &a, uint32_t g
 }
 
 // The kernels' GroupArgs (one by-value kernel argument, 4 KB).  The deepest
-// instances (D = kGrpLevels) read it in place in the kernarg segment: their
-// inlined four levels of element functions make the compiler give the
-// argument a private copy otherwise (4 KB of scratch per lane, a 4 KB copy
-// per lane at entry).  The others keep the plain argument (no change in their
-// code).
+// instances (D = kGrpLevels) and the element-parallel kernels (g_kargs<
+// kGrpLevels>) read it in place in the kernarg segment: their inlined code
+// makes the compiler give the argument a private copy otherwise (4 KB of
+// scratch per lane, a 4 KB copy per lane at entry).  The others keep the
+// plain argument (no change in their code).
 template <int D>
 __device__ __forceinline__ const GroupArgs &g_kargs(const GroupArgs &a) {
     if constexpr (D > 2) return *(const GroupArgs *)__builtin_amdgcn_kernarg_segment_ptr();
@@ -613,7 +613,8 @@ __device__ __forceinline__ uint32_t g_enc_top_img(const GroupArgs &a, uint64_t r
 // (`profiles/r04_groups/enc_el_split_ab.jsonl`), so they are not.
 __host__ __device__ inline uint32_t enc_el_split(uint64_t nblocks) { return nblocks >= 1024 ? 1u : nblocks >= 512 ? 2u : 4u; }
 template <bool COND, bool SHARE>   // COND: the schema has conditional fields; SHARE: split > 1
-__global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArgs a) {
+__global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArgs a_) {
+    const GroupArgs &a = g_kargs<kGrpLevels>(a_);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *soff = (uint64_t *)smem;                       // [RPB + 1] record offsets in the stream
     uint32_t *xs = (uint32_t *)(soff + kRecPerBlock + 1);    // [cap + 1] element offsets in the sub-batch's elements
@@ -787,9 +788,11 @@ __device__ __forceinline__ uint32_t g_walk_dyn(const GField &f, const uint8_t *i
 // a list reads xdrDecodeBoolean() before every element, any non-zero = another,
 // Xdr.java:404-407); cnt[s] += the counts of the counted columns it meets.
 // L = depth: an element at depth 0 may hold an inner group, walked the same way.
+// emap (the element-parallel place's group, GroupArgs::emap): a 1 at the
+// stream word of every element start.
 template <int L, int D>
 __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t end, uint64_t &pos,
-                                 uint32_t (&cnt)[kMaxSlots], GDisc &d) {
+                                 uint32_t (&cnt)[kMaxSlots], GDisc &d, uint8_t *emap = nullptr) {
     g = g_uni(g);
     const GField &f = a.f[g];
     uint64_t n;
@@ -804,6 +807,8 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
     }
     if (!f.ndm && !f.ncm && f.kind != XDRG_K_LIST) {   // elements of one size
         if ((end - pos) / f.efix < n) return XDRG_E_SHORT;
+        if (emap)
+            for (uint64_t i = 0; i < n; ++i) emap[(pos + i * f.efix) >> 2] = 1;
         pos += n * f.efix;
     } else if (g + 1 == a.lay_g) {   // one layout: the same checks, member descriptors not read
         // (a run of fixed members is SHORT iff one of them is, with the same sub)
@@ -818,6 +823,7 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
             } else if (i == n) {
                 break;
             }
+            if (emap) emap[pos >> 2] = 1;
             if (end - pos < pre) return XDRG_E_SHORT;
             pos += pre;
             if (nd > 0) {
@@ -850,6 +856,7 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
             } else if (i == n) {
                 break;
             }
+            if (emap) emap[pos >> 2] = 1;
             for (uint32_t j = 1; j <= f.nmem; ++j) {
                 j = g_uni(j);
                 const GField &m = a.f[g + j];
@@ -905,7 +912,7 @@ __device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint3
             continue;
         }
         if (f.type == XDRG_T_GROUP) {
-            const uint32_t err = g_walk_group<0, D>(a, k, in, e.b, pos, cnt, d);
+            const uint32_t err = g_walk_group<0, D>(a, k, in, e.b, pos, cnt, d, k == a.el_g ? a.emap : nullptr);
             if (err) return err;
             k += 1 + f.nmem;
             continue;
@@ -1256,6 +1263,41 @@ struct GElDesc {   // (scalar members: an indexed array here went to scratch)
 __device__ __forceinline__ uint64_t g_dyn_words_z(uint32_t z, uint64_t cnt) {
     return z == 1 ? (cnt + 3) >> 2 : cnt * (z >> 2);
 }
+// The lengths of one element's (at most two) dynamic members, by slot: the
+// run g_elem_skip advances when only the element's own lengths matter.
+struct GLen2 {
+    uint32_t s0, s1;
+    uint64_t l0, l1;
+    __device__ __forceinline__ uint64_t get(uint32_t slot) const { return slot == s0 ? l0 : slot == s1 ? l1 : 0; }
+    __device__ __forceinline__ void set(uint32_t slot, uint64_t x) {
+        if (slot == s0) l0 = x;
+        else if (slot == s1) l1 = x;
+    }
+};
+// Element at tile offset pos of the element-parallel group: pos past it and
+// its dynamic members' lengths (LAY: the layout's one length word each).
+template <bool LAY>
+__device__ __forceinline__ void g_el_parse(const GroupArgs &a, const GElDesc &el, uint32_t g, const uint8_t *in,
+                                           uint64_t &pos, uint64_t &l0, uint64_t &l1) {
+    l0 = l1 = 0;
+    if constexpr (LAY) {
+        pos += el.pre;
+        if (el.nm > 0) {
+            l0 = g_ld(in + pos);
+            pos += 4 + 4 * g_dyn_words_z(el.z0, l0) + el.mid;
+            if (el.nm > 1) {
+                l1 = g_ld(in + pos);
+                pos += 4 + 4 * g_dyn_words_z(el.z1, l1) + el.post;
+            }
+        }
+    } else {
+        GLen2 len{el.ms0 ? el.ms0 : ~0u, el.ms1 ? el.ms1 : ~0u, 0, 0};
+        GDisc d{};
+        g_elem_skip(a, g, in, pos, ~0ull, d, len);
+        l0 = len.l0;
+        l1 = len.l1;
+    }
+}
 
 // in: where stream offset x is read, in + (x - base) (the stream with base 0,
 // or an LDS tile holding this record's bytes whose first byte is stream offset
@@ -1267,7 +1309,10 @@ __device__ __forceinline__ uint64_t g_dyn_words_z(uint32_t z, uint64_t cnt) {
 // *el instead of decoding its elements (the block decodes them afterwards,
 // a lane per element).
 // rl: the lane's GRunL column (D > 2).
-template <int D, bool EL = false>
+// MAP (with EL): the elements' positions and member offsets are already in
+// *el (found from GroupArgs::emap); the record lane steps over its group
+// from its last element's position.
+template <int D, bool EL = false, bool MAP = false>
 __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, const uint8_t *in, uint64_t base = 0,
                                              const GElDesc &el = GElDesc{}, uint64_t *rl = nullptr) {
     const GExtent ex = g_extent(a, r);   // the extent the walk checked (clamped to in_len)
@@ -1309,6 +1354,17 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
                 g_run_init(a, k, r, e0, run);
             }
             if (f.kind == XDRG_K_DYNAMIC) pos += 4;
+            if constexpr (EL && MAP) {
+                if (cnt) {   // past the last element (its TRUE is before its position)
+                    pos = el.pos[e0 + cnt - 1 - el.E0];
+                    uint64_t l0, l1;
+                    if (el.lay) g_el_parse<true>(a, el, k, in, pos, l0, l1);
+                    else g_el_parse<false>(a, el, k, in, pos, l0, l1);
+                }
+                if (f.kind == XDRG_K_LIST) pos += 4;   // its FALSE
+                k += 1 + f.nmem;
+                continue;
+            }
             if constexpr (EL) {
                 if (el.lay) {   // elements of a fixed layout: one length word per dynamic member
                     const uint32_t lb = f.kind == XDRG_K_LIST ? 4u : 0u;
@@ -1475,8 +1531,15 @@ constexpr size_t kElMeta = 4 * (kRecThreads + 1) * 8;
 #ifndef XDRG_EL_OCC
 #define XDRG_EL_OCC 1   // blocks per CU the register budget is sized for (experiment builds: 2, 3)
 #endif
-template <bool LAY>   // LAY: the group is GroupArgs::lay_g (the record walk reads the layout)
-__global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(const GroupArgs a) {
+// MAP (GroupArgs::emap, tuning key 44): the walk left a 1 at the stream word
+// of every element start, so a sub-batch finds its elements' positions by a
+// block scan over the map, every lane parses a run of elements for their
+// dynamic members' lengths, a block scan places those, and a record lane only
+// steps over its group from its last element: no serial walk through the
+// elements.  A block with a record not 4-aligned takes the record walk.
+template <bool LAY, bool MAP>   // LAY: the group is GroupArgs::lay_g (the record walk reads the layout)
+__global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(const GroupArgs a_) {
+    const GroupArgs &a = g_kargs<kGrpLevels>(a_);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint64_t *mx = (uint64_t *)smem;             // [257] record extents (clamped to in_len)
     uint64_t *mE = mx + (kRecThreads + 1);       // [257] the group's first element of each record
@@ -1530,7 +1593,17 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
         if (el.nm > 0) mb0[j] = r < a.n ? g_rec_base(a, el.ms0, r) : a.totals[el.ms0 - 1];
         if (el.nm > 1) mb1[j] = r < a.n ? g_rec_base(a, el.ms1, r) : a.totals[el.ms1 - 1];
     }
-    __syncthreads();
+    bool use_map = false;
+    if constexpr (MAP) {   // element starts map to words exactly when records are 4-aligned
+        bool al = true;
+        for (uint32_t j = tid; j <= nlive; j += kRecThreads) {
+            const uint64_t x = a.rec_in[rb + j];
+            al = al && (x & 3) == 0;
+        }
+        use_map = __syncthreads_and(al);
+    } else {
+        __syncthreads();
+    }
     uint32_t js = 0;
     while (js < nlive) {
         const uint32_t je1 = js + 1 + tid;
@@ -1556,7 +1629,66 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
         el.sb1 = mb1[js];
         __syncthreads();
         // stream offset x at tile + (x - (a0 - xb))
-        if (js + tid < je) g_dec_record<1, true>(a, rb + js + tid, tile, a0 - xb, el, runs + tid);
+        const uint32_t nel_sb = (uint32_t)(mE[je] - el.E0);
+        bool mapped = false;
+        if (MAP && use_map) {
+            // positions: the flagged words of the sub-batch's records, in order
+            const uint64_t tb = a0 - xb;
+            const uint64_t wlo = mx[js] >> 2, whi = mx[je] >> 2;
+            uint32_t found = 0;
+            for (uint64_t cw = wlo & ~15ull; cw < whi; cw += 16 * kRecThreads) {   // (block-uniform)
+                const uint64_t w0 = cw + 16ull * tid;
+                typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
+                u32x4g v = {0u, 0u, 0u, 0u};
+                if (w0 < whi) v = *(const u32x4g *)(a.emap + w0);
+                uint32_t fl = 0;   // bit b: word w0 + b starts an element
+#pragma unroll
+                for (int b = 0; b < 16; ++b) {
+                    const uint64_t w = w0 + b;
+                    if (((v[b >> 2] >> (8 * (b & 3))) & 0xffu) && w >= wlo && w < whi) fl |= 1u << b;
+                }
+                uint64_t tot;
+                uint32_t idx = found + (uint32_t)block_excl_scan(__popc(fl), &tot);
+                for (uint32_t m = fl; m; m &= m - 1, ++idx)
+                    if (idx < nel_sb) dpos[idx] = (uint32_t)(4 * (w0 + __ffs(m) - 1) - tb);
+                found += (uint32_t)tot;
+            }
+            XDRG_DCHECK(found == nel_sb);
+            mapped = found == nel_sb;   // (block-uniform; else the record walk below)
+            __syncthreads();   // dpos
+        }
+        if (MAP && mapped) {
+            // the dynamic members' native offsets: each lane a run of elements
+            const uint64_t tb = a0 - xb;
+            const uint32_t nel = nel_sb;
+            const uint32_t per = (nel + kRecThreads - 1) / kRecThreads;
+            uint64_t sum = 0;
+            for (uint32_t u = 0; u < per; ++u) {
+                const uint32_t i = tid * per + u;
+                if (i >= nel) break;
+                uint64_t pos = dpos[i], l0, l1;
+                if constexpr (LAY) g_el_parse<true>(a, el, g, tile, pos, l0, l1);
+                else g_el_parse<false>(a, el, g, tile, pos, l0, l1);
+                drel[i] = (uint32_t)l0;
+                drel[el.cap + i] = (uint32_t)l1;
+                sum += l0 | l1 << 32;   // (a sub-batch's lengths fit 32 bits each)
+            }
+            uint64_t tot;
+            const uint64_t pre = block_excl_scan(sum, &tot);
+            uint32_t r0 = (uint32_t)pre, r1 = (uint32_t)(pre >> 32);
+            for (uint32_t u = 0; u < per; ++u) {
+                const uint32_t i = tid * per + u;
+                if (i >= nel) break;
+                const uint32_t l0 = drel[i], l1 = drel[el.cap + i];
+                drel[i] = r0;
+                drel[el.cap + i] = r1;
+                r0 += l0;
+                r1 += l1;
+            }
+            if (js + tid < je) g_dec_record<1, true, true>(a, rb + js + tid, tile, tb, el, runs + tid);
+        } else {
+            if (js + tid < je) g_dec_record<1, true>(a, rb + js + tid, tile, a0 - xb, el, runs + tid);
+        }
         __syncthreads();   // descriptors
         const uint64_t nel = mE[je] - el.E0;
         XDRG_DCHECK(nel <= a.dec_el);   // (the fit count bounded the sub-batch's elements)
@@ -1621,8 +1753,10 @@ static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_
     case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
         if (D == 1 && a.dec_el && a.dec_tile) {
             const size_t lds = kElMeta + a.dec_tile + 12 * (size_t)a.dec_el;
-            if (a.lay_g == a.el_g + 1) hipLaunchKernelGGL(k_grp_dec_place_el<true>, rgrid, block, lds, st, a);
-            else hipLaunchKernelGGL(k_grp_dec_place_el<false>, rgrid, block, lds, st, a);
+            if (a.lay_g == a.el_g + 1 && a.emap) hipLaunchKernelGGL((k_grp_dec_place_el<true, true>), rgrid, block, lds, st, a);
+            else if (a.lay_g == a.el_g + 1) hipLaunchKernelGGL((k_grp_dec_place_el<true, false>), rgrid, block, lds, st, a);
+            else if (a.emap) hipLaunchKernelGGL((k_grp_dec_place_el<false, true>), rgrid, block, lds, st, a);
+            else hipLaunchKernelGGL((k_grp_dec_place_el<false, false>), rgrid, block, lds, st, a);
         }
         else if (a.dec_tile) hipLaunchKernelGGL(k_grp_dec_place_lds<D>, rgrid, block, a.dec_tile, st, a);
         else hipLaunchKernelGGL(k_grp_dec_place<D>, rgrid, block, 0, st, a);

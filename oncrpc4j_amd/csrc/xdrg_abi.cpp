@@ -392,6 +392,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 41: if (v && (!in(4096, 49152) || (v & 15))) return -1; t.grp_enc_img = (int32_t)v; return 0;
     case 42: if (!in(0, 1)) return -1; t.recv_win = (int32_t)v; return 0;
     case 43: if (v != 0 && v != 1 && v != 2 && v != 4) return -1; t.grp_enc_split = (int32_t)v; return 0;
+    case 44: if (!in(0, 1)) return -1; t.grp_dec_emap = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -684,8 +685,9 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
 }
 
 // Kernel arguments and workspace of a schema with repeated groups.
+// map_bytes (decode): workspace for GroupArgs::emap, 16-byte aligned after the rest.
 static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool framed,
-                      bool decode, GroupArgs &a) {
+                      bool decode, GroupArgs &a, uint64_t map_bytes = 0) {
     memset(&a, 0, sizeof a);
     a.n = n;
     a.nf = (uint32_t)s->f.size();
@@ -769,8 +771,10 @@ static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols
     // and native offsets [nslot][n]
     const size_t sums = rows * a.nblocks + rows + 8;
     const size_t per_rec = decode ? (a.nslot * n + 1) / 2 + a.nslot * n : n;
-    int rc = ensure_ws(c, sums + per_rec + 1);
+    const size_t map_words = (map_bytes + 7) / 8 + 2;
+    int rc = ensure_ws(c, sums + per_rec + 1 + map_words);
     if (rc) return rc;
+    a.emap = map_bytes ? (uint8_t *)(((uintptr_t)(c->d_ws + sums + per_rec + 1) + 15) & ~(uintptr_t)15) : nullptr;
     a.block_sums = c->d_ws;
     a.totals = c->d_ws + rows * a.nblocks;
     if (decode) {
@@ -1057,8 +1061,12 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
     if (s->ngroups) {
         if (byref) return inval(c, "payload views in a schema with repeated groups");
         GroupArgs a;
-        rc = fill_group(c, s, cols, n, framed, true, a);
+        // the element-start map: a byte per stream word, read 16 at a time
+        const uint64_t map_bytes = c->tune.grp_dec_emap && c->tune.grp_dec_el && s->ngroups == 1 ? in_len / 4 + 32 : 0;
+        rc = fill_group(c, s, cols, n, framed, true, a, map_bytes);
         if (rc) return rc;
+        uint8_t *const emap = a.emap;
+        a.emap = nullptr;
         a.dec_tile = (uint32_t)c->tune.grp_dec_tile;
         // the element-parallel place: one top-level group without inner groups,
         // at most two dynamic members, LDS for the tile and the descriptors
@@ -1071,6 +1079,18 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
                     a.el_g = k;
                 }
         }
+        // elements found by their start words: each element has a word of its own
+        // (a list's TRUE before it, else at least 4 unconditional bytes).  Not for
+        // a group with a layout: its record walk reads one length word per
+        // dynamic member, cheaper than the map's stores and scan (DUMP decode
+        // 1.05 -> 1.60 ms, READDIR 2.22 -> 3.13 with it)
+        if (a.dec_el && emap && a.lay_g != a.el_g + 1) {
+            const GField &G = a.f[a.el_g];
+            uint64_t minb = 0;
+            for (uint32_t j = 1; j <= G.nmem; ++j)
+                if (!a.f[a.el_g + j].cond) minb += a.f[a.el_g + j].kind == XDRG_K_DYNAMIC ? 4 : a.f[a.el_g + j].xbytes;
+            if (G.kind == XDRG_K_LIST || minb >= 4) a.emap = emap;
+        }
         if (n == 0) {
             for (uint32_t q = 0; q < a.nslot; ++q)
                 if (!a.f[a.slot_field[q]].grp) HIPCHK(c, hipMemsetAsync(cols[a.slot_field[q]].offsets, 0, 8, c->stream));
@@ -1080,6 +1100,7 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         a.xdr_cap = in_len;
         a.rec_in = rec_offsets;
         HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
+        if (a.emap) HIPCHK(c, hipMemsetAsync(a.emap, 0, in_len / 4 + 32, c->stream));
         {
             TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE);
             HIPCHK(c, (hipError_t)launch_group_phase(a, GRP_DEC_WALK, c->stream));

@@ -209,6 +209,8 @@ struct Tuning {
                                     // staged walk, deframe and body decode (three; A/B only)
     int32_t grp_enc_split = 0;      // key 43: element-parallel group encode, blocks per scan block (1, 2,
                                     // 4; 0 = by batch size, enc_el_split)
+    int32_t grp_dec_emap = 1;       // key 44: element-parallel group decode finds its elements from the
+                                    // walk's element-start map (0: each record lane walks its elements)
     int32_t spec_sizes = 2;         // key 31: sweep decode whose last dynamic field is a word vector
                                     // followed by fixed fields only: 1 derive its counts from the record
                                     // extents (sizes reads one length word per record, the place kernel
@@ -393,6 +395,8 @@ struct GroupArgs {
     uint32_t levels;             // group levels of the schema (1 + the deepest nesting; the kernels' D)
     uint32_t dec_el;             // decode place: element-parallel, descriptors per sub-batch (0: off; key 38)
     uint32_t el_g;               // the element-parallel place's group (the schema's one top-level group)
+    uint8_t *emap;               // decode, element-parallel place (key 44): a byte per stream word, 1 where
+                                 // the walk met an element of group el_g (zeroed first; null: off)
     // 1 + the top-level group whose elements have one layout (no conditional
     // members, no inner groups, at most two dynamic members), 0: none.  The walk
     // and the element-parallel place then read one length word per dynamic

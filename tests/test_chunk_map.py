@@ -107,9 +107,9 @@ def _mutations(want, offs, n, rng):
     return out
 
 
-@pytest.fixture(params=[(8, 32768, 1024, 16384, 0), (8, 32768, 0, 0, 0), (64, 0, 0, 0, 0), (4, 1024, 0, 4096, 1),
-                        (8, 16384, 256, 32768, 2)],
-                ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}-img{p[3]}-split{p[4]}")
+@pytest.fixture(params=[(8, 32768, 1024, 16384, 0, 1), (8, 32768, 1024, 16384, 0, 0), (8, 32768, 0, 0, 0, 1),
+                        (64, 0, 0, 0, 0, 1), (4, 1024, 0, 4096, 1, 1), (8, 16384, 256, 32768, 2, 1)],
+                ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}-img{p[3]}-split{p[4]}-map{p[5]}")
 def enc_lanes(request, gpu_ctx):
     """Group kernels under each production choice (tuning keys 32 / 33, as
     tests/test_group_cond.py)."""
@@ -118,6 +118,7 @@ def enc_lanes(request, gpu_ctx):
     gpu_ctx.tune(38, request.param[2])   # element-parallel place (one top-level group)
     gpu_ctx.tune(41, request.param[3])   # element-parallel encode (key 41; 0: lanes per record)
     gpu_ctx.tune(43, request.param[4])   # element-parallel encode blocks per scan block (0: by batch size)
+    gpu_ctx.tune(44, request.param[5])   # element-parallel decode from the walk's element-start map (0: record walk)
     yield request.param
     gpu_ctx.tune(0)
 
