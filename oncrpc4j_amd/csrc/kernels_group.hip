@@ -790,9 +790,18 @@ __device__ __forceinline__ uint32_t g_walk_dyn(const GField &f, const uint8_t *i
 // L = depth: an element at depth 0 may hold an inner group, walked the same way.
 // emap (the element-parallel place's group, GroupArgs::emap): a 1 at the
 // stream word of every element start.
-template <int L, int D>
+// The walk's per-slot counts: registers (slot-indexed selects) or an LDS
+// column per lane (WCntL).  The LDS form frees 16 registers (walk<1> 125 ->
+// 82 VGPRs, walk<2> 158 -> 99, walk<4> 222 -> 129): READDIRPLUS decode 0.864
+// -> 0.833 ms, volume_index 2.25 -> 2.16; a schema with a layout group keeps
+// registers (READDIR 2.22 vs 2.31 ms; profiles/r05_groups/walk_cnt_ab.jsonl).
+struct WCntL {   // slot s of lane t at p[s * kRecThreads], p = base + t
+    uint32_t *p;
+    __device__ __forceinline__ uint32_t &operator[](uint32_t s) const { return p[s * kRecThreads]; }
+};
+template <int L, int D, class C>
 __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t end, uint64_t &pos,
-                                 uint32_t (&cnt)[kMaxSlots], GDisc &d, uint8_t *emap = nullptr) {
+                                 C &cnt, GDisc &d, uint8_t *emap = nullptr) {
     g = g_uni(g);
     const GField &f = a.f[g];
     uint64_t n;
@@ -864,7 +873,7 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
                 if (m.type == XDRG_T_GROUP) {   // an inner array / list of this element
                     if constexpr (L + 1 < D) {
                         if (present) {
-                            const uint32_t err = g_walk_group<L + 1, D>(a, g + j, in, end, pos, cnt, d);
+                            const uint32_t err = g_walk_group<L + 1, D, C>(a, g + j, in, end, pos, cnt, d);
                             if (err) return err;
                         }
                     }
@@ -890,8 +899,8 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
 }
 
 // Walk record r; cnt[s] = the record's count of counted column s.
-template <int D>
-__device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint32_t (&cnt)[kMaxSlots], uint32_t *sub) {
+template <int D, class C>
+__device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, C &cnt, uint32_t *sub) {
     const GExtent e = g_extent(a, r);
     const uint8_t *in = a.xdr;
     uint64_t pos = e.a;
@@ -912,7 +921,7 @@ __device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint3
             continue;
         }
         if (f.type == XDRG_T_GROUP) {
-            const uint32_t err = g_walk_group<0, D>(a, k, in, e.b, pos, cnt, d, k == a.el_g ? a.emap : nullptr);
+            const uint32_t err = g_walk_group<0, D, C>(a, k, in, e.b, pos, cnt, d, k == a.el_g ? a.emap : nullptr);
             if (err) return err;
             k += 1 + f.nmem;
             continue;
@@ -931,7 +940,7 @@ __device__ __forceinline__ uint32_t g_walk(const GroupArgs &a, uint64_t r, uint3
     return 0;
 }
 
-template <int D>
+template <int D, bool CL>   // CL: the counts in LDS (WCntL)
 __global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a_) {
     const GroupArgs &a = g_kargs<D>(a_);
     constexpr int per = kRecPerThread / kWalkSplit;
@@ -943,7 +952,9 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_walk(const GroupArgs a_
     for (int j = 0; j < per; ++j) {
         const uint64_t r = r0 + j;
         if (r >= a.n) break;
-        uint32_t cnt[kMaxSlots];
+        __shared__ uint32_t wcnt[CL ? kMaxSlots * kRecThreads : 1];
+        typename std::conditional<CL, WCntL, uint32_t[kMaxSlots]>::type cnt;
+        if constexpr (CL) cnt.p = wcnt + threadIdx.x;
         for (uint32_t s = 0; s < a.nslot; ++s) cnt[s] = 0;
         uint32_t sub;
         const uint32_t err = g_walk<D>(a, r, cnt, &sub);
@@ -1747,7 +1758,12 @@ static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_
             const hipError_t e = hipMemsetAsync(a.block_sums, 0, (size_t)a.nslot * a.nblocks * 8, st);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_grp_dec_walk<D>, dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
+        if constexpr (D == 1) {
+            if (a.lay_g) hipLaunchKernelGGL((k_grp_dec_walk<1, false>), dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
+            else hipLaunchKernelGGL((k_grp_dec_walk<1, true>), dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
+        } else {
+            hipLaunchKernelGGL((k_grp_dec_walk<D, true>), dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
+        }
         break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
     case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
