@@ -799,9 +799,49 @@ struct WCntL {   // slot s of lane t at p[s * kRecThreads], p = base + t
     uint32_t *p;
     __device__ __forceinline__ uint32_t &operator[](uint32_t s) const { return p[s * kRecThreads]; }
 };
+struct WCntNull {   // counts nobody reads (a walk for the position only)
+    uint32_t x;
+    __device__ __forceinline__ uint32_t &operator[](uint32_t) { return x; }
+};
 template <int L, int D, class C>
 __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t end, uint64_t &pos,
-                                 C &cnt, GDisc &d, uint8_t *emap = nullptr) {
+                                 C &cnt, GDisc &d, uint8_t *emap = nullptr);
+// The members of one element of group g (after a list element's TRUE), inner
+// groups included: pos past it, cnt[s] += its counts of counted column s.
+template <int L, int D, class C>
+__device__ __forceinline__ uint32_t g_walk_elem(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t end,
+                                                uint64_t &pos, C &cnt, GDisc &d) {
+    const GField &f = a.f[g];
+    for (uint32_t j = 1; j <= f.nmem; ++j) {
+        j = g_uni(j);
+        const GField &m = a.f[g + j];
+        const bool present = !f.ncm || g_dec_field_present(a, g + j, in, pos, end, d);
+        if (m.type == XDRG_T_GROUP) {   // an inner array / list of this element
+            if constexpr (L + 1 < D) {
+                if (present) {
+                    const uint32_t err = g_walk_group<L + 1, D, C>(a, g + j, in, end, pos, cnt, d);
+                    if (err) return err;
+                }
+            }
+            j += m.nmem;
+            continue;
+        }
+        if (!present) continue;
+        if (m.kind != XDRG_K_DYNAMIC) {
+            if (end - pos < m.xbytes) return XDRG_E_SHORT;
+            pos += m.xbytes;
+        } else {
+            uint32_t len = 0;
+            const uint32_t err = g_walk_dyn(m, in, end, pos, len);
+            if (err) return err;
+            cnt[m.slot - 1] += len;
+        }
+    }
+    return 0;
+}
+template <int L, int D, class C>
+__device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g, const uint8_t *in, uint64_t end, uint64_t &pos,
+                                 C &cnt, GDisc &d, uint8_t *emap) {
     g = g_uni(g);
     const GField &f = a.f[g];
     uint64_t n;
@@ -866,31 +906,8 @@ __device__ __forceinline__ uint32_t g_walk_group(const GroupArgs &a, uint32_t g,
                 break;
             }
             if (emap) emap[pos >> 2] = 1;
-            for (uint32_t j = 1; j <= f.nmem; ++j) {
-                j = g_uni(j);
-                const GField &m = a.f[g + j];
-                const bool present = !f.ncm || g_dec_field_present(a, g + j, in, pos, end, d);
-                if (m.type == XDRG_T_GROUP) {   // an inner array / list of this element
-                    if constexpr (L + 1 < D) {
-                        if (present) {
-                            const uint32_t err = g_walk_group<L + 1, D, C>(a, g + j, in, end, pos, cnt, d);
-                            if (err) return err;
-                        }
-                    }
-                    j += m.nmem;
-                    continue;
-                }
-                if (!present) continue;
-                if (m.kind != XDRG_K_DYNAMIC) {
-                    if (end - pos < m.xbytes) return XDRG_E_SHORT;
-                    pos += m.xbytes;
-                } else {
-                    uint32_t len = 0;
-                    const uint32_t err = g_walk_dyn(m, in, end, pos, len);
-                    if (err) return err;
-                    cnt[m.slot - 1] += len;
-                }
-            }
+            const uint32_t err = g_walk_elem<L, D, C>(a, g, in, end, pos, cnt, d);
+            if (err) return err;
         }
         n = i;
     }
@@ -1356,9 +1373,13 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
                 const uint32_t j = (uint32_t)(r - el.rb);
                 e0 = el.mE[j];
                 cnt = el.mE[j + 1] - e0;
-                run.zero();
-                if (el.nm > 0) { run.set(el.ms0, el.mb0[j]); a.f[el.mk0].offsets[e0] = el.mb0[j]; }
-                if (el.nm > 1) { run.set(el.ms1, el.mb1[j]); a.f[el.mk1].offsets[e0] = el.mb1[j]; }
+                if constexpr (D > 1) {   // (k_grp_dec_place_eln) every counted column of the span
+                    g_run_init(a, k, r, e0, run);
+                } else {
+                    run.zero();
+                    if (el.nm > 0) { run.set(el.ms0, el.mb0[j]); a.f[el.mk0].offsets[e0] = el.mb0[j]; }
+                    if (el.nm > 1) { run.set(el.ms1, el.mb1[j]); a.f[el.mk1].offsets[e0] = el.mb1[j]; }
+                }
             } else {
                 e0 = f.kind == XDRG_K_FIXED ? r * f.count : g_rec_base(a, f.slot, r);
                 cnt = f.kind == XDRG_K_FIXED ? f.count : a.rec_cnt[(uint64_t)(f.slot - 1) * a.n + r];
@@ -1368,9 +1389,15 @@ __device__ __forceinline__ void g_dec_record(const GroupArgs &a, uint64_t r, con
             if constexpr (EL && MAP) {
                 if (cnt) {   // past the last element (its TRUE is before its position)
                     pos = el.pos[e0 + cnt - 1 - el.E0];
-                    uint64_t l0, l1;
-                    if (el.lay) g_el_parse<true>(a, el, k, in, pos, l0, l1);
-                    else g_el_parse<false>(a, el, k, in, pos, l0, l1);
+                    if constexpr (D > 1) {   // inner groups included
+                        WCntNull nc;
+                        GDisc de{};
+                        (void)g_walk_elem<0, D>(a, k, in, ~0ull, pos, nc, de);
+                    } else {
+                        uint64_t l0, l1;
+                        if (el.lay) g_el_parse<true>(a, el, k, in, pos, l0, l1);
+                        else g_el_parse<false>(a, el, k, in, pos, l0, l1);
+                    }
                 }
                 if (f.kind == XDRG_K_LIST) pos += 4;   // its FALSE
                 k += 1 + f.nmem;
@@ -1723,6 +1750,167 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
     }
 }
 
+// Element-parallel place for a schema whose one top-level group holds inner
+// groups (D > 1; GroupArgs::emap set, tuning keys 38 / 44): a sub-batch of
+// records is staged as in k_grp_dec_place_el and its elements found from the
+// walk's element-start map; every lane walks a run of elements (inner groups
+// included) for their counts of every counted column of the group's span, a
+// block scan per column places them, a record lane writes its first rows'
+// offsets and steps over its group from its last element, and every lane
+// then decodes elements, inner groups included, from running offsets that
+// start at its element's scanned positions (GRunL columns).  A block with a
+// record not 4-aligned, or a sub-batch whose map count differs, decodes a
+// record per lane from the tile (k_grp_dec_place_lds).
+// LDS: eln_lds_bytes (xdrg_internal.h).
+template <int D>
+__global__ __launch_bounds__(kRecThreads) void k_grp_dec_place_eln(const GroupArgs a_) {
+    const GroupArgs &a = g_kargs<kGrpLevels>(a_);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint64_t sbase[kMaxSlots];   // each column's native offset at the sub-batch's first record
+    uint64_t *mx = (uint64_t *)smem;             // [257] record extents (clamped to in_len)
+    uint64_t *mE = mx + (kRecThreads + 1);       // [257] the group's first element of each record
+    uint8_t *tile = smem + kElnMeta;
+    const uint32_t cap = a.dec_el;
+    uint32_t *dpos = (uint32_t *)(tile + a.dec_tile);
+    uint32_t *drel = dpos + cap;
+    const uint32_t g = a.el_g;
+    const GField &G = a.f[g];
+    uint32_t ns = 0;   // counted columns of the group's span
+    for (uint32_t j = 1; j <= G.nmem; ++j) ns += a.f[g_uni(g + j)].slot ? 1u : 0u;
+    uint64_t *runs = (uint64_t *)(dpos + (((size_t)cap * (1 + ns) + 1) & ~(size_t)1));   // (8-aligned)
+    uint64_t *const rl = runs + threadIdx.x;
+    const unsigned long long key = *a.errkey;   // final: walk and capacity kernels ran before
+    const uint64_t bad = key == kNoError ? a.n : (uint64_t)(key >> 16);
+    const uint64_t rb = (uint64_t)blockIdx.x * kRecThreads;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t lim = bad < a.n ? bad : a.n;
+    const uint32_t nlive = lim > rb ? (uint32_t)(lim - rb < (uint64_t)kRecThreads ? lim - rb : (uint64_t)kRecThreads) : 0u;
+    const uintptr_t xb = (uintptr_t)a.xdr;
+    GElDesc el{};
+    el.pos = dpos;
+    el.cap = cap;
+    el.tile = tile;
+    el.rb = rb;
+    el.mE = mE;
+    bool al = true;
+    for (uint32_t j = tid; j <= nlive; j += kRecThreads) {
+        const uint64_t r = rb + j;
+        const uint64_t x = a.rec_in[r];
+        al = al && (x & 3) == 0;
+        mx[j] = x < a.xdr_cap ? x : a.xdr_cap;
+        mE[j] = G.kind == XDRG_K_FIXED ? r * G.count : (r < a.n ? g_rec_base(a, G.slot, r) : a.totals[G.slot - 1]);
+    }
+    const bool use_map = __syncthreads_and(al);
+    uint32_t js = 0;
+    while (js < nlive) {
+        const uint32_t je1 = js + 1 + tid;
+        bool fits = false;
+        if (je1 <= nlive) {
+            const uintptr_t lo = (xb + mx[js]) & ~(uintptr_t)15;
+            const uintptr_t hi = (xb + mx[je1] + 15) & ~(uintptr_t)15;
+            fits = hi >= lo && hi - lo <= a.dec_tile && mE[je1] - mE[js] <= cap;
+        }
+        const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
+        if (k1 == 0) {   // one record larger than the tile or the positions: its lane decodes from HBM
+            if (tid == 0) g_dec_record<D>(a, rb + js, a.xdr, 0, GElDesc{}, rl);
+            ++js;
+            continue;
+        }
+        const uint32_t je = js + k1;
+        const uintptr_t a0 = (xb + mx[js]) & ~(uintptr_t)15;
+        const uintptr_t a1 = (xb + mx[je] + 15) & ~(uintptr_t)15;
+        const uint64_t tb = a0 - xb;
+        g_stage_tile(tile, a0, a1 > a0 ? (uint32_t)((a1 - a0) >> 4) : 0u);
+        el.E0 = mE[js];
+        if (tid < a.nslot) {
+            const uint64_t r = rb + js;
+            sbase[tid] = r < a.n ? g_rec_base(a, tid + 1, r) : a.totals[tid];
+        }
+        __syncthreads();
+        const uint32_t nel = (uint32_t)(mE[je] - el.E0);
+        bool mapped = false;
+        if (use_map) {   // positions: the flagged words of the sub-batch's records, in order
+            const uint64_t wlo = mx[js] >> 2, whi = mx[je] >> 2;
+            uint32_t found = 0;
+            for (uint64_t cw = wlo & ~15ull; cw < whi; cw += 16 * kRecThreads) {   // (block-uniform)
+                const uint64_t w0 = cw + 16ull * tid;
+                typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
+                u32x4g v = {0u, 0u, 0u, 0u};
+                if (w0 < whi) v = *(const u32x4g *)(a.emap + w0);
+                uint32_t fl = 0;   // bit b: word w0 + b starts an element
+#pragma unroll
+                for (int b = 0; b < 16; ++b) {
+                    const uint64_t w = w0 + b;
+                    if (((v[b >> 2] >> (8 * (b & 3))) & 0xffu) && w >= wlo && w < whi) fl |= 1u << b;
+                }
+                uint64_t tot;
+                uint32_t idx = found + (uint32_t)block_excl_scan(__popc(fl), &tot);
+                for (uint32_t m = fl; m; m &= m - 1, ++idx)
+                    if (idx < nel) dpos[idx] = (uint32_t)(4 * (w0 + __ffs(m) - 1) - tb);
+                found += (uint32_t)tot;
+            }
+            XDRG_DCHECK(found == nel);
+            mapped = found == nel;   // (block-uniform)
+            __syncthreads();   // dpos
+        }
+        if (!mapped) {   // a record per lane from the tile
+            if (js + tid < je) g_dec_record<D>(a, rb + js + tid, tile, tb, GElDesc{}, rl);
+            __syncthreads();   // the tile's next use
+            js = je;
+            continue;
+        }
+        // each lane's run of elements: their counts of every span column
+        const uint32_t per = (nel + kRecThreads - 1) / kRecThreads;
+        WCntL cnt{(uint32_t *)runs + tid};   // (the lane's GRunL column as counters until the decode)
+        for (uint32_t u = 0; u < per; ++u) {
+            const uint32_t i = tid * per + u;
+            if (i >= nel) break;
+            for (uint32_t s = 0; s < a.nslot; ++s) cnt[s] = 0;
+            uint64_t pos = dpos[i];
+            GDisc d{};
+            (void)g_walk_elem<0, D>(a, g, tile, ~0ull, pos, cnt, d);
+            uint32_t q = 0;
+            for (uint32_t j = 1; j <= G.nmem; ++j) {
+                const uint32_t sl = a.f[g_uni(g + j)].slot;
+                if (sl) drel[(size_t)q++ * cap + i] = cnt[sl - 1];
+            }
+        }
+        // a block scan per column: counts -> positions relative to sbase
+        for (uint32_t q = 0; q < ns; ++q) {
+            uint32_t *c = drel + (size_t)q * cap;
+            uint64_t sum = 0;
+            for (uint32_t u = 0; u < per; ++u) {
+                const uint32_t i = tid * per + u;
+                if (i < nel) sum += c[i];
+            }
+            uint64_t tot;
+            uint32_t p = (uint32_t)block_excl_scan(sum, &tot);
+            for (uint32_t u = 0; u < per; ++u) {
+                const uint32_t i = tid * per + u;
+                if (i >= nel) break;
+                const uint32_t x = c[i];
+                c[i] = p;
+                p += x;
+            }
+        }
+        if (js + tid < je) g_dec_record<D, true, true>(a, rb + js + tid, tile, tb, el, rl);
+        __syncthreads();   // positions, scanned counts
+        for (uint32_t i = tid; i < nel; i += kRecThreads) {
+            GRunL run{rl};
+            uint32_t q = 0;
+            for (uint32_t j = 1; j <= G.nmem; ++j) {
+                const uint32_t sl = a.f[g_uni(g + j)].slot;
+                if (sl) run.set(sl, sbase[sl - 1] + drel[(size_t)q++ * cap + i]);
+            }
+            GDisc d{};
+            uint64_t pos = dpos[i];
+            g_dec_elem<0, D>(a, g, el.E0 + i, tile, pos, ~0ull, d, run);
+        }
+        __syncthreads();   // the tile's and the positions' next use
+        js = je;
+    }
+}
+
 // Kernels are instantiated per group levels D: 1 (no group inside an element:
 // the inner-group code compiled out, running offsets in registers), 2 (one
 // level of groups inside elements, the common nested shapes) and kGrpLevels
@@ -1767,7 +1955,12 @@ static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_
         break;
     case GRP_DEC_OFFSETS: if (a.nslot) hipLaunchKernelGGL(k_grp_dec_offsets, grid, block, 0, st, a); break;
     case GRP_DEC_PLACE:   // a lane per record, from an LDS tile (tuning key 33 > 0) or from HBM
-        if (D == 1 && a.dec_el && a.dec_tile) {
+        if (D > 1 && a.emap && a.dec_el && a.dec_tile) {   // element-parallel, inner groups
+            uint32_t ns = 0;
+            for (uint32_t j = 1; j <= a.f[a.el_g].nmem; ++j) ns += a.f[a.el_g + j].slot ? 1u : 0u;
+            if constexpr (D > 1)
+                hipLaunchKernelGGL(k_grp_dec_place_eln<D>, rgrid, block, eln_lds_bytes(a.dec_tile, a.dec_el, ns, a.nslot), st, a);
+        } else if (D == 1 && a.dec_el && a.dec_tile) {
             const size_t lds = kElMeta + a.dec_tile + 12 * (size_t)a.dec_el;
             if (a.lay_g == a.el_g + 1 && a.emap) hipLaunchKernelGGL((k_grp_dec_place_el<true, true>), rgrid, block, lds, st, a);
             else if (a.lay_g == a.el_g + 1) hipLaunchKernelGGL((k_grp_dec_place_el<true, false>), rgrid, block, lds, st, a);

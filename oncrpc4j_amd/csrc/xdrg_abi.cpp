@@ -1045,6 +1045,14 @@ static int finish_decode(xdrg_ctx *c, uint64_t n, unsigned long long host_key, b
     return code;
 }
 
+// k_grp_dec_place_eln's sub-batch: at most this tile (key 33) and these
+// elements (key 38); volume_index decode 1.39 ms at 16 KiB / 512, 1.16 at
+// 16 KiB / 256, 1.71 at 8 KiB / 256 (profiles/r05_groups/eln_tune.txt)
+#ifndef XDRG_ELN_TILE
+#define XDRG_ELN_TILE 16384
+#endif
+constexpr uint32_t kElnTile = XDRG_ELN_TILE, kElnCap = 256;
+
 static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t in_len,
                        const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
                        uint64_t *first_bad, int *err, uint32_t byref, uint64_t *ref_pos) {
@@ -1084,13 +1092,39 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         // a group with a layout: its record walk reads one length word per
         // dynamic member, cheaper than the map's stores and scan (DUMP decode
         // 1.05 -> 1.60 ms, READDIR 2.22 -> 3.13 with it)
-        if (a.dec_el && emap && a.lay_g != a.el_g + 1) {
-            const GField &G = a.f[a.el_g];
+        auto own_word = [&](uint32_t g) {
+            const GField &G = a.f[g];
             uint64_t minb = 0;
-            for (uint32_t j = 1; j <= G.nmem; ++j)
-                if (!a.f[a.el_g + j].cond) minb += a.f[a.el_g + j].kind == XDRG_K_DYNAMIC ? 4 : a.f[a.el_g + j].xbytes;
-            if (G.kind == XDRG_K_LIST || minb >= 4) a.emap = emap;
-        }
+            for (uint32_t j = 1; j <= G.nmem; ++j) {
+                const GField &m = a.f[g + j];
+                if (!m.cond) minb += m.type == XDRG_T_GROUP ? (m.kind == XDRG_K_FIXED ? 0 : 4)
+                                                            : m.kind == XDRG_K_DYNAMIC ? 4 : m.xbytes;
+                if (m.type == XDRG_T_GROUP) j += m.nmem;
+            }
+            return G.kind == XDRG_K_LIST || minb >= 4;
+        };
+        if (a.dec_el && emap && a.lay_g != a.el_g + 1 && own_word(a.el_g)) a.emap = emap;
+        // the element-parallel place of a group holding inner groups
+        // (k_grp_dec_place_eln): a smaller tile and fewer elements per sub-batch,
+        // its LDS also holding every span column's positions and running offsets
+        if (!a.dec_el && emap && a.nest && c->tune.grp_dec_el && a.dec_tile)
+            for (uint32_t k = 0; k < a.nf; ++k) {
+                const GField &G = a.f[k];
+                if (G.type != XDRG_T_GROUP || G.grp || (G.kind == XDRG_K_FIXED && G.cond) || !own_word(k)) continue;
+                uint32_t ns = 0;
+                for (uint32_t j = 1; j <= G.nmem; ++j) ns += a.f[k + j].slot ? 1u : 0u;
+                uint32_t tile = a.dec_tile < kElnTile ? a.dec_tile : kElnTile;
+                uint32_t cap = (uint32_t)c->tune.grp_dec_el < kElnCap ? (uint32_t)c->tune.grp_dec_el : kElnCap;
+                while (eln_lds_bytes(tile, cap, ns, a.nslot) > 65536 && tile > 4096) {
+                    tile /= 2;
+                    cap = cap > 128 ? cap / 2 : cap;
+                }
+                if (eln_lds_bytes(tile, cap, ns, a.nslot) > 65536) break;
+                a.dec_tile = tile;
+                a.dec_el = cap;
+                a.el_g = k;
+                a.emap = emap;
+            }
         if (n == 0) {
             for (uint32_t q = 0; q < a.nslot; ++q)
                 if (!a.f[a.slot_field[q]].grp) HIPCHK(c, hipMemsetAsync(cols[a.slot_field[q]].offsets, 0, 8, c->stream));

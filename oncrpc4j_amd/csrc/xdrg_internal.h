@@ -424,5 +424,13 @@ constexpr int kRecThreads = 256;   // record path: threads per block
 constexpr int kRecPerThread = 4;   // records per thread in the size/scan pass
 constexpr int kRecPerBlock = kRecThreads * kRecPerThread;
 constexpr int kMaxDynLds = 4;      // dynamic fields whose per-record metadata is staged in LDS
+// LDS of k_grp_dec_place_eln (element-parallel place of a nested group):
+// extents and first elements (2 x 257 u64) | tile | positions [cap] | scanned
+// counts [ns span columns][cap] | GRunL columns [nslot][256 lanes].
+constexpr size_t kElnMeta = 2 * (kRecThreads + 1) * 8 + 16;
+inline size_t eln_lds_bytes(uint32_t tile, uint32_t cap, uint32_t ns, uint32_t nslot) {
+    return kElnMeta + tile + 4 * (size_t)cap * (1 + ns) + 8 + 8 * (size_t)kRecThreads * (nslot ? nslot : 1);
+}
+
 
 }  // namespace xdrg
