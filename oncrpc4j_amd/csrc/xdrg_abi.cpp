@@ -1046,10 +1046,11 @@ static int finish_decode(xdrg_ctx *c, uint64_t n, unsigned long long host_key, b
 }
 
 // k_grp_dec_place_eln's sub-batch: at most this tile (key 33) and these
-// elements (key 38); volume_index decode 1.39 ms at 16 KiB / 512, 1.16 at
-// 16 KiB / 256, 1.71 at 8 KiB / 256 (profiles/r05_groups/eln_tune.txt)
+// elements (key 38).  volume_index / acl_tree decode ms: 16 KiB / 512
+// elements 1.39 / 3.59, 16 KiB / 256 1.15 / 3.59, 8 KiB / 256 1.71 / 5.87,
+// 32 KiB / 256 1.11 / 2.36 (profiles/r05_groups/eln_tune*.txt)
 #ifndef XDRG_ELN_TILE
-#define XDRG_ELN_TILE 16384
+#define XDRG_ELN_TILE 32768
 #endif
 constexpr uint32_t kElnTile = XDRG_ELN_TILE, kElnCap = 256;
 
