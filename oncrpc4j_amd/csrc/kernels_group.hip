@@ -334,12 +334,14 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_sizes(const GroupArgs a
     }
 }
 
-// One lane writes element e of group g at stream byte p; returns its end.
+// One lane writes element e of group g at byte p of out (the stream, or an
+// LDS image of a sub-batch's stream bytes); returns its end.
 template <int L, int D>
-__device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, uint64_t row, uint64_t p, GDisc &d);
+__device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint8_t *out, uint32_t g, uint64_t row, uint64_t p,
+                                                GDisc &d);
 template <int L, int D>
-__device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint32_t g, uint64_t e, uint64_t p, GDisc d) {
-    uint8_t *out = a.xdr;
+__device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint8_t *out, uint32_t g, uint64_t e, uint64_t p,
+                                               GDisc d) {
     g = g_uni(g);
     const GField &G = a.f[g];
     if (G.kind == XDRG_K_LIST) {   // xdrEncodeBoolean(true) (pmaplist.java:65-67)
@@ -352,7 +354,7 @@ __device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint32_t g, u
         const bool present = !G.ncm || g_enc_field_present(a, g + j, e, d);   // an element's absent arm
         if (m.type == XDRG_T_GROUP) {   // an inner array / list: this lane writes it whole
             if constexpr (L + 1 < D) {
-                if (present) p = g_enc_group<L + 1, D>(a, g + j, e, p, d);
+                if (present) p = g_enc_group<L + 1, D>(a, out, g + j, e, p, d);
             }
             j += m.nmem;
             continue;
@@ -373,8 +375,8 @@ __device__ __forceinline__ uint64_t g_enc_elem(const GroupArgs &a, uint32_t g, u
 }
 // Group g at row `row` of its column, by one lane from stream byte p.
 template <int L, int D>
-__device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, uint64_t row, uint64_t p, GDisc &d) {
-    uint8_t *out = a.xdr;
+__device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint8_t *out, uint32_t g, uint64_t row, uint64_t p,
+                                                GDisc &d) {
     g = g_uni(g);
     const GField &G = a.f[g];
     uint64_t e0, cnt;
@@ -383,7 +385,7 @@ __device__ __forceinline__ uint64_t g_enc_group(const GroupArgs &a, uint32_t g, 
         *(uint32_t *)(out + p) = bswap32r((uint32_t)cnt);
         p += 4;
     }
-    for (uint64_t e = e0; e < e0 + cnt; ++e) p = g_enc_elem<L, D>(a, g, e, p, d);
+    for (uint64_t e = e0; e < e0 + cnt; ++e) p = g_enc_elem<L, D>(a, out, g, e, p, d);
     if (G.kind == XDRG_K_LIST) {      // xdrEncodeBoolean(false)
         *(uint32_t *)(out + p) = 0;
         p += 4;
@@ -430,7 +432,7 @@ __device__ __forceinline__ void g_enc_record(const GroupArgs &a, uint64_t r, uin
                 pos += 4;
             }
             if (!f.ndm && !f.ncm) {   // elements of one size: a lane per element
-                for (uint64_t i = ln; i < cnt; i += G) g_enc_elem<0, D>(a, k, e0 + i, pos + i * f.efix, d);
+                for (uint64_t i = ln; i < cnt; i += G) g_enc_elem<0, D>(a, out, k, e0 + i, pos + i * f.efix, d);
                 pos += cnt * f.efix;
             } else {        // a lane per element at its scanned position
                 // (the group's lanes stay together: the scan's shuffles need all G)
@@ -438,7 +440,7 @@ __device__ __forceinline__ void g_enc_record(const GroupArgs &a, uint64_t r, uin
                     const uint64_t i = b + ln;
                     const uint64_t z = i < cnt ? g_elem_bytes<0, D>(a, k, e0 + i, d) : 0;
                     const uint64_t incl = g_incl_scan<G>(z, ln);
-                    if (i < cnt) g_enc_elem<0, D>(a, k, e0 + i, pos + incl - z, d);
+                    if (i < cnt) g_enc_elem<0, D>(a, out, k, e0 + i, pos + incl - z, d);
                     pos += __shfl(incl, G - 1, G);
                 }
             }
@@ -612,7 +614,9 @@ __device__ __forceinline__ uint32_t g_enc_top_img(const GroupArgs &a, uint64_t r
 // 1.68 to 1.11 ms; batches of 1,024 scan blocks and more lose 1-3 % when split
 // (`profiles/r04_groups/enc_el_split_ab.jsonl`), so they are not.
 __host__ __device__ inline uint32_t enc_el_split(uint64_t nblocks) { return nblocks >= 1024 ? 1u : nblocks >= 512 ? 2u : 4u; }
-template <bool COND, bool SHARE>   // COND: the schema has conditional fields; SHARE: split > 1
+// D > 1: the group's elements hold inner groups (their sizes and words by the
+// recursive element functions, into the image as into the stream).
+template <bool COND, bool SHARE, int D>   // COND: the schema has conditional fields; SHARE: split > 1
 __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArgs a_) {
     const GroupArgs &a = g_kargs<kGrpLevels>(a_);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -666,7 +670,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArg
             fits = soff[je1] - soff[js] <= a.enc_img && gfirst(je1) - gfirst(js) <= kEncElCap;
         const uint32_t k1 = (uint32_t)__syncthreads_count(fits);
         if (k1 == 0) {   // one record larger than the image: wave 0 writes it to the stream
-            if (tid < 64) g_enc_record<64, false>(a, rb + js, soff[js], soff[js + 1] - soff[js], tid);
+            if (tid < 64) g_enc_record<64, D>(a, rb + js, soff[js], soff[js + 1] - soff[js], tid);
             ++js;
             continue;
         }
@@ -700,7 +704,7 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArg
             const uint32_t i = 4 * tid + u;
             z[u] = 0;
             if (i < nel && own[i] != kNoOwner)
-                z[u] = lay ? g_lay_elem_bytes(a, G, E0 + i) : (uint32_t)g_elem_bytes<0, 1>(a, g, E0 + i, GDisc{});
+                z[u] = lay ? g_lay_elem_bytes(a, G, E0 + i) : (uint32_t)g_elem_bytes<0, D>(a, g, E0 + i, GDisc{});
             zs += z[u];
         }
         uint64_t ztot;
@@ -723,7 +727,9 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_enc_place_el(const GroupArg
         __syncthreads();
         for (uint32_t i = tid; i < nel; i += kRecThreads) {
             const uint32_t t = own[i];
-            if (t != kNoOwner) g_enc_elem_img<COND>(a, g, E0 + i, img, rst[t] + xs[i] - xs[fj[t]]);
+            if (t == kNoOwner) continue;
+            if constexpr (D == 1) g_enc_elem_img<COND>(a, g, E0 + i, img, rst[t] + xs[i] - xs[fj[t]]);
+            else (void)g_enc_elem<0, D>(a, img, g, E0 + i, rst[t] + xs[i] - xs[fj[t]], GDisc{});
         }
         __syncthreads();
         // the image out: dwords up to a 16-byte boundary, 16-byte stores, dwords
@@ -1931,10 +1937,19 @@ static hipError_t launch_group_phase_t(const GroupArgs &a, int phase, hipStream_
         hipLaunchKernelGGL(k_grp_enc_sizes<D>, dim3((uint32_t)a.nblocks * kWalkSplit), block, 0, st, a);
         break;
     case GRP_ENC_PLACE:   // element-parallel (key 41) or G lanes per record (key 32)
-        if (D == 1 && a.enc_img && a.ncond && esh) hipLaunchKernelGGL((k_grp_enc_place_el<true, true>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
-        else if (D == 1 && a.enc_img && a.ncond) hipLaunchKernelGGL((k_grp_enc_place_el<true, false>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
-        else if (D == 1 && a.enc_img && esh) hipLaunchKernelGGL((k_grp_enc_place_el<false, true>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
-        else if (D == 1 && a.enc_img) hipLaunchKernelGGL((k_grp_enc_place_el<false, false>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        if constexpr (D > 2) {   // deep schemas' records are large: a 32 KiB image at least (acl_tree
+                                 // encode 3.49 ms at 16 KiB, 2.15 at 32; volume_index keeps 16 KiB:
+                                 // 1.04 vs 1.28 ms, profiles/r05_groups/enc_nest_ab.txt)
+            if (a.enc_img && a.enc_img < 32768) {
+                GroupArgs b = a;
+                b.enc_img = 32768;
+                return launch_group_phase_t<D>(b, phase, st);
+            }
+        }
+        if (a.enc_img && a.ncond && esh) hipLaunchKernelGGL((k_grp_enc_place_el<true, true, D>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (a.enc_img && a.ncond) hipLaunchKernelGGL((k_grp_enc_place_el<true, false, D>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (a.enc_img && esh) hipLaunchKernelGGL((k_grp_enc_place_el<false, true, D>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
+        else if (a.enc_img) hipLaunchKernelGGL((k_grp_enc_place_el<false, false, D>), egrid, block, enc_el_lds_bytes(a.enc_img), st, a);
         else if (a.enc_lanes == 4) hipLaunchKernelGGL((k_grp_enc_place<4, D>), grid, block, 0, st, a);
         else if (a.enc_lanes == 8) hipLaunchKernelGGL((k_grp_enc_place<8, D>), grid, block, 0, st, a);
         else if (a.enc_lanes == 16) hipLaunchKernelGGL((k_grp_enc_place<16, D>), grid, block, 0, st, a);

@@ -393,6 +393,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 42: if (!in(0, 1)) return -1; t.recv_win = (int32_t)v; return 0;
     case 43: if (v != 0 && v != 1 && v != 2 && v != 4) return -1; t.grp_enc_split = (int32_t)v; return 0;
     case 44: if (!in(0, 1)) return -1; t.grp_dec_emap = (int32_t)v; return 0;
+    case 45: if (!in(0, 1)) return -1; t.grp_enc_img_nest = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -801,10 +802,10 @@ static int group_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *co
     if (rc) return rc;
     a.enc_lanes = (uint32_t)c->tune.grp_enc_lanes;
     a.enc_split = (uint32_t)c->tune.grp_enc_split;
-    // the element-parallel place: one top-level group without inner groups
-    if (c->tune.grp_enc_img && s->ngroups == 1 && !a.nest)
+    // the element-parallel place: one top-level group (inner groups included)
+    if (c->tune.grp_enc_img && s->ngroups == 1 && (!a.nest || c->tune.grp_enc_img_nest))
         for (uint32_t k = 0; k < a.nf; ++k)
-            if (a.f[k].type == XDRG_T_GROUP && !a.f[k].grp && !a.f[k].ngm) {
+            if (a.f[k].type == XDRG_T_GROUP && !a.f[k].grp) {
                 a.enc_img = (uint32_t)c->tune.grp_enc_img;
                 a.el_g = k;
             }

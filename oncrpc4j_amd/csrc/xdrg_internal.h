@@ -211,6 +211,8 @@ struct Tuning {
                                     // 4; 0 = by batch size, enc_el_split)
     int32_t grp_dec_emap = 1;       // key 44: element-parallel group decode finds its elements from the
                                     // walk's element-start map (0: each record lane walks its elements)
+    int32_t grp_enc_img_nest = 1;   // key 45: the element-parallel encode (key 41) for a group holding inner
+                                    // groups too (0: lanes per record, key 32)
     int32_t spec_sizes = 2;         // key 31: sweep decode whose last dynamic field is a word vector
                                     // followed by fixed fields only: 1 derive its counts from the record
                                     // extents (sizes reads one length word per record, the place kernel

@@ -192,11 +192,13 @@ def test_oracle_random_roundtrip():
 
 
 # ---- GPU ---------------------------------------------------------------------
-@pytest.fixture(params=[(8, 32768), (8, 0), (64, 0), (4, 1024)], ids=lambda p: f"enc{p[0]}-dtile{p[1]}")
+@pytest.fixture(params=[(8, 32768, 16384), (8, 0, 0), (64, 0, 4096), (4, 1024, 0)],
+                ids=lambda p: f"enc{p[0]}-dtile{p[1]}-img{p[2]}")
 def grp_tune(request, gpu_ctx):
-    """Group kernels under each production choice (tuning keys 32 / 33)."""
+    """Group kernels under each production choice (tuning keys 32 / 33 / 41)."""
     gpu_ctx.tune(32, request.param[0])
     gpu_ctx.tune(33, request.param[1])
+    gpu_ctx.tune(41, request.param[2])   # element-parallel encode image (0: lanes per record)
     yield request.param
     gpu_ctx.tune(0)
 

@@ -179,13 +179,15 @@ def test_oracle_random_roundtrip():
     assert out.equal(hb)
 
 
-@pytest.fixture(params=[(8, 32768, 1024), (8, 32768, 0), (64, 0, 0), (4, 1024, 0), (8, 16384, 256)],
-                ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}")
+@pytest.fixture(params=[(8, 32768, 1024, 16384), (8, 32768, 0, 0), (64, 0, 0, 4096), (4, 1024, 0, 0),
+                        (8, 16384, 256, 32768)],
+                ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}-img{p[3]}")
 def grp_tune(request, gpu_ctx):
     """Group kernels under each production choice (tuning keys 32 / 33)."""
     gpu_ctx.tune(32, request.param[0])
     gpu_ctx.tune(33, request.param[1])
     gpu_ctx.tune(38, request.param[2])   # element-parallel place (one top-level group)
+    gpu_ctx.tune(41, request.param[3])   # element-parallel encode image (0: lanes per record)
     yield request.param
     gpu_ctx.tune(0)
 
