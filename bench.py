@@ -65,6 +65,9 @@ def parse(argv=None):
     p.add_argument("--gather-reps", type=int, default=3)
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="cpu_baseline budget (0 = skip)")
     p.add_argument("--no-host-inclusive", action="store_true")
+    p.add_argument("--no-check", action="store_true",
+                   help="skip the round-trip checks (timing probe builds whose output is wrong by design; "
+                        "never a bench line)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--test-codec", default="",
                    help="tests only: module providing make_workload() (CPU launcher test, gloo)")
@@ -472,14 +475,16 @@ def measure(R, args, make, cfg, framed, n, steps, warmup, with_gather):
     for _ in range(warmup):
         wl.step()
     R.sync()
-    wl.check()   # correctness of the measured path, outside the timed region
+    if not args.no_check:
+        wl.check()   # correctness of the measured path, outside the timed region
     wl.reset_stats()
     dt = R.timed(lambda: [wl.step() for _ in range(steps)])
     roof, step_ms = wl.roofline(steps)
     t_enc = R.timed(lambda: [wl.encode() for _ in range(steps)])
     t_dec = R.timed(lambda: [wl.decode() for _ in range(steps)])
     R.sync()
-    wl.check()
+    if not args.no_check:
+        wl.check()
     recs = wl.n * R.world * steps
     e = {"config": cfg, "framed": bool(framed), "workload": wl.desc, "records_per_gpu": wl.n,
          "xdr_bytes_per_gpu": wl.xlen, "native_bytes_per_gpu": wl.native_bytes,
@@ -1089,6 +1094,8 @@ def run_rank(args):
             "host_inclusive_byref": hbyref,
             "extra_configs": extra,
         }
+        if args.no_check:
+            line["unchecked"] = True   # a probe build's timing, not a measurement of the product
         print(json.dumps(line), flush=True)
     if ctx is not None:
         ctx.close()
