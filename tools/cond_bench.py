@@ -15,7 +15,8 @@
   group levels.
 
 Device-resident, HIP-event timed encode and decode (median of reps); bytes =
-native + XDR per direction, as bench.py counts them; round trip checked."""
+native + XDR per direction, as bench.py counts them; roundtrip_ok = the decode
+succeeds and its output re-encodes to the same stream and offsets."""
 import json
 import os
 import sys
@@ -81,6 +82,12 @@ def run(name, fields, conds, n, dyn_len, group_len=(0, 4)):
     bcols = back.columns()
     t_dec = timed(lambda: ctx.decode(sch, out, total, n, bcols, rec_offsets=ro))
     ok = ctx.decode(sch, out, total, n, bcols, rec_offsets=ro) == (0, n, 0)
+    # an output check at full size: the decoded batch re-encodes to the same
+    # stream and record offsets (absent arms, lists and counts included)
+    out2 = torch.zeros_like(out)
+    ro2 = torch.zeros_like(ro)
+    ok = ok and ctx.encode(sch, bcols, n, out2, cap, rec_offsets=ro2) == total and \
+        bool(torch.equal(out2, out)) and bool(torch.equal(ro2, ro))
     nat = hb.native_bytes()
     per_dir = nat + total
     return {"shape": name, "records": n, "xdr_bytes": total, "native_bytes": nat,
