@@ -1106,6 +1106,18 @@ struct GRunL {
 constexpr bool g_run_lds(int D) { return D > XDRG_RUN_LDS_D; }
 template <int D>
 using GRunOf = typename std::conditional<g_run_lds(D), GRunL, GRun>::type;
+// The running offsets of an element of the one-level element-parallel place:
+// its (at most two) dynamic members' slots and offsets, two compares instead
+// of a 16-way select per access.
+struct GRun2 {
+    uint32_t s0, s1;
+    uint64_t v0, v1;
+    __device__ __forceinline__ uint64_t get(uint32_t slot) const { return slot == s0 ? v0 : slot == s1 ? v1 : 0; }
+    __device__ __forceinline__ void set(uint32_t slot, uint64_t x) {   // (selects: kept in registers)
+        v1 = slot == s1 && slot != s0 ? x : v1;
+        v0 = slot == s0 ? x : v0;
+    }
+};
 __device__ __forceinline__ void g_run_bind(GRun &, uint64_t *) {}
 __device__ __forceinline__ void g_run_bind(GRunL &run, uint64_t *rl) { run.v = rl; }
 constexpr uint32_t kRunLds = kMaxSlots * kRecThreads;   // GRunL words of a block
@@ -1148,8 +1160,8 @@ __device__ __forceinline__ void g_run_init(const GroupArgs &a, uint32_t k, uint6
 
 // Element e of group g with no bytes on the wire (an absent T x[N]'s N
 // elements): fixed members zero, dynamic members and inner arrays empty.
-template <int L, int D>
-__device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, uint64_t e, GRunOf<D> &run) {
+template <int L, int D, class R>
+__device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, uint64_t e, R &run) {
     g = g_uni(g);
     const GField &G = a.f[g];
     for (uint32_t j = 1; j <= G.nmem; ++j) {
@@ -1168,15 +1180,15 @@ __device__ __forceinline__ void g_absent_elem(const GroupArgs &a, uint32_t g, ui
     }
 }
 
-template <int L, int D>
+template <int L, int D, class R>
 __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in, uint64_t &pos,
-                           uint64_t end, GDisc &d, GRunOf<D> &run);
+                           uint64_t end, GDisc &d, R &run);
 // Inner group g (at depth L, a member of an element at depth L - 1) of outer
 // element e: its count word or list bools, read as the walk checked them,
 // then its elements.
-template <int L, int D>
+template <int L, int D, class R>
 __device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in,
-                                            uint64_t &pos, uint64_t end, GDisc &d, GRunOf<D> &run) {
+                                            uint64_t &pos, uint64_t end, GDisc &d, R &run) {
     g = g_uni(g);
     const GField &G = a.f[g];
     const uint64_t i0 = G.kind == XDRG_K_FIXED ? e * G.count : run.get(G.slot);
@@ -1203,9 +1215,9 @@ __device__ __forceinline__ void g_dec_inner(const GroupArgs &a, uint32_t g, uint
 }
 
 // The members of element e of group g (after a list element's TRUE).
-template <int L, int D>
+template <int L, int D, class R>
 __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint64_t e, const uint8_t *in, uint64_t &pos,
-                           uint64_t end, GDisc &d, GRunOf<D> &run) {
+                           uint64_t end, GDisc &d, R &run) {
     g = g_uni(g);
     const GField &f = a.f[g];
     for (uint32_t j = 1; j <= f.nmem; ++j) {
@@ -1271,6 +1283,9 @@ __device__ __forceinline__ void g_elem_skip(const GroupArgs &a, uint32_t g, cons
     }
 }
 
+#ifndef XDRG_EL_RUN2
+#define XDRG_EL_RUN2 1   // the element decode's running offsets as GRun2 (0: the 16-slot GRun)
+#endif
 // Element-parallel place (tuning key 38): the element descriptors a record
 // lane leaves for a sub-batch — element i (= e - E0) starts at tile offset
 // pos[i], and dynamic member q (of at most 2) at native offset sb[q] +
@@ -1737,9 +1752,13 @@ __global__ __launch_bounds__(kRecThreads, XDRG_EL_OCC) void k_grp_dec_place_el(c
         const uint64_t nel = mE[je] - el.E0;
         XDRG_DCHECK(nel <= a.dec_el);   // (the fit count bounded the sub-batch's elements)
         for (uint32_t i = tid; i < nel; i += kRecThreads) {
+#if XDRG_EL_RUN2
+            GRun2 run{el.ms0 ? el.ms0 : ~0u, el.ms1 ? el.ms1 : ~0u, 0, 0};
+#else
             GRunOf<1> run;
             g_run_bind(run, runs + tid);
             run.zero();
+#endif
             // the record walk left every element a tile position inside the staged
             // bytes and member offsets inside the members' capacities
             XDRG_DCHECK(dpos[i] < 16u * nch);
