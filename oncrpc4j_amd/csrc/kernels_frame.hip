@@ -760,8 +760,10 @@ __global__ __launch_bounds__(256, 4) void k_fr_mark(const uint32_t *__restrict__
 // messages, res[5] = fragments of the first `cap` messages (k_fr_emit lowers
 // it), res[3] = consumed stream bytes (set by k_fr_emit).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64_t nsup, FrameBase *bases,
-                                                    uint64_t *res) {
+// Super-chunks at or past nv are off the real chain (the speculative walk's
+// supers after its terminal) and count as empty; bases[] is written for all.
+__device__ __forceinline__ void fr_bases_block(const FrameSuper *sup, uint64_t nsup, uint64_t nv, FrameBase *bases,
+                                               uint64_t *res) {
     // thread t takes the run of super-chunks [t R, t R + R): its sums and
     // "last non-empty tail" in registers, one block scan of the runs, then the
     // run again with the carried prefix
@@ -770,7 +772,8 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
     __shared__ uint64_t fc;
     const uint32_t tid = threadIdx.x;
     if (tid == 0) fc = 0;
-    if (res[0] == kFUnal) return;   // block-uniform
+    const FrameSuper none = {0, 0, 2, 0, 0};
+    auto get = [&](uint64_t s) { return s < nv ? sup[s] : none; };
     const uint64_t R = (nsup + 1023) / 1024;
     const uint64_t s0 = tid * R, s1 = min(s0 + R, nsup);
     uint64_t f = 0, l = 0;
@@ -780,7 +783,7 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
     if (R <= kRun) {
 #pragma unroll
         for (int i = 0; i < kRun; ++i)
-            if (s0 + i < s1) run[i] = sup[s0 + i];
+            if (s0 + i < s1) run[i] = get(s0 + i);
 #pragma unroll
         for (int i = 0; i < kRun; ++i)
             if (s0 + i < s1) {
@@ -790,7 +793,7 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
             }
     } else {
         for (uint64_t s = s0; s < s1; ++s) {
-            const FrameSuper v = sup[s];
+            const FrameSuper v = get(s);
             f += v.nfrag;
             l += v.nlast;
             if (v.nfrag) t = v.tail;
@@ -830,7 +833,7 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
         for (int i = 0; i < kRun; ++i)
             if (s0 + i < s1) emit(s0 + i, run[i]);
     } else {
-        for (uint64_t s = s0; s < s1; ++s) emit(s, sup[s]);
+        for (uint64_t s = s0; s < s1; ++s) emit(s, get(s));
     }
     if (best) atomicMax((unsigned long long *)&fc, (unsigned long long)best);
     __syncthreads();
@@ -841,6 +844,12 @@ __global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64
         res[3] = 0;
         res[6] = 0;             // k_fr_emit: a message offset off the expected stride
     }
+}
+__global__ __launch_bounds__(1024) void k_fr_bases(const FrameSuper *sup, uint64_t nsup, FrameBase *bases,
+                                                    uint64_t *res) {
+    if (threadIdx.x == 0) res[7] = 0;   // (a speculative walk that gave up may have set it)
+    if (res[0] == kFUnal) return;       // block-uniform
+    fr_bases_block(sup, nsup, nsup, bases, res);
 }
 
 // ---------------------------------------------------------------------------
@@ -946,7 +955,7 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
     __shared__ uint32_t wsum[2][2], wtail[2], wlo[2], whi[2];
     __shared__ uint16_t so[kFChunk + 1];           // staged message offsets
     const uint64_t r0 = res[0], F = res[1], M = res[4];
-    if (r0 == kFUnal) return;
+    if (r0 == kFUnal || res[7]) return;   // byte walk next, or the speculative walk gave up
     // `per` consecutive sub-chunks per block (fewer, longer blocks: the
     // per-sub-chunk work is a few hundred stores)
     const uint64_t k0 = (uint64_t)blockIdx.x * per;
@@ -1021,6 +1030,416 @@ __global__ __launch_bounds__(256) void k_fr_copy(const uint8_t *in, const uint64
     }
 }
 
+// ---------------------------------------------------------------------------
+// Speculative walk (word mode, round 6): one read of the stream, chain work
+// in proportion to the marks, no per-word exit table.
+// ---------------------------------------------------------------------------
+// One wave per super-chunk (k_fs_walk), its sub-chunks in order; a sub-chunk
+// is a tile of 64 segments of 64 words, lane l owning segment l:
+//   1. each lane walks its segment from its first word whose chain leaves the
+//      segment plausibly (exit in the next kSpWin words, or exactly at the
+//      stream end); words of rejected chains are skipped (same exit).  The
+//      accepted chain: its complete words S, their LAST flags, the last word
+//      T and the exit X.  Payload read as a mark almost always jumps far, so
+//      the accepted chain is normally the real one from the segment's first
+//      mark on.
+//   2. from the sub-chunk's entry e (exact inside a super-chunk: the previous
+//      sub-chunk's exit), the segments the real chain visits are found by
+//      binary lifting over the segment successors (lane shuffles): a segment
+//      is on the path when its predecessor's exit lands in it, and its
+//      landing must lie on its accepted chain (or be its last word).  All
+//      landings on their chains: the marks are the chains from the landings
+//      on.  Otherwise (rare: a false chain accepted before the landing, a
+//      landing on an incomplete last fragment) one exact walk from e that
+//      takes a segment's chain wherever the walk meets it.
+//   3. bitmaps and counts as k_fr_mark leaves them (k_fr_emit reads both).
+// A super-chunk's own entry is the one guess: the exit of the first
+// plausible chain through the last kSpHalo words of the previous super-chunk
+// (else its first accepted segment chain).  k_fs_fix checks every guess
+// against the previous super-chunk's exit (both in sx), walks the first
+// wrong one again from its true entry, and repeats, at most kSpFixIters
+// times; then the bases.  A stream it cannot settle (fragments longer than a
+// super-chunk, bodies of mark-like words everywhere) sets res[7] and is
+// walked again by the exact kernels above.
+constexpr uint32_t kSpWin = 2048;    // plausible exits: the next kSpWin words past a segment
+constexpr uint32_t kSpHalo = 128;    // words of the previous super-chunk walked for the entry guess
+constexpr uint32_t kSpNoT = 0xffu;   // a segment without an accepted chain
+constexpr int kSpFixIters = 4;
+struct SpLds {                       // one wave's share (18.5 KiB)
+    uint32_t tile[kFChunk];          // the sub-chunk, swizzled (sp_idx)
+    uint64_t nS[64], nLM[64];        // accepted chains (the exact walk's shortcuts)
+    uint32_t nX[64], nT[64];
+    uint32_t fb[128], lb[128];       // the exact walk's bitmaps
+};
+// Word q of a tile: segment l = q / 64 keeps its 64 words in LDS row l, word
+// c at c ^ sw(l).  sw's bits 2-4 are l % 8 and bits 0-1 (l / 8) % 4, so the
+// 32 lanes of a half-wave reading the same offset c of their segments hit 32
+// banks; the staging store of 4 words keeps its 16-byte slot (bits 0-1 of sw
+// are the same for every segment a staging vector k covers: l / 8 = k / 2).
+__device__ __forceinline__ uint32_t sp_idx(uint32_t q) {
+    const uint32_t l = q >> 6;
+    return (q & ~63u) | ((q & 63u) ^ (((l & 7u) << 2) | ((l >> 3) & 3u)));
+}
+__device__ __forceinline__ uint64_t sp_shfl64(uint64_t v, uint32_t src) {
+    const uint32_t lo = __shfl((uint32_t)v, (int)src, 64), hi = __shfl((uint32_t)(v >> 32), (int)src, 64);
+    return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ void sp_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+// Loads of sub-chunk words base + 4 l + 256 k .. + 3 (k < 16): 1 KiB per
+// wave-instruction; words past Q read as 0 (never walked).
+__device__ __forceinline__ void sp_load(const uint32_t *w, uint32_t Q, uint32_t base, uint32_t l, u32x4f (&y)[16]) {
+    if (base + kFChunk <= Q) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) y[k] = __builtin_nontemporal_load((const u32x4f *)(w + base + 4 * l + 256 * k));
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t q = base + 4 * l + 256 * k;
+            y[k] = u32x4f{q < Q ? w[q] : 0u, q + 1 < Q ? w[q + 1] : 0u, q + 2 < Q ? w[q + 2] : 0u,
+                          q + 3 < Q ? w[q + 3] : 0u};
+        }
+    }
+}
+__device__ __forceinline__ void sp_stage(uint32_t *tile, uint32_t l, const u32x4f (&y)[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t q0 = 4 * l + 256 * k;
+        const uint32_t sg = q0 >> 6;
+        const uint32_t sw = ((sg & 7u) << 2) | ((sg >> 3) & 3u);
+        const int p = (k >> 1) & 3;   // == sw & 3
+        const uint32_t at = (q0 & ~63u) | ((q0 & 63u) ^ (sw & ~3u));
+        const u32x4f v = y[k];
+        const uint32_t a[4] = {v.x, v.y, v.z, v.w};
+        *(u32x4f *)&tile[at] = u32x4f{a[0 ^ p], a[1 ^ p], a[2 ^ p], a[3 ^ p]};
+    }
+}
+
+// The wave's walk of super-chunk s (lane = threadIdx.x % 64).  given: the
+// entry is gent (a re-walk from k_fs_fix); else 0 for s = 0 and guessed for
+// the others.  Writes the 16 FrameSub of s, the bitmaps of its sub-chunks
+// with marks, sup[s] and sx[2 s] = entry (kFNone: none found), sx[2 s + 1] =
+// exit (the first chain word past the super-chunk, or a terminal).
+__device__ __forceinline__ void fs_super(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb, uint32_t s, bool given,
+                         uint32_t gent, FrameSub *sub, uint32_t *fbits, uint32_t *lbits, FrameSuper *sup,
+                         uint32_t *sx, SpLds *sp) {
+    const uint32_t l = threadIdx.x & 63;
+    uint32_t *const tile = sp->tile;
+    const uint32_t sbeg = s * kFSuper;
+    const uint32_t send = min(sbeg + kFSuper, Q);
+    const uint32_t nsub = (send - sbeg + kFChunk - 1) / kFChunk;
+    bool known = true;
+    uint32_t e = given ? gent : 0u;
+    if (!given && s > 0) {
+        // the entry guess: chains through the last kSpHalo words of s - 1,
+        // lane l from word l, then l + 64; the lowest accepted start's exit
+        const uint32_t hb = sbeg - kSpHalo;
+        tile[l] = w[hb + l];
+        tile[l + 64] = w[hb + l + 64];
+        sp_fence();
+        uint32_t c = l, cur = l, hx = 0, key = 0xffu;
+        bool act = true;
+        while (__ballot(act)) {
+            if (act) {
+                const uint32_t m = fr_bswap(tile[cur]);
+                const uint32_t nx = fr_next<4>(m, hb + cur, Q, tb);
+                const bool comp = nx < kFUnal;
+                const uint32_t d = nx - hb;
+                if (comp && d < kSpHalo) {
+                    cur = d;
+                } else {
+                    if (comp && nx - sbeg < kSpWin) {
+                        hx = nx;
+                        key = c;
+                        act = false;
+                    } else if (c < 64) {
+                        c += 64;
+                        cur = c;
+                    } else {
+                        act = false;
+                    }
+                }
+            }
+        }
+        const uint32_t kmin = fr_wave_min(key);
+        if (kmin != 0xffu) {
+            const uint32_t src = __builtin_ctzll(__ballot(key == kmin));
+            e = __shfl(hx, (int)src, 64);
+        } else {
+            known = false;
+        }
+        sp_fence();
+    }
+    const uint32_t E0 = known ? e : kFNone;
+    uint32_t entry = E0;
+    uint32_t pre_f = 0, pre_l = 0, tail = 2, lastlast = 0, has_ll = 0;
+    u32x4f y[16];
+    sp_load(w, Q, sbeg, l, y);
+    const uint64_t sub0 = (uint64_t)s * (kFSuper / kFChunk);
+    for (uint32_t j = 0; j < kFSuper / kFChunk; ++j) {
+        const uint32_t base = sbeg + j * kFChunk;
+        const uint32_t bend = base + kFChunk;
+        const uint64_t sj = sub0 + j;
+        FrameSub info;
+        info.nfrag = info.nlast = info.upto_ll = info.has_ll = info.rsv = 0;
+        info.pre_frag = pre_f;
+        info.pre_last = pre_l;
+        info.prev_tail = tail;
+        const bool need = j < nsub && (!known || (e >= base && e < bend && e < Q));
+        if (!need) {
+            if (j + 1 < nsub) sp_load(w, Q, base + kFChunk, l, y);
+            if (l == 0) sub[sj] = info;
+            continue;
+        }
+        sp_stage(tile, l, y);
+        if (j + 1 < nsub) sp_load(w, Q, base + kFChunk, l, y);
+        sp_fence();
+        // 1. the segment's accepted chain
+        const uint32_t gsb = base + 64 * l;
+        const uint32_t nval = Q > gsb ? min(Q - gsb, 64u) : 0u;
+        uint64_t S = 0, LM = 0;
+        uint32_t X = 0, T = kSpNoT, sig = 0;
+        {
+            const uint64_t valid = nval >= 64 ? ~0ull : ((1ull << nval) - 1ull);
+            uint64_t rej = 0, ms = 0, ml = 0, vis = 0;
+            uint32_t c = 0, cur = 0;
+            bool act = nval > 0;
+            while (__ballot(act)) {
+                if (act) {
+                    vis |= 1ull << cur;
+                    const uint32_t m = fr_bswap(tile[sp_idx(64 * l + cur)]);
+                    const uint32_t nx = fr_next<4>(m, gsb + cur, Q, tb);
+                    const bool comp = nx < kFUnal;
+                    if (comp) {
+                        ms |= 1ull << cur;
+                        ml |= (uint64_t)(m >> 31) << cur;
+                    }
+                    const uint32_t d = nx - gsb;
+                    if (comp && d < nval) {
+                        cur = d;
+                    } else if (comp && (nx == Q || (d >= 64 && d - 64 < kSpWin))) {
+                        S = ms;
+                        LM = ml;
+                        X = nx;
+                        T = cur;
+                        sig = c;
+                        act = false;
+                    } else {
+                        rej |= vis;
+                        const uint64_t fr = ~rej & valid & (c < 63 ? ~0ull << (c + 1) : 0ull);
+                        if (fr) {
+                            c = (uint32_t)__builtin_ctzll(fr);
+                            cur = c;
+                            ms = ml = vis = 0;
+                        } else {
+                            act = false;
+                        }
+                    }
+                }
+            }
+        }
+        const bool acc = T != kSpNoT;
+        if (!known) {   // no guess yet: the first accepted chain of this sub-chunk
+            const uint64_t am = __ballot(acc);
+            if (!am) {
+                if (l == 0) sub[sj] = info;
+                sp_fence();
+                continue;
+            }
+            const uint32_t ka = __builtin_ctzll(am);
+            e = base + 64 * ka + __shfl(sig, (int)ka, 64);
+            entry = e;
+            known = true;
+        }
+        // 2. the path from e
+        const uint32_t el = e - base, ke = el >> 6;
+        const uint32_t succ = acc && X < Q && X < bend ? (X - base) >> 6 : 64u;
+        uint32_t J[6];
+        J[0] = succ;
+#pragma unroll
+        for (int r = 1; r < 6; ++r) {
+            const uint32_t t = __shfl(J[r - 1], (int)(J[r - 1] & 63u), 64);
+            J[r] = J[r - 1] < 64 ? t : 64u;
+        }
+        uint32_t p = ke;   // the last path segment before l (for l > ke)
+#pragma unroll
+        for (int r = 5; r >= 0; --r) {
+            const uint32_t n = __shfl(J[r], (int)p, 64);
+            if (n + 1 <= l) p = n;
+        }
+        const uint32_t sp_ = __shfl(succ, (int)p, 64), xp = __shfl(X, (int)p, 64);
+        const bool on = l == ke || (l > ke && sp_ == l);
+        const uint32_t lam = l == ke ? (el & 63u) : xp - gsb;
+        bool ok = true;
+        if (on) ok = acc && (((S >> lam) & 1ull) || lam == T);
+        uint64_t F, Lb;
+        uint32_t exitv;
+        if (__ballot(!ok) == 0) {
+            F = on ? S & (~0ull << lam) : 0ull;
+            Lb = F & LM;
+            const uint64_t onm = __ballot(on);
+            exitv = __shfl(X, 63 - __builtin_clzll(onm), 64);
+        } else {
+            // the exact walk from e, through accepted chains where it meets them
+            sp->nS[l] = S;
+            sp->nLM[l] = LM;
+            sp->nX[l] = X;
+            sp->nT[l] = acc ? T : kSpNoT;
+            sp->fb[l] = 0;
+            sp->fb[l + 64] = 0;
+            sp->lb[l] = 0;
+            sp->lb[l + 64] = 0;
+            sp_fence();
+            uint32_t x = e;
+            while (x < bend && x < Q) {
+                const uint32_t q = x - base, k = q >> 6, lm = q & 63u;
+                const uint32_t Tk = sp->nT[k];
+                const uint64_t Sk = sp->nS[k];
+                if (Tk != kSpNoT && (((Sk >> lm) & 1ull) || lm == Tk)) {
+                    const uint64_t f = Sk & (~0ull << lm), lf = f & sp->nLM[k];
+                    if (l == 0) {
+                        sp->fb[2 * k] |= (uint32_t)f;
+                        sp->fb[2 * k + 1] |= (uint32_t)(f >> 32);
+                        sp->lb[2 * k] |= (uint32_t)lf;
+                        sp->lb[2 * k + 1] |= (uint32_t)(lf >> 32);
+                    }
+                    x = sp->nX[k];
+                } else {
+                    const uint32_t m = fr_bswap(tile[sp_idx(q)]);
+                    const uint32_t nx = fr_next<4>(m, x, Q, tb);
+                    if (nx < kFUnal && l == 0) {
+                        sp->fb[q >> 5] |= 1u << (q & 31);
+                        if (m >> 31) sp->lb[q >> 5] |= 1u << (q & 31);
+                    }
+                    x = nx;
+                }
+                sp_fence();
+            }
+            exitv = x;
+            F = (uint64_t)sp->fb[2 * l + 1] << 32 | sp->fb[2 * l];
+            Lb = (uint64_t)sp->lb[2 * l + 1] << 32 | sp->lb[2 * l];
+            sp_fence();
+        }
+        // 3. bitmaps and counts
+        ((uint64_t *)fbits)[sj * 64 + l] = F;
+        ((uint64_t *)lbits)[sj * 64 + l] = Lb;
+        const uint32_t pf = __popcll(F), pl = __popcll(Lb);
+        const uint32_t incl = fr_wave_incl(pf);
+        const uint32_t nf = __shfl(incl, 63, 64);
+        const uint32_t nl = fr_wave_sum(pl);
+        const uint64_t lmask = __ballot(Lb != 0), fmask = __ballot(F != 0);
+        uint32_t upto = 0, tl = 2;
+        if (lmask) {
+            const uint32_t hl = 63 - __builtin_clzll(lmask);
+            uint32_t v = 0;
+            if (Lb) {
+                const uint32_t bl = 63 - __builtin_clzll(Lb);
+                v = incl - pf + __popcll(F & (bl == 63 ? ~0ull : (2ull << bl) - 1ull));
+            }
+            upto = __shfl(v, (int)hl, 64);
+        }
+        if (fmask) {
+            const uint32_t hf = 63 - __builtin_clzll(fmask);
+            const uint32_t tv = F ? (uint32_t)(Lb >> (63 - __builtin_clzll(F))) & 1u : 0u;
+            tl = __shfl(tv, (int)hf, 64);
+        }
+        info.nfrag = nf;
+        info.nlast = nl;
+        if (nl) {
+            info.has_ll = 1;
+            info.upto_ll = upto;
+            has_ll = 1;
+            lastlast = pre_f + upto;
+        }
+        if (l == 0) sub[sj] = info;
+        pre_f += nf;
+        pre_l += nl;
+        if (nf) tail = tl;
+        e = exitv;
+        sp_fence();
+    }
+    if (l == 0) {
+        FrameSuper v;
+        v.nfrag = pre_f;
+        v.nlast = pre_l;
+        v.tail = tail;
+        v.has_ll = has_ll;
+        v.upto_ll = lastlast;
+        sup[s] = v;
+        sx[2 * (uint64_t)s] = entry;
+        sx[2 * (uint64_t)s + 1] = known ? e : kFNone;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_fs_walk(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
+                                                FrameSub *sub, uint32_t *fbits, uint32_t *lbits, FrameSuper *sup,
+                                                uint32_t *sx) {
+    __shared__ SpLds sp;
+    fs_super(w, Q, tb, blockIdx.x, false, 0u, sub, fbits, lbits, sup, sx, &sp);
+}
+
+// One block: check every super-chunk's entry guess against its predecessor's
+// exit, walk the first wrong one again from its true entry (wave 0), repeat;
+// then the bases over the super-chunks the real chain reaches (res[0] = the
+// chain's end: >= Q, kFStop or kFUnal).  res[7] = 1: gave up.
+__global__ __launch_bounds__(1024) void k_fs_fix(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
+                                                 uint32_t nsup, FrameSub *sub, uint32_t *fbits, uint32_t *lbits,
+                                                 FrameSuper *sup, uint32_t *sx, FrameBase *bases, uint64_t *res) {
+    __shared__ SpLds sp;
+    __shared__ uint32_t s_fail, s_term;
+    const uint32_t tid = threadIdx.x;
+    bool done = false;
+    uint32_t term = ~0u;
+    for (int it = 0;; ++it) {
+        if (tid == 0) {
+            s_fail = ~0u;
+            s_term = ~0u;
+        }
+        __syncthreads();
+        uint32_t f = ~0u, t = ~0u;
+        for (uint32_t s = 1 + tid; s < nsup; s += 1024) {
+            const uint32_t E1 = sx[2 * (uint64_t)(s - 1)], L = sx[2 * (uint64_t)(s - 1) + 1];
+            if (E1 == kFNone) continue;   // s - 1 has no chain: if the chain reaches it, s - 1 fails
+            if (L >= kFUnal || L >= Q) {  // the chain ends in s - 1
+                t = min(t, s);
+                continue;
+            }
+            if (!(L < s * kFSuper + kFSuper && sx[2 * (uint64_t)s] == L)) f = min(f, s);
+        }
+        f = fr_wave_min(f);
+        t = fr_wave_min(t);
+        if ((tid & 63) == 0) {
+            if (f != ~0u) atomicMin(&s_fail, f);
+            if (t != ~0u) atomicMin(&s_term, t);
+        }
+        __syncthreads();
+        const uint32_t F = s_fail, T = s_term;
+        if (F == ~0u || T < F) {
+            done = true;
+            term = T;
+            break;
+        }
+        if (it == kSpFixIters) break;
+        if (tid < 64) fs_super(w, Q, tb, F, true, sx[2 * (uint64_t)(F - 1) + 1], sub, fbits, lbits, sup, sx, &sp);
+        __threadfence_block();
+        __syncthreads();
+    }
+    if (!done) {
+        if (tid == 0) res[7] = 1;
+        return;
+    }
+    const uint32_t nv = min(term, nsup);
+    if (tid == 0) {
+        res[0] = sx[2 * (uint64_t)(nv - 1) + 1];
+        res[7] = 0;
+    }
+    __syncthreads();
+    if (sx[2 * (uint64_t)(nv - 1) + 1] == kFUnal) return;   // the byte walk next (block-uniform)
+    fr_bases_block(sup, nsup, nv, bases, res);
+}
+
 // ---- launchers -------------------------------------------------------------------
 template <int B>
 static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
@@ -1059,6 +1478,24 @@ int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, ui
                                     (hipStream_t)stream)
                   : frame_launch<4>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per, stride,
                                     (hipStream_t)stream);
+}
+
+int frame_spec(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+               uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    const uint32_t *w = (const uint32_t *)in;
+    const uint32_t Q = frame_positions(len, 4), tb = (uint32_t)(len & 3);
+    const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
+    hipLaunchKernelGGL(k_fs_walk, dim3((uint32_t)nsup), dim3(64), 0, st, w, Q, tb, ws.sub, ws.fbits, ws.lbits,
+                       ws.sup, ws.sx);
+    hipLaunchKernelGGL(k_fs_fix, dim3(1), dim3(1024), 0, st, w, Q, tb, (uint32_t)nsup, ws.sub, ws.fbits, ws.lbits,
+                       ws.sup, ws.sx, ws.bases, ws.res);
+    uint32_t per = emit_per > 0 ? (uint32_t)emit_per : 1u;
+    while (per > 1 && nsub / per < 64) per >>= 1;
+    hipLaunchKernelGGL(k_fr_emit<4>, dim3((uint32_t)((nsub + per - 1) / per)), dim3(128), 0, st, w, Q, ws.sub,
+                       ws.bases, ws.fbits, ws.lbits, cap, stream_offsets ? 1 : 0, msg_offsets,
+                       frag_list ? ws.frag_pos : nullptr, ws.res, (uint64_t)nsub, per, stream_offsets ? stride : 0ull);
+    return (int)hipGetLastError();
 }
 
 int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,

@@ -1081,7 +1081,7 @@ struct GRun {
 #pragma unroll
         for (int q = 0; q < kMaxSlots; ++q) v[q] = (uint32_t)q + 1 == slot ? x : v[q];
     }
-    __device__ __forceinline__ void zero() {
+    __device__ __forceinline__ void zero(uint32_t = kMaxSlots) {
 #pragma unroll
         for (int q = 0; q < kMaxSlots; ++q) v[q] = 0;
     }
@@ -1090,14 +1090,24 @@ struct GRun {
 // v = base + t), for the deepest instances (D > 2): their inlined levels left
 // no registers for 16 running offsets and their selects (dec place 245-256
 // VGPRs, one wave per SIMD).
+// n: the columns behind v (k_grp_dec_place_eln reserves max(nslot, 1) of
+// them, the NEST kernels' static array kMaxSlots); zero(n) clears the
+// schema's nslot columns only.
 struct GRunL {
     uint64_t *v;
-    __device__ __forceinline__ uint64_t get(uint32_t slot) const { return slot ? v[(slot - 1) * kRecThreads] : 0; }
+    uint32_t n = kMaxSlots;
+    __device__ __forceinline__ uint64_t get(uint32_t slot) const {
+        XDRG_DCHECK(slot <= n);
+        return slot ? v[(slot - 1) * kRecThreads] : 0;
+    }
     __device__ __forceinline__ void set(uint32_t slot, uint64_t x) {
+        XDRG_DCHECK(slot <= n);
         if (slot) v[(slot - 1) * kRecThreads] = x;
     }
-    __device__ __forceinline__ void zero() {
-        for (int q = 0; q < kMaxSlots; ++q) v[q * kRecThreads] = 0;
+    __device__ __forceinline__ void zero(uint32_t nslot) {
+        XDRG_DCHECK(nslot <= kMaxSlots);
+        n = nslot ? nslot : 1u;
+        for (uint32_t q = 0; q < nslot; ++q) v[q * kRecThreads] = 0;
     }
 };
 #ifndef XDRG_RUN_LDS_D
@@ -1142,7 +1152,7 @@ __device__ __forceinline__ uint64_t g_first_row(const GroupArgs &a, uint32_t k, 
 // entry is written (an empty record leaves the next record's entry the same).
 template <class R>
 __device__ __forceinline__ void g_run_init(const GroupArgs &a, uint32_t k, uint64_t r, uint64_t e0, R &run) {
-    run.zero();
+    run.zero(a.nslot);
     const GField &f = a.f[k];
     for (uint32_t j = 1; j <= f.nmem; ++j) {
         j = g_uni(j);

@@ -290,6 +290,8 @@ struct xdrg_ctx {
     StageRing ring;             // XDRG_HOST_PTRS staging (allocated on first use)
     uint8_t *d_rx = nullptr;    // receive scratch: assembled message bodies / message offsets
     size_t rx_bytes = 0;
+    uint64_t frame_spec_calls = 0;     // speculative word walks (xdrg_internal_stat 1)
+    uint64_t frame_spec_gave_up = 0;   // ... of them walked again by the exact kernels (key 2)
 };
 
 static int hip_fail(xdrg_ctx *c, hipError_t e, const char *what) {
@@ -394,6 +396,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 43: if (v != 0 && v != 1 && v != 2 && v != 4) return -1; t.grp_enc_split = (int32_t)v; return 0;
     case 44: if (!in(0, 1)) return -1; t.grp_dec_emap = (int32_t)v; return 0;
     case 45: if (!in(0, 1)) return -1; t.grp_enc_img_nest = (int32_t)v; return 0;
+    case 47: if (!in(0, 1)) return -1; t.frame_spec = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -405,6 +408,17 @@ extern "C" int xdrg_internal_tune(xdrg_ctx *c, int key, long long value) {
     if (!c) return XDRG_E_INVAL;
     if (key == 0) { c->tune = Tuning(); return XDRG_OK; }
     return set_tuning(c->tune, key, value) ? XDRG_E_INVAL : XDRG_OK;
+}
+
+// Not part of include/xdrg.h: counters for the parity tests (1: speculative
+// frame walks, 2: those that gave up and ran the exact kernels).
+extern "C" long long xdrg_internal_stat(xdrg_ctx *c, int key) {
+    if (!c) return -1;
+    switch (key) {
+    case 1: return (long long)c->frame_spec_calls;
+    case 2: return (long long)c->frame_spec_gave_up;
+    default: return -1;
+    }
 }
 
 extern "C" const char *xdrg_status_string(int status) {
@@ -1117,16 +1131,22 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
                 for (uint32_t j = 1; j <= G.nmem; ++j) ns += a.f[k + j].slot ? 1u : 0u;
                 uint32_t tile = a.dec_tile < kElnTile ? a.dec_tile : kElnTile;
                 uint32_t cap = (uint32_t)c->tune.grp_dec_el < kElnCap ? (uint32_t)c->tune.grp_dec_el : kElnCap;
-                while (eln_lds_bytes(tile, cap, ns, a.nslot) > 65536 && tile > 4096) {
+                const size_t budget = kPlaceLdsBudget - kPlaceStaticLds;
+                while (eln_lds_bytes(tile, cap, ns, a.nslot) > budget && tile > 4096) {
                     tile /= 2;
                     cap = cap > 128 ? cap / 2 : cap;
                 }
-                if (eln_lds_bytes(tile, cap, ns, a.nslot) > 65536) break;
+                if (eln_lds_bytes(tile, cap, ns, a.nslot) > budget) break;
                 a.dec_tile = tile;
                 a.dec_el = cap;
                 a.el_g = k;
                 a.emap = emap;
             }
+        // a nested schema's lane-per-record places (k_grp_dec_place_lds<D > 1>)
+        // keep their running-offset columns in static LDS beside the tile
+        if (a.levels > 1 && !(a.emap && a.dec_el) && a.dec_tile &&
+            a.dec_tile + kNestRunLdsBytes + kPlaceStaticLds > kPlaceLdsBudget)
+            a.dec_tile = (uint32_t)((kPlaceLdsBudget - kNestRunLdsBytes - kPlaceStaticLds) & ~(size_t)15);
         if (n == 0) {
             for (uint32_t q = 0; q < a.nslot; ++q)
                 if (!a.f[a.slot_field[q]].grp) HIPCHK(c, hipMemsetAsync(cols[a.slot_field[q]].offsets, 0, 8, c->stream));
@@ -1975,7 +1995,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     const size_t o_ex = take(2 * Q), o_al = take(4 * (size_t)kFChunk * nsub), o_ac = take(4 * nsub), o_se = take(4 * nsup), o_wt = take(4 * 256 * nsup), o_gs = take(4 * 256 * (nsup + 64)), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
                  o_fb = take(512 * nsub), o_lb = take(512 * nsub), o_su = take(sizeof(FrameSuper) * nsup),
-                 o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_re = take(64);
+                 o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_sx = take(8 * nsup), o_re = take(64);
     if (off > c->fws_bytes) {
         if (c->d_fws) {
             HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2001,6 +2021,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     ws.sup = (FrameSuper *)(b + o_su);
     ws.bases = (FrameBase *)(b + o_ba);
     ws.frag_pos = (uint64_t *)(b + o_fp);
+    ws.sx = (uint32_t *)(b + o_sx);
     ws.res = (uint64_t *)(b + o_re);
     return XDRG_OK;
 }
@@ -2032,10 +2053,25 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
     const bool stream_offsets = payload == nullptr;
     bool serial = !aligned(in, 4) || Q == 0;
     if (!serial) {   // parallel walk over words; a real chain meeting a size % 4 != 0 walks again over bytes
-        HIPCHK(c, (hipError_t)frame_parallel(in, len, 4, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
+        bool exact = !c->tune.frame_spec;
+        if (!exact) {   // the speculative walk; the exact kernels when it gives up (res[7])
+            ++c->frame_spec_calls;
+            HIPCHK(c, (hipError_t)frame_spec(in, len, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
                                              c->tune.emit_per, stride, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 56, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 64, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            if (c->h_stat[2 + 7]) {
+                ++c->frame_spec_gave_up;
+                exact = true;
+                HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));
+            }
+        }
+        if (exact) {
+            HIPCHK(c, (hipError_t)frame_parallel(in, len, 4, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
+                                                 c->tune.emit_per, stride, c->stream));
+            HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 56, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+        }
         if (c->h_stat[2] == kFUnal) {
             if (len < kFByteMaxLen) {
                 rc = frame_ws(c, frame_positions(len, 1), ws);

@@ -193,6 +193,8 @@ struct Tuning {
                                     // bit 0 encode, bit 1 decode (0 in block order)
     int32_t emit_per = 4;           // key 36: frame walk, sub-chunks per k_fr_emit block (at most;
                                     // halved until the grid has >= 64 blocks)
+    int32_t frame_spec = 1;         // key 47: word-mode frame walk: 1 the speculative walk (k_fs_*,
+                                    // the exact kernels when it gives up), 0 the exact kernels only
     int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of
                                     // records (0: each lane walks its record in HBM)
     int32_t grp_enc_lanes = 8;      // key 32: repeated-group encode, lanes per record (64 = a wave)
@@ -294,9 +296,12 @@ struct FrameWs {                              // device workspace of one walk
     FrameBase *bases;                         // [nsup]
     uint64_t *frag_pos;                       // [Q + 2] stream offset of each complete fragment's mark
                                               // (xdrg_deframe; one entry past the last copied fragment)
+    uint32_t *sx;                             // [nsup][2] speculative walk: each super-chunk's entry
+                                              // guess and exit
     uint64_t *res;                            // [0] chain terminal [1] complete fragments (through the
                                               // last LAST one) [3] consumed bytes [4] complete messages
-                                              // [5] fragments of the first `cap` messages
+                                              // [5] fragments of the first `cap` messages [6] off-stride
+                                              // [7] 1: the speculative walk gave up
 };
 // Walk positions of a len-byte stream: B = 4 words (len / 4), B = 1 bytes a
 // whole mark can start at (len - 3).
@@ -315,6 +320,11 @@ int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, ui
                    uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream);
 int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
                  uint64_t *msg_offsets, void *stream);
+// The speculative word walk (k_fs_walk, k_fs_fix, k_fr_emit): the same
+// results as frame_parallel(B = 4) unless res[7] = 1 (it gave up; nothing
+// was emitted), then frame_parallel runs.
+int frame_spec(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+               uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream);
 // Bodies of the first nf fragments into payload (marks stripped).
 int frame_copy(const uint8_t *in, const FrameWs &ws, uint64_t nf, uint64_t payload_bytes, uint8_t *payload,
                void *stream);
@@ -430,6 +440,13 @@ constexpr int kMaxDynLds = 4;      // dynamic fields whose per-record metadata i
 // extents and first elements (2 x 257 u64) | tile | positions [cap] | scanned
 // counts [ns span columns][cap] | GRunL columns [nslot][256 lanes].
 constexpr size_t kElnMeta = 2 * (kRecThreads + 1) * 8 + 16;
+// LDS budget of one group place block (dynamic + static): two blocks per CU.
+// The static parts: k_grp_dec_place_eln's sbase and scan words (416 B at
+// round 6, kept under kPlaceStaticLds), and for D > 1 the lane-per-record
+// places' running-offset columns (kMaxSlots x kRecThreads words).
+constexpr size_t kPlaceLdsBudget = 65536;
+constexpr size_t kPlaceStaticLds = 512;
+constexpr size_t kNestRunLdsBytes = 8 * (size_t)kMaxSlots * kRecThreads;
 inline size_t eln_lds_bytes(uint32_t tile, uint32_t cap, uint32_t ns, uint32_t nslot) {
     return kElnMeta + tile + 4 * (size_t)cap * (1 + ns) + 8 + 8 * (size_t)kRecThreads * (nslot ? nslot : 1);
 }

@@ -34,6 +34,8 @@ def lib():
         # not in include/xdrg.h: per-context kernel choices (xdrg_internal.h Tuning)
         _LIB.xdrg_internal_tune.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong]
         _LIB.xdrg_internal_tune.restype = ctypes.c_int
+        _LIB.xdrg_internal_stat.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _LIB.xdrg_internal_stat.restype = ctypes.c_longlong
         v = _LIB.xdrg_abi_version()
         if v != abi.ABI_VERSION:
             raise RuntimeError(f"libxdrgpu.so ABI {v} != {abi.ABI_VERSION}")
@@ -361,6 +363,12 @@ class Context:
         rc = lib().xdrg_internal_tune(self._h, int(key), int(value))
         if rc:
             raise ValueError(f"tuning key {key} = {value} rejected")
+
+    def internal_stat(self, key):
+        """Internal counters (xdrg_internal_stat: 1 speculative frame walks,
+        2 of them walked again by the exact kernels).  Not part of the drop-in
+        boundary."""
+        return int(lib().xdrg_internal_stat(self._h, int(key)))
 
     def kernel_stats(self, kernel):
         """-> (launches, total_ms) for one XDRG_KERNEL_* id (needs timing=True)."""

@@ -350,8 +350,9 @@ class _Tape:
             sub.decl(d, f"{where}.{d.name}", None, stack + (st.name,))
         fields, conds = sub.result()
         if self.depth + 1 >= GROUP_LEVELS and any(f[0] == abi.T_GROUP for f in fields):
-            raise NotBatchable(f"{where}: elements of {st.name} hold arrays of structs or lists "
-                               f"{GROUP_LEVELS} group levels down ({GROUP_LEVELS} levels are batched)")
+            raise NotBatchable(f"{where}: elements of {st.name} hold arrays of structs or lists, which "
+                               f"would need group level {GROUP_LEVELS + 1} (the engine batches "
+                               f"{GROUP_LEVELS} levels)")
         if not fields:
             raise NotBatchable(f"{where}: elements of {st.name} have no fields")
         g = self.add((abi.T_GROUP, kind, count, len(fields)), guard)

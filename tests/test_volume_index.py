@@ -180,7 +180,7 @@ def test_oracle_random_roundtrip():
 
 
 @pytest.fixture(params=[(8, 32768, 1024, 16384), (8, 32768, 0, 0), (64, 0, 0, 4096), (4, 1024, 0, 0),
-                        (8, 16384, 256, 32768)],
+                        (8, 16384, 256, 32768), (8, 65536, 0, 0)],
                 ids=lambda p: f"enc{p[0]}-dtile{p[1]}-el{p[2]}-img{p[3]}")
 def grp_tune(request, gpu_ctx):
     """Group kernels under each production choice (tuning keys 32 / 33)."""
