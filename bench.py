@@ -1088,6 +1088,7 @@ def run_rank(args):
             "encode_only": head["encode_only"],
             "decode_only": head["decode_only"],
             "gather": head["gather"],
+            "receive": head.get("receive"),
             "cpu_baseline": cpu,
             "host_inclusive": hinc,
             "host_inclusive_var": hvar,

@@ -41,6 +41,8 @@
 // Word positions are 32-bit (streams < 16 GiB - 2 MiB, kFMaxLen).
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "xdrg_internal.h"
 
 namespace xdrg {
@@ -955,7 +957,7 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
     __shared__ uint32_t wsum[2][2], wtail[2], wlo[2], whi[2];
     __shared__ uint16_t so[kFChunk + 1];           // staged message offsets
     const uint64_t r0 = res[0], F = res[1], M = res[4];
-    if (r0 == kFUnal || res[7]) return;   // byte walk next, or the speculative walk gave up
+    if (r0 == kFUnal || (res[7] & 3)) return;   // byte walk next, the walk's checks failed or it gave up
     // `per` consecutive sub-chunks per block (fewer, longer blocks: the
     // per-sub-chunk work is a few hundred stores)
     const uint64_t k0 = (uint64_t)blockIdx.x * per;
@@ -1065,21 +1067,18 @@ constexpr uint32_t kSpWin = 2048;    // plausible exits: the next kSpWin words p
 constexpr uint32_t kSpHalo = 128;    // words of the previous super-chunk walked for the entry guess
 constexpr uint32_t kSpNoT = 0xffu;   // a segment without an accepted chain
 constexpr int kSpFixIters = 4;
-struct SpLds {                       // one wave's share (18.5 KiB)
-    uint32_t tile[kFChunk];          // the sub-chunk, swizzled (sp_idx)
+constexpr uint32_t kSpRow = 65;      // LDS words per segment row (one pad word)
+struct SpLds {                       // one wave's share (19 KiB)
+    uint32_t tile[64 * kSpRow];      // the sub-chunk, segment l in row l (sp_idx)
     uint64_t nS[64], nLM[64];        // accepted chains (the exact walk's shortcuts)
     uint32_t nX[64], nT[64];
     uint32_t fb[128], lb[128];       // the exact walk's bitmaps
 };
-// Word q of a tile: segment l = q / 64 keeps its 64 words in LDS row l, word
-// c at c ^ sw(l).  sw's bits 2-4 are l % 8 and bits 0-1 (l / 8) % 4, so the
-// 32 lanes of a half-wave reading the same offset c of their segments hit 32
-// banks; the staging store of 4 words keeps its 16-byte slot (bits 0-1 of sw
-// are the same for every segment a staging vector k covers: l / 8 = k / 2).
-__device__ __forceinline__ uint32_t sp_idx(uint32_t q) {
-    const uint32_t l = q >> 6;
-    return (q & ~63u) | ((q & 63u) ^ (((l & 7u) << 2) | ((l >> 3) & 3u)));
-}
+// Word q of a tile: segment l = q / 64 in row l, kSpRow words apart, so the
+// 32 lanes of a half-wave reading offset c of their own segments hit 32
+// banks ((65 l + c) % 32), and lane l staging word l of every segment writes
+// consecutive banks.
+__device__ __forceinline__ uint32_t sp_idx(uint32_t q) { return (q >> 6) * kSpRow + (q & 63u); }
 __device__ __forceinline__ uint64_t sp_shfl64(uint64_t v, uint32_t src) {
     const uint32_t lo = __shfl((uint32_t)v, (int)src, 64), hi = __shfl((uint32_t)(v >> 32), (int)src, 64);
     return (uint64_t)hi << 32 | lo;
@@ -1088,32 +1087,94 @@ __device__ __forceinline__ void sp_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
-// Loads of sub-chunk words base + 4 l + 256 k .. + 3 (k < 16): 1 KiB per
-// wave-instruction; words past Q read as 0 (never walked).
-__device__ __forceinline__ void sp_load(const uint32_t *w, uint32_t Q, uint32_t base, uint32_t l, u32x4f (&y)[16]) {
+// Loads of a sub-chunk: word base + 64 k + l into y[k] (k < 64), one
+// coalesced 256-byte dword load per k, so that lane l holds word l of every
+// segment k; words past Q read as 0 (never walked).
+__device__ __forceinline__ void sp_load(const uint32_t *w, uint32_t Q, uint32_t base, uint32_t l, uint32_t (&y)[64]) {
     if (base + kFChunk <= Q) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) y[k] = __builtin_nontemporal_load((const u32x4f *)(w + base + 4 * l + 256 * k));
+        for (int k = 0; k < 64; ++k) y[k] = __builtin_nontemporal_load(w + base + 64 * k + l);
     } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t q = base + 4 * l + 256 * k;
-            y[k] = u32x4f{q < Q ? w[q] : 0u, q + 1 < Q ? w[q + 1] : 0u, q + 2 < Q ? w[q + 2] : 0u,
-                          q + 3 < Q ? w[q + 3] : 0u};
+        for (int k = 0; k < 64; ++k) {
+            const uint32_t q = base + 64 * k + l;
+            y[k] = q < Q ? w[q] : 0u;
         }
     }
 }
-__device__ __forceinline__ void sp_stage(uint32_t *tile, uint32_t l, const u32x4f (&y)[16]) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const uint32_t q0 = 4 * l + 256 * k;
-        const uint32_t sg = q0 >> 6;
-        const uint32_t sw = ((sg & 7u) << 2) | ((sg >> 3) & 3u);
-        const int p = (k >> 1) & 3;   // == sw & 3
-        const uint32_t at = (q0 & ~63u) | ((q0 & 63u) ^ (sw & ~3u));
-        const u32x4f v = y[k];
-        const uint32_t a[4] = {v.x, v.y, v.z, v.w};
-        *(u32x4f *)&tile[at] = u32x4f{a[0 ^ p], a[1 ^ p], a[2 ^ p], a[3 ^ p]};
+// Stage y into the tile and return this lane's segment's candidate starts:
+// bit c = word c of segment l could be a mark whose fragment is shorter than
+// 16 KiB (size < 2^14, size % 4 == 0: in the raw big-endian word, bits 0-6,
+// 8-15, 22-23 and 24-25 clear).  One ballot per segment k is segment k's
+// mask; lane k keeps it.
+constexpr uint32_t kSpCandMask = 0x03C0FF7Fu;
+template <int K>
+__device__ __forceinline__ void sp_stage1(uint32_t *tile, uint32_t l, uint32_t v, uint32_t &lo, uint32_t &hi) {
+    tile[kSpRow * K + l] = v;
+    const uint64_t b = __ballot((v & kSpCandMask) == 0);
+    const uint32_t blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(lo) : "s"(blo), "n"(K));
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(hi) : "s"(bhi), "n"(K));
+}
+template <int... K>
+__device__ __forceinline__ uint64_t sp_stage_seq(uint32_t *tile, uint32_t l, const uint32_t (&y)[64],
+                                                 std::integer_sequence<int, K...>) {
+    uint32_t lo = 0, hi = 0;
+    (sp_stage1<K>(tile, l, y[K], lo, hi), ...);
+    return (uint64_t)hi << 32 | lo;
+}
+__device__ __forceinline__ uint64_t sp_stage(uint32_t *tile, uint32_t l, const uint32_t (&y)[64]) {
+    return sp_stage_seq(tile, l, y, std::make_integer_sequence<int, 64>{});
+}
+
+// A lane's segment chain: candidate starts in order, the words of a
+// rejected chain dropped with it (they share its exit); branch-free body.
+// INTERIOR (the sub-chunk ends kSpWin words or more before the stream's end):
+// every next mark that stays in the segment or exits plausibly is inside the
+// stream, so no fit test.
+template <bool INTERIOR>
+__device__ __forceinline__ void sp_lane_walk(const uint32_t *tile, uint32_t l, uint32_t gsb, uint32_t nval,
+                                             uint64_t cand, uint32_t Q, uint32_t tb, uint64_t &S, uint64_t &LM,
+                                             uint32_t &X, uint32_t &T, uint32_t &sig) {
+    const uint64_t valid = nval >= 64 ? ~0ull : ((1ull << nval) - 1ull);
+    uint64_t avail = cand & valid, ms = 0, ml = 0, vis = 0;
+    bool act = avail != 0;
+    uint32_t c = act ? (uint32_t)__builtin_ctzll(avail) : 0u, cur = c;
+    const uint32_t row = l * kSpRow;
+    while (__ballot(act)) {
+        const uint32_t m = fr_bswap(tile[row + cur]);
+        uint32_t d;
+        bool comp;
+        if (INTERIOR) {
+            comp = (m & 3u) == 0;
+            d = cur + 1 + ((m >> 2) & 0x1fffffffu);
+        } else {
+            const uint32_t nx = fr_next<4>(m, gsb + cur, Q, tb);
+            comp = nx < kFUnal;
+            d = nx - gsb;
+        }
+        const uint64_t bit = 1ull << cur;
+        vis |= bit;
+        ms |= comp ? bit : 0ull;
+        ml |= comp && (m >> 31) ? bit : 0ull;
+        const bool cont = comp && d < nval;
+        const bool take = act && !cont && comp && (gsb + d == Q || (d >= 64 && d - 64 < kSpWin));
+        const bool rej = act && !cont && !take;
+        if (take) {
+            S = ms;
+            LM = ml;
+            X = gsb + d;
+            T = cur;
+            sig = c;
+        }
+        avail = rej ? avail & ~vis & ~((2ull << c) - 1ull) : avail;
+        const uint32_t nc = avail ? (uint32_t)__builtin_ctzll(avail) : 0u;
+        cur = cont ? d : rej ? nc : cur;
+        c = rej ? nc : c;
+        ms = rej ? 0ull : ms;
+        ml = rej ? 0ull : ml;
+        vis = rej ? 0ull : vis;
+        act = act && !take && !(rej && !avail);
     }
 }
 
@@ -1122,7 +1183,13 @@ __device__ __forceinline__ void sp_stage(uint32_t *tile, uint32_t l, const u32x4
 // the others.  Writes the 16 FrameSub of s, the bitmaps of its sub-chunks
 // with marks, sup[s] and sx[2 s] = entry (kFNone: none found), sx[2 s + 1] =
 // exit (the first chain word past the super-chunk, or a terminal).
-__device__ __forceinline__ void fs_super(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb, uint32_t s, bool given,
+struct SpRec {                       // a run of super-chunks (k_fs_walk's look-back)
+    uint64_t nf, nl, up;             // complete fragments, LAST ones, fragments through the last LAST one
+    uint32_t E, X;                   // the first one's entry, the last one's exit
+    uint32_t fl;                     // kSpTail bits: LAST flag of the last fragment (2: none); kSpHas ..
+};
+constexpr uint32_t kSpTail = 3u, kSpHas = 4u, kSpTerm = 8u, kSpFail = 16u, kSpEmpty = 32u;
+__device__ __forceinline__ SpRec fs_super(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb, uint32_t s, bool given,
                          uint32_t gent, FrameSub *sub, uint32_t *fbits, uint32_t *lbits, FrameSuper *sup,
                          uint32_t *sx, SpLds *sp) {
     const uint32_t l = threadIdx.x & 63;
@@ -1175,7 +1242,7 @@ __device__ __forceinline__ void fs_super(const uint32_t *__restrict__ w, uint32_
     const uint32_t E0 = known ? e : kFNone;
     uint32_t entry = E0;
     uint32_t pre_f = 0, pre_l = 0, tail = 2, lastlast = 0, has_ll = 0;
-    u32x4f y[16];
+    uint32_t y[64];
     sp_load(w, Q, sbeg, l, y);
     const uint64_t sub0 = (uint64_t)s * (kFSuper / kFChunk);
     for (uint32_t j = 0; j < kFSuper / kFChunk; ++j) {
@@ -1193,53 +1260,19 @@ __device__ __forceinline__ void fs_super(const uint32_t *__restrict__ w, uint32_
             if (l == 0) sub[sj] = info;
             continue;
         }
-        sp_stage(tile, l, y);
+        const uint64_t cand = sp_stage(tile, l, y);
         if (j + 1 < nsub) sp_load(w, Q, base + kFChunk, l, y);
         sp_fence();
-        // 1. the segment's accepted chain
+        // 1. the segment's accepted chain: candidate starts in order, the
+        // words of a rejected chain dropped with it (they share its exit)
         const uint32_t gsb = base + 64 * l;
         const uint32_t nval = Q > gsb ? min(Q - gsb, 64u) : 0u;
         uint64_t S = 0, LM = 0;
         uint32_t X = 0, T = kSpNoT, sig = 0;
-        {
-            const uint64_t valid = nval >= 64 ? ~0ull : ((1ull << nval) - 1ull);
-            uint64_t rej = 0, ms = 0, ml = 0, vis = 0;
-            uint32_t c = 0, cur = 0;
-            bool act = nval > 0;
-            while (__ballot(act)) {
-                if (act) {
-                    vis |= 1ull << cur;
-                    const uint32_t m = fr_bswap(tile[sp_idx(64 * l + cur)]);
-                    const uint32_t nx = fr_next<4>(m, gsb + cur, Q, tb);
-                    const bool comp = nx < kFUnal;
-                    if (comp) {
-                        ms |= 1ull << cur;
-                        ml |= (uint64_t)(m >> 31) << cur;
-                    }
-                    const uint32_t d = nx - gsb;
-                    if (comp && d < nval) {
-                        cur = d;
-                    } else if (comp && (nx == Q || (d >= 64 && d - 64 < kSpWin))) {
-                        S = ms;
-                        LM = ml;
-                        X = nx;
-                        T = cur;
-                        sig = c;
-                        act = false;
-                    } else {
-                        rej |= vis;
-                        const uint64_t fr = ~rej & valid & (c < 63 ? ~0ull << (c + 1) : 0ull);
-                        if (fr) {
-                            c = (uint32_t)__builtin_ctzll(fr);
-                            cur = c;
-                            ms = ml = vis = 0;
-                        } else {
-                            act = false;
-                        }
-                    }
-                }
-            }
-        }
+        if ((uint64_t)bend + kSpWin <= Q)
+            sp_lane_walk<true>(tile, l, gsb, nval, cand, Q, tb, S, LM, X, T, sig);
+        else
+            sp_lane_walk<false>(tile, l, gsb, nval, cand, Q, tb, S, LM, X, T, sig);
         const bool acc = T != kSpNoT;
         if (!known) {   // no guess yet: the first accepted chain of this sub-chunk
             const uint64_t am = __ballot(acc);
@@ -1360,6 +1393,7 @@ __device__ __forceinline__ void fs_super(const uint32_t *__restrict__ w, uint32_
         e = exitv;
         sp_fence();
     }
+    const uint32_t X = known ? e : kFNone;
     if (l == 0) {
         FrameSuper v;
         v.nfrag = pre_f;
@@ -1369,21 +1403,216 @@ __device__ __forceinline__ void fs_super(const uint32_t *__restrict__ w, uint32_
         v.upto_ll = lastlast;
         sup[s] = v;
         sx[2 * (uint64_t)s] = entry;
-        sx[2 * (uint64_t)s + 1] = known ? e : kFNone;
+        sx[2 * (uint64_t)s + 1] = X;
+    }
+    SpRec r;
+    r.nf = pre_f;
+    r.nl = pre_l;
+    r.up = lastlast;
+    r.E = entry;
+    r.X = X;
+    r.fl = tail | (has_ll ? kSpHas : 0u) | (X >= kFUnal || X >= Q ? kSpTerm : 0u);
+    return r;
+}
+
+// ---- the walk's look-back: each super-chunk's bases and the entry checks --
+// A run's record: its counts, first entry, last exit and whether it stops (a
+// terminal or the stream's end: later super-chunks are off the chain; a
+// failed check: the speculative results are void).  Records combine in
+// stream order (associative): a stopped left run absorbs the right one; else
+// the right run's entry must be the left run's exit, landing in the right
+// run's first super-chunk r0.
+__device__ __forceinline__ SpRec sp_combine(const SpRec &L, const SpRec &R, uint32_t r0) {
+    if (L.fl & kSpEmpty) return R;
+    if (R.fl & kSpEmpty) return L;
+    if (L.fl & (kSpTerm | kSpFail)) return L;
+    SpRec o = L;
+    if (!(R.E == L.X && (uint64_t)L.X < (uint64_t)r0 * kFSuper + kFSuper)) {
+        o.fl |= kSpFail;
+        return o;
+    }
+    const uint32_t rt = R.fl & kSpTail;
+    o.X = R.X;
+    o.nf = L.nf + R.nf;
+    o.nl = L.nl + R.nl;
+    o.up = (R.fl & kSpHas) ? L.nf + R.up : L.up;
+    o.fl = (rt != 2u ? rt : (L.fl & kSpTail)) | ((L.fl | R.fl) & kSpHas) | (R.fl & (kSpTerm | kSpFail));
+    return o;
+}
+__device__ __forceinline__ SpRec sp_shfl_rec(const SpRec &r, uint32_t src) {
+    SpRec o;
+    o.nf = sp_shfl64(r.nf, src);
+    o.nl = sp_shfl64(r.nl, src);
+    o.up = sp_shfl64(r.up, src);
+    o.E = __shfl(r.E, (int)src, 64);
+    o.X = __shfl(r.X, (int)src, 64);
+    o.fl = __shfl(r.fl, (int)src, 64);
+    return o;
+}
+// Five tagged words per super-chunk (flag in bits 62-63: 1 its own record,
+// 2 the record of [0, s]), word k of super-chunk s at lbw[k nsup + s], stored
+// and polled with agent-scope atomics.  A reader takes a record whose five
+// flags agree (an upgrade from own to inclusive is five stores).
+__device__ __forceinline__ void sp_put(uint64_t *lbw, uint64_t ns, uint32_t s, const SpRec &r, uint64_t flag) {
+    const uint64_t f = flag << 62;
+    const uint64_t v[5] = {f | r.X | (uint64_t)(r.fl & 31u) << 32, f | r.nf, f | r.nl, f | r.up, f | r.E};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) __hip_atomic_store(lbw + k * ns + s, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Decoupled look-back over block records (wave 0 of the block): record b
+// covers super-chunks [b span, b span + span); publish agg (own), look back
+// 64 records at a time down to the nearest inclusive one, waiting only for
+// the records up to it (an ordered lane reduction), publish [0, b] and return
+// the exclusive prefix.  Every block of the small k_fs_scan grid is resident,
+// so the records waited on are being computed.
+__device__ __forceinline__ SpRec sp_lookback(const SpRec &agg, uint32_t b, uint32_t nrec, uint32_t span,
+                                             uint64_t *lbw) {
+    const uint32_t l = threadIdx.x & 63;
+    const uint64_t ns = nrec;
+    if (l == 0) sp_put(lbw, ns, b, agg, b ? 1u : 2u);
+    SpRec P;
+    P.nf = P.nl = P.up = 0;
+    P.E = P.X = 0;
+    P.fl = kSpEmpty;
+    if (b) {
+        SpRec acc = P;
+        uint32_t acc_first = b;   // (records)
+        int64_t p0 = (int64_t)b - 1;
+        for (;;) {
+            const int64_t p = p0 - (int64_t)l;
+            uint64_t v[5] = {0, 0, 0, 0, 0};
+            uint64_t im;
+            for (;;) {
+                bool ready = true;
+                if (p >= 0) {
+#pragma unroll
+                    for (int k = 0; k < 5; ++k)
+                        v[k] = __hip_atomic_load(lbw + k * ns + (uint64_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t f = v[0] >> 62;
+                    ready = f != 0;
+#pragma unroll
+                    for (int k = 1; k < 5; ++k) ready = ready && (v[k] >> 62) == f;
+                }
+                const uint64_t rm = __ballot(ready);
+                im = __ballot(ready && p >= 0 && (v[0] >> 62) == 2);
+                const uint64_t below = ~rm ? (1ull << __builtin_ctzll(~rm)) - 1ull : ~0ull;   // the ready prefix
+                if ((im & below) || !~rm) {
+                    im &= below;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            const uint32_t lim = im ? (uint32_t)__builtin_ctzll(im) : (uint32_t)(p0 < 63 ? p0 : 63);
+            constexpr uint64_t kV = (1ull << 62) - 1;
+            SpRec r;
+            r.X = (uint32_t)v[0];
+            r.fl = p >= 0 ? (uint32_t)(v[0] >> 32) & 31u : kSpEmpty;
+            r.nf = v[1] & kV;
+            r.nl = v[2] & kV;
+            r.up = v[3] & kV;
+            r.E = (uint32_t)v[4];
+            for (uint32_t d = 1; d < 64; d <<= 1) {   // lane i: records [p0 - min(i + 2d - 1, lim), p0 - i]
+                const SpRec o = sp_shfl_rec(r, (l + d) & 63u);
+                if (l + d <= lim) r = sp_combine(o, r, (uint32_t)(p0 - (int64_t)(l + d - 1)) * span);
+            }
+            const SpRec bb = sp_shfl_rec(r, 0);   // records [p0 - lim, p0]
+            acc = sp_combine(bb, acc, acc_first * span);
+            acc_first = (uint32_t)(p0 - (int64_t)lim);
+            if (im) break;
+            p0 -= 64;
+        }
+        P = acc;
+        if (l == 0) sp_put(lbw, ns, b, sp_combine(P, agg, b * span), 2u);
+    }
+    return P;
+}
+
+// The super-chunk records after the walk: a thread per super-chunk (its
+// FrameSuper and sx pair), an ordered block scan, the look-back over blocks,
+// then bases[s] (the exclusive prefix) and, from the last super-chunk, the
+// walk's results (res[7] = 2: some entry check failed, k_fs_fix next).
+constexpr uint32_t kSpScan = 256;
+__global__ __launch_bounds__(kSpScan) void k_fs_scan(uint32_t Q, uint32_t nsup, const FrameSuper *sup,
+                                                      const uint32_t *sx, uint64_t *lbw, FrameBase *bases,
+                                                      uint64_t *res) {
+    __shared__ SpRec wt[kSpScan / 64];
+    __shared__ SpRec bp;
+    const uint32_t tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+    const uint32_t b = blockIdx.x, nrec = gridDim.x;
+    const uint32_t s = b * kSpScan + tid;
+    SpRec r;
+    r.fl = kSpEmpty;
+    r.nf = r.nl = r.up = 0;
+    r.E = r.X = 0;
+    if (s < nsup) {
+        const FrameSuper v = sup[s];
+        const uint2 e = ((const uint2 *)sx)[s];
+        r.nf = v.nfrag;
+        r.nl = v.nlast;
+        r.up = v.upto_ll;
+        r.E = e.x;
+        r.X = e.y;
+        r.fl = (v.tail & kSpTail) | (v.has_ll ? kSpHas : 0u) | (e.y >= kFUnal || e.y >= Q ? kSpTerm : 0u);
+    }
+    // inclusive scan in the wave (lane i: supers [s - 2d + 1, s] after step d)
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const SpRec o = sp_shfl_rec(r, (l - d) & 63u);
+        if (l >= d) r = sp_combine(o, r, s - d + 1);
+    }
+    if (l == 63) wt[wv] = r;
+    __syncthreads();
+    SpRec wp;   // waves before this one
+    wp.fl = kSpEmpty;
+    wp.nf = wp.nl = wp.up = 0;
+    wp.E = wp.X = 0;
+    for (uint32_t k = 0; k < wv; ++k) wp = sp_combine(wp, wt[k], b * kSpScan + 64 * k);
+    const SpRec incl = sp_combine(wp, r, b * kSpScan + 64 * wv);   // supers [b kSpScan, s]
+    if (tid == kSpScan - 1) bp = incl;                              // the block's aggregate
+    __syncthreads();
+    if (wv == 0) {
+        const SpRec P = sp_lookback(bp, b, nrec, kSpScan, lbw);
+        if (l == 0) wt[0] = P;   // (wave 0 read wt[*] above; the barrier below orders the rest)
+    }
+    __syncthreads();
+    const SpRec P = wt[0];
+    // exclusive prefix of s: P + the in-block inclusive of s - 1
+    SpRec ex = sp_shfl_rec(incl, (l - 1) & 63u);
+    if (l == 0) ex = wp;
+    const SpRec E = sp_combine(P, ex, b * kSpScan);
+    if (s < nsup) {
+        FrameBase fb;
+        const uint32_t pt = E.fl & kSpTail;
+        fb.frag = E.nf;
+        fb.last = E.nl;
+        fb.prev_tail = (E.fl & kSpEmpty) || pt == 2u ? 1u : pt;   // fragment 0 starts a message
+        fb.rsv = 0;
+        bases[s] = fb;
+    }
+    if (s + 1 == nsup) {
+        const SpRec I = sp_combine(P, incl, b * kSpScan);
+        res[0] = I.X;          // >= Q, kFStop or kFUnal (the byte walk next)
+        res[1] = I.up;         // complete fragments: through the last LAST one
+        res[4] = I.nl;         // complete messages
+        res[5] = I.up;
+        res[3] = 0;
+        res[6] = 0;
+        res[7] = (I.fl & kSpFail) ? 2u : 0u;
     }
 }
 
+// Block = one wave = one super-chunk.
 __global__ __launch_bounds__(64) void k_fs_walk(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
                                                 FrameSub *sub, uint32_t *fbits, uint32_t *lbits, FrameSuper *sup,
                                                 uint32_t *sx) {
     __shared__ SpLds sp;
-    fs_super(w, Q, tb, blockIdx.x, false, 0u, sub, fbits, lbits, sup, sx, &sp);
+    (void)fs_super(w, Q, tb, blockIdx.x, false, 0u, sub, fbits, lbits, sup, sx, &sp);
 }
 
 // One block: check every super-chunk's entry guess against its predecessor's
 // exit, walk the first wrong one again from its true entry (wave 0), repeat;
 // then the bases over the super-chunks the real chain reaches (res[0] = the
-// chain's end: >= Q, kFStop or kFUnal).  res[7] = 1: gave up.
+// chain's end: >= Q, kFStop or kFUnal).  res[7] = re-walks << 8 | 1 when it
+// gave up.
 __global__ __launch_bounds__(1024) void k_fs_fix(const uint32_t *__restrict__ w, uint32_t Q, uint32_t tb,
                                                  uint32_t nsup, FrameSub *sub, uint32_t *fbits, uint32_t *lbits,
                                                  FrameSuper *sup, uint32_t *sx, FrameBase *bases, uint64_t *res) {
@@ -1392,21 +1621,37 @@ __global__ __launch_bounds__(1024) void k_fs_fix(const uint32_t *__restrict__ w,
     const uint32_t tid = threadIdx.x;
     bool done = false;
     uint32_t term = ~0u;
-    for (int it = 0;; ++it) {
+    int it = 0;
+    for (;; ++it) {
         if (tid == 0) {
             s_fail = ~0u;
             s_term = ~0u;
         }
         __syncthreads();
         uint32_t f = ~0u, t = ~0u;
-        for (uint32_t s = 1 + tid; s < nsup; s += 1024) {
-            const uint32_t E1 = sx[2 * (uint64_t)(s - 1)], L = sx[2 * (uint64_t)(s - 1) + 1];
-            if (E1 == kFNone) continue;   // s - 1 has no chain: if the chain reaches it, s - 1 fails
-            if (L >= kFUnal || L >= Q) {  // the chain ends in s - 1
+        // thread tid checks super-chunks [s0, s1) (the bases' runs below):
+        // super-chunk s against s - 1, the pairs loaded at once (uint2: entry, exit)
+        const uint32_t R = (nsup + 1023) / 1024, s0 = tid * R, s1 = min(s0 + R, nsup);
+        auto check = [&](uint32_t s, uint2 p, uint32_t Es) {   // p = (entry, exit) of s - 1
+            if (p.x == kFNone) return;              // s - 1 has no chain: if the chain reaches it, s - 1 fails
+            if (p.y >= kFUnal || p.y >= Q) {        // the chain ends in s - 1
                 t = min(t, s);
-                continue;
+                return;
             }
-            if (!(L < s * kFSuper + kFSuper && sx[2 * (uint64_t)s] == L)) f = min(f, s);
+            if (!(p.y < s * kFSuper + kFSuper && Es == p.y)) f = min(f, s);
+        };
+        const uint2 *px = (const uint2 *)sx;
+        constexpr uint32_t kRun = 12;
+        if (R <= kRun) {
+            uint2 pr[kRun + 1];
+#pragma unroll
+            for (uint32_t i = 0; i <= kRun; ++i)
+                if (s0 + i >= 1 && s0 + i - 1 < s1 && i <= R) pr[i] = px[s0 + i - 1];
+#pragma unroll
+            for (uint32_t i = 1; i <= kRun; ++i)
+                if (s0 + i - 1 < s1 && s0 + i - 1 >= 1) check(s0 + i - 1, pr[i - 1], pr[i].x);
+        } else {
+            for (uint32_t s = max(s0, 1u); s < s1; ++s) check(s, px[s - 1], px[s].x);
         }
         f = fr_wave_min(f);
         t = fr_wave_min(t);
@@ -1422,18 +1667,18 @@ __global__ __launch_bounds__(1024) void k_fs_fix(const uint32_t *__restrict__ w,
             break;
         }
         if (it == kSpFixIters) break;
-        if (tid < 64) fs_super(w, Q, tb, F, true, sx[2 * (uint64_t)(F - 1) + 1], sub, fbits, lbits, sup, sx, &sp);
+        if (tid < 64) (void)fs_super(w, Q, tb, F, true, sx[2 * (uint64_t)(F - 1) + 1], sub, fbits, lbits, sup, sx, &sp);
         __threadfence_block();
         __syncthreads();
     }
     if (!done) {
-        if (tid == 0) res[7] = 1;
+        if (tid == 0) res[7] = (uint64_t)it << 8 | 1u;
         return;
     }
     const uint32_t nv = min(term, nsup);
     if (tid == 0) {
         res[0] = sx[2 * (uint64_t)(nv - 1) + 1];
-        res[7] = 0;
+        res[7] = (uint64_t)it << 8;
     }
     __syncthreads();
     if (sx[2 * (uint64_t)(nv - 1) + 1] == kFUnal) return;   // the byte walk next (block-uniform)
@@ -1481,15 +1726,23 @@ int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, ui
 }
 
 int frame_spec(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-               uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream) {
+               uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, bool fix, void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t *w = (const uint32_t *)in;
     const uint32_t Q = frame_positions(len, 4), tb = (uint32_t)(len & 3);
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
-    hipLaunchKernelGGL(k_fs_walk, dim3((uint32_t)nsup), dim3(64), 0, st, w, Q, tb, ws.sub, ws.fbits, ws.lbits,
-                       ws.sup, ws.sx);
-    hipLaunchKernelGGL(k_fs_fix, dim3(1), dim3(1024), 0, st, w, Q, tb, (uint32_t)nsup, ws.sub, ws.fbits, ws.lbits,
-                       ws.sup, ws.sx, ws.bases, ws.res);
+    if (fix) {   // the walk's checks failed: settle the stream, bases again
+        hipLaunchKernelGGL(k_fs_fix, dim3(1), dim3(1024), 0, st, w, Q, tb, (uint32_t)nsup, ws.sub, ws.fbits,
+                           ws.lbits, ws.sup, ws.sx, ws.bases, ws.res);
+    } else {
+        const uint32_t nrec = (uint32_t)((nsup + kSpScan - 1) / kSpScan);
+        const hipError_t e = hipMemsetAsync(ws.lbw, 0, 8 * 5 * (size_t)nrec, st);
+        if (e != hipSuccess) return (int)e;
+        hipLaunchKernelGGL(k_fs_walk, dim3((uint32_t)nsup), dim3(64), 0, st, w, Q, tb, ws.sub, ws.fbits, ws.lbits,
+                           ws.sup, ws.sx);
+        hipLaunchKernelGGL(k_fs_scan, dim3(nrec), dim3(kSpScan), 0, st, Q, (uint32_t)nsup, ws.sup, ws.sx, ws.lbw,
+                           ws.bases, ws.res);
+    }
     uint32_t per = emit_per > 0 ? (uint32_t)emit_per : 1u;
     while (per > 1 && nsub / per < 64) per >>= 1;
     hipLaunchKernelGGL(k_fr_emit<4>, dim3((uint32_t)((nsub + per - 1) / per)), dim3(128), 0, st, w, Q, ws.sub,

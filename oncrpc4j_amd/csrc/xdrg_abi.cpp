@@ -292,6 +292,7 @@ struct xdrg_ctx {
     size_t rx_bytes = 0;
     uint64_t frame_spec_calls = 0;     // speculative word walks (xdrg_internal_stat 1)
     uint64_t frame_spec_gave_up = 0;   // ... of them walked again by the exact kernels (key 2)
+    uint64_t frame_spec_rewalks = 0;   // super-chunks k_fs_fix walked again (key 3)
 };
 
 static int hip_fail(xdrg_ctx *c, hipError_t e, const char *what) {
@@ -411,12 +412,14 @@ extern "C" int xdrg_internal_tune(xdrg_ctx *c, int key, long long value) {
 }
 
 // Not part of include/xdrg.h: counters for the parity tests (1: speculative
-// frame walks, 2: those that gave up and ran the exact kernels).
+// frame walks, 2: those that gave up and ran the exact kernels, 3: super-
+// chunks their fix-up walked again).
 extern "C" long long xdrg_internal_stat(xdrg_ctx *c, int key) {
     if (!c) return -1;
     switch (key) {
     case 1: return (long long)c->frame_spec_calls;
     case 2: return (long long)c->frame_spec_gave_up;
+    case 3: return (long long)c->frame_spec_rewalks;
     default: return -1;
     }
 }
@@ -1995,7 +1998,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     const size_t o_ex = take(2 * Q), o_al = take(4 * (size_t)kFChunk * nsub), o_ac = take(4 * nsub), o_se = take(4 * nsup), o_wt = take(4 * 256 * nsup), o_gs = take(4 * 256 * (nsup + 64)), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
                  o_fb = take(512 * nsub), o_lb = take(512 * nsub), o_su = take(sizeof(FrameSuper) * nsup),
-                 o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_sx = take(8 * nsup), o_re = take(64);
+                 o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_sx = take(8 * nsup), o_lw = take(8 * (5 * nsup + 1)), o_re = take(64);
     if (off > c->fws_bytes) {
         if (c->d_fws) {
             HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2022,6 +2025,7 @@ static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
     ws.bases = (FrameBase *)(b + o_ba);
     ws.frag_pos = (uint64_t *)(b + o_fp);
     ws.sx = (uint32_t *)(b + o_sx);
+    ws.lbw = (uint64_t *)(b + o_lw);
     ws.res = (uint64_t *)(b + o_re);
     return XDRG_OK;
 }
@@ -2057,10 +2061,17 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
         if (!exact) {   // the speculative walk; the exact kernels when it gives up (res[7])
             ++c->frame_spec_calls;
             HIPCHK(c, (hipError_t)frame_spec(in, len, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
-                                             c->tune.emit_per, stride, c->stream));
+                                             c->tune.emit_per, stride, false, c->stream));
             HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 64, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
-            if (c->h_stat[2 + 7]) {
+            if ((c->h_stat[2 + 7] & 2) && c->h_stat[2] != kFUnal) {   // a failed entry check: re-walks
+                HIPCHK(c, (hipError_t)frame_spec(in, len, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
+                                                 c->tune.emit_per, stride, true, c->stream));
+                HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 64, hipMemcpyDeviceToHost, c->stream));
+                HIPCHK(c, hipStreamSynchronize(c->stream));
+            }
+            c->frame_spec_rewalks += c->h_stat[2 + 7] >> 8;
+            if (c->h_stat[2 + 7] & 1) {
                 ++c->frame_spec_gave_up;
                 exact = true;
                 HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));

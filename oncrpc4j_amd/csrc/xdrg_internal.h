@@ -298,10 +298,12 @@ struct FrameWs {                              // device workspace of one walk
                                               // (xdrg_deframe; one entry past the last copied fragment)
     uint32_t *sx;                             // [nsup][2] speculative walk: each super-chunk's entry
                                               // guess and exit
+    uint64_t *lbw;                            // [5 nsup + 1] its look-back words and block ticket
     uint64_t *res;                            // [0] chain terminal [1] complete fragments (through the
                                               // last LAST one) [3] consumed bytes [4] complete messages
                                               // [5] fragments of the first `cap` messages [6] off-stride
-                                              // [7] 1: the speculative walk gave up
+                                              // [7] bit 0: the speculative walk gave up, bit 1:
+                                              // its checks failed (k_fs_fix next), bits 8+: re-walks
 };
 // Walk positions of a len-byte stream: B = 4 words (len / 4), B = 1 bytes a
 // whole mark can start at (len - 3).
@@ -320,11 +322,12 @@ int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, ui
                    uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream);
 int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
                  uint64_t *msg_offsets, void *stream);
-// The speculative word walk (k_fs_walk, k_fs_fix, k_fr_emit): the same
-// results as frame_parallel(B = 4) unless res[7] = 1 (it gave up; nothing
-// was emitted), then frame_parallel runs.
+// The speculative word walk (k_fs_walk + look-back, k_fr_emit): the same
+// results as frame_parallel(B = 4) unless res[7] & 2 (a failed check:
+// nothing emitted; call again with fix = true, k_fs_fix + k_fr_emit) or,
+// after the fix, res[7] & 1 (it gave up; frame_parallel runs).
 int frame_spec(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-               uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream);
+               uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, bool fix, void *stream);
 // Bodies of the first nf fragments into payload (marks stripped).
 int frame_copy(const uint8_t *in, const FrameWs &ws, uint64_t nf, uint64_t payload_bytes, uint8_t *payload,
                void *stream);

@@ -366,7 +366,8 @@ class Context:
 
     def internal_stat(self, key):
         """Internal counters (xdrg_internal_stat: 1 speculative frame walks,
-        2 of them walked again by the exact kernels).  Not part of the drop-in
+        2 of them walked again by the exact kernels, 3 super-chunks re-walked
+        by their fix-up).  Not part of the drop-in
         boundary."""
         return int(lib().xdrg_internal_stat(self._h, int(key)))
 

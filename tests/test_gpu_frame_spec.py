@@ -156,6 +156,18 @@ def test_fragments_longer_than_a_super_chunk(gpu_ctx):
     assert k == 3 * 9000 + 3
 
 
+def test_one_skip_is_rewalked(gpu_ctx):
+    """A 300 KiB fragment: the super-chunk it covers fails its entry check and
+    is walked again (k_fs_fix), without the exact kernels."""
+    rng = np.random.default_rng(17)
+    small = cfg2_stream(20000, 18)
+    big = oracle.fragment(rng.integers(0, 256, 300 << 10, dtype=np.uint8).tobytes(), 1 << 30)
+    w0 = gpu_ctx.internal_stat(3)
+    (k, g) = gave_up(gpu_ctx, lambda: check(gpu_ctx, small + big + small))
+    assert k == 40001 and g == 0
+    assert gpu_ctx.internal_stat(3) > w0
+
+
 def test_unaligned_mark_on_the_chain(gpu_ctx):
     """A 6-byte fragment in the middle: the word walk meets a size % 4 != 0
     mark and the byte walk takes over, with the same results."""
