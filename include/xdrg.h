@@ -436,8 +436,10 @@ int  xdrg_deframe(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *paylo
  * call GARBAGE_ARGS, RpcDispatcher.java:126-131, and the caller resumes at
  * *consumed) — except XDRG_E_CAPACITY, which delivers up to it (*n_msgs =
  * first_bad) so the caller can retry it with larger columns.  Host staging
- * of a schema with repeated groups walks, deframes and then decodes the
- * complete messages' bodies (three staged passes; the same results).      */
+ * streams every schema through the staging windows in one crossing, a
+ * window's group element rows placed by the previous window's totals —
+ * except a schema whose group elements hold inner groups, which is walked,
+ * deframed and then decoded (three staged passes; the same results).      */
 int  xdrg_frame_scan_ex(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint64_t *msg_offsets,
                         uint64_t cap, uint64_t *n_msgs, uint64_t *consumed, uint32_t flags);
 int  xdrg_deframe_ex(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *payload,
@@ -466,7 +468,12 @@ int  xdrg_receive_batch(xdrg_ctx *ctx, const xdrg_schema *schema, const uint8_t 
  * stream in[i] resident on its device (in_len bytes; rec_offsets[i] = the
  * stream's n_total + 1 record offsets, or NULL for fixed-size schemas) into
  * its shard's columns cols[i].  *first_bad / *err (host) = the reference's
- * first error over the whole batch: the smallest failing record.          */
+ * first error over the whole batch: the smallest failing record.
+ *
+ * Any schema shards, repeated groups and conditional members included: a
+ * shard's columns are the columns one context would hold for its records
+ * alone (group element rows and member offsets counted from the shard's
+ * first record), as xdrg_encode_batch / xdrg_decode_batch take them.      */
 int  xdrg_encode_batch_multi(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *schema,
                              const xdrg_column *const *cols, const uint64_t *counts,
                              uint8_t *const *out, uint64_t out_cap, uint64_t *const *rec_offsets,

@@ -48,6 +48,11 @@
 namespace xdrg {
 
 __device__ __forceinline__ uint32_t fr_bswap(uint32_t x) { return __builtin_bswap32(x); }
+// Order one wave's LDS accesses across lanes (a one-wave block needs no barrier).
+__device__ __forceinline__ void sp_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
 
 // Positions: the walk runs in word mode (B = 4: position q = stream word q,
 // Q = len / 4 words, tb = len % 4 trailing bytes) and, when the real chain
@@ -967,6 +972,128 @@ __global__ __launch_bounds__(128) void k_fr_emit(const uint32_t *__restrict__ w,
                        stride, so, wsum, wtail, wlo, whi);
 }
 
+// k_fr_emit_w: the same results from one wave per sub-chunk, lane l owning
+// bitmap words 2 l and 2 l + 1 (positions 64 l .. 64 l + 63): no cross-wave
+// exchange, and the per-fragment loop in 32-bit sub-chunk-relative counters
+// (fragment and message indices relative to fb0 / lb0, limits clamped).
+__device__ __forceinline__ uint32_t fr_wave_incl_max(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t a = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v = max(v, a);
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t fr_rel(uint64_t x, uint64_t base) {   // x - base clamped to [0, 2^32 - 1]
+    return x <= base ? 0u : x - base >= 0xffffffffull ? 0xffffffffu : (uint32_t)(x - base);
+}
+template <int B>
+__device__ __forceinline__ void fr_emit_wave(const uint32_t *__restrict__ w, uint32_t Q, const FrameSub *sub,
+                                             const FrameBase *bases, const uint64_t *fb64, const uint64_t *lb64,
+                                             uint64_t cap, int stream_offsets, uint64_t *msg_offsets,
+                                             uint64_t *frag_pos, uint64_t *res, uint64_t F, uint64_t M, uint64_t k,
+                                             uint64_t stride, uint16_t *so) {
+    const uint32_t l = threadIdx.x & 63;
+    const uint64_t s = k / (kFSuper / kFChunk);
+    const FrameSub info = sub[k];
+    const FrameBase b = bases[s];
+    const uint64_t Fl = fb64[k * 64 + l], Ll = lb64[k * 64 + l];
+    if (k * kFChunk >= Q || !info.nfrag) return;
+    const uint64_t fb0 = b.frag + info.pre_frag, lb0 = b.last + info.pre_last;
+    if (fb0 >= F) return;   // past the last complete message
+    const uint32_t in_tail = info.prev_tail != 2u ? info.prev_tail : b.prev_tail;
+    const uint32_t pf = __popcll(Fl), pl = __popcll(Ll);
+    uint32_t rf = fr_wave_incl(pf) - pf, rm = fr_wave_incl(pl) - pl;   // relative f, m of the lane's first
+    // the LAST flag of the fragment before the lane's first: the latest lane below with one
+    const uint32_t tag = Fl ? 1u + (l << 1 | (uint32_t)((Ll >> (63 - __builtin_clzll(Fl))) & 1u)) : 0u;
+    uint32_t tex = __shfl_up(fr_wave_incl_max(tag), 1, 64);
+    if (l == 0) tex = 0;
+    bool prev_last = tex ? ((tex - 1) & 1u) != 0 : in_tail != 0;
+    const uint64_t mlim = min(M, cap + 1);           // msg_offsets[m] is written for m < mlim
+    const uint32_t rF = fr_rel(F, fb0), rmlim = fr_rel(mlim, lb0);
+    const bool capin = cap >= lb0;                    // m == cap / m <= cap possible in this sub-chunk
+    const uint32_t rcap = capin ? fr_rel(cap, lb0) : 0u;
+    const bool first0 = fb0 == 0;
+    const uint64_t base = k * kFChunk;
+    uint32_t klo = ~0u, khi = 0;
+    for (uint64_t bits = Fl; bits; bits &= bits - 1) {
+        if (rf >= rF) break;
+        const uint32_t bt = (uint32_t)__builtin_ctzll(bits);
+        const uint32_t lp = 64 * l + bt;
+        const bool last = (Ll >> bt) & 1ull;
+        const bool first = prev_last || (first0 && rf == 0);
+        if (first && rm < rmlim) {   // payload offsets: fragments tile the stream (p - 4 f)
+            so[rm] = (uint16_t)(stream_offsets ? B * lp : B * lp - 4 * rf);
+            klo = min(klo, rm);
+            khi = max(khi, rm + 1);
+        }
+        if (capin && rm <= rcap) {
+            const uint64_t p = B * (base + lp);   // stream byte of the mark
+            if (first && rm == rcap) { res[3] = p; res[5] = fb0 + rf; }   // handleRead's split point (:57-60)
+            if (frag_pos) frag_pos[fb0 + rf] = p;
+        }
+        if (rf + 1 == rF) {   // the last LAST fragment closes the last complete message
+            const uint64_t p = B * (base + lp), f = fb0 + rf, m = lb0 + rm;
+            const uint64_t size = fr_bswap(fr_at<B>(w, Q, (uint32_t)(base + lp))) & kSizeMask;
+            if (m + 1 <= cap) msg_offsets[m + 1] = stream_offsets ? p + 4 + size : p - 4 * f + size;
+            if (M <= cap) {
+                res[3] = p + 4 + size;
+                if (frag_pos) frag_pos[F] = p + 4 + size;
+            }
+        }
+        prev_last = last;
+        rm += last ? 1u : 0u;
+        ++rf;
+    }
+    klo = fr_wave_min(klo);
+    khi = fr_wave_max(khi);
+    sp_fence();
+    const uint64_t vbase = stream_offsets ? B * base : B * base - 4 * fb0;
+    bool off_stride = false;   // stride > 0: message m should start at m * stride (the receive's fixed-size decode)
+    for (uint32_t kk = klo + l; kk < khi; kk += 64) {
+        const uint64_t o = vbase + so[kk];
+        msg_offsets[lb0 + kk] = o;
+        off_stride |= stride && o != (lb0 + kk) * stride;
+    }
+    if (__ballot(off_stride) && l == 0) atomicOr((unsigned long long *)(res + 6), 1ull);
+    sp_fence();   // so free for the block's next sub-chunk
+}
+
+template <int B>
+__global__ __launch_bounds__(64) void k_fr_emit_w(const uint32_t *__restrict__ w, uint32_t Q, const FrameSub *sub,
+                                                  const FrameBase *bases, const uint32_t *fbits,
+                                                  const uint32_t *lbits, uint64_t cap, int stream_offsets,
+                                                  uint64_t *msg_offsets, uint64_t *frag_pos, uint64_t *res,
+                                                  uint64_t nsub, uint32_t per, uint64_t stride) {
+    __shared__ uint16_t so[kFChunk + 1];           // staged message offsets
+    const uint64_t r0 = res[0], F = res[1], M = res[4];
+    if (r0 == kFUnal || (res[7] & 3)) return;
+    const uint64_t k0 = (uint64_t)blockIdx.x * per;
+    const uint64_t k1 = min(k0 + per, nsub);
+    for (uint64_t k = k0; k < k1; ++k)
+        fr_emit_wave<B>(w, Q, sub, bases, (const uint64_t *)fbits, (const uint64_t *)lbits, cap, stream_offsets,
+                        msg_offsets, frag_pos, res, F, M, k, stride, so);
+}
+// Emit with the context's variant (tuning key 48: 1 a wave per sub-chunk, 0 k_fr_emit).
+template <int B>
+static void fr_emit_launch(const uint32_t *w, uint32_t Q, const FrameWs &ws, uint64_t cap, bool stream_offsets,
+                           uint64_t *msg_offsets, bool frag_list, int emit_per, int emit_wave, uint64_t stride,
+                           uint64_t nsub, hipStream_t st) {
+    uint32_t per = emit_per > 0 ? (uint32_t)emit_per : 1u;
+    const uint64_t minb = emit_wave ? 256 : 64;   // keep the grid wide for short streams
+    while (per > 1 && nsub / per < minb) per >>= 1;
+    const dim3 grid((uint32_t)((nsub + per - 1) / per));
+    if (emit_wave)
+        hipLaunchKernelGGL(k_fr_emit_w<B>, grid, dim3(64), 0, st, w, Q, ws.sub, ws.bases, ws.fbits, ws.lbits, cap,
+                           stream_offsets ? 1 : 0, msg_offsets, frag_list ? ws.frag_pos : nullptr, ws.res, nsub, per,
+                           stream_offsets ? stride : 0ull);
+    else
+        hipLaunchKernelGGL(k_fr_emit<B>, grid, dim3(128), 0, st, w, Q, ws.sub, ws.bases, ws.fbits, ws.lbits, cap,
+                           stream_offsets ? 1 : 0, msg_offsets, frag_list ? ws.frag_pos : nullptr, ws.res, nsub, per,
+                           stream_offsets ? stride : 0ull);
+}
+
 // ---------------------------------------------------------------------------
 // Exact serial walk (any fragment sizes): the fallback.  Same results as the
 // parallel path (fragment list with its end entry, message offsets).
@@ -1082,10 +1209,6 @@ __device__ __forceinline__ uint32_t sp_idx(uint32_t q) { return (q >> 6) * kSpRo
 __device__ __forceinline__ uint64_t sp_shfl64(uint64_t v, uint32_t src) {
     const uint32_t lo = __shfl((uint32_t)v, (int)src, 64), hi = __shfl((uint32_t)(v >> 32), (int)src, 64);
     return (uint64_t)hi << 32 | lo;
-}
-__device__ __forceinline__ void sp_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
 }
 // Loads of a sub-chunk: word base + 64 k + l into y[k] (k < 64), one
 // coalesced 256-byte dword load per k, so that lane l holds word l of every
@@ -1688,7 +1811,8 @@ __global__ __launch_bounds__(1024) void k_fs_fix(const uint32_t *__restrict__ w,
 // ---- launchers -------------------------------------------------------------------
 template <int B>
 static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                        uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, hipStream_t st) {
+                        uint64_t *msg_offsets, bool frag_list, int emit_per, int emit_wave, uint64_t stride,
+                        hipStream_t st) {
     const uint32_t *w = (const uint32_t *)in;
     const uint32_t Q = frame_positions(len, B), tb = B == 4 ? (uint32_t)(len & 3) : 0u;
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper, nsub = nsup * (kFSuper / kFChunk);
@@ -1707,26 +1831,24 @@ static int frame_launch(const uint8_t *in, uint64_t len, const FrameWs &ws, uint
     hipLaunchKernelGGL(k_fr_mark<B>, dim3((uint32_t)nsup), dim3(256), 0, st, w, Q, tb, ws.sentry, ws.res, ws.alist,
                        ws.acnt, ws.sub, ws.fbits, ws.lbits, ws.sup);
     hipLaunchKernelGGL(k_fr_bases, dim3(1), dim3(1024), 0, st, ws.sup, nsup, ws.bases, ws.res);
-    // several sub-chunks per block, while the grid keeps >= 64 blocks (short
-    // streams keep their parallelism)
-    uint32_t per = emit_per > 0 ? (uint32_t)emit_per : 1u;
-    while (per > 1 && nsub / per < 64) per >>= 1;
-    hipLaunchKernelGGL(k_fr_emit<B>, dim3((uint32_t)((nsub + per - 1) / per)), dim3(128), 0, st, w, Q, ws.sub,
-                       ws.bases, ws.fbits, ws.lbits, cap, stream_offsets ? 1 : 0, msg_offsets,
-                       frag_list ? ws.frag_pos : nullptr, ws.res, (uint64_t)nsub, per, stream_offsets ? stride : 0ull);
+    // several sub-chunks per block, while the grid stays wide (short streams
+    // keep their parallelism)
+    fr_emit_launch<B>(w, Q, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per, emit_wave, stride, nsub, st);
     return (int)hipGetLastError();
 }
 
 int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                   uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream) {
-    return B == 1 ? frame_launch<1>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per, stride,
-                                    (hipStream_t)stream)
-                  : frame_launch<4>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per, stride,
-                                    (hipStream_t)stream);
+                   uint64_t *msg_offsets, bool frag_list, int emit_per, int emit_wave, uint64_t stride,
+                   void *stream) {
+    return B == 1 ? frame_launch<1>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per, emit_wave,
+                                    stride, (hipStream_t)stream)
+                  : frame_launch<4>(in, len, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per, emit_wave,
+                                    stride, (hipStream_t)stream);
 }
 
 int frame_spec(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-               uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, bool fix, void *stream) {
+               uint64_t *msg_offsets, bool frag_list, int emit_per, int emit_wave, uint64_t stride, bool fix,
+               void *stream) {
     const hipStream_t st = (hipStream_t)stream;
     const uint32_t *w = (const uint32_t *)in;
     const uint32_t Q = frame_positions(len, 4), tb = (uint32_t)(len & 3);
@@ -1743,11 +1865,7 @@ int frame_spec(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap,
         hipLaunchKernelGGL(k_fs_scan, dim3(nrec), dim3(kSpScan), 0, st, Q, (uint32_t)nsup, ws.sup, ws.sx, ws.lbw,
                            ws.bases, ws.res);
     }
-    uint32_t per = emit_per > 0 ? (uint32_t)emit_per : 1u;
-    while (per > 1 && nsub / per < 64) per >>= 1;
-    hipLaunchKernelGGL(k_fr_emit<4>, dim3((uint32_t)((nsub + per - 1) / per)), dim3(128), 0, st, w, Q, ws.sub,
-                       ws.bases, ws.fbits, ws.lbits, cap, stream_offsets ? 1 : 0, msg_offsets,
-                       frag_list ? ws.frag_pos : nullptr, ws.res, (uint64_t)nsub, per, stream_offsets ? stride : 0ull);
+    fr_emit_launch<4>(w, Q, ws, cap, stream_offsets, msg_offsets, frag_list, emit_per, emit_wave, stride, nsub, st);
     return (int)hipGetLastError();
 }
 

@@ -398,6 +398,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 44: if (!in(0, 1)) return -1; t.grp_dec_emap = (int32_t)v; return 0;
     case 45: if (!in(0, 1)) return -1; t.grp_enc_img_nest = (int32_t)v; return 0;
     case 47: if (!in(0, 1)) return -1; t.frame_spec = (int32_t)v; return 0;
+    case 48: if (!in(0, 1)) return -1; t.emit_wave = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -2061,12 +2062,12 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
         if (!exact) {   // the speculative walk; the exact kernels when it gives up (res[7])
             ++c->frame_spec_calls;
             HIPCHK(c, (hipError_t)frame_spec(in, len, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
-                                             c->tune.emit_per, stride, false, c->stream));
+                                             c->tune.emit_per, c->tune.emit_wave, stride, false, c->stream));
             HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 64, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
             if ((c->h_stat[2 + 7] & 2) && c->h_stat[2] != kFUnal) {   // a failed entry check: re-walks
                 HIPCHK(c, (hipError_t)frame_spec(in, len, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
-                                                 c->tune.emit_per, stride, true, c->stream));
+                                                 c->tune.emit_per, c->tune.emit_wave, stride, true, c->stream));
                 HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 64, hipMemcpyDeviceToHost, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
             }
@@ -2079,7 +2080,7 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
         }
         if (exact) {
             HIPCHK(c, (hipError_t)frame_parallel(in, len, 4, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
-                                                 c->tune.emit_per, stride, c->stream));
+                                                 c->tune.emit_per, c->tune.emit_wave, stride, c->stream));
             HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 56, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
         }
@@ -2089,7 +2090,8 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
                 if (rc) return rc;
                 HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));
                 HIPCHK(c, (hipError_t)frame_parallel(in, len, 1, ws, cap, stream_offsets, msg_offsets,
-                                                     !stream_offsets, c->tune.emit_per, stride, c->stream));
+                                                     !stream_offsets, c->tune.emit_per, c->tune.emit_wave, stride,
+                                                     c->stream));
                 HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, ws.res, 56, hipMemcpyDeviceToHost, c->stream));
                 HIPCHK(c, hipStreamSynchronize(c->stream));
             } else {
@@ -2405,7 +2407,6 @@ static int multi_args(xdrg_ctx *const *ctxs, uint32_t nctx, const xdrg_schema *s
         if (!ctxs[i]) return XDRG_E_INVAL;
     if (flags & ~XDRG_FRAME_RM)   // synchronous, device memory (xdrg_device_alloc / xdrg_copy for a JVM)
         return inval(ctxs[0], "multi-GPU calls take XDRG_FRAME_RM only (device memory, synchronous)");
-    if (s->ngroups) return inval(ctxs[0], "multi-GPU calls take schemas without repeated groups");
     return XDRG_OK;
 }
 
@@ -2419,6 +2420,18 @@ static int shard_size_launch(xdrg_ctx *c, const xdrg_schema *s, const xdrg_colum
         return XDRG_OK;
     }
     HIPCHK(c, hipSetDevice(c->device));
+    if (s->ngroups) {   // repeated groups: the group size pass and its scan (group_encode's first two)
+        GroupArgs g;
+        int rc = fill_group(c, s, cols, n, framed, false, g);
+        if (rc) return rc;
+        g.enc_lanes = (uint32_t)c->tune.grp_enc_lanes;
+        g.enc_split = (uint32_t)c->tune.grp_enc_split;
+        HIPCHK(c, (hipError_t)launch_group_phase(g, GRP_ENC_SIZES, c->stream));
+        HIPCHK(c, (hipError_t)launch_scan_rows(g.block_sums, g.nblocks, g.totals, 1, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_stat + 2, g.totals, 8, hipMemcpyDeviceToHost, c->stream));
+        *on_device = true;
+        return XDRG_OK;
+    }
     RecArgs a;
     int rc = fill_rec(c, s, (xdrg_column *)cols, n, framed, a);
     if (rc) return rc;

@@ -193,6 +193,7 @@ struct Tuning {
                                     // bit 0 encode, bit 1 decode (0 in block order)
     int32_t emit_per = 4;           // key 36: frame walk, sub-chunks per k_fr_emit block (at most;
                                     // halved until the grid has >= 64 blocks)
+    int32_t emit_wave = 1;          // key 48: frame walk emit: 1 a wave per sub-chunk (k_fr_emit_w), 0 k_fr_emit
     int32_t frame_spec = 1;         // key 47: word-mode frame walk: 1 the speculative walk (k_fs_*,
                                     // the exact kernels when it gives up), 0 the exact kernels only
     int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of
@@ -319,7 +320,8 @@ constexpr uint64_t kFByteMaxLen = 1ull << 31;   // byte-mode walks (positions an
 // message index x stride (xdrg_receive_batch's fixed-size decode skips its own
 // check of the offsets when none is off)
 int frame_parallel(const uint8_t *in, uint64_t len, int B, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-                   uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, void *stream);
+                   uint64_t *msg_offsets, bool frag_list, int emit_per, int emit_wave, uint64_t stride,
+                   void *stream);
 int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
                  uint64_t *msg_offsets, void *stream);
 // The speculative word walk (k_fs_walk + look-back, k_fr_emit): the same
@@ -327,7 +329,8 @@ int frame_serial(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t ca
 // nothing emitted; call again with fix = true, k_fs_fix + k_fr_emit) or,
 // after the fix, res[7] & 1 (it gave up; frame_parallel runs).
 int frame_spec(const uint8_t *in, uint64_t len, const FrameWs &ws, uint64_t cap, bool stream_offsets,
-               uint64_t *msg_offsets, bool frag_list, int emit_per, uint64_t stride, bool fix, void *stream);
+               uint64_t *msg_offsets, bool frag_list, int emit_per, int emit_wave, uint64_t stride, bool fix,
+               void *stream);
 // Bodies of the first nf fragments into payload (marks stripped).
 int frame_copy(const uint8_t *in, const FrameWs &ws, uint64_t nf, uint64_t payload_bytes, uint8_t *payload,
                void *stream);

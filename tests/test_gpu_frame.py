@@ -17,11 +17,13 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-@pytest.fixture(autouse=True, params=[1, 4, 7], ids=lambda v: f"emit{v}")
+@pytest.fixture(autouse=True, params=[(1, 1), (4, 1), (7, 1), (4, 0)], ids=lambda v: f"emit{v[0]}-{'wave' if v[1] else 'pair'}")
 def emit_per(request, gpu_ctx):
-    """Sub-chunks per k_fr_emit block (tuning key 36; 7 leaves a partial last
-    block)."""
-    gpu_ctx.tune(36, request.param)
+    """Sub-chunks per emit block (tuning key 36; 7 leaves a partial last
+    block) and the emit kernel (key 48: a wave per sub-chunk, or k_fr_emit's
+    two waves)."""
+    gpu_ctx.tune(36, request.param[0])
+    gpu_ctx.tune(48, request.param[1])
     yield request.param
     gpu_ctx.tune(0)
 
