@@ -667,6 +667,94 @@ def cpu_baseline(budget_s):
                     "the whole host"}
 
 
+def cpu_var_baseline(cfg, seconds):
+    """Oracle (oracle/xdr_oracle.c xo_encode_batch / xo_decode_batch, the
+    reference Xdr semantics) on a bounded sample of configs[2] / configs[3]:
+    one Python thread per core of the share, each encoding and decoding its
+    own slice of records of the config's shape (ctypes drops the GIL), GiB/s
+    of native + XDR bytes both ways, as the GPU line counts them."""
+    import threading
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from oncrpc4j_amd import abi
+    L = oracle.lib()
+    threads, _ = _cpu_threads()
+    n = 2048 if cfg == 3 else 65536
+    I, SC, DY = abi.T_INT, abi.K_SCALAR, abi.K_DYNAMIC
+    fields = [(I, SC, 0)] * 6 + [(abi.T_OPAQUE, DY, 0)] if cfg == 3 else \
+        [(I, SC, 0), (abi.T_STRING, DY, 0), (I, DY, 0)]
+    fa = oracle.fields_array(fields)
+
+    def make(seed):
+        rng = np.random.default_rng(0x0DCAC4E5 + 100 * cfg + seed)
+        if cfg == 3:
+            hdr = rng.integers(-2**31, 2**31 - 1, (n, 6), dtype=np.int32)
+            vals = rng.integers(0, 256, n * 4096, dtype=np.uint8)
+            offs = np.arange(0, 4096 * (n + 1), 4096, dtype=np.uint64)
+            dyn = [(vals, offs)]
+        else:
+            hdr = rng.integers(-2**31, 2**31 - 1, (n, 1), dtype=np.int32)
+            lens = rng.integers(8, 257, n)
+            so = np.zeros(n + 1, np.uint64)
+            np.cumsum(lens, out=so[1:])
+            sv = rng.integers(97, 123, int(so[-1]), dtype=np.uint8)
+            k = rng.integers(0, 17, n)
+            io = np.zeros(n + 1, np.uint64)
+            np.cumsum(k, out=io[1:])
+            iv = rng.integers(-2**31, 2**31 - 1, int(io[-1]), dtype=np.int32)
+            dyn = [(sv, so), (iv, io)]
+        nh = hdr.shape[1]
+
+        def cols(h, d):
+            arr = (abi.Column * len(fields))()
+            for j in range(nh):
+                arr[j].data = h.ctypes.data + 4 * j
+                arr[j].stride = 4 * nh
+            for j, (v, o) in enumerate(d):
+                arr[nh + j].data, arr[nh + j].offsets, arr[nh + j].cap = v.ctypes.data, o.ctypes.data, v.size
+            arr._keep = (h, d)
+            return arr
+        hb = np.zeros_like(hdr)
+        db = [(np.zeros_like(v), np.zeros_like(o)) for v, o in dyn]
+        native = hdr.nbytes + sum(int(o[-1]) * v.itemsize for v, o in dyn)
+        xcap = 2 * native + 16 * n + 4096   # >= every record's XDR bytes (pads included)
+        return cols(hdr, dyn), cols(hb, db), native, np.zeros(xcap, np.uint8), \
+            np.zeros(n + 1, np.uint64), (hdr, dyn, hb, db)
+
+    work = [make(t) for t in range(threads)]
+    done = [0] * threads
+    xbytes = [0] * threads
+
+    def run(t):
+        cin, cout, native, x, ro, _ = work[t]
+        ol = ctypes.c_uint64()
+        fb, er = ctypes.c_uint64(), ctypes.c_int()
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            rc = L.xo_encode_batch(fa, len(fields), ctypes.addressof(cin), n, x.ctypes.data, x.size, ro.ctypes.data,
+                                   0, ctypes.byref(ol))
+            rc |= L.xo_decode_batch(fa, len(fields), x.ctypes.data, ol.value, ro.ctypes.data, n,
+                                    ctypes.addressof(cout), 0, ctypes.byref(fb), ctypes.byref(er))
+            assert rc == 0
+            done[t] += 1
+            xbytes[t] = ol.value
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    assert np.array_equal(work[0][5][0], work[0][5][2]), "oracle round trip"
+    tot = sum(done[t] * 2 * (work[t][2] + xbytes[t]) for t in range(threads))
+    recs = sum(done) * n
+    return {"value": round(tot / dt / GIB, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "mrecords_per_s": round(recs / dt / 1e6, 3),
+            "sample": f"{sum(done)} x encode+decode of {n} configs[{cfg - 1}] records ({threads} threads, one "
+                      f"record slice each, oracle/xdr_oracle.c), {dt:.1f} s"}
+
+
 def _host_buffer(nbytes, register):
     """Page-aligned host buffer (anonymous mapping), optionally pinned with
     xdrg_host_register the way a JNI caller pins its pooled direct buffers."""
@@ -1060,6 +1148,9 @@ def run_rank(args):
             e, w = measure(R, args, make, cfg, framed, SIZES[cfg], args.extra_steps, 2,
                            with_gather=(cfg == 4))
             del w
+            if R.rank == 0 and R.world == 1 and cfg in (3, 4) and not framed and args.cpu_seconds > 0 \
+                    and not args.test_codec:
+                e["cpu_baseline"] = cpu_var_baseline(cfg, min(args.cpu_seconds / 3.0, 6.0))
             if R.cuda:
                 torch.cuda.empty_cache()
             extra.append(e)

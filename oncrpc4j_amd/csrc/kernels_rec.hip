@@ -1522,6 +1522,12 @@ __device__ uint32_t payload_rec_word(const RecArgs &a, uint64_t r, uint64_t o, u
     }
     uint64_t q = a.framed ? 4 : 0;   // a fixed field's word
     if (o >= fb) o -= 4 + P;
+    const uint64_t j = (o - q) >> 2;
+    if (j < a.pay_nw) {   // its direct rule (fill_rec)
+        const PayWord w = a.pw[j];
+        const uint8_t *p = w.data + (int64_t)r * w.stride + w.off;
+        return w.type == XDRG_T_OPAQUE ? load_bytes(p, w.rem) : enc_elem(w.type, p, w.half);
+    }
     for (uint32_t k = 0; k < a.nf; ++k) {
         const VField &f = a.f[k];
         if (f.kind == XDRG_K_DYNAMIC) continue;

@@ -684,6 +684,24 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
     }
     a.pay_fb += framed ? 4 : 0;   // bytes before the first dynamic field (the payload kernels' field)
     a.ncond = s->ncond;
+    // the fixed words as direct rules (VField::xbytes words of each fixed field)
+    if (!s->ncond && s->fixed_part / 4 <= (uint64_t)kPayWords) {
+        uint32_t j = 0;
+        for (size_t k = 0; k < s->f.size(); ++k) {
+            const VField &v = a.f[k];
+            if (v.kind == XDRG_K_DYNAMIC) continue;
+            for (uint32_t i = 0; i < v.xbytes / 4; ++i, ++j) {
+                PayWord &w = a.pw[j];
+                w.data = v.data;
+                w.stride = v.stride;
+                w.type = v.type;
+                w.half = v.xsz == 8 ? (uint8_t)(i & 1) : 0;
+                w.off = (uint16_t)(v.type == XDRG_T_OPAQUE ? 4 * i : v.xsz == 8 ? (i >> 1) * 8 : i * v.nsz);
+                w.rem = (uint8_t)(v.type == XDRG_T_OPAQUE ? std::min<uint32_t>(v.count - 4 * i, 4u) : 0u);
+            }
+        }
+        a.pay_nw = j;
+    }
     for (size_t i = 0; i < s->cvals.size(); ++i) a.cvals[i] = s->cvals[i];
     a.nblocks = (n + kRecPerBlock - 1) / kRecPerBlock;
     if (!a.nblocks) a.nblocks = 1;

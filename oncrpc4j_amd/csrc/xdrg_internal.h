@@ -110,6 +110,16 @@ struct VField {
     uint32_t rsv;
 };
 
+// One fixed XDR word of a record: field data + r * stride + off, converted
+// as enc_elem(type, ., half) (XDRG_T_OPAQUE: load_bytes of min(rem, 4)).
+constexpr int kPayWords = 16;
+struct PayWord {
+    const uint8_t *data;
+    int64_t stride;
+    uint32_t type;
+    uint16_t off;
+    uint8_t half, rem;
+};
 struct RecArgs {
     uint64_t n;
     uint32_t nf;
@@ -150,6 +160,12 @@ struct RecArgs {
     uint32_t dyn_idx[kMaxFields]; // dynamic field -> field index
     VField f[kMaxFields];
     int32_t cvals[XDRG_MAX_CASES];  // case values of the conditional fields
+    // the fixed XDR words of a record (mark excluded, in stream order, the
+    // dynamic field skipped) as direct element rules, so k_enc_payload's head
+    // and tail words need no walk over the fields (pay_nw = 0: schemas with
+    // more words or conditional fields walk them)
+    uint32_t pay_nw;
+    PayWord pw[kPayWords];
 };
 static_assert(sizeof(RecArgs) <= 4096, "RecArgs must fit the kernel-argument segment");
 
