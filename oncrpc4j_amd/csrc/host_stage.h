@@ -40,6 +40,9 @@
 //                  const uint64_t *limit, uint32_t nextra);
 //                                                // result words 2 + i = index[i] ? (*index[i] <= limit[i] ?
 //                                                // extra[i][*index[i]] : 0) : *extra[i] (device words); event
+//   const uint64_t *res_word(uint32_t s, uint32_t i);  // device address of slot s's result word 2 + i
+//                                                // (an index of a later kernel_end entry: the totals
+//                                                // of an inner group's members follow its own)
 //   int wait_kernel(uint32_t s, uint64_t *words); // host-blocking; words[0 .. 2 + nextra)
 //   int d2h_begin(uint32_t s);                   // copy stream waits slot s's kernels
 //   int dma_d2h(void *host, const uint8_t *dev, uint64_t bytes);
@@ -69,6 +72,7 @@
 #include <algorithm>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <vector>
 
 #include "../../include/xdrg.h"
@@ -201,6 +205,9 @@ struct Layout {
 
 // Rows of a chunk of records [lo, lo + m): records for top-level fields, the
 // chunk's elements for group members (encode: from the host group offsets).
+// Groups nest (a group's members may hold groups): the tape is in pre-order,
+// so a group's own rows (records, or its parent's elements) are known when
+// its turn comes, and its element offsets are indexed by them.
 inline void chunk_rows(const Schema &s, const xdrg_column *cols, uint64_t lo, uint64_t m, Rows &R) {
     R.lo.assign(s.f.size(), lo);
     R.n.assign(s.f.size(), m);
@@ -209,17 +216,30 @@ inline void chunk_rows(const Schema &s, const xdrg_column *cols, uint64_t lo, ui
         if (!is_group(f)) continue;
         uint64_t elo, em;
         if (f.kind == XDRG_K_FIXED) {
-            elo = lo * f.count;
-            em = m * f.count;
+            elo = R.lo[g] * f.count;
+            em = R.n[g] * f.count;
         } else {
-            elo = cols[g].offsets[lo];
-            em = cols[g].offsets[lo + m] - elo;
+            elo = cols[g].offsets[R.lo[g]];
+            em = cols[g].offsets[R.lo[g] + R.n[g]] - elo;
         }
-        for (uint32_t k = g + 1; k < s.f.size() && s.f[k].grp == g + 1; ++k) {
-            R.lo[k] = elo;
-            R.n[k] = em;
-        }
+        for (uint32_t k = g + 1; k < s.f.size(); ++k)
+            if (s.f[k].grp == g + 1) {
+                R.lo[k] = elo;
+                R.n[k] = em;
+            }
     }
+}
+// Whether the pipeline moves a schema's element rows: groups at any depth,
+// except a T x[N] group whose rows are another group's elements (its member
+// rows would be N times a device total).
+inline bool stage_groups_ok(const Schema &s) {
+    for (uint32_t k = 0; k < s.f.size(); ++k) {
+        const Field &f = s.f[k];
+        if (!is_group(f) || f.kind != XDRG_K_FIXED) continue;
+        for (uint32_t p = f.grp; p; p = s.f[p - 1].grp)
+            if (s.f[p - 1].kind != XDRG_K_FIXED) return false;
+    }
+    return true;
 }
 // Elements of group g in a chunk (encode), from its first member's rows.
 inline uint64_t group_elems(const Rows &R, uint32_t g) { return R.n[g + 1]; }
@@ -233,8 +253,8 @@ inline uint64_t bound_xdr(const Schema &s, bool framed, uint64_t m, const xdrg_c
         if (k + 1 == byref) {   // by reference: the length word stays, the payload goes out on its own
             b += 4 * R.n[k];
         } else if (is_group(f)) {   // a count word, or a bool per element and the closing one
-            if (f.kind == XDRG_K_DYNAMIC) b += 4 * m;
-            if (f.kind == XDRG_K_LIST) b += 4 * m + 4 * group_elems(R, k);
+            if (f.kind == XDRG_K_DYNAMIC) b += 4 * R.n[k];
+            if (f.kind == XDRG_K_LIST) b += 4 * R.n[k] + 4 * group_elems(R, k);
         } else if (f.kind != XDRG_K_DYNAMIC) {
             b += (uint64_t)f.xbytes * R.n[k];
         } else {
@@ -281,8 +301,9 @@ inline void enc_layout(const EncPlan &p, uint64_t lo, uint64_t m, Layout &L, Row
     L.vcap.assign(s.f.size(), 0);
     for (uint32_t k = 0; k < s.f.size(); ++k) {
         const Field &f = s.f[k];
-        if (is_group(f)) {   // the group's per-record element offsets
-            if (f.kind != XDRG_K_FIXED) L.off[k] = b.take((m + 1) * 8, (uintptr_t)(p.cols[k].offsets + lo));
+        if (is_group(f)) {   // the group's element offsets per row (record, or parent element)
+            if (f.kind != XDRG_K_FIXED)
+                L.off[k] = b.take((R.n[k] + 1) * 8, (uintptr_t)(p.cols[k].offsets + R.lo[k]));
             continue;
         }
         if (f.kind != XDRG_K_DYNAMIC) continue;
@@ -304,10 +325,21 @@ inline void enc_layout(const EncPlan &p, uint64_t lo, uint64_t m, Layout &L, Row
 // batch (the device call has the same precondition); the pipeline checks the
 // ends it cuts at.
 inline bool dyn_offsets_sane(const Schema &s, const xdrg_column *cols, uint64_t n) {
-    for (uint32_t g = 0; g < s.f.size(); ++g)
-        if (is_group(s.f[g]) && s.f[g].kind != XDRG_K_FIXED && cols[g].offsets[n] < cols[g].offsets[0]) return false;
     Rows R;
-    chunk_rows(s, cols, 0, n, R);
+    R.lo.assign(s.f.size(), 0);
+    R.n.assign(s.f.size(), n);
+    for (uint32_t g = 0; g < s.f.size(); ++g) {   // each group's range before its members' rows come from it
+        const Field &f = s.f[g];
+        if (!is_group(f)) continue;
+        if (f.kind != XDRG_K_FIXED && cols[g].offsets[R.lo[g] + R.n[g]] < cols[g].offsets[R.lo[g]]) return false;
+        const uint64_t elo = f.kind == XDRG_K_FIXED ? R.lo[g] * f.count : cols[g].offsets[R.lo[g]];
+        const uint64_t em = f.kind == XDRG_K_FIXED ? R.n[g] * f.count : cols[g].offsets[R.lo[g] + R.n[g]] - elo;
+        for (uint32_t k = g + 1; k < s.f.size(); ++k)
+            if (s.f[k].grp == g + 1) {
+                R.lo[k] = elo;
+                R.n[k] = em;
+            }
+    }
     for (uint32_t k = 0; k < s.f.size(); ++k)
         if (!is_group(s.f[k]) && s.f[k].kind == XDRG_K_DYNAMIC &&
             cols[k].offsets[R.lo[k] + R.n[k]] < cols[k].offsets[R.lo[k]])
@@ -535,7 +567,7 @@ int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uin
             const Field &fd = s.f[k2];
             if (is_group(fd)) {
                 if (fd.kind != XDRG_K_FIXED) {
-                    HS_TRY(st.h2d(s_, slot + L.off[k2], cols[k2].offsets + lo, (m + 1) * 8));
+                    HS_TRY(st.h2d(s_, slot + L.off[k2], cols[k2].offsets + R.lo[k2], (R.n[k2] + 1) * 8));
                     dc[k2].offsets = (uint64_t *)(slot + L.off[k2]);
                 }
                 dc[k2].cap = group_elems(R, k2);
@@ -556,8 +588,8 @@ int stage_encode(X &x, const Schema &s, const xdrg_column *cols, uint64_t n, uin
         HS_TRY(x.kernel_begin(s_));
         for (uint32_t k2 = 0; k2 < s.f.size(); ++k2) {   // offsets relative to the chunk's first value / element
             const Field &fd = s.f[k2];
-            if (is_group(fd) && fd.kind != XDRG_K_FIXED && cols[k2].offsets[lo])
-                HS_TRY(x.add_u64(0, dc[k2].offsets, m + 1, (uint64_t)0 - cols[k2].offsets[lo]));
+            if (is_group(fd) && fd.kind != XDRG_K_FIXED && cols[k2].offsets[R.lo[k2]])
+                HS_TRY(x.add_u64(0, dc[k2].offsets, R.n[k2] + 1, (uint64_t)0 - cols[k2].offsets[R.lo[k2]]));
             else if (!is_group(fd) && fd.kind == XDRG_K_DYNAMIC && cols[k2].offsets[R.lo[k2]])
                 HS_TRY(x.add_u64(0, dc[k2].offsets, R.n[k2] + 1, (uint64_t)0 - cols[k2].offsets[R.lo[k2]]));
         }
@@ -618,9 +650,9 @@ inline void dec_window(const DecPlan &p, uint64_t lo, uint64_t m, uint64_t &win,
 // Element rows a decode window may produce for group g: each element takes
 // at least emin XDR bytes (a LIST's TRUE, the unconditional members); a
 // group whose elements may be empty is bounded by its column's capacity.
-inline uint64_t elem_bound(const Schema &s, const xdrg_column *cols, uint32_t g, uint64_t m, uint64_t wlen) {
+inline uint64_t elem_bound(const Schema &s, const xdrg_column *cols, uint32_t g, uint64_t rows, uint64_t wlen) {
     const Field &f = s.f[g];
-    if (f.kind == XDRG_K_FIXED) return m * f.count;
+    if (f.kind == XDRG_K_FIXED) return rows * f.count;   // rows: records, or (nested) the parent's elements
     return f.emin ? wlen / f.emin + 1 : cols[g].cap;
 }
 
@@ -633,10 +665,11 @@ inline void dec_layout(const DecPlan &p, uint64_t lo, uint64_t m, Layout &L) {
     L.xdr = b.take(L.wlen, (uintptr_t)(p.in + L.win));
     L.rec = p.ro ? b.take((m + 1) * 8, (uintptr_t)(p.ro + lo)) : 0;
     L.rows.assign(s.f.size(), m);
-    for (uint32_t g = 0; g < s.f.size(); ++g)
+    for (uint32_t g = 0; g < s.f.size(); ++g)   // (pre-order: a group's rows are set before its members')
         if (is_group(s.f[g])) {
-            const uint64_t eb = elem_bound(s, p.cols, g, m, L.wlen);
-            for (uint32_t k = g + 1; k < s.f.size() && s.f[k].grp == g + 1; ++k) L.rows[k] = eb;
+            const uint64_t eb = elem_bound(s, p.cols, g, L.rows[g], L.wlen);
+            for (uint32_t k = g + 1; k < s.f.size(); ++k)
+                if (s.f[k].grp == g + 1) L.rows[k] = eb;
         }
     L.reg.assign(p.regs.size(), 0);
     for (size_t r = 0; r < p.regs.size(); ++r) {
@@ -650,7 +683,7 @@ inline void dec_layout(const DecPlan &p, uint64_t lo, uint64_t m, Layout &L) {
     for (uint32_t k = 0; k < s.f.size(); ++k) {
         const Field &f = s.f[k];
         if (is_group(f)) {
-            if (f.kind != XDRG_K_FIXED) L.off[k] = b.take((m + 1) * 8);
+            if (f.kind != XDRG_K_FIXED) L.off[k] = b.take((L.rows[k] + 1) * 8);
             continue;
         }
         if (f.kind != XDRG_K_DYNAMIC) continue;
@@ -729,24 +762,25 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
         const Layout &L = f.L;
         uint8_t *slot = x.slot(s_);
         // rows of a field's column in this chunk and the first of them
-        auto rows_of = [&](uint32_t k) -> uint64_t {
+        // (a T x[N] group's rows are records or T x[M] elements: stage_groups_ok)
+        std::function<uint64_t(uint32_t)> rows_of = [&](uint32_t k) -> uint64_t {
             if (!s.f[k].grp) return L.m;
             const uint32_t g = s.f[k].grp - 1;
-            return s.f[g].kind == XDRG_K_FIXED ? L.m * s.f[g].count : tot[g];
+            return s.f[g].kind == XDRG_K_FIXED ? rows_of(g) * s.f[g].count : tot[g];
         };
-        auto first_of = [&](uint32_t k) -> uint64_t {
+        std::function<uint64_t(uint32_t)> first_of = [&](uint32_t k) -> uint64_t {
             if (!s.f[k].grp) return L.lo;
             const uint32_t g = s.f[k].grp - 1;
-            return s.f[g].kind == XDRG_K_FIXED ? L.lo * s.f[g].count : f.base[g];
+            return s.f[g].kind == XDRG_K_FIXED ? first_of(g) * s.f[g].count : f.base[g];
         };
         HS_TRY(x.d2h_begin(s_));
         for (size_t r = 0; r < p.regs.size(); ++r) {
             const uint32_t k0 = region_field0(p.regs[r]);
             HS_TRY(st.d2h_region(s_, p.regs[r], first_of(k0), slot + L.reg[r], rows_of(k0)));
         }
-        for (uint32_t k : cnt) {
-            const uint64_t rows = is_group(s.f[k]) ? L.m : rows_of(k);
-            const uint64_t first = is_group(s.f[k]) ? L.lo : first_of(k);
+        for (uint32_t k : cnt) {   // a group's offsets: one per row of its own (records, or parent elements)
+            const uint64_t rows = rows_of(k);
+            const uint64_t first = first_of(k);
             HS_TRY(x.add_u64(1, (uint64_t *)(slot + L.off[k]), rows + 1, f.base[k]));
             HS_TRY(st.d2h(s_, cols[k].offsets + first, slot + L.off[k], (rows + 1) * 8));
             if (!is_group(s.f[k]) && k + 1 != byref)
@@ -832,7 +866,7 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
             const Field &fd = s.f[k2];
             if (is_group(fd)) {   // elements: after the chunks before, within the window's bound
                 if (fd.kind == XDRG_K_FIXED) {
-                    f.cap[k2] = m * fd.count;
+                    f.cap[k2] = L.rows[k2] * fd.count;
                     dc[k2].cap = f.cap[k2];
                     continue;
                 }
@@ -867,19 +901,28 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
         // (the element total is read on the device only when within the member's
         // laid-out rows: a failing decode may leave it anywhere, and then the
         // totals are the grants anyway)
+        // (nested: a column whose rows are a DYNAMIC / LIST group's elements is
+        // read at that group's total, an earlier entry's result word)
         std::vector<const uint64_t *> extra, index;
         std::vector<uint64_t> limit;
+        std::vector<uint32_t> pos(s.f.size(), 0);   // counted field -> its entry
+        for (uint32_t i = 0; i < cnt.size(); ++i) pos[cnt[i]] = i;
         for (uint32_t k2 : cnt) {
             const Field &fd = s.f[k2];
             const uint64_t *o = (const uint64_t *)(slot + L.off[k2]);
             limit.push_back(L.rows[k2]);
-            if (!fd.grp || is_group(fd)) {
-                extra.push_back(o + m);
+            uint32_t g = fd.grp;   // the nearest DYNAMIC / LIST ancestor whose elements index this column
+            uint64_t mult = 1;
+            while (g && s.f[g - 1].kind == XDRG_K_FIXED) {
+                mult *= s.f[g - 1].count;
+                g = s.f[g - 1].grp;
+            }
+            if (!g) {   // rows: records (times the T x[N] counts above it)
+                extra.push_back(o + m * mult);
                 index.push_back(nullptr);
-            } else {
-                const Field &gf = s.f[fd.grp - 1];
-                extra.push_back(gf.kind == XDRG_K_FIXED ? o + m * gf.count : o);
-                index.push_back(gf.kind == XDRG_K_FIXED ? nullptr : (const uint64_t *)(slot + L.off[fd.grp - 1]) + m);
+            } else {    // rows: group g - 1's elements in this chunk (mult == 1: stage_groups_ok)
+                extra.push_back(o);
+                index.push_back(x.res_word(s_, pos[g - 1]));
             }
         }
         HS_TRY(x.kernel_end(s_, extra.data(), index.data(), limit.data(), (uint32_t)extra.size()));

@@ -293,6 +293,7 @@ struct xdrg_ctx {
     uint64_t frame_spec_calls = 0;     // speculative word walks (xdrg_internal_stat 1)
     uint64_t frame_spec_gave_up = 0;   // ... of them walked again by the exact kernels (key 2)
     uint64_t frame_spec_rewalks = 0;   // super-chunks k_fs_fix walked again (key 3)
+    uint64_t host_bounces = 0;         // XDRG_HOST_PTRS calls moved whole through device scratch (key 4)
 };
 
 static int hip_fail(xdrg_ctx *c, hipError_t e, const char *what) {
@@ -414,13 +415,15 @@ extern "C" int xdrg_internal_tune(xdrg_ctx *c, int key, long long value) {
 
 // Not part of include/xdrg.h: counters for the parity tests (1: speculative
 // frame walks, 2: those that gave up and ran the exact kernels, 3: super-
-// chunks their fix-up walked again).
+// chunks their fix-up walked again, 4: host-memory calls that bounced whole
+// through device scratch instead of streaming through the staging ring).
 extern "C" long long xdrg_internal_stat(xdrg_ctx *c, int key) {
     if (!c) return -1;
     switch (key) {
     case 1: return (long long)c->frame_spec_calls;
     case 2: return (long long)c->frame_spec_gave_up;
     case 3: return (long long)c->frame_spec_rewalks;
+    case 4: return (long long)c->host_bounces;
     default: return -1;
     }
 }
@@ -1652,6 +1655,7 @@ struct HipExec {
         HIPCHK(c, hipEventRecord(r.e_kern[i], r.comp));
         return XDRG_OK;
     }
+    const uint64_t *res_word(uint32_t i, uint32_t j) const { return r.d_res + (uint64_t)i * kResWords + 2 + j; }
     int wait_kernel(uint32_t i, uint64_t *w) {
         HIPCHK(c, hipEventSynchronize(r.e_kern[i]));
         memcpy(w, r.h_res + (uint64_t)i * kResWords, 8 * r.nres[i]);
@@ -1736,10 +1740,15 @@ static void stage_schema(const xdrg_schema *s, hs::Schema &v) {
         v.f[k] = hs::Field{f.type, f.kind, f.count, s->nsz[k], s->xsz[k], s->xbytes[k], s->grp[k], 0};
         ndyn += f.kind == XDRG_K_DYNAMIC;
         if (f.type != XDRG_T_GROUP) continue;
-        // fewest XDR bytes of an element: a list's TRUE, its unconditional members
+        // fewest XDR bytes of an element: a list's TRUE, its unconditional
+        // direct members (an inner group: its count word or its closing FALSE)
         uint32_t e = f.kind == XDRG_K_LIST ? 4 : 0;
-        for (uint32_t j = 1; j <= f.reserved; ++j)
-            if (!s->cond[k + j]) e += s->f[k + j].kind == XDRG_K_DYNAMIC ? 4 : s->xbytes[k + j];
+        for (uint32_t j = 1; j <= f.reserved; ++j) {
+            const xdrg_field &m = s->f[k + j];
+            if (s->grp[k + j] != k + 1 || s->cond[k + j]) continue;
+            if (m.type == XDRG_T_GROUP) e += m.kind == XDRG_K_FIXED ? 0 : 4;
+            else e += m.kind == XDRG_K_DYNAMIC ? 4 : s->xbytes[k + j];
+        }
         v.f[k].emin = e;
         v.groups = true;
     }
@@ -1823,8 +1832,8 @@ static int mapped_cols(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
     }, byref);
 }
 
-// Host memory of a schema the staging ring does not window (groups inside
-// group elements: it moves one level of element rows) goes whole through
+// Host memory of a schema the staging ring does not window (a T x[N] group
+// inside a counted group's elements, hs::stage_groups_ok) goes whole through
 // device scratch: the host spans the call touches — columns, stream, offsets;
 // overlapping ones merged (array-of-structs columns share bytes) — are copied
 // in, the device call runs, and the spans it writes are copied back.
@@ -1879,6 +1888,7 @@ static int bounce_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *c
                          uint64_t out_cap, uint64_t *rec_offsets, uint32_t dflags, uint64_t *out_len) {
     Bounce B;
     std::vector<xdrg_column> dc;
+    c->host_bounces++;
     int rc = map_cols(c, s, cols, n, false, dc, [&](const void *p, uint64_t b) { B.add(p, b, false); return (void *)p; });
     if (rc) return rc;
     B.add(out, out_cap, true);
@@ -1899,6 +1909,7 @@ static int bounce_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, u
                          uint64_t *first_bad, int *err) {
     Bounce B;
     std::vector<xdrg_column> dc;
+    c->host_bounces++;
     int rc = map_cols(c, s, cols, n, true, dc, [&](const void *p, uint64_t b) { B.add(p, b, true); return (void *)p; });
     if (rc) return rc;
     B.add(in, in_len, false);
@@ -1948,9 +1959,9 @@ static int host_encode(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *col
         if (byref && n && !dspl) return inval(c, "XDRG_HOST_MAPPED: splice positions not registered");
         return encode_impl(c, s, dc.data(), n, dout, out_cap, drec, dflags, out_len, byref, dspl);
     }
-    if (s->nested) return bounce_encode(c, s, cols, n, out, out_cap, rec_offsets, dflags, out_len);
     hs::Schema v;
     stage_schema(s, v);
+    if (!hs::stage_groups_ok(v)) return bounce_encode(c, s, cols, n, out, out_cap, rec_offsets, dflags, out_len);
     rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));   // the caller's earlier work on this context
@@ -1990,9 +2001,9 @@ static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         if (byref && n && !dpos) return inval(c, "XDRG_HOST_MAPPED: payload positions not registered");
         return decode_impl(c, s, din, in_len, drec, n, dc.data(), dflags, first_bad, err, byref, dpos);
     }
-    if (s->nested) return bounce_decode(c, s, in, in_len, rec_offsets, n, cols, dflags, first_bad, err);
     hs::Schema v;
     stage_schema(s, v);
+    if (!hs::stage_groups_ok(v)) return bounce_decode(c, s, in, in_len, rec_offsets, n, cols, dflags, first_bad, err);
     rc = ring_ready(c, c->ring.slot > c->ring.want_slot ? c->ring.slot : c->ring.want_slot);
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));

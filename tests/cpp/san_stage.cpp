@@ -130,7 +130,8 @@ struct CpuExec {
         for (uint32_t j = 0; j < ne; ++j) {
             const uint64_t *p = extra[j];
             if (index && index[j]) {
-                CHECK(in_arena((const uint8_t *)index[j], 8));
+                CHECK(in_arena((const uint8_t *)index[j], 8) ||
+                      (index[j] >= &res[s][2] && index[j] < &res[s][2 + j]));   // an earlier entry's word
                 if (*index[j] > limit[j]) {
                     res[s][2 + j] = 0;
                     continue;
@@ -143,6 +144,7 @@ struct CpuExec {
         nres[s] = 2 + ne;
         return XDRG_OK;
     }
+    const uint64_t *res_word(uint32_t s, uint32_t i) const { return &res[s][2 + i]; }
     int wait_kernel(uint32_t s, uint64_t *w) {
         std::memcpy(w, res[s], 8 * nres[s]);
         return XDRG_OK;
@@ -241,7 +243,23 @@ struct Batch {
     hs::Schema hs;
 };
 
-static void random_schema(std::mt19937_64 &g, Batch &b, bool with_groups = false) {
+static xdrg_field random_member(std::mt19937_64 &g) {
+    static const uint32_t types[] = {XDRG_T_INT, XDRG_T_UINT, XDRG_T_ENUM, XDRG_T_BOOL, XDRG_T_HYPER,
+                                     XDRG_T_UHYPER, XDRG_T_FLOAT, XDRG_T_DOUBLE, XDRG_T_SHORT, XDRG_T_BYTE,
+                                     XDRG_T_OPAQUE, XDRG_T_STRING};
+    xdrg_field x{types[g() % 12], 0, 0, 0};
+    if (x.type == XDRG_T_STRING) x.kind = XDRG_K_DYNAMIC;
+    else if (x.type == XDRG_T_BOOL) x.kind = XDRG_K_SCALAR;
+    else if (x.type == XDRG_T_OPAQUE) x.kind = 1 + g() % 2;
+    else x.kind = g() % 3;
+    if (x.kind == XDRG_K_FIXED) x.count = 1 + (uint32_t)(g() % 5);
+    return x;
+}
+
+// nested: a group's members may hold one inner group (an array of structs or
+// a list inside the element; a T x[N] one only inside a T x[M] group, the
+// staging pipeline's hs::stage_groups_ok)
+static void random_schema(std::mt19937_64 &g, Batch &b, bool with_groups = false, bool nested = false) {
     static const uint32_t types[] = {XDRG_T_INT, XDRG_T_UINT, XDRG_T_ENUM, XDRG_T_BOOL, XDRG_T_HYPER,
                                      XDRG_T_UHYPER, XDRG_T_FLOAT, XDRG_T_DOUBLE, XDRG_T_SHORT, XDRG_T_BYTE,
                                      XDRG_T_OPAQUE, XDRG_T_STRING};
@@ -264,28 +282,33 @@ static void random_schema(std::mt19937_64 &g, Batch &b, bool with_groups = false
     if (with_groups && g() % 3 == 0) {
         const uint32_t m = 1 + (uint32_t)(g() % 3);
         const uint32_t kind = 1 + (uint32_t)(g() % 3);   // FIXED, DYNAMIC, LIST
+        const size_t gk = b.f.size();
         b.f.push_back({XDRG_T_GROUP, kind, kind == XDRG_K_FIXED ? (uint32_t)(g() % 4) : 0u, m});
-        for (uint32_t j = 0; j < m; ++j) {
-            xdrg_field x{types[g() % 12], 0, 0, 0};
-            if (x.type == XDRG_T_STRING) x.kind = XDRG_K_DYNAMIC;
-            else if (x.type == XDRG_T_BOOL) x.kind = XDRG_K_SCALAR;
-            else if (x.type == XDRG_T_OPAQUE) x.kind = 1 + g() % 2;
-            else x.kind = g() % 3;
-            if (x.kind == XDRG_K_FIXED) x.count = 1 + (uint32_t)(g() % 5);
-            b.f.push_back(x);
+        const uint32_t at = nested && g() % 2 ? (uint32_t)(g() % (m + 1)) : UINT32_MAX;   // the inner group's place
+        for (uint32_t j = 0; j <= m; ++j) {
+            if (j == at) {
+                const uint32_t m2 = 1 + (uint32_t)(g() % 2);
+                const uint32_t k2 = kind == XDRG_K_FIXED ? 1 + (uint32_t)(g() % 3) : 2 + (uint32_t)(g() % 2);
+                b.f.push_back({XDRG_T_GROUP, k2, k2 == XDRG_K_FIXED ? (uint32_t)(g() % 3) : 0u, m2});
+                for (uint32_t i = 0; i < m2; ++i) b.f.push_back(random_member(g));
+                b.f[gk].reserved += 1 + m2;
+            }
+            if (j < m) b.f.push_back(random_member(g));
         }
     }
     uint64_t fixed = 0;
     bool var = !b.c.empty();
-    uint32_t grp = 0, left = 0;
+    std::vector<std::pair<uint32_t, size_t>> open;   // (group + 1, end of its span)
     for (size_t k = 0; k < b.f.size(); ++k) {
+        while (!open.empty() && k >= open.back().second) open.pop_back();
+        const uint32_t parent = open.empty() ? 0u : open.back().first;
         const auto &x = b.f[k];
         if (x.type == XDRG_T_GROUP) {
-            b.hs.f.push_back({x.type, x.kind, x.count, 0, 0, 0, 0, 0});
+            b.hs.f.push_back({x.type, x.kind, x.count, 0, 0, 0, parent, x.kind == XDRG_K_LIST ? 4u : 0u});
             b.hs.groups = true;
-            grp = (uint32_t)k + 1;
-            left = x.reserved;
             var = true;
+            if (parent) b.hs.f[parent - 1].emin += x.kind == XDRG_K_FIXED ? 0 : 4;   // its count / closing FALSE
+            open.push_back({(uint32_t)k + 1, k + 1 + x.reserved});
             continue;
         }
         const uint32_t ns = nsz_of(x.type), xs = xsz_of(x.type);
@@ -297,12 +320,8 @@ static void random_schema(std::mt19937_64 &g, Batch &b, bool with_groups = false
         } else {
             var = true;
         }
-        b.hs.f.push_back({x.type, x.kind, x.count, ns, xs, xb, left ? grp : 0u, 0});
-        if (left && grp) {
-            auto &gf = b.hs.f[grp - 1];
-            gf.emin += x.kind == XDRG_K_DYNAMIC ? 4 : xb;
-            if (--left == 0 && gf.kind == XDRG_K_LIST) gf.emin += 4;
-        }
+        b.hs.f.push_back({x.type, x.kind, x.count, ns, xs, xb, parent, 0});
+        if (parent) b.hs.f[parent - 1].emin += x.kind == XDRG_K_DYNAMIC ? 4 : xb;
     }
     b.hs.fixed_part = fixed;
     b.hs.var_size = var;
@@ -313,8 +332,9 @@ static uint64_t rows_of(const Batch &b, size_t k, uint64_t upto) {
     const uint32_t gp = b.hs.f[k].grp;
     if (!gp) return upto;
     const xdrg_field &gf = b.f[gp - 1];
-    if (gf.kind == XDRG_K_FIXED) return upto * gf.count;
-    return b.offs[gp - 1][upto];
+    const uint64_t pr = rows_of(b, gp - 1, upto);   // the group's own rows (nested: its parent's elements)
+    if (gf.kind == XDRG_K_FIXED) return pr * gf.count;
+    return b.offs[gp - 1][pr];
 }
 
 static void random_values(std::mt19937_64 &g, Batch &b, bool for_encode) {
@@ -327,15 +347,17 @@ static void random_values(std::mt19937_64 &g, Batch &b, bool for_encode) {
         const auto &x = b.f[k];
         if (x.type != XDRG_T_GROUP) continue;
         xdrg_column &col = b.cols[k];
+        const uint64_t gr = rows_of(b, k, b.n);   // its rows: records, or its parent's elements
         if (x.kind == XDRG_K_FIXED) {
-            col.cap = b.n * x.count;
+            col.cap = gr * x.count;
             continue;
         }
         auto &o = b.offs[k];
-        o.assign(b.n + 1, 0);
-        for (uint64_t i = 0; i < b.n; ++i) o[i + 1] = o[i] + (g() % 10 == 0 ? g() % 40 : g() % 4);
+        o.assign(gr + 1, 0);
+        const uint64_t big = b.hs.f[k].grp ? 8 : 40, small = b.hs.f[k].grp ? 3 : 4;
+        for (uint64_t i = 0; i < gr; ++i) o[i + 1] = o[i] + (g() % 10 == 0 ? g() % big : g() % small);
         col.offsets = o.data();
-        col.cap = o[b.n];
+        col.cap = o[gr];
     }
     // AoS record: the fixed fields that draw it, each aligned to its element size
     uint64_t so = 0;
@@ -408,17 +430,18 @@ static void empty_like(std::mt19937_64 &g, const Batch &b, Batch &o, uint64_t sl
     o.aos.assign(b.aos.size(), 0x5a);
     o.cols.assign(nf, xdrg_column{nullptr, 0, nullptr, 0});
     std::vector<uint64_t> rows(nf, b.n);   // rows of each column (members: the group's element capacity)
-    for (size_t k = 0; k < nf; ++k) {
+    for (size_t k = 0; k < nf; ++k) {      // (pre-order: a group's own rows are set before its members')
         const auto &x = b.f[k];
         if (x.type != XDRG_T_GROUP) continue;
-        uint64_t cap = x.kind == XDRG_K_FIXED ? b.n * x.count : b.offs[k][b.n] + slack;
+        uint64_t cap = x.kind == XDRG_K_FIXED ? rows[k] * x.count : b.offs[k][rows_of(b, k, b.n)] + slack;
         if (x.kind != XDRG_K_FIXED) {
             if (g() % 8 == 0 && cap) cap = g() % cap;   // too few elements: CAPACITY
-            o.offs[k].assign(b.n + 1, 0x77);
+            o.offs[k].assign(rows[k] + 1, 0x77);
             o.cols[k].offsets = o.offs[k].data();
         }
         o.cols[k].cap = cap;
-        for (size_t j = k + 1; j < nf && b.hs.f[j].grp == k + 1; ++j) rows[j] = cap;
+        for (size_t j = k + 1; j < nf; ++j)
+            if (b.hs.f[j].grp == k + 1) rows[j] = cap;
     }
     for (size_t k = 0; k < nf; ++k) {
         const auto &x = b.f[k];
@@ -451,7 +474,8 @@ static void compare_prefix(const Batch &a, const Batch &b, uint64_t upto) {
     for (size_t k = 0; k < a.f.size(); ++k) {   // group element offsets (they index the members below)
         const auto &x = a.f[k];
         if (x.type != XDRG_T_GROUP || x.kind == XDRG_K_FIXED || !a.n) continue;
-        for (uint64_t i = 0; i <= upto; ++i) CHECK(a.offs[k][i] == b.offs[k][i]);
+        const uint64_t gr = rows_of(b, k, upto);   // the group's rows of the records before upto
+        for (uint64_t i = 0; i <= gr; ++i) CHECK(a.offs[k][i] == b.offs[k][i]);
     }
     for (size_t k = 0; k < a.f.size(); ++k) {
         const auto &x = a.f[k];
@@ -749,11 +773,12 @@ static void byref_rounds(std::mt19937_64 &g, int rounds) {
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 300;
     std::mt19937_64 g(0x0DCAC4E5);
-    uint64_t chunks_grown = 0, errs = 0, caps = 0, bounced = 0, direct = 0, group_rounds = 0;
+    uint64_t chunks_grown = 0, errs = 0, caps = 0, bounced = 0, direct = 0, group_rounds = 0, nested_rounds = 0;
     for (int r = 0; r < rounds; ++r) {
         Batch b;
-        random_schema(g, b, true);
+        random_schema(g, b, true, true);   // (nested groups: the staging ring moves every level's rows)
         group_rounds += b.hs.groups;
+        for (const auto &f : b.hs.f) nested_rounds += f.grp && f.type == XDRG_T_GROUP;
         b.n = g() % 5 == 0 ? g() % 4 : g() % 1500;
         random_values(g, b, true);
         const uint32_t flags = g() % 2 ? XDRG_FRAME_RM : 0;
@@ -849,7 +874,9 @@ int main(int argc, char **argv) {
         direct += x.direct;
     }
     CHECK(chunks_grown > 0 && errs > 0 && caps > 0 && bounced > 0 && direct > 0 && group_rounds > 0);
-    std::printf("san_stage: %llu rounds with a repeated group\n", (unsigned long long)group_rounds);
+    CHECK(nested_rounds > 0);
+    std::printf("san_stage: %llu rounds with a repeated group, %llu with groups inside its elements\n",
+                (unsigned long long)group_rounds, (unsigned long long)nested_rounds);
     byref_rounds(g, rounds);
     const uint64_t rx = receive_rounds(g, rounds);
     std::printf("san_stage: %d receive rounds ok (%llu windows)\n", rounds, (unsigned long long)rx);

@@ -285,9 +285,9 @@ def test_gpu_acl_tree_random_vs_oracle(gpu_ctx, grp_tune, framed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["pageable", "registered"])
 def test_gpu_acl_tree_host_ptrs(kind):
-    """XDRG_HOST_PTRS on the four-level schema (spans bounced through device
-    scratch, as every nested schema): encode == the fixture, decode == the
-    batch."""
+    """XDRG_HOST_PTRS on the four-level schema (streamed through the staging
+    ring, every level's element rows with their records): encode == the
+    fixture, decode == the batch."""
     import torch
     from oncrpc4j_amd import engine
     from hostmem import Pageable, Registered, moved

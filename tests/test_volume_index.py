@@ -300,9 +300,9 @@ def test_gpu_volume_index_mapped_host():
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["pageable", "registered"])
 def test_gpu_volume_index_host_ptrs(kind):
-    """XDRG_HOST_PTRS on the nested schema: the staging ring moves one level
-    of element rows, so the call bounces the spans it touches through device
-    scratch (merged where columns share bytes).  Encode == the xdrlib fixture,
+    """XDRG_HOST_PTRS on the nested schema: the staging ring moves every
+    level's element rows with their records (test_nested_host_stream.py has
+    the many-chunk batches).  Encode == the xdrlib fixture,
     decode == the batch, and a broken stream's status and the records before
     its first bad one == the oracle's."""
     import torch
