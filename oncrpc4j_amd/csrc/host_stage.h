@@ -966,16 +966,14 @@ int stage_decode(X &x, const Schema &s, const uint8_t *in, uint64_t in_len, cons
 // serial walk).
 enum RecvMode { RECV_SCAN = 0, RECV_DEFRAME = 1, RECV_DECODE = 2 };
 
-// Schemas whose decode a receive window carries: repeated groups one level
-// deep (an inner group inside an element is moved whole by the caller) whose
-// elements take at least one XDR byte each, so a window's bytes bound its
-// element rows.
+// Schemas whose decode a receive window carries: repeated groups at any
+// level the staging ring moves (stage_groups_ok) whose counted elements take
+// at least one XDR byte each, so a window's bytes bound every level's element
+// rows.
 inline bool recv_groups_ok(const Schema &s) {
-    for (const Field &f : s.f) {
-        if (!is_group(f)) continue;
-        if (f.grp) return false;
-        if (f.kind != XDRG_K_FIXED && f.emin == 0) return false;
-    }
+    if (!stage_groups_ok(s)) return false;
+    for (const Field &f : s.f)
+        if (is_group(f) && f.kind != XDRG_K_FIXED && f.emin == 0) return false;
     return true;
 }
 
@@ -1012,12 +1010,15 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
         minmsg += sp->min_xdr;
     }
     // rows of field k's column for `msgs` messages in a window of W bytes:
-    // messages, or the elements of its group (FIXED: msgs x count; else at most
-    // one per emin bytes of the window, as stage_decode's elem_bound)
-    auto rows_in = [&](uint32_t k, uint64_t msgs, uint64_t W) -> uint64_t {
+    // messages, or the elements of its group (FIXED: the group's rows x count;
+    // else at most one per emin bytes of the window, at any depth, as
+    // stage_decode's elem_bound)
+    std::function<uint64_t(uint32_t, uint64_t, uint64_t)> rows_in = [&](uint32_t k, uint64_t msgs,
+                                                                        uint64_t W) -> uint64_t {
         if (!sp->f[k].grp) return msgs;
-        const Field &gf = sp->f[sp->f[k].grp - 1];
-        return gf.kind == XDRG_K_FIXED ? msgs * gf.count : W / gf.emin + 1;
+        const uint32_t g = sp->f[k].grp - 1;
+        const Field &gf = sp->f[g];
+        return gf.kind == XDRG_K_FIXED ? rows_in(g, msgs, W) * gf.count : W / gf.emin + 1;
     };
     if (msg_offsets) msg_offsets[0] = 0;
     if (cap == 0 || len < 4) return XDRG_E_INCOMPLETE;
@@ -1043,11 +1044,8 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             // (a window's regions keep their host address modulo 16: the worst case)
             for (const Region &r : regs) b.take((uint64_t)r.stride * rows_in(region_field0(r), g.rows, g.W), 15);
             for (uint32_t k : dyn) {
-                if (is_group(sp->f[k])) {
-                    b.take((g.rows + 1) * 8);
-                    continue;
-                }
                 b.take((rows_in(k, g.rows, g.W) + 1) * 8);
+                if (is_group(sp->f[k])) continue;
                 b.take((g.W / sp->f[k].xsz + 1) * sp->f[k].nsz);
             }
         }
@@ -1112,15 +1110,16 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             next_base[k] = c.base[k] + tot[k];
         }
         // rows of a field's column in this window and the first of them
-        auto rows_of = [&](uint32_t k) -> uint64_t {
+        // (a group's own rows: messages, or its parent group's elements)
+        std::function<uint64_t(uint32_t)> rows_of = [&](uint32_t k) -> uint64_t {
             if (!sp->f[k].grp) return c.m;
             const uint32_t g = sp->f[k].grp - 1;
-            return sp->f[g].kind == XDRG_K_FIXED ? c.m * sp->f[g].count : tot[g];
+            return sp->f[g].kind == XDRG_K_FIXED ? rows_of(g) * sp->f[g].count : tot[g];
         };
-        auto first_of = [&](uint32_t k) -> uint64_t {
+        std::function<uint64_t(uint32_t)> first_of = [&](uint32_t k) -> uint64_t {
             if (!sp->f[k].grp) return c.lo;
             const uint32_t g = sp->f[k].grp - 1;
-            return sp->f[g].kind == XDRG_K_FIXED ? c.lo * sp->f[g].count : c.base[g];
+            return sp->f[g].kind == XDRG_K_FIXED ? first_of(g) * sp->f[g].count : c.base[g];
         };
         uint8_t *slot = x.slot(c.slot);
         HS_TRY(x.d2h_begin(c.slot));
@@ -1129,11 +1128,10 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             HS_TRY(st.d2h_region(c.slot, regs[r], first_of(k0), slot + c.L.reg[r], rows_of(k0)));
         }
         for (uint32_t k : dyn) {
-            const bool grp = is_group(sp->f[k]);
-            const uint64_t rows = grp ? c.m : rows_of(k), first = grp ? c.lo : first_of(k);
+            const uint64_t rows = rows_of(k), first = first_of(k);
             HS_TRY(x.add_u64(1, (uint64_t *)(slot + c.L.off[k]), rows + 1, c.base[k]));
             HS_TRY(st.d2h(c.slot, cols[k].offsets + first, slot + c.L.off[k], (rows + 1) * 8));
-            if (!grp)
+            if (!is_group(sp->f[k]))
                 HS_TRY(st.d2h(c.slot, (uint8_t *)cols[k].data + c.base[k] * sp->f[k].nsz, slot + c.L.val[k],
                               tot[k] * sp->f[k].nsz));
         }
@@ -1259,11 +1257,11 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
                 const Field &fd = sp->f[k2];
                 if (is_group(fd)) {   // elements: after the windows before, within the window's bound
                     if (fd.kind == XDRG_K_FIXED) {
-                        c.capg[k2] = m * fd.count;
+                        c.capg[k2] = c.L.rows[k2] * fd.count;
                         dc[k2].cap = c.capg[k2];
                         continue;
                     }
-                    c.L.off[k2] = b.take((m + 1) * 8);
+                    c.L.off[k2] = b.take((c.L.rows[k2] + 1) * 8);
                     c.base[k2] = next_base[k2];
                     const uint64_t left = cols[k2].cap > c.base[k2] ? cols[k2].cap - c.base[k2] : 0;
                     c.capg[k2] = std::min(left, c.L.rows[k2 + 1]);
@@ -1294,24 +1292,26 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             } else {
                 HS_TRY(x.decode(cur.slot, x.body(), res[3], dboffs, m, dc.data(), 0, 0, nullptr));
             }
-            // totals (stage_decode's): a field's offsets at its last row; a
-            // member of a DYNAMIC / LIST group at the window's element total,
-            // read on the device when within the member's laid-out rows
+            // totals (stage_decode's): a column whose rows are messages (times
+            // the T x[N] counts above it) at its last row; one whose rows are a
+            // DYNAMIC / LIST group's elements at that group's window total, an
+            // earlier entry's result word, read on the device when within the
+            // column's laid-out rows
             std::vector<const uint64_t *> extra, index;
             std::vector<uint64_t> limit;
+            std::vector<uint32_t> pos(sp->f.size(), 0);   // counted field -> its entry
+            for (uint32_t i = 0; i < dyn.size(); ++i) pos[dyn[i]] = i;
             for (uint32_t k2 : dyn) {
-                const Field &fd = sp->f[k2];
                 const uint64_t *o = (const uint64_t *)(slot + c.L.off[k2]);
                 limit.push_back(c.L.rows[k2]);
-                if (!fd.grp || is_group(fd)) {
-                    extra.push_back(o + m);
-                    index.push_back(nullptr);
-                } else {
-                    const Field &gf = sp->f[fd.grp - 1];
-                    extra.push_back(gf.kind == XDRG_K_FIXED ? o + m * gf.count : o);
-                    index.push_back(gf.kind == XDRG_K_FIXED ? nullptr
-                                                            : (const uint64_t *)(slot + c.L.off[fd.grp - 1]) + m);
+                uint32_t g = sp->f[k2].grp;
+                uint64_t mult = 1;
+                while (g && sp->f[g - 1].kind == XDRG_K_FIXED) {
+                    mult *= sp->f[g - 1].count;
+                    g = sp->f[g - 1].grp;
                 }
+                extra.push_back(g ? o : o + m * mult);
+                index.push_back(g ? x.res_word(cur.slot, pos[g - 1]) : nullptr);
             }
             HS_TRY(x.kernel_end(cur.slot, extra.data(), index.data(), limit.data(), (uint32_t)extra.size()));
             if (c.hoffs) {   // the caller's message offsets (without them the device copy stays

@@ -1048,8 +1048,15 @@ __global__ __launch_bounds__(kRecThreads) void k_grp_dec_offsets(const GroupArgs
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) {   // offsets[rows] = the column's total
             uint64_t rows;
-            if (!f.grp) f.offsets[a.n] = a.totals[s];
-            else if (a.totals[s] <= f.cap && g_batch_rows(a, f.grp - 1, rows)) f.offsets[rows] = a.totals[s];
+            if (!f.grp) {
+                f.offsets[a.n] = a.totals[s];
+            } else {
+                // a member's first entry: record 0's place writes it, but a
+                // batch whose record 0 fails places nothing (the staging ring
+                // cuts batches anywhere, so that is any chunk's first record)
+                f.offsets[0] = 0;
+                if (a.totals[s] <= f.cap && g_batch_rows(a, f.grp - 1, rows)) f.offsets[rows] = a.totals[s];
+            }
         }
     }
 }

@@ -294,6 +294,7 @@ struct xdrg_ctx {
     uint64_t frame_spec_gave_up = 0;   // ... of them walked again by the exact kernels (key 2)
     uint64_t frame_spec_rewalks = 0;   // super-chunks k_fs_fix walked again (key 3)
     uint64_t host_bounces = 0;         // XDRG_HOST_PTRS calls moved whole through device scratch (key 4)
+    uint64_t recv_three_pass = 0;      // host receives by walk, deframe, decode (key 5)
 };
 
 static int hip_fail(xdrg_ctx *c, hipError_t e, const char *what) {
@@ -416,7 +417,8 @@ extern "C" int xdrg_internal_tune(xdrg_ctx *c, int key, long long value) {
 // Not part of include/xdrg.h: counters for the parity tests (1: speculative
 // frame walks, 2: those that gave up and ran the exact kernels, 3: super-
 // chunks their fix-up walked again, 4: host-memory calls that bounced whole
-// through device scratch instead of streaming through the staging ring).
+// through device scratch instead of streaming through the staging ring, 5:
+// host receives that took three passes instead of the receive windows).
 extern "C" long long xdrg_internal_stat(xdrg_ctx *c, int key) {
     if (!c) return -1;
     switch (key) {
@@ -424,6 +426,7 @@ extern "C" long long xdrg_internal_stat(xdrg_ctx *c, int key) {
     case 2: return (long long)c->frame_spec_gave_up;
     case 3: return (long long)c->frame_spec_rewalks;
     case 4: return (long long)c->host_bounces;
+    case 5: return (long long)c->recv_three_pass;
     default: return -1;
     }
 }
@@ -1173,8 +1176,8 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
             a.dec_tile + kNestRunLdsBytes + kPlaceStaticLds > kPlaceLdsBudget)
             a.dec_tile = (uint32_t)((kPlaceLdsBudget - kNestRunLdsBytes - kPlaceStaticLds) & ~(size_t)15);
         if (n == 0) {
-            for (uint32_t q = 0; q < a.nslot; ++q)
-                if (!a.f[a.slot_field[q]].grp) HIPCHK(c, hipMemsetAsync(cols[a.slot_field[q]].offsets, 0, 8, c->stream));
+            for (uint32_t q = 0; q < a.nslot; ++q)   // (members too: zero rows, offsets[0] = 0)
+                HIPCHK(c, hipMemsetAsync(cols[a.slot_field[q]].offsets, 0, 8, c->stream));
             return finish_decode(c, n, kNoError, false, async, first_bad, err);
         }
         a.xdr = (uint8_t *)in;
@@ -2257,17 +2260,19 @@ static int recv_staged(xdrg_ctx *c, int mode, const xdrg_schema *s, const uint8_
     return rc ? rc : fr;
 }
 
-// Schemas the receive windows do not carry (groups inside group elements,
-// group elements of no XDR bytes) on host memory: the staged walk (stream
+// Schemas the receive windows do not carry (a T x[N] group inside a counted
+// group's elements, group elements of no XDR bytes: hs::recv_groups_ok) on
+// host memory: the staged walk (stream
 // offsets of the complete messages), the staged deframe of those messages
 // (their bodies into host scratch), then the staged decode of the bodies
 // (xdrg_decode_batch with XDRG_HOST_PTRS).  The same results as the device
 // receive; each stream byte crosses PCIe three times here.  Every other
-// schema, repeated groups included, goes through hs::stage_receive's windows
-// (one crossing).
+// schema, nested repeated groups included, goes through hs::stage_receive's
+// windows (one crossing).
 static int recv_staged_groups(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t len, uint64_t cap,
                               xdrg_column *cols, uint64_t *msg_offsets, uint64_t *n_msgs, uint64_t *consumed,
                               uint64_t *first_bad, int *err) {
+    c->recv_three_pass++;
     std::vector<uint64_t> so(cap + 1, 0);
     hs::RecvResult R;
     int rc = recv_staged(c, hs::RECV_SCAN, nullptr, in, len, cap, nullptr, nullptr, 0, so.data(), R);
@@ -2376,8 +2381,9 @@ extern "C" int xdrg_receive_batch(xdrg_ctx *c, const xdrg_schema *s, const uint8
     if ((flags & XDRG_HOST_PTRS) && !(flags & XDRG_HOST_MAPPED)) {
         hs::Schema v;
         stage_schema(s, v);
-        if (!hs::recv_groups_ok(v) || (s->ngroups && !c->tune.recv_win))   // inner groups / elements of no
-                                                                            // bytes: walk, deframe, decode
+        if (!hs::recv_groups_ok(v) || (s->ngroups && !c->tune.recv_win))   // T x[N] under a counted group /
+                                                                            // elements of no bytes: walk,
+                                                                            // deframe, decode
             return recv_staged_groups(c, s, in, len, cap, cols, msg_offsets, n_msgs, consumed, first_bad, err);
         hs::RecvResult R;
         rc = recv_staged(c, hs::RECV_DECODE, s, in, len, cap, cols, nullptr, 0, msg_offsets, R);

@@ -368,7 +368,7 @@ class Context:
         """Internal counters (xdrg_internal_stat: 1 speculative frame walks,
         2 of them walked again by the exact kernels, 3 super-chunks re-walked
         by their fix-up, 4 host-memory calls bounced whole through device
-        scratch).  Not part of the drop-in boundary."""
+        scratch, 5 host receives taken in three passes).  Not part of the drop-in boundary."""
         return int(lib().xdrg_internal_stat(self._h, int(key)))
 
     def kernel_stats(self, kernel):

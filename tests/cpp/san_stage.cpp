@@ -540,10 +540,10 @@ static CpuExec make_exec(std::mt19937_64 &g, const Batch &b) {
 // consumed, first_bad, err, offsets, columns), SCAN vs xo_frame_scan,
 // DEFRAME vs the assembled bodies.
 static uint64_t receive_rounds(std::mt19937_64 &g, int rounds) {
-    uint64_t windows = 0, multi = 0, stops = 0, errs = 0, assembled = 0, grp_dec = 0;
+    uint64_t windows = 0, multi = 0, stops = 0, errs = 0, assembled = 0, grp_dec = 0, nested_dec = 0;
     for (int r = 0; r < rounds; ++r) {
         Batch src;
-        random_schema(g, src, true);   // (repeated groups ride with the windows' messages)
+        random_schema(g, src, true, true);   // (repeated groups, nested ones too, ride with the windows' messages)
         src.n = g() % 4 == 0 ? g() % 5 : g() % 700;
         random_values(g, src, false);
         for (auto &c : src.c) c.values = src.cvals.data();
@@ -604,6 +604,7 @@ static uint64_t receive_rounds(std::mt19937_64 &g, int rounds) {
             if (wrc != XDRG_E_INCOMPLETE) compare_prefix(a, o, werr ? wfb : wn);
             errs += werr != 0;
             grp_dec += src.hs.groups;
+            for (const auto &f : src.hs.f) nested_dec += f.grp && f.type == XDRG_T_GROUP;
         } else if (mode == 1) {
             std::vector<uint8_t> pay(len + 8, 0xee);
             const uint64_t pcap = g() % 3 == 0 ? g() % (len + 1) : len;
@@ -663,11 +664,11 @@ static uint64_t receive_rounds(std::mt19937_64 &g, int rounds) {
         multi += style != 0;
         stops += R.n_msgs == 0;
     }
-    CHECK(windows > 4 * (uint64_t)rounds && assembled > 0 && errs > 0 && stops > 0 && grp_dec > 0);
+    CHECK(windows > 4 * (uint64_t)rounds && assembled > 0 && errs > 0 && stops > 0 && grp_dec > 0 && nested_dec > 0);
     std::printf("san_stage: receive: %llu multi-fragment rounds, %llu decode errors, %llu STOP, %llu assembled windows, "
-                "%llu decode rounds with a repeated group\n",
+                "%llu decode rounds with a repeated group (%llu inner groups)\n",
                 (unsigned long long)multi, (unsigned long long)errs, (unsigned long long)stops,
-                (unsigned long long)assembled, (unsigned long long)grp_dec);
+                (unsigned long long)assembled, (unsigned long long)grp_dec, (unsigned long long)nested_dec);
     return windows;
 }
 

@@ -110,3 +110,97 @@ def test_nested_host_capacity(name):
     finally:
         mem.close()
         c.close()
+
+
+@pytest.mark.parametrize("win", [1, 0], ids=["windows", "three_pass"])
+@pytest.mark.parametrize("kind", ["pageable", "registered"])
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_nested_host_receive(name, kind, win):
+    """xdrg_receive_batch on a host socket buffer of nested-group messages:
+    the receive windows carry every level's element rows with their messages
+    (tuning key 42 = 1: one PCIe crossing, no three-pass fallback taken) or
+    the staged walk, deframe and body decode run (key 42 = 0).  Both equal
+    the oracle's handleRead + decode (RpcMessageParserTCP.java:44-61,
+    109-140) on single-fragment and re-fragmented streams with a cut tail,
+    on corrupted bodies (first bad message delivered, GARBAGE_ARGS) and with
+    an inner group's elements running out (CAPACITY)."""
+    from oncrpc4j_amd import engine
+    from test_receive import build_stream, engine_receive, oracle_receive
+    fields, conds, make = CASES[name]
+    n = 3000
+    hb = make(n, 123)
+    c = engine.Context(0)
+    try:
+        c.host_staging(SLOT, 3)
+        c.tune(42, win)
+        t0 = c.internal_stat(5)
+        inner = [k for k, f in enumerate(fields)
+                 if f[0] == abi.T_GROUP and hb.parent[k] >= 0 and f[1] != abi.K_FIXED]
+        small = hb.dyn_caps()
+        small[inner[0]] = small[inner[0]] * 2 // 3
+        cases = [("single", 0, hb.dyn_caps()), ("mixed", 0, hb.dyn_caps()), ("single", 1500, hb.dyn_caps()),
+                 ("single", 0, small)]
+        for style, corrupt, caps in cases:
+            stream = build_stream(fields, conds, hb, style, seed=n + len(style) + corrupt, tail=True,
+                                  corrupt=corrupt)
+            want, woffs, ref = oracle_receive(fields, conds, stream, n + 3, caps)
+            got, goffs, out, host = engine_receive(c, fields, conds, stream, n + 3, caps, kind)
+            try:
+                rc, got_n, used, fb, err = want
+                assert got[:3] == (rc, got_n, used), (style, corrupt, got, want)
+                assert got[3:] == (fb, err), (style, corrupt, got, want)
+                assert goffs[:got_n + 1].tolist() == woffs[:got_n + 1]
+                assert out.equal(ref, upto=fb if err else got_n)
+                if caps is small:
+                    assert err == abi.E_CAPACITY and 0 < got_n < n
+                elif corrupt:
+                    assert err != 0
+                else:
+                    assert (rc, got_n) == (0, n)
+            finally:
+                host.close()
+        if win:
+            assert c.internal_stat(5) == t0, "the receive windows carried the nested schema"
+        else:
+            assert c.internal_stat(5) == t0 + len(cases)
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_first_record_bad_member_offsets(name):
+    """A batch whose record 0 fails delivers no records, and every offsets
+    column holds its one entry, 0 (Xdr.java:1028-1031: nothing decoded):
+    the members' first entries too, which only record 0's place wrote — the
+    staging ring starts a chunk at any record, so a chunk whose first record
+    is the batch's first bad one returned stale slot bytes there.  Device
+    columns filled with a sentinel first."""
+    from oncrpc4j_amd import engine
+    from oncrpc4j_amd.columns import DeviceBatch
+    fields, conds, make = CASES[name]
+    hb = make(200, 5)
+    rc, want, offs = oracle.encode_batch(fields, hb.columns(), hb.n, hb.xdr_total() + 64, conds=conds)
+    c = engine.Context(0)
+    try:
+        for cut in (0, 2, 6):   # record 0 cut inside its first words
+            db = DeviceBatch.empty(fields, hb.n, hb.dyn_caps())
+            cnt = []   # every counted column's offsets: dynamic fields and DYNAMIC / LIST groups
+            for k, f in enumerate(fields):
+                t = db.tensors[k]
+                if isinstance(t, tuple):
+                    cnt.append((k, t[1]))
+                elif f[0] == abi.T_GROUP and f[1] != abi.K_FIXED:
+                    cnt.append((k, t))
+            for _, o in cnt:
+                o.fill_(0x5a5a5a5a)
+            x = torch.zeros(len(want) + 64, dtype=torch.uint8, device="cuda")
+            if cut:
+                x[:cut] = torch.from_numpy(np.frombuffer(want[:cut], np.uint8).copy()).cuda()
+            ro = torch.from_numpy(offs.view(np.int64).copy()).cuda()
+            st = c.decode(engine.Schema(fields, conds), x, cut, hb.n, db.columns(), rec_offsets=ro,
+                          raise_on_error=False)
+            assert st[1] == 0 and st[0] != 0
+            for k, o in cnt:
+                assert int(o[0]) == 0, (cut, k, fields[k])
+    finally:
+        c.close()
