@@ -63,6 +63,14 @@
 //   int d2d(uint8_t *dst, const uint8_t *src, uint64_t bytes);   // copy stream, in order with dma_h2d
 //   int offs_copy(uint64_t *dst, const uint64_t *src, uint64_t n, uint64_t delta);   // compute stream:
 //                                                // dst[i] = src[i] + delta
+//   int decode_count(uint32_t s, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m,
+//                    uint32_t flags, uint64_t *tot, uint64_t *bad);
+//       host-blocking, compute stream: the first half of a repeated-group schema's decode (its
+//       walk): tot[i] = values / elements of the i-th counted field (dynamic fields and DYNAMIC /
+//       LIST groups, in field order) over the m records, at least what the place writes for
+//       the records before the first bad one (*bad, m if none)
+//   int decode_place(<decode's arguments>);      // async: the rest of that decode (the walk's
+//                                                // counts, dcols sized by tot)
 // Every call returns XDRG_OK or an XDRG_E_* status.
 #pragma once
 
@@ -977,6 +985,17 @@ inline bool recv_groups_ok(const Schema &s) {
     return true;
 }
 
+// Rows of field k's column for `msgs` messages in a receive window of W
+// bytes: messages, or the elements of its group (FIXED: the group's rows x
+// count; else at most one per emin bytes of the window, at any depth, as
+// stage_decode's elem_bound).
+inline uint64_t recv_rows_bound(const Schema &s, uint32_t k, uint64_t msgs, uint64_t W) {
+    if (!s.f[k].grp) return msgs;
+    const uint32_t g = s.f[k].grp - 1;
+    const Field &gf = s.f[g];
+    return gf.kind == XDRG_K_FIXED ? recv_rows_bound(s, g, msgs, W) * gf.count : W / gf.emin + 1;
+}
+
 struct RecvResult {
     uint64_t n_msgs = 0, consumed = 0, first_bad = 0, payload = 0;
     int err = XDRG_OK;
@@ -1009,17 +1028,15 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
         if (dyn.size() > 32) return XDRG_E_INVAL;
         minmsg += sp->min_xdr;
     }
-    // rows of field k's column for `msgs` messages in a window of W bytes:
-    // messages, or the elements of its group (FIXED: the group's rows x count;
-    // else at most one per emin bytes of the window, at any depth, as
-    // stage_decode's elem_bound)
-    std::function<uint64_t(uint32_t, uint64_t, uint64_t)> rows_in = [&](uint32_t k, uint64_t msgs,
-                                                                        uint64_t W) -> uint64_t {
-        if (!sp->f[k].grp) return msgs;
-        const uint32_t g = sp->f[k].grp - 1;
-        const Field &gf = sp->f[g];
-        return gf.kind == XDRG_K_FIXED ? rows_in(g, msgs, W) * gf.count : W / gf.emin + 1;
-    };
+    auto rows_in = [&](uint32_t k, uint64_t msgs, uint64_t W) { return recv_rows_bound(*sp, k, msgs, W); };
+    // A repeated-group schema decodes in two halves (decode_count, then
+    // decode_place): the columns are laid out for the window's counted rows
+    // and values, not for the bounds above (for nested groups those reserve
+    // several times the window), so a window can take most of its slot.  The
+    // geometry then reserves kColBudget window bytes for the columns; a
+    // window whose columns need more delivers fewer messages.
+    const bool two = mode == RECV_DECODE && sp->groups;
+    constexpr double kColBudget = 2.0;
     if (msg_offsets) msg_offsets[0] = 0;
     if (cap == 0 || len < 4) return XDRG_E_INCOMPLETE;
     Stager<X> st(x);
@@ -1040,7 +1057,9 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
         g.boffs = b.take((g.rows + 1) * 8);
         g.body = mode == RECV_DEFRAME ? b.take(g.W) : 0;
         g.cols = b.used;
-        if (mode == RECV_DECODE) {
+        if (two) {
+            b.take((uint64_t)(kColBudget * (double)g.W));
+        } else if (mode == RECV_DECODE) {
             // (a window's regions keep their host address modulo 16: the worst case)
             for (const Region &r : regs) b.take((uint64_t)r.stride * rows_in(region_field0(r), g.rows, g.W), 15);
             for (uint32_t k : dyn) {
@@ -1164,6 +1183,25 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
         return XDRG_OK;
     };
 
+    // two halves: rows of field k's column for m messages whose counted
+    // fields hold t[] values / elements, and the slot bytes of that layout
+    std::function<uint64_t(uint32_t, uint64_t, const std::vector<uint64_t> &)> rows_counted =
+        [&](uint32_t k, uint64_t m, const std::vector<uint64_t> &t) -> uint64_t {
+        if (!sp->f[k].grp) return m;
+        const uint32_t g = sp->f[k].grp - 1;
+        return sp->f[g].kind == XDRG_K_FIXED ? rows_counted(g, m, t) * sp->f[g].count : t[g];
+    };
+    auto col_need = [&](uint64_t m, const std::vector<uint64_t> &t) -> uint64_t {
+        Bump b;
+        b.used = G.cols;
+        for (const Region &r : regs) b.take((uint64_t)r.stride * rows_counted(region_field0(r), m, t), 15);
+        for (uint32_t k2 : dyn) {
+            b.take((rows_counted(k2, m, t) + 1) * 8);
+            if (!is_group(sp->f[k2])) b.take(t[k2] * sp->f[k2].nsz);
+        }
+        return b.used;
+    };
+
     const uint32_t S = x.nslots();
     Win cur;
     HS_TRY(st.acquire(0));
@@ -1186,7 +1224,7 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
         uint64_t *doffs = (uint64_t *)(slot + G.offs), *dboffs = (uint64_t *)(slot + G.boffs);
         uint8_t *dbody = mode == RECV_DEFRAME ? slot + G.body : nullptr;
         const int bodies = mode == RECV_DEFRAME ? 2 : (mode == RECV_DECODE ? 1 : 0);
-        const uint64_t want0 = std::min<uint64_t>(cap - k, G.rows);
+        uint64_t want0 = std::min<uint64_t>(cap - k, G.rows);
         uint64_t want = want0;
         uint64_t res[4] = {0, 0, 1, 0};
         HS_TRY(x.kernel_begin(cur.slot));
@@ -1202,16 +1240,44 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
         // the previous window's kernels ran before this walk (one compute stream): settle it
         while (!pend.empty()) HS_TRY(settle());
         if (stop) break;
-        const uint64_t m = res[0], used = res[1];
+        uint64_t m = res[0], used = res[1];
         if (mode == RECV_DEFRAME && m && pbytes + res[3] > payload_cap) {
             rc_final = XDRG_E_CAPACITY;   // not one more body fits the payload buffer
             break;
         }
-        if (m == 0) {
-            if (wend == len) break;   // the remainder is not a complete message: STOP (:51-53)
-            // the message at pos is longer than a window: drain, grow the ring, restage
+        // two halves: the window's counts, then (if its columns do not fit the
+        // slot) fewer messages, or for one message a larger ring
+        std::vector<uint64_t> tot2;
+        uint64_t grow_to = 0;
+        if (two && m) {
+            for (;;) {
+                if (res[2]) HS_TRY(x.offs_copy(dboffs, doffs, m + 1, cur.off));   // window -> slot offsets
+                std::vector<uint64_t> t(dyn.size(), 0);
+                uint64_t bad = m;
+                HS_TRY(x.decode_count(cur.slot, res[2] ? slot : x.body(), res[2] ? cur.off + cur.wl : res[3], dboffs,
+                                      m, res[2] ? XDRG_FRAME_RM : 0, t.data(), &bad));
+                tot2.assign(sp->f.size(), 0);
+                for (size_t i = 0; i < dyn.size(); ++i) tot2[dyn[i]] = t[i];
+                const uint64_t need = col_need(m, tot2);
+                if (need <= x.slot_bytes()) break;
+                if (m == 1) {
+                    grow_to = up(need + need / 2, 1 << 12);
+                    break;
+                }
+                want = std::max<uint64_t>(1, std::min<uint64_t>(m - 1, (uint64_t)((double)m * 0.9 *
+                       (double)(x.slot_bytes() - G.cols) / (double)(need - G.cols))));
+                want0 = want;   // (fewer by choice: not the stream's end)
+                HS_TRY(x.scan(cur.slot, slot + cur.off, cur.wl, want, doffs, bodies, dbody, dboffs, res));
+                m = res[0];
+                used = res[1];
+            }
+        }
+        if (m == 0 || grow_to) {
+            if (m == 0 && wend == len) break;   // the remainder is not a complete message: STOP (:51-53)
+            // the message at pos is longer than a window (or its columns than a
+            // slot): drain, grow the ring, restage
             HS_TRY(st.drain());
-            HS_TRY(x.grow(up(x.slot_bytes() * 2, 1 << 12)));
+            HS_TRY(x.grow(std::max<uint64_t>(grow_to, up(x.slot_bytes() * 2, 1 << 12))));
             G = fit_geo();
             chunk_no = 0;
             cur = Win();
@@ -1240,7 +1306,8 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             c.L.rows.assign(sp->f.size(), 0);
             c.base.assign(sp->f.size(), 0);
             c.capg.assign(sp->f.size(), 0);
-            for (uint32_t k2 = 0; k2 < sp->f.size(); ++k2) c.L.rows[k2] = rows_in(k2, m, cur.wl);
+            for (uint32_t k2 = 0; k2 < sp->f.size(); ++k2)
+                c.L.rows[k2] = two ? rows_counted(k2, m, tot2) : rows_in(k2, m, cur.wl);
             std::vector<xdrg_column> dc(sp->f.size());
             for (size_t r = 0; r < regs.size(); ++r) {
                 // (group members: the elements of the window's messages; a
@@ -1264,12 +1331,13 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
                     c.L.off[k2] = b.take((c.L.rows[k2] + 1) * 8);
                     c.base[k2] = next_base[k2];
                     const uint64_t left = cols[k2].cap > c.base[k2] ? cols[k2].cap - c.base[k2] : 0;
-                    c.capg[k2] = std::min(left, c.L.rows[k2 + 1]);
+                    c.capg[k2] = std::min(left, two ? tot2[k2] : c.L.rows[k2 + 1]);
                     dc[k2].offsets = (uint64_t *)(slot + c.L.off[k2]);
                     dc[k2].cap = c.capg[k2];
                 } else if (fd.kind == XDRG_K_DYNAMIC) {
                     c.L.off[k2] = b.take((c.L.rows[k2] + 1) * 8);
-                    const uint64_t vc = cur.wl / fd.xsz + 1;   // a window holds at most this many elements
+                    // a window holds at most this many elements (two halves: its count)
+                    const uint64_t vc = two ? tot2[k2] : cur.wl / fd.xsz + 1;
                     c.L.val[k2] = b.take(vc * fd.nsz);
                     c.base[k2] = next_base[k2];
                     const uint64_t left = cols[k2].cap > c.base[k2] ? cols[k2].cap - c.base[k2] : 0;
@@ -1285,8 +1353,10 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
             if (b.used > x.slot_bytes()) return XDRG_E_NOMEM;   // (the geometry reserved G.rows rows)
             // single fragments decode in place, record-marked (one mark per message,
             // GrizzlyRpcTransport.java:103-110); assembled bodies without marks
-            const bool single = res[2] != 0;
-            if (single) {
+            if (two) {
+                HS_TRY(x.decode_place(cur.slot, res[2] ? slot : x.body(), res[2] ? cur.off + cur.wl : res[3], dboffs,
+                                      m, dc.data(), res[2] ? XDRG_FRAME_RM : 0, 0, nullptr));
+            } else if (res[2]) {
                 HS_TRY(x.offs_copy(dboffs, doffs, m + 1, cur.off));   // window -> slot offsets
                 HS_TRY(x.decode(cur.slot, slot, cur.off + cur.wl, dboffs, m, dc.data(), XDRG_FRAME_RM, 0, nullptr));
             } else {

@@ -1097,18 +1097,32 @@ static int finish_decode(xdrg_ctx *c, uint64_t n, unsigned long long host_key, b
 #endif
 constexpr uint32_t kElnTile = XDRG_ELN_TILE, kElnCap = 256;
 
+// A repeated-group schema's decode in two halves (the receive windows,
+// hs::stage_receive, lay their columns out for the counted rows): kDecCount
+// runs the walk and the row scan only, its columns are not touched (may be
+// dummies), and copies the error key and every counted column's total to
+// count_out[0], count_out[1 ..] (host, pinned; ready after the stream
+// synchronises); kDecPlace then runs the rest on the same workspace (same
+// schema, records and stream, nothing else on the context's stream between).
+constexpr uint32_t kDecCount = 1u << 30;
+constexpr uint32_t kDecPlace = 1u << 29;
+
 static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uint64_t in_len,
                        const uint64_t *rec_offsets, uint64_t n, xdrg_column *cols, uint32_t flags,
-                       uint64_t *first_bad, int *err, uint32_t byref, uint64_t *ref_pos) {
+                       uint64_t *first_bad, int *err, uint32_t byref, uint64_t *ref_pos,
+                       uint64_t *count_out = nullptr) {
     if (!c || !s) return XDRG_E_INVAL;
     DeviceGuard dg;
     HIPCHK(c, hipSetDevice(c->device));
     const bool framed = flags & XDRG_FRAME_RM;
     const bool async = flags & XDRG_ASYNC;
+    const bool count_half = flags & kDecCount, place_half = flags & kDecPlace;
+    if ((count_half || place_half) && (!s->ngroups || !async || byref || (count_half && !count_out)))
+        return inval(c, "two-half decode: repeated-group schemas, asynchronous");
     if (!aligned(in, 4)) return inval(c, "XDR buffer not 4-byte aligned");
     if (n && in_len && !in) return inval(c, "XDR buffer is NULL");
     if (s->var_size && !rec_offsets) return inval(c, "variable-size schema needs record offsets");
-    int rc = check_columns(c, s, cols, n, true);
+    int rc = count_half ? XDRG_OK : check_columns(c, s, cols, n, true);
     if (rc) return rc;
     if (s->ngroups) {
         if (byref) return inval(c, "payload views in a schema with repeated groups");
@@ -1175,6 +1189,11 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         if (a.levels > 1 && !(a.emap && a.dec_el) && a.dec_tile &&
             a.dec_tile + kNestRunLdsBytes + kPlaceStaticLds > kPlaceLdsBudget)
             a.dec_tile = (uint32_t)((kPlaceLdsBudget - kNestRunLdsBytes - kPlaceStaticLds) & ~(size_t)15);
+        if (n == 0 && count_half) {
+            memset(count_out, 0, 8 * (1 + (size_t)a.nslot));
+            count_out[0] = kNoError;
+            return XDRG_OK;
+        }
         if (n == 0) {
             for (uint32_t q = 0; q < a.nslot; ++q)   // (members too: zero rows, offsets[0] = 0)
                 HIPCHK(c, hipMemsetAsync(cols[a.slot_field[q]].offsets, 0, 8, c->stream));
@@ -1183,15 +1202,23 @@ static int decode_impl(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
         a.xdr = (uint8_t *)in;
         a.xdr_cap = in_len;
         a.rec_in = rec_offsets;
-        HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
-        if (a.emap) HIPCHK(c, hipMemsetAsync(a.emap, 0, in_len / 4 + 32, c->stream));
-        {
-            TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE);
-            HIPCHK(c, (hipError_t)launch_group_phase(a, GRP_DEC_WALK, c->stream));
+        if (!place_half) {
+            HIPCHK(c, hipMemsetAsync(c->d_stat, 0xff, 8, c->stream));
+            if (a.emap) HIPCHK(c, hipMemsetAsync(a.emap, 0, in_len / 4 + 32, c->stream));
+            {
+                TimedLaunch t(c, XDRG_KERNEL_VAR_SIZE);
+                HIPCHK(c, (hipError_t)launch_group_phase(a, GRP_DEC_WALK, c->stream));
+            }
+            {
+                TimedLaunch t(c, XDRG_KERNEL_VAR_SCAN);
+                HIPCHK(c, (hipError_t)launch_scan_rows(a.block_sums, a.nblocks, a.totals, a.nslot, c->stream));
+            }
         }
-        {
-            TimedLaunch t(c, XDRG_KERNEL_VAR_SCAN);
-            HIPCHK(c, (hipError_t)launch_scan_rows(a.block_sums, a.nblocks, a.totals, a.nslot, c->stream));
+        if (count_half) {
+            HIPCHK(c, hipMemcpyAsync(count_out, c->d_stat, 8, hipMemcpyDeviceToHost, c->stream));
+            if (a.nslot)
+                HIPCHK(c, hipMemcpyAsync(count_out + 1, a.totals, 8 * (size_t)a.nslot, hipMemcpyDeviceToHost, c->stream));
+            return XDRG_OK;
         }
         {
             TimedLaunch t(c, XDRG_KERNEL_VAR_DECODE);
@@ -1643,6 +1670,30 @@ struct HipExec {
         const int rc = decode_impl(c, s, in, len, rec, m, dc, flags | XDRG_ASYNC, w, (int *)(w + 1), byref, ref);
         c->stream = keep;
         return rc;
+    }
+    // the two halves of a repeated-group decode (hs::stage_receive); the counts
+    // land in the slot's result words 47.. (kernel_end writes at most 2 + 32)
+    int decode_count(uint32_t i, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m, uint32_t flags,
+                     uint64_t *tot, uint64_t *bad) {
+        hipStream_t keep = c->stream;
+        c->stream = r.comp;
+        std::vector<xdrg_column> dummy(s->f.size());
+        uint64_t *h = r.h_res + (uint64_t)i * kResWords + (kResWords - 1 - kMaxSlots);
+        int rc = decode_impl(c, s, in, len, rec, m, dummy.data(), flags | XDRG_ASYNC | kDecCount, nullptr, nullptr, 0,
+                             nullptr, h);
+        c->stream = keep;
+        if (rc) return rc;
+        HIPCHK(c, hipStreamSynchronize(r.comp));
+        uint32_t ns = 0;
+        for (size_t k = 0; k < s->f.size(); ++k)
+            ns += (s->f[k].type == XDRG_T_GROUP) ? s->f[k].kind != XDRG_K_FIXED : s->f[k].kind == XDRG_K_DYNAMIC;
+        memcpy(tot, h + 1, 8 * (size_t)ns);
+        *bad = h[0] == kNoError ? m : (uint64_t)(h[0] >> 16);
+        return XDRG_OK;
+    }
+    int decode_place(uint32_t i, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m, xdrg_column *dc,
+                     uint32_t flags, uint32_t, uint64_t *) {
+        return decode(i, in, len, rec, m, dc, flags | kDecPlace, 0, nullptr);
     }
     int kernel_end(uint32_t i, const uint64_t *const *extra, const uint64_t *const *index, const uint64_t *limit,
                    uint32_t nextra) {

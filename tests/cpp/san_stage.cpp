@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <random>
 #include <vector>
 
@@ -207,6 +208,73 @@ struct CpuExec {
         return XDRG_OK;
     }
     const uint8_t *body() const { return bodyb.data(); }
+    // the two halves of a repeated-group decode (the receive windows): the
+    // oracle decodes the window into scratch columns sized by the window's
+    // bounds (hs::recv_rows_bound); the totals are the records' before the
+    // first bad one, plus one per byte from it on (every element and value
+    // takes a byte or more, so the failing record's partial rows fit)
+    const hs::Schema *hsch = nullptr;
+    uint64_t counts = 0, count_fails = 0;
+    int decode_count(uint32_t, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m, uint32_t flags,
+                     uint64_t *tot, uint64_t *bad) {
+        CHECK(hsch && m > 0);
+        CHECK(len == 0 || in_arena(in, len) || (in == bodyb.data() && len <= bodyb.size()));
+        const hs::Schema &S = *hsch;
+        const size_t F = S.f.size();
+        std::vector<std::vector<uint8_t>> data(F);
+        std::vector<std::vector<uint64_t>> offs(F);
+        std::vector<xdrg_column> dc(F);
+        for (uint32_t k = 0; k < F; ++k) {
+            const hs::Field &f = S.f[k];
+            const uint64_t rows = hs::recv_rows_bound(S, k, m, len);
+            dc[k] = xdrg_column{nullptr, 0, nullptr, 0};
+            if (f.type == XDRG_T_GROUP) {
+                if (f.kind == XDRG_K_FIXED) {
+                    dc[k].cap = rows * f.count;
+                    continue;
+                }
+                offs[k].assign(rows + 1, 0);
+                dc[k].offsets = offs[k].data();
+                dc[k].cap = hs::recv_rows_bound(S, k + 1, m, len);
+            } else if (f.kind == XDRG_K_DYNAMIC) {
+                offs[k].assign(rows + 1, 0);
+                data[k].assign((len / f.xsz + 1) * f.nsz, 0);
+                dc[k].data = data[k].data();
+                dc[k].offsets = offs[k].data();
+                dc[k].cap = len / f.xsz + 1;
+            } else {
+                data[k].assign(std::max<uint64_t>(std::max<uint64_t>(rows, 1) * f.nsz * (f.kind == XDRG_K_FIXED ? f.count : 1), 8), 0);
+                dc[k].data = data[k].data();
+            }
+        }
+        uint64_t fb = 0;
+        int err = 0;
+        (void)xo_decode_batch_cond(fields, nf, conds, nc, in, len, rec, m, dc.data(), flags, &fb, &err);
+        *bad = err ? fb : m;
+        const uint64_t upto = err ? fb : m;
+        const uint64_t slack = err ? len - std::min<uint64_t>(len, rec[fb]) + 1 : 0;
+        std::vector<uint64_t> t(F, 0);
+        std::function<uint64_t(uint32_t)> rows_pre = [&](uint32_t k) -> uint64_t {
+            if (!S.f[k].grp) return upto;
+            const uint32_t g = S.f[k].grp - 1;
+            return S.f[g].kind == XDRG_K_FIXED ? rows_pre(g) * S.f[g].count : t[g];
+        };
+        uint32_t i = 0;
+        for (uint32_t k = 0; k < F; ++k) {
+            const hs::Field &f = S.f[k];
+            const bool counted = f.type == XDRG_T_GROUP ? f.kind != XDRG_K_FIXED : f.kind == XDRG_K_DYNAMIC;
+            if (!counted) continue;
+            t[k] = offs[k][rows_pre(k)];
+            tot[i++] = t[k] + slack;
+        }
+        ++counts;
+        count_fails += err != 0;
+        return XDRG_OK;
+    }
+    int decode_place(uint32_t s, const uint8_t *in, uint64_t len, const uint64_t *rec, uint64_t m, xdrg_column *dc,
+                     uint32_t flags, uint32_t byref, uint64_t *ref) {
+        return decode(s, in, len, rec, m, dc, flags, byref, ref);
+    }
     int d2d(uint8_t *dst, const uint8_t *src, uint64_t n) {
         CHECK(n == 0 || (in_arena(dst, n) && in_arena(src, n)));
         std::memmove(dst, src, n);
@@ -528,6 +596,7 @@ static CpuExec make_exec(std::mt19937_64 &g, const Batch &b) {
     x.nf = b.f.size();
     x.conds = b.c.empty() ? nullptr : b.c.data();
     x.nc = b.c.size();
+    x.hsch = &b.hs;
     return x;
 }
 
@@ -540,7 +609,8 @@ static CpuExec make_exec(std::mt19937_64 &g, const Batch &b) {
 // consumed, first_bad, err, offsets, columns), SCAN vs xo_frame_scan,
 // DEFRAME vs the assembled bodies.
 static uint64_t receive_rounds(std::mt19937_64 &g, int rounds) {
-    uint64_t windows = 0, multi = 0, stops = 0, errs = 0, assembled = 0, grp_dec = 0, nested_dec = 0;
+    uint64_t windows = 0, multi = 0, stops = 0, errs = 0, assembled = 0, grp_dec = 0, nested_dec = 0, counts = 0,
+             count_fails = 0;
     for (int r = 0; r < rounds; ++r) {
         Batch src;
         random_schema(g, src, true, true);   // (repeated groups, nested ones too, ride with the windows' messages)
@@ -604,6 +674,8 @@ static uint64_t receive_rounds(std::mt19937_64 &g, int rounds) {
             if (wrc != XDRG_E_INCOMPLETE) compare_prefix(a, o, werr ? wfb : wn);
             errs += werr != 0;
             grp_dec += src.hs.groups;
+            counts += x.counts;
+            count_fails += x.count_fails;
             for (const auto &f : src.hs.f) nested_dec += f.grp && f.type == XDRG_T_GROUP;
         } else if (mode == 1) {
             std::vector<uint8_t> pay(len + 8, 0xee);
@@ -664,11 +736,14 @@ static uint64_t receive_rounds(std::mt19937_64 &g, int rounds) {
         multi += style != 0;
         stops += R.n_msgs == 0;
     }
-    CHECK(windows > 4 * (uint64_t)rounds && assembled > 0 && errs > 0 && stops > 0 && grp_dec > 0 && nested_dec > 0);
+    CHECK(windows > 4 * (uint64_t)rounds && assembled > 0 && errs > 0 && stops > 0 && grp_dec > 0 && nested_dec > 0 &&
+          counts > 0 && count_fails > 0);
     std::printf("san_stage: receive: %llu multi-fragment rounds, %llu decode errors, %llu STOP, %llu assembled windows, "
-                "%llu decode rounds with a repeated group (%llu inner groups)\n",
+                "%llu decode rounds with a repeated group (%llu inner groups; %llu windows counted first, %llu of "
+                "them failing)\n",
                 (unsigned long long)multi, (unsigned long long)errs, (unsigned long long)stops,
-                (unsigned long long)assembled, (unsigned long long)grp_dec, (unsigned long long)nested_dec);
+                (unsigned long long)assembled, (unsigned long long)grp_dec, (unsigned long long)nested_dec,
+                (unsigned long long)counts, (unsigned long long)count_fails);
     return windows;
 }
 
