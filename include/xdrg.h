@@ -128,10 +128,10 @@ typedef struct xdrg_field {
  * errors keep the reference's order: the count / list bools / member checks
  * as the element loops meet them; a negative count is XDRG_E_NEG_SIZE.
  * A deeper inner group's column is indexed by the elements of the group
- * that holds it, the same way.  XDRG_HOST_PTRS staging windows one level of
- * groups; a schema with inner
- * groups on host memory goes through device scratch whole (the spans the call
- * touches copied in and back, overlapping column spans merged).            */
+ * that holds it, the same way.  XDRG_HOST_PTRS staging moves every level's
+ * element rows with their records; only a FIXED (T x[N]) group inside a
+ * DYNAMIC / LIST group's elements goes through device scratch whole (the
+ * spans the call touches copied in and back, overlapping spans merged).    */
 
 /* One native column.  Fixed-size fields (SCALAR / FIXED): record i's first
  * element is at  data + i*stride  (stride 0 = packed = elem_size*count), so
@@ -437,9 +437,10 @@ int  xdrg_deframe(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *paylo
  * *consumed) — except XDRG_E_CAPACITY, which delivers up to it (*n_msgs =
  * first_bad) so the caller can retry it with larger columns.  Host staging
  * streams every schema through the staging windows in one crossing, a
- * window's group element rows placed by the previous window's totals —
- * except a schema whose group elements hold inner groups, which is walked,
- * deframed and then decoded (three staged passes; the same results).      */
+ * window's group element rows (every level) placed by the previous window's
+ * totals — except a schema with a FIXED (T x[N]) group inside a DYNAMIC /
+ * LIST group's elements, or with group elements of no XDR bytes, which is
+ * walked, deframed and then decoded (three staged passes; same results).   */
 int  xdrg_frame_scan_ex(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint64_t *msg_offsets,
                         uint64_t cap, uint64_t *n_msgs, uint64_t *consumed, uint32_t flags);
 int  xdrg_deframe_ex(xdrg_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *payload,
