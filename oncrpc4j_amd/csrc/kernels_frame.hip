@@ -1251,7 +1251,7 @@ __device__ __forceinline__ uint64_t sp_stage(uint32_t *tile, uint32_t l, const u
 }
 
 // A lane's segment chain: candidate starts in order, the words of a
-// rejected chain dropped with it (they share its exit); branch-free body.
+// rejected chain dropped with it (they share its exit).
 // INTERIOR (the sub-chunk ends kSpWin words or more before the stream's end):
 // every next mark that stays in the segment or exits plausibly is inside the
 // stream, so no fit test.
@@ -1260,44 +1260,50 @@ __device__ __forceinline__ void sp_lane_walk(const uint32_t *tile, uint32_t l, u
                                              uint64_t cand, uint32_t Q, uint32_t tb, uint64_t &S, uint64_t &LM,
                                              uint32_t &X, uint32_t &T, uint32_t &sig) {
     const uint64_t valid = nval >= 64 ? ~0ull : ((1ull << nval) - 1ull);
-    uint64_t avail = cand & valid, ms = 0, ml = 0, vis = 0;
+    uint64_t avail = cand & valid, ms = 0, ml = 0;
+    const uint32_t row = l * kSpRow;
     bool act = avail != 0;
     uint32_t c = act ? (uint32_t)__builtin_ctzll(avail) : 0u, cur = c;
-    const uint32_t row = l * kSpRow;
+    // The loop follows each lane's chain one mark a step (lean: a mark that
+    // stays in the segment is the common step); a chain's end, taken or
+    // rejected, is handled under a wave-uniform branch.  Rejected: its words
+    // share its exit, so the walk resumes at the next candidate past them.
     while (__ballot(act)) {
         const uint32_t m = fr_bswap(tile[row + cur]);
+        bool cm;
         uint32_t d;
-        bool comp;
         if (INTERIOR) {
-            comp = (m & 3u) == 0;
+            cm = (m & 3u) == 0;
             d = cur + 1 + ((m >> 2) & 0x1fffffffu);
         } else {
             const uint32_t nx = fr_next<4>(m, gsb + cur, Q, tb);
-            comp = nx < kFUnal;
+            cm = nx < kFUnal;
             d = nx - gsb;
         }
-        const uint64_t bit = 1ull << cur;
-        vis |= bit;
-        ms |= comp ? bit : 0ull;
-        ml |= comp && (m >> 31) ? bit : 0ull;
-        const bool cont = comp && d < nval;
-        const bool take = act && !cont && comp && (gsb + d == Q || (d >= 64 && d - 64 < kSpWin));
-        const bool rej = act && !cont && !take;
-        if (take) {
-            S = ms;
-            LM = ml;
-            X = gsb + d;
-            T = cur;
-            sig = c;
+        const uint64_t bit = act && cm ? 1ull << cur : 0ull;
+        ms |= bit;
+        ml |= (m >> 31) ? bit : 0ull;
+        const bool cont = act && cm && d < nval;
+        const bool end = act && !cont;
+        if (__ballot(end)) {
+            const bool take = end && cm && (gsb + d == Q || (d >= 64 && d - 64 < kSpWin));
+            if (take) {
+                S = ms;
+                LM = ml;
+                X = gsb + d;
+                T = cur;
+                sig = c;
+            }
+            const bool rej = end && !take;
+            avail = rej ? avail & ~(ms | (1ull << cur)) & ~((2ull << c) - 1ull) : avail;
+            const uint32_t nc = avail ? (uint32_t)__builtin_ctzll(avail) : 0u;
+            c = rej ? nc : c;
+            ms = rej ? 0ull : ms;
+            ml = rej ? 0ull : ml;
+            act = act && !take && !(rej && !avail);
+            cur = rej ? nc : cur;
         }
-        avail = rej ? avail & ~vis & ~((2ull << c) - 1ull) : avail;
-        const uint32_t nc = avail ? (uint32_t)__builtin_ctzll(avail) : 0u;
-        cur = cont ? d : rej ? nc : cur;
-        c = rej ? nc : c;
-        ms = rej ? 0ull : ms;
-        ml = rej ? 0ull : ml;
-        vis = rej ? 0ull : vis;
-        act = act && !take && !(rej && !avail);
+        cur = cont ? d : cur;
     }
 }
 
