@@ -130,11 +130,16 @@ __device__ __forceinline__ uint64_t g_dyn_words(const GField &f, uint64_t cnt) {
 // A field's presence follows its discriminant (an earlier field of the same
 // level: top-level fields per record, a group's members per element), as the
 // generated xdrEncode / xdrDecode switch on it (jrpcgen.java:1240-1340).
-// pres: bit k = field k present; v: discriminant values by slot (uniform
-// slot indices, unrolled selects: no scratch).
+// pres: bit k = discriminant k present; v: discriminant values by slot
+// (uniform slot indices, unrolled selects: no scratch).  ccid / cp: the last
+// condition evaluated (GField::cneg >> 8, its class: fields whose conditions
+// are the same test) and its result — the members of an optional struct or a
+// union arm share one test, evaluated once per element; noting a
+// discriminant forgets it.
 struct GDisc {
     uint32_t pres;
     int32_t v[XDRG_MAX_DISC];
+    uint32_t ccid, cp;
 };
 __device__ __forceinline__ int32_t gd_get(const GDisc &d, uint32_t slot) {
     int32_t r = 0;
@@ -142,22 +147,31 @@ __device__ __forceinline__ int32_t gd_get(const GDisc &d, uint32_t slot) {
     for (int j = 0; j < XDRG_MAX_DISC; ++j) r = slot == (uint32_t)j ? d.v[j] : r;
     return r;
 }
-__device__ __forceinline__ bool g_present(const GroupArgs &a, const GField &f, const GDisc &d) {
+__device__ __forceinline__ bool g_present(const GroupArgs &a, const GField &f, GDisc &d) {
     if (!f.cond) return true;
+    const uint32_t cid = f.cneg >> 8;   // (wave-uniform: the field is)
+    if (d.ccid == cid) return d.cp != 0;
     const uint32_t dk = f.cond - 1;
-    if (!((d.pres >> dk) & 1u)) return false;
-    const int32_t v = gd_get(d, a.f[dk].dslot - 1);
-    bool in = false;
-    for (uint32_t j = 0; j < f.cnum; ++j) in |= a.cvals[f.cfirst + j] == v;
-    return in != (f.cneg != 0);
+    bool p = false;
+    if ((d.pres >> dk) & 1u) {
+        const int32_t v = gd_get(d, a.f[dk].dslot - 1);
+        bool in = false;
+        for (uint32_t j = 0; j < f.cnum; ++j) in |= a.cvals[f.cfirst + j] == v;
+        p = in != ((f.cneg & 1u) != 0);
+    }
+    d.ccid = cid;
+    d.cp = p;
+    return p;
 }
-// Field k's presence (and its value when it is a discriminant) into d.
+// A discriminant's presence and value into d (only discriminants are read
+// back: a condition names one, which has a value slot).
 __device__ __forceinline__ void g_note(GDisc &d, uint32_t k, const GField &f, bool present, int32_t val) {
-    d.pres = present ? (d.pres | (1u << k)) : (d.pres & ~(1u << k));
     if (f.dslot) {
+        d.pres = present ? (d.pres | (1u << k)) : (d.pres & ~(1u << k));
 #pragma unroll
         for (int j = 0; j < XDRG_MAX_DISC; ++j)
             if (f.dslot - 1 == (uint32_t)j) d.v[j] = present ? val : 0;
+        d.ccid = 0;
     }
 }
 // A discriminant's value: from its native row (encode; bool as 0 / 1) or

@@ -729,6 +729,20 @@ static int fill_rec(xdrg_ctx *c, const xdrg_schema *s, xdrg_column *cols, uint64
 
 // Kernel arguments and workspace of a schema with repeated groups.
 // map_bytes (decode): workspace for GroupArgs::emap, 16-byte aligned after the rest.
+// The class of field k's condition for the group kernels (GField::cneg >> 8):
+// 1 + the first field whose condition is the same test (same discriminant,
+// negation and case values), 0 for an unconditional field.
+static uint32_t cond_class(const xdrg_schema *s, size_t k) {
+    if (!s->cond[k]) return 0;
+    for (size_t i = 0; i <= k; ++i) {
+        if (s->cond[i] != s->cond[k] || s->cneg[i] != s->cneg[k] || s->cnum[i] != s->cnum[k]) continue;
+        bool same = true;
+        for (uint32_t j = 0; j < s->cnum[k] && same; ++j) same = s->cvals[s->cfirst[i] + j] == s->cvals[s->cfirst[k] + j];
+        if (same) return (uint32_t)i + 1;
+    }
+    return (uint32_t)k + 1;
+}
+
 static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols, uint64_t n, bool framed,
                       bool decode, GroupArgs &a, uint64_t map_bytes = 0) {
     memset(&a, 0, sizeof a);
@@ -776,7 +790,7 @@ static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols
             }
         }
         v.cond = s->cond[k];
-        v.cneg = s->cneg[k];
+        v.cneg = s->cneg[k] | (cond_class(s, k) << 8);
         v.cfirst = s->cfirst[k];
         v.cnum = s->cnum[k];
         v.dslot = s->slot[k];
