@@ -846,11 +846,13 @@ __device__ __forceinline__ uint32_t g_walk_elem(const GroupArgs &a, uint32_t g, 
             j += m.nmem;
             continue;
         }
-        if (!present) continue;
-        if (m.kind != XDRG_K_DYNAMIC) {
-            if (end - pos < m.xbytes) return XDRG_E_SHORT;
-            pos += m.xbytes;
-        } else {
+        if (m.kind != XDRG_K_DYNAMIC) {   // (a run of fixed members of one condition: at once)
+            const uint32_t nb = m.run ? m.run >> 8 : m.xbytes;
+            j += m.run ? (m.run & 0xffu) - 1 : 0;
+            if (!present) continue;
+            if (end - pos < nb) return XDRG_E_SHORT;
+            pos += nb;
+        } else if (present) {
             uint32_t len = 0;
             const uint32_t err = g_walk_dyn(m, in, end, pos, len);
             if (err) return err;
@@ -1303,11 +1305,14 @@ __device__ __forceinline__ void g_elem_skip(const GroupArgs &a, uint32_t g, cons
     for (uint32_t j = 1; j <= f.nmem; ++j) {
         j = g_uni(j);
         const GField &m = a.f[g + j];
-        if (f.ncm && !g_dec_field_present(a, g + j, in, pos, end, d)) continue;
-        if (m.kind != XDRG_K_DYNAMIC) {
-            pos += m.xbytes;
+        const bool present = !f.ncm || g_dec_field_present(a, g + j, in, pos, end, d);
+        if (m.kind != XDRG_K_DYNAMIC) {   // (a run of fixed members of one condition: at once)
+            const uint32_t nb = m.run ? m.run >> 8 : m.xbytes;
+            j += m.run ? (m.run & 0xffu) - 1 : 0;
+            if (present) pos += nb;
             continue;
         }
+        if (!present) continue;
         const uint64_t len = g_ld(in + pos);
         run.set(m.slot, run.get(m.slot) + len);
         pos += 4 + 4 * g_dyn_words(m, len);

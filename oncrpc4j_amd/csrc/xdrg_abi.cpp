@@ -795,6 +795,19 @@ static int fill_group(xdrg_ctx *c, const xdrg_schema *s, const xdrg_column *cols
         v.cnum = s->cnum[k];
         v.dslot = s->slot[k];
     }
+    // runs of fixed members (GField::run)
+    for (uint32_t k = 0; k < a.nf; ++k) {
+        GField &v = a.f[k];
+        auto runnable = [&](const GField &w) {
+            return w.grp == v.grp && w.type != XDRG_T_GROUP && w.kind != XDRG_K_DYNAMIC && !w.dslot &&
+                   (w.cneg >> 8) == (v.cneg >> 8);
+        };
+        if (!v.grp || !runnable(v)) continue;
+        uint32_t n = 1;
+        uint64_t bytes = v.xbytes;
+        while (k + n < a.nf && n < 255 && runnable(a.f[k + n])) bytes += a.f[k + n++].xbytes;
+        if (n >= 2 && bytes < (1u << 24)) v.run = (uint32_t)bytes << 8 | n;
+    }
     a.ncond = s->ncond;
     a.nest = s->nested ? 1u : 0u;
     a.levels = 1;

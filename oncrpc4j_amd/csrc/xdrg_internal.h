@@ -400,6 +400,11 @@ struct GField {
     // is (cneg = 0) / is not (cneg = 1) in cvals[cfirst, cfirst + cnum)
     uint32_t cond, cneg, cfirst, cnum;
     uint32_t dslot;   // 0, or 1 + this field's discriminant value slot
+    // a group member that starts a run of fixed members of one condition
+    // class with no discriminant among them (the walks skip such a run as
+    // one: a member's SHORT carries its group's sub either way): run bytes
+    // << 8 | members (>= 2), else 0 (fill_group; in GField's padding)
+    uint32_t run;
     uint8_t *data;
     int64_t stride;
     uint64_t *offsets;
