@@ -2100,16 +2100,19 @@ static int host_decode(xdrg_ctx *c, const xdrg_schema *s, const uint8_t *in, uin
 // framing
 // ---------------------------------------------------------------------------
 // Carve the frame-walk workspace for a stream of Q words (the fragment list:
-// one entry per word at most).
-static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws) {
+// one entry per word at most).  The speculative walk needs neither the exact
+// kernels' tables (exact: the 2-B exit table and the active-word lists,
+// 6 B per word) nor, for stream offsets, the fragment list (frags: 8 B per
+// word): without them the workspace is ~0.3 B per word instead of ~14.
+static int frame_ws(xdrg_ctx *c, uint64_t Q, FrameWs &ws, bool exact = true, bool frags = true) {
     const uint64_t nsup = (Q + kFSuper - 1) / kFSuper + 1, nsub = nsup * (kFSuper / kFChunk);
     const uint64_t ngrp = nsup / 64 + 2;
     const uint64_t F = Q + 2;
     size_t off = 0;
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
-    const size_t o_ex = take(2 * Q), o_al = take(4 * (size_t)kFChunk * nsub), o_ac = take(4 * nsub), o_se = take(4 * nsup), o_wt = take(4 * 256 * nsup), o_gs = take(4 * 256 * (nsup + 64)), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
+    const size_t o_ex = take(exact ? 2 * Q : 0), o_al = take(exact ? 4 * (size_t)kFChunk * nsub : 0), o_ac = take(4 * nsub), o_se = take(4 * nsup), o_wt = take(4 * 256 * nsup), o_gs = take(4 * 256 * (nsup + 64)), o_ge = take(4 * 256 * ngrp), o_gn = take(4 * ngrp), o_sb = take(sizeof(FrameSub) * nsub),
                  o_fb = take(512 * nsub), o_lb = take(512 * nsub), o_su = take(sizeof(FrameSuper) * nsup),
-                 o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(8 * F), o_sx = take(8 * nsup), o_lw = take(8 * (5 * nsup + 1)), o_re = take(64);
+                 o_ba = take(sizeof(FrameBase) * nsup), o_fp = take(frags ? 8 * F : 0), o_sx = take(8 * nsup), o_lw = take(8 * (5 * nsup + 1)), o_re = take(64);
     if (off > c->fws_bytes) {
         if (c->d_fws) {
             HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2163,12 +2166,12 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
     HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));
     const uint64_t Q = len / 4;
     FrameWs ws;
-    int rc = frame_ws(c, Q, ws);
-    if (rc) return rc;
     const bool stream_offsets = payload == nullptr;
     bool serial = !aligned(in, 4) || Q == 0;
+    bool exact = !c->tune.frame_spec;
+    int rc = frame_ws(c, Q, ws, exact || serial, !stream_offsets || serial);
+    if (rc) return rc;
     if (!serial) {   // parallel walk over words; a real chain meeting a size % 4 != 0 walks again over bytes
-        bool exact = !c->tune.frame_spec;
         if (!exact) {   // the speculative walk; the exact kernels when it gives up (res[7])
             ++c->frame_spec_calls;
             HIPCHK(c, (hipError_t)frame_spec(in, len, ws, cap, stream_offsets, msg_offsets, !stream_offsets,
@@ -2186,6 +2189,8 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
                 ++c->frame_spec_gave_up;
                 exact = true;
                 HIPCHK(c, hipMemsetAsync(msg_offsets, 0, 8, c->stream));
+                rc = frame_ws(c, Q, ws);   // (the exact kernels' tables)
+                if (rc) return rc;
             }
         }
         if (exact) {
@@ -2206,6 +2211,8 @@ static int frame_walk(xdrg_ctx *c, const uint8_t *in, uint64_t len, uint8_t *pay
                 HIPCHK(c, hipStreamSynchronize(c->stream));
             } else {
                 serial = true;
+                rc = frame_ws(c, Q, ws);
+                if (rc) return rc;
             }
         }
     }

@@ -143,18 +143,27 @@ def test_exact_shape_vs_oracle(gpu_ctx, cfg, n, framed):
 
 
 @pytest.mark.slow
+@pytest.mark.parametrize("framed", [False, True], ids=["raw", "rm"])
 @pytest.mark.parametrize("cfg", [3, 4])
-def test_full_size_properties(gpu_ctx, cfg):
-    """16 Mi configs[2] records / 32 Mi configs[3] records, device resident:
-    decode(encode(x)) == x, offsets == exclusive sum of the per-record sizes,
-    and 4096 sampled records (first, last, random) byte-equal to the oracle's
-    encode of the same records."""
+def test_full_size_properties(gpu_ctx, cfg, framed):
+    """16 Mi configs[2] records / 32 Mi configs[3] records, device resident,
+    raw and record-marked: decode(encode(x)) == x, offsets == exclusive sum
+    of the per-record sizes, and 4096 sampled records (first, last, random)
+    byte-equal to the oracle's encode of the same records.  Record-marked
+    (config 4: a walk takes up to 16 GiB of stream): the frame scan of the
+    whole stream (the receive side, RpcMessageParserTCP.java:63-140) finds
+    exactly the encode's offsets."""
     n = 16 << 20 if cfg == 3 else 32 << 20
     sh = Shape(cfg, n, seed=0x0DCAC4E5 + 100 + cfg)
-    out, ro, total = _encode(gpu_ctx, sh, False)
-    sizes = sh.sizes(False)
+    out, ro, total = _encode(gpu_ctx, sh, framed)
+    sizes = sh.sizes(framed)
     assert int(ro[0]) == 0 and torch.equal(ro[1:], torch.cumsum(sizes, 0))
-    st, hb, dyn = _decode(gpu_ctx, sh, out, total, ro, False)
+    if framed and total < 16 << 30:   # (one frame walk takes up to 16 GiB: config 4's stream, not config 3's)
+        offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        assert gpu_ctx.frame_scan(out, total, offs, n) == n
+        assert torch.equal(offs, ro)
+        del offs
+    st, hb, dyn = _decode(gpu_ctx, sh, out, total, ro, framed)
     assert st == (0, n, 0)
     assert torch.equal(hb, sh.hdr)
     for (v, o), (vb, ob) in zip(sh.dyn, dyn):
@@ -163,7 +172,7 @@ def test_full_size_properties(gpu_ctx, cfg):
     rng = np.random.default_rng(cfg)
     idx = np.unique(np.concatenate([[0, 1, n - 2, n - 1], rng.integers(0, n, 4092)])).astype(np.int64)
     sub = sh.host_records(idx)
-    rc, want, want_offs = oracle.encode_batch(sh.fields, sub.columns(), len(idx), sub.xdr_total(), framed=False)
+    rc, want, want_offs = oracle.encode_batch(sh.fields, sub.columns(), len(idx), sub.xdr_total(framed), framed=framed)
     assert rc == 0
     roh = ro.cpu().numpy()
     ti = torch.from_numpy(idx).cuda()
