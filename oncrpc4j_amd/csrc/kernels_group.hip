@@ -234,8 +234,12 @@ __device__ __forceinline__ uint64_t g_elem_bytes(const GroupArgs &a, uint32_t g,
             j += m.nmem;
             continue;
         }
-        if (!p) continue;
-        s += m.kind == XDRG_K_DYNAMIC ? g_dyn_bytes(m, m.offsets[e + 1] - m.offsets[e]) : (uint64_t)m.xbytes;
+        if (m.kind != XDRG_K_DYNAMIC) {   // (a run of fixed members of one condition: at once)
+            if (p) s += m.run ? m.run >> 8 : m.xbytes;
+            j += m.run ? (m.run & 0xffu) - 1 : 0;
+            continue;
+        }
+        if (p) s += g_dyn_bytes(m, m.offsets[e + 1] - m.offsets[e]);
     }
     return s;
 }
