@@ -1010,7 +1010,7 @@ struct RecvResult {
 template <class X>
 int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t len, uint64_t cap,
                   xdrg_column *cols, uint8_t *payload, uint64_t payload_cap, uint64_t *msg_offsets,
-                  RecvResult &out) {
+                  RecvResult &out, double col_budget = 2.0) {
     out = RecvResult();
     std::vector<Region> regs;
     // the counted columns (stage_decode's): dynamic fields (values) and
@@ -1033,10 +1033,10 @@ int stage_receive(X &x, int mode, const Schema *sp, const uint8_t *in, uint64_t 
     // decode_place): the columns are laid out for the window's counted rows
     // and values, not for the bounds above (for nested groups those reserve
     // several times the window), so a window can take most of its slot.  The
-    // geometry then reserves kColBudget window bytes for the columns; a
+    // geometry then reserves col_budget column bytes per window byte; a
     // window whose columns need more delivers fewer messages.
     const bool two = mode == RECV_DECODE && sp->groups;
-    constexpr double kColBudget = 2.0;
+    const double kColBudget = col_budget > 0 ? col_budget : 2.0;
     if (msg_offsets) msg_offsets[0] = 0;
     if (cap == 0 || len < 4) return XDRG_E_INCOMPLETE;
     Stager<X> st(x);

@@ -401,6 +401,7 @@ int xdrg::set_tuning(Tuning &t, int key, long long v) {
     case 45: if (!in(0, 1)) return -1; t.grp_enc_img_nest = (int32_t)v; return 0;
     case 47: if (!in(0, 1)) return -1; t.frame_spec = (int32_t)v; return 0;
     case 48: if (!in(0, 1)) return -1; t.emit_wave = (int32_t)v; return 0;
+    case 49: if (!in(1, 100)) return -1; t.recv_budget = (int32_t)v; return 0;
     default: return -1;
     }
 }
@@ -2339,7 +2340,8 @@ static int recv_staged(xdrg_ctx *c, int mode, const xdrg_schema *s, const uint8_
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));   // the caller's earlier work on this context
     HipExec x(c, s);
-    rc = hs::stage_receive(x, mode, s ? &v : nullptr, in, len, cap, cols, payload, payload_cap, msg_offsets, R);
+    rc = hs::stage_receive(x, mode, s ? &v : nullptr, in, len, cap, cols, payload, payload_cap, msg_offsets, R,
+                           c->tune.recv_budget / 10.0);
     const int fr = x.finish();
     if (rc && rc != XDRG_E_INCOMPLETE && rc != XDRG_E_HIP && c->err.empty()) c->err = xdrg_status_string(rc);
     return rc ? rc : fr;

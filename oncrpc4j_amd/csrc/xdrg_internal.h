@@ -210,6 +210,9 @@ struct Tuning {
     int32_t emit_per = 4;           // key 36: frame walk, sub-chunks per k_fr_emit block (at most;
                                     // halved until the grid has >= 64 blocks)
     int32_t emit_wave = 1;          // key 48: frame walk emit: 1 a wave per sub-chunk (k_fr_emit_w), 0 k_fr_emit
+    int32_t recv_budget = 20;       // key 49: receive windows of group schemas: column bytes reserved per
+                                    // window byte, in tenths (hs::stage_receive; tests force the paths
+                                    // that deliver fewer messages or grow the ring with small values)
     int32_t frame_spec = 1;         // key 47: word-mode frame walk: 1 the speculative walk (k_fs_*,
                                     // the exact kernels when it gives up), 0 the exact kernels only
     int32_t grp_dec_tile = 32768;   // key 33: repeated-group decode place, LDS tile per sub-batch of

@@ -112,14 +112,17 @@ def test_nested_host_capacity(name):
         c.close()
 
 
-@pytest.mark.parametrize("win", [1, 0], ids=["windows", "three_pass"])
+@pytest.mark.parametrize("win,budget", [(1, 20), (1, 2), (0, 20)], ids=["windows", "windows_tight", "three_pass"])
 @pytest.mark.parametrize("kind", ["pageable", "registered"])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_nested_host_receive(name, kind, win):
+def test_nested_host_receive(name, kind, win, budget):
     """xdrg_receive_batch on a host socket buffer of nested-group messages:
     the receive windows carry every level's element rows with their messages
     (tuning key 42 = 1: one PCIe crossing, no three-pass fallback taken) or
-    the staged walk, deframe and body decode run (key 42 = 0).  Both equal
+    the staged walk, deframe and body decode run (key 42 = 0); windows_tight
+    reserves a fifth of a window's bytes for its columns (key 49 = 2), so
+    windows deliver fewer messages than they hold and single messages grow
+    the ring (host_stage.h stage_receive's two halves).  All equal
     the oracle's handleRead + decode (RpcMessageParserTCP.java:44-61,
     109-140) on single-fragment and re-fragmented streams with a cut tail,
     on corrupted bodies (first bad message delivered, GARBAGE_ARGS) and with
@@ -133,6 +136,7 @@ def test_nested_host_receive(name, kind, win):
     try:
         c.host_staging(SLOT, 3)
         c.tune(42, win)
+        c.tune(49, budget)
         t0 = c.internal_stat(5)
         inner = [k for k, f in enumerate(fields)
                  if f[0] == abi.T_GROUP and hb.parent[k] >= 0 and f[1] != abi.K_FIXED]
