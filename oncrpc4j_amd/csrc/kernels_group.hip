@@ -1274,15 +1274,24 @@ __device__ __forceinline__ void g_dec_elem(const GroupArgs &a, uint32_t g, uint6
             j += m.nmem;
             continue;
         }
-        const uint64_t v0 = m.kind == XDRG_K_DYNAMIC ? run.get(m.slot) : 0;
-        if (!present) {
-            if (m.kind != XDRG_K_DYNAMIC) g_zero_fixed(m, e);
-            else m.offsets[e + 1] = v0;
+        if (m.kind != XDRG_K_DYNAMIC) {   // a run of fixed members of one condition: one test
+            const uint32_t nr = m.run ? (m.run & 0xffu) : 1u;
+            for (uint32_t q = 0; q < nr; ++q) {
+                const GField &mq = a.f[g + j + q];
+                if (!present) {
+                    g_zero_fixed(mq, e);
+                    continue;
+                }
+                for (uint32_t w = 0; w < mq.xbytes >> 2; ++w)
+                    g_fixed_store(mq, e, w, *(const uint32_t *)(in + pos + 4 * w));
+                pos += mq.xbytes;
+            }
+            j += nr - 1;
             continue;
         }
-        if (m.kind != XDRG_K_DYNAMIC) {
-            for (uint32_t w = 0; w < m.xbytes >> 2; ++w) g_fixed_store(m, e, w, *(const uint32_t *)(in + pos + 4 * w));
-            pos += m.xbytes;
+        const uint64_t v0 = run.get(m.slot);
+        if (!present) {
+            m.offsets[e + 1] = v0;
             continue;
         }
         const uint64_t len = g_ld(in + pos);
